@@ -1,0 +1,210 @@
+/*
+ * libcpr_hip — MI355X-native batched episode engine for pkel/cpr's gym hot path.
+ *
+ * C ABI (plain pointers and sizes, no exceptions across the boundary). Every entry
+ * point returns an int status (CPR_OK = 0, negative = error); cpr_last_error() holds a
+ * message for the calling thread.
+ *
+ * Reference interfaces each group of entry points replaces (file:line under the
+ * pkel/cpr tree):
+ *   cpr_version                    -> engine.cpr_lib_version   simulator/gym/cpr_gym_engine.ml:40
+ *   cpr_batch_create               -> engine.create + Engine.Parameters.t + Engine.of_module
+ *                                      simulator/gym/cpr_gym_engine.ml:42-89,
+ *                                      simulator/gym/engine.ml:37-51,97-107
+ *   cpr_reset                      -> engine.reset             cpr_gym_engine.ml:90-95, engine.ml:164-170
+ *   cpr_step                       -> engine.step              cpr_gym_engine.ml:96-109, engine.ml:176-249
+ *   cpr_policy_actions             -> engine.policies(...)[name](obs)
+ *                                                              cpr_gym_engine.ml:110-138, engine.ml:258-261
+ *   cpr_observation_spec           -> engine.n_actions / observation_low / observation_high
+ *                                                              cpr_gym_engine.ml:146-162
+ *   cpr_policy_name                -> keys of engine.policies  nakamoto_ssz.ml:442-450
+ *   cpr_run_episodes               -> a Python loop of env.reset()/env.step(env.policy(obs))
+ *                                      (experiments/rl-eval, gym/ocaml/test/test_benchmark.py:5-15)
+ *                                      fused into one device launch per batch
+ *   cpr_run_episodes (LOOP mode)   -> Simulator.loop ~activations + head
+ *                                      simulator/lib/simulator.ml:519-543, csv_runner.ml:244-265
+ *   cpr_stream_fill                -> the randomness the reference draws from OCaml Random
+ *                                      (distributions.ml:17,24,90,93; simulator.ml:123),
+ *                                      re-specified as a keyed Philox stream
+ */
+#ifndef CPR_HIP_H
+#define CPR_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CPR_ABI_VERSION 1
+
+typedef struct cpr_ctx cpr_ctx;
+typedef struct cpr_batch cpr_batch;
+
+enum cpr_status {
+  CPR_OK = 0,
+  CPR_E_INVALID_ARG = -1,   /* engine.ml:37-51 Failure / network.ml:63-72 Invalid_argument */
+  CPR_E_UNSUPPORTED = -2,   /* configuration the device engine does not implement */
+  CPR_E_HIP = -3,           /* HIP runtime error */
+  CPR_E_CAPACITY = -4,      /* lane capacity exceeded */
+  CPR_E_STATE = -5          /* call order violated (step before reset, ...) */
+};
+
+enum cpr_protocol { CPR_PROTO_NAKAMOTO = 0 };
+
+enum cpr_network {
+  CPR_NET_SELFISH_MINING = 0, /* network.ml:343-387, as the gym builds it (engine.ml:100-107) */
+  CPR_NET_TWO_AGENTS = 1      /* network.ml:332-341 */
+};
+
+enum cpr_mode {
+  CPR_MODE_GYM = 0,  /* episode = reset + steps until done (engine.ml:209-214) */
+  CPR_MODE_LOOP = 1  /* episode = Simulator.loop ~activations (simulator.ml:519-533) */
+};
+
+/* policy ids of the nakamoto_ssz attack space, nakamoto_ssz.ml:374-450 */
+enum cpr_policy {
+  CPR_POLICY_HONEST = 0,
+  CPR_POLICY_SIMPLE = 1,
+  CPR_POLICY_EYAL_SIRER_2014 = 2,
+  CPR_POLICY_SAPIRSHTEIN_2016_SM1 = 3,
+  CPR_POLICY_TABLE = 4 /* action = table[(min(pub,D-1)*D + min(priv,D-1))*2 + event] */
+};
+
+/* nakamoto_ssz.ml:216-254, Variants.to_rank */
+enum cpr_nakamoto_action { CPR_ADOPT = 0, CPR_OVERRIDE = 1, CPR_MATCH = 2, CPR_WAIT = 3 };
+
+/* per-episode status bits */
+enum cpr_episode_status {
+  CPR_ST_OK = 0u,
+  CPR_ST_TIE = 1u,      /* a defender resolved an equal-time, equal-height delivery */
+  CPR_ST_OVERLAP = 2u,  /* an activation fired while finite-delay messages were in flight;
+                           the device resolves it by delivering first */
+  CPR_ST_DEEP_FORK = 4u /* more than 2^30 withheld blocks (never expected) */
+};
+
+typedef struct cpr_config {
+  int32_t protocol;          /* enum cpr_protocol */
+  int32_t network;           /* enum cpr_network */
+  int32_t mode;              /* enum cpr_mode */
+  int32_t policy;            /* enum cpr_policy; for cpr_step lanes the caller acts */
+  const uint8_t* policy_table; /* host pointer, dim*dim*2 actions (CPR_POLICY_TABLE) */
+  int32_t policy_table_dim;
+  int32_t unit_observation;  /* ssz_tools.ml NormalizeObs ~unit */
+  double alpha;              /* attacker compute, [0,1] */
+  double gamma;              /* selfish-mining gamma, [0,1] */
+  int32_t defenders;         /* >= 2 for CPR_NET_SELFISH_MINING */
+  int32_t _pad0;
+  double activation_delay;   /* expected block interval, > 0 */
+  double propagation_delay;  /* defender<->defender delay; the gym uses 1e-9 */
+  int64_t max_steps;         /* GYM mode termination; <= 0 means max_int */
+  double max_progress;       /* GYM mode termination; <= 0 means +inf */
+  double max_time;           /* GYM mode termination; <= 0 means +inf */
+  int64_t activations;       /* LOOP mode: activations per episode */
+  uint64_t seed;             /* keyed-stream seed */
+  int64_t n_lanes;           /* lockstep lanes for cpr_reset/cpr_step; 0 = none */
+} cpr_config;
+
+/* one finished episode; identical layout is produced by the CPU oracle */
+typedef struct cpr_episode_record {
+  double reward_attacker;    /* head.rewards[0]              engine.ml:215-219 */
+  double reward_defender;    /* sum of head.rewards[1..]     */
+  double progress;           /* Ref.progress head            engine.ml:208 */
+  double chain_time;         /* Simulator.timestamp head     simulator.ml:14-21 */
+  double sim_time;           /* clock.now                    */
+  int64_t n_steps;           /* episode_n_steps              engine.ml:236 */
+  int64_t n_activations;     /* episode_n_activations        engine.ml:237 */
+  int32_t head_height;
+  int32_t head_miner;        /* -1 = n/a (genesis) */
+  uint32_t status;           /* enum cpr_episode_status bits */
+  uint32_t _pad;
+} cpr_episode_record;
+
+#define CPR_HIST_BINS 64
+
+/* batch reduction; integer-exact so 1/2/4/8-GPU totals are bit-identical */
+typedef struct cpr_summary {
+  int64_t episodes;
+  int64_t steps;
+  int64_t activations;
+  int64_t reward_attacker_fx;   /* sum of reward_attacker * 2^20 */
+  int64_t reward_defender_fx;   /* sum of reward_defender * 2^20 */
+  int64_t progress_fx;          /* sum of progress * 2^20 */
+  uint64_t rel_revenue_fx;      /* sum of round(attacker/(attacker+defender) * 2^32) */
+  uint64_t rel_revenue_sq_fx;   /* sum of round((attacker/(attacker+defender))^2 * 2^32) */
+  int64_t orphans;              /* activations - head height */
+  int64_t status_tie;           /* episodes with CPR_ST_TIE */
+  int64_t status_overlap;       /* episodes with CPR_ST_OVERLAP */
+  int64_t status_other;
+  int64_t hist[CPR_HIST_BINS];  /* relative revenue histogram, bin = floor(rel*64) */
+} cpr_summary;
+
+/* lockstep info, structure of arrays, one entry per lane (engine.ml:224-241) */
+typedef struct cpr_step_info {
+  double* episode_reward_attacker;
+  double* episode_reward_defender;
+  double* episode_progress;
+  double* episode_chain_time;
+  double* episode_sim_time;
+  int64_t* episode_n_steps;
+  int64_t* episode_n_activations;
+  int32_t* head_height;
+  int32_t* head_miner;
+} cpr_step_info;
+
+const char* cpr_version(void);
+int cpr_abi_version(void);
+const char* cpr_last_error(void);
+
+/* device_ordinal: HIP device index (one context per GPU / per process) */
+int cpr_ctx_create(int device_ordinal, cpr_ctx** out);
+int cpr_ctx_destroy(cpr_ctx* ctx);
+int cpr_device_count(int* out);
+
+int cpr_batch_create(cpr_ctx* ctx, const cpr_config* cfg, cpr_batch** out);
+int cpr_batch_destroy(cpr_batch* b);
+
+/* Run episodes [first_episode, first_episode + n_episodes) to completion on the device.
+ * summary: host pointer, accumulated (+=) — zero it before the first call.
+ * records: NULL, or n_episodes records; records_on_device != 0 means a device pointer.
+ * Synchronous. */
+int cpr_run_episodes(cpr_batch* b, int64_t n_episodes, uint64_t first_episode,
+                     cpr_summary* summary, cpr_episode_record* records,
+                     int records_on_device);
+/* Same, asynchronous on the context's stream; summary must be a device pointer to a
+ * zeroed cpr_summary and records (optional) a device pointer. */
+int cpr_run_episodes_async(cpr_batch* b, int64_t n_episodes, uint64_t first_episode,
+                           cpr_summary* summary_dev, cpr_episode_record* records_dev);
+int cpr_synchronize(cpr_ctx* ctx);
+
+/* Lockstep env API over cfg->n_lanes lanes (host pointers).
+ * reset: lanes with mask[i] != 0 (mask NULL = all) start episode episode_ids[i]
+ *        (episode_ids NULL = lane index); obs gets obs_len doubles per lane.
+ * step:  actions[i] in [0, n_actions); writes obs, reward (engine.ml:223), done, info. */
+int cpr_reset(cpr_batch* b, const uint8_t* mask, const uint64_t* episode_ids, double* obs);
+int cpr_step(cpr_batch* b, const int32_t* actions, double* obs, double* reward,
+             uint8_t* done, cpr_step_info* info);
+/* integer observation fields of every lane (public, private, diff, event) */
+int cpr_observe_fields(cpr_batch* b, int32_t* fields);
+
+/* policy evaluated on encoded observations (host): obs n x obs_len -> actions n */
+int cpr_policy_actions(cpr_batch* b, int32_t policy, const double* obs, int64_t n,
+                       int32_t* actions);
+
+int cpr_observation_spec(cpr_batch* b, int32_t* obs_len, int32_t* n_actions, double* low,
+                         double* high);
+/* policy names in the reference's registry order (Collection prepends): index -> name */
+int cpr_policy_count(int32_t protocol);
+const char* cpr_policy_name(int32_t protocol, int32_t index, int32_t* policy_id);
+
+/* Keyed stream: out[4*i..4*i+3] = Philox4x32-10 block of
+ * ctr = (episode_lo, episode_hi, idx0 + i, tag), key = (seed_lo, seed_hi), computed on
+ * the device; exp_out (optional) = -log(u53(w2,w3)) of each block via cpr_log. */
+int cpr_stream_fill(cpr_ctx* ctx, uint64_t seed, uint64_t episode, uint32_t idx0,
+                    uint32_t tag, int64_t n, uint32_t* out, double* exp_out);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* CPR_HIP_H */

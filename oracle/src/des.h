@@ -1,0 +1,315 @@
+// TEST INFRASTRUCTURE ONLY — CPU oracle (faithful restatement of the reference DES).
+//
+// This is the checker for libcpr_hip, never the thing measured or shipped. It restates
+// the OCaml discrete-event simulator of pkel/cpr function by function:
+//   OrderedQueue (skew heap)        simulator/lib/orderedQueue.ml:17-47
+//   Dag (vertices, children order)  simulator/lib/dag.ml:1-45
+//   Distributions (alias, exp, uni) simulator/lib/distributions.ml:110-196
+//   Network topologies              simulator/lib/network.ml:318-387
+//   Simulator (events, visibility)  simulator/lib/simulator.ml:122-543
+//   Dagtools.common_ancestor        simulator/lib/dagtools.ml:73-121
+//   Nakamoto referee / honest node  simulator/protocols/nakamoto.ml:19-96
+//   SSZ'16 attack space + policies  simulator/protocols/nakamoto_ssz.ml:23-350
+//   Gym engine (reset/step/info)    simulator/gym/engine.ml:97-273
+// Randomness: either the OCaml 4.12 `Random` replica (sequential, reproduces the
+// reference's recorded outputs) or the keyed Philox stream shared with the GPU.
+#pragma once
+#include <cstdint>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "keyed_stream.h"
+#include "ocaml_random.h"
+
+namespace oracle {
+
+enum VisKind : uint8_t { INVISIBLE = 0, RECEIVED, RELEASED, WITHHELD };
+struct Vis {
+  VisKind kind = INVISIBLE;
+  double time = 0.0;
+};
+
+struct NakData {
+  int height = 0;
+  int miner = -1;  // -1 = None
+  bool operator==(const NakData& o) const { return height == o.height && miner == o.miner; }
+};
+
+struct Block {
+  int serial = 0;
+  std::vector<Block*> parents;
+  std::vector<Block*> children_app;  // append order; Dag's list is newest first
+  int depth = 0;
+  NakData value;
+  bool has_pow = false;
+  int32_t pow_hash = 0;
+  int signature = -1;
+  std::vector<Vis> vis;
+  std::vector<double> received_at;
+  std::vector<double> rewards;
+};
+
+struct Draft {
+  std::vector<Block*> parents;
+  NakData data;
+  bool sign = false;
+};
+
+enum EvType { EV_CLOCK, EV_DAG, EV_NET_TX, EV_NET_RX, EV_ONNODE, EV_MAKEVIS, EV_MADEVIS };
+enum Kind { K_APPEND = 0, K_POW = 1, K_NETWORK = 2 };
+
+struct Event {
+  EvType type;
+  int node;
+  Kind kind;
+  Block* blk;
+  int draft;
+};
+
+// persistent skew heap of orderedQueue.ml, implemented in place (old versions are never
+// reused by the simulator, so in-place mutation is observationally identical)
+struct SkewHeap {
+  struct N {
+    double t;
+    int ev;
+    int l, r;
+  };
+  std::vector<N> pool;
+  std::vector<int> freelist;
+  int root = -1;
+  int len = 0;
+  void clear() { pool.clear(); freelist.clear(); root = -1; len = 0; }
+  int alloc(double t, int ev);
+  int ins(int node, double t, int ev);
+  int remove_top(int node);
+  void queue(double t, int ev) { root = ins(root, t, ev); len++; }
+  bool dequeue(double* t, int* ev);
+};
+
+int float_compare(double a, double b);  // OCaml Float.compare
+
+enum DelayKind { D_CONST, D_UNIFORM, D_EXP };
+struct Link {
+  int dest;
+  DelayKind kind;
+  double a, b;  // const: a; uniform: [a, b); exp: ev = a
+};
+struct NetNode {
+  double compute;
+  std::vector<Link> links;
+};
+struct Network {
+  std::vector<NetNode> nodes;
+  bool flooding = false;
+  double activation_delay = 1.0;
+  // network.ml:332-341
+  static Network two_agents(double activation_delay, double alpha);
+  // network.ml:343-387 (raises on defenders < 2 or gamma > (d-1)/d)
+  static Network selfish_mining(double alpha, double activation_delay, double gamma,
+                                double propagation_delay, int defenders);
+};
+
+struct SimRng {
+  virtual ~SimRng() {}
+  virtual int miner(int k) = 0;
+  virtual double act_delay(int j) = 0;
+  virtual int32_t pow_bits(int serial) = 0;
+  virtual double link_delay(const Link& l, int serial, int src) = 0;
+};
+
+// OCaml Random: alias sampling exactly as distributions.ml:143-196
+struct OcamlSimRng : SimRng {
+  OcamlRandom* r;
+  std::vector<double> p;
+  std::vector<int> alias;
+  double ev;
+  OcamlSimRng(OcamlRandom* r, const Network& net);
+  int miner(int k) override;
+  double act_delay(int j) override;
+  int32_t pow_bits(int serial) override;
+  double link_delay(const Link& l, int serial, int src) override;
+};
+
+// keyed Philox stream (keyed_stream.h); weights must be [alpha, equal rest]
+struct KeyedSimRng : SimRng {
+  KeyedStream ks;
+  uint64_t t_att;
+  int d;
+  double ev;
+  KeyedSimRng(uint64_t seed, uint64_t episode, const Network& net);
+  int miner(int k) override;
+  double act_delay(int j) override;
+  int32_t pow_bits(int serial) override;
+  double link_delay(const Link& l, int serial, int src) override;
+};
+
+struct Sim;
+
+struct Action {
+  std::vector<Block*> share;
+  std::vector<Draft> append;
+};
+
+struct NodeImpl {
+  Sim* sim = nullptr;
+  int id = 0;
+  virtual ~NodeImpl() {}
+  virtual Draft puzzle_payload() = 0;
+  virtual Action handler(Kind k, Block* b) = 0;
+  virtual Block* preferred() = 0;
+};
+
+// diagnostics (not part of the reference; used to audit the GPU lane machine)
+enum : uint32_t {
+  DIAG_TIE = 1u,      // a defender saw two equal-height candidates at the same instant
+  DIAG_OVERLAP = 2u,  // an activation fired while finite-time messages were in flight
+};
+
+struct Sim {
+  double now = 0.0;
+  SkewHeap queue;
+  int c_activations = 0;
+  std::vector<Event> events;
+  std::vector<Draft> drafts;
+  std::vector<std::unique_ptr<Block>> dag;
+  std::vector<Block*> roots;  // Dag.roots order (newest first)
+  std::vector<std::unique_ptr<NodeImpl>> nodes;
+  std::vector<int> activations;
+  Network net;
+  SimRng* rng;
+  int n_nodes = 0;
+  uint32_t diag = 0;
+  int pending_finite_rx = 0;
+
+  Sim(const Network& net, SimRng* rng);
+  void init(std::vector<std::unique_ptr<NodeImpl>> nodes_);
+  void schedule(double delay, const Event& ev);
+  void schedule_now(const Event& ev) { schedule(0.0, ev); }
+  void schedule_pow();
+  bool visible(int node, const Block* b) const { return b->vis[node].kind != INVISIBLE; }
+  Block* raw_append(bool pow, int node, const Draft& d);
+  Block* append(bool pow, int node, const Draft& d);
+  void handle_action(int node, const Action& act);
+  void handle_event(const Event& ev);
+  bool dequeue(Event* ev);
+  void loop(int activations);
+  Block* head();
+  // Nakamoto referee (nakamoto.ml:19-57)
+  static bool validity(const Block* b);
+  static Block* winner(const std::vector<Block*>& l);
+  static double timestamp(const Block* b);
+};
+
+// Dagtools.common_ancestor over node `view`'s parents (dagtools.ml:102-121)
+Block* common_ancestor(const Sim& sim, int view, Block* a, Block* b);
+
+struct NakHonest : NodeImpl {
+  Block* state = nullptr;
+  Draft puzzle_payload() override;
+  Action handler(Kind k, Block* b) override;
+  Block* preferred() override { return state; }
+};
+
+enum Policy { POL_HONEST = 0, POL_SIMPLE = 1, POL_ES2014 = 2, POL_SM1 = 3, POL_TABLE = 4 };
+// nakamoto_ssz.ml:116-154 — Variants.to_rank
+enum NakAction { ADOPT = 0, OVERRIDE = 1, MATCH = 2, WAIT = 3 };
+
+struct NakObs {
+  int public_blocks, private_blocks, diff_blocks, event;  // event: 0 PoW, 1 Network
+};
+
+struct TablePolicy {
+  int dim = 0;                  // observation clamp
+  std::vector<uint8_t> actions; // [(pub * dim + priv) * 2 + event]
+};
+
+int nak_policy(int policy, const NakObs& o, const TablePolicy* table);
+void nak_obs_to_floats(const NakObs& o, bool unit, double out[4]);
+NakObs nak_obs_of_floats(const double in[4], bool unit);
+
+// nakamoto_ssz.ml Agent (:256-360)
+struct NakSszAgent {
+  Sim* sim = nullptr;
+  int my_id = 0;
+  Block* pub = nullptr;
+  Block* priv = nullptr;
+  std::vector<Block*> pending;
+  // observable state
+  Block* o_pub = nullptr;
+  Block* o_priv = nullptr;
+  Block* o_common = nullptr;
+  int o_event = 0;
+  void init(Block* root) { pub = priv = root; pending.clear(); }
+  Draft puzzle_payload() const;
+  void prepare(Kind k, Block* x);
+  NakObs observe() const;
+  Action apply(int action);
+};
+
+// attacker as a simulator node (nakamoto_ssz.ml:362-372), used by Simulator.loop tasks
+struct NakSszAttackerNode : NodeImpl {
+  NakSszAgent agent;
+  int policy;
+  const TablePolicy* table = nullptr;
+  Draft puzzle_payload() override { return agent.puzzle_payload(); }
+  Action handler(Kind k, Block* b) override;
+  Block* preferred() override { return agent.priv; }
+};
+
+// engine.ml:82-95
+struct DummyNode : NodeImpl {
+  Block* state = nullptr;
+  Draft puzzle_payload() override;
+  Action handler(Kind, Block*) override;
+  Block* preferred() override { return state; }
+};
+
+struct GymParams {
+  double alpha = 0.25, gamma = 0.5;
+  int defenders = 2;
+  double activation_delay = 1.0;
+  long max_steps = 0x3fffffffffffffffL;
+  double max_progress = 1.0 / 0.0;
+  double max_time = 1.0 / 0.0;
+  bool unit_obs = true;
+};
+
+struct StepInfo {
+  double step_reward_attacker, step_reward_defender, step_progress, step_chain_time,
+      step_sim_time;
+  double episode_reward_attacker, episode_reward_defender, episode_progress,
+      episode_chain_time, episode_sim_time;
+  long episode_n_steps, episode_n_activations;
+  int head_height, head_miner;  // head_miner -1 = n/a
+};
+
+// engine.ml of_module for the nakamoto_ssz attack space
+struct GymNakamoto {
+  GymParams p;
+  Network net;
+  // rng factory state
+  int rng_mode = 0;  // 0 = ocaml (shared), 1 = keyed
+  OcamlRandom* ocaml = nullptr;
+  uint64_t seed = 0, episode = 0;
+  std::unique_ptr<SimRng> rng;
+  std::unique_ptr<Sim> sim;
+  NakSszAgent agent;
+  long episode_steps = 0;
+  double last_progress = 0, last_chain_time = 0, last_sim_time = 0, last_reward_attacker = 0,
+         last_reward_defender = 0;
+
+  GymNakamoto(const GymParams& p, int rng_mode, OcamlRandom* ocaml, uint64_t seed,
+              uint64_t episode);
+  void init();
+  void reset(double obs[4]);
+  void observe(double obs[4]) const;
+  NakObs observe_int() const { return agent.observe(); }
+  double step(int action, double obs[4], bool* done, StepInfo* info);
+  Kind skip_to_interaction(Block** blk);
+};
+
+// validation of engine.ml:37-51; returns empty string if ok
+std::string gym_params_error(const GymParams& p);
+
+}  // namespace oracle

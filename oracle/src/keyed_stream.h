@@ -1,0 +1,177 @@
+// TEST INFRASTRUCTURE ONLY — CPU oracle side of the "cpr keyed stream v1".
+//
+// The reference draws every random number from one sequential OCaml `Random` stream
+// (distributions.ml:17,24,90,93; simulator.ml:123), which makes results depend on the
+// order in which a discrete-event queue happens to pop same-time events. A batched GPU
+// engine cannot reproduce that order cheaply, so the build defines a *keyed* stream in
+// which every draw is addressed by its semantic coordinates instead of its position:
+//
+//   key   = (seed_lo, seed_hi)                          Philox4x32-10 (Salmon et al. 2011)
+//   act   : ctr = (ep_lo, ep_hi, j, TAG_ACT)   w0,w1 -> miner of activation j
+//                                              w2,w3 -> 53-bit u, delay of clock j
+//   link  : ctr = (ep_lo, ep_hi, serial, TAG_LINK | dest>>1)  words (2*(dest&1), +1) -> u
+//   pow   : ctr = (ep_lo, ep_hi, serial, TAG_POW)  w0 & 0x3FFFFFFF
+//
+// exponential(ev) = (-1 * ev) * cpr_log(u)   (same expression shape as distributions.ml:24)
+// uniform(lo,hi)  = u * (hi - lo) + lo       (distributions.ml:17)
+// miner           = 0 if w0 < floor(alpha * 2^32) else 1 + ((w1 * d) >> 32)
+//
+// cpr_log is fdlibm's e_log.c algorithm (only IEEE +,-,*,/), so the GPU and the CPU
+// oracle compute bit-identical event times. This file is an independent restatement of
+// the same specification the HIP code implements (cpr_amd/csrc/cpr_stream.h); the two
+// are cross-checked draw-by-draw in tests/test_gpu_parity.py.
+#pragma once
+#include <cstdint>
+#include <cstring>
+
+namespace oracle {
+
+static const uint32_t TAG_ACT = 0u;
+static const uint32_t TAG_LINK = 0x10000000u;
+static const uint32_t TAG_POW = 0x20000000u;
+
+struct Philox4x32 {
+  static void block(const uint32_t ctr_in[4], const uint32_t key_in[2], uint32_t out[4]) {
+    uint32_t c0 = ctr_in[0], c1 = ctr_in[1], c2 = ctr_in[2], c3 = ctr_in[3];
+    uint32_t k0 = key_in[0], k1 = key_in[1];
+    for (int r = 0; r < 10; r++) {
+      uint64_t p0 = (uint64_t)0xD2511F53u * c0;
+      uint64_t p1 = (uint64_t)0xCD9E8D57u * c2;
+      uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
+      uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
+      uint32_t n0 = hi1 ^ c1 ^ k0;
+      uint32_t n1 = lo1;
+      uint32_t n2 = hi0 ^ c3 ^ k1;
+      uint32_t n3 = lo0;
+      c0 = n0; c1 = n1; c2 = n2; c3 = n3;
+      k0 += 0x9E3779B9u;
+      k1 += 0xBB67AE85u;
+    }
+    out[0] = c0; out[1] = c1; out[2] = c2; out[3] = c3;
+  }
+};
+
+static inline double u53(uint32_t a, uint32_t b) {
+  return ((double)(a >> 5) * 67108864.0 + (double)(b >> 6)) * (1.0 / 9007199254740992.0);
+}
+
+static inline double bits_to_double(uint64_t b) {
+  double d;
+  memcpy(&d, &b, 8);
+  return d;
+}
+static inline uint64_t double_to_bits(double d) {
+  uint64_t b;
+  memcpy(&b, &d, 8);
+  return b;
+}
+
+// fdlibm __ieee754_log (e_log.c), restated. Input domain used by the stream: [0, 1).
+static inline double cpr_log(double x) {
+  const double ln2_hi = bits_to_double(0x3fe62e42fee00000ull);
+  const double ln2_lo = bits_to_double(0x3dea39ef35793c76ull);
+  const double two54 = bits_to_double(0x4350000000000000ull);
+  const double Lg1 = bits_to_double(0x3FE5555555555593ull);
+  const double Lg2 = bits_to_double(0x3FD999999997FA04ull);
+  const double Lg3 = bits_to_double(0x3FD2492494229359ull);
+  const double Lg4 = bits_to_double(0x3FCC71C51D8E78AFull);
+  const double Lg5 = bits_to_double(0x3FC7466496CB03DEull);
+  const double Lg6 = bits_to_double(0x3FC39A09D078C69Full);
+  const double Lg7 = bits_to_double(0x3FC2F112DF3E5244ull);
+  uint64_t ux = double_to_bits(x);
+  int32_t hx = (int32_t)(ux >> 32);
+  uint32_t lx = (uint32_t)ux;
+  int32_t k = 0;
+  if (hx < 0x00100000) {
+    if (((hx & 0x7fffffff) | lx) == 0) return -1.0 / 0.0;
+    if (hx < 0) return (x - x) / 0.0;
+    k -= 54;
+    x *= two54;
+    ux = double_to_bits(x);
+    hx = (int32_t)(ux >> 32);
+  }
+  if (hx >= 0x7ff00000) return x + x;
+  k += (hx >> 20) - 1023;
+  hx &= 0x000fffff;
+  int32_t i = (hx + 0x95f64) & 0x100000;
+  ux = ((uint64_t)(uint32_t)(hx | (i ^ 0x3ff00000)) << 32) | (ux & 0xffffffffull);
+  x = bits_to_double(ux);
+  k += (i >> 20);
+  double f = x - 1.0;
+  double dk, R;
+  if ((0x000fffff & (2 + hx)) < 3) {
+    if (f == 0.0) {
+      if (k == 0) return 0.0;
+      dk = (double)k;
+      return dk * ln2_hi + dk * ln2_lo;
+    }
+    R = f * f * (0.5 - 0.33333333333333333 * f);
+    if (k == 0) return f - R;
+    dk = (double)k;
+    return dk * ln2_hi - ((R - dk * ln2_lo) - f);
+  }
+  double s = f / (2.0 + f);
+  dk = (double)k;
+  double z = s * s;
+  i = hx - 0x6147a;
+  double w = z * z;
+  int32_t j = 0x6b851 - hx;
+  double t1 = w * (Lg2 + w * (Lg4 + w * Lg6));
+  double t2 = z * (Lg1 + w * (Lg3 + w * (Lg5 + w * Lg7)));
+  i |= j;
+  R = t2 + t1;
+  if (i > 0) {
+    double hfsq = 0.5 * f * f;
+    if (k == 0) return f - (hfsq - s * (hfsq + R));
+    return dk * ln2_hi - ((hfsq - (s * (hfsq + R) + dk * ln2_lo)) - f);
+  }
+  if (k == 0) return f - s * (f - R);
+  return dk * ln2_hi - ((s * (f - R) - dk * ln2_lo) - f);
+}
+
+struct KeyedStream {
+  uint32_t key[2];
+  uint32_t ep[2];
+  KeyedStream(uint64_t seed, uint64_t episode) {
+    key[0] = (uint32_t)seed;
+    key[1] = (uint32_t)(seed >> 32);
+    ep[0] = (uint32_t)episode;
+    ep[1] = (uint32_t)(episode >> 32);
+  }
+  void block(uint32_t idx, uint32_t tag, uint32_t out[4]) const {
+    uint32_t ctr[4] = {ep[0], ep[1], idx, tag};
+    Philox4x32::block(ctr, key, out);
+  }
+  // miner of activation j among [attacker] + d equal-weight defenders
+  int miner(uint32_t j, uint64_t t_att, int d) const {
+    uint32_t w[4];
+    block(j, TAG_ACT, w);
+    if ((uint64_t)w[0] < t_att) return 0;
+    return 1 + (int)(((uint64_t)w[1] * (uint64_t)d) >> 32);
+  }
+  double act_u(uint32_t j) const {
+    uint32_t w[4];
+    block(j, TAG_ACT, w);
+    return u53(w[2], w[3]);
+  }
+  double link_u(uint32_t serial, uint32_t dest) const {
+    uint32_t w[4];
+    block(serial, TAG_LINK | (dest >> 1), w);
+    return (dest & 1) ? u53(w[2], w[3]) : u53(w[0], w[1]);
+  }
+  uint32_t pow_bits(uint32_t serial) const {
+    uint32_t w[4];
+    block(serial, TAG_POW, w);
+    return w[0] & 0x3FFFFFFFu;
+  }
+};
+
+static inline uint64_t alpha_threshold(double alpha) {
+  // floor(alpha * 2^32), alpha in [0, 1]
+  double t = alpha * 4294967296.0;
+  if (t <= 0.0) return 0;
+  if (t >= 4294967296.0) return 4294967296ull;
+  return (uint64_t)t;
+}
+
+}  // namespace oracle

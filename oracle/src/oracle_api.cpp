@@ -1,0 +1,275 @@
+// TEST INFRASTRUCTURE ONLY — C entry points of the CPU oracle for tests/ and for
+// bench.py's cpu_baseline leg. Never used by the product path.
+#include <chrono>
+#include <cmath>
+#include <cstring>
+#include <stdexcept>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../include/cpr_hip.h"
+#include "des.h"
+
+using namespace oracle;
+
+static thread_local std::string g_err;
+
+static void set_err(const char* what) { g_err = what; }
+
+extern "C" {
+
+const char* oracle_last_error() { return g_err.c_str(); }
+
+// ---------------- OCaml Random replica
+void* oracle_ocaml_rng_new(long seed) {
+  return seed < 0 ? new OcamlRandom() : new OcamlRandom(seed);
+}
+void oracle_ocaml_rng_free(void* r) { delete (OcamlRandom*)r; }
+int32_t oracle_ocaml_rng_bits(void* r) { return ((OcamlRandom*)r)->bits(); }
+int32_t oracle_ocaml_rng_int(void* r, int32_t n) { return ((OcamlRandom*)r)->int_(n); }
+double oracle_ocaml_rng_float(void* r, double b) { return ((OcamlRandom*)r)->float_(b); }
+
+// ---------------- keyed stream
+void oracle_keyed_block(uint64_t seed, uint64_t episode, uint32_t idx, uint32_t tag,
+                        uint32_t out[4]) {
+  KeyedStream(seed, episode).block(idx, tag, out);
+}
+void oracle_philox_raw(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]) {
+  Philox4x32::block(ctr, key, out);
+}
+double oracle_cpr_log(double x) { return cpr_log(x); }
+double oracle_u53(uint32_t a, uint32_t b) { return u53(a, b); }
+
+// ---------------- nakamoto_ssz policies / observation encoding
+int oracle_nak_policy(int policy, const int32_t obs[4], const uint8_t* table, int dim) {
+  TablePolicy t;
+  if (policy == POL_TABLE) {
+    t.dim = dim;
+    t.actions.assign(table, table + dim * dim * 2);
+  }
+  NakObs o{obs[0], obs[1], obs[2], obs[3]};
+  return nak_policy(policy, o, &t);
+}
+void oracle_nak_obs_to_floats(const int32_t obs[4], int unit, double out[4]) {
+  NakObs o{obs[0], obs[1], obs[2], obs[3]};
+  nak_obs_to_floats(o, unit != 0, out);
+}
+void oracle_nak_obs_of_floats(const double in[4], int unit, int32_t out[4]) {
+  NakObs o = nak_obs_of_floats(in, unit != 0);
+  out[0] = o.public_blocks;
+  out[1] = o.private_blocks;
+  out[2] = o.diff_blocks;
+  out[3] = o.event;
+}
+
+// ---------------- Simulator.loop task on the two-agents network with an SSZ attacker
+// (experiments/simulate/models.ml:29-46, withholding.ml:90-108, csv_runner.ml:244-265)
+// rng_mode 0: OCaml Random state `rng` (carried over between calls like a Parany worker)
+// rng_mode 1: keyed stream (seed, episode)
+int oracle_two_agents_task(int rng_mode, void* rng, uint64_t seed, uint64_t episode,
+                           double alpha, int policy, int activations, int64_t acts_out[2],
+                           double rewards_out[2], double* head_time, double* head_progress,
+                           int32_t* head_height, uint32_t* diag) {
+  try {
+    Network net = Network::two_agents(1.0, alpha);
+    std::unique_ptr<SimRng> r;
+    if (rng_mode == 0)
+      r.reset(new OcamlSimRng((OcamlRandom*)rng, net));
+    else
+      r.reset(new KeyedSimRng(seed, episode, net));
+    Sim sim(net, r.get());
+    std::vector<std::unique_ptr<NodeImpl>> nodes;
+    auto* att = new NakSszAttackerNode();
+    att->policy = policy;
+    nodes.emplace_back(att);
+    nodes.emplace_back(new NakHonest());
+    sim.init(std::move(nodes));
+    Block* root = sim.roots.back();
+    att->agent.sim = &sim;
+    att->agent.my_id = 0;
+    att->agent.init(root);
+    static_cast<NakHonest*>(sim.nodes[1].get())->state = root;
+    sim.loop(activations);
+    Block* h = sim.head();
+    for (int i = 0; i < 2; i++) {
+      acts_out[i] = sim.activations[i];
+      rewards_out[i] = h->rewards[i];
+    }
+    *head_time = Sim::timestamp(h);
+    *head_progress = (double)h->value.height;
+    *head_height = h->value.height;
+    if (diag) *diag = sim.diag;
+    return 0;
+  } catch (std::exception& e) {
+    set_err(e.what());
+    return -1;
+  }
+}
+
+// ---------------- gym env handle (engine.ml:97-273 for nakamoto_ssz)
+static GymParams params_of(const cpr_config* c) {
+  GymParams p;
+  p.alpha = c->alpha;
+  p.gamma = c->gamma;
+  p.defenders = c->defenders;
+  p.activation_delay = c->activation_delay;
+  p.max_steps = c->max_steps > 0 ? c->max_steps : 0x3fffffffffffffffL;
+  p.max_progress = c->max_progress > 0 ? c->max_progress : 1.0 / 0.0;
+  p.max_time = c->max_time > 0 ? c->max_time : 1.0 / 0.0;
+  p.unit_obs = c->unit_observation != 0;
+  return p;
+}
+
+void* oracle_gym_new(const cpr_config* c, int rng_mode, void* ocaml_rng, uint64_t episode) {
+  try {
+    return new GymNakamoto(params_of(c), rng_mode, (OcamlRandom*)ocaml_rng, c->seed, episode);
+  } catch (std::exception& e) {
+    set_err(e.what());
+    return nullptr;
+  }
+}
+void oracle_gym_free(void* g) { delete (GymNakamoto*)g; }
+
+int oracle_gym_reset(void* g, double obs[4]) {
+  try {
+    ((GymNakamoto*)g)->reset(obs);
+    return 0;
+  } catch (std::exception& e) {
+    set_err(e.what());
+    return -1;
+  }
+}
+
+int oracle_gym_obs_fields(void* g, int32_t out[4]) {
+  NakObs o = ((GymNakamoto*)g)->observe_int();
+  out[0] = o.public_blocks;
+  out[1] = o.private_blocks;
+  out[2] = o.diff_blocks;
+  out[3] = o.event;
+  return 0;
+}
+
+// info_out: 12 doubles in engine.ml:226-237 order + head_height + head_miner
+int oracle_gym_step(void* g, int action, double obs[4], double* reward, int* done,
+                    double info_out[14]) {
+  try {
+    bool d = false;
+    StepInfo i;
+    *reward = ((GymNakamoto*)g)->step(action, obs, &d, &i);
+    *done = d ? 1 : 0;
+    if (info_out) {
+      double v[14] = {i.step_reward_attacker,    i.step_reward_defender,
+                      i.step_progress,           i.step_chain_time,
+                      i.step_sim_time,           i.episode_reward_attacker,
+                      i.episode_reward_defender, i.episode_progress,
+                      i.episode_chain_time,      i.episode_sim_time,
+                      (double)i.episode_n_steps, (double)i.episode_n_activations,
+                      (double)i.head_height,     (double)i.head_miner};
+      memcpy(info_out, v, sizeof(v));
+    }
+    return 0;
+  } catch (std::exception& e) {
+    set_err(e.what());
+    return -1;
+  }
+}
+
+uint32_t oracle_gym_diag(void* g) { return ((GymNakamoto*)g)->sim->diag; }
+
+// ---------------- batch of full episodes (keyed stream), the CPU baseline workload
+static int run_gym_episode(const cpr_config* c, const TablePolicy* tab, uint64_t ep,
+                           cpr_episode_record* rec) {
+  GymNakamoto g(params_of(c), 1, nullptr, c->seed, ep);
+  double obs[4];
+  g.reset(obs);
+  bool done = false;
+  StepInfo info{};
+  while (!done) {
+    int a = nak_policy(c->policy, g.observe_int(), tab);
+    g.step(a, obs, &done, &info);
+  }
+  rec->reward_attacker = info.episode_reward_attacker;
+  rec->reward_defender = info.episode_reward_defender;
+  rec->progress = info.episode_progress;
+  rec->chain_time = info.episode_chain_time;
+  rec->sim_time = info.episode_sim_time;
+  rec->n_steps = info.episode_n_steps;
+  rec->n_activations = info.episode_n_activations;
+  rec->head_height = info.head_height;
+  rec->head_miner = info.head_miner;
+  rec->status = ((g.sim->diag & DIAG_TIE) ? (uint32_t)CPR_ST_TIE : 0u) |
+                ((g.sim->diag & DIAG_OVERLAP) ? (uint32_t)CPR_ST_OVERLAP : 0u);
+  rec->_pad = 0;
+  return 0;
+}
+
+static int run_loop_episode(const cpr_config* c, uint64_t ep, cpr_episode_record* rec) {
+  int64_t acts[2];
+  double rew[2], ht, hp;
+  int32_t hh;
+  uint32_t diag = 0;
+  if (c->network != CPR_NET_TWO_AGENTS) {
+    set_err("oracle loop mode: two-agents network only");
+    return -2;
+  }
+  if (oracle_two_agents_task(1, nullptr, c->seed, ep, c->alpha, c->policy,
+                             (int)c->activations, acts, rew, &ht, &hp, &hh, &diag) != 0)
+    return -1;
+  rec->reward_attacker = rew[0];
+  rec->reward_defender = rew[1];
+  rec->progress = hp;
+  rec->chain_time = ht;
+  rec->sim_time = 0.0;
+  rec->n_steps = 0;
+  rec->n_activations = acts[0] + acts[1];
+  rec->head_height = hh;
+  rec->head_miner = -1;
+  rec->status = 0;
+  rec->_pad = 0;
+  return 0;
+}
+
+// threads: number of worker threads (episode-parallel, like Parany workers)
+int oracle_run_episodes(const cpr_config* c, uint64_t first, int64_t n, cpr_episode_record* out,
+                        int threads) {
+  TablePolicy tab;
+  if (c->policy == POL_TABLE) {
+    tab.dim = c->policy_table_dim;
+    tab.actions.assign(c->policy_table, c->policy_table + tab.dim * tab.dim * 2);
+  }
+  if (threads < 1) threads = 1;
+  std::vector<int> rc(threads, 0);
+  std::vector<std::string> errs(threads);
+  auto work = [&](int t) {
+    try {
+      for (int64_t i = t; i < n; i += threads) {
+        int r = c->mode == CPR_MODE_GYM ? run_gym_episode(c, &tab, first + i, &out[i])
+                                        : run_loop_episode(c, first + i, &out[i]);
+        if (r != 0) {
+          rc[t] = r;
+          errs[t] = g_err;
+          return;
+        }
+      }
+    } catch (std::exception& e) {
+      rc[t] = -1;
+      errs[t] = e.what();
+    }
+  };
+  if (threads == 1)
+    work(0);
+  else {
+    std::vector<std::thread> ts;
+    for (int t = 0; t < threads; t++) ts.emplace_back(work, t);
+    for (auto& th : ts) th.join();
+  }
+  for (int t = 0; t < threads; t++)
+    if (rc[t] != 0) {
+      g_err = errs[t];
+      return rc[t];
+    }
+  return 0;
+}
+
+}  // extern "C"
