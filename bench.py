@@ -1,0 +1,182 @@
+"""Headline benchmark: simulated block activations/s for the Nakamoto SM1 alpha x gamma
+sweep of BASELINE.json configs[1], one process per GPU.
+
+A step = one pass of the sweep: for every (alpha, gamma) point each GPU simulates its own
+E gym episodes of 2016 steps (cpr-nakamoto-v0 semantics: selfish-mining network with
+d = max(2, ceil(1/(1-gamma))) defenders, policy sapirshtein-2016-sm1, 2017 activations per
+episode), fused into one kernel launch per point; the batch summary is integer-exact and
+all-reduced once over RCCL. Weak scaling: E is per GPU.
+
+gamma = 1 is rejected by the reference (gym/ocaml/cpr_gym/envs.py:73-75,
+network.ml:351-354), so the sweep runs gamma in {0, 0.5}.
+
+Prints one JSON line (rank 0).
+"""
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ALPHAS = [0.05, 0.10, 0.15, 0.20, 0.25, 0.30, 0.35, 0.40, 0.45, 0.50]
+GAMMAS = [0.0, 0.5]
+STEPS_PER_EPISODE = 2016
+OPS_PER_ACTIVATION = 40  # build-defined algorithmic VALU cost
+VALU_PEAK_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12  # 256 CU x 4 SIMD32 x 32 lanes/clk x 2.4 GHz
+SEED = 0x5EED0000
+
+
+def cpu_baseline(seconds, points):
+    """The CPU oracle (faithful DES restatement) on the host cores, bounded sample."""
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "tests"))
+    import oracle_py
+    from cpr_amd import device
+
+    try:
+        cores = len(os.sched_getaffinity(0))
+    except AttributeError:
+        cores = os.cpu_count() or 1
+    threads = max(1, min(16, cores))
+    per_point = 4 * threads
+    acts = 0
+    eps = 0
+    t0 = time.perf_counter()
+    i = 0
+    while time.perf_counter() - t0 < seconds:
+        alpha, gamma = points[i % len(points)]
+        cfg, _ = device.make_config(alpha=alpha, gamma=gamma, max_steps=STEPS_PER_EPISODE,
+                                    seed=SEED)
+        rec = oracle_py.run_episodes(cfg, 10**9 + i * per_point, per_point, threads=threads)
+        acts += int(rec["n_activations"].sum())
+        eps += per_point
+        i += 1
+    dt = time.perf_counter() - t0
+    return {
+        "value": acts / dt,
+        "unit": "activations/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": f"{eps} episodes x {STEPS_PER_EPISODE} steps of the same sweep points "
+                  f"({dt:.1f} s, {threads} threads, oracle/src/des.cpp event-driven DES)",
+        "episodes_per_s": eps / dt,
+    }
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--episodes", type=int, default=131072, help="per GPU per sweep point")
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--no-cpu", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+
+    from cpr_amd import _lib as L
+    from cpr_amd import device, parallel
+
+    rank, ws, local = parallel.init("nccl")
+    if ws != args.gpus and rank == 0:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={ws}", file=sys.stderr)
+    torch.cuda.set_device(local)
+    tdev = torch.device("cuda", local)
+    ctx = device.Context(local)
+    points = [(a, g) for g in GAMMAS for a in ALPHAS]
+    batches = []
+    for a, g in points:
+        cfg, keep = device.make_config(alpha=a, gamma=g, max_steps=STEPS_PER_EPISODE, seed=SEED)
+        batches.append(device.Batch(cfg, ctx=ctx, keep=keep))
+    E = args.episodes
+
+    def one_step(step_idx, sums, launches):
+        base = (step_idx * ws + rank) * E  # disjoint episode ids per rank and step
+        for i, b in enumerate(batches):
+            b.run(E, first_episode=base, summary=sums[i])
+            launches.append(b.last_launch())
+
+    for w in range(args.warmup):
+        one_step(10**6 + w, [L.Summary() for _ in points], [])
+    sums = [L.Summary() for _ in points]
+    launches = []
+    parallel.barrier(tdev)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        one_step(k, sums, launches)
+    ctx.synchronize()
+    torch.cuda.synchronize()
+    parallel.barrier(tdev)
+    dt = parallel.allreduce_max(time.perf_counter() - t0, tdev)
+    totals = [parallel.allreduce_summary(s, tdev) for s in sums]
+    acts = sum(int(s.activations) for s in totals)
+    episodes = sum(int(s.episodes) for s in totals)
+
+    # dominant kernel = k_run_episodes; achieved from HIP events on the library's stream
+    kms = np.array([m for m, _ in launches])
+    kacts = np.array([a for _, a in launches], dtype=np.float64)
+    act_per_s_kernel = float(kacts.sum() / (kms.sum() / 1e3))
+    achieved = act_per_s_kernel * OPS_PER_ACTIVATION / 1e12
+    if rank == 0:
+        sweep = {}
+        for (a, g), s in zip(points, totals):
+            st = parallel.summary_stats(s)
+            sweep[f"{a:.2f},{g:.1f}"] = [round(st["mean"], 6), round(st["stderr"], 6)]
+        ties = sum(int(s.status_tie) for s in totals)
+        overlaps = sum(int(s.status_overlap) for s in totals)
+        other = sum(int(s.status_other) for s in totals)
+        out = {
+            "metric": "simulated block activations/sec (whole node) at 1/2/4/8 MI355X; episodes/sec",
+            "value": acts / dt,
+            "unit": "activations/s",
+            "n_gpus": ws,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": dt / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "int32 state machine + f64 event times",
+            "data": "synthetic: keyed Philox4x32-10 stream (DESIGN.md §3), seed 0x5eed0000",
+            "config": {
+                "workload": "BASELINE configs[1]: Nakamoto SM1 (sapirshtein-2016-sm1) selfish "
+                            "mining, alpha 0.05..0.50 x gamma {0, 0.5} (gamma=1 is rejected by "
+                            "the reference), 2016-step cpr-nakamoto-v0 episodes",
+                "episodes_per_point_per_gpu": E,
+                "points": len(points),
+                "activations_per_episode": STEPS_PER_EPISODE + 1,
+                "parallelism": f"dp{ws} (episode shards, 1 RCCL all-reduce of the summary)",
+            },
+            "episodes_per_s": episodes / dt,
+            "roofline": {
+                "bound": "valu",
+                "achieved": achieved,
+                "peak": VALU_PEAK_TOPS,
+                "unit": "Tops/s (VALU lane-ops, 40 ops/activation cost model)",
+                "frac": achieved / VALU_PEAK_TOPS,
+                "traffic": None,
+                "kernel": "k_run_episodes",
+                "kernel_ms_mean": float(kms.mean()),
+                "kernel_activations_per_s": act_per_s_kernel,
+            },
+            "status": {"tie_episodes": ties, "overlap_episodes": overlaps, "other": other},
+            "sweep_mean_rel_revenue": sweep,
+        }
+        if not args.no_cpu and ws == 1:
+            out["cpu_baseline"] = cpu_baseline(args.cpu_seconds, points)
+        print(json.dumps(out), flush=True)
+    for b in batches:
+        b.close()
+    ctx.close()
+    if ws > 1:
+        import torch.distributed as dist
+
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

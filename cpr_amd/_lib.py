@@ -1,0 +1,247 @@
+"""ctypes binding of libcpr_hip (include/cpr_hip.h).
+
+The shared object is built in-tree by ``__graft_entry__.build()`` (hipcc, gfx950). There
+is no fallback: if the library is missing or no HIP device is present, the product path
+raises instead of silently computing anything on the CPU.
+"""
+
+import ctypes
+import os
+import pathlib
+
+import numpy as np
+
+LIB_PATH = pathlib.Path(__file__).resolve().parent / "libcpr_hip.so"
+
+# enums (include/cpr_hip.h)
+CPR_OK = 0
+CPR_E_INVALID_ARG = -1
+CPR_E_UNSUPPORTED = -2
+CPR_E_HIP = -3
+CPR_E_CAPACITY = -4
+CPR_E_STATE = -5
+
+PROTO_NAKAMOTO = 0
+NET_SELFISH_MINING = 0
+NET_TWO_AGENTS = 1
+MODE_GYM = 0
+MODE_LOOP = 1
+
+POLICY_HONEST = 0
+POLICY_SIMPLE = 1
+POLICY_EYAL_SIRER_2014 = 2
+POLICY_SAPIRSHTEIN_2016_SM1 = 3
+POLICY_TABLE = 4
+
+ST_TIE = 1
+ST_OVERLAP = 2
+ST_DEEP_FORK = 4
+ST_TIE_UNRESOLVED = 8
+
+HIST_BINS = 64
+
+
+class Config(ctypes.Structure):
+    _fields_ = [
+        ("protocol", ctypes.c_int32),
+        ("network", ctypes.c_int32),
+        ("mode", ctypes.c_int32),
+        ("policy", ctypes.c_int32),
+        ("policy_table", ctypes.POINTER(ctypes.c_uint8)),
+        ("policy_table_dim", ctypes.c_int32),
+        ("unit_observation", ctypes.c_int32),
+        ("alpha", ctypes.c_double),
+        ("gamma", ctypes.c_double),
+        ("defenders", ctypes.c_int32),
+        ("_pad0", ctypes.c_int32),
+        ("activation_delay", ctypes.c_double),
+        ("propagation_delay", ctypes.c_double),
+        ("max_steps", ctypes.c_int64),
+        ("max_progress", ctypes.c_double),
+        ("max_time", ctypes.c_double),
+        ("activations", ctypes.c_int64),
+        ("seed", ctypes.c_uint64),
+        ("n_lanes", ctypes.c_int64),
+    ]
+
+
+class EpisodeRecord(ctypes.Structure):
+    _fields_ = [
+        ("reward_attacker", ctypes.c_double),
+        ("reward_defender", ctypes.c_double),
+        ("progress", ctypes.c_double),
+        ("chain_time", ctypes.c_double),
+        ("sim_time", ctypes.c_double),
+        ("n_steps", ctypes.c_int64),
+        ("n_activations", ctypes.c_int64),
+        ("head_height", ctypes.c_int32),
+        ("head_miner", ctypes.c_int32),
+        ("status", ctypes.c_uint32),
+        ("_pad", ctypes.c_uint32),
+    ]
+
+
+RECORD_DTYPE = np.dtype(
+    [
+        ("reward_attacker", "<f8"),
+        ("reward_defender", "<f8"),
+        ("progress", "<f8"),
+        ("chain_time", "<f8"),
+        ("sim_time", "<f8"),
+        ("n_steps", "<i8"),
+        ("n_activations", "<i8"),
+        ("head_height", "<i4"),
+        ("head_miner", "<i4"),
+        ("status", "<u4"),
+        ("_pad", "<u4"),
+    ]
+)
+assert RECORD_DTYPE.itemsize == ctypes.sizeof(EpisodeRecord)
+
+
+class Summary(ctypes.Structure):
+    _fields_ = [
+        ("episodes", ctypes.c_int64),
+        ("steps", ctypes.c_int64),
+        ("activations", ctypes.c_int64),
+        ("reward_attacker_fx", ctypes.c_int64),
+        ("reward_defender_fx", ctypes.c_int64),
+        ("progress_fx", ctypes.c_int64),
+        ("rel_revenue_fx", ctypes.c_uint64),
+        ("rel_revenue_sq_fx", ctypes.c_uint64),
+        ("orphans", ctypes.c_int64),
+        ("status_tie", ctypes.c_int64),
+        ("status_overlap", ctypes.c_int64),
+        ("status_other", ctypes.c_int64),
+        ("hist", ctypes.c_int64 * HIST_BINS),
+    ]
+
+    FIELDS = [f for f, _ in _fields_ if f != "hist"]
+
+    def to_array(self):
+        """int64 vector (fields then histogram) — the RCCL all-reduce payload."""
+        head = [getattr(self, f) for f in self.FIELDS]
+        head = [x - (1 << 64) if x >= (1 << 63) else x for x in head]
+        return np.array(head + list(self.hist), dtype=np.int64)
+
+    @classmethod
+    def from_array(cls, a):
+        s = cls()
+        for i, f in enumerate(cls.FIELDS):
+            v = int(a[i])
+            if f.startswith("rel_") and v < 0:
+                v += 1 << 64
+            setattr(s, f, v)
+        for i in range(HIST_BINS):
+            s.hist[i] = int(a[len(cls.FIELDS) + i])
+        return s
+
+    def as_dict(self):
+        d = {f: int(getattr(self, f)) for f in self.FIELDS}
+        d["hist"] = [int(x) for x in self.hist]
+        n = max(1, d["episodes"])
+        d["mean_rel_revenue"] = d["rel_revenue_fx"] / 2**32 / n
+        d["mean_reward_attacker"] = d["reward_attacker_fx"] / 2**20 / n
+        d["mean_progress"] = d["progress_fx"] / 2**20 / n
+        return d
+
+
+class StepInfo(ctypes.Structure):
+    _fields_ = [
+        ("episode_reward_attacker", ctypes.POINTER(ctypes.c_double)),
+        ("episode_reward_defender", ctypes.POINTER(ctypes.c_double)),
+        ("episode_progress", ctypes.POINTER(ctypes.c_double)),
+        ("episode_chain_time", ctypes.POINTER(ctypes.c_double)),
+        ("episode_sim_time", ctypes.POINTER(ctypes.c_double)),
+        ("episode_n_steps", ctypes.POINTER(ctypes.c_int64)),
+        ("episode_n_activations", ctypes.POINTER(ctypes.c_int64)),
+        ("head_height", ctypes.POINTER(ctypes.c_int32)),
+        ("head_miner", ctypes.POINTER(ctypes.c_int32)),
+    ]
+
+
+# every symbol include/cpr_hip.h declares
+EXPORTS = [
+    "cpr_version",
+    "cpr_abi_version",
+    "cpr_last_error",
+    "cpr_ctx_create",
+    "cpr_ctx_destroy",
+    "cpr_device_count",
+    "cpr_batch_create",
+    "cpr_batch_destroy",
+    "cpr_run_episodes",
+    "cpr_run_episodes_async",
+    "cpr_synchronize",
+    "cpr_last_launch",
+    "cpr_reset",
+    "cpr_step",
+    "cpr_observe_fields",
+    "cpr_policy_actions",
+    "cpr_observation_spec",
+    "cpr_policy_count",
+    "cpr_policy_name",
+    "cpr_stream_fill",
+]
+
+
+class CprError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(msg)
+        self.code = code
+
+
+_lib = None
+
+
+def _declare(L):
+    P = ctypes.POINTER
+    vp = ctypes.c_void_p
+    L.cpr_version.restype = ctypes.c_char_p
+    L.cpr_abi_version.restype = ctypes.c_int
+    L.cpr_last_error.restype = ctypes.c_char_p
+    L.cpr_ctx_create.argtypes = [ctypes.c_int, P(vp)]
+    L.cpr_ctx_destroy.argtypes = [vp]
+    L.cpr_device_count.argtypes = [P(ctypes.c_int)]
+    L.cpr_batch_create.argtypes = [vp, P(Config), P(vp)]
+    L.cpr_batch_destroy.argtypes = [vp]
+    L.cpr_run_episodes.argtypes = [vp, ctypes.c_int64, ctypes.c_uint64, P(Summary), vp, ctypes.c_int]
+    L.cpr_run_episodes_async.argtypes = [vp, ctypes.c_int64, ctypes.c_uint64, vp, vp]
+    L.cpr_synchronize.argtypes = [vp]
+    L.cpr_last_launch.argtypes = [vp, P(ctypes.c_double), P(ctypes.c_int64)]
+    L.cpr_reset.argtypes = [vp, vp, vp, vp]
+    L.cpr_step.argtypes = [vp, vp, vp, vp, vp, P(StepInfo)]
+    L.cpr_observe_fields.argtypes = [vp, vp]
+    L.cpr_policy_actions.argtypes = [vp, ctypes.c_int32, vp, ctypes.c_int64, vp]
+    L.cpr_observation_spec.argtypes = [vp, P(ctypes.c_int32), P(ctypes.c_int32), vp, vp]
+    L.cpr_policy_count.argtypes = [ctypes.c_int32]
+    L.cpr_policy_name.restype = ctypes.c_char_p
+    L.cpr_policy_name.argtypes = [ctypes.c_int32, ctypes.c_int32, P(ctypes.c_int32)]
+    L.cpr_stream_fill.argtypes = [
+        vp, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int64, vp, vp
+    ]
+
+
+def lib():
+    """Load libcpr_hip.so (no fallback: raises if it is missing)."""
+    global _lib
+    if _lib is None:
+        path = os.environ.get("CPR_HIP_LIB", str(LIB_PATH))
+        if not os.path.exists(path):
+            raise ImportError(
+                f"libcpr_hip.so not found at {path}; run __graft_entry__.build() (hipcc, gfx950)"
+            )
+        L = ctypes.CDLL(path)
+        _declare(L)
+        _lib = L
+    return _lib
+
+
+def check(rc):
+    if rc != CPR_OK:
+        raise CprError(rc, lib().cpr_last_error().decode())
+    return rc
+
+
+def ptr(a):
+    return ctypes.c_void_p(a.ctypes.data) if a is not None else None

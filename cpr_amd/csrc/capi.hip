@@ -1,0 +1,544 @@
+// libcpr_hip C ABI (include/cpr_hip.h): host side. Validation mirrors the reference's
+// engine.ml:37-51 (Parameters.t) and network.ml:343-358 (selfish_mining) so invalid
+// configurations fail with the same messages; all episode work runs on the device.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/cpr_hip.h"
+#include "kernels.h"
+
+using namespace cpr;
+
+#ifndef CPR_VERSION_STRING
+#define CPR_VERSION_STRING "cpr-hip 0.1.0 (gfx950)"
+#endif
+
+static thread_local std::string g_err;
+
+static int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+#define HIP_TRY(expr)                                                                    \
+  do {                                                                                   \
+    hipError_t e_ = (expr);                                                              \
+    if (e_ != hipSuccess)                                                                \
+      return fail(CPR_E_HIP, std::string(#expr " failed: ") + hipGetErrorString(e_));   \
+  } while (0)
+
+struct cpr_ctx {
+  int device;
+  hipStream_t stream;
+  int cus;
+};
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t bytes = 0;
+  hipError_t ensure(size_t n) {
+    if (n <= bytes) return hipSuccess;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    bytes = 0;
+    hipError_t e = hipMalloc(&p, n);
+    if (e == hipSuccess) bytes = n;
+    return e;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    bytes = 0;
+  }
+};
+
+struct cpr_batch {
+  cpr_ctx* ctx;
+  cpr_config cfg;
+  NakParams P;
+  std::vector<uint8_t> table_host;
+  DevBuf table_dev, tabs_dev;  // policy table; unit-observation tables
+  DevBuf chain_k, chain_t, replay, summary, records;
+  int64_t chain_lanes = 0;
+  // lockstep
+  DevBuf lanes, lchain_k, lchain_t, lreplay, l_obs, l_act, l_rew, l_done, l_mask, l_eps, l_info;
+  bool reset_done = false;
+  int32_t tab_n = 4096;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  double last_ms = 0.0;
+  int64_t last_acts = 0;
+};
+
+extern "C" {
+
+const char* cpr_version(void) { return CPR_VERSION_STRING; }
+int cpr_abi_version(void) { return CPR_ABI_VERSION; }
+const char* cpr_last_error(void) { return g_err.c_str(); }
+
+int cpr_device_count(int* out) {
+  int n = 0;
+  hipError_t e = hipGetDeviceCount(&n);
+  if (e != hipSuccess) return fail(CPR_E_HIP, std::string("hipGetDeviceCount: ") + hipGetErrorString(e));
+  *out = n;
+  return CPR_OK;
+}
+
+int cpr_ctx_create(int device, cpr_ctx** out) {
+  if (!out) return fail(CPR_E_INVALID_ARG, "out is NULL");
+  int n = 0;
+  HIP_TRY(hipGetDeviceCount(&n));
+  if (device < 0 || device >= n) return fail(CPR_E_INVALID_ARG, "no such HIP device");
+  HIP_TRY(hipSetDevice(device));
+  hipDeviceProp_t prop;
+  HIP_TRY(hipGetDeviceProperties(&prop, device));
+  cpr_ctx* c = new cpr_ctx;
+  c->device = device;
+  c->cus = prop.multiProcessorCount;
+  hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+  if (e != hipSuccess) {
+    delete c;
+    return fail(CPR_E_HIP, std::string("hipStreamCreate: ") + hipGetErrorString(e));
+  }
+  *out = c;
+  return CPR_OK;
+}
+
+int cpr_ctx_destroy(cpr_ctx* c) {
+  if (!c) return CPR_OK;
+  (void)hipSetDevice(c->device);
+  (void)hipStreamDestroy(c->stream);
+  delete c;
+  return CPR_OK;
+}
+
+int cpr_synchronize(cpr_ctx* c) {
+  HIP_TRY(hipSetDevice(c->device));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  return CPR_OK;
+}
+
+static uint64_t alpha_threshold(double alpha) {
+  double t = alpha * 4294967296.0;
+  if (t <= 0.0) return 0;
+  if (t >= 4294967296.0) return 4294967296ull;
+  return (uint64_t)t;
+}
+
+// engine.ml:37-51 and network.ml:343-358 (messages kept verbatim)
+static int validate(const cpr_config* c, NakParams* P) {
+  if (c->protocol != CPR_PROTO_NAKAMOTO)
+    return fail(CPR_E_UNSUPPORTED, "protocol not implemented on the device yet");
+  if (std::isnan(c->activation_delay)) return fail(CPR_E_INVALID_ARG, "activation_delay cannot be NaN");
+  if (std::isnan(c->alpha)) return fail(CPR_E_INVALID_ARG, "alpha cannot be NaN");
+  if (std::isnan(c->gamma)) return fail(CPR_E_INVALID_ARG, "gamma cannot be NaN");
+  if (c->alpha < 0. || c->alpha > 1.) return fail(CPR_E_INVALID_ARG, "alpha < 0 || alpha > 1");
+  if (c->gamma < 0. || c->gamma > 1.) return fail(CPR_E_INVALID_ARG, "gamma < 0 || gamma > 1");
+  if (c->activation_delay <= 0.) return fail(CPR_E_INVALID_ARG, "activation_delay <= 0");
+  if (c->mode != CPR_MODE_GYM && c->mode != CPR_MODE_LOOP)
+    return fail(CPR_E_INVALID_ARG, "unknown mode");
+  if (c->policy < CPR_POLICY_HONEST || c->policy > CPR_POLICY_TABLE)
+    return fail(CPR_E_INVALID_ARG, "unknown policy");
+  if (c->policy == CPR_POLICY_TABLE) {
+    if (!c->policy_table || c->policy_table_dim <= 0 || c->policy_table_dim > 256)
+      return fail(CPR_E_INVALID_ARG, "policy table missing or dim out of range (1..256)");
+    for (int i = 0; i < c->policy_table_dim * c->policy_table_dim * 2; i++)
+      if (c->policy_table[i] > 3) return fail(CPR_E_INVALID_ARG, "policy table action out of range");
+  }
+  memset(P, 0, sizeof(*P));
+  P->ev = c->activation_delay;
+  P->t_att = alpha_threshold(c->alpha);
+  P->policy = c->policy;
+  P->table_dim = c->policy_table_dim;
+  if (c->network == CPR_NET_SELFISH_MINING) {
+    if (c->defenders < 1) return fail(CPR_E_INVALID_ARG, "defenders < 0");
+    if (c->defenders < 2) return fail(CPR_E_INVALID_ARG, "defenders must be at least 2");
+    if (c->defenders > 64)
+      return fail(CPR_E_UNSUPPORTED, "device lanes support at most 64 defenders");
+    const double dd = (double)c->defenders;
+    if (c->gamma > (dd - 1.) / dd)
+      return fail(CPR_E_INVALID_ARG, "gamma must not be greater ( (defenders - 1) / defenders )");
+    const double prop = c->propagation_delay > 0 ? c->propagation_delay : 1e-9;
+    P->d = c->defenders;
+    P->delta = prop;
+    P->dmax = (dd - 1.) / dd * prop / c->gamma;
+    P->arrive = std::isfinite(P->dmax) ? 1 : 0;
+    if (c->mode == CPR_MODE_LOOP && !P->arrive)
+      return fail(CPR_E_UNSUPPORTED,
+                  "loop mode with gamma = 0 (messages delivered at t = inf) is not implemented");
+  } else if (c->network == CPR_NET_TWO_AGENTS) {
+    if (c->mode == CPR_MODE_GYM)
+      return fail(CPR_E_UNSUPPORTED, "the gym engine always uses the selfish-mining network");
+    P->d = 1;
+    P->delta = 0.0;
+    P->dmax = 0.0;
+    P->arrive = 1;
+  } else {
+    return fail(CPR_E_INVALID_ARG, "unknown network");
+  }
+  int64_t span;
+  if (c->mode == CPR_MODE_GYM) {
+    const int64_t ms = c->max_steps > 0 ? c->max_steps : INT64_MAX;
+    if (ms <= 0) return fail(CPR_E_INVALID_ARG, "max_steps <= 0");
+    P->max_steps = ms;
+    P->max_progress = c->max_progress > 0 ? c->max_progress : __builtin_inf();
+    P->max_time = c->max_time > 0 ? c->max_time : __builtin_inf();
+    span = ms < (1 << 20) ? ms + 2 : 4096;
+  } else {
+    if (c->activations <= 0) return fail(CPR_E_INVALID_ARG, "activations <= 0");
+    if (c->activations > (1 << 24)) return fail(CPR_E_UNSUPPORTED, "activations > 2^24");
+    P->max_steps = INT64_MAX;
+    P->max_progress = __builtin_inf();
+    P->max_time = __builtin_inf();
+    span = c->activations + 2;
+  }
+  P->cap = (int32_t)(((span + 63) / 64) * 64);
+  return CPR_OK;
+}
+
+int cpr_batch_create(cpr_ctx* ctx, const cpr_config* cfg, cpr_batch** out) {
+  if (!ctx || !cfg || !out) return fail(CPR_E_INVALID_ARG, "NULL argument");
+  NakParams P;
+  int rc = validate(cfg, &P);
+  if (rc) return rc;
+  HIP_TRY(hipSetDevice(ctx->device));
+  cpr_batch* b = new cpr_batch;
+  b->ctx = ctx;
+  b->cfg = *cfg;
+  b->P = P;
+  b->cfg.policy_table = nullptr;
+  if (cfg->policy == CPR_POLICY_TABLE) {
+    const size_t nb = (size_t)cfg->policy_table_dim * cfg->policy_table_dim * 2;
+    b->table_host.assign(cfg->policy_table, cfg->policy_table + nb);
+  }
+  // unit-observation tables (ssz_tools.ml:487-491) evaluated with the host libm
+  std::vector<double> tabs(3 * (size_t)b->tab_n);
+  for (int i = 0; i < b->tab_n; i++) tabs[i] = 2. / M_PI * std::atan((double)i / 1.0);
+  for (int i = 0; i < 2 * b->tab_n; i++)
+    tabs[b->tab_n + i] = 0.5 + (1. / M_PI * std::atan((double)(i - b->tab_n) / 1.0));
+  hipError_t e = b->tabs_dev.ensure(tabs.size() * sizeof(double));
+  if (e == hipSuccess)
+    e = hipMemcpy(b->tabs_dev.p, tabs.data(), tabs.size() * sizeof(double), hipMemcpyHostToDevice);
+  if (e == hipSuccess && !b->table_host.empty()) {
+    e = b->table_dev.ensure(b->table_host.size());
+    if (e == hipSuccess)
+      e = hipMemcpy(b->table_dev.p, b->table_host.data(), b->table_host.size(),
+                    hipMemcpyHostToDevice);
+  }
+  if (e != hipSuccess) {
+    delete b;
+    return fail(CPR_E_HIP, std::string("batch buffers: ") + hipGetErrorString(e));
+  }
+  b->P.table = (const uint8_t*)b->table_dev.p;
+  *out = b;
+  return CPR_OK;
+}
+
+int cpr_last_launch(cpr_batch* b, double* kernel_ms, int64_t* activations) {
+  if (!b) return fail(CPR_E_INVALID_ARG, "NULL argument");
+  if (kernel_ms) *kernel_ms = b->last_ms;
+  if (activations) *activations = b->last_acts;
+  return CPR_OK;
+}
+
+int cpr_batch_destroy(cpr_batch* b) {
+  if (!b) return CPR_OK;
+  (void)hipSetDevice(b->ctx->device);
+  (void)hipStreamSynchronize(b->ctx->stream);
+  if (b->ev0) (void)hipEventDestroy(b->ev0);
+  if (b->ev1) (void)hipEventDestroy(b->ev1);
+  for (DevBuf* d : {&b->table_dev, &b->tabs_dev, &b->chain_k, &b->chain_t, &b->summary,
+                    &b->records, &b->replay, &b->lanes, &b->lchain_k, &b->lchain_t, &b->lreplay, &b->l_obs, &b->l_act,
+                    &b->l_rew, &b->l_done, &b->l_mask, &b->l_eps, &b->l_info})
+    d->release();
+  delete b;
+  return CPR_OK;
+}
+
+// lanes resident per launch: fill every CU with 4 workgroups of 256 lanes, bounded by a
+// 16 GiB budget for the private-chain slots (12 B per slot)
+static int64_t episode_lanes(cpr_batch* b, int64_t n_eps) {
+  const int64_t full = (int64_t)b->ctx->cus * 4 * 256;
+  const int64_t budget = (int64_t)(16ll << 30) / ((int64_t)b->P.cap * 12 + REPLAY_BYTES);
+  int64_t lanes = std::min(full, std::max<int64_t>(256, budget));
+  const int64_t need = ((n_eps + 255) / 256) * 256;
+  lanes = std::min(lanes, need);
+  return std::max<int64_t>(256, (lanes / 256) * 256);
+}
+
+static int run_async(cpr_batch* b, int64_t n, uint64_t first, cpr_summary* sum_dev,
+                     cpr_episode_record* rec_dev) {
+  const int64_t lanes = episode_lanes(b, n);
+  if (lanes > b->chain_lanes) {
+    HIP_TRY(b->chain_k.ensure((size_t)lanes * b->P.cap * sizeof(int32_t)));
+    HIP_TRY(b->chain_t.ensure((size_t)lanes * b->P.cap * sizeof(double)));
+    HIP_TRY(b->replay.ensure((size_t)lanes * REPLAY_BYTES));
+    b->chain_lanes = lanes;
+  }
+  if (!b->ev0) {
+    HIP_TRY(hipEventCreate(&b->ev0));
+    HIP_TRY(hipEventCreate(&b->ev1));
+  }
+  HIP_TRY(hipEventRecord(b->ev0, b->ctx->stream));
+  HIP_TRY(launch_run_episodes(b->P, b->cfg.seed, first, n, b->cfg.mode, b->cfg.activations,
+                              (int32_t*)b->chain_k.p, (double*)b->chain_t.p,
+                              (uint8_t*)b->replay.p, lanes, rec_dev,
+                              sum_dev, b->ctx->stream));
+  HIP_TRY(hipEventRecord(b->ev1, b->ctx->stream));
+  return CPR_OK;
+}
+
+int cpr_run_episodes_async(cpr_batch* b, int64_t n, uint64_t first, cpr_summary* sum_dev,
+                           cpr_episode_record* rec_dev) {
+  if (!b || !sum_dev) return fail(CPR_E_INVALID_ARG, "NULL argument");
+  if (n <= 0) return CPR_OK;
+  HIP_TRY(hipSetDevice(b->ctx->device));
+  return run_async(b, n, first, sum_dev, rec_dev);
+}
+
+int cpr_run_episodes(cpr_batch* b, int64_t n, uint64_t first, cpr_summary* summary,
+                     cpr_episode_record* records, int records_on_device) {
+  if (!b || !summary) return fail(CPR_E_INVALID_ARG, "NULL argument");
+  if (n <= 0) return CPR_OK;
+  HIP_TRY(hipSetDevice(b->ctx->device));
+  hipStream_t st = b->ctx->stream;
+  HIP_TRY(b->summary.ensure(sizeof(cpr_summary)));
+  HIP_TRY(hipMemsetAsync(b->summary.p, 0, sizeof(cpr_summary), st));
+  cpr_episode_record* rec_dev = nullptr;
+  if (records) {
+    if (records_on_device)
+      rec_dev = records;
+    else {
+      HIP_TRY(b->records.ensure((size_t)n * sizeof(cpr_episode_record)));
+      rec_dev = (cpr_episode_record*)b->records.p;
+    }
+  }
+  int rc = run_async(b, n, first, (cpr_summary*)b->summary.p, rec_dev);
+  if (rc) return rc;
+  cpr_summary s;
+  HIP_TRY(hipMemcpyAsync(&s, b->summary.p, sizeof(s), hipMemcpyDeviceToHost, st));
+  if (records && !records_on_device)
+    HIP_TRY(hipMemcpyAsync(records, rec_dev, (size_t)n * sizeof(cpr_episode_record),
+                           hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  float ms = 0.f;
+  HIP_TRY(hipEventElapsedTime(&ms, b->ev0, b->ev1));
+  b->last_ms = ms;
+  b->last_acts = s.activations;
+  summary->episodes += s.episodes;
+  summary->steps += s.steps;
+  summary->activations += s.activations;
+  summary->reward_attacker_fx += s.reward_attacker_fx;
+  summary->reward_defender_fx += s.reward_defender_fx;
+  summary->progress_fx += s.progress_fx;
+  summary->rel_revenue_fx += s.rel_revenue_fx;
+  summary->rel_revenue_sq_fx += s.rel_revenue_sq_fx;
+  summary->orphans += s.orphans;
+  summary->status_tie += s.status_tie;
+  summary->status_overlap += s.status_overlap;
+  summary->status_other += s.status_other;
+  for (int i = 0; i < CPR_HIST_BINS; i++) summary->hist[i] += s.hist[i];
+  return CPR_OK;
+}
+
+// ---------------------------------------------------------------- lockstep API
+
+static int ensure_lockstep(cpr_batch* b) {
+  const int64_t n = b->cfg.n_lanes;
+  if (n <= 0) return fail(CPR_E_STATE, "batch has no lockstep lanes (cfg.n_lanes = 0)");
+  if (b->cfg.mode != CPR_MODE_GYM) return fail(CPR_E_STATE, "lockstep lanes need CPR_MODE_GYM");
+  HIP_TRY(b->lanes.ensure((size_t)n * lock_lane_bytes()));
+  HIP_TRY(b->lchain_k.ensure((size_t)n * b->P.cap * sizeof(int32_t)));
+  HIP_TRY(b->lchain_t.ensure((size_t)n * b->P.cap * sizeof(double)));
+  HIP_TRY(b->lreplay.ensure((size_t)n * REPLAY_BYTES));
+  HIP_TRY(b->l_obs.ensure((size_t)n * 4 * sizeof(double)));
+  HIP_TRY(b->l_act.ensure((size_t)n * sizeof(int32_t)));
+  HIP_TRY(b->l_rew.ensure((size_t)n * sizeof(double)));
+  HIP_TRY(b->l_done.ensure((size_t)n));
+  HIP_TRY(b->l_mask.ensure((size_t)n));
+  HIP_TRY(b->l_eps.ensure((size_t)n * sizeof(uint64_t)));
+  HIP_TRY(b->l_info.ensure((size_t)n * (7 * 8 + 2 * 4)));
+  return CPR_OK;
+}
+
+int cpr_reset(cpr_batch* b, const uint8_t* mask, const uint64_t* eps, double* obs) {
+  if (!b || !obs) return fail(CPR_E_INVALID_ARG, "NULL argument");
+  HIP_TRY(hipSetDevice(b->ctx->device));
+  int rc = ensure_lockstep(b);
+  if (rc) return rc;
+  const int64_t n = b->cfg.n_lanes;
+  hipStream_t st = b->ctx->stream;
+  if (!b->reset_done && mask) {
+    for (int64_t i = 0; i < n; i++)
+      if (!mask[i]) return fail(CPR_E_STATE, "first reset must include every lane");
+  }
+  const uint8_t* dmask = nullptr;
+  const uint64_t* deps = nullptr;
+  if (mask) {
+    HIP_TRY(hipMemcpyAsync(b->l_mask.p, mask, (size_t)n, hipMemcpyHostToDevice, st));
+    dmask = (const uint8_t*)b->l_mask.p;
+  }
+  if (eps) {
+    HIP_TRY(hipMemcpyAsync(b->l_eps.p, eps, (size_t)n * 8, hipMemcpyHostToDevice, st));
+    deps = (const uint64_t*)b->l_eps.p;
+  }
+  const double* tabs = (const double*)b->tabs_dev.p;
+  HIP_TRY(launch_reset(b->P, b->cfg.seed, b->lanes.p, n, dmask, deps, (int32_t*)b->lchain_k.p,
+                       (double*)b->lchain_t.p, b->cfg.unit_observation, tabs, tabs + b->tab_n,
+                       b->tab_n, (double*)b->l_obs.p, st));
+  HIP_TRY(hipMemcpyAsync(obs, b->l_obs.p, (size_t)n * 4 * sizeof(double), hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  b->reset_done = true;
+  return CPR_OK;
+}
+
+int cpr_step(cpr_batch* b, const int32_t* actions, double* obs, double* reward, uint8_t* done,
+             cpr_step_info* info) {
+  if (!b || !actions || !obs || !reward || !done) return fail(CPR_E_INVALID_ARG, "NULL argument");
+  if (!b->reset_done) return fail(CPR_E_STATE, "step before reset");
+  const int64_t n = b->cfg.n_lanes;
+  for (int64_t i = 0; i < n; i++)
+    if (actions[i] < 0 || actions[i] > 3)
+      return fail(CPR_E_INVALID_ARG, "Invalid_argument \"index out of bounds\" (action)");
+  HIP_TRY(hipSetDevice(b->ctx->device));
+  hipStream_t st = b->ctx->stream;
+  HIP_TRY(hipMemcpyAsync(b->l_act.p, actions, (size_t)n * 4, hipMemcpyHostToDevice, st));
+  char* ib = (char*)b->l_info.p;
+  StepBuffers sb;
+  sb.obs = (double*)b->l_obs.p;
+  sb.reward = (double*)b->l_rew.p;
+  sb.done = (uint8_t*)b->l_done.p;
+  sb.era = (double*)(ib);
+  sb.erd = (double*)(ib + n * 8);
+  sb.eprog = (double*)(ib + 2 * n * 8);
+  sb.ect = (double*)(ib + 3 * n * 8);
+  sb.est = (double*)(ib + 4 * n * 8);
+  sb.esteps = (int64_t*)(ib + 5 * n * 8);
+  sb.eacts = (int64_t*)(ib + 6 * n * 8);
+  sb.hh = (int32_t*)(ib + 7 * n * 8);
+  sb.hm = (int32_t*)(ib + 7 * n * 8 + n * 4);
+  const double* tabs = (const double*)b->tabs_dev.p;
+  HIP_TRY(launch_step(b->P, b->cfg.seed, b->lanes.p, n, (const int32_t*)b->l_act.p,
+                      (int32_t*)b->lchain_k.p, (double*)b->lchain_t.p, (uint8_t*)b->lreplay.p,
+                      b->cfg.unit_observation, tabs, tabs + b->tab_n, b->tab_n, sb, st));
+  HIP_TRY(hipMemcpyAsync(obs, sb.obs, (size_t)n * 32, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipMemcpyAsync(reward, sb.reward, (size_t)n * 8, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipMemcpyAsync(done, sb.done, (size_t)n, hipMemcpyDeviceToHost, st));
+  if (info) {
+    struct {
+      void* dst;
+      void* src;
+      size_t sz;
+    } cp[] = {{info->episode_reward_attacker, sb.era, 8},  {info->episode_reward_defender, sb.erd, 8},
+              {info->episode_progress, sb.eprog, 8},       {info->episode_chain_time, sb.ect, 8},
+              {info->episode_sim_time, sb.est, 8},         {info->episode_n_steps, sb.esteps, 8},
+              {info->episode_n_activations, sb.eacts, 8},  {info->head_height, sb.hh, 4},
+              {info->head_miner, sb.hm, 4}};
+    for (auto& x : cp)
+      if (x.dst) HIP_TRY(hipMemcpyAsync(x.dst, x.src, (size_t)n * x.sz, hipMemcpyDeviceToHost, st));
+  }
+  HIP_TRY(hipStreamSynchronize(st));
+  return CPR_OK;
+}
+
+int cpr_observe_fields(cpr_batch* b, int32_t* fields) {
+  if (!b || !fields) return fail(CPR_E_INVALID_ARG, "NULL argument");
+  if (!b->reset_done) return fail(CPR_E_STATE, "observe before reset");
+  const int64_t n = b->cfg.n_lanes;
+  HIP_TRY(hipSetDevice(b->ctx->device));
+  hipStream_t st = b->ctx->stream;
+  DevBuf tmp;
+  HIP_TRY(tmp.ensure((size_t)n * 16));
+  HIP_TRY(launch_observe_fields(b->lanes.p, n, (int32_t*)tmp.p, st));
+  HIP_TRY(hipMemcpyAsync(fields, tmp.p, (size_t)n * 16, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  tmp.release();
+  return CPR_OK;
+}
+
+int cpr_policy_actions(cpr_batch* b, int32_t policy, const double* obs, int64_t n,
+                       int32_t* actions) {
+  if (!b || !obs || !actions) return fail(CPR_E_INVALID_ARG, "NULL argument");
+  if (policy < 0 || policy > CPR_POLICY_TABLE) return fail(CPR_E_INVALID_ARG, "unknown policy");
+  if (policy == CPR_POLICY_TABLE && b->table_host.empty())
+    return fail(CPR_E_INVALID_ARG, "batch has no policy table");
+  if (n <= 0) return CPR_OK;
+  HIP_TRY(hipSetDevice(b->ctx->device));
+  hipStream_t st = b->ctx->stream;
+  DevBuf o, a;
+  HIP_TRY(o.ensure((size_t)n * 32));
+  HIP_TRY(a.ensure((size_t)n * 4));
+  HIP_TRY(hipMemcpyAsync(o.p, obs, (size_t)n * 32, hipMemcpyHostToDevice, st));
+  HIP_TRY(launch_policy(policy, b->cfg.unit_observation, (const double*)o.p, n,
+                        (const uint8_t*)b->table_dev.p, b->cfg.policy_table_dim, (int32_t*)a.p,
+                        st));
+  HIP_TRY(hipMemcpyAsync(actions, a.p, (size_t)n * 4, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  o.release();
+  a.release();
+  return CPR_OK;
+}
+
+// ssz_tools.ml:515-524 ranges; nakamoto_ssz.ml:143-161
+int cpr_observation_spec(cpr_batch* b, int32_t* obs_len, int32_t* n_actions, double* low,
+                         double* high) {
+  if (!b) return fail(CPR_E_INVALID_ARG, "NULL argument");
+  if (obs_len) *obs_len = 4;
+  if (n_actions) *n_actions = 4;
+  const double inf = __builtin_inf();
+  if (b->cfg.unit_observation) {
+    for (int i = 0; i < 4; i++) {
+      if (low) low[i] = 0.0;
+      if (high) high[i] = 1.0;
+    }
+  } else {
+    const double lo[4] = {0.0, 0.0, -inf, 0.0}, hi[4] = {inf, inf, inf, 1.0};
+    for (int i = 0; i < 4; i++) {
+      if (low) low[i] = lo[i];
+      if (high) high[i] = hi[i];
+    }
+  }
+  return CPR_OK;
+}
+
+// Collection.add prepends (collection.ml:13): registry order is the reverse of the adds
+// in nakamoto_ssz.ml:442-450
+static const char* kNames[4] = {"sapirshtein-2016-sm1", "eyal-sirer-2014", "simple", "honest"};
+static const int32_t kIds[4] = {CPR_POLICY_SAPIRSHTEIN_2016_SM1, CPR_POLICY_EYAL_SIRER_2014,
+                                CPR_POLICY_SIMPLE, CPR_POLICY_HONEST};
+
+int cpr_policy_count(int32_t protocol) { return protocol == CPR_PROTO_NAKAMOTO ? 4 : 0; }
+
+const char* cpr_policy_name(int32_t protocol, int32_t index, int32_t* policy_id) {
+  if (protocol != CPR_PROTO_NAKAMOTO || index < 0 || index >= 4) {
+    g_err = "no such policy";
+    return nullptr;
+  }
+  if (policy_id) *policy_id = kIds[index];
+  return kNames[index];
+}
+
+int cpr_stream_fill(cpr_ctx* ctx, uint64_t seed, uint64_t ep, uint32_t idx0, uint32_t tag,
+                    int64_t n, uint32_t* out, double* exp_out) {
+  if (!ctx || !out) return fail(CPR_E_INVALID_ARG, "NULL argument");
+  if (n <= 0) return CPR_OK;
+  HIP_TRY(hipSetDevice(ctx->device));
+  DevBuf o, e;
+  HIP_TRY(o.ensure((size_t)n * 16));
+  if (exp_out) HIP_TRY(e.ensure((size_t)n * 8));
+  HIP_TRY(launch_stream_fill(seed, ep, idx0, tag, n, (uint32_t*)o.p, (double*)e.p, ctx->stream));
+  HIP_TRY(hipMemcpyAsync(out, o.p, (size_t)n * 16, hipMemcpyDeviceToHost, ctx->stream));
+  if (exp_out)
+    HIP_TRY(hipMemcpyAsync(exp_out, e.p, (size_t)n * 8, hipMemcpyDeviceToHost, ctx->stream));
+  HIP_TRY(hipStreamSynchronize(ctx->stream));
+  o.release();
+  e.release();
+  return CPR_OK;
+}
+
+}  // extern "C"

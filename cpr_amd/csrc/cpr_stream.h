@@ -1,0 +1,128 @@
+// Keyed random stream v1, device side.
+//
+// Every draw of the reference (OCaml Random, distributions.ml:17,24,90,93 and
+// simulator.ml:123) is re-addressed by semantic coordinates so one GPU lane can produce
+// exactly the values the CPU oracle's event-driven simulator consumes, whatever order
+// the event queue pops them in:
+//   activation j : Philox4x32-10(ctr = (ep_lo, ep_hi, j, 0), key = seed)
+//                  w0 -> attacker iff w0 < floor(alpha 2^32); w1 -> defender (w1*d)>>32
+//                  w2,w3 -> u53 -> delay = (-1*ev) * cpr_log(u)
+//   link (serial s, dest j) : ctr = (ep, s, TAG_LINK | j>>1), words 2*(j&1),+1 -> u53
+// cpr_log = fdlibm e_log.c (IEEE +,-,*,/ only) so device and host agree bit for bit;
+// this TU must be compiled with -ffp-contract=off.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#pragma clang fp contract(off)
+
+namespace cpr {
+
+constexpr uint32_t TAG_ACT = 0u;
+constexpr uint32_t TAG_LINK = 0x10000000u;
+constexpr uint32_t TAG_POW = 0x20000000u;
+
+struct Words4 {
+  uint32_t w0, w1, w2, w3;
+};
+
+__host__ __device__ inline Words4 philox4x32_10(uint32_t c0, uint32_t c1, uint32_t c2,
+                                                uint32_t c3, uint32_t k0, uint32_t k1) {
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    const uint64_t p0 = (uint64_t)0xD2511F53u * c0;
+    const uint64_t p1 = (uint64_t)0xCD9E8D57u * c2;
+    const uint32_t n0 = (uint32_t)(p1 >> 32) ^ c1 ^ k0;
+    const uint32_t n2 = (uint32_t)(p0 >> 32) ^ c3 ^ k1;
+    c1 = (uint32_t)p1;
+    c3 = (uint32_t)p0;
+    c0 = n0;
+    c2 = n2;
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+  return Words4{c0, c1, c2, c3};
+}
+
+// 53-bit uniform in [0, 1)
+__host__ __device__ inline double u53(uint32_t a, uint32_t b) {
+  return ((double)(a >> 5) * 67108864.0 + (double)(b >> 6)) * (1.0 / 9007199254740992.0);
+}
+
+__host__ __device__ inline double dbits(uint64_t b) { return __builtin_bit_cast(double, b); }
+__host__ __device__ inline uint64_t bitsd(double d) { return __builtin_bit_cast(uint64_t, d); }
+
+// fdlibm __ieee754_log; domain used here: [0, 1)
+__host__ __device__ inline double cpr_log(double x) {
+  const double ln2_hi = dbits(0x3fe62e42fee00000ull);
+  const double ln2_lo = dbits(0x3dea39ef35793c76ull);
+  const double two54 = dbits(0x4350000000000000ull);
+  const double Lg1 = dbits(0x3FE5555555555593ull), Lg2 = dbits(0x3FD999999997FA04ull);
+  const double Lg3 = dbits(0x3FD2492494229359ull), Lg4 = dbits(0x3FCC71C51D8E78AFull);
+  const double Lg5 = dbits(0x3FC7466496CB03DEull), Lg6 = dbits(0x3FC39A09D078C69Full);
+  const double Lg7 = dbits(0x3FC2F112DF3E5244ull);
+  uint64_t ux = bitsd(x);
+  int32_t hx = (int32_t)(ux >> 32);
+  const uint32_t lx = (uint32_t)ux;
+  int32_t k = 0;
+  if (hx < 0x00100000) {
+    if (((hx & 0x7fffffff) | (int32_t)lx) == 0) return -__builtin_inf();
+    if (hx < 0) return __builtin_nan("");
+    k -= 54;
+    x *= two54;
+    ux = bitsd(x);
+    hx = (int32_t)(ux >> 32);
+  }
+  if (hx >= 0x7ff00000) return x + x;
+  k += (hx >> 20) - 1023;
+  hx &= 0x000fffff;
+  int32_t i = (hx + 0x95f64) & 0x100000;
+  ux = ((uint64_t)(uint32_t)(hx | (i ^ 0x3ff00000)) << 32) | (ux & 0xffffffffull);
+  x = dbits(ux);
+  k += (i >> 20);
+  const double f = x - 1.0;
+  double dk, R;
+  if ((0x000fffff & (2 + hx)) < 3) {
+    if (f == 0.0) {
+      if (k == 0) return 0.0;
+      dk = (double)k;
+      return dk * ln2_hi + dk * ln2_lo;
+    }
+    R = f * f * (0.5 - 0.33333333333333333 * f);
+    if (k == 0) return f - R;
+    dk = (double)k;
+    return dk * ln2_hi - ((R - dk * ln2_lo) - f);
+  }
+  const double s = f / (2.0 + f);
+  dk = (double)k;
+  const double z = s * s;
+  i = hx - 0x6147a;
+  const double w = z * z;
+  const int32_t j = 0x6b851 - hx;
+  const double t1 = w * (Lg2 + w * (Lg4 + w * Lg6));
+  const double t2 = z * (Lg1 + w * (Lg3 + w * (Lg5 + w * Lg7)));
+  i |= j;
+  R = t2 + t1;
+  if (i > 0) {
+    const double hfsq = 0.5 * f * f;
+    if (k == 0) return f - (hfsq - s * (hfsq + R));
+    return dk * ln2_hi - ((hfsq - (s * (hfsq + R) + dk * ln2_lo)) - f);
+  }
+  if (k == 0) return f - s * (f - R);
+  return dk * ln2_hi - ((s * (f - R) - dk * ln2_lo) - f);
+}
+
+struct Stream {
+  uint32_t k0, k1;  // seed
+  uint32_t e0, e1;  // episode
+  __host__ __device__ inline Words4 block(uint32_t idx, uint32_t tag) const {
+    return philox4x32_10(e0, e1, idx, tag, k0, k1);
+  }
+  // uniform for the message of block `serial` to node `dest`
+  __host__ __device__ inline double link_u(uint32_t serial, uint32_t dest) const {
+    const Words4 w = block(serial, TAG_LINK | (dest >> 1));
+    return (dest & 1u) ? u53(w.w2, w.w3) : u53(w.w0, w.w1);
+  }
+};
+
+}  // namespace cpr

@@ -1,0 +1,46 @@
+// Host-visible launchers for the gfx950 kernels in kernels.hip.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+#include "../../include/cpr_hip.h"
+#include "nakamoto_lane.h"
+
+namespace cpr {
+
+struct StepBuffers {
+  double* obs;
+  double* reward;
+  uint8_t* done;
+  double* era;
+  double* erd;
+  double* eprog;
+  double* ect;
+  double* est;
+  int64_t* esteps;
+  int64_t* eacts;
+  int32_t* hh;
+  int32_t* hm;
+};
+
+hipError_t launch_run_episodes(const NakParams& P, uint64_t seed, uint64_t first, int64_t n_eps,
+                               int32_t mode, int64_t activations, int32_t* chain_k,
+                               double* chain_t, uint8_t* replay, int64_t lanes,
+                               cpr_episode_record* recs, cpr_summary* sum, hipStream_t st);
+hipError_t launch_reset(const NakParams& P, uint64_t seed, void* lanes, int64_t n,
+                        const uint8_t* mask, const uint64_t* eps, int32_t* chain_k,
+                        double* chain_t, int unit, const double* tab_nn, const double* tab_sg,
+                        int32_t tab_n, double* obs, hipStream_t st);
+hipError_t launch_step(const NakParams& P, uint64_t seed, void* lanes, int64_t n,
+                       const int32_t* actions, int32_t* chain_k, double* chain_t,
+                       uint8_t* replay, int unit, const double* tab_nn, const double* tab_sg,
+                       int32_t tab_n, const StepBuffers& b, hipStream_t st);
+hipError_t launch_observe_fields(const void* lanes, int64_t n, int32_t* f, hipStream_t st);
+hipError_t launch_policy(int32_t policy, int unit, const double* obs, int64_t n,
+                         const uint8_t* table, int32_t dim, int32_t* actions, hipStream_t st);
+hipError_t launch_stream_fill(uint64_t seed, uint64_t ep, uint32_t idx0, uint32_t tag, int64_t n,
+                              uint32_t* out, double* exp_out, hipStream_t st);
+size_t lock_lane_bytes();
+
+}  // namespace cpr

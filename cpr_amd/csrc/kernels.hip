@@ -1,0 +1,385 @@
+// HIP kernels for gfx950 (MI355X): one lane = one independent episode / gym env.
+//
+// Work is integer/branch (VALU) bound; nothing is a contraction, so no MFMA. Per-lane
+// state lives in VGPRs; the private chain (mining activation + time per withheld block)
+// is the only per-lane memory and is touched once per attacker block. Episode outcomes
+// are reduced wave-wide with DPP/shuffle sums, then per workgroup in LDS, then one
+// 64-bit atomic per field per workgroup, all in integer arithmetic so totals are
+// independent of scheduling and of how episodes are sharded over GPUs.
+#include <hip/hip_runtime.h>
+
+#include "../../include/cpr_hip.h"
+#include "kernels.h"
+#include "nakamoto_lane.h"
+
+#pragma clang fp contract(off)
+
+namespace cpr {
+
+constexpr int kBlock = 256;
+
+__device__ inline int64_t wave_sum(int64_t v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+
+struct Acc {
+  int64_t episodes, steps, activations, ra_fx, rd_fx, prog_fx, orphans, tie, overlap, other;
+  uint64_t rel_fx, rel_sq_fx;
+};
+
+__device__ inline void acc_add(Acc& a, const BRef& hd, int64_t steps, int64_t acts,
+                               uint32_t status, int32_t* hist_lds) {
+  a.episodes += 1;
+  a.steps += steps;
+  a.activations += acts;
+  a.ra_fx += (int64_t)hd.ra << 20;
+  a.rd_fx += (int64_t)(hd.h - hd.ra) << 20;
+  a.prog_fx += (int64_t)hd.h << 20;
+  a.orphans += acts - hd.h;
+  a.tie += (status & ST_TIE) ? 1 : 0;
+  a.overlap += (status & ST_OVERLAP) ? 1 : 0;
+  a.other += (status & ~(ST_TIE | ST_OVERLAP)) ? 1 : 0;
+  // wrappers.py:14-26 SparseRelativeRewardWrapper
+  const double rel = hd.h != 0 ? (double)hd.ra / (double)hd.h : 0.0;
+  a.rel_fx += (uint64_t)__builtin_rint(rel * 4294967296.0);
+  a.rel_sq_fx += (uint64_t)__builtin_rint(rel * rel * 4294967296.0);
+  int bin = (int)(rel * (double)CPR_HIST_BINS);
+  bin = bin < 0 ? 0 : (bin >= CPR_HIST_BINS ? CPR_HIST_BINS - 1 : bin);
+  atomicAdd(&hist_lds[bin], 1);
+}
+
+__device__ inline void block_flush(const Acc& a, int32_t* hist_lds, cpr_summary* out) {
+  __shared__ int64_t red[kBlock / 64][12];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  int64_t v[12] = {a.episodes, a.steps,   a.activations, a.ra_fx,
+                   a.rd_fx,    a.prog_fx, a.orphans,     a.tie,
+                   a.overlap,  a.other,   (int64_t)a.rel_fx, (int64_t)a.rel_sq_fx};
+#pragma unroll
+  for (int i = 0; i < 12; ++i) v[i] = wave_sum(v[i]);
+  if (lane == 0)
+#pragma unroll
+    for (int i = 0; i < 12; ++i) red[wave][i] = v[i];
+  __syncthreads();
+  if (threadIdx.x < 12) {
+    int64_t s = 0;
+    for (int w = 0; w < kBlock / 64; ++w) s += red[w][threadIdx.x];
+    unsigned long long* dst;
+    switch (threadIdx.x) {
+      case 0: dst = (unsigned long long*)&out->episodes; break;
+      case 1: dst = (unsigned long long*)&out->steps; break;
+      case 2: dst = (unsigned long long*)&out->activations; break;
+      case 3: dst = (unsigned long long*)&out->reward_attacker_fx; break;
+      case 4: dst = (unsigned long long*)&out->reward_defender_fx; break;
+      case 5: dst = (unsigned long long*)&out->progress_fx; break;
+      case 6: dst = (unsigned long long*)&out->orphans; break;
+      case 7: dst = (unsigned long long*)&out->status_tie; break;
+      case 8: dst = (unsigned long long*)&out->status_overlap; break;
+      case 9: dst = (unsigned long long*)&out->status_other; break;
+      case 10: dst = (unsigned long long*)&out->rel_revenue_fx; break;
+      default: dst = (unsigned long long*)&out->rel_revenue_sq_fx; break;
+    }
+    if (s) atomicAdd(dst, (unsigned long long)s);
+  }
+  if (threadIdx.x < CPR_HIST_BINS && hist_lds[threadIdx.x])
+    atomicAdd((unsigned long long*)&out->hist[threadIdx.x],
+              (unsigned long long)hist_lds[threadIdx.x]);
+}
+
+__device__ inline Stream make_stream(uint64_t seed, uint64_t ep) {
+  Stream S;
+  S.k0 = (uint32_t)seed;
+  S.k1 = (uint32_t)(seed >> 32);
+  S.e0 = (uint32_t)ep;
+  S.e1 = (uint32_t)(ep >> 32);
+  return S;
+}
+
+// One gym episode (engine.ml:164-249): reset = first activation up to the attacker's
+// interaction; step = apply, deliveries, next activation, observe; head at the end.
+__device__ inline BRef run_gym(NakLane& L, const NakParams& P, const Stream& S, const Chain& c,
+                               const ReplayMem& M, int64_t* steps_out) {
+  L.init();
+  L.activate(P, S, c);
+  const bool check_prog = P.max_progress < __builtin_inf();
+  int64_t steps = 0;
+  for (;;) {
+    const int32_t a = L.policy_action(P);
+    L.apply(a);
+    L.resolve(P, S, c, M);
+    L.activate(P, S, c);
+    ++steps;
+    bool go = steps < P.max_steps && L.t < P.max_time;
+    if (check_prog && go) go = (double)L.head(P, c).h < P.max_progress;
+    if (!go) break;
+  }
+  *steps_out = steps;
+  return L.head(P, c);
+}
+
+// Simulator.loop ~activations with the SSZ attacker as node 0 (simulator.ml:519-533,
+// nakamoto_ssz.ml:362-372); all messages delivered before the head is taken.
+__device__ inline BRef run_loop(NakLane& L, const NakParams& P, const Stream& S, const Chain& c,
+                                const ReplayMem& M, int64_t activations) {
+  L.init();
+  for (int64_t i = 0; i < activations; ++i) {
+    L.activate(P, S, c);
+    L.apply(L.policy_action(P));
+    L.resolve(P, S, c, M);
+  }
+  return L.head(P, c);
+}
+
+__global__ __launch_bounds__(kBlock) void k_run_episodes(
+    NakParams P, uint64_t seed, uint64_t first, int64_t n_eps, int32_t mode, int64_t activations,
+    int32_t* chain_k, double* chain_t, uint8_t* replay, cpr_episode_record* recs,
+    cpr_summary* sum) {
+  __shared__ int32_t hist[CPR_HIST_BINS];
+  if (threadIdx.x < CPR_HIST_BINS) hist[threadIdx.x] = 0;
+  __syncthreads();
+  const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t nthreads = (int64_t)gridDim.x * blockDim.x;
+  Chain c;
+  c.k = chain_k + tid * P.cap;
+  c.t = chain_t + tid * P.cap;
+  c.stride = 1;
+  const ReplayMem M = ReplayMem::at(replay + tid * REPLAY_BYTES);
+  Acc acc = {};
+  NakLane L;
+  for (int64_t e = tid; e < n_eps; e += nthreads) {
+    const uint64_t ep = first + (uint64_t)e;
+    const Stream S = make_stream(seed, ep);
+    int64_t steps = 0;
+    BRef hd = mode == CPR_MODE_GYM ? run_gym(L, P, S, c, M, &steps)
+                                    : run_loop(L, P, S, c, M, activations);
+    acc_add(acc, hd, steps, L.k, L.status, hist);
+    if (recs) {
+      cpr_episode_record r;
+      r.reward_attacker = (double)hd.ra;
+      r.reward_defender = (double)(hd.h - hd.ra);
+      r.progress = (double)hd.h;
+      r.chain_time = hd.tm;
+      r.sim_time = mode == CPR_MODE_GYM ? L.t : 0.0;
+      r.n_steps = steps;
+      r.n_activations = L.k;
+      r.head_height = hd.h;
+      r.head_miner = mode == CPR_MODE_GYM ? miner_of(P, S, hd.k) : -1;
+      r.status = L.status;
+      r._pad = 0u;
+      recs[e] = r;
+    }
+  }
+  __syncthreads();
+  block_flush(acc, hist, sum);
+}
+
+// ---- lockstep gym lanes (engine.reset / engine.step over n lanes)
+
+struct LockLane {
+  NakLane L;
+  uint64_t ep;
+  int64_t steps;
+  double last_ra, last_rd, last_prog, last_ct, last_st;
+  int32_t live;
+  int32_t _pad;
+};
+
+__device__ inline void write_obs(const NakLane& L, int unit, const double* tab_nn,
+                                 const double* tab_sg, int32_t tab_n, double* o) {
+  int32_t h, a, d, ev;
+  L.observe(&h, &a, &d, &ev);
+  if (unit) {
+    // ssz_tools.ml:480-491; host-tabulated (libm) for |x| < tab_n
+    o[0] = h < tab_n ? tab_nn[h] : 2.0 / 3.141592653589793 * atan((double)h / 1.0);
+    o[1] = a < tab_n ? tab_nn[a] : 2.0 / 3.141592653589793 * atan((double)a / 1.0);
+    o[2] = (d > -tab_n && d < tab_n) ? tab_sg[d + tab_n]
+                                     : 0.5 + (1.0 / 3.141592653589793 * atan((double)d / 1.0));
+    o[3] = (double)ev / 1.0;
+  } else {
+    o[0] = (double)h;
+    o[1] = (double)a;
+    o[2] = (double)d;
+    o[3] = (double)ev;
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void k_reset(NakParams P, uint64_t seed, LockLane* lanes,
+                                                   int64_t n, const uint8_t* mask,
+                                                   const uint64_t* eps, int32_t* chain_k,
+                                                   double* chain_t, int unit, const double* tab_nn,
+                                                   const double* tab_sg, int32_t tab_n, double* obs) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  LockLane& LL = lanes[i];
+  if (mask == nullptr || mask[i]) {
+    Chain c{chain_k + i * P.cap, chain_t + i * P.cap, 1};
+    NakLane L;
+    L.init();
+    const uint64_t ep = eps ? eps[i] : (uint64_t)i;
+    L.activate(P, make_stream(seed, ep), c);
+    LL.L = L;
+    LL.ep = ep;
+    LL.steps = 0;
+    LL.last_ra = LL.last_rd = LL.last_prog = LL.last_ct = LL.last_st = 0.0;
+    LL.live = 1;
+  }
+  write_obs(LL.L, unit, tab_nn, tab_sg, tab_n, obs + 4 * i);
+}
+
+struct StepOut {
+  double* obs;
+  double* reward;
+  uint8_t* done;
+  double* era;
+  double* erd;
+  double* eprog;
+  double* ect;
+  double* est;
+  int64_t* esteps;
+  int64_t* eacts;
+  int32_t* hh;
+  int32_t* hm;
+};
+
+__global__ __launch_bounds__(kBlock) void k_step(NakParams P, uint64_t seed, LockLane* lanes,
+                                                  int64_t n, const int32_t* actions,
+                                                  int32_t* chain_k, double* chain_t,
+                                                  uint8_t* replay, int unit,
+                                                  const double* tab_nn, const double* tab_sg,
+                                                  int32_t tab_n, StepOut out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  LockLane& LL = lanes[i];
+  NakLane L = LL.L;
+  Chain c{chain_k + i * P.cap, chain_t + i * P.cap, 1};
+  const Stream S = make_stream(seed, LL.ep);
+  const ReplayMem M = ReplayMem::at(replay + i * REPLAY_BYTES);
+  L.apply(actions[i]);
+  L.resolve(P, S, c, M);
+  L.activate(P, S, c);
+  LL.steps += 1;
+  const BRef hd = L.head(P, c);
+  const double progress = (double)hd.h;
+  const bool done = !(LL.steps < P.max_steps && progress < P.max_progress && L.t < P.max_time);
+  const double ra = (double)hd.ra, rd = (double)(hd.h - hd.ra);
+  out.reward[i] = ra - LL.last_ra;  // engine.ml:223
+  out.done[i] = done ? 1 : 0;
+  if (out.era) {
+    out.era[i] = ra;
+    out.erd[i] = rd;
+    out.eprog[i] = progress;
+    out.ect[i] = hd.tm;
+    out.est[i] = L.t;
+    out.esteps[i] = LL.steps;
+    out.eacts[i] = L.k;
+    out.hh[i] = hd.h;
+    out.hm[i] = miner_of(P, S, hd.k);
+  }
+  LL.last_ra = ra;
+  LL.last_rd = rd;
+  LL.last_prog = progress;
+  LL.last_ct = hd.tm;
+  LL.last_st = L.t;
+  LL.L = L;
+  write_obs(L, unit, tab_nn, tab_sg, tab_n, out.obs + 4 * i);
+}
+
+__global__ void k_observe_fields(const LockLane* lanes, int64_t n, int32_t* f) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  lanes[i].L.observe(f + 4 * i, f + 4 * i + 1, f + 4 * i + 2, f + 4 * i + 3);
+}
+
+// engine.ml:258-261: decode the observation (ssz_tools.ml:493-510), apply the policy
+__global__ void k_policy(int32_t policy, int unit, const double* obs, int64_t n,
+                         const uint8_t* table, int32_t dim, int32_t* actions) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const double* o = obs + 4 * i;
+  int32_t h, a, ev;
+  if (unit) {
+    h = (int32_t)__builtin_round(tan(3.141592653589793 / 2.0 * o[0]) * 1.0);
+    a = (int32_t)__builtin_round(tan(3.141592653589793 / 2.0 * o[1]) * 1.0);
+    ev = (int32_t)floor(o[3] * 1.0);
+  } else {
+    h = (int32_t)o[0];
+    a = (int32_t)o[1];
+    ev = (int32_t)o[3];
+  }
+  actions[i] = nak_policy(policy, h, a, ev, table, dim);
+}
+
+__global__ void k_stream_fill(uint64_t seed, uint64_t ep, uint32_t idx0, uint32_t tag, int64_t n,
+                              uint32_t* out, double* exp_out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const Stream S = make_stream(seed, ep);
+  const Words4 w = S.block(idx0 + (uint32_t)i, tag);
+  out[4 * i] = w.w0;
+  out[4 * i + 1] = w.w1;
+  out[4 * i + 2] = w.w2;
+  out[4 * i + 3] = w.w3;
+  if (exp_out) exp_out[i] = (-1.0 * 1.0) * cpr_log(u53(w.w2, w.w3));
+}
+
+// ---------------------------------------------------------------- launchers
+
+hipError_t launch_run_episodes(const NakParams& P, uint64_t seed, uint64_t first, int64_t n_eps,
+                               int32_t mode, int64_t activations, int32_t* chain_k,
+                               double* chain_t, uint8_t* replay, int64_t lanes,
+                               cpr_episode_record* recs, cpr_summary* sum, hipStream_t st) {
+  const int64_t blocks = lanes / kBlock;
+  hipLaunchKernelGGL(k_run_episodes, dim3((unsigned)blocks), dim3(kBlock), 0, st, P, seed, first,
+                     n_eps, mode, activations, chain_k, chain_t, replay, recs, sum);
+  return hipGetLastError();
+}
+
+hipError_t launch_reset(const NakParams& P, uint64_t seed, void* lanes, int64_t n,
+                        const uint8_t* mask, const uint64_t* eps, int32_t* chain_k,
+                        double* chain_t, int unit, const double* tab_nn, const double* tab_sg,
+                        int32_t tab_n, double* obs, hipStream_t st) {
+  const unsigned blocks = (unsigned)((n + kBlock - 1) / kBlock);
+  hipLaunchKernelGGL(k_reset, dim3(blocks), dim3(kBlock), 0, st, P, seed, (LockLane*)lanes, n,
+                     mask, eps, chain_k, chain_t, unit, tab_nn, tab_sg, tab_n, obs);
+  return hipGetLastError();
+}
+
+hipError_t launch_step(const NakParams& P, uint64_t seed, void* lanes, int64_t n,
+                       const int32_t* actions, int32_t* chain_k, double* chain_t,
+                       uint8_t* replay, int unit, const double* tab_nn, const double* tab_sg,
+                       int32_t tab_n, const StepBuffers& b, hipStream_t st) {
+  const unsigned blocks = (unsigned)((n + kBlock - 1) / kBlock);
+  StepOut o{b.obs, b.reward, b.done, b.era, b.erd, b.eprog, b.ect, b.est, b.esteps, b.eacts,
+            b.hh, b.hm};
+  hipLaunchKernelGGL(k_step, dim3(blocks), dim3(kBlock), 0, st, P, seed, (LockLane*)lanes, n,
+                     actions, chain_k, chain_t, replay, unit, tab_nn, tab_sg, tab_n, o);
+  return hipGetLastError();
+}
+
+hipError_t launch_observe_fields(const void* lanes, int64_t n, int32_t* f, hipStream_t st) {
+  const unsigned blocks = (unsigned)((n + kBlock - 1) / kBlock);
+  hipLaunchKernelGGL(k_observe_fields, dim3(blocks), dim3(kBlock), 0, st, (const LockLane*)lanes,
+                     n, f);
+  return hipGetLastError();
+}
+
+hipError_t launch_policy(int32_t policy, int unit, const double* obs, int64_t n,
+                         const uint8_t* table, int32_t dim, int32_t* actions, hipStream_t st) {
+  const unsigned blocks = (unsigned)((n + kBlock - 1) / kBlock);
+  hipLaunchKernelGGL(k_policy, dim3(blocks), dim3(kBlock), 0, st, policy, unit, obs, n, table,
+                     dim, actions);
+  return hipGetLastError();
+}
+
+hipError_t launch_stream_fill(uint64_t seed, uint64_t ep, uint32_t idx0, uint32_t tag, int64_t n,
+                              uint32_t* out, double* exp_out, hipStream_t st) {
+  const unsigned blocks = (unsigned)((n + kBlock - 1) / kBlock);
+  hipLaunchKernelGGL(k_stream_fill, dim3(blocks), dim3(kBlock), 0, st, seed, ep, idx0, tag, n,
+                     out, exp_out);
+  return hipGetLastError();
+}
+
+size_t lock_lane_bytes() { return sizeof(LockLane); }
+
+}  // namespace cpr

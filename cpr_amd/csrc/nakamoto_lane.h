@@ -1,0 +1,597 @@
+// One GPU lane = one gym episode of the nakamoto_ssz attack space (SSZ'16, four actions)
+// on the selfish-mining network the gym builds, or one Simulator.loop task on the
+// two-agents network. The reference runs an event-driven simulator with a DAG, per-node
+// views and a skew-heap event queue (simulator.ml:421-508); for Nakamoto on these
+// networks every outcome-relevant fact fits in a few block references and counters, so
+// the lane is a branch-light integer state machine driven by the keyed stream.
+//
+// What the lane tracks, and the reference code it stands for:
+//   p0, n, rel      attacker private chain = p0 + n withheld/released blocks, released
+//                   prefix rel (nakamoto_ssz.ml:256-360, simulator.ml:401-419 share)
+//   pub             attacker's model of the defender head (deliver_private_to_public,
+//                   nakamoto_ssz.ml:291-318), with its common-ancestor height `fork`
+//   D, A, onA       defender tips: every defender holds D or A (bitmask); honest
+//                   update_head (nakamoto.ml:85-95) with first-received tie breaking
+//   b, wminer       the block of the activation the attacker is reacting to
+//   BRef.ra         attacker reward count along the chain = rewards[0] (simulator.ml:377-388)
+//   BRef.fork       height of the block's common ancestor with the private chain
+//                   (Dagtools.common_ancestor, dagtools.ml:102-121)
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "cpr_stream.h"
+
+#pragma clang fp contract(off)
+
+namespace cpr {
+
+enum : int32_t { A_ADOPT = 0, A_OVERRIDE = 1, A_MATCH = 2, A_WAIT = 3 };
+enum : int32_t { P_HONEST = 0, P_SIMPLE = 1, P_ES2014 = 2, P_SM1 = 3, P_TABLE = 4 };
+enum : uint32_t { ST_TIE = 1u, ST_OVERLAP = 2u, ST_DEEP_FORK = 4u, ST_TIE_UNRESOLVED = 8u };
+
+// ---- exact replay of one delivery window (used only when two deliveries tie in fp64)
+//
+// At every activation the reference's event queue holds exactly one element, the clock
+// (all earlier windows have drained; overlaps are flagged separately). So when a defender
+// receives the fresh defender block and the attacker's matching release at the very same
+// instant, the winner is fixed by replaying this window's events through the same skew
+// heap (orderedQueue.ml:17-47) with the handlers of simulator.ml:421-508. Blocks of the
+// window: x = 0 is the defender block b, x = 1..r the released chain a_rlo..a_rhi.
+constexpr int32_t RCAP = 512;  // heap nodes per lane
+constexpr int32_t RMAX = 16;   // released blocks per window the replay supports
+
+struct ReplayNode {
+  double t;
+  int32_t ev;
+  int16_t l, r;
+};
+
+constexpr int64_t REPLAY_BYTES = 8704;  // RCAP * 16 + 2 * (RMAX + 1) * 8, rounded
+
+struct ReplayMem {
+  ReplayNode* nodes;  // RCAP
+  uint64_t* masks;    // 2 * (RMAX + 1): received, visible per block, bit j-1 = defender j
+  __host__ __device__ static inline ReplayMem at(uint8_t* base) {
+    ReplayMem m;
+    m.nodes = (ReplayNode*)base;
+    m.masks = (uint64_t*)(base + (int64_t)RCAP * sizeof(ReplayNode));
+    return m;
+  }
+};
+
+enum : int32_t { RE_SC = 0, RE_SC2 = 1, RE_DAG = 2, RE_MV = 3, RE_ON = 4, RE_MDV = 5, RE_TX = 6, RE_RX = 7 };
+
+__host__ __device__ inline int32_t re_ev(int32_t ty, int32_t node, int32_t x) {
+  return ty | (node << 3) | (x << 11);
+}
+
+struct SkewHeapLane {
+  ReplayNode* n;
+  int32_t root, freeh, used;
+  bool ok;
+  __host__ __device__ inline int32_t alloc(double t, int32_t ev) {
+    int32_t i;
+    if (freeh >= 0) {
+      i = freeh;
+      freeh = n[i].l;
+    } else if (used < RCAP) {
+      i = used++;
+    } else {
+      ok = false;
+      return -1;
+    }
+    n[i].t = t;
+    n[i].ev = ev;
+    n[i].l = -1;
+    n[i].r = -1;
+    return i;
+  }
+  // orderedQueue.ml:17-26, iterative: new equal-time elements sink below existing ones
+  __host__ __device__ inline void push(double t, int32_t ev) {
+    int32_t parent = -1, side = 0;  // side 0 = left
+    int32_t node = root;
+    for (;;) {
+      if (node < 0) {
+        const int32_t a = alloc(t, ev);
+        if (parent < 0)
+          root = a;
+        else if (side == 0)
+          n[parent].l = (int16_t)a;
+        else
+          n[parent].r = (int16_t)a;
+        return;
+      }
+      if (t < n[node].t) {
+        const double ot = n[node].t;
+        const int32_t oe = n[node].ev;
+        n[node].t = t;
+        n[node].ev = ev;
+        t = ot;
+        ev = oe;
+      } else {
+        const int16_t tmp = n[node].l;
+        n[node].l = n[node].r;
+        n[node].r = tmp;
+      }
+      parent = node;
+      side = 0;
+      node = n[node].l;
+    }
+  }
+  // orderedQueue.ml:28-47 (ties prefer the left subtree)
+  __host__ __device__ inline bool pop(double* t, int32_t* ev) {
+    if (root < 0) return false;
+    *t = n[root].t;
+    *ev = n[root].ev;
+    int32_t parent = -1, side = 0, node = root;
+    for (;;) {
+      const int32_t l = n[node].l, r = n[node].r;
+      int32_t repl = -2;
+      if (r < 0)
+        repl = l;
+      else if (l < 0)
+        repl = r;
+      if (repl != -2) {
+        if (parent < 0)
+          root = repl;
+        else if (side == 0)
+          n[parent].l = (int16_t)repl;
+        else
+          n[parent].r = (int16_t)repl;
+        n[node].l = (int16_t)freeh;
+        freeh = node;
+        return true;
+      }
+      if (n[l].t <= n[r].t) {
+        n[node].t = n[l].t;
+        n[node].ev = n[l].ev;
+        parent = node;
+        side = 0;
+        node = l;
+      } else {
+        n[node].t = n[r].t;
+        n[node].ev = n[r].ev;
+        parent = node;
+        side = 1;
+        node = r;
+      }
+    }
+  }
+};
+
+struct BRef {
+  int32_t h;     // height (nakamoto.ml:11-14)
+  int32_t ra;    // attacker blocks on the chain up to here
+  int32_t k;     // activation index that mined it (DAG serial - 1); -1 = genesis
+  int32_t fork;  // height of the common ancestor with the attacker's private chain
+  double tm;     // mining time = Simulator.timestamp for these networks
+};
+
+struct NakParams {
+  uint64_t t_att;       // floor(alpha * 2^32)
+  int32_t d;            // defenders
+  int32_t arrive;       // attacker messages reach defenders (gamma > 0 or two-agents)
+  double ev;            // activation delay (expected block interval)
+  double delta;         // defender -> defender delay (network.ml:375)
+  double dmax;          // attacker -> defender uniform [0, dmax) (network.ml:350-357)
+  int64_t max_steps;
+  double max_progress;
+  double max_time;
+  int32_t policy;
+  int32_t table_dim;
+  const uint8_t* table;
+  int32_t cap;          // chain slots per lane
+  int32_t _pad;
+};
+
+// per-lane private chain storage, slot m in [1, cap): mining activation and time
+struct Chain {
+  int32_t* k;
+  double* t;
+  int64_t stride;
+  __host__ __device__ inline int32_t getk(int32_t m) const { return k[(int64_t)m * stride]; }
+  __host__ __device__ inline double gett(int32_t m) const { return t[(int64_t)m * stride]; }
+  __host__ __device__ inline void put(int32_t m, int32_t kk, double tt) const {
+    k[(int64_t)m * stride] = kk;
+    t[(int64_t)m * stride] = tt;
+  }
+};
+
+__host__ __device__ inline uint64_t all_mask(int32_t d) {
+  return d >= 64 ? ~0ull : ((1ull << d) - 1ull);
+}
+
+// nakamoto_ssz.ml:374-440 (policy registry: sapirshtein-2016-sm1, eyal-sirer-2014,
+// simple, honest)
+__host__ __device__ inline int32_t nak_policy(int32_t policy, int32_t h, int32_t a, int32_t ev,
+                                              const uint8_t* table, int32_t dim) {
+  switch (policy) {
+    case P_HONEST:
+      return a > h ? A_OVERRIDE : (a < h ? A_ADOPT : A_WAIT);
+    case P_SIMPLE:
+      return h > 0 ? (a < h ? A_ADOPT : A_OVERRIDE) : A_WAIT;
+    case P_ES2014:
+      if (a < h) return A_ADOPT;
+      if (h == 0 && a == 1) return A_WAIT;
+      if (h == 1 && a == 1) return A_MATCH;
+      if (h == 1 && a == 2) return A_OVERRIDE;
+      if (h == 2 && a == 1) return A_ADOPT;
+      if (h > 0) return (a - h == 1) ? A_OVERRIDE : A_MATCH;
+      return A_WAIT;
+    case P_SM1:
+      if (h > a) return A_ADOPT;
+      if (h == 1 && a == 1) return A_MATCH;
+      if (h == a - 1 && h >= 1) return A_OVERRIDE;
+      return A_WAIT;
+    default: {
+      const int32_t hp = h < 0 ? 0 : (h >= dim ? dim - 1 : h);
+      const int32_t ap = a < 0 ? 0 : (a >= dim ? dim - 1 : a);
+      return (int32_t)table[(hp * dim + ap) * 2 + ev];
+    }
+  }
+}
+
+// Replay of a defender-mined window in which the attacker released a_rlo..a_rhi, the top
+// one at the fresh block's height. Returns the set of non-miner defenders that end on the
+// released top (first received wins, nakamoto.ml:85-89). *ok = false on capacity overflow.
+__host__ __device__ inline uint64_t tie_replay(const NakParams& P, const Stream& S, const Chain& c,
+                                               const ReplayMem& M, int32_t miner, double t,
+                                               int32_t rlo, int32_t rhi, bool* ok) {
+  const int32_t r = rhi - rlo + 1;
+  if (r > RMAX) {
+    *ok = false;
+    return 0ull;
+  }
+  uint64_t* recv = M.masks;
+  uint64_t* vis = M.masks + (RMAX + 1);
+  for (int32_t x = 0; x <= r; ++x) recv[x] = vis[x] = 0ull;
+  bool recv0 = false, vis0 = false;
+  uint64_t decided = 0ull, on_top = 0ull;
+  SkewHeapLane H{M.nodes, -1, -1, 0, true};
+  H.push(t, re_ev(RE_SC, 0, 0));
+  double now;
+  int32_t ev;
+  while (H.ok && H.pop(&now, &ev)) {
+    const int32_t ty = ev & 7, j = (ev >> 3) & 255, x = ev >> 11;
+    const uint64_t bit = j ? (1ull << (j - 1)) : 0ull;
+    switch (ty) {
+      case RE_SC:  // StochasticClock: Dag now, next clock later (simulator.ml:465-472)
+        H.push(now, re_ev(RE_DAG, miner, 0));
+        H.push(__builtin_inf(), re_ev(RE_SC2, 0, 0));
+        break;
+      case RE_SC2:
+        *ok = true;
+        return on_top;
+      case RE_DAG:  // append, MakeVisible (:473-480)
+        H.push(now, re_ev(RE_MV, miner, 0));
+        break;
+      case RE_MV: {  // :424-450
+        if (j == 0) {
+          if (!vis0) {
+            vis0 = true;
+            H.push(now, re_ev(RE_ON, 0, 0));
+            H.push(now, re_ev(RE_MDV, 0, 0));
+          }
+          break;
+        }
+        const bool pvis = x <= 1 ? true : ((vis[x - 1] & bit) != 0ull);
+        if (!(vis[x] & bit) && pvis) {
+          vis[x] |= bit;
+          H.push(now, re_ev(RE_ON, j, x));
+          H.push(now, re_ev(RE_MDV, j, x));
+        }
+        break;
+      }
+      case RE_ON:  // :451-464
+        if (j == 0) {
+          // the attacker's interaction; its action shares a_rhi, recursing to a_rlo
+          for (int32_t m = rhi; m >= rlo; --m) H.push(now, re_ev(RE_TX, 0, m - rlo + 1));
+        } else if (j == miner && x == 0) {
+          H.push(now, re_ev(RE_TX, miner, 0));  // honest PoW handler shares b
+        } else if (j != miner && !(decided & bit)) {
+          if (x == 0) {
+            decided |= bit;
+          } else if (x == r) {
+            decided |= bit;
+            on_top |= bit;
+          }
+        }
+        break;
+      case RE_MDV:  // :494-508, children of a_m is a_m+1 only
+        if (j != 0 && x >= 1 && x < r && (recv[x + 1] & bit)) H.push(now, re_ev(RE_MV, j, x + 1));
+        break;
+      case RE_TX:  // :481-487, links in destination order
+        if (x == 0) {
+          H.push(now + 0.0, re_ev(RE_RX, 0, 0));
+          for (int32_t jj = 1; jj <= P.d; ++jj)
+            if (jj != miner) H.push(now + P.delta, re_ev(RE_RX, jj, 0));
+        } else {
+          const uint32_t serial = (uint32_t)(c.getk(rlo + x - 1) + 1);
+          for (int32_t jj = 1; jj <= P.d; ++jj) {
+            const double u = S.link_u(serial, (uint32_t)jj);
+            H.push(now + (u * (P.dmax - 0.0) + 0.0), re_ev(RE_RX, jj, x));
+          }
+        }
+        break;
+      case RE_RX:  // :488-493
+        if (j == 0) {
+          if (!recv0) {
+            recv0 = true;
+            H.push(now, re_ev(RE_MV, 0, 0));
+          }
+        } else if (!(recv[x] & bit)) {
+          recv[x] |= bit;
+          H.push(now, re_ev(RE_MV, j, x));
+        }
+        break;
+    }
+  }
+  *ok = false;
+  return 0ull;
+}
+
+struct NakLane {
+  double t;          // time of the latest activation (clock.now at the interaction)
+  int32_t k;         // activations so far (clock.c_activations)
+  int32_t n;         // private blocks above p0 (observable state)
+  int32_t rel;       // released prefix of the private chain
+  int32_t n_ba;      // private length of the BetweenActions state (attacker's preferred)
+  int32_t pend;      // pending private->public message: chain index, -1 = none
+  int32_t wminer;    // miner of the current window's activation (0 = attacker)
+  int32_t event;     // observation event: 0 ProofOfWork, 1 Network
+  int32_t rlo, rhi;  // chain indices released by the last action
+  uint32_t status;
+  BRef p0, pub, D, A, b;
+  uint64_t onA;      // bit j-1: defender j prefers A (else D)
+  int32_t lca_da;    // height of LCA(D, A)
+  // previous window, for the exact overlap check of the next activation
+  double w_t, w_bound;
+  int32_t w_rlo, w_rhi, w_hasb, w_miner;
+
+  __host__ __device__ inline BRef chain_ref(const Chain& c, int32_t m) const {
+    if (m <= 0) return p0;
+    BRef r;
+    r.h = p0.h + m;
+    r.ra = p0.ra + m;
+    r.k = c.getk(m);
+    r.fork = r.h;
+    r.tm = c.gett(m);
+    return r;
+  }
+
+  __host__ __device__ inline void init() {
+    BRef g;
+    g.h = 0; g.ra = 0; g.k = -1; g.fork = 0; g.tm = 0.0;
+    p0 = pub = D = A = b = g;
+    t = 0.0;
+    k = 0; n = 0; rel = 0; n_ba = 0; pend = -1; wminer = 0; event = 0;
+    rlo = 1; rhi = 0; status = 0u; onA = 0ull; lca_da = 0;
+    w_t = 0.0; w_bound = -__builtin_inf(); w_rlo = 1; w_rhi = 0; w_hasb = 0; w_miner = 0;
+  }
+
+  // latest finite arrival of the previous window (exact; only evaluated when the next
+  // activation lands inside the conservative bound, ~1e-9 of activations in the gym)
+  __host__ __device__ inline double window_last_arrival(const NakParams& P, const Stream& S,
+                                                        const Chain& c) const {
+    double last = -__builtin_inf();
+    if (w_hasb && P.d >= 2) last = w_t + P.delta;
+    if (w_rhi >= w_rlo && P.arrive) {
+      for (int32_t j = 1; j <= P.d; ++j)
+        for (int32_t m = w_rlo; m <= w_rhi; ++m) {
+          const double u = S.link_u((uint32_t)(c.getk(m) + 1), (uint32_t)j);
+          const double a = w_t + (u * (P.dmax - 0.0) + 0.0);
+          last = a > last ? a : last;
+        }
+    }
+    return last;
+  }
+
+  // StochasticClock + Dag + the attacker's prepare (simulator.ml:465-480, engine.ml:108-121,
+  // nakamoto_ssz.ml:291-318)
+  __host__ __device__ inline void activate(const NakParams& P, const Stream& S, const Chain& c) {
+    const Words4 w = S.block((uint32_t)k, TAG_ACT);
+    const double tn = t + (-1.0 * P.ev) * cpr_log(u53(w.w2, w.w3));
+    if (tn <= w_bound) {
+      if (tn <= window_last_arrival(P, S, c)) status |= ST_OVERLAP;
+    }
+    t = tn;
+    const int32_t ka = k;
+    ++k;
+    int32_t miner = 0;
+    if ((uint64_t)w.w0 >= P.t_att) miner = 1 + (int32_t)(((uint64_t)w.w1 * (uint64_t)P.d) >> 32);
+    wminer = miner;
+    // deliver pending releases to the attacker's public model (strict >)
+    if (pend >= 0) {
+      const BRef f = chain_ref(c, pend);
+      if (f.h > pub.h) pub = f;
+    }
+    if (miner == 0) {
+      int32_t m = n + 1;
+      if (m >= P.cap) {
+        status |= ST_DEEP_FORK;
+        m = P.cap - 1;
+      }
+      c.put(m, ka, t);
+      n = m;
+      event = 0;
+    } else {
+      const BRef par = ((onA >> (miner - 1)) & 1ull) ? A : D;
+      b.h = par.h + 1;
+      b.ra = par.ra;
+      b.k = ka;
+      b.fork = par.fork;
+      b.tm = t;
+      if (b.h > pub.h) pub = b;
+      event = 1;
+    }
+    rlo = 1;
+    rhi = 0;
+  }
+
+  __host__ __device__ inline void observe(int32_t* pub_blocks, int32_t* priv_blocks,
+                                          int32_t* diff_blocks, int32_t* ev) const {
+    const int32_t ca = pub.fork;
+    const int32_t ph = p0.h + n;
+    *pub_blocks = pub.h - ca;
+    *priv_blocks = ph - ca;
+    *diff_blocks = ph - pub.h;
+    *ev = event;
+  }
+
+  // Agent.apply (nakamoto_ssz.ml:332-359) + Simulator.handle_action share (:401-419)
+  __host__ __device__ inline void apply(int32_t action) {
+    if (action == A_ADOPT) {
+      const bool pub_on_chain = pub.fork == pub.h;
+      if (wminer != 0 && pub.k == b.k) {
+        b.fork = b.h;  // new private chain = ancestry of the fresh defender block
+      } else if (pub_on_chain) {
+        const int32_t hp = pub.h;
+        D.fork = D.fork < hp ? D.fork : hp;
+        A.fork = A.fork < hp ? A.fork : hp;
+        b.fork = b.fork < hp ? b.fork : hp;
+      } else {  // pub is the off-chain defender tip D
+        D.fork = D.h;
+        A.fork = lca_da;
+      }
+      p0 = pub;
+      p0.fork = p0.h;
+      pub.fork = pub.h;
+      n = 0;
+      rel = 0;
+      pend = -1;
+      n_ba = 0;
+      return;
+    }
+    if (action == A_MATCH || action == A_OVERRIDE) {
+      const int32_t target = pub.h + (action == A_OVERRIDE ? 1 : 0);
+      int32_t mf = target - p0.h;
+      mf = mf < 0 ? 0 : (mf > n ? n : mf);
+      if (mf > rel) {
+        rlo = rel + 1;
+        rhi = mf;
+        rel = mf;
+      }
+      pend = mf;
+      n_ba = n;
+      return;
+    }
+    pend = -1;  // Wait (and any out-of-range action is rejected by the host)
+    n_ba = n;
+  }
+
+  // deliveries of the window: the fresh defender block and the attacker's release reach
+  // the defenders (simulator.ml:481-508 with update_head, nakamoto.ml:85-89)
+  __host__ __device__ inline void resolve(const NakParams& P, const Stream& S, const Chain& c,
+                                          const ReplayMem& M) {
+    const bool released = rhi >= rlo && P.arrive;
+    const uint64_t all = all_mask(P.d);
+    double bound = -__builtin_inf();
+    if (wminer != 0) {
+      if (P.d >= 2) bound = t + P.delta;
+      if (released) {
+        const BRef x = chain_ref(c, rhi);
+        if (x.h > b.h) {
+          A = x;
+          onA = all;
+          lca_da = b.fork;
+        } else if (x.h == b.h) {
+          // race at every defender except the miner: first visible wins
+          const double tb = t + P.delta;
+          uint64_t mask = 0ull;
+          bool tie = false;
+          for (int32_t j = 1; j <= P.d; ++j) {
+            if (j == wminer) continue;
+            double v = -__builtin_inf();
+            for (int32_t m = rlo; m <= rhi; ++m) {
+              const double u = S.link_u((uint32_t)(c.getk(m) + 1), (uint32_t)j);
+              const double a = t + (u * (P.dmax - 0.0) + 0.0);
+              v = a > v ? a : v;
+            }
+            if (v < tb) mask |= 1ull << (j - 1);
+            tie |= v == tb;
+          }
+          if (tie) {
+            // same instant at some defender: the queue order decides
+            status |= ST_TIE;
+            bool ok = false;
+            const uint64_t exact = tie_replay(P, S, c, M, wminer, t, rlo, rhi, &ok);
+            if (ok)
+              mask = exact;
+            else
+              status |= ST_TIE_UNRESOLVED;
+          }
+          A = x;
+          onA = mask;
+          lca_da = b.fork;
+        } else {
+          onA = 0ull;
+        }
+        D = b;
+      } else {
+        D = b;
+        onA = 0ull;
+      }
+    } else if (released) {
+      const BRef x = chain_ref(c, rhi);
+      const int32_t hs = onA ? A.h : D.h;
+      if (x.h > hs) {
+        lca_da = D.fork;
+        A = x;
+        onA = all;
+      }
+    }
+    if (released) {
+      const double ub = t + (P.dmax - 0.0);
+      bound = ub > bound ? ub : bound;
+    }
+    w_t = t;
+    w_bound = bound;
+    w_rlo = rlo;
+    w_rhi = released ? rhi : 0;
+    w_hasb = wminer != 0;
+    w_miner = wminer;
+    wminer = 0;
+    rlo = 1;
+    rhi = 0;
+  }
+
+  // Ref.winner over [attacker preferred; defender tips 1..d] (engine.ml:195-206,
+  // nakamoto.ml:43-48): first maximal height, attacker listed first
+  __host__ __device__ inline BRef head(const NakParams& P, const Chain& c) const {
+    BRef best = chain_ref(c, n_ba);
+    const uint64_t all = all_mask(P.d);
+    const uint64_t mb = wminer ? (1ull << (wminer - 1)) : 0ull;
+    const uint64_t ma = onA & ~mb;
+    const uint64_t md = all & ~onA & ~mb;
+    int32_t bh = -1, bj = 1 << 30;
+    BRef cand = best;
+    if (wminer) { bh = b.h; bj = wminer; cand = b; }
+    if (ma) {
+      const int32_t j = 1 + __builtin_ctzll(ma);
+      if (A.h > bh || (A.h == bh && j < bj)) { bh = A.h; bj = j; cand = A; }
+    }
+    if (md) {
+      const int32_t j = 1 + __builtin_ctzll(md);
+      if (D.h > bh || (D.h == bh && j < bj)) { bh = D.h; bj = j; cand = D; }
+    }
+    if (bh > best.h) best = cand;
+    return best;
+  }
+
+  __host__ __device__ inline int32_t policy_action(const NakParams& P) const {
+    int32_t h, a, dd, ev;
+    observe(&h, &a, &dd, &ev);
+    return nak_policy(P.policy, h, a, ev, P.table, P.table_dim);
+  }
+};
+
+// miner of activation index ka (for head_miner of the record)
+__host__ __device__ inline int32_t miner_of(const NakParams& P, const Stream& S, int32_t ka) {
+  if (ka < 0) return -1;
+  const Words4 w = S.block((uint32_t)ka, TAG_ACT);
+  if ((uint64_t)w.w0 < P.t_att) return 0;
+  return 1 + (int32_t)(((uint64_t)w.w1 * (uint64_t)P.d) >> 32);
+}
+
+}  // namespace cpr

@@ -1,0 +1,237 @@
+"""Device contexts and episode batches over libcpr_hip.
+
+A ``Context`` is one HIP device (one process per GPU, see ``cpr_amd.parallel``); a
+``Batch`` is one configuration of the episode engine (protocol, network, attack policy,
+alpha/gamma, termination) on that device. ``Batch.run`` fuses the reference's Python
+reset/step/policy loop (gym/ocaml/test/test_benchmark.py:5-15, rl-eval) into one kernel
+launch; ``Batch.reset``/``Batch.step`` expose the per-step gym API over many lanes.
+"""
+
+import ctypes
+import math
+import os
+
+import numpy as np
+
+from . import _lib as L
+
+_default_ctx = {}
+
+
+class Context:
+    def __init__(self, device=0):
+        self.device = device
+        h = ctypes.c_void_p()
+        L.check(L.lib().cpr_ctx_create(device, ctypes.byref(h)))
+        self.handle = h
+
+    def close(self):
+        if self.handle:
+            L.lib().cpr_ctx_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def synchronize(self):
+        L.check(L.lib().cpr_synchronize(self.handle))
+
+    def stream_fill(self, seed, episode, idx0, tag, n, with_exp=False):
+        """Keyed-stream Philox blocks computed on the device."""
+        out = np.zeros((n, 4), dtype=np.uint32)
+        ex = np.zeros(n, dtype=np.float64) if with_exp else None
+        L.check(
+            L.lib().cpr_stream_fill(
+                self.handle, seed, episode, idx0, tag, n, L.ptr(out), L.ptr(ex) if with_exp else None
+            )
+        )
+        return (out, ex) if with_exp else out
+
+
+def default_context():
+    dev = int(os.environ.get("LOCAL_RANK", "0"))
+    if dev not in _default_ctx:
+        n = ctypes.c_int()
+        L.check(L.lib().cpr_device_count(ctypes.byref(n)))
+        if n.value == 0:
+            raise RuntimeError("cpr_amd: no HIP device visible")
+        _default_ctx[dev] = Context(dev % n.value)
+    return _default_ctx[dev]
+
+
+def make_config(
+    alpha,
+    gamma=0.5,
+    defenders=None,
+    policy=L.POLICY_SAPIRSHTEIN_2016_SM1,
+    network=L.NET_SELFISH_MINING,
+    mode=L.MODE_GYM,
+    activation_delay=1.0,
+    propagation_delay=1e-9,
+    max_steps=None,
+    max_progress=None,
+    max_time=None,
+    activations=0,
+    seed=0,
+    unit_observation=True,
+    n_lanes=0,
+    table=None,
+):
+    """Build a cpr_config. ``defenders=None`` applies the gym's rule
+    d = max(2, ceil(1 / (1 - gamma))) (gym/ocaml/cpr_gym/envs.py:146-153)."""
+    if defenders is None and network == L.NET_SELFISH_MINING:
+        if gamma >= 1:
+            raise ValueError("gamma must be smaller than 1")
+        defenders = max(2, int(math.ceil(1 / (1 - gamma))))
+    c = L.Config()
+    c.protocol = L.PROTO_NAKAMOTO
+    c.network = network
+    c.mode = mode
+    c.policy = policy
+    c.unit_observation = 1 if unit_observation else 0
+    c.alpha = alpha
+    c.gamma = gamma
+    c.defenders = defenders or 1
+    c.activation_delay = activation_delay
+    c.propagation_delay = propagation_delay
+    c.max_steps = 0 if max_steps is None else int(max_steps)
+    c.max_progress = 0.0 if max_progress is None else float(max_progress)
+    c.max_time = 0.0 if max_time is None else float(max_time)
+    c.activations = int(activations)
+    c.seed = int(seed) & ((1 << 64) - 1)
+    c.n_lanes = int(n_lanes)
+    keep = None
+    if table is not None:
+        keep = np.ascontiguousarray(table, dtype=np.uint8)
+        dim = int(round((keep.size // 2) ** 0.5))
+        if dim * dim * 2 != keep.size:
+            raise ValueError("policy table must have dim*dim*2 entries")
+        c.policy = L.POLICY_TABLE
+        c.policy_table = keep.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8))
+        c.policy_table_dim = dim
+    return c, keep
+
+
+class Batch:
+    def __init__(self, config, ctx=None, keep=None):
+        self.ctx = ctx or default_context()
+        self.config = config
+        self._keep = keep
+        h = ctypes.c_void_p()
+        L.check(L.lib().cpr_batch_create(self.ctx.handle, ctypes.byref(config), ctypes.byref(h)))
+        self.handle = h
+        self.n_lanes = int(config.n_lanes)
+
+    def close(self):
+        if self.handle:
+            L.lib().cpr_batch_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ---- fused episodes
+    def run(self, n_episodes, first_episode=0, records=False, summary=None):
+        s = summary if summary is not None else L.Summary()
+        rec = np.zeros(n_episodes, dtype=L.RECORD_DTYPE) if records else None
+        L.check(
+            L.lib().cpr_run_episodes(
+                self.handle, n_episodes, first_episode, ctypes.byref(s), L.ptr(rec), 0
+            )
+        )
+        return (s, rec) if records else s
+
+    def last_launch(self):
+        """(kernel_ms, activations) of the last fused-episode launch (HIP events)."""
+        ms = ctypes.c_double()
+        acts = ctypes.c_int64()
+        L.check(L.lib().cpr_last_launch(self.handle, ctypes.byref(ms), ctypes.byref(acts)))
+        return ms.value, acts.value
+
+    def run_async(self, n_episodes, first_episode, summary_dev_ptr, records_dev_ptr=None):
+        L.check(
+            L.lib().cpr_run_episodes_async(
+                self.handle, n_episodes, first_episode, summary_dev_ptr, records_dev_ptr
+            )
+        )
+
+    # ---- lockstep gym lanes
+    def reset(self, mask=None, episode_ids=None):
+        obs = np.zeros((self.n_lanes, 4), dtype=np.float64)
+        m = None if mask is None else np.ascontiguousarray(mask, dtype=np.uint8)
+        e = None if episode_ids is None else np.ascontiguousarray(episode_ids, dtype=np.uint64)
+        L.check(L.lib().cpr_reset(self.handle, L.ptr(m), L.ptr(e), L.ptr(obs)))
+        return obs
+
+    def step(self, actions, with_info=True):
+        n = self.n_lanes
+        a = np.ascontiguousarray(actions, dtype=np.int32)
+        obs = np.zeros((n, 4), dtype=np.float64)
+        rew = np.zeros(n, dtype=np.float64)
+        done = np.zeros(n, dtype=np.uint8)
+        info = None
+        si = None
+        if with_info:
+            info = {
+                "episode_reward_attacker": np.zeros(n),
+                "episode_reward_defender": np.zeros(n),
+                "episode_progress": np.zeros(n),
+                "episode_chain_time": np.zeros(n),
+                "episode_sim_time": np.zeros(n),
+                "episode_n_steps": np.zeros(n, dtype=np.int64),
+                "episode_n_activations": np.zeros(n, dtype=np.int64),
+                "head_height": np.zeros(n, dtype=np.int32),
+                "head_miner": np.zeros(n, dtype=np.int32),
+            }
+            si = L.StepInfo()
+            for k, v in info.items():
+                ct = np.ctypeslib.as_ctypes_type(v.dtype)
+                setattr(si, k, v.ctypes.data_as(ctypes.POINTER(ct)))
+        L.check(
+            L.lib().cpr_step(
+                self.handle, L.ptr(a), L.ptr(obs), L.ptr(rew), L.ptr(done),
+                ctypes.byref(si) if si is not None else None,
+            )
+        )
+        return obs, rew, done.astype(bool), info
+
+    def observe_fields(self):
+        f = np.zeros((self.n_lanes, 4), dtype=np.int32)
+        L.check(L.lib().cpr_observe_fields(self.handle, L.ptr(f)))
+        return f
+
+    def policy_actions(self, policy, obs):
+        o = np.ascontiguousarray(np.atleast_2d(obs), dtype=np.float64)
+        if o.shape[1] != 4:
+            raise ValueError("invalid dimensions")
+        out = np.zeros(o.shape[0], dtype=np.int32)
+        L.check(L.lib().cpr_policy_actions(self.handle, policy, L.ptr(o), o.shape[0], L.ptr(out)))
+        return out
+
+    def observation_spec(self):
+        ol = ctypes.c_int32()
+        na = ctypes.c_int32()
+        low = np.zeros(4)
+        high = np.zeros(4)
+        L.check(
+            L.lib().cpr_observation_spec(
+                self.handle, ctypes.byref(ol), ctypes.byref(na), L.ptr(low), L.ptr(high)
+            )
+        )
+        return ol.value, na.value, low, high
+
+
+def policy_registry(protocol=L.PROTO_NAKAMOTO):
+    """[(name, id)] in the reference's registry order (nakamoto_ssz.ml:442-450)."""
+    out = []
+    for i in range(L.lib().cpr_policy_count(protocol)):
+        pid = ctypes.c_int32()
+        name = L.lib().cpr_policy_name(protocol, i, ctypes.byref(pid))
+        out.append((name.decode(), pid.value))
+    return out

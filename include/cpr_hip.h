@@ -176,6 +176,9 @@ int cpr_run_episodes(cpr_batch* b, int64_t n_episodes, uint64_t first_episode,
 int cpr_run_episodes_async(cpr_batch* b, int64_t n_episodes, uint64_t first_episode,
                            cpr_summary* summary_dev, cpr_episode_record* records_dev);
 int cpr_synchronize(cpr_ctx* ctx);
+/* device time (HIP events on the context's stream) of the last episode-kernel launch of
+ * this batch, and the activations it simulated (valid after cpr_run_episodes returns) */
+int cpr_last_launch(cpr_batch* b, double* kernel_ms, int64_t* activations);
 
 /* Lockstep env API over cfg->n_lanes lanes (host pointers).
  * reset: lanes with mask[i] != 0 (mask NULL = all) start episode episode_ids[i]

@@ -1,0 +1,216 @@
+"""ctypes binding of the CPU oracle (oracle/build/liboracle.so) — TEST INFRASTRUCTURE.
+
+The oracle is the checker: a faithful C++ restatement of the reference DES
+(oracle/src/des.h). Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline
+leg load it.
+"""
+
+import ctypes
+import pathlib
+import subprocess
+
+import numpy as np
+
+ROOT = pathlib.Path(__file__).resolve().parent.parent
+LIB = ROOT / "oracle" / "build" / "liboracle.so"
+
+_lib = None
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", str(ROOT / "oracle")], check=True)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not LIB.exists():
+            build()
+        import sys
+
+        sys.path.insert(0, str(ROOT))
+        from cpr_amd import _lib as C  # struct layouts only (no GPU needed)
+
+        L = ctypes.CDLL(str(LIB))
+        P = ctypes.POINTER
+        vp = ctypes.c_void_p
+        L.oracle_last_error.restype = ctypes.c_char_p
+        L.oracle_ocaml_rng_new.restype = vp
+        L.oracle_ocaml_rng_new.argtypes = [ctypes.c_long]
+        L.oracle_ocaml_rng_free.argtypes = [vp]
+        L.oracle_ocaml_rng_bits.argtypes = [vp]
+        L.oracle_ocaml_rng_int.argtypes = [vp, ctypes.c_int32]
+        L.oracle_ocaml_rng_float.argtypes = [vp, ctypes.c_double]
+        L.oracle_ocaml_rng_float.restype = ctypes.c_double
+        L.oracle_keyed_block.argtypes = [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32,
+                                         ctypes.c_uint32, vp]
+        L.oracle_philox_raw.argtypes = [vp, vp, vp]
+        L.oracle_cpr_log.argtypes = [ctypes.c_double]
+        L.oracle_cpr_log.restype = ctypes.c_double
+        L.oracle_u53.argtypes = [ctypes.c_uint32, ctypes.c_uint32]
+        L.oracle_u53.restype = ctypes.c_double
+        L.oracle_nak_policy.argtypes = [ctypes.c_int, vp, vp, ctypes.c_int]
+        L.oracle_nak_obs_to_floats.argtypes = [vp, ctypes.c_int, vp]
+        L.oracle_nak_obs_of_floats.argtypes = [vp, ctypes.c_int, vp]
+        L.oracle_two_agents_task.argtypes = [
+            ctypes.c_int, vp, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_double, ctypes.c_int,
+            ctypes.c_int, vp, vp, P(ctypes.c_double), P(ctypes.c_double), P(ctypes.c_int32),
+            P(ctypes.c_uint32),
+        ]
+        L.oracle_gym_new.restype = vp
+        L.oracle_gym_new.argtypes = [P(C.Config), ctypes.c_int, vp, ctypes.c_uint64]
+        L.oracle_gym_free.argtypes = [vp]
+        L.oracle_gym_reset.argtypes = [vp, vp]
+        L.oracle_gym_obs_fields.argtypes = [vp, vp]
+        L.oracle_gym_step.argtypes = [vp, ctypes.c_int, vp, P(ctypes.c_double), P(ctypes.c_int), vp]
+        L.oracle_gym_diag.argtypes = [vp]
+        L.oracle_gym_diag.restype = ctypes.c_uint32
+        L.oracle_run_episodes.argtypes = [P(C.Config), ctypes.c_uint64, ctypes.c_int64, vp,
+                                          ctypes.c_int]
+        _lib = L
+    return _lib
+
+
+def check(rc):
+    if rc != 0:
+        raise RuntimeError(lib().oracle_last_error().decode())
+
+
+class OcamlRandom:
+    def __init__(self, seed=-1):
+        self.h = lib().oracle_ocaml_rng_new(seed)
+
+    def __del__(self):
+        try:
+            lib().oracle_ocaml_rng_free(self.h)
+        except Exception:
+            pass
+
+    def bits(self):
+        return lib().oracle_ocaml_rng_bits(self.h)
+
+    def int(self, n):
+        return lib().oracle_ocaml_rng_int(self.h, n)
+
+    def float(self, b):
+        return lib().oracle_ocaml_rng_float(self.h, b)
+
+
+POLICIES = {"honest": 0, "simple": 1, "eyal-sirer-2014": 2, "sapirshtein-2016-sm1": 3}
+
+
+def two_agents_task(alpha, policy, activations, rng=None, seed=0, episode=0):
+    """Simulator.loop task (csv_runner.ml:244-265) on the two-agents network."""
+    acts = np.zeros(2, dtype=np.int64)
+    rew = np.zeros(2, dtype=np.float64)
+    ht, hp = ctypes.c_double(), ctypes.c_double()
+    hh, dg = ctypes.c_int32(), ctypes.c_uint32()
+    mode = 0 if rng is not None else 1
+    check(
+        lib().oracle_two_agents_task(
+            mode, rng.h if rng is not None else None, seed, episode, alpha,
+            POLICIES.get(policy, policy), activations, acts.ctypes.data, rew.ctypes.data,
+            ctypes.byref(ht), ctypes.byref(hp), ctypes.byref(hh), ctypes.byref(dg),
+        )
+    )
+    return dict(activations=acts.tolist(), reward=rew.tolist(), head_time=ht.value,
+                head_progress=hp.value, head_height=hh.value, diag=dg.value)
+
+
+def keyed_block(seed, episode, idx, tag):
+    out = np.zeros(4, dtype=np.uint32)
+    lib().oracle_keyed_block(seed, episode, idx, tag, out.ctypes.data)
+    return out
+
+
+def philox(ctr, key):
+    c = np.asarray(ctr, dtype=np.uint32)
+    k = np.asarray(key, dtype=np.uint32)
+    out = np.zeros(4, dtype=np.uint32)
+    lib().oracle_philox_raw(c.ctypes.data, k.ctypes.data, out.ctypes.data)
+    return out
+
+
+def cpr_log(x):
+    return lib().oracle_cpr_log(x)
+
+
+def u53(a, b):
+    return lib().oracle_u53(a, b)
+
+
+def nak_policy(policy, obs_fields, table=None):
+    o = np.asarray(obs_fields, dtype=np.int32)
+    if table is not None:
+        t = np.ascontiguousarray(table, dtype=np.uint8)
+        dim = int(round((t.size // 2) ** 0.5))
+        return lib().oracle_nak_policy(policy, o.ctypes.data, t.ctypes.data, dim)
+    return lib().oracle_nak_policy(policy, o.ctypes.data, None, 0)
+
+
+def obs_to_floats(fields, unit):
+    o = np.asarray(fields, dtype=np.int32)
+    out = np.zeros(4)
+    lib().oracle_nak_obs_to_floats(o.ctypes.data, 1 if unit else 0, out.ctypes.data)
+    return out
+
+
+def obs_of_floats(floats, unit):
+    f = np.asarray(floats, dtype=np.float64)
+    out = np.zeros(4, dtype=np.int32)
+    lib().oracle_nak_obs_of_floats(f.ctypes.data, 1 if unit else 0, out.ctypes.data)
+    return out
+
+
+class GymEnv:
+    """The oracle's engine.ml restatement (one env, keyed stream or OCaml Random)."""
+
+    INFO_KEYS = [
+        "step_reward_attacker", "step_reward_defender", "step_progress", "step_chain_time",
+        "step_sim_time", "episode_reward_attacker", "episode_reward_defender",
+        "episode_progress", "episode_chain_time", "episode_sim_time", "episode_n_steps",
+        "episode_n_activations", "head_height", "head_miner",
+    ]
+
+    def __init__(self, config, episode=0, ocaml_rng=None):
+        self.cfg = config
+        self.h = lib().oracle_gym_new(ctypes.byref(config), 0 if ocaml_rng else 1,
+                                      ocaml_rng.h if ocaml_rng else None, episode)
+        if not self.h:
+            raise ValueError(lib().oracle_last_error().decode())
+
+    def __del__(self):
+        try:
+            lib().oracle_gym_free(self.h)
+        except Exception:
+            pass
+
+    def reset(self):
+        obs = np.zeros(4)
+        check(lib().oracle_gym_reset(self.h, obs.ctypes.data))
+        return obs
+
+    def fields(self):
+        f = np.zeros(4, dtype=np.int32)
+        lib().oracle_gym_obs_fields(self.h, f.ctypes.data)
+        return f
+
+    def step(self, action):
+        obs = np.zeros(4)
+        r = ctypes.c_double()
+        d = ctypes.c_int()
+        info = np.zeros(14)
+        check(lib().oracle_gym_step(self.h, int(action), obs.ctypes.data, ctypes.byref(r),
+                                    ctypes.byref(d), info.ctypes.data))
+        return obs, r.value, bool(d.value), dict(zip(self.INFO_KEYS, info.tolist()))
+
+    def diag(self):
+        return lib().oracle_gym_diag(self.h)
+
+
+def run_episodes(config, first, n, threads=1):
+    from cpr_amd import _lib as C
+
+    rec = np.zeros(n, dtype=C.RECORD_DTYPE)
+    check(lib().oracle_run_episodes(ctypes.byref(config), first, n, rec.ctypes.data, threads))
+    return rec

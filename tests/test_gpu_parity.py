@@ -1,0 +1,199 @@
+"""Parity of the HIP path (through the C ABI) with the CPU oracle — needs an MI355X.
+
+Integer/index results must be bit-identical; event times (f64) too, because both sides
+evaluate the keyed stream and the clock with the same IEEE operation sequence
+(-ffp-contract=off, fdlibm log). Observation floats of the lockstep API are compared
+exactly as well (host-tabulated libm atan on both sides).
+"""
+
+import math
+
+import numpy as np
+import pytest
+
+import oracle_py as O
+from cpr_amd import _lib as L
+from cpr_amd import device
+
+pytestmark = pytest.mark.gpu
+
+FIELDS = [f for f in L.RECORD_DTYPE.names if f != "_pad"]
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    return device.default_context()
+
+
+def _records_equal(a, b):
+    bad = {}
+    for f in FIELDS:
+        neq = np.nonzero(a[f] != b[f])[0]
+        if len(neq):
+            bad[f] = (int(neq[0]), a[f][neq[0]], b[f][neq[0]], len(neq))
+    return bad
+
+
+def test_stream_fill_matches_oracle(ctx):
+    for seed, ep, tag in [(0, 0, 0), (0x5EED0000, 12345, 0), (2**63 + 7, 2**40 + 3, 0x10000002)]:
+        blocks, ex = ctx.stream_fill(seed, ep, 17, tag, 4096, with_exp=True)
+        for i in [0, 1, 2, 100, 4095]:
+            assert blocks[i].tolist() == O.keyed_block(seed, ep, 17 + i, tag).tolist()
+        for i in range(0, 4096, 7):
+            u = O.u53(int(blocks[i][2]), int(blocks[i][3]))
+            assert ex[i] == (-1.0 * 1.0) * O.cpr_log(u)
+
+
+GRID = [
+    # alpha, gamma, policy, steps, episodes
+    (0.33, 0.5, L.POLICY_SAPIRSHTEIN_2016_SM1, 300, 512),
+    (0.45, 0.5, L.POLICY_EYAL_SIRER_2014, 300, 512),
+    (0.25, 0.0, L.POLICY_SAPIRSHTEIN_2016_SM1, 300, 256),
+    (0.25, 0.3, L.POLICY_SIMPLE, 300, 256),
+    (0.10, 0.75, L.POLICY_HONEST, 300, 256),
+    (0.40, 0.9, L.POLICY_SAPIRSHTEIN_2016_SM1, 300, 256),
+    (0.50, 0.5, L.POLICY_SIMPLE, 300, 256),
+    (0.05, 0.5, L.POLICY_HONEST, 300, 256),
+    (0.35, 0.5, L.POLICY_EYAL_SIRER_2014, 2016, 512),
+]
+
+
+@pytest.mark.parametrize("alpha,gamma,policy,steps,n", GRID)
+def test_gym_episodes_bit_exact(ctx, alpha, gamma, policy, steps, n):
+    cfg, keep = device.make_config(alpha=alpha, gamma=gamma, policy=policy, max_steps=steps,
+                                   seed=0x5EED0000)
+    b = device.Batch(cfg, ctx=ctx, keep=keep)
+    s, rec = b.run(n, first_episode=1000, records=True)
+    ref = O.run_episodes(cfg, 1000, n, threads=8)
+    assert _records_equal(rec, ref) == {}
+    assert s.episodes == n
+    assert s.activations == int(ref["n_activations"].sum())
+    assert (rec["n_activations"] == steps + 1).all()
+
+
+def test_gym_many_defenders_and_table_policy(ctx):
+    rng = np.random.default_rng(3)
+    table = rng.integers(0, 4, size=16 * 16 * 2).astype(np.uint8)
+    for kw in [dict(alpha=0.3, gamma=0.95, defenders=42, policy=L.POLICY_SAPIRSHTEIN_2016_SM1),
+               dict(alpha=0.3, gamma=0.6, defenders=5, table=table)]:
+        cfg, keep = device.make_config(max_steps=400, seed=99, **kw)
+        b = device.Batch(cfg, ctx=ctx, keep=keep)
+        _, rec = b.run(256, first_episode=0, records=True)
+        ref = O.run_episodes(cfg, 0, 256, threads=8)
+        assert _records_equal(rec, ref) == {}
+
+
+def test_tie_windows_replayed_exactly(ctx):
+    # Match-heavy play: equal-time deliveries (fp64 ties) occur in ~1% of long episodes;
+    # the device replays those windows through the skew heap and must agree exactly
+    cfg, keep = device.make_config(alpha=0.33, gamma=0.5, policy=L.POLICY_EYAL_SIRER_2014,
+                                   max_steps=2016, seed=0xABCDEF)
+    b = device.Batch(cfg, ctx=ctx, keep=keep)
+    _, rec = b.run(3072, first_episode=0, records=True)
+    ref = O.run_episodes(cfg, 0, 3072, threads=8)
+    assert _records_equal(rec, ref) == {}
+    ties = int(((rec["status"] & L.ST_TIE) != 0).sum())
+    assert ties > 0  # the case is actually exercised
+    assert int(((rec["status"] & L.ST_TIE_UNRESOLVED) != 0).sum()) == 0
+
+
+@pytest.mark.parametrize("policy", [0, 1, 2, 3])
+@pytest.mark.parametrize("alpha", [0.1, 0.33, 0.45])
+def test_loop_two_agents_bit_exact(ctx, alpha, policy):
+    cfg, keep = device.make_config(alpha=alpha, gamma=0.0, network=L.NET_TWO_AGENTS,
+                                   mode=L.MODE_LOOP, activations=10000, policy=policy, seed=5)
+    b = device.Batch(cfg, ctx=ctx, keep=keep)
+    _, rec = b.run(64, first_episode=0, records=True)
+    for e in range(0, 64, 9):
+        o = O.two_agents_task(alpha, policy, 10000, seed=5, episode=e)
+        assert rec["reward_attacker"][e] == o["reward"][0]
+        assert rec["reward_defender"][e] == o["reward"][1]
+        assert rec["chain_time"][e] == o["head_time"]
+        assert rec["head_height"][e] == o["head_height"]
+        assert rec["n_activations"][e] == sum(o["activations"])
+
+
+def test_lockstep_matches_oracle_step_by_step(ctx):
+    n = 48
+    cfg, keep = device.make_config(alpha=0.35, gamma=0.5, max_steps=150, seed=77,
+                                   unit_observation=True, n_lanes=n)
+    b = device.Batch(cfg, ctx=ctx, keep=keep)
+    obs = b.reset()
+    envs = [O.GymEnv(cfg, episode=i) for i in range(n)]
+    ref_obs = np.array([e.reset() for e in envs])
+    assert np.array_equal(obs, ref_obs)
+    rng = np.random.default_rng(0)
+    for t in range(150):
+        acts = rng.integers(0, 4, size=n).astype(np.int32)
+        obs, rew, done, info = b.step(acts)
+        for i, e in enumerate(envs):
+            o, r, d, inf = e.step(int(acts[i]))
+            assert np.array_equal(obs[i], o), (t, i)
+            assert rew[i] == r and done[i] == d
+            for k in ["episode_reward_attacker", "episode_reward_defender", "episode_progress",
+                      "episode_chain_time", "episode_sim_time", "episode_n_steps",
+                      "episode_n_activations", "head_height", "head_miner"]:
+                assert info[k][i] == inf[k], (t, i, k)
+    assert done.all()
+
+
+def test_policy_actions_decode(ctx):
+    cfg, keep = device.make_config(alpha=0.3, gamma=0.5, n_lanes=1)
+    b = device.Batch(cfg, ctx=ctx, keep=keep)
+    fields = [[h, a, a - h, ev] for h in range(0, 7) for a in range(0, 9) for ev in (0, 1)]
+    obs = np.array([O.obs_to_floats(f, True) for f in fields])
+    for name, pid in device.policy_registry():
+        got = b.policy_actions(pid, obs)
+        want = [O.nak_policy(pid, f) for f in fields]
+        assert got.tolist() == want, name
+
+
+def test_invalid_configs_rejected(ctx):
+    bad = [
+        dict(alpha=1.5, gamma=0.5),  # engine.ml:42
+        dict(alpha=0.3, gamma=0.9, defenders=2),  # network.ml:351-354
+        dict(alpha=0.3, gamma=0.5, defenders=1),  # network.ml:345-346
+        dict(alpha=float("nan"), gamma=0.5),
+    ]
+    for kw in bad:
+        cfg, keep = device.make_config(max_steps=10, **kw)
+        with pytest.raises(L.CprError) as e:
+            device.Batch(cfg, ctx=ctx, keep=keep)
+        assert e.value.code == L.CPR_E_INVALID_ARG
+
+
+def test_summary_is_reduction_of_records(ctx):
+    cfg, keep = device.make_config(alpha=0.4, gamma=0.5, max_steps=500, seed=1)
+    b = device.Batch(cfg, ctx=ctx, keep=keep)
+    s, rec = b.run(20000, first_episode=0, records=True)
+    h = rec["head_height"].astype(np.int64)
+    ra = rec["reward_attacker"].astype(np.int64)
+    assert s.episodes == 20000
+    assert s.activations == int(rec["n_activations"].sum())
+    assert s.reward_attacker_fx == int(ra.sum()) << 20
+    assert s.progress_fx == int(h.sum()) << 20
+    rel = np.where(h > 0, ra / np.maximum(h, 1), 0.0)
+    assert s.rel_revenue_fx == int(np.rint(rel * 2**32).astype(np.uint64).sum())
+    bins = np.clip((rel * 64).astype(np.int64), 0, 63)
+    assert list(s.hist) == np.bincount(bins, minlength=64).tolist()
+
+
+def test_full_size_properties(ctx):
+    """BASELINE configs[1] size per point (2016 steps), checked by size-free properties."""
+    cfg, keep = device.make_config(alpha=1 / 3, gamma=0.5, max_steps=2016, seed=0x5EED0000)
+    b = device.Batch(cfg, ctx=ctx, keep=keep)
+    n = 1 << 18
+    s1 = b.run(n, first_episode=0)
+    # shard invariance: two halves sum to the whole, bit for bit
+    s2 = L.Summary()
+    b.run(n // 2, first_episode=0, summary=s2)
+    b.run(n // 2, first_episode=n // 2, summary=s2)
+    assert s1.to_array().tolist() == s2.to_array().tolist()
+    assert s1.activations == n * 2017 and s1.steps == n * 2016
+    assert (s1.reward_attacker_fx + s1.reward_defender_fx) == s1.progress_fx
+    assert s1.orphans == s1.activations - (s1.progress_fx >> 20)
+    assert s1.status_other == 0
+    # SM1 at alpha=1/3, gamma=0.5: Eyal-Sirer closed form 0.384615; 2016-step episodes
+    # are within 2e-3 of the stationary value (finite-horizon start/end effects)
+    m = s1.rel_revenue_fx / 2**32 / n
+    assert abs(m - 0.384615) < 2e-3, m

@@ -1,0 +1,65 @@
+"""Host-side checks that need no GPU: the C-ABI library loads, exports every symbol
+include/cpr_hip.h declares, and its struct layouts match the ctypes mirrors."""
+
+import ctypes
+import pathlib
+import re
+import subprocess
+
+import pytest
+
+from cpr_amd import _lib as L
+
+ROOT = pathlib.Path(__file__).resolve().parent.parent
+HEADER = ROOT / "include" / "cpr_hip.h"
+
+
+def _declared():
+    text = HEADER.read_text()
+    return sorted(set(re.findall(r"^\S.*?\b(cpr_[a-z_0-9]+)\(", text, flags=re.M)))
+
+
+def test_library_exports_every_declared_symbol():
+    lib = ctypes.CDLL(str(L.LIB_PATH))
+    declared = _declared()
+    assert len(declared) >= 19
+    for name in declared:
+        assert hasattr(lib, name), name
+    assert sorted(L.EXPORTS) == declared
+
+
+def test_version_and_registry():
+    lib = L.lib()
+    assert lib.cpr_abi_version() == 1
+    assert lib.cpr_version().decode().startswith("cpr-hip")
+    from cpr_amd import device
+
+    # Collection.add prepends (collection.ml:13): reverse of nakamoto_ssz.ml:442-450
+    assert [n for n, _ in device.policy_registry()] == [
+        "sapirshtein-2016-sm1", "eyal-sirer-2014", "simple", "honest"]
+
+
+def test_struct_layouts_match_header(tmp_path):
+    src = tmp_path / "sz.c"
+    src.write_text(
+        '#include <stdio.h>\n#include <stddef.h>\n#include "cpr_hip.h"\n'
+        'int main(){printf("%zu %zu %zu %zu %zu\\n", sizeof(cpr_config), sizeof(cpr_episode_record),'
+        ' sizeof(cpr_summary), sizeof(cpr_step_info), offsetof(cpr_config, seed));return 0;}\n')
+    exe = tmp_path / "sz"
+    subprocess.run(["gcc", "-I", str(ROOT / "include"), "-o", str(exe), str(src)], check=True)
+    got = [int(x) for x in subprocess.run([str(exe)], capture_output=True, text=True).stdout.split()]
+    want = [ctypes.sizeof(L.Config), ctypes.sizeof(L.EpisodeRecord), ctypes.sizeof(L.Summary),
+            ctypes.sizeof(L.StepInfo), L.Config.seed.offset]
+    assert got == want
+
+
+def test_no_device_raises_loudly(monkeypatch):
+    # without a HIP device the product path must fail, never fall back to the CPU
+    import torch
+
+    if torch.cuda.device_count() > 0:
+        pytest.skip("a HIP device is present")
+    from cpr_amd import device
+
+    with pytest.raises(Exception):
+        device.Context(0)

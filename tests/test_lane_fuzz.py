@@ -1,0 +1,26 @@
+"""Differential fuzz of the device lane state machine against the oracle, on the CPU.
+
+tests/native/lane_vs_oracle.cpp compiles cpr_amd/csrc/nakamoto_lane.h for the host and
+runs it step by step beside the oracle's event-driven simulator on the same keyed stream:
+every observation and every head (rewards, height, chain time, clock, activations,
+miner) must match, for the four SSZ policies and two random-action fuzz policies over
+alpha x gamma (defenders 2..42) and for Simulator.loop on the two-agents network.
+(The GPU runs the same header; tests/test_gpu_parity.py checks device == oracle.)
+"""
+
+import json
+import pathlib
+import subprocess
+
+ROOT = pathlib.Path(__file__).resolve().parent.parent
+
+
+def test_lane_matches_oracle_fuzz():
+    subprocess.run(["make", "-s", "-C", str(ROOT / "tests" / "native")], check=True)
+    exe = ROOT / "tests" / "native" / "build" / "lane_vs_oracle"
+    p = subprocess.run([str(exe), "6", "600"], capture_output=True, text=True, timeout=600)
+    out = json.loads(p.stdout.strip().splitlines()[-1])
+    assert p.returncode == 0, p.stderr[-2000:]
+    assert out["mismatches"] == 0 and out["hazard_mismatches"] == 0, p.stderr[-2000:]
+    assert out["unresolved"] == 0
+    assert out["episodes"] > 1000
