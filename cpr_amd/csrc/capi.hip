@@ -260,10 +260,10 @@ int cpr_batch_destroy(cpr_batch* b) {
   return CPR_OK;
 }
 
-// lanes resident per launch: fill every CU with 4 workgroups of 256 lanes, bounded by a
-// 16 GiB budget for the private-chain slots (12 B per slot)
+// lanes per launch: exactly the resident capacity (occupancy API: workgroups per CU at
+// this kernel's register use x CUs x 256), bounded by a 16 GiB budget for per-lane memory
 static int64_t episode_lanes(cpr_batch* b, int64_t n_eps) {
-  const int64_t full = (int64_t)b->ctx->cus * 4 * 256;
+  const int64_t full = (int64_t)b->ctx->cus * run_episodes_blocks_per_cu() * 256;
   const int64_t budget = (int64_t)(16ll << 30) / ((int64_t)b->P.cap * 12 + REPLAY_BYTES);
   int64_t lanes = std::min(full, std::max<int64_t>(256, budget));
   const int64_t need = ((n_eps + 255) / 256) * 256;

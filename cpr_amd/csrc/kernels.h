@@ -42,5 +42,6 @@ hipError_t launch_policy(int32_t policy, int unit, const double* obs, int64_t n,
 hipError_t launch_stream_fill(uint64_t seed, uint64_t ep, uint32_t idx0, uint32_t tag, int64_t n,
                               uint32_t* out, double* exp_out, hipStream_t st);
 size_t lock_lane_bytes();
+int run_episodes_blocks_per_cu();  // resident 256-lane workgroups per CU
 
 }  // namespace cpr

@@ -382,4 +382,13 @@ hipError_t launch_stream_fill(uint64_t seed, uint64_t ep, uint32_t idx0, uint32_
 
 size_t lock_lane_bytes() { return sizeof(LockLane); }
 
+int run_episodes_blocks_per_cu() {
+  int blocks = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, k_run_episodes, kBlock, 0) !=
+          hipSuccess ||
+      blocks <= 0)
+    blocks = 2;
+  return blocks;
+}
+
 }  // namespace cpr

@@ -403,8 +403,7 @@ struct NakLane {
     wminer = miner;
     // deliver pending releases to the attacker's public model (strict >)
     if (pend >= 0) {
-      const BRef f = chain_ref(c, pend);
-      if (f.h > pub.h) pub = f;
+      if (p0.h + pend > pub.h) pub = chain_ref(c, pend);  // loads only when it moves
     }
     if (miner == 0) {
       int32_t m = n + 1;
@@ -490,12 +489,12 @@ struct NakLane {
     if (wminer != 0) {
       if (P.d >= 2) bound = t + P.delta;
       if (released) {
-        const BRef x = chain_ref(c, rhi);
-        if (x.h > b.h) {
-          A = x;
+        const int32_t xh = p0.h + rhi;
+        if (xh > b.h) {
+          A = chain_ref(c, rhi);
           onA = all;
           lca_da = b.fork;
-        } else if (x.h == b.h) {
+        } else if (xh == b.h) {
           // race at every defender except the miner: first visible wins
           const double tb = t + P.delta;
           uint64_t mask = 0ull;
@@ -521,7 +520,7 @@ struct NakLane {
             else
               status |= ST_TIE_UNRESOLVED;
           }
-          A = x;
+          A = chain_ref(c, rhi);
           onA = mask;
           lca_da = b.fork;
         } else {
@@ -533,11 +532,10 @@ struct NakLane {
         onA = 0ull;
       }
     } else if (released) {
-      const BRef x = chain_ref(c, rhi);
       const int32_t hs = onA ? A.h : D.h;
-      if (x.h > hs) {
+      if (p0.h + rhi > hs) {
         lca_da = D.fork;
-        A = x;
+        A = chain_ref(c, rhi);
         onA = all;
       }
     }

@@ -17,7 +17,10 @@ from cpr_amd import device
 
 pytestmark = pytest.mark.gpu
 
-FIELDS = [f for f in L.RECORD_DTYPE.names if f != "_pad"]
+# every outcome field; `status` holds engine-specific diagnostics (the oracle flags any
+# same-instant equal-height delivery, the device only the races it replays) and is
+# checked separately
+FIELDS = [f for f in L.RECORD_DTYPE.names if f not in ("_pad", "status")]
 
 
 @pytest.fixture(scope="module")
@@ -92,8 +95,10 @@ def test_tie_windows_replayed_exactly(ctx):
     _, rec = b.run(3072, first_episode=0, records=True)
     ref = O.run_episodes(cfg, 0, 3072, threads=8)
     assert _records_equal(rec, ref) == {}
-    ties = int(((rec["status"] & L.ST_TIE) != 0).sum())
-    assert ties > 0  # the case is actually exercised
+    ties = (rec["status"] & L.ST_TIE) != 0
+    assert ties.sum() > 0  # the case is actually exercised
+    # every race the device replayed is one the oracle saw as a same-instant tie
+    assert ((ref["status"][ties] & L.ST_TIE) != 0).all()
     assert int(((rec["status"] & L.ST_TIE_UNRESOLVED) != 0).sum()) == 0
 
 

@@ -1,0 +1,58 @@
+"""Summarise a tools/profile.sh run (gpurun_out/prof_*) into profiles/<tag>_*.
+
+Usage: python tools/summarize_profile.py <tag> [episodes_per_launch]
+"""
+import collections
+import csv
+import json
+import shutil
+import sys
+
+tag = sys.argv[1]
+eps = int(sys.argv[2]) if len(sys.argv) > 2 else 393216
+K = "cpr::k_run_episodes"
+
+
+def agg(path):
+    a = collections.defaultdict(lambda: collections.defaultdict(float))
+    n = collections.Counter()
+    for r in csv.DictReader(open(path)):
+        k = r["Kernel_Name"].split("(")[0]
+        a[k][r["Counter_Name"]] += float(r["Counter_Value"])
+        n[(k, r["Counter_Name"])] += 1
+    return a, n
+
+
+res = {}
+for p in ["prof_pmc_sq", "prof_pmc_fetch", "prof_pmc_write"]:
+    a, n = agg(f"gpurun_out/{p}/run_counter_collection.csv")
+    for k, v in a.items():
+        for c, x in v.items():
+            res.setdefault(k, {})[c] = {"sum": x, "dispatches": n[(k, c)], "per_dispatch": x / n[(k, c)]}
+tr = list(csv.DictReader(open("gpurun_out/prof_trace/run_kernel_trace.csv")))
+durs = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in tr if r["Kernel_Name"].startswith(K)]
+acts = eps * 2017
+r = res[K]
+s = {
+    "kernel": K,
+    "dispatches": len(durs),
+    "mean_duration_ms": sum(durs) / len(durs) / 1e6,
+    "episodes_per_dispatch": eps,
+    "activations_per_dispatch": acts,
+    "activations_per_s_in_kernel": acts / (sum(durs) / len(durs) / 1e9),
+    "valu_wave_instr_per_activation": r["SQ_INSTS_VALU"]["per_dispatch"] * 64 / acts,
+    "salu_wave_instr_per_activation": r["SQ_INSTS_SALU"]["per_dispatch"] * 64 / acts,
+    "vmem_rd_wave_instr_per_activation": r["SQ_INSTS_VMEM_RD"]["per_dispatch"] * 64 / acts,
+    "vmem_wr_wave_instr_per_activation": r["SQ_INSTS_VMEM_WR"]["per_dispatch"] * 64 / acts,
+    "valu_lane_ops_per_s": r["SQ_INSTS_VALU"]["per_dispatch"] * 64 / (sum(durs) / len(durs) / 1e9),
+    "hbm_read_bytes_per_dispatch (FETCH_SIZE x1024 x2, gfx950 correction)": r["FETCH_SIZE"]["per_dispatch"] * 1024 * 2,
+    "hbm_write_bytes_per_dispatch (WRITE_SIZE x1024)": r["WRITE_SIZE"]["per_dispatch"] * 1024,
+    "counters": r,
+}
+s["valu_issue_frac_of_78.6T"] = s["valu_lane_ops_per_s"] / 7.86432e13
+s["hbm_bytes_per_activation"] = (s["hbm_read_bytes_per_dispatch (FETCH_SIZE x1024 x2, gfx950 correction)"]
+                                 + s["hbm_write_bytes_per_dispatch (WRITE_SIZE x1024)"]) / acts
+json.dump(s, open(f"profiles/{tag}_pmc_summary.json", "w"), indent=1)
+shutil.copy("gpurun_out/prof_trace/run_kernel_stats.csv", f"profiles/{tag}_kernel_stats.csv")
+shutil.copy("gpurun_out/bench.log", f"profiles/{tag}_bench.jsonl") if False else None
+print(json.dumps({k: v for k, v in s.items() if k != "counters"}, indent=1))
