@@ -64,10 +64,10 @@ struct cpr_batch {
   NakParams P;
   std::vector<uint8_t> table_host;
   DevBuf table_dev, tabs_dev;  // policy table; unit-observation tables
-  DevBuf chain_k, chain_t, replay, summary, records;
-  int64_t chain_lanes = 0;
-  // lockstep
-  DevBuf lanes, lchain_k, lchain_t, lreplay, l_obs, l_act, l_rew, l_done, l_mask, l_eps, l_info;
+  DevBuf spill, tlog, replay, summary, records;
+  int64_t lanes_alloc = 0;
+  // lockstep lanes
+  DevBuf lanes, lring, lspill, ltlog, lreplay, l_obs, l_act, l_rew, l_done, l_mask, l_eps, l_info;
   bool reset_done = false;
   int32_t tab_n = 4096;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
@@ -130,6 +130,12 @@ static uint64_t alpha_threshold(double alpha) {
   return (uint64_t)t;
 }
 
+static int32_t pow2_at_least(int64_t x, int32_t cap) {
+  int32_t p = 64;
+  while (p < x && p < cap) p <<= 1;
+  return p;
+}
+
 // engine.ml:37-51 and network.ml:343-358 (messages kept verbatim)
 static int validate(const cpr_config* c, NakParams* P) {
   if (c->protocol != CPR_PROTO_NAKAMOTO)
@@ -181,10 +187,9 @@ static int validate(const cpr_config* c, NakParams* P) {
   } else {
     return fail(CPR_E_INVALID_ARG, "unknown network");
   }
-  int64_t span;
+  int64_t span;  // activations per episode + 1 (bound on chain length and clock index)
   if (c->mode == CPR_MODE_GYM) {
     const int64_t ms = c->max_steps > 0 ? c->max_steps : INT64_MAX;
-    if (ms <= 0) return fail(CPR_E_INVALID_ARG, "max_steps <= 0");
     P->max_steps = ms;
     P->max_progress = c->max_progress > 0 ? c->max_progress : __builtin_inf();
     P->max_time = c->max_time > 0 ? c->max_time : __builtin_inf();
@@ -197,7 +202,8 @@ static int validate(const cpr_config* c, NakParams* P) {
     P->max_time = __builtin_inf();
     span = c->activations + 2;
   }
-  P->cap = (int32_t)(((span + 63) / 64) * 64);
+  P->cap = (int32_t)(((std::min<int64_t>(span, 1 << 20) + 63) / 64) * 64);
+  P->tlog_len = pow2_at_least(span, 2048);
   return CPR_OK;
 }
 
@@ -252,19 +258,20 @@ int cpr_batch_destroy(cpr_batch* b) {
   (void)hipStreamSynchronize(b->ctx->stream);
   if (b->ev0) (void)hipEventDestroy(b->ev0);
   if (b->ev1) (void)hipEventDestroy(b->ev1);
-  for (DevBuf* d : {&b->table_dev, &b->tabs_dev, &b->chain_k, &b->chain_t, &b->summary,
-                    &b->records, &b->replay, &b->lanes, &b->lchain_k, &b->lchain_t, &b->lreplay, &b->l_obs, &b->l_act,
-                    &b->l_rew, &b->l_done, &b->l_mask, &b->l_eps, &b->l_info})
+  for (DevBuf* d : {&b->table_dev, &b->tabs_dev, &b->spill, &b->tlog, &b->replay, &b->summary,
+                    &b->records, &b->lanes, &b->lring, &b->lspill, &b->ltlog, &b->lreplay,
+                    &b->l_obs, &b->l_act, &b->l_rew, &b->l_done, &b->l_mask, &b->l_eps,
+                    &b->l_info})
     d->release();
   delete b;
   return CPR_OK;
 }
 
 // lanes per launch: exactly the resident capacity (occupancy API: workgroups per CU at
-// this kernel's register use x CUs x 256), bounded by a 16 GiB budget for per-lane memory
+// this kernel's register/LDS use x CUs x 256), bounded by a 16 GiB budget for per-lane HBM
 static int64_t episode_lanes(cpr_batch* b, int64_t n_eps) {
-  const int64_t full = (int64_t)b->ctx->cus * run_episodes_blocks_per_cu() * 256;
-  const int64_t budget = (int64_t)(16ll << 30) / ((int64_t)b->P.cap * 12 + REPLAY_BYTES);
+  const int64_t full = (int64_t)b->ctx->cus * run_episodes_blocks_per_cu(b->cfg.mode) * 256;
+  const int64_t budget = (int64_t)(16ll << 30) / episode_lane_bytes(b->P);
   int64_t lanes = std::min(full, std::max<int64_t>(256, budget));
   const int64_t need = ((n_eps + 255) / 256) * 256;
   lanes = std::min(lanes, need);
@@ -274,11 +281,11 @@ static int64_t episode_lanes(cpr_batch* b, int64_t n_eps) {
 static int run_async(cpr_batch* b, int64_t n, uint64_t first, cpr_summary* sum_dev,
                      cpr_episode_record* rec_dev) {
   const int64_t lanes = episode_lanes(b, n);
-  if (lanes > b->chain_lanes) {
-    HIP_TRY(b->chain_k.ensure((size_t)lanes * b->P.cap * sizeof(int32_t)));
-    HIP_TRY(b->chain_t.ensure((size_t)lanes * b->P.cap * sizeof(double)));
+  if (lanes > b->lanes_alloc) {
+    HIP_TRY(b->spill.ensure((size_t)lanes * b->P.cap * sizeof(int32_t)));
+    HIP_TRY(b->tlog.ensure((size_t)lanes * b->P.tlog_len * sizeof(double)));
     HIP_TRY(b->replay.ensure((size_t)lanes * REPLAY_BYTES));
-    b->chain_lanes = lanes;
+    b->lanes_alloc = lanes;
   }
   if (!b->ev0) {
     HIP_TRY(hipEventCreate(&b->ev0));
@@ -286,9 +293,8 @@ static int run_async(cpr_batch* b, int64_t n, uint64_t first, cpr_summary* sum_d
   }
   HIP_TRY(hipEventRecord(b->ev0, b->ctx->stream));
   HIP_TRY(launch_run_episodes(b->P, b->cfg.seed, first, n, b->cfg.mode, b->cfg.activations,
-                              (int32_t*)b->chain_k.p, (double*)b->chain_t.p,
-                              (uint8_t*)b->replay.p, lanes, rec_dev,
-                              sum_dev, b->ctx->stream));
+                              (int32_t*)b->spill.p, (double*)b->tlog.p, (uint8_t*)b->replay.p,
+                              lanes, rec_dev, sum_dev, b->ctx->stream));
   HIP_TRY(hipEventRecord(b->ev1, b->ctx->stream));
   return CPR_OK;
 }
@@ -353,8 +359,9 @@ static int ensure_lockstep(cpr_batch* b) {
   if (n <= 0) return fail(CPR_E_STATE, "batch has no lockstep lanes (cfg.n_lanes = 0)");
   if (b->cfg.mode != CPR_MODE_GYM) return fail(CPR_E_STATE, "lockstep lanes need CPR_MODE_GYM");
   HIP_TRY(b->lanes.ensure((size_t)n * lock_lane_bytes()));
-  HIP_TRY(b->lchain_k.ensure((size_t)n * b->P.cap * sizeof(int32_t)));
-  HIP_TRY(b->lchain_t.ensure((size_t)n * b->P.cap * sizeof(double)));
+  HIP_TRY(b->lring.ensure((size_t)n * RING * sizeof(int32_t)));
+  HIP_TRY(b->lspill.ensure((size_t)n * b->P.cap * sizeof(int32_t)));
+  HIP_TRY(b->ltlog.ensure((size_t)n * b->P.tlog_len * sizeof(double)));
   HIP_TRY(b->lreplay.ensure((size_t)n * REPLAY_BYTES));
   HIP_TRY(b->l_obs.ensure((size_t)n * 4 * sizeof(double)));
   HIP_TRY(b->l_act.ensure((size_t)n * sizeof(int32_t)));
@@ -364,6 +371,16 @@ static int ensure_lockstep(cpr_batch* b) {
   HIP_TRY(b->l_eps.ensure((size_t)n * sizeof(uint64_t)));
   HIP_TRY(b->l_info.ensure((size_t)n * (7 * 8 + 2 * 4)));
   return CPR_OK;
+}
+
+static LockBuffers lock_buffers(cpr_batch* b) {
+  LockBuffers B;
+  B.lanes = b->lanes.p;
+  B.ring = (int32_t*)b->lring.p;
+  B.spill = (int32_t*)b->lspill.p;
+  B.tlog = (double*)b->ltlog.p;
+  B.replay = (uint8_t*)b->lreplay.p;
+  return B;
 }
 
 int cpr_reset(cpr_batch* b, const uint8_t* mask, const uint64_t* eps, double* obs) {
@@ -388,9 +405,9 @@ int cpr_reset(cpr_batch* b, const uint8_t* mask, const uint64_t* eps, double* ob
     deps = (const uint64_t*)b->l_eps.p;
   }
   const double* tabs = (const double*)b->tabs_dev.p;
-  HIP_TRY(launch_reset(b->P, b->cfg.seed, b->lanes.p, n, dmask, deps, (int32_t*)b->lchain_k.p,
-                       (double*)b->lchain_t.p, b->cfg.unit_observation, tabs, tabs + b->tab_n,
-                       b->tab_n, (double*)b->l_obs.p, st));
+  HIP_TRY(launch_reset(b->P, b->cfg.seed, lock_buffers(b), n, dmask, deps,
+                       b->cfg.unit_observation, tabs, tabs + b->tab_n, b->tab_n,
+                       (double*)b->l_obs.p, st));
   HIP_TRY(hipMemcpyAsync(obs, b->l_obs.p, (size_t)n * 4 * sizeof(double), hipMemcpyDeviceToHost, st));
   HIP_TRY(hipStreamSynchronize(st));
   b->reset_done = true;
@@ -423,8 +440,7 @@ int cpr_step(cpr_batch* b, const int32_t* actions, double* obs, double* reward, 
   sb.hh = (int32_t*)(ib + 7 * n * 8);
   sb.hm = (int32_t*)(ib + 7 * n * 8 + n * 4);
   const double* tabs = (const double*)b->tabs_dev.p;
-  HIP_TRY(launch_step(b->P, b->cfg.seed, b->lanes.p, n, (const int32_t*)b->l_act.p,
-                      (int32_t*)b->lchain_k.p, (double*)b->lchain_t.p, (uint8_t*)b->lreplay.p,
+  HIP_TRY(launch_step(b->P, b->cfg.seed, lock_buffers(b), n, (const int32_t*)b->l_act.p,
                       b->cfg.unit_observation, tabs, tabs + b->tab_n, b->tab_n, sb, st));
   HIP_TRY(hipMemcpyAsync(obs, sb.obs, (size_t)n * 32, hipMemcpyDeviceToHost, st));
   HIP_TRY(hipMemcpyAsync(reward, sb.reward, (size_t)n * 8, hipMemcpyDeviceToHost, st));

@@ -7,7 +7,8 @@
 //   activation j : Philox4x32-10(ctr = (ep_lo, ep_hi, j, 0), key = seed)
 //                  w0 -> attacker iff w0 < floor(alpha 2^32); w1 -> defender (w1*d)>>32
 //                  w2,w3 -> u53 -> delay = (-1*ev) * cpr_log(u)
-//   link (serial s, dest j) : ctr = (ep, s, TAG_LINK | j>>1), words 2*(j&1),+1 -> u53
+//   link (shared at activation count kw, share position off, dest j) :
+//                  ctr = (ep, kw, TAG_LINK | off<<12 | j>>1), words 2*(j&1),+1 -> u53
 // cpr_log = fdlibm e_log.c (IEEE +,-,*,/ only) so device and host agree bit for bit;
 // this TU must be compiled with -ffp-contract=off.
 #pragma once
@@ -118,9 +119,10 @@ struct Stream {
   __host__ __device__ inline Words4 block(uint32_t idx, uint32_t tag) const {
     return philox4x32_10(e0, e1, idx, tag, k0, k1);
   }
-  // uniform for the message of block `serial` to node `dest`
-  __host__ __device__ inline double link_u(uint32_t serial, uint32_t dest) const {
-    const Words4 w = block(serial, TAG_LINK | (dest >> 1));
+  // uniform for the message shared at activation count kw, position off in that share
+  // order, to node dest
+  __host__ __device__ inline double link_u(uint32_t kw, uint32_t off, uint32_t dest) const {
+    const Words4 w = block(kw, TAG_LINK | (off << 12) | (dest >> 1));
     return (dest & 1u) ? u53(w.w2, w.w3) : u53(w.w0, w.w1);
   }
 };

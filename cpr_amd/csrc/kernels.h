@@ -9,6 +9,7 @@
 
 namespace cpr {
 
+// per-step outputs of the lockstep kernel (device pointers)
 struct StepBuffers {
   double* obs;
   double* reward;
@@ -24,24 +25,37 @@ struct StepBuffers {
   int32_t* hm;
 };
 
+// persistent per-lane memory of the lockstep lanes (device pointers)
+struct LockBuffers {
+  void* lanes;      // LockLane[n]
+  int32_t* ring;    // [RING][n]
+  int32_t* spill;   // [n][cap]
+  double* tlog;     // [tlog_len][n]
+  uint8_t* replay;  // [n][REPLAY_BYTES]
+};
+
+// per-lane bytes the fused kernel needs in HBM besides LDS
+inline int64_t episode_lane_bytes(const NakParams& P) {
+  return (int64_t)P.cap * 4 + (int64_t)P.tlog_len * 8 + REPLAY_BYTES;
+}
+
 hipError_t launch_run_episodes(const NakParams& P, uint64_t seed, uint64_t first, int64_t n_eps,
-                               int32_t mode, int64_t activations, int32_t* chain_k,
-                               double* chain_t, uint8_t* replay, int64_t lanes,
-                               cpr_episode_record* recs, cpr_summary* sum, hipStream_t st);
-hipError_t launch_reset(const NakParams& P, uint64_t seed, void* lanes, int64_t n,
-                        const uint8_t* mask, const uint64_t* eps, int32_t* chain_k,
-                        double* chain_t, int unit, const double* tab_nn, const double* tab_sg,
-                        int32_t tab_n, double* obs, hipStream_t st);
-hipError_t launch_step(const NakParams& P, uint64_t seed, void* lanes, int64_t n,
-                       const int32_t* actions, int32_t* chain_k, double* chain_t,
-                       uint8_t* replay, int unit, const double* tab_nn, const double* tab_sg,
-                       int32_t tab_n, const StepBuffers& b, hipStream_t st);
+                               int32_t mode, int64_t activations, int32_t* spill, double* tlog,
+                               uint8_t* replay, int64_t lanes, cpr_episode_record* recs,
+                               cpr_summary* sum, hipStream_t st);
+hipError_t launch_reset(const NakParams& P, uint64_t seed, const LockBuffers& B, int64_t n,
+                        const uint8_t* mask, const uint64_t* eps, int unit, const double* tab_nn,
+                        const double* tab_sg, int32_t tab_n, double* obs, hipStream_t st);
+hipError_t launch_step(const NakParams& P, uint64_t seed, const LockBuffers& B, int64_t n,
+                       const int32_t* actions, int unit, const double* tab_nn,
+                       const double* tab_sg, int32_t tab_n, const StepBuffers& b,
+                       hipStream_t st);
 hipError_t launch_observe_fields(const void* lanes, int64_t n, int32_t* f, hipStream_t st);
 hipError_t launch_policy(int32_t policy, int unit, const double* obs, int64_t n,
                          const uint8_t* table, int32_t dim, int32_t* actions, hipStream_t st);
 hipError_t launch_stream_fill(uint64_t seed, uint64_t ep, uint32_t idx0, uint32_t tag, int64_t n,
                               uint32_t* out, double* exp_out, hipStream_t st);
 size_t lock_lane_bytes();
-int run_episodes_blocks_per_cu();  // resident 256-lane workgroups per CU
+int run_episodes_blocks_per_cu(int32_t mode);  // resident 256-lane workgroups per CU
 
 }  // namespace cpr

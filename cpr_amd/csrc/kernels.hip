@@ -1,10 +1,11 @@
 // HIP kernels for gfx950 (MI355X): one lane = one independent episode / gym env.
 //
 // Work is integer/branch (VALU) bound; nothing is a contraction, so no MFMA. Per-lane
-// state lives in VGPRs; the private chain (mining activation + time per withheld block)
-// is the only per-lane memory and is touched once per attacker block. Episode outcomes
-// are reduced wave-wide with DPP/shuffle sums, then per workgroup in LDS, then one
-// 64-bit atomic per field per workgroup, all in integer arithmetic so totals are
+// state lives in VGPRs; the last 16 private-chain blocks live in LDS (16 KB per
+// workgroup), deeper ones spill to HBM, and every activation time goes to a [k][lane] log
+// (one coalesced 512 B store per wave and activation, read back only for the head).
+// Episode outcomes are reduced wave-wide with shuffles, then per workgroup in LDS, then
+// one 64-bit atomic per field per workgroup, all in integer arithmetic so totals are
 // independent of scheduling and of how episodes are sharded over GPUs.
 #include <hip/hip_runtime.h>
 
@@ -65,22 +66,10 @@ __device__ inline void block_flush(const Acc& a, int32_t* hist_lds, cpr_summary*
   if (threadIdx.x < 12) {
     int64_t s = 0;
     for (int w = 0; w < kBlock / 64; ++w) s += red[w][threadIdx.x];
-    unsigned long long* dst;
-    switch (threadIdx.x) {
-      case 0: dst = (unsigned long long*)&out->episodes; break;
-      case 1: dst = (unsigned long long*)&out->steps; break;
-      case 2: dst = (unsigned long long*)&out->activations; break;
-      case 3: dst = (unsigned long long*)&out->reward_attacker_fx; break;
-      case 4: dst = (unsigned long long*)&out->reward_defender_fx; break;
-      case 5: dst = (unsigned long long*)&out->progress_fx; break;
-      case 6: dst = (unsigned long long*)&out->orphans; break;
-      case 7: dst = (unsigned long long*)&out->status_tie; break;
-      case 8: dst = (unsigned long long*)&out->status_overlap; break;
-      case 9: dst = (unsigned long long*)&out->status_other; break;
-      case 10: dst = (unsigned long long*)&out->rel_revenue_fx; break;
-      default: dst = (unsigned long long*)&out->rel_revenue_sq_fx; break;
-    }
-    if (s) atomicAdd(dst, (unsigned long long)s);
+    unsigned long long* base = (unsigned long long*)out;
+    // cpr_summary word index of each accumulator (rel sums sit before orphans)
+    const int idx[12] = {0, 1, 2, 3, 4, 5, 8, 9, 10, 11, 6, 7};
+    if (s) atomicAdd(base + idx[threadIdx.x], (unsigned long long)s);
   }
   if (threadIdx.x < CPR_HIST_BINS && hist_lds[threadIdx.x])
     atomicAdd((unsigned long long*)&out->hist[threadIdx.x],
@@ -98,73 +87,80 @@ __device__ inline Stream make_stream(uint64_t seed, uint64_t ep) {
 
 // One gym episode (engine.ml:164-249): reset = first activation up to the attacker's
 // interaction; step = apply, deliveries, next activation, observe; head at the end.
-__device__ inline BRef run_gym(NakLane& L, const NakParams& P, const Stream& S, const Chain& c,
-                               const ReplayMem& M, int64_t* steps_out) {
+__device__ inline BRef run_gym(NakLane& L, const NakParams& P, const Stream& S, const LaneMem& M,
+                               int64_t* steps_out) {
   L.init();
-  L.activate(P, S, c);
+  L.activate(P, S, M);
   const bool check_prog = P.max_progress < __builtin_inf();
   int64_t steps = 0;
   for (;;) {
     const int32_t a = L.policy_action(P);
     L.apply(a);
-    L.resolve(P, S, c, M);
-    L.activate(P, S, c);
+    L.resolve(P, S, M);
+    L.activate(P, S, M);
     ++steps;
     bool go = steps < P.max_steps && L.t < P.max_time;
-    if (check_prog && go) go = (double)L.head(P, c).h < P.max_progress;
+    if (check_prog && go) go = (double)L.head(P, M).h < P.max_progress;
     if (!go) break;
   }
   *steps_out = steps;
-  return L.head(P, c);
+  return L.head(P, M);
 }
 
 // Simulator.loop ~activations with the SSZ attacker as node 0 (simulator.ml:519-533,
 // nakamoto_ssz.ml:362-372); all messages delivered before the head is taken.
-__device__ inline BRef run_loop(NakLane& L, const NakParams& P, const Stream& S, const Chain& c,
-                                const ReplayMem& M, int64_t activations) {
+__device__ inline BRef run_loop(NakLane& L, const NakParams& P, const Stream& S, const LaneMem& M,
+                                int64_t activations) {
   L.init();
   for (int64_t i = 0; i < activations; ++i) {
-    L.activate(P, S, c);
+    L.activate(P, S, M);
     L.apply(L.policy_action(P));
-    L.resolve(P, S, c, M);
+    L.resolve(P, S, M);
   }
-  return L.head(P, c);
+  return L.head(P, M);
 }
 
+template <int MODE>
 __global__ __launch_bounds__(kBlock) void k_run_episodes(
-    NakParams P, uint64_t seed, uint64_t first, int64_t n_eps, int32_t mode, int64_t activations,
-    int32_t* chain_k, double* chain_t, uint8_t* replay, cpr_episode_record* recs,
-    cpr_summary* sum) {
+    NakParams P, uint64_t seed, uint64_t first, int64_t n_eps, int64_t activations,
+    int32_t* spill, double* tlog, uint8_t* replay, cpr_episode_record* recs, cpr_summary* sum) {
   __shared__ int32_t hist[CPR_HIST_BINS];
+  __shared__ int32_t ring[RING * kBlock];
   if (threadIdx.x < CPR_HIST_BINS) hist[threadIdx.x] = 0;
   __syncthreads();
   const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t nthreads = (int64_t)gridDim.x * blockDim.x;
-  Chain c;
-  c.k = chain_k + tid * P.cap;
-  c.t = chain_t + tid * P.cap;
-  c.stride = 1;
-  const ReplayMem M = ReplayMem::at(replay + tid * REPLAY_BYTES);
+  LaneMem M;
+  M.ring = ring + threadIdx.x;
+  M.ring_stride = kBlock;
+  M.spill = spill + tid * P.cap;
+  M.spill_stride = 1;
+  M.tlog = tlog + tid;
+  M.tlog_stride = nthreads;
+  M.tmask = P.tlog_len - 1;
+  M.cap = P.cap;
+  M.replay = ReplayMem::at(replay + tid * REPLAY_BYTES);
   Acc acc = {};
   NakLane L;
   for (int64_t e = tid; e < n_eps; e += nthreads) {
     const uint64_t ep = first + (uint64_t)e;
     const Stream S = make_stream(seed, ep);
     int64_t steps = 0;
-    BRef hd = mode == CPR_MODE_GYM ? run_gym(L, P, S, c, M, &steps)
-                                    : run_loop(L, P, S, c, M, activations);
+    const BRef hd = MODE == CPR_MODE_GYM ? run_gym(L, P, S, M, &steps)
+                                         : run_loop(L, P, S, M, activations);
+    const double tm = L.time_of(M, hd);
     acc_add(acc, hd, steps, L.k, L.status, hist);
     if (recs) {
       cpr_episode_record r;
       r.reward_attacker = (double)hd.ra;
       r.reward_defender = (double)(hd.h - hd.ra);
       r.progress = (double)hd.h;
-      r.chain_time = hd.tm;
-      r.sim_time = mode == CPR_MODE_GYM ? L.t : 0.0;
+      r.chain_time = tm;
+      r.sim_time = MODE == CPR_MODE_GYM ? L.t : 0.0;
       r.n_steps = steps;
       r.n_activations = L.k;
       r.head_height = hd.h;
-      r.head_miner = mode == CPR_MODE_GYM ? miner_of(P, S, hd.k) : -1;
+      r.head_miner = MODE == CPR_MODE_GYM ? miner_of(P, S, hd.k) : -1;
       r.status = L.status;
       r._pad = 0u;
       recs[e] = r;
@@ -180,10 +176,24 @@ struct LockLane {
   NakLane L;
   uint64_t ep;
   int64_t steps;
-  double last_ra, last_rd, last_prog, last_ct, last_st;
+  double last_ra;
   int32_t live;
   int32_t _pad;
 };
+
+__device__ inline LaneMem lock_mem(const NakParams& P, const LockBuffers& B, int64_t i, int64_t n) {
+  LaneMem M;
+  M.ring = B.ring + i;
+  M.ring_stride = n;
+  M.spill = B.spill + i * P.cap;
+  M.spill_stride = 1;
+  M.tlog = B.tlog + i;
+  M.tlog_stride = n;
+  M.tmask = P.tlog_len - 1;
+  M.cap = P.cap;
+  M.replay = ReplayMem::at(B.replay + i * REPLAY_BYTES);
+  return M;
+}
 
 __device__ inline void write_obs(const NakLane& L, int unit, const double* tab_nn,
                                  const double* tab_sg, int32_t tab_n, double* o) {
@@ -204,72 +214,54 @@ __device__ inline void write_obs(const NakLane& L, int unit, const double* tab_n
   }
 }
 
-__global__ __launch_bounds__(kBlock) void k_reset(NakParams P, uint64_t seed, LockLane* lanes,
+__global__ __launch_bounds__(kBlock) void k_reset(NakParams P, uint64_t seed, LockBuffers B,
                                                    int64_t n, const uint8_t* mask,
-                                                   const uint64_t* eps, int32_t* chain_k,
-                                                   double* chain_t, int unit, const double* tab_nn,
-                                                   const double* tab_sg, int32_t tab_n, double* obs) {
+                                                   const uint64_t* eps, int unit,
+                                                   const double* tab_nn, const double* tab_sg,
+                                                   int32_t tab_n, double* obs) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  LockLane& LL = lanes[i];
+  LockLane& LL = ((LockLane*)B.lanes)[i];
   if (mask == nullptr || mask[i]) {
-    Chain c{chain_k + i * P.cap, chain_t + i * P.cap, 1};
+    const LaneMem M = lock_mem(P, B, i, n);
     NakLane L;
     L.init();
     const uint64_t ep = eps ? eps[i] : (uint64_t)i;
-    L.activate(P, make_stream(seed, ep), c);
+    L.activate(P, make_stream(seed, ep), M);
     LL.L = L;
     LL.ep = ep;
     LL.steps = 0;
-    LL.last_ra = LL.last_rd = LL.last_prog = LL.last_ct = LL.last_st = 0.0;
+    LL.last_ra = 0.0;
     LL.live = 1;
   }
   write_obs(LL.L, unit, tab_nn, tab_sg, tab_n, obs + 4 * i);
 }
 
-struct StepOut {
-  double* obs;
-  double* reward;
-  uint8_t* done;
-  double* era;
-  double* erd;
-  double* eprog;
-  double* ect;
-  double* est;
-  int64_t* esteps;
-  int64_t* eacts;
-  int32_t* hh;
-  int32_t* hm;
-};
-
-__global__ __launch_bounds__(kBlock) void k_step(NakParams P, uint64_t seed, LockLane* lanes,
-                                                  int64_t n, const int32_t* actions,
-                                                  int32_t* chain_k, double* chain_t,
-                                                  uint8_t* replay, int unit,
+__global__ __launch_bounds__(kBlock) void k_step(NakParams P, uint64_t seed, LockBuffers B,
+                                                  int64_t n, const int32_t* actions, int unit,
                                                   const double* tab_nn, const double* tab_sg,
-                                                  int32_t tab_n, StepOut out) {
+                                                  int32_t tab_n, StepBuffers out) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  LockLane& LL = lanes[i];
+  LockLane& LL = ((LockLane*)B.lanes)[i];
   NakLane L = LL.L;
-  Chain c{chain_k + i * P.cap, chain_t + i * P.cap, 1};
+  const LaneMem M = lock_mem(P, B, i, n);
   const Stream S = make_stream(seed, LL.ep);
-  const ReplayMem M = ReplayMem::at(replay + i * REPLAY_BYTES);
   L.apply(actions[i]);
-  L.resolve(P, S, c, M);
-  L.activate(P, S, c);
+  L.resolve(P, S, M);
+  L.activate(P, S, M);
   LL.steps += 1;
-  const BRef hd = L.head(P, c);
+  const BRef hd = L.head(P, M);
   const double progress = (double)hd.h;
   const bool done = !(LL.steps < P.max_steps && progress < P.max_progress && L.t < P.max_time);
-  const double ra = (double)hd.ra, rd = (double)(hd.h - hd.ra);
+  const double ra = (double)hd.ra;
   out.reward[i] = ra - LL.last_ra;  // engine.ml:223
   out.done[i] = done ? 1 : 0;
   if (out.era) {
     out.era[i] = ra;
-    out.erd[i] = rd;
+    out.erd[i] = (double)(hd.h - hd.ra);
     out.eprog[i] = progress;
-    out.ect[i] = hd.tm;
+    out.ect[i] = L.time_of(M, hd);
     out.est[i] = L.t;
     out.esteps[i] = LL.steps;
     out.eacts[i] = L.k;
@@ -277,18 +269,14 @@ __global__ __launch_bounds__(kBlock) void k_step(NakParams P, uint64_t seed, Loc
     out.hm[i] = miner_of(P, S, hd.k);
   }
   LL.last_ra = ra;
-  LL.last_rd = rd;
-  LL.last_prog = progress;
-  LL.last_ct = hd.tm;
-  LL.last_st = L.t;
   LL.L = L;
   write_obs(L, unit, tab_nn, tab_sg, tab_n, out.obs + 4 * i);
 }
 
-__global__ void k_observe_fields(const LockLane* lanes, int64_t n, int32_t* f) {
+__global__ void k_observe_fields(const void* lanes, int64_t n, int32_t* f) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  lanes[i].L.observe(f + 4 * i, f + 4 * i + 1, f + 4 * i + 2, f + 4 * i + 3);
+  ((const LockLane*)lanes)[i].L.observe(f + 4 * i, f + 4 * i + 1, f + 4 * i + 2, f + 4 * i + 3);
 }
 
 // engine.ml:258-261: decode the observation (ssz_tools.ml:493-510), apply the policy
@@ -326,41 +314,41 @@ __global__ void k_stream_fill(uint64_t seed, uint64_t ep, uint32_t idx0, uint32_
 // ---------------------------------------------------------------- launchers
 
 hipError_t launch_run_episodes(const NakParams& P, uint64_t seed, uint64_t first, int64_t n_eps,
-                               int32_t mode, int64_t activations, int32_t* chain_k,
-                               double* chain_t, uint8_t* replay, int64_t lanes,
-                               cpr_episode_record* recs, cpr_summary* sum, hipStream_t st) {
-  const int64_t blocks = lanes / kBlock;
-  hipLaunchKernelGGL(k_run_episodes, dim3((unsigned)blocks), dim3(kBlock), 0, st, P, seed, first,
-                     n_eps, mode, activations, chain_k, chain_t, replay, recs, sum);
+                               int32_t mode, int64_t activations, int32_t* spill, double* tlog,
+                               uint8_t* replay, int64_t lanes, cpr_episode_record* recs,
+                               cpr_summary* sum, hipStream_t st) {
+  const unsigned blocks = (unsigned)(lanes / kBlock);
+  if (mode == CPR_MODE_GYM)
+    hipLaunchKernelGGL(k_run_episodes<CPR_MODE_GYM>, dim3(blocks), dim3(kBlock), 0, st, P, seed,
+                       first, n_eps, activations, spill, tlog, replay, recs, sum);
+  else
+    hipLaunchKernelGGL(k_run_episodes<CPR_MODE_LOOP>, dim3(blocks), dim3(kBlock), 0, st, P, seed,
+                       first, n_eps, activations, spill, tlog, replay, recs, sum);
   return hipGetLastError();
 }
 
-hipError_t launch_reset(const NakParams& P, uint64_t seed, void* lanes, int64_t n,
-                        const uint8_t* mask, const uint64_t* eps, int32_t* chain_k,
-                        double* chain_t, int unit, const double* tab_nn, const double* tab_sg,
-                        int32_t tab_n, double* obs, hipStream_t st) {
+hipError_t launch_reset(const NakParams& P, uint64_t seed, const LockBuffers& B, int64_t n,
+                        const uint8_t* mask, const uint64_t* eps, int unit, const double* tab_nn,
+                        const double* tab_sg, int32_t tab_n, double* obs, hipStream_t st) {
   const unsigned blocks = (unsigned)((n + kBlock - 1) / kBlock);
-  hipLaunchKernelGGL(k_reset, dim3(blocks), dim3(kBlock), 0, st, P, seed, (LockLane*)lanes, n,
-                     mask, eps, chain_k, chain_t, unit, tab_nn, tab_sg, tab_n, obs);
+  hipLaunchKernelGGL(k_reset, dim3(blocks), dim3(kBlock), 0, st, P, seed, B, n, mask, eps, unit,
+                     tab_nn, tab_sg, tab_n, obs);
   return hipGetLastError();
 }
 
-hipError_t launch_step(const NakParams& P, uint64_t seed, void* lanes, int64_t n,
-                       const int32_t* actions, int32_t* chain_k, double* chain_t,
-                       uint8_t* replay, int unit, const double* tab_nn, const double* tab_sg,
-                       int32_t tab_n, const StepBuffers& b, hipStream_t st) {
+hipError_t launch_step(const NakParams& P, uint64_t seed, const LockBuffers& B, int64_t n,
+                       const int32_t* actions, int unit, const double* tab_nn,
+                       const double* tab_sg, int32_t tab_n, const StepBuffers& b,
+                       hipStream_t st) {
   const unsigned blocks = (unsigned)((n + kBlock - 1) / kBlock);
-  StepOut o{b.obs, b.reward, b.done, b.era, b.erd, b.eprog, b.ect, b.est, b.esteps, b.eacts,
-            b.hh, b.hm};
-  hipLaunchKernelGGL(k_step, dim3(blocks), dim3(kBlock), 0, st, P, seed, (LockLane*)lanes, n,
-                     actions, chain_k, chain_t, replay, unit, tab_nn, tab_sg, tab_n, o);
+  hipLaunchKernelGGL(k_step, dim3(blocks), dim3(kBlock), 0, st, P, seed, B, n, actions, unit,
+                     tab_nn, tab_sg, tab_n, b);
   return hipGetLastError();
 }
 
 hipError_t launch_observe_fields(const void* lanes, int64_t n, int32_t* f, hipStream_t st) {
   const unsigned blocks = (unsigned)((n + kBlock - 1) / kBlock);
-  hipLaunchKernelGGL(k_observe_fields, dim3(blocks), dim3(kBlock), 0, st, (const LockLane*)lanes,
-                     n, f);
+  hipLaunchKernelGGL(k_observe_fields, dim3(blocks), dim3(kBlock), 0, st, lanes, n, f);
   return hipGetLastError();
 }
 
@@ -382,12 +370,14 @@ hipError_t launch_stream_fill(uint64_t seed, uint64_t ep, uint32_t idx0, uint32_
 
 size_t lock_lane_bytes() { return sizeof(LockLane); }
 
-int run_episodes_blocks_per_cu() {
+int run_episodes_blocks_per_cu(int32_t mode) {
   int blocks = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, k_run_episodes, kBlock, 0) !=
-          hipSuccess ||
-      blocks <= 0)
-    blocks = 2;
+  hipError_t e = mode == CPR_MODE_GYM
+                     ? hipOccupancyMaxActiveBlocksPerMultiprocessor(
+                           &blocks, k_run_episodes<CPR_MODE_GYM>, kBlock, 0)
+                     : hipOccupancyMaxActiveBlocksPerMultiprocessor(
+                           &blocks, k_run_episodes<CPR_MODE_LOOP>, kBlock, 0);
+  if (e != hipSuccess || blocks <= 0) blocks = 2;
   return blocks;
 }
 

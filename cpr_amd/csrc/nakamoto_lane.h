@@ -16,6 +16,10 @@
 //   BRef.ra         attacker reward count along the chain = rewards[0] (simulator.ml:377-388)
 //   BRef.fork       height of the block's common ancestor with the private chain
 //                   (Dagtools.common_ancestor, dagtools.ml:102-121)
+//
+// Per-lane memory (LaneMem): the private chain's mining activations in a 16-slot ring
+// (LDS in the fused kernel) with a global spill for deeper chains, and the time of every
+// activation in a coalesced [k][lane] log that is read only for the final head.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -28,26 +32,24 @@ namespace cpr {
 
 enum : int32_t { A_ADOPT = 0, A_OVERRIDE = 1, A_MATCH = 2, A_WAIT = 3 };
 enum : int32_t { P_HONEST = 0, P_SIMPLE = 1, P_ES2014 = 2, P_SM1 = 3, P_TABLE = 4 };
-enum : uint32_t { ST_TIE = 1u, ST_OVERLAP = 2u, ST_DEEP_FORK = 4u, ST_TIE_UNRESOLVED = 8u };
+enum : uint32_t {
+  ST_TIE = 1u,
+  ST_OVERLAP = 2u,
+  ST_DEEP_FORK = 4u,
+  ST_TIE_UNRESOLVED = 8u,
+  ST_STALE_TIME = 16u
+};
 
-// ---- exact replay of one delivery window (used only when two deliveries tie in fp64)
-//
-// At every activation the reference's event queue holds exactly one element, the clock
-// (all earlier windows have drained; overlaps are flagged separately). So when a defender
-// receives the fresh defender block and the attacker's matching release at the very same
-// instant, the winner is fixed by replaying this window's events through the same skew
-// heap (orderedQueue.ml:17-47) with the handlers of simulator.ml:421-508. Blocks of the
-// window: x = 0 is the defender block b, x = 1..r the released chain a_rlo..a_rhi.
-constexpr int32_t RCAP = 512;  // heap nodes per lane
+constexpr int32_t RING = 16;   // private-chain slots kept in the ring
+constexpr int32_t RCAP = 512;  // tie-replay heap nodes per lane
 constexpr int32_t RMAX = 16;   // released blocks per window the replay supports
+constexpr int64_t REPLAY_BYTES = 8704;  // RCAP * 16 + 2 * (RMAX + 1) * 8, rounded
 
 struct ReplayNode {
   double t;
   int32_t ev;
   int16_t l, r;
 };
-
-constexpr int64_t REPLAY_BYTES = 8704;  // RCAP * 16 + 2 * (RMAX + 1) * 8, rounded
 
 struct ReplayMem {
   ReplayNode* nodes;  // RCAP
@@ -59,6 +61,82 @@ struct ReplayMem {
     return m;
   }
 };
+
+struct LaneMem {
+  int32_t* ring;      // ring[(m & (RING-1)) * ring_stride]: mining activation of chain block m
+  int32_t* spill;     // spill[m * spill_stride], m < cap: chain blocks evicted from the ring
+  double* tlog;       // tlog[(k & tmask) * tlog_stride]: time of activation k
+  int64_t ring_stride, spill_stride, tlog_stride;
+  int32_t tmask, cap;
+  ReplayMem replay;
+};
+
+struct BRef {
+  int32_t h;     // height (nakamoto.ml:11-14)
+  int32_t ra;    // attacker blocks on the chain up to here
+  int32_t k;     // activation that mined it (DAG serial - 1); -1 = genesis
+  int32_t fork;  // height of the common ancestor with the attacker's private chain
+};
+
+struct NakParams {
+  uint64_t t_att;       // floor(alpha * 2^32)
+  int32_t d;            // defenders
+  int32_t arrive;       // attacker messages reach defenders (gamma > 0 or two-agents)
+  double ev;            // activation delay (expected block interval)
+  double delta;         // defender -> defender delay (network.ml:375)
+  double dmax;          // attacker -> defender uniform [0, dmax) (network.ml:350-357)
+  int64_t max_steps;
+  double max_progress;
+  double max_time;
+  int32_t policy;
+  int32_t table_dim;
+  const uint8_t* table;
+  int32_t cap;          // spill slots per lane
+  int32_t tlog_len;     // time-log slots per lane (power of two)
+};
+
+__host__ __device__ inline uint64_t all_mask(int32_t d) {
+  return d >= 64 ? ~0ull : ((1ull << d) - 1ull);
+}
+
+// nakamoto_ssz.ml:374-440 (policy registry: sapirshtein-2016-sm1, eyal-sirer-2014,
+// simple, honest)
+__host__ __device__ inline int32_t nak_policy(int32_t policy, int32_t h, int32_t a, int32_t ev,
+                                              const uint8_t* table, int32_t dim) {
+  switch (policy) {
+    case P_HONEST:
+      return a > h ? A_OVERRIDE : (a < h ? A_ADOPT : A_WAIT);
+    case P_SIMPLE:
+      return h > 0 ? (a < h ? A_ADOPT : A_OVERRIDE) : A_WAIT;
+    case P_ES2014:
+      if (a < h) return A_ADOPT;
+      if (h == 0 && a == 1) return A_WAIT;
+      if (h == 1 && a == 1) return A_MATCH;
+      if (h == 1 && a == 2) return A_OVERRIDE;
+      if (h == 2 && a == 1) return A_ADOPT;
+      if (h > 0) return (a - h == 1) ? A_OVERRIDE : A_MATCH;
+      return A_WAIT;
+    case P_SM1:
+      if (h > a) return A_ADOPT;
+      if (h == 1 && a == 1) return A_MATCH;
+      if (h == a - 1 && h >= 1) return A_OVERRIDE;
+      return A_WAIT;
+    default: {
+      const int32_t hp = h < 0 ? 0 : (h >= dim ? dim - 1 : h);
+      const int32_t ap = a < 0 ? 0 : (a >= dim ? dim - 1 : a);
+      return (int32_t)table[(hp * dim + ap) * 2 + ev];
+    }
+  }
+}
+
+// ---- exact replay of one delivery window (used only when two deliveries tie in fp64)
+//
+// At every activation the reference's event queue holds exactly one element, the clock
+// (all earlier windows have drained; overlaps are flagged separately). So when a defender
+// receives the fresh defender block and the attacker's matching release at the very same
+// instant, the winner is fixed by replaying this window's events through the same skew
+// heap (orderedQueue.ml:17-47) with the handlers of simulator.ml:421-508. Blocks of the
+// window: x = 0 is the defender block b, x = 1..r the released chain a_rlo..a_rhi.
 
 enum : int32_t { RE_SC = 0, RE_SC2 = 1, RE_DAG = 2, RE_MV = 3, RE_ON = 4, RE_MDV = 5, RE_TX = 6, RE_RX = 7 };
 
@@ -89,17 +167,15 @@ struct SkewHeapLane {
   }
   // orderedQueue.ml:17-26, iterative: new equal-time elements sink below existing ones
   __host__ __device__ inline void push(double t, int32_t ev) {
-    int32_t parent = -1, side = 0;  // side 0 = left
+    int32_t parent = -1;
     int32_t node = root;
     for (;;) {
       if (node < 0) {
         const int32_t a = alloc(t, ev);
         if (parent < 0)
           root = a;
-        else if (side == 0)
-          n[parent].l = (int16_t)a;
         else
-          n[parent].r = (int16_t)a;
+          n[parent].l = (int16_t)a;
         return;
       }
       if (t < n[node].t) {
@@ -115,7 +191,6 @@ struct SkewHeapLane {
         n[node].r = tmp;
       }
       parent = node;
-      side = 0;
       node = n[node].l;
     }
   }
@@ -160,84 +235,13 @@ struct SkewHeapLane {
   }
 };
 
-struct BRef {
-  int32_t h;     // height (nakamoto.ml:11-14)
-  int32_t ra;    // attacker blocks on the chain up to here
-  int32_t k;     // activation index that mined it (DAG serial - 1); -1 = genesis
-  int32_t fork;  // height of the common ancestor with the attacker's private chain
-  double tm;     // mining time = Simulator.timestamp for these networks
-};
-
-struct NakParams {
-  uint64_t t_att;       // floor(alpha * 2^32)
-  int32_t d;            // defenders
-  int32_t arrive;       // attacker messages reach defenders (gamma > 0 or two-agents)
-  double ev;            // activation delay (expected block interval)
-  double delta;         // defender -> defender delay (network.ml:375)
-  double dmax;          // attacker -> defender uniform [0, dmax) (network.ml:350-357)
-  int64_t max_steps;
-  double max_progress;
-  double max_time;
-  int32_t policy;
-  int32_t table_dim;
-  const uint8_t* table;
-  int32_t cap;          // chain slots per lane
-  int32_t _pad;
-};
-
-// per-lane private chain storage, slot m in [1, cap): mining activation and time
-struct Chain {
-  int32_t* k;
-  double* t;
-  int64_t stride;
-  __host__ __device__ inline int32_t getk(int32_t m) const { return k[(int64_t)m * stride]; }
-  __host__ __device__ inline double gett(int32_t m) const { return t[(int64_t)m * stride]; }
-  __host__ __device__ inline void put(int32_t m, int32_t kk, double tt) const {
-    k[(int64_t)m * stride] = kk;
-    t[(int64_t)m * stride] = tt;
-  }
-};
-
-__host__ __device__ inline uint64_t all_mask(int32_t d) {
-  return d >= 64 ? ~0ull : ((1ull << d) - 1ull);
-}
-
-// nakamoto_ssz.ml:374-440 (policy registry: sapirshtein-2016-sm1, eyal-sirer-2014,
-// simple, honest)
-__host__ __device__ inline int32_t nak_policy(int32_t policy, int32_t h, int32_t a, int32_t ev,
-                                              const uint8_t* table, int32_t dim) {
-  switch (policy) {
-    case P_HONEST:
-      return a > h ? A_OVERRIDE : (a < h ? A_ADOPT : A_WAIT);
-    case P_SIMPLE:
-      return h > 0 ? (a < h ? A_ADOPT : A_OVERRIDE) : A_WAIT;
-    case P_ES2014:
-      if (a < h) return A_ADOPT;
-      if (h == 0 && a == 1) return A_WAIT;
-      if (h == 1 && a == 1) return A_MATCH;
-      if (h == 1 && a == 2) return A_OVERRIDE;
-      if (h == 2 && a == 1) return A_ADOPT;
-      if (h > 0) return (a - h == 1) ? A_OVERRIDE : A_MATCH;
-      return A_WAIT;
-    case P_SM1:
-      if (h > a) return A_ADOPT;
-      if (h == 1 && a == 1) return A_MATCH;
-      if (h == a - 1 && h >= 1) return A_OVERRIDE;
-      return A_WAIT;
-    default: {
-      const int32_t hp = h < 0 ? 0 : (h >= dim ? dim - 1 : h);
-      const int32_t ap = a < 0 ? 0 : (a >= dim ? dim - 1 : a);
-      return (int32_t)table[(hp * dim + ap) * 2 + ev];
-    }
-  }
-}
-
-// Replay of a defender-mined window in which the attacker released a_rlo..a_rhi, the top
-// one at the fresh block's height. Returns the set of non-miner defenders that end on the
-// released top (first received wins, nakamoto.ml:85-89). *ok = false on capacity overflow.
-__host__ __device__ inline uint64_t tie_replay(const NakParams& P, const Stream& S, const Chain& c,
+// Replay of a defender-mined window in which the attacker released a_rlo..a_rhi (shared
+// at activation count kw, top first), the top one at the fresh block's height. Returns the
+// non-miner defenders that end on the released top (first received wins,
+// nakamoto.ml:85-89). *ok = false on capacity overflow.
+__host__ __device__ inline uint64_t tie_replay(const NakParams& P, const Stream& S,
                                                const ReplayMem& M, int32_t miner, double t,
-                                               int32_t rlo, int32_t rhi, bool* ok) {
+                                               int32_t rlo, int32_t rhi, int32_t kw, bool* ok) {
   const int32_t r = rhi - rlo + 1;
   if (r > RMAX) {
     *ok = false;
@@ -307,9 +311,9 @@ __host__ __device__ inline uint64_t tie_replay(const NakParams& P, const Stream&
           for (int32_t jj = 1; jj <= P.d; ++jj)
             if (jj != miner) H.push(now + P.delta, re_ev(RE_RX, jj, 0));
         } else {
-          const uint32_t serial = (uint32_t)(c.getk(rlo + x - 1) + 1);
+          const uint32_t off = (uint32_t)(r - x);  // share order: top first
           for (int32_t jj = 1; jj <= P.d; ++jj) {
-            const double u = S.link_u(serial, (uint32_t)jj);
+            const double u = S.link_u((uint32_t)kw, off, (uint32_t)jj);
             H.push(now + (u * (P.dmax - 0.0) + 0.0), re_ev(RE_RX, jj, x));
           }
         }
@@ -341,45 +345,54 @@ struct NakLane {
   int32_t wminer;    // miner of the current window's activation (0 = attacker)
   int32_t event;     // observation event: 0 ProofOfWork, 1 Network
   int32_t rlo, rhi;  // chain indices released by the last action
+  int32_t rkw;       // activation count when they were shared (keyed-stream coordinate)
   uint32_t status;
   BRef p0, pub, D, A, b;
   uint64_t onA;      // bit j-1: defender j prefers A (else D)
   int32_t lca_da;    // height of LCA(D, A)
   // previous window, for the exact overlap check of the next activation
   double w_t, w_bound;
-  int32_t w_rlo, w_rhi, w_hasb, w_miner;
+  int32_t w_rlo, w_rhi, w_hasb, w_kw;
 
-  __host__ __device__ inline BRef chain_ref(const Chain& c, int32_t m) const {
+  __host__ __device__ inline int32_t chain_k(const LaneMem& M, int32_t m) const {
+    // two loads in their own address spaces (ds_read, then a rare global load) rather than
+    // a select of pointers, which would compile to a generic flat load
+    int32_t v = M.ring[(int64_t)(m & (RING - 1)) * M.ring_stride];
+    // volatile: stops the compiler from sinking both loads into one generic (flat) load
+    if (m <= n - RING) v = *(volatile const int32_t*)&M.spill[(int64_t)m * M.spill_stride];
+    return v;
+  }
+
+  __host__ __device__ inline BRef chain_ref(const LaneMem& M, int32_t m) const {
     if (m <= 0) return p0;
     BRef r;
     r.h = p0.h + m;
     r.ra = p0.ra + m;
-    r.k = c.getk(m);
+    r.k = chain_k(M, m);
     r.fork = r.h;
-    r.tm = c.gett(m);
     return r;
   }
 
   __host__ __device__ inline void init() {
     BRef g;
-    g.h = 0; g.ra = 0; g.k = -1; g.fork = 0; g.tm = 0.0;
+    g.h = 0; g.ra = 0; g.k = -1; g.fork = 0;
     p0 = pub = D = A = b = g;
     t = 0.0;
     k = 0; n = 0; rel = 0; n_ba = 0; pend = -1; wminer = 0; event = 0;
-    rlo = 1; rhi = 0; status = 0u; onA = 0ull; lca_da = 0;
-    w_t = 0.0; w_bound = -__builtin_inf(); w_rlo = 1; w_rhi = 0; w_hasb = 0; w_miner = 0;
+    rlo = 1; rhi = 0; rkw = 0; status = 0u; onA = 0ull; lca_da = 0;
+    w_t = 0.0; w_bound = -__builtin_inf(); w_rlo = 1; w_rhi = 0; w_hasb = 0; w_kw = 0;
   }
 
   // latest finite arrival of the previous window (exact; only evaluated when the next
   // activation lands inside the conservative bound, ~1e-9 of activations in the gym)
-  __host__ __device__ inline double window_last_arrival(const NakParams& P, const Stream& S,
-                                                        const Chain& c) const {
+  __host__ __device__ inline double window_last_arrival(const NakParams& P,
+                                                        const Stream& S) const {
     double last = -__builtin_inf();
     if (w_hasb && P.d >= 2) last = w_t + P.delta;
     if (w_rhi >= w_rlo && P.arrive) {
       for (int32_t j = 1; j <= P.d; ++j)
         for (int32_t m = w_rlo; m <= w_rhi; ++m) {
-          const double u = S.link_u((uint32_t)(c.getk(m) + 1), (uint32_t)j);
+          const double u = S.link_u((uint32_t)w_kw, (uint32_t)(w_rhi - m), (uint32_t)j);
           const double a = w_t + (u * (P.dmax - 0.0) + 0.0);
           last = a > last ? a : last;
         }
@@ -389,29 +402,30 @@ struct NakLane {
 
   // StochasticClock + Dag + the attacker's prepare (simulator.ml:465-480, engine.ml:108-121,
   // nakamoto_ssz.ml:291-318)
-  __host__ __device__ inline void activate(const NakParams& P, const Stream& S, const Chain& c) {
+  __host__ __device__ inline void activate(const NakParams& P, const Stream& S, const LaneMem& M) {
     const Words4 w = S.block((uint32_t)k, TAG_ACT);
     const double tn = t + (-1.0 * P.ev) * cpr_log(u53(w.w2, w.w3));
     if (tn <= w_bound) {
-      if (tn <= window_last_arrival(P, S, c)) status |= ST_OVERLAP;
+      if (tn <= window_last_arrival(P, S)) status |= ST_OVERLAP;
     }
     t = tn;
+    M.tlog[(int64_t)(k & M.tmask) * M.tlog_stride] = tn;
     const int32_t ka = k;
     ++k;
     int32_t miner = 0;
     if ((uint64_t)w.w0 >= P.t_att) miner = 1 + (int32_t)(((uint64_t)w.w1 * (uint64_t)P.d) >> 32);
     wminer = miner;
     // deliver pending releases to the attacker's public model (strict >)
-    if (pend >= 0) {
-      if (p0.h + pend > pub.h) pub = chain_ref(c, pend);  // loads only when it moves
-    }
+    if (pend >= 0 && p0.h + pend > pub.h) pub = chain_ref(M, pend);
     if (miner == 0) {
       int32_t m = n + 1;
-      if (m >= P.cap) {
+      if (m >= M.cap) {
         status |= ST_DEEP_FORK;
-        m = P.cap - 1;
+        m = M.cap - 1;
       }
-      c.put(m, ka, t);
+      int32_t* slot = M.ring + (int64_t)(m & (RING - 1)) * M.ring_stride;
+      if (m > RING) M.spill[(int64_t)(m - RING) * M.spill_stride] = *slot;  // evict
+      *slot = ka;
       n = m;
       event = 0;
     } else {
@@ -420,7 +434,6 @@ struct NakLane {
       b.ra = par.ra;
       b.k = ka;
       b.fork = par.fork;
-      b.tm = t;
       if (b.h > pub.h) pub = b;
       event = 1;
     }
@@ -469,6 +482,7 @@ struct NakLane {
       if (mf > rel) {
         rlo = rel + 1;
         rhi = mf;
+        rkw = k;
         rel = mf;
       }
       pend = mf;
@@ -481,8 +495,7 @@ struct NakLane {
 
   // deliveries of the window: the fresh defender block and the attacker's release reach
   // the defenders (simulator.ml:481-508 with update_head, nakamoto.ml:85-89)
-  __host__ __device__ inline void resolve(const NakParams& P, const Stream& S, const Chain& c,
-                                          const ReplayMem& M) {
+  __host__ __device__ inline void resolve(const NakParams& P, const Stream& S, const LaneMem& M) {
     const bool released = rhi >= rlo && P.arrive;
     const uint64_t all = all_mask(P.d);
     double bound = -__builtin_inf();
@@ -491,7 +504,7 @@ struct NakLane {
       if (released) {
         const int32_t xh = p0.h + rhi;
         if (xh > b.h) {
-          A = chain_ref(c, rhi);
+          A = chain_ref(M, rhi);
           onA = all;
           lca_da = b.fork;
         } else if (xh == b.h) {
@@ -503,7 +516,7 @@ struct NakLane {
             if (j == wminer) continue;
             double v = -__builtin_inf();
             for (int32_t m = rlo; m <= rhi; ++m) {
-              const double u = S.link_u((uint32_t)(c.getk(m) + 1), (uint32_t)j);
+              const double u = S.link_u((uint32_t)rkw, (uint32_t)(rhi - m), (uint32_t)j);
               const double a = t + (u * (P.dmax - 0.0) + 0.0);
               v = a > v ? a : v;
             }
@@ -514,13 +527,13 @@ struct NakLane {
             // same instant at some defender: the queue order decides
             status |= ST_TIE;
             bool ok = false;
-            const uint64_t exact = tie_replay(P, S, c, M, wminer, t, rlo, rhi, &ok);
+            const uint64_t exact = tie_replay(P, S, M.replay, wminer, t, rlo, rhi, rkw, &ok);
             if (ok)
               mask = exact;
             else
               status |= ST_TIE_UNRESOLVED;
           }
-          A = chain_ref(c, rhi);
+          A = chain_ref(M, rhi);
           onA = mask;
           lca_da = b.fork;
         } else {
@@ -535,7 +548,7 @@ struct NakLane {
       const int32_t hs = onA ? A.h : D.h;
       if (p0.h + rhi > hs) {
         lca_da = D.fork;
-        A = chain_ref(c, rhi);
+        A = chain_ref(M, rhi);
         onA = all;
       }
     }
@@ -547,8 +560,8 @@ struct NakLane {
     w_bound = bound;
     w_rlo = rlo;
     w_rhi = released ? rhi : 0;
+    w_kw = rkw;
     w_hasb = wminer != 0;
-    w_miner = wminer;
     wminer = 0;
     rlo = 1;
     rhi = 0;
@@ -556,8 +569,8 @@ struct NakLane {
 
   // Ref.winner over [attacker preferred; defender tips 1..d] (engine.ml:195-206,
   // nakamoto.ml:43-48): first maximal height, attacker listed first
-  __host__ __device__ inline BRef head(const NakParams& P, const Chain& c) const {
-    BRef best = chain_ref(c, n_ba);
+  __host__ __device__ inline BRef head(const NakParams& P, const LaneMem& M) const {
+    BRef best = chain_ref(M, n_ba);
     const uint64_t all = all_mask(P.d);
     const uint64_t mb = wminer ? (1ull << (wminer - 1)) : 0ull;
     const uint64_t ma = onA & ~mb;
@@ -575,6 +588,13 @@ struct NakLane {
     }
     if (bh > best.h) best = cand;
     return best;
+  }
+
+  // Simulator.timestamp of a block = its mining time for these networks
+  __host__ __device__ inline double time_of(const LaneMem& M, const BRef& x) {
+    if (x.k < 0) return 0.0;
+    if (k - x.k > M.tmask + 1) status |= ST_STALE_TIME;  // slot already reused
+    return M.tlog[(int64_t)(x.k & M.tmask) * M.tlog_stride];
   }
 
   __host__ __device__ inline int32_t policy_action(const NakParams& P) const {

@@ -197,7 +197,7 @@ double OcamlSimRng::act_delay(int) {
 
 int32_t OcamlSimRng::pow_bits(int) { return r->bits(); }
 
-double OcamlSimRng::link_delay(const Link& l, int, int) {
+double OcamlSimRng::link_delay(const Link& l, const Block*) {
   switch (l.kind) {
     case D_CONST: return l.a;
     case D_UNIFORM: return r->float_(l.b - l.a) + l.a;
@@ -229,11 +229,12 @@ double KeyedSimRng::act_delay(int j) {
 
 int32_t KeyedSimRng::pow_bits(int serial) { return (int32_t)ks.pow_bits((uint32_t)serial); }
 
-double KeyedSimRng::link_delay(const Link& l, int serial, int) {
+double KeyedSimRng::link_delay(const Link& l, const Block* m) {
+  const uint32_t kw = (uint32_t)m->share_k, off = (uint32_t)m->share_off;
   switch (l.kind) {
     case D_CONST: return l.a;
-    case D_UNIFORM: return ks.link_u((uint32_t)serial, (uint32_t)l.dest) * (l.b - l.a) + l.a;
-    case D_EXP: return -1. * l.a * cpr_log(ks.link_u((uint32_t)serial, (uint32_t)l.dest));
+    case D_UNIFORM: return ks.link_u(kw, off, (uint32_t)l.dest) * (l.b - l.a) + l.a;
+    case D_EXP: return -1. * l.a * cpr_log(ks.link_u(kw, off, (uint32_t)l.dest));
   }
   return 0.0;
 }
@@ -340,6 +341,7 @@ void Sim::handle_action(int node, const Action& act) {
   struct Rec {
     Sim* s;
     int node;
+    int off;
     void share(Block* msg) {
       Vis& v = msg->vis[node];
       switch (v.kind) {
@@ -349,11 +351,13 @@ void Sim::handle_action(int node, const Action& act) {
         case WITHHELD:
           s->schedule_now(Event{EV_NET_TX, node, K_NETWORK, msg, -1});
           v.kind = RELEASED;
+          msg->share_k = s->c_activations;
+          msg->share_off = off++;
           for (auto* p : msg->parents) share(p);
           return;
       }
     }
-  } rec{this, node};
+  } rec{this, node, 0};
   for (auto* b : act.share) rec.share(b);
   for (auto& d : act.append) {
     int id = (int)drafts.size();
@@ -415,7 +419,7 @@ void Sim::handle_event(const Event& ev) {
     }
     case EV_NET_TX: {
       for (auto& l : net.nodes[ev.node].links) {
-        double delay = rng->link_delay(l, ev.blk->serial, ev.node);
+        double delay = rng->link_delay(l, ev.blk);
         schedule(delay, Event{EV_NET_RX, l.dest, K_NETWORK, ev.blk, -1});
       }
       break;

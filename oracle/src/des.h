@@ -48,6 +48,9 @@ struct Block {
   std::vector<Vis> vis;
   std::vector<double> received_at;
   std::vector<double> rewards;
+  // keyed-stream coordinates of the message (set when the block is shared)
+  int share_k = -1;
+  int share_off = 0;
 };
 
 struct Draft {
@@ -115,7 +118,7 @@ struct SimRng {
   virtual int miner(int k) = 0;
   virtual double act_delay(int j) = 0;
   virtual int32_t pow_bits(int serial) = 0;
-  virtual double link_delay(const Link& l, int serial, int src) = 0;
+  virtual double link_delay(const Link& l, const Block* msg) = 0;
 };
 
 // OCaml Random: alias sampling exactly as distributions.ml:143-196
@@ -128,7 +131,7 @@ struct OcamlSimRng : SimRng {
   int miner(int k) override;
   double act_delay(int j) override;
   int32_t pow_bits(int serial) override;
-  double link_delay(const Link& l, int serial, int src) override;
+  double link_delay(const Link& l, const Block* msg) override;
 };
 
 // keyed Philox stream (keyed_stream.h); weights must be [alpha, equal rest]
@@ -141,7 +144,7 @@ struct KeyedSimRng : SimRng {
   int miner(int k) override;
   double act_delay(int j) override;
   int32_t pow_bits(int serial) override;
-  double link_delay(const Link& l, int serial, int src) override;
+  double link_delay(const Link& l, const Block* msg) override;
 };
 
 struct Sim;

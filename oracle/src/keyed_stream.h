@@ -9,7 +9,9 @@
 //   key   = (seed_lo, seed_hi)                          Philox4x32-10 (Salmon et al. 2011)
 //   act   : ctr = (ep_lo, ep_hi, j, TAG_ACT)   w0,w1 -> miner of activation j
 //                                              w2,w3 -> 53-bit u, delay of clock j
-//   link  : ctr = (ep_lo, ep_hi, serial, TAG_LINK | dest>>1)  words (2*(dest&1), +1) -> u
+//   link  : ctr = (ep_lo, ep_hi, kw, TAG_LINK | off<<12 | dest>>1)  words (2*(dest&1), +1) -> u
+//           kw  = activations simulated when the message was shared (c_activations),
+//           off = position of the message in that action's recursive share order
 //   pow   : ctr = (ep_lo, ep_hi, serial, TAG_POW)  w0 & 0x3FFFFFFF
 //
 // exponential(ev) = (-1 * ev) * cpr_log(u)   (same expression shape as distributions.ml:24)
@@ -154,9 +156,9 @@ struct KeyedStream {
     block(j, TAG_ACT, w);
     return u53(w[2], w[3]);
   }
-  double link_u(uint32_t serial, uint32_t dest) const {
+  double link_u(uint32_t kw, uint32_t off, uint32_t dest) const {
     uint32_t w[4];
-    block(serial, TAG_LINK | (dest >> 1), w);
+    block(kw, TAG_LINK | (off << 12) | (dest >> 1), w);
     return (dest & 1) ? u53(w[2], w[3]) : u53(w[0], w[1]);
   }
   uint32_t pow_bits(uint32_t serial) const {

@@ -31,6 +31,26 @@ struct Cfg {
   int two_agents;  // loop mode on the two-agents network
 };
 
+// host stand-in for the kernel's per-lane memory (ring, spill, time log, replay scratch)
+struct HostMem {
+  std::vector<int32_t> ring, spill;
+  std::vector<double> tlog;
+  std::vector<uint8_t> replay;
+  explicit HostMem(const NakParams& P)
+      : ring(RING), spill(P.cap), tlog(P.tlog_len), replay(REPLAY_BYTES) {}
+  LaneMem lane() {
+    LaneMem M;
+    M.ring = ring.data();
+    M.spill = spill.data();
+    M.tlog = tlog.data();
+    M.ring_stride = M.spill_stride = M.tlog_stride = 1;
+    M.tmask = (int32_t)tlog.size() - 1;
+    M.cap = (int32_t)spill.size();
+    M.replay = ReplayMem::at(replay.data());
+    return M;
+  }
+};
+
 extern "C" int oracle_two_agents_task(int, void*, uint64_t, uint64_t, double, int, int, int64_t*,
                                       double*, double*, double*, int32_t*, uint32_t*);
 
@@ -63,15 +83,13 @@ static bool run_gym(const Cfg& cf, uint64_t seed, uint64_t ep, Counters& C, std:
   P.max_time = __builtin_inf();
   P.policy = cf.policy < 4 ? cf.policy : 0;
   P.cap = cf.steps + 64;
-  std::vector<int32_t> ck(P.cap);
-  std::vector<double> ct(P.cap);
-  Chain c{ck.data(), ct.data(), 1};
-  std::vector<uint8_t> rbuf(REPLAY_BYTES);
-  const ReplayMem M = ReplayMem::at(rbuf.data());
+  P.tlog_len = 1 << 20;
+  HostMem mem(P);
+  const LaneMem M = mem.lane();
   Stream S{(uint32_t)seed, (uint32_t)(seed >> 32), (uint32_t)ep, (uint32_t)(ep >> 32)};
   NakLane L;
   L.init();
-  L.activate(P, S, c);
+  L.activate(P, S, M);
   bool ok = true;
   char buf[512];
   for (int s = 0;; s++) {
@@ -97,16 +115,17 @@ static bool run_gym(const Cfg& cf, uint64_t seed, uint64_t ep, Counters& C, std:
     oracle::StepInfo info{};
     g.step(act, obs, &done, &info);
     L.apply(act);
-    L.resolve(P, S, c, M);
-    L.activate(P, S, c);
-    BRef hd = L.head(P, c);
+    L.resolve(P, S, M);
+    L.activate(P, S, M);
+    BRef hd = L.head(P, M);
+    const double hd_tm = L.time_of(M, hd);
     if (hd.ra != (int)info.episode_reward_attacker || hd.h - hd.ra != (int)info.episode_reward_defender ||
-        hd.h != info.head_height || hd.tm != info.episode_chain_time || L.t != info.episode_sim_time ||
+        hd.h != info.head_height || hd_tm != info.episode_chain_time || L.t != info.episode_sim_time ||
         L.k != info.episode_n_activations || miner_of(P, S, hd.k) != info.head_miner) {
       snprintf(buf, sizeof buf,
                "step %d head lane (ra %d h %d tm %.17g t %.17g k %d miner %d) oracle (ra %g rd %g h %d "
                "tm %.17g t %.17g k %ld miner %d)",
-               s, hd.ra, hd.h, hd.tm, L.t, L.k, miner_of(P, S, hd.k), info.episode_reward_attacker,
+               s, hd.ra, hd.h, hd_tm, L.t, L.k, miner_of(P, S, hd.k), info.episode_reward_attacker,
                info.episode_reward_defender, info.head_height, info.episode_chain_time,
                info.episode_sim_time, info.episode_n_activations, info.head_miner);
       why = buf;
@@ -147,26 +166,25 @@ static bool run_loop(const Cfg& cf, uint64_t seed, uint64_t ep, Counters& C, std
   P.max_progress = __builtin_inf();
   P.max_time = __builtin_inf();
   P.cap = cf.steps + 64;
-  std::vector<int32_t> ck(P.cap);
-  std::vector<double> ct(P.cap);
-  Chain c{ck.data(), ct.data(), 1};
-  std::vector<uint8_t> rbuf(REPLAY_BYTES);
-  const ReplayMem M = ReplayMem::at(rbuf.data());
+  P.tlog_len = 1 << 20;
+  HostMem mem(P);
+  const LaneMem M = mem.lane();
   Stream S{(uint32_t)seed, (uint32_t)(seed >> 32), (uint32_t)ep, (uint32_t)(ep >> 32)};
   NakLane L;
   L.init();
   for (int i = 0; i < cf.steps; i++) {
-    L.activate(P, S, c);
+    L.activate(P, S, M);
     L.apply(L.policy_action(P));
-    L.resolve(P, S, c, M);
+    L.resolve(P, S, M);
   }
-  BRef hd = L.head(P, c);
+  BRef hd = L.head(P, M);
+    const double hd_tm = L.time_of(M, hd);
   C.episodes++;
-  if (hd.ra != (int)rew[0] || hd.h - hd.ra != (int)rew[1] || hd.h != hh || hd.tm != ht ||
+  if (hd.ra != (int)rew[0] || hd.h - hd.ra != (int)rew[1] || hd.h != hh || hd_tm != ht ||
       L.k != acts[0] + acts[1]) {
     char buf[256];
     snprintf(buf, sizeof buf, "loop lane (ra %d rd %d tm %.17g) oracle (%g %g %.17g)", hd.ra,
-             hd.h - hd.ra, hd.tm, rew[0], rew[1], ht);
+             hd.h - hd.ra, hd_tm, rew[0], rew[1], ht);
     why = buf;
     C.mismatches++;
     return false;

@@ -10,14 +10,14 @@ import sys
 
 tag = sys.argv[1]
 eps = int(sys.argv[2]) if len(sys.argv) > 2 else 393216
-K = "cpr::k_run_episodes"
+K = "k_run_episodes"
 
 
 def agg(path):
     a = collections.defaultdict(lambda: collections.defaultdict(float))
     n = collections.Counter()
     for r in csv.DictReader(open(path)):
-        k = r["Kernel_Name"].split("(")[0]
+        k = "k_run_episodes" if "k_run_episodes" in r["Kernel_Name"] else r["Kernel_Name"].split("(")[0]
         a[k][r["Counter_Name"]] += float(r["Counter_Value"])
         n[(k, r["Counter_Name"])] += 1
     return a, n
@@ -30,7 +30,7 @@ for p in ["prof_pmc_sq", "prof_pmc_fetch", "prof_pmc_write"]:
         for c, x in v.items():
             res.setdefault(k, {})[c] = {"sum": x, "dispatches": n[(k, c)], "per_dispatch": x / n[(k, c)]}
 tr = list(csv.DictReader(open("gpurun_out/prof_trace/run_kernel_trace.csv")))
-durs = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in tr if r["Kernel_Name"].startswith(K)]
+durs = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in tr if K in r["Kernel_Name"]]
 acts = eps * 2017
 r = res[K]
 s = {
