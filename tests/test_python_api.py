@@ -1,0 +1,128 @@
+"""The Python drop-in API on the device (mirrors gym/ocaml/test/test_engine.py,
+test_envs.py and test_protocols.py of the reference)."""
+
+import numpy as np
+import pytest
+
+from cpr_amd import engine, envs, protocols, wrappers
+
+pytestmark = pytest.mark.gpu
+
+
+def run_episode(env, policy):
+    obs = env.reset()
+    done = False
+    while not done:
+        obs, rew, done, info = env.step(env.policy(obs, policy))
+    return obs, rew, done, info
+
+
+def fuzz_episode(env):
+    obs = env.reset()
+    done = False
+    while not done:
+        obs, rew, done, info = env.step(env.action_space.sample())
+    return obs, rew, done, info
+
+
+def test_engine():
+    # test_engine.py:4-30
+    env = engine.create(proto=protocols.nakamoto(unit_observation=False), alpha=0.33,
+                        gamma=0.5, defenders=2, activation_delay=1)
+    engine.reset(env)
+    obs, rew, done, info = engine.step(env, 0)
+    assert not done
+    env = engine.create(proto=protocols.nakamoto(unit_observation=True), alpha=0.33,
+                        gamma=0.5, defenders=2, activation_delay=1)
+    engine.reset(env)
+    for _ in range(600):
+        obs, rew, done, info = engine.step(env, 3)
+    assert not done
+    assert info["episode_n_activations"] == 601
+    assert list(info)[:12] == [
+        "step_reward_attacker", "step_reward_defender", "step_progress", "step_chain_time",
+        "step_sim_time", "episode_reward_attacker", "episode_reward_defender",
+        "episode_progress", "episode_chain_time", "episode_sim_time", "episode_n_steps",
+        "episode_n_activations"]
+
+
+def test_render_strings(capsys):
+    # test_protocols.py:12-20 and test_envs.py:145-152
+    envs.Core(max_steps=1000).render()
+    assert capsys.readouterr().out.splitlines()[0] == (
+        "Nakamoto consensus; SSZ'16 attack space with unit observations; α=0.25 attacker")
+    envs.make("cpr_gym:cpr-nakamoto-v0").render()
+    out = capsys.readouterr().out.splitlines()
+    assert out[0] == "Nakamoto consensus; SSZ'16 attack space with unit observations; α=0.45 attacker"
+    assert out[-1] == "Actions: (0) Adopt | (1) Override | (2) Match | (3) Wait"
+
+
+def test_core_env_policies_and_spaces():
+    env = envs.make("core-v0", max_steps=2016)
+    assert list(env.policies()) == ["sapirshtein-2016-sm1", "eyal-sirer-2014", "simple", "honest"]
+    obs, rew, done, info = run_episode(env, "honest")
+    assert done and env.observation_space.contains(obs)
+    assert info["episode_n_steps"] == 2016
+    fuzz_episode(env)
+    with pytest.raises(ValueError):
+        env.policy(obs, "no-such-policy")
+    with pytest.raises(ValueError):
+        engine.policies(env.ocaml_env)["honest"](np.zeros(3))
+
+
+def test_reward_wrappers():
+    # test_envs.py:33-58
+    env = wrappers.SparseRelativeRewardWrapper(envs.make("core-v0", max_steps=32))
+    for _ in range(5):
+        _, r, done, info = run_episode(env, "honest")
+        tot = info["episode_reward_attacker"] + info["episode_reward_defender"]
+        assert r == pytest.approx(info["episode_reward_attacker"] / tot)
+        fuzz_episode(env)
+    env = wrappers.SparseRewardPerProgressWrapper(envs.make("core-v0", max_steps=32))
+    _, r, _, info = run_episode(env, "honest")
+    assert r == pytest.approx(info["episode_reward_attacker"] / info["episode_progress"])
+    env = wrappers.DenseRewardPerProgressWrapper(
+        envs.make("core-v0", max_progress=None), episode_len=32)
+    for _ in range(3):
+        run_episode(env, "honest")
+        fuzz_episode(env)
+
+
+def test_assumption_schedule_wrapper():
+    # test_envs.py:61-86
+    env = wrappers.AssumptionScheduleWrapper(envs.make("core-v0", max_steps=32), alpha=0.33,
+                                             gamma=0.1)
+    for _ in range(2):
+        obs, _, _, i = fuzz_episode(env)
+        assert i["alpha"] == 0.33 and i["gamma"] == 0.1
+        assert obs[-2] == 0.33 and obs[-1] == 0.1
+    env = wrappers.AssumptionScheduleWrapper(env, alpha=[0.1, 0.2, 0.3], gamma=[0.1, 0.5, 0.9])
+    seen = set()
+    for _ in range(6):
+        obs, _, _, i = run_episode(env, "honest")
+        assert i["alpha"] == obs[-2] and i["gamma"] == obs[-1]
+        seen.add(i["alpha"])
+    assert seen == {0.1, 0.2, 0.3}
+
+
+def test_episode_recorder():
+    env = wrappers.EpisodeRecorderWrapper(envs.make("core-v0", max_progress=100), n=10,
+                                          info_keys=["head_height"])
+    for _ in range(12):
+        run_episode(env, "honest")
+    assert len(env.erw_history) == 10
+    assert all("episode_reward" in e and "head_height" in e for e in env.erw_history)
+
+
+def test_registered_env_normalized_reward():
+    env = envs.make("cpr-nakamoto-v0", episode_len=64, alpha=0.3, gamma=0.5)
+    _, r, done, info = run_episode(env, "honest")
+    assert done and info["alpha"] == 0.3
+    # honest play: relative reward ~ alpha, normalised by alpha -> ~1
+    assert 0.0 <= r < 3.0
+
+
+def test_unsupported_protocol_is_loud():
+    with pytest.raises(NotImplementedError):
+        protocols.tailstorm(k=8, reward="discount", subblock_selection="heuristic",
+                            unit_observation=True)
