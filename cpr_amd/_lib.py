@@ -22,6 +22,14 @@ CPR_E_CAPACITY = -4
 CPR_E_STATE = -5
 
 PROTO_NAKAMOTO = 0
+PROTO_ETHEREUM = 1
+REWARD_CONSTANT = 0
+REWARD_DISCOUNT = 1
+ETH_POLICY_HONEST = 0
+ETH_POLICY_SELFISH_RELEASE = 1
+ETH_POLICY_SELFISH_DISCARD = 2
+ETH_POLICY_FN19 = 3
+ETH_POLICY_FN19PKEL = 4
 NET_SELFISH_MINING = 0
 NET_TWO_AGENTS = 1
 MODE_GYM = 0
@@ -53,7 +61,7 @@ class Config(ctypes.Structure):
         ("alpha", ctypes.c_double),
         ("gamma", ctypes.c_double),
         ("defenders", ctypes.c_int32),
-        ("_pad0", ctypes.c_int32),
+        ("reward_scheme", ctypes.c_int32),
         ("activation_delay", ctypes.c_double),
         ("propagation_delay", ctypes.c_double),
         ("max_steps", ctypes.c_int64),
@@ -77,7 +85,7 @@ class EpisodeRecord(ctypes.Structure):
         ("head_height", ctypes.c_int32),
         ("head_miner", ctypes.c_int32),
         ("status", ctypes.c_uint32),
-        ("_pad", ctypes.c_uint32),
+        ("head_work", ctypes.c_int32),
     ]
 
 
@@ -93,7 +101,7 @@ RECORD_DTYPE = np.dtype(
         ("head_height", "<i4"),
         ("head_miner", "<i4"),
         ("status", "<u4"),
-        ("_pad", "<u4"),
+        ("head_work", "<i4"),
     ]
 )
 assert RECORD_DTYPE.itemsize == ctypes.sizeof(EpisodeRecord)

@@ -162,7 +162,7 @@ __global__ __launch_bounds__(kBlock) void k_run_episodes(
       r.head_height = hd.h;
       r.head_miner = MODE == CPR_MODE_GYM ? miner_of(P, S, hd.k) : -1;
       r.status = L.status;
-      r._pad = 0u;
+      r.head_work = 0;
       recs[e] = r;
     }
   }

@@ -79,6 +79,8 @@ def make_config(
     unit_observation=True,
     n_lanes=0,
     table=None,
+    protocol=L.PROTO_NAKAMOTO,
+    reward_scheme=L.REWARD_CONSTANT,
 ):
     """Build a cpr_config. ``defenders=None`` applies the gym's rule
     d = max(2, ceil(1 / (1 - gamma))) (gym/ocaml/cpr_gym/envs.py:146-153)."""
@@ -87,7 +89,8 @@ def make_config(
             raise ValueError("gamma must be smaller than 1")
         defenders = max(2, int(math.ceil(1 / (1 - gamma))))
     c = L.Config()
-    c.protocol = L.PROTO_NAKAMOTO
+    c.protocol = protocol
+    c.reward_scheme = reward_scheme
     c.network = network
     c.mode = mode
     c.policy = policy

@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define CPR_ABI_VERSION 1
+#define CPR_ABI_VERSION 2
 
 typedef struct cpr_ctx cpr_ctx;
 typedef struct cpr_batch cpr_batch;
@@ -50,7 +50,32 @@ enum cpr_status {
   CPR_E_STATE = -5          /* call order violated (step before reset, ...) */
 };
 
-enum cpr_protocol { CPR_PROTO_NAKAMOTO = 0 };
+enum cpr_protocol {
+  CPR_PROTO_NAKAMOTO = 0, /* nakamoto.ml + nakamoto_ssz.ml */
+  CPR_PROTO_ETHEREUM = 1  /* ethereum.ml Byzantium + ethereum_ssz.ml (cpr_protocols.ml:39-49) */
+};
+
+/* incentive schemes (ethereum.ml:3,173-197) */
+enum cpr_reward_scheme {
+  CPR_REWARD_CONSTANT = 0, /* Ethereum `Constant` (whitepaper): uncle 15/16 */
+  CPR_REWARD_DISCOUNT = 1  /* Ethereum `Discount` (Byzantium): uncle (8 - dh) / 8 */
+};
+
+/* policy ids of the ethereum_ssz attack space (ethereum_ssz.ml:444-538) */
+enum cpr_ethereum_policy {
+  CPR_ETH_POLICY_HONEST = 0,
+  CPR_ETH_POLICY_SELFISH_RELEASE = 1,
+  CPR_ETH_POLICY_SELFISH_DISCARD = 2,
+  CPR_ETH_POLICY_FN19 = 3,
+  CPR_ETH_POLICY_FN19PKEL = 4
+};
+
+/* ethereum_ssz.ml:161-277: action = rank * 4 + own * 2 + foreign, rank in
+ * {Adopt_discard, Adopt_release, Override, Match, Release1, Wait} */
+enum cpr_ethereum_action_rank {
+  CPR_ETH_ADOPT_DISCARD = 0, CPR_ETH_ADOPT_RELEASE = 1, CPR_ETH_OVERRIDE = 2,
+  CPR_ETH_MATCH = 3, CPR_ETH_RELEASE1 = 4, CPR_ETH_WAIT = 5
+};
 
 enum cpr_network {
   CPR_NET_SELFISH_MINING = 0, /* network.ml:343-387, as the gym builds it (engine.ml:100-107) */
@@ -94,7 +119,7 @@ typedef struct cpr_config {
   double alpha;              /* attacker compute, [0,1] */
   double gamma;              /* selfish-mining gamma, [0,1] */
   int32_t defenders;         /* >= 2 for CPR_NET_SELFISH_MINING */
-  int32_t _pad0;
+  int32_t reward_scheme;     /* enum cpr_reward_scheme (Ethereum) */
   double activation_delay;   /* expected block interval, > 0 */
   double propagation_delay;  /* defender<->defender delay; the gym uses 1e-9 */
   int64_t max_steps;         /* GYM mode termination; <= 0 means max_int */
@@ -117,7 +142,7 @@ typedef struct cpr_episode_record {
   int32_t head_height;
   int32_t head_miner;        /* -1 = n/a (genesis) */
   uint32_t status;           /* enum cpr_episode_status bits */
-  uint32_t _pad;
+  int32_t head_work;         /* Ethereum head work (ethereum.ml:93-97); 0 for Nakamoto */
 } cpr_episode_record;
 
 #define CPR_HIST_BINS 64

@@ -280,9 +280,18 @@ void Sim::schedule_pow() {
   schedule(x, Event{EV_CLOCK, 0, K_POW, nullptr, -1});
 }
 
-bool Sim::validity(const Block* b) {
+bool Sim::validity(const Block* b) const {
+  if (proto == 1) return eth_validity(b);
   if (!b->has_pow || b->parents.size() != 1) return false;
   return b->value.height == b->parents[0]->value.height + 1 && b->value.miner >= 0;
+}
+
+void Sim::reward(Block* x) const {
+  if (proto == 1) {
+    eth_reward(x, eth_scheme, x->rewards);
+    return;
+  }
+  if (x->value.miner >= 0) x->rewards[x->value.miner] += 1.;
 }
 
 // simulator.ml:122-136
@@ -332,7 +341,7 @@ Block* Sim::append(bool pow, int node, const Draft& d) {
   Block* pre = x->parents.empty() ? nullptr : x->parents[0];
   if (!pre) throw std::runtime_error("Referee.precursor should go back to DAG root.");
   x->rewards = pre->rewards;
-  if (x->value.miner >= 0) x->rewards[x->value.miner] += 1.;
+  reward(x);
   return x;
 }
 

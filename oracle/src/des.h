@@ -30,10 +30,15 @@ struct Vis {
   double time = 0.0;
 };
 
+// block payload: Nakamoto {height; miner} (nakamoto.ml:8-12); Ethereum adds work
+// (ethereum.ml:69-73, always 0 for Nakamoto)
 struct NakData {
   int height = 0;
   int miner = -1;  // -1 = None
-  bool operator==(const NakData& o) const { return height == o.height && miner == o.miner; }
+  int work = 0;
+  bool operator==(const NakData& o) const {
+    return height == o.height && miner == o.miner && work == o.work;
+  }
 };
 
 struct Block {
@@ -52,6 +57,11 @@ struct Block {
   int share_k = -1;
   int share_off = 0;
 };
+
+// Ethereum referee pieces (ethereum.cpp): validity (ethereum.ml:102-151, Byzantium
+// max_uncles = 2) and the Constant / Discount reward functions (ethereum.ml:173-197)
+bool eth_validity(const Block* b);
+void eth_reward(const Block* x, int scheme, std::vector<double>& r);
 
 struct Draft {
   std::vector<Block*> parents;
@@ -184,6 +194,9 @@ struct Sim {
   int n_nodes = 0;
   uint32_t diag = 0;
   int pending_finite_rx = 0;
+  // protocol of the referee: 0 = Nakamoto, 1 = Ethereum (Byzantium parameters)
+  int proto = 0;
+  int eth_scheme = 0;  // Ethereum incentive scheme: 0 = Constant, 1 = Discount
 
   Sim(const Network& net, SimRng* rng);
   void init(std::vector<std::unique_ptr<NodeImpl>> nodes_);
@@ -198,8 +211,13 @@ struct Sim {
   bool dequeue(Event* ev);
   void loop(int activations);
   Block* head();
-  // Nakamoto referee (nakamoto.ml:19-57)
-  static bool validity(const Block* b);
+  // referee: Nakamoto (nakamoto.ml:19-57) or Ethereum (ethereum.ml:89-199)
+  bool validity(const Block* b) const;
+  void reward(Block* x) const;  // set_rewards (simulator.ml:377-388)
+  double progress(const Block* b) const {
+    return proto == 1 ? (double)b->value.work : (double)b->value.height;
+  }
+  // nakamoto.ml:43-48 and ethereum.ml:159-162 (both: first maximum height)
   static Block* winner(const std::vector<Block*>& l);
   static double timestamp(const Block* b);
 };
@@ -285,6 +303,7 @@ struct StepInfo {
       episode_chain_time, episode_sim_time;
   long episode_n_steps, episode_n_activations;
   int head_height, head_miner;  // head_miner -1 = n/a
+  int head_work;                // Ethereum head info (ethereum.ml:93-97)
 };
 
 // engine.ml of_module for the nakamoto_ssz attack space

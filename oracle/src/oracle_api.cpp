@@ -10,6 +10,8 @@
 
 #include "../../include/cpr_hip.h"
 #include "des.h"
+#include "ethereum.h"
+#include "ocaml_sort.h"
 
 using namespace oracle;
 
@@ -177,9 +179,192 @@ int oracle_gym_step(void* g, int action, double obs[4], double* reward, int* don
 
 uint32_t oracle_gym_diag(void* g) { return ((GymNakamoto*)g)->sim->diag; }
 
+// ---------------- OCaml Array.sort replica (stdlib/array.ml), Int.compare keys
+void oracle_ocaml_sort_ints(int32_t* a, int n) {
+  std::vector<int32_t> v(a, a + n);
+  ocaml_array_sort(v, [](int32_t x, int32_t y) { return x < y ? -1 : (x > y ? 1 : 0); });
+  memcpy(a, v.data(), sizeof(int32_t) * n);
+}
+// sort (key, tag) pairs by key only: exposes the heap sort's order among equal keys
+void oracle_ocaml_sort_pairs(int32_t* keys, int32_t* tags, int n) {
+  std::vector<std::pair<int32_t, int32_t>> v;
+  for (int i = 0; i < n; i++) v.push_back({keys[i], tags[i]});
+  ocaml_array_sort(v, [](const std::pair<int32_t, int32_t>& x,
+                         const std::pair<int32_t, int32_t>& y) {
+    return x.first < y.first ? -1 : (x.first > y.first ? 1 : 0);
+  });
+  for (int i = 0; i < n; i++) {
+    keys[i] = v[i].first;
+    tags[i] = v[i].second;
+  }
+}
+int oracle_at_most_first_ints(int32_t* a, int n, int k) {
+  std::vector<int32_t> v(a, a + n);
+  v = ocaml_at_most_first(v, [](int32_t x, int32_t y) { return x < y ? -1 : (x > y ? 1 : 0); }, k);
+  memcpy(a, v.data(), sizeof(int32_t) * v.size());
+  return (int)v.size();
+}
+
+// ---------------- Ethereum validity on a hand-built DAG (ethereum_test.ml:44-77)
+struct EthDag {
+  std::vector<std::unique_ptr<Block>> blocks;
+};
+void* oracle_eth_dag_new(int root_height, int root_work) {
+  auto* d = new EthDag();
+  auto r = std::make_unique<Block>();
+  r->value.height = root_height;
+  r->value.work = root_work;
+  r->value.miner = -1;
+  r->has_pow = true;
+  d->blocks.push_back(std::move(r));
+  return d;
+}
+void oracle_eth_dag_free(void* d) { delete (EthDag*)d; }
+// appends a block (always, like Dag.append) and returns its validity; *id = its index
+int oracle_eth_dag_mine(void* dp, int parent, const int32_t* uncles, int n_uncles, int32_t* id) {
+  auto* d = (EthDag*)dp;
+  auto b = std::make_unique<Block>();
+  Block* p = d->blocks[parent].get();
+  b->parents.push_back(p);
+  for (int i = 0; i < n_uncles; i++) b->parents.push_back(d->blocks[uncles[i]].get());
+  b->value.height = p->value.height + 1;
+  b->value.work = p->value.work + n_uncles + 1;
+  b->value.miner = 42;
+  b->has_pow = true;
+  for (auto* q : b->parents) q->children_app.push_back(b.get());
+  *id = (int32_t)d->blocks.size();
+  Block* raw = b.get();
+  d->blocks.push_back(std::move(b));
+  return eth_validity(raw) ? 1 : 0;
+}
+
+// ---------------- ethereum_ssz policies / observation encoding
+int oracle_eth_policy(int policy, const int32_t obs[10]) {
+  EthObs o{obs[0], obs[1], obs[2], obs[3], obs[4], obs[5], obs[6], obs[7], obs[8], obs[9]};
+  return eth_policy(policy, o);
+}
+void oracle_eth_obs_to_floats(const int32_t obs[10], int unit, double out[10]) {
+  EthObs o{obs[0], obs[1], obs[2], obs[3], obs[4], obs[5], obs[6], obs[7], obs[8], obs[9]};
+  eth_obs_to_floats(o, unit != 0, out);
+}
+void oracle_eth_obs_of_floats(const double in[10], int unit, int32_t out[10]) {
+  EthObs o = eth_obs_of_floats(in, unit != 0);
+  const int32_t v[10] = {o.public_height,  o.public_work,
+                         o.private_height, o.private_work,
+                         o.diff_height,    o.diff_work,
+                         o.public_orphans, o.private_orphans_inclusive,
+                         o.private_orphans_exclusive, o.event};
+  memcpy(out, v, sizeof(v));
+}
+
+// ---------------- Ethereum gym env handle (engine.ml:97-273 for ethereum_ssz)
+void* oracle_eth_gym_new(const cpr_config* c, int rng_mode, void* ocaml_rng, uint64_t episode) {
+  try {
+    return new GymEthereum(params_of(c), c->reward_scheme, rng_mode, (OcamlRandom*)ocaml_rng,
+                           c->seed, episode);
+  } catch (std::exception& e) {
+    set_err(e.what());
+    return nullptr;
+  }
+}
+void oracle_eth_gym_free(void* g) { delete (GymEthereum*)g; }
+int oracle_eth_gym_reset(void* g, double obs[10]) {
+  try {
+    ((GymEthereum*)g)->reset(obs);
+    return 0;
+  } catch (std::exception& e) {
+    set_err(e.what());
+    return -1;
+  }
+}
+int oracle_eth_gym_obs_fields(void* g, int32_t out[10]) {
+  double tmp[10];
+  EthObs o = ((GymEthereum*)g)->observe_int();
+  eth_obs_to_floats(o, false, tmp);
+  for (int i = 0; i < 10; i++) out[i] = (int32_t)tmp[i];
+  return 0;
+}
+// info_out: 12 doubles in engine.ml:226-237 order + head_height + head_miner + head_work
+int oracle_eth_gym_step(void* g, int action, double obs[10], double* reward, int* done,
+                        double info_out[15]) {
+  try {
+    bool d = false;
+    StepInfo i;
+    *reward = ((GymEthereum*)g)->step(action, obs, &d, &i);
+    *done = d ? 1 : 0;
+    if (info_out) {
+      double v[15] = {i.step_reward_attacker,    i.step_reward_defender,
+                      i.step_progress,           i.step_chain_time,
+                      i.step_sim_time,           i.episode_reward_attacker,
+                      i.episode_reward_defender, i.episode_progress,
+                      i.episode_chain_time,      i.episode_sim_time,
+                      (double)i.episode_n_steps, (double)i.episode_n_activations,
+                      (double)i.head_height,     (double)i.head_miner,
+                      (double)i.head_work};
+      memcpy(info_out, v, sizeof(v));
+    }
+    return 0;
+  } catch (std::exception& e) {
+    set_err(e.what());
+    return -1;
+  }
+}
+uint32_t oracle_eth_gym_diag(void* g) { return ((GymEthereum*)g)->sim->diag; }
+
+int oracle_eth_two_agents_task(int rng_mode, void* rng, uint64_t seed, uint64_t episode,
+                               double alpha, int scheme, int policy, int activations,
+                               int64_t acts_out[2], double rewards_out[2], double* head_time,
+                               double* head_progress, int32_t* head_height,
+                               int32_t* head_work, uint32_t* diag) {
+  try {
+    EthLoopResult r;
+    eth_two_agents_task(rng_mode, (OcamlRandom*)rng, seed, episode, alpha, scheme, policy,
+                        activations, &r);
+    for (int i = 0; i < 2; i++) {
+      acts_out[i] = r.activations[i];
+      rewards_out[i] = r.rewards[i];
+    }
+    *head_time = r.head_time;
+    *head_progress = r.head_progress;
+    *head_height = r.head_height;
+    *head_work = r.head_work;
+    if (diag) *diag = r.diag;
+    return 0;
+  } catch (std::exception& e) {
+    set_err(e.what());
+    return -1;
+  }
+}
+
 // ---------------- batch of full episodes (keyed stream), the CPU baseline workload
+static int run_eth_gym_episode(const cpr_config* c, uint64_t ep, cpr_episode_record* rec) {
+  GymEthereum g(params_of(c), c->reward_scheme, 1, nullptr, c->seed, ep);
+  double obs[10];
+  g.reset(obs);
+  bool done = false;
+  StepInfo info{};
+  while (!done) {
+    int a = eth_policy(c->policy, g.observe_int());
+    g.step(a, obs, &done, &info);
+  }
+  rec->reward_attacker = info.episode_reward_attacker;
+  rec->reward_defender = info.episode_reward_defender;
+  rec->progress = info.episode_progress;
+  rec->chain_time = info.episode_chain_time;
+  rec->sim_time = info.episode_sim_time;
+  rec->n_steps = info.episode_n_steps;
+  rec->n_activations = info.episode_n_activations;
+  rec->head_height = info.head_height;
+  rec->head_miner = info.head_miner;
+  rec->status = ((g.sim->diag & DIAG_TIE) ? (uint32_t)CPR_ST_TIE : 0u) |
+                ((g.sim->diag & DIAG_OVERLAP) ? (uint32_t)CPR_ST_OVERLAP : 0u);
+  rec->head_work = info.head_work;
+  return 0;
+}
+
 static int run_gym_episode(const cpr_config* c, const TablePolicy* tab, uint64_t ep,
                            cpr_episode_record* rec) {
+  if (c->protocol == CPR_PROTO_ETHEREUM) return run_eth_gym_episode(c, ep, rec);
   GymNakamoto g(params_of(c), 1, nullptr, c->seed, ep);
   double obs[4];
   g.reset(obs);
@@ -200,7 +385,7 @@ static int run_gym_episode(const cpr_config* c, const TablePolicy* tab, uint64_t
   rec->head_miner = info.head_miner;
   rec->status = ((g.sim->diag & DIAG_TIE) ? (uint32_t)CPR_ST_TIE : 0u) |
                 ((g.sim->diag & DIAG_OVERLAP) ? (uint32_t)CPR_ST_OVERLAP : 0u);
-  rec->_pad = 0;
+  rec->head_work = 0;
   return 0;
 }
 
@@ -212,6 +397,25 @@ static int run_loop_episode(const cpr_config* c, uint64_t ep, cpr_episode_record
   if (c->network != CPR_NET_TWO_AGENTS) {
     set_err("oracle loop mode: two-agents network only");
     return -2;
+  }
+  if (c->protocol == CPR_PROTO_ETHEREUM) {
+    int32_t hw = 0;
+    if (oracle_eth_two_agents_task(1, nullptr, c->seed, ep, c->alpha, c->reward_scheme,
+                                   c->policy, (int)c->activations, acts, rew, &ht, &hp, &hh,
+                                   &hw, &diag) != 0)
+      return -1;
+    rec->reward_attacker = rew[0];
+    rec->reward_defender = rew[1];
+    rec->progress = hp;
+    rec->chain_time = ht;
+    rec->sim_time = 0.0;
+    rec->n_steps = 0;
+    rec->n_activations = acts[0] + acts[1];
+    rec->head_height = hh;
+    rec->head_miner = -1;
+    rec->status = 0;
+    rec->head_work = hw;
+    return 0;
   }
   if (oracle_two_agents_task(1, nullptr, c->seed, ep, c->alpha, c->policy,
                              (int)c->activations, acts, rew, &ht, &hp, &hh, &diag) != 0)
@@ -226,7 +430,7 @@ static int run_loop_episode(const cpr_config* c, uint64_t ep, cpr_episode_record
   rec->head_height = hh;
   rec->head_miner = -1;
   rec->status = 0;
-  rec->_pad = 0;
+  rec->head_work = 0;
   return 0;
 }
 

@@ -67,6 +67,30 @@ def lib():
         L.oracle_gym_diag.restype = ctypes.c_uint32
         L.oracle_run_episodes.argtypes = [P(C.Config), ctypes.c_uint64, ctypes.c_int64, vp,
                                           ctypes.c_int]
+        L.oracle_ocaml_sort_ints.argtypes = [vp, ctypes.c_int]
+        L.oracle_ocaml_sort_pairs.argtypes = [vp, vp, ctypes.c_int]
+        L.oracle_at_most_first_ints.argtypes = [vp, ctypes.c_int, ctypes.c_int]
+        L.oracle_eth_dag_new.restype = vp
+        L.oracle_eth_dag_new.argtypes = [ctypes.c_int, ctypes.c_int]
+        L.oracle_eth_dag_free.argtypes = [vp]
+        L.oracle_eth_dag_mine.argtypes = [vp, ctypes.c_int, vp, ctypes.c_int, P(ctypes.c_int32)]
+        L.oracle_eth_policy.argtypes = [ctypes.c_int, vp]
+        L.oracle_eth_obs_to_floats.argtypes = [vp, ctypes.c_int, vp]
+        L.oracle_eth_obs_of_floats.argtypes = [vp, ctypes.c_int, vp]
+        L.oracle_eth_gym_new.restype = vp
+        L.oracle_eth_gym_new.argtypes = [P(C.Config), ctypes.c_int, vp, ctypes.c_uint64]
+        L.oracle_eth_gym_free.argtypes = [vp]
+        L.oracle_eth_gym_reset.argtypes = [vp, vp]
+        L.oracle_eth_gym_obs_fields.argtypes = [vp, vp]
+        L.oracle_eth_gym_step.argtypes = [vp, ctypes.c_int, vp, P(ctypes.c_double),
+                                          P(ctypes.c_int), vp]
+        L.oracle_eth_gym_diag.argtypes = [vp]
+        L.oracle_eth_gym_diag.restype = ctypes.c_uint32
+        L.oracle_eth_two_agents_task.argtypes = [
+            ctypes.c_int, vp, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_double, ctypes.c_int,
+            ctypes.c_int, ctypes.c_int, vp, vp, P(ctypes.c_double), P(ctypes.c_double),
+            P(ctypes.c_int32), P(ctypes.c_int32), P(ctypes.c_uint32),
+        ]
         _lib = L
     return _lib
 
@@ -214,3 +238,134 @@ def run_episodes(config, first, n, threads=1):
     rec = np.zeros(n, dtype=C.RECORD_DTYPE)
     check(lib().oracle_run_episodes(ctypes.byref(config), first, n, rec.ctypes.data, threads))
     return rec
+
+
+# ---------------------------------------------------------------- OCaml Array.sort
+
+
+def ocaml_sort(xs):
+    a = np.ascontiguousarray(xs, dtype=np.int32).copy()
+    lib().oracle_ocaml_sort_ints(a.ctypes.data, a.size)
+    return a.tolist()
+
+
+def ocaml_sort_pairs(keys, tags):
+    k = np.ascontiguousarray(keys, dtype=np.int32).copy()
+    t = np.ascontiguousarray(tags, dtype=np.int32).copy()
+    lib().oracle_ocaml_sort_pairs(k.ctypes.data, t.ctypes.data, k.size)
+    return list(zip(k.tolist(), t.tolist()))
+
+
+def at_most_first(xs, n):
+    a = np.ascontiguousarray(xs, dtype=np.int32).copy()
+    m = lib().oracle_at_most_first_ints(a.ctypes.data, a.size, n)
+    return a[:m].tolist()
+
+
+# ---------------------------------------------------------------- Ethereum
+
+ETH_POLICIES = {"honest": 0, "selfish_release": 1, "selfish_discard": 2, "fn19": 3,
+                "fn19pkel": 4}
+ETH_OBS_FIELDS = ["public_height", "public_work", "private_height", "private_work",
+                  "diff_height", "diff_work", "public_orphans", "private_orphans_inclusive",
+                  "private_orphans_exclusive", "event"]
+
+
+class EthDag:
+    """Hand-built Ethereum DAG for the validity KATs (ethereum_test.ml:44-77)."""
+
+    def __init__(self, height, work):
+        self.h = lib().oracle_eth_dag_new(height, work)
+        self.root = 0
+
+    def __del__(self):
+        try:
+            lib().oracle_eth_dag_free(self.h)
+        except Exception:
+            pass
+
+    def mine(self, parent, uncles=()):
+        u = np.ascontiguousarray(list(uncles) or [0], dtype=np.int32)
+        out = ctypes.c_int32()
+        ok = lib().oracle_eth_dag_mine(self.h, parent, u.ctypes.data, len(uncles),
+                                       ctypes.byref(out))
+        return out.value, bool(ok)
+
+
+def eth_policy(policy, fields):
+    o = np.ascontiguousarray(fields, dtype=np.int32)
+    return lib().oracle_eth_policy(ETH_POLICIES.get(policy, policy), o.ctypes.data)
+
+
+def eth_obs_to_floats(fields, unit):
+    o = np.ascontiguousarray(fields, dtype=np.int32)
+    out = np.zeros(10)
+    lib().oracle_eth_obs_to_floats(o.ctypes.data, 1 if unit else 0, out.ctypes.data)
+    return out
+
+
+def eth_obs_of_floats(floats, unit):
+    f = np.ascontiguousarray(floats, dtype=np.float64)
+    out = np.zeros(10, dtype=np.int32)
+    lib().oracle_eth_obs_of_floats(f.ctypes.data, 1 if unit else 0, out.ctypes.data)
+    return out
+
+
+class EthGymEnv:
+    """The oracle's engine.ml restatement for the ethereum_ssz attack space."""
+
+    INFO_KEYS = GymEnv.INFO_KEYS + ["head_work"]
+
+    def __init__(self, config, episode=0, ocaml_rng=None):
+        self.cfg = config
+        self.h = lib().oracle_eth_gym_new(ctypes.byref(config), 0 if ocaml_rng else 1,
+                                          ocaml_rng.h if ocaml_rng else None, episode)
+        if not self.h:
+            raise ValueError(lib().oracle_last_error().decode())
+
+    def __del__(self):
+        try:
+            lib().oracle_eth_gym_free(self.h)
+        except Exception:
+            pass
+
+    def reset(self):
+        obs = np.zeros(10)
+        check(lib().oracle_eth_gym_reset(self.h, obs.ctypes.data))
+        return obs
+
+    def fields(self):
+        f = np.zeros(10, dtype=np.int32)
+        lib().oracle_eth_gym_obs_fields(self.h, f.ctypes.data)
+        return f
+
+    def step(self, action):
+        obs = np.zeros(10)
+        r = ctypes.c_double()
+        d = ctypes.c_int()
+        info = np.zeros(15)
+        check(lib().oracle_eth_gym_step(self.h, int(action), obs.ctypes.data, ctypes.byref(r),
+                                        ctypes.byref(d), info.ctypes.data))
+        return obs, r.value, bool(d.value), dict(zip(self.INFO_KEYS, info.tolist()))
+
+    def diag(self):
+        return lib().oracle_eth_gym_diag(self.h)
+
+
+def eth_two_agents_task(alpha, policy, activations, scheme=1, rng=None, seed=0, episode=0):
+    acts = np.zeros(2, dtype=np.int64)
+    rew = np.zeros(2, dtype=np.float64)
+    ht, hp = ctypes.c_double(), ctypes.c_double()
+    hh, hw, dg = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_uint32()
+    mode = 0 if rng is not None else 1
+    check(
+        lib().oracle_eth_two_agents_task(
+            mode, rng.h if rng is not None else None, seed, episode, alpha, scheme,
+            ETH_POLICIES.get(policy, policy), activations, acts.ctypes.data, rew.ctypes.data,
+            ctypes.byref(ht), ctypes.byref(hp), ctypes.byref(hh), ctypes.byref(hw),
+            ctypes.byref(dg),
+        )
+    )
+    return dict(activations=acts.tolist(), reward=rew.tolist(), head_time=ht.value,
+                head_progress=hp.value, head_height=hh.value, head_work=hw.value,
+                diag=dg.value)
