@@ -62,6 +62,9 @@ struct cpr_batch {
   cpr_ctx* ctx;
   cpr_config cfg;
   NakParams P;
+  eth::EthParams EP;     // CPR_PROTO_ETHEREUM
+  DevBuf eth_mem;        // lanes x eth_lane_bytes
+  int64_t eth_bytes = 0;
   std::vector<uint8_t> table_host;
   DevBuf table_dev, tabs_dev;  // policy table; unit-observation tables
   DevBuf spill, tlog, replay, summary, records;
@@ -137,7 +140,10 @@ static int32_t pow2_at_least(int64_t x, int32_t cap) {
 }
 
 // engine.ml:37-51 and network.ml:343-358 (messages kept verbatim)
-static int validate(const cpr_config* c, NakParams* P) {
+static int validate_eth(const cpr_config* c, eth::EthParams* P);
+
+static int validate(const cpr_config* c, NakParams* P, eth::EthParams* EP) {
+  if (c->protocol == CPR_PROTO_ETHEREUM) return validate_eth(c, EP);
   if (c->protocol != CPR_PROTO_NAKAMOTO)
     return fail(CPR_E_UNSUPPORTED, "protocol not implemented on the device yet");
   if (std::isnan(c->activation_delay)) return fail(CPR_E_INVALID_ARG, "activation_delay cannot be NaN");
@@ -207,16 +213,89 @@ static int validate(const cpr_config* c, NakParams* P) {
   return CPR_OK;
 }
 
+// Ethereum: engine.ml:37-51 checks shared with Nakamoto, network.ml:343-358, ethereum_ssz
+// policies 0..4, Constant / Discount rewards
+static int validate_eth(const cpr_config* c, eth::EthParams* P) {
+  if (std::isnan(c->activation_delay)) return fail(CPR_E_INVALID_ARG, "activation_delay cannot be NaN");
+  if (std::isnan(c->alpha)) return fail(CPR_E_INVALID_ARG, "alpha cannot be NaN");
+  if (std::isnan(c->gamma)) return fail(CPR_E_INVALID_ARG, "gamma cannot be NaN");
+  if (c->alpha < 0. || c->alpha > 1.) return fail(CPR_E_INVALID_ARG, "alpha < 0 || alpha > 1");
+  if (c->gamma < 0. || c->gamma > 1.) return fail(CPR_E_INVALID_ARG, "gamma < 0 || gamma > 1");
+  if (c->activation_delay <= 0.) return fail(CPR_E_INVALID_ARG, "activation_delay <= 0");
+  if (c->mode != CPR_MODE_GYM && c->mode != CPR_MODE_LOOP)
+    return fail(CPR_E_INVALID_ARG, "unknown mode");
+  if (c->policy < CPR_ETH_POLICY_HONEST || c->policy > CPR_ETH_POLICY_FN19PKEL)
+    return fail(CPR_E_INVALID_ARG, "unknown policy");
+  if (c->reward_scheme != CPR_REWARD_CONSTANT && c->reward_scheme != CPR_REWARD_DISCOUNT)
+    return fail(CPR_E_INVALID_ARG, "unknown incentive scheme");
+  memset(P, 0, sizeof(*P));
+  P->ev = c->activation_delay;
+  P->t_att = alpha_threshold(c->alpha);
+  P->policy = c->policy;
+  P->scheme = c->reward_scheme;
+  P->mode = c->mode;
+  if (c->network == CPR_NET_SELFISH_MINING) {
+    if (c->defenders < 1) return fail(CPR_E_INVALID_ARG, "defenders < 0");
+    if (c->defenders < 2) return fail(CPR_E_INVALID_ARG, "defenders must be at least 2");
+    if (c->defenders > 64)
+      return fail(CPR_E_UNSUPPORTED, "device lanes support at most 64 defenders");
+    const double dd = (double)c->defenders;
+    if (c->gamma > (dd - 1.) / dd)
+      return fail(CPR_E_INVALID_ARG, "gamma must not be greater ( (defenders - 1) / defenders )");
+    const double prop = c->propagation_delay > 0 ? c->propagation_delay : 1e-9;
+    P->d = c->defenders;
+    P->net = 0;
+    P->delta = prop;
+    P->dmax = (dd - 1.) / dd * prop / c->gamma;
+  } else if (c->network == CPR_NET_TWO_AGENTS) {
+    if (c->mode == CPR_MODE_GYM)
+      return fail(CPR_E_UNSUPPORTED, "the gym engine always uses the selfish-mining network");
+    P->d = 1;
+    P->net = 1;
+  } else {
+    return fail(CPR_E_INVALID_ARG, "unknown network");
+  }
+  P->n = P->d + 1;
+  int64_t span;
+  if (c->mode == CPR_MODE_GYM) {
+    const int64_t ms = c->max_steps > 0 ? c->max_steps : INT64_MAX;
+    P->max_steps = ms;
+    P->max_progress = c->max_progress > 0 ? c->max_progress : __builtin_inf();
+    P->max_time = c->max_time > 0 ? c->max_time : __builtin_inf();
+    span = ms < (1 << 20) ? ms + 2 : 4096;
+  } else {
+    if (c->activations <= 0) return fail(CPR_E_INVALID_ARG, "activations <= 0");
+    if (c->activations > (1 << 24)) return fail(CPR_E_UNSUPPORTED, "activations > 2^24");
+    P->max_steps = INT64_MAX;
+    P->activations = c->activations;
+    P->max_progress = __builtin_inf();
+    P->max_time = __builtin_inf();
+    span = c->activations + 2;
+  }
+  // the block ring holds a whole episode up to 2^15 blocks (longer episodes flag
+  // CPR_ST_CAPACITY only if a fork outlives the ring); heap: 512 in-flight events per node
+  int32_t cb = 64;
+  while (cb < span && cb < (1 << 15)) cb <<= 1;
+  P->cap_b = cb;
+  P->cap_e = 64 + 512 * P->n;
+  return CPR_OK;
+}
+
 int cpr_batch_create(cpr_ctx* ctx, const cpr_config* cfg, cpr_batch** out) {
   if (!ctx || !cfg || !out) return fail(CPR_E_INVALID_ARG, "NULL argument");
   NakParams P;
-  int rc = validate(cfg, &P);
+  eth::EthParams EP;
+  memset(&P, 0, sizeof(P));
+  memset(&EP, 0, sizeof(EP));
+  int rc = validate(cfg, &P, &EP);
   if (rc) return rc;
   HIP_TRY(hipSetDevice(ctx->device));
   cpr_batch* b = new cpr_batch;
   b->ctx = ctx;
   b->cfg = *cfg;
   b->P = P;
+  b->EP = EP;
+  b->eth_bytes = eth::eth_lane_bytes(EP.cap_b, EP.cap_e, EP.n);
   b->cfg.policy_table = nullptr;
   if (cfg->policy == CPR_POLICY_TABLE) {
     const size_t nb = (size_t)cfg->policy_table_dim * cfg->policy_table_dim * 2;
@@ -258,6 +337,7 @@ int cpr_batch_destroy(cpr_batch* b) {
   (void)hipStreamSynchronize(b->ctx->stream);
   if (b->ev0) (void)hipEventDestroy(b->ev0);
   if (b->ev1) (void)hipEventDestroy(b->ev1);
+  b->eth_mem.release();
   for (DevBuf* d : {&b->table_dev, &b->tabs_dev, &b->spill, &b->tlog, &b->replay, &b->summary,
                     &b->records, &b->lanes, &b->lring, &b->lspill, &b->ltlog, &b->lreplay,
                     &b->l_obs, &b->l_act, &b->l_rew, &b->l_done, &b->l_mask, &b->l_eps,
@@ -278,8 +358,29 @@ static int64_t episode_lanes(cpr_batch* b, int64_t n_eps) {
   return std::max<int64_t>(256, (lanes / 256) * 256);
 }
 
+// Ethereum lanes: resident capacity bounded by a 32 GiB budget for the per-lane regions
+static int run_async_eth(cpr_batch* b, int64_t n, uint64_t first, cpr_summary* sum_dev,
+                         cpr_episode_record* rec_dev) {
+  const int64_t full = (int64_t)b->ctx->cus * eth_blocks_per_cu() * 256;
+  const int64_t budget = (int64_t)(32ll << 30) / b->eth_bytes;
+  int64_t lanes = std::min(full, std::max<int64_t>(256, budget));
+  lanes = std::min(lanes, ((n + 255) / 256) * 256);
+  lanes = std::max<int64_t>(256, (lanes / 256) * 256);
+  HIP_TRY(b->eth_mem.ensure((size_t)lanes * (size_t)b->eth_bytes));
+  if (!b->ev0) {
+    HIP_TRY(hipEventCreate(&b->ev0));
+    HIP_TRY(hipEventCreate(&b->ev1));
+  }
+  HIP_TRY(hipEventRecord(b->ev0, b->ctx->stream));
+  HIP_TRY(launch_eth_run_episodes(b->EP, b->cfg.seed, first, n, (uint8_t*)b->eth_mem.p,
+                                  b->eth_bytes, lanes, rec_dev, sum_dev, b->ctx->stream));
+  HIP_TRY(hipEventRecord(b->ev1, b->ctx->stream));
+  return CPR_OK;
+}
+
 static int run_async(cpr_batch* b, int64_t n, uint64_t first, cpr_summary* sum_dev,
                      cpr_episode_record* rec_dev) {
+  if (b->cfg.protocol == CPR_PROTO_ETHEREUM) return run_async_eth(b, n, first, sum_dev, rec_dev);
   const int64_t lanes = episode_lanes(b, n);
   if (lanes > b->lanes_alloc) {
     HIP_TRY(b->spill.ensure((size_t)lanes * b->P.cap * sizeof(int32_t)));
@@ -355,6 +456,8 @@ int cpr_run_episodes(cpr_batch* b, int64_t n, uint64_t first, cpr_summary* summa
 // ---------------------------------------------------------------- lockstep API
 
 static int ensure_lockstep(cpr_batch* b) {
+  if (b->cfg.protocol != CPR_PROTO_NAKAMOTO)
+    return fail(CPR_E_UNSUPPORTED, "lockstep lanes are implemented for Nakamoto only");
   const int64_t n = b->cfg.n_lanes;
   if (n <= 0) return fail(CPR_E_STATE, "batch has no lockstep lanes (cfg.n_lanes = 0)");
   if (b->cfg.mode != CPR_MODE_GYM) return fail(CPR_E_STATE, "lockstep lanes need CPR_MODE_GYM");
@@ -464,6 +567,8 @@ int cpr_step(cpr_batch* b, const int32_t* actions, double* obs, double* reward, 
 
 int cpr_observe_fields(cpr_batch* b, int32_t* fields) {
   if (!b || !fields) return fail(CPR_E_INVALID_ARG, "NULL argument");
+  if (b->cfg.protocol != CPR_PROTO_NAKAMOTO)
+    return fail(CPR_E_UNSUPPORTED, "lockstep lanes are implemented for Nakamoto only");
   if (!b->reset_done) return fail(CPR_E_STATE, "observe before reset");
   const int64_t n = b->cfg.n_lanes;
   HIP_TRY(hipSetDevice(b->ctx->device));
@@ -480,6 +585,8 @@ int cpr_observe_fields(cpr_batch* b, int32_t* fields) {
 int cpr_policy_actions(cpr_batch* b, int32_t policy, const double* obs, int64_t n,
                        int32_t* actions) {
   if (!b || !obs || !actions) return fail(CPR_E_INVALID_ARG, "NULL argument");
+  if (b->cfg.protocol != CPR_PROTO_NAKAMOTO)
+    return fail(CPR_E_UNSUPPORTED, "policy evaluation on encoded observations: Nakamoto only");
   if (policy < 0 || policy > CPR_POLICY_TABLE) return fail(CPR_E_INVALID_ARG, "unknown policy");
   if (policy == CPR_POLICY_TABLE && b->table_host.empty())
     return fail(CPR_E_INVALID_ARG, "batch has no policy table");
@@ -504,9 +611,25 @@ int cpr_policy_actions(cpr_batch* b, int32_t policy, const double* obs, int64_t 
 int cpr_observation_spec(cpr_batch* b, int32_t* obs_len, int32_t* n_actions, double* low,
                          double* high) {
   if (!b) return fail(CPR_E_INVALID_ARG, "NULL argument");
+  const double inf = __builtin_inf();
+  if (b->cfg.protocol == CPR_PROTO_ETHEREUM) {
+    // ethereum_ssz.ml:47-80: 10 fields (diff_* signed, event discrete), 24 actions
+    if (obs_len) *obs_len = 10;
+    if (n_actions) *n_actions = 24;
+    for (int i = 0; i < 10; i++) {
+      const bool sgn = i == 4 || i == 5;
+      double lo = 0.0, hi = 1.0;
+      if (!b->cfg.unit_observation && i != 9) {
+        lo = sgn ? -inf : 0.0;
+        hi = inf;
+      }
+      if (low) low[i] = lo;
+      if (high) high[i] = hi;
+    }
+    return CPR_OK;
+  }
   if (obs_len) *obs_len = 4;
   if (n_actions) *n_actions = 4;
-  const double inf = __builtin_inf();
   if (b->cfg.unit_observation) {
     for (int i = 0; i < 4; i++) {
       if (low) low[i] = 0.0;
@@ -528,12 +651,25 @@ static const char* kNames[4] = {"sapirshtein-2016-sm1", "eyal-sirer-2014", "simp
 static const int32_t kIds[4] = {CPR_POLICY_SAPIRSHTEIN_2016_SM1, CPR_POLICY_EYAL_SIRER_2014,
                                 CPR_POLICY_SIMPLE, CPR_POLICY_HONEST};
 
-int cpr_policy_count(int32_t protocol) { return protocol == CPR_PROTO_NAKAMOTO ? 4 : 0; }
+// ethereum_ssz.ml:523-538, same reversal
+static const char* kEthNames[5] = {"fn19pkel", "fn19", "selfish_discard", "selfish_release",
+                                   "honest"};
+static const int32_t kEthIds[5] = {CPR_ETH_POLICY_FN19PKEL, CPR_ETH_POLICY_FN19,
+                                   CPR_ETH_POLICY_SELFISH_DISCARD,
+                                   CPR_ETH_POLICY_SELFISH_RELEASE, CPR_ETH_POLICY_HONEST};
+
+int cpr_policy_count(int32_t protocol) {
+  return protocol == CPR_PROTO_NAKAMOTO ? 4 : (protocol == CPR_PROTO_ETHEREUM ? 5 : 0);
+}
 
 const char* cpr_policy_name(int32_t protocol, int32_t index, int32_t* policy_id) {
-  if (protocol != CPR_PROTO_NAKAMOTO || index < 0 || index >= 4) {
+  if (index < 0 || index >= cpr_policy_count(protocol)) {
     g_err = "no such policy";
     return nullptr;
+  }
+  if (protocol == CPR_PROTO_ETHEREUM) {
+    if (policy_id) *policy_id = kEthIds[index];
+    return kEthNames[index];
   }
   if (policy_id) *policy_id = kIds[index];
   return kNames[index];

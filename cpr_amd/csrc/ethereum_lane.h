@@ -1,0 +1,886 @@
+// Ethereum (Byzantium + Constant/Discount rewards) with the ethereum_ssz attack space:
+// one episode per lane, as an exact per-lane discrete-event engine.
+//
+// Why an event engine here (and closed-form windows for Nakamoto): Ethereum's fork choice
+// reads far more of the DAG than heights — uncle candidates are the visible children of
+// the last six ancestors of each node's tip (ethereum.ml:234-277), the attacker's common
+// ancestor walks uncle edges (dagtools.ml:102-121) and its observation runs three dry-run
+// uncle selections (ethereum_ssz.ml:364-396). Replaying the reference's event semantics
+// per lane keeps every one of those reads exact, including same-instant ties, whose order
+// the skew heap decides (orderedQueue.ml:17-47).
+//
+// Per-lane memory (one contiguous region per resident lane):
+//   blocks  [cap_b] x 64 B   ring indexed by serial & (cap_b-1); a stale slot (serial
+//                            mismatch) marks the episode CPR_ST_CAPACITY
+//   vis     [cap_b][n] u8    per node: kind (invisible/received/released/withheld) + got bit
+//   heap    [cap_e] x 24 B   skew-heap nodes of the event queue (time, event, block)
+//   tips    [n] i32          defenders' preferred blocks (Honest.state)
+//   scratch 192 i32          candidate lists, ancestor frontiers, share stack
+//
+// Reference map: simulator.ml:122-543 (engine), ethereum.ml:89-297 (referee, honest node),
+// ethereum_ssz.ml:279-521 (agent, policies), engine.ml:97-249 (gym step), network.ml
+// selfish_mining / two_agents (links), distributions.ml (re-specified keyed stream).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "cpr_stream.h"
+
+#pragma clang fp contract(off)
+
+namespace cpr {
+namespace eth {
+
+constexpr uint32_t EST_CAPACITY = 32u;  // CPR_ST_CAPACITY
+
+enum : uint32_t { EV_CLOCK = 0, EV_DAG = 1, EV_TX = 2, EV_RX = 3, EV_ON = 4, EV_MV = 5, EV_MDV = 6 };
+enum : uint32_t { KD_POW = 1, KD_NET = 2 };
+enum : uint8_t { V_INV = 0, V_RECV = 1, V_REL = 2, V_WH = 3, V_KIND = 3, V_GOT = 4 };
+
+__host__ __device__ inline uint32_t mkev(uint32_t ty, uint32_t node, uint32_t kind) {
+  return ty | (kind << 3) | (node << 5);
+}
+
+struct EBlock {
+  int32_t serial;
+  int32_t p[3];  // parent serials; p[0] = parent, p[1..] = uncles
+  int32_t np;
+  int32_t height, work;
+  int32_t miner;             // -1 = genesis
+  int32_t rew_att, rew_def;  // cumulative rewards of the first-parent chain, units of 1/32
+  int32_t share_k, share_off;
+  double time;  // Simulator.timestamp = append time (the miner sees it first)
+  int32_t _pad[2];
+};
+static_assert(sizeof(EBlock) == 64, "EBlock layout");
+
+struct HNode {
+  double t;
+  uint32_t ev;
+  int32_t blk;
+  int32_t l, r;
+};
+static_assert(sizeof(HNode) == 24, "HNode layout");
+
+struct EthParams {
+  uint64_t t_att;
+  int32_t d, n;  // defenders, nodes
+  int32_t net;   // 0 selfish mining, 1 two agents
+  int32_t mode;  // 0 gym, 1 loop
+  int32_t policy, scheme;
+  int32_t cap_b, cap_e;
+  double ev, delta, dmax;
+  int64_t max_steps, activations;
+  double max_progress, max_time;
+};
+
+constexpr int32_t NCAND = 32, NQ = 32, NSTACK = 64;
+constexpr int32_t SCR_CAND = 0, SCR_KEY = 32, SCR_QA = 64, SCR_QB = 96, SCR_STACK = 128;
+constexpr int32_t SCR_INTS = 192;
+
+struct EthMem {
+  EBlock* blk;
+  uint8_t* vis;
+  HNode* heap;
+  int32_t* tips;
+  int32_t* scr;
+};
+
+__host__ __device__ inline int64_t align128(int64_t x) { return (x + 127) / 128 * 128; }
+
+__host__ __device__ inline int64_t eth_lane_bytes(int32_t cap_b, int32_t cap_e, int32_t n) {
+  return align128((int64_t)cap_b * 64) + align128((int64_t)cap_b * n) +
+         align128((int64_t)cap_e * 24) + align128((int64_t)n * 4) + align128(SCR_INTS * 4);
+}
+
+__host__ __device__ inline EthMem eth_mem_at(uint8_t* base, int32_t cap_b, int32_t cap_e,
+                                             int32_t n) {
+  EthMem M;
+  int64_t o = 0;
+  M.blk = (EBlock*)(base + o);
+  o += align128((int64_t)cap_b * 64);
+  M.vis = base + o;
+  o += align128((int64_t)cap_b * n);
+  M.heap = (HNode*)(base + o);
+  o += align128((int64_t)cap_e * 24);
+  M.tips = (int32_t*)(base + o);
+  o += align128((int64_t)n * 4);
+  M.scr = (int32_t*)(base + o);
+  return M;
+}
+
+// ---- policies (ethereum_ssz.ml:444-521); action = rank * 4 + own * 2 + foreign
+enum : int32_t { A_ADOPT_DISCARD = 0, A_ADOPT_RELEASE = 1, A_OVERRIDE = 2, A_MATCH = 3,
+                 A_RELEASE1 = 4, A_WAIT = 5 };
+
+struct EthObs {
+  int32_t public_height, public_work, private_height, private_work, diff_height, diff_work,
+      public_orphans, private_orphans_inclusive, private_orphans_exclusive, event;
+};
+
+__host__ __device__ inline int32_t eth_policy(int32_t policy, const EthObs& o) {
+  switch (policy) {
+    case 0:  // honest
+      return (o.public_work > 0 ? A_ADOPT_RELEASE : A_OVERRIDE) * 4 + 3;
+    case 1:    // selfish_release
+    case 2: {  // selfish_discard; Byzantium preference `HeaviestChain` -> work
+      const int32_t pp = o.private_work, qp = o.public_work;
+      int32_t a;
+      if (pp < qp)
+        a = policy == 1 ? A_ADOPT_RELEASE : A_ADOPT_DISCARD;
+      else if (qp == 0)
+        a = A_WAIT;
+      else
+        a = A_OVERRIDE;
+      return a * 4 + 2;
+    }
+    default: {  // 3 fn19, 4 fn19pkel
+      const int32_t ph = o.private_height, qh = o.public_height;
+      int32_t a;
+      if (o.event == 0)
+        a = (ph == 2 && qh == 1) ? A_OVERRIDE : A_WAIT;
+      else if (ph < qh)
+        a = policy == 4 ? A_ADOPT_RELEASE : A_ADOPT_DISCARD;
+      else if (ph == qh)
+        a = A_MATCH;
+      else if (ph == qh + 1)
+        a = A_OVERRIDE;
+      else
+        a = A_RELEASE1;
+      return a * 4 + (policy == 4 ? 2 : 3);
+    }
+  }
+}
+
+// uncle filters of Honest.puzzle_payload' callers
+enum : int32_t { F_ALL = 0, F_MINING = 1, F_PUBLIC = 2 };
+
+struct Payload {
+  int32_t p[3];
+  int32_t np;
+  int32_t height, work;
+};
+
+struct EthLane {
+  double now;
+  int32_t c_act, newest;
+  int32_t act0;  // attacker activations
+  int32_t hroot, hfree, hused;
+  uint32_t status;
+  int32_t dead;  // capacity exceeded: 1 block ring, 2 event heap, 3 candidates, 4 frontier, 5 stack
+                 // 6 queue drained
+  // the one outstanding draft (clock -> Dag at the same instant)
+  Payload dr;
+  int32_t dr_node;
+  // ethereum_ssz agent (BetweenActions + Observable)
+  int32_t pub, priv, pending, own, foreign;
+  int32_t o_pub, o_priv, o_common, o_event;
+  int64_t steps;
+
+  // ------------------------------------------------------------------ storage
+  __host__ __device__ inline void fail(int32_t why) {
+    status |= EST_CAPACITY;
+    if (!dead) dead = why;
+  }
+  __host__ __device__ inline EBlock& B(const EthParams& P, const EthMem& M, int32_t s) {
+    EBlock& b = M.blk[s & (P.cap_b - 1)];
+    if (b.serial != s) fail(1);
+    return b;
+  }
+  __host__ __device__ inline uint8_t& V(const EthParams& P, const EthMem& M, int32_t s,
+                                        int32_t node) {
+    return M.vis[(int64_t)(s & (P.cap_b - 1)) * P.n + node];
+  }
+  __host__ __device__ inline bool visible(const EthParams& P, const EthMem& M, int32_t s,
+                                          int32_t node) {
+    return (V(P, M, s, node) & V_KIND) != V_INV;
+  }
+
+  // ------------------------------------------------------------------ event queue
+  // orderedQueue.ml:17-47 as an in-place skew heap (equal times: the earlier insertion
+  // pops first). Events at +inf (messages that never arrive, gamma = 0) are not stored.
+  __host__ __device__ inline int32_t halloc(const EthParams& P, const EthMem& M) {
+    int32_t i;
+    if (hfree >= 0) {
+      i = hfree;
+      hfree = M.heap[i].l;
+    } else if (hused < P.cap_e) {
+      i = hused++;
+    } else {
+      fail(2);
+      return -1;
+    }
+    return i;
+  }
+  __host__ __device__ inline void push(const EthParams& P, const EthMem& M, double t,
+                                       uint32_t ev, int32_t blk) {
+    if (!(t < __builtin_inf())) return;
+    int32_t parent = -1, node = hroot;
+    for (;;) {
+      if (node < 0) {
+        const int32_t a = halloc(P, M);
+        if (a < 0) return;
+        HNode& h = M.heap[a];
+        h.t = t;
+        h.ev = ev;
+        h.blk = blk;
+        h.l = -1;
+        h.r = -1;
+        if (parent < 0)
+          hroot = a;
+        else
+          M.heap[parent].l = a;
+        return;
+      }
+      HNode& h = M.heap[node];
+      if (t < h.t) {
+        const double ot = h.t;
+        const uint32_t oe = h.ev;
+        const int32_t ob = h.blk;
+        h.t = t;
+        h.ev = ev;
+        h.blk = blk;
+        t = ot;
+        ev = oe;
+        blk = ob;
+      } else {
+        const int32_t tmp = h.l;
+        h.l = h.r;
+        h.r = tmp;
+      }
+      parent = node;
+      node = h.l;
+    }
+  }
+  __host__ __device__ inline bool pop(const EthMem& M, double* t, uint32_t* ev, int32_t* blk) {
+    if (hroot < 0) return false;
+    *t = M.heap[hroot].t;
+    *ev = M.heap[hroot].ev;
+    *blk = M.heap[hroot].blk;
+    int32_t parent = -1, side = 0, node = hroot;
+    for (;;) {
+      const int32_t l = M.heap[node].l, r = M.heap[node].r;
+      int32_t repl = -2;
+      if (r < 0)
+        repl = l;
+      else if (l < 0)
+        repl = r;
+      if (repl != -2) {
+        if (parent < 0)
+          hroot = repl;
+        else if (side == 0)
+          M.heap[parent].l = repl;
+        else
+          M.heap[parent].r = repl;
+        M.heap[node].l = hfree;
+        hfree = node;
+        return true;
+      }
+      const int32_t c = (M.heap[l].t <= M.heap[r].t) ? l : r;
+      M.heap[node].t = M.heap[c].t;
+      M.heap[node].ev = M.heap[c].ev;
+      M.heap[node].blk = M.heap[c].blk;
+      parent = node;
+      side = c == l ? 0 : 1;
+      node = c;
+    }
+  }
+  __host__ __device__ inline void push_now(const EthParams& P, const EthMem& M, uint32_t ev,
+                                           int32_t blk) {
+    push(P, M, now, ev, blk);
+  }
+
+  // ------------------------------------------------------------------ randomness
+  __host__ __device__ inline int32_t miner_of(const EthParams& P, const Stream& S, int32_t k) {
+    const Words4 w = S.block((uint32_t)k, TAG_ACT);
+    if ((uint64_t)w.w0 < P.t_att) return 0;
+    return 1 + (int32_t)(((uint64_t)w.w1 * (uint64_t)P.d) >> 32);
+  }
+  __host__ __device__ inline double act_delay(const EthParams& P, const Stream& S, int32_t j) {
+    const Words4 w = S.block((uint32_t)j, TAG_ACT);
+    return (-1.0 * P.ev) * cpr_log(u53(w.w2, w.w3));
+  }
+  __host__ __device__ inline void schedule_pow(const EthParams& P, const Stream& S,
+                                               const EthMem& M) {
+    push(P, M, now + act_delay(P, S, c_act), mkev(EV_CLOCK, 0, KD_POW), -1);
+  }
+
+  // ------------------------------------------------------------------ DAG
+  // simulator.ml:233-332 (genesis) and 122-136 / 377-399 (append + set_rewards with
+  // ethereum.ml:173-197; precursor = first parent)
+  __host__ __device__ inline int32_t append(const EthParams& P, const EthMem& M, int32_t node,
+                                            const Payload& d) {
+    EBlock& pb = B(P, M, d.p[0]);
+    int32_t ra = pb.rew_att, rd = pb.rew_def;
+    const int32_t nu = d.np - 1;
+    if (node == 0)
+      ra += 32 + nu;
+    else
+      rd += 32 + nu;
+    for (int32_t i = 1; i < d.np; ++i) {
+      EBlock& u = B(P, M, d.p[i]);
+      const int32_t amt = P.scheme == 0 ? 30 : 4 * (8 - (d.height - u.height));
+      if (u.miner == 0)
+        ra += amt;
+      else if (u.miner > 0)
+        rd += amt;
+    }
+    const int32_t s = ++newest;
+    EBlock& b = M.blk[s & (P.cap_b - 1)];
+    b.serial = s;
+    b.p[0] = d.p[0];
+    b.p[1] = d.np > 1 ? d.p[1] : -1;
+    b.p[2] = d.np > 2 ? d.p[2] : -1;
+    b.np = d.np;
+    b.height = d.height;
+    b.work = d.work;
+    b.miner = node;
+    b.rew_att = ra;
+    b.rew_def = rd;
+    b.share_k = -1;
+    b.share_off = 0;
+    b.time = now;
+    for (int32_t j = 0; j < P.n; ++j) V(P, M, s, j) = V_INV;
+    return s;
+  }
+
+  // Honest.puzzle_payload' (ethereum.ml:234-277) in node `view`'s view
+  __host__ __device__ inline Payload payload(const EthParams& P, const EthMem& M, int32_t view,
+                                             int32_t tip, int32_t filter, int32_t f_own,
+                                             int32_t f_foreign) {
+    int32_t* cand = M.scr + SCR_CAND;
+    int32_t* key = M.scr + SCR_KEY;
+    int32_t* ic = M.scr + SCR_QA;  // in-chain set (tip + parents of tip..gen5), <= 19
+    int32_t nua[6];
+    int32_t ng = 0, nic = 0, lowest = -1;
+    ic[nic++] = tip;
+    {
+      int32_t b = tip;
+#pragma unroll
+      for (int32_t gen = 0; gen < 6; ++gen) {
+        nua[gen] = -2;
+        if (b >= 0) {
+          const EBlock& x = B(P, M, b);
+          if (x.np == 0) {
+            b = -1;
+          } else {
+            nua[gen] = x.p[0];
+            lowest = x.p[0];
+            ng = gen + 1;
+            for (int32_t i = 0; i < x.np; ++i) ic[nic++] = x.p[i];
+            b = x.p[0];
+          }
+        }
+      }
+    }
+    // candidates: visible children of nua blocks (via the first parent), not in chain;
+    // order: generation ascending, then newest first (children lists are newest first)
+    int32_t nc = 0;
+    if (ng > 0) {
+      for (int32_t s = newest; s > lowest && !dead; --s) {
+        const uint8_t vk = V(P, M, s, view) & V_KIND;
+        if (vk == V_INV) continue;
+        const EBlock& c = B(P, M, s);
+        if (c.np == 0) continue;
+        int32_t g = -1;
+#pragma unroll
+        for (int32_t i = 0; i < 6; ++i)
+          if (nua[i] == c.p[0]) g = i;
+        if (g < 0) continue;
+        bool inchain = false;
+        for (int32_t i = 0; i < nic; ++i) inchain |= ic[i] == s;
+        if (inchain) continue;
+        const bool mine = vk == V_REL || vk == V_WH;
+        bool keep = true;
+        if (filter == F_MINING)
+          keep = (f_own && mine) || (f_foreign && !mine);
+        else if (filter == F_PUBLIC)
+          keep = vk == V_REL || vk == V_RECV;
+        if (!keep) continue;
+        if (nc >= NCAND) {
+          fail(3);
+          break;
+        }
+        // stable insertion by generation
+        int32_t pos = nc;
+        while (pos > 0 && (key[pos - 1] >> 28) > g) {
+          cand[pos] = cand[pos - 1];
+          key[pos] = key[pos - 1];
+          --pos;
+        }
+        cand[pos] = s;
+        // sort key: not own (bit 27), height (27 bits); generation kept in bits 28+
+        key[pos] = (g << 28) | ((mine ? 0 : 1) << 27) | (c.height & 0x7ffffff);
+        ++nc;
+      }
+    }
+    for (int32_t i = 0; i < nc; ++i) key[i] &= 0x0fffffff;
+    ocaml_heap_sort(cand, key, nc);
+    Payload d;
+    const EBlock& t = B(P, M, tip);
+    const int32_t nu = nc < 2 ? nc : 2;
+    d.p[0] = tip;
+    d.p[1] = nu > 0 ? cand[0] : -1;
+    d.p[2] = nu > 1 ? cand[1] : -1;
+    d.np = 1 + nu;
+    d.height = t.height + 1;
+    d.work = t.work + 1 + nu;
+    return d;
+  }
+
+  // OCaml stdlib Array.sort (ternary heap sort, not stable) on (key, cand) pairs, keys
+  // compared as integers; restated for the device (the tie order is semantics:
+  // Compare.at_most_first, compare.ml:66-75, ethereum.ml:269)
+  __host__ __device__ static inline void ocaml_heap_sort(int32_t* v, int32_t* k, int32_t l) {
+    if (l < 2) return;
+    auto maxson = [&](int32_t len, int32_t i) -> int32_t {
+      const int32_t i31 = i + i + i + 1;
+      int32_t x = i31;
+      if (i31 + 2 < len) {
+        if (k[i31] < k[i31 + 1]) x = i31 + 1;
+        if (k[x] < k[i31 + 2]) x = i31 + 2;
+        return x;
+      }
+      if (i31 + 1 < len && k[i31] < k[i31 + 1]) return i31 + 1;
+      if (i31 < len) return i31;
+      return -1;
+    };
+    for (int32_t i = (l + 1) / 3 - 1; i >= 0; --i) {
+      // trickle
+      const int32_t ek = k[i], ev = v[i];
+      int32_t p = i;
+      for (;;) {
+        const int32_t j = maxson(l, p);
+        if (j < 0 || !(k[j] > ek)) break;
+        k[p] = k[j];
+        v[p] = v[j];
+        p = j;
+      }
+      k[p] = ek;
+      v[p] = ev;
+    }
+    for (int32_t i = l - 1; i >= 2; --i) {
+      const int32_t ek = k[i], ev = v[i];
+      k[i] = k[0];
+      v[i] = v[0];
+      // bubble: hole from the root to a leaf
+      int32_t p = 0;
+      for (;;) {
+        const int32_t j = maxson(i, p);
+        if (j < 0) break;
+        k[p] = k[j];
+        v[p] = v[j];
+        p = j;
+      }
+      // trickleup
+      for (;;) {
+        const int32_t father = (p - 1) / 3;
+        if (k[father] < ek) {
+          k[p] = k[father];
+          v[p] = v[father];
+          if (father > 0) {
+            p = father;
+            continue;
+          }
+          k[0] = ek;
+          v[0] = ev;
+          break;
+        }
+        k[p] = ek;
+        v[p] = ev;
+        break;
+      }
+    }
+    const int32_t tk = k[0], tv = v[0];
+    k[0] = k[1];
+    v[0] = v[1];
+    k[1] = tk;
+    v[1] = tv;
+  }
+
+  // Dagtools.common_ancestor (dagtools.ml:102-121) in the attacker's view; ancestors are
+  // visited by descending (depth, serial), depth = height + 1 on valid Ethereum DAGs
+  __host__ __device__ static inline uint64_t ca_key(int32_t h, int32_t s) {
+    return ((uint64_t)(uint32_t)h << 32) | (uint32_t)s;
+  }
+  // frontier: (height, serial) pairs sorted by descending key, set semantics
+  __host__ __device__ inline void q_insert(int32_t* q, int32_t* nq, int32_t s, int32_t h) {
+    const uint64_t kk = ca_key(h, s);
+    int32_t i = *nq;
+    for (int32_t j = 0; j < *nq; ++j)
+      if (q[2 * j + 1] == s) return;  // set semantics
+    if (*nq >= NQ / 2) {
+      fail(4);
+      return;
+    }
+    while (i > 0 && ca_key(q[2 * (i - 1)], q[2 * (i - 1) + 1]) < kk) {
+      q[2 * i] = q[2 * (i - 1)];
+      q[2 * i + 1] = q[2 * (i - 1) + 1];
+      --i;
+    }
+    q[2 * i] = h;
+    q[2 * i + 1] = s;
+    ++*nq;
+  }
+  __host__ __device__ inline int32_t q_next(const EthParams& P, const EthMem& M, int32_t* q,
+                                            int32_t* nq) {
+    if (*nq == 0) return -1;
+    const int32_t s = q[1];
+    for (int32_t j = 1; j < *nq; ++j) {
+      q[2 * (j - 1)] = q[2 * j];
+      q[2 * (j - 1) + 1] = q[2 * j + 1];
+    }
+    --*nq;
+    const EBlock& b = B(P, M, s);
+    for (int32_t i = 0; i < b.np; ++i) {
+      const int32_t ps = b.p[i];
+      if (!visible(P, M, ps, 0)) continue;
+      q_insert(q, nq, ps, B(P, M, ps).height);
+    }
+    return s;
+  }
+  __host__ __device__ inline int32_t common_ancestor(const EthParams& P, const EthMem& M,
+                                                     int32_t a, int32_t b) {
+    int32_t* qa = M.scr + SCR_QA;
+    int32_t* qb = M.scr + SCR_QB;
+    int32_t na = 0, nb = 0;
+    q_insert(qa, &na, a, B(P, M, a).height);
+    q_insert(qb, &nb, b, B(P, M, b).height);
+    int32_t x = q_next(P, M, qa, &na);
+    int32_t y = q_next(P, M, qb, &nb);
+    while (x >= 0 && y >= 0 && !dead) {
+      if (x == y) return x;
+      const uint64_t kx = ca_key(B(P, M, x).height, x), ky = ca_key(B(P, M, y).height, y);
+      if (kx > ky)
+        x = q_next(P, M, qa, &na);
+      else
+        y = q_next(P, M, qb, &nb);
+    }
+    fail(4);
+    return 0;
+  }
+
+  // ------------------------------------------------------------------ actions
+  // Simulator.handle_action share part (simulator.ml:401-419): recursive release of
+  // withheld blocks, parents in order; keyed link coordinates (c_act, position)
+  __host__ __device__ inline void share(const EthParams& P, const EthMem& M, int32_t node,
+                                        int32_t s0) {
+    int32_t* st = M.scr + SCR_STACK;
+    int32_t sp = 0, off = 0;
+    st[sp++] = s0;
+    while (sp > 0 && !dead) {
+      const int32_t s = st[--sp];
+      uint8_t& v = V(P, M, s, node);
+      if ((v & V_KIND) != V_WH) continue;  // received / released: nothing; invisible: n/a
+      v = (uint8_t)((v & ~V_KIND) | V_REL);
+      EBlock& b = B(P, M, s);
+      b.share_k = c_act;
+      b.share_off = off++;
+      push_now(P, M, mkev(EV_TX, node, KD_NET), s);
+      if (sp + b.np > NSTACK) {
+        fail(5);
+        return;
+      }
+      for (int32_t i = b.np - 1; i >= 0; --i) st[sp++] = b.p[i];
+    }
+  }
+
+  __host__ __device__ inline int32_t update_head(const EthParams& P, const EthMem& M,
+                                                 int32_t old, int32_t cand) {
+    return B(P, M, cand).height > B(P, M, old).height ? cand : old;
+  }
+
+  // ------------------------------------------------------------------ agent
+  __host__ __device__ inline void agent_init(int32_t root) {
+    pub = priv = root;
+    pending = -1;
+    own = foreign = 1;
+  }
+  // ethereum_ssz.ml:325-362
+  __host__ __device__ inline void prepare(const EthParams& P, const EthMem& M, uint32_t kind,
+                                          int32_t x) {
+    int32_t p = pub;
+    if (pending >= 0) p = update_head(P, M, p, pending);
+    int32_t q = priv;
+    if (kind == KD_NET) {
+      p = update_head(P, M, p, x);
+      o_event = 1;
+    } else {
+      q = x;
+      o_event = 0;
+    }
+    o_pub = p;
+    o_priv = q;
+    o_common = common_ancestor(P, M, p, q);
+  }
+  // ethereum_ssz.ml:364-396; orphans only when asked (the built-in policies never read
+  // them)
+  __host__ __device__ inline EthObs observe(const EthParams& P, const EthMem& M,
+                                            bool orphans) {
+    const EBlock& c = B(P, M, o_common);
+    const EBlock& pr = B(P, M, o_priv);
+    const EBlock& pu = B(P, M, o_pub);
+    EthObs o;
+    o.public_height = pu.height - c.height;
+    o.public_work = pu.work - c.work;
+    o.private_height = pr.height - c.height;
+    o.private_work = pr.work - c.work;
+    o.diff_height = o.private_height - o.public_height;
+    o.diff_work = o.private_work - o.public_work;
+    o.event = o_event;
+    o.public_orphans = o.private_orphans_inclusive = o.private_orphans_exclusive = 0;
+    if (orphans) {
+      o.public_orphans = payload(P, M, 0, o_pub, F_PUBLIC, 0, 0).np - 1;
+      o.private_orphans_inclusive = payload(P, M, 0, o_priv, F_MINING, 1, 1).np - 1;
+      o.private_orphans_exclusive = payload(P, M, 0, o_priv, F_MINING, 1, 0).np - 1;
+    }
+    return o;
+  }
+  // ethereum_ssz.ml:398-429; returns the block to share (-1: none); index in [0, 24)
+  __host__ __device__ inline int32_t apply(const EthParams& P, const EthMem& M, int32_t index) {
+    const int32_t action = index >> 2;
+    auto release_upto = [&](int32_t target) {
+      int32_t b = o_priv;
+      while (!dead) {
+        const EBlock& x = B(P, M, b);
+        if (x.height <= target) break;
+        b = x.p[0];
+      }
+      return b;
+    };
+    int32_t sh = -1, np = o_priv;
+    switch (action) {
+      case A_ADOPT_RELEASE:
+        sh = o_priv;
+        np = o_pub;
+        break;
+      case A_ADOPT_DISCARD: np = o_pub; break;
+      case A_MATCH: sh = release_upto(B(P, M, o_pub).height); break;
+      case A_OVERRIDE: sh = release_upto(B(P, M, o_pub).height + 1); break;
+      case A_RELEASE1: sh = release_upto(B(P, M, o_common).height + 1); break;
+      default: break;
+    }
+    pub = o_pub;
+    priv = np;
+    pending = sh;
+    own = (index >> 1) & 1;
+    foreign = index & 1;
+    return sh;
+  }
+
+  // ------------------------------------------------------------------ engine
+  __host__ __device__ inline void init(const EthParams& P, const Stream& S, const EthMem& M) {
+    now = 0.0;
+    c_act = 0;
+    newest = 0;
+    act0 = 0;
+    hroot = -1;
+    hfree = -1;
+    hused = 0;
+    status = 0u;
+    dead = 0;
+    steps = 0;
+    dr_node = -1;
+    EBlock& r = M.blk[0];
+    r.serial = 0;
+    r.p[0] = r.p[1] = r.p[2] = -1;
+    r.np = 0;
+    r.height = 0;
+    r.work = 0;
+    r.miner = -1;
+    r.rew_att = r.rew_def = 0;
+    r.share_k = -1;
+    r.share_off = 0;
+    r.time = 0.0;
+    for (int32_t j = 0; j < P.n; ++j) {
+      V(P, M, 0, j) = V_RECV | V_GOT;
+      M.tips[j] = 0;
+    }
+    agent_init(0);
+    schedule_pow(P, S, M);
+  }
+
+  // one popped event that is not the attacker's gym interaction (simulator.ml:421-508)
+  __host__ __device__ inline void handle(const EthParams& P, const Stream& S, const EthMem& M,
+                                         uint32_t ev, int32_t s) {
+    const uint32_t ty = ev & 7u, kind = (ev >> 3) & 3u;
+    const int32_t node = (int32_t)(ev >> 5);
+    switch (ty) {
+      case EV_MV: {
+        uint8_t& v = V(P, M, s, node);
+        if ((v & V_KIND) != V_INV) break;
+        const EBlock& b = B(P, M, s);
+        bool ok = true;
+        for (int32_t i = 0; i < b.np; ++i) ok &= visible(P, M, b.p[i], node);
+        if (!ok) break;
+        v = (uint8_t)((v & ~V_KIND) | (kind == KD_NET ? V_RECV : V_WH));
+        push_now(P, M, mkev(EV_ON, node, kind), s);
+        push_now(P, M, mkev(EV_MDV, node, kind), s);
+        break;
+      }
+      case EV_ON: {
+        if (node == 0) {
+          // loop mode: the attacker node's handler (ethereum_ssz.ml:433-441)
+          prepare(P, M, kind, s);
+          const EthObs o = observe(P, M, false);
+          const int32_t sh = apply(P, M, eth_policy(P.policy, o));
+          if (sh >= 0) share(P, M, 0, sh);
+          break;
+        }
+        // Honest.handler (ethereum.ml:284-297)
+        int32_t& tip = M.tips[node];
+        tip = update_head(P, M, tip, s);
+        if ((V(P, M, s, node) & V_KIND) == V_WH) share(P, M, node, s);
+        break;
+      }
+      case EV_CLOCK: {
+        const int32_t m = miner_of(P, S, c_act);
+        if (m == 0) {
+          ++act0;
+          dr_node = 0;
+          if (P.mode == 1) dr = payload(P, M, 0, priv, F_MINING, own, foreign);
+        } else {
+          dr_node = m;
+          dr = payload(P, M, m, M.tips[m], F_ALL, 0, 0);
+        }
+        push_now(P, M, mkev(EV_DAG, m, KD_POW), -1);
+        ++c_act;
+        schedule_pow(P, S, M);
+        break;
+      }
+      case EV_DAG: {
+        const int32_t v = append(P, M, node, dr);
+        push_now(P, M, mkev(EV_MV, node, KD_POW), v);
+        break;
+      }
+      case EV_TX: {
+        const EBlock& b = B(P, M, s);
+        for (int32_t dst = 0; dst < P.n; ++dst) {
+          if (dst == node) continue;
+          double delay;
+          if (P.net == 1)
+            delay = 0.0;
+          else if (node == 0)
+            delay = S.link_u((uint32_t)b.share_k, (uint32_t)b.share_off, (uint32_t)dst) *
+                        (P.dmax - 0.0) +
+                    0.0;
+          else
+            delay = dst == 0 ? 0.0 : P.delta;
+          push(P, M, now + delay, mkev(EV_RX, dst, KD_NET), s);
+        }
+        break;
+      }
+      case EV_RX: {
+        uint8_t& v = V(P, M, s, node);
+        if (!(v & V_GOT)) {
+          v |= V_GOT;
+          push_now(P, M, mkev(EV_MV, node, KD_NET), s);
+        }
+        break;
+      }
+      case EV_MDV: {
+        // children (newest first) already received at this node become visible
+        for (int32_t c = newest; c > s && !dead; --c) {
+          if (!(V(P, M, c, node) & V_GOT)) continue;
+          const EBlock& cb = B(P, M, c);
+          bool child = false;
+          for (int32_t i = 0; i < cb.np; ++i) child |= cb.p[i] == s;
+          if (child) push_now(P, M, mkev(EV_MV, node, KD_NET), c);
+        }
+        break;
+      }
+    }
+  }
+
+  // engine.ml:108-121
+  __host__ __device__ inline bool skip_to_interaction(const EthParams& P, const Stream& S,
+                                                      const EthMem& M, uint32_t* kind,
+                                                      int32_t* blk) {
+    double t;
+    uint32_t ev;
+    int32_t s;
+    while (!dead) {
+      if (!pop(M, &t, &ev, &s)) {
+        fail(6);
+        return false;
+      }
+      now = t;
+      const uint32_t ty = ev & 7u;
+      const int32_t node = (int32_t)(ev >> 5);
+      if (ty == EV_ON && node == 0) {
+        *kind = (ev >> 3) & 3u;
+        *blk = s;
+        return true;
+      }
+      if (ty == EV_DAG && node == 0) {
+        const Payload d = payload(P, M, 0, priv, F_MINING, own, foreign);
+        const int32_t v = append(P, M, 0, d);
+        push_now(P, M, mkev(EV_MV, 0, KD_POW), v);
+        continue;
+      }
+      handle(P, S, M, ev, s);
+    }
+    return false;
+  }
+
+  // winner over [attacker preference; defenders' tips] (ethereum.ml:159-162)
+  __host__ __device__ inline int32_t head(const EthParams& P, const EthMem& M, int32_t att) {
+    int32_t h = att;
+    int32_t hh = B(P, M, att).height;
+    for (int32_t j = 1; j < P.n; ++j) {
+      const int32_t t = M.tips[j];
+      const int32_t th = B(P, M, t).height;
+      if (th > hh) {
+        h = t;
+        hh = th;
+      }
+    }
+    return h;
+  }
+
+  // gym: reset (engine.ml:122-170)
+  __host__ __device__ inline void gym_reset(const EthParams& P, const Stream& S,
+                                            const EthMem& M) {
+    init(P, S, M);
+    uint32_t kind;
+    int32_t b;
+    if (skip_to_interaction(P, S, M, &kind, &b)) prepare(P, M, kind, b);
+  }
+
+  // gym: step (engine.ml:176-249); returns the head, sets *done
+  __host__ __device__ inline int32_t gym_step(const EthParams& P, const Stream& S,
+                                              const EthMem& M, int32_t action, bool* done) {
+    const int32_t sh = apply(P, M, action);
+    if (sh >= 0) share(P, M, 0, sh);
+    ++steps;
+    uint32_t kind;
+    int32_t b;
+    const int32_t att = priv;
+    if (skip_to_interaction(P, S, M, &kind, &b)) prepare(P, M, kind, b);
+    const int32_t hd = head(P, M, att);
+    const double progress = (double)B(P, M, hd).work;
+    *done = dead || !(steps < P.max_steps && progress < P.max_progress && now < P.max_time);
+    return hd;
+  }
+
+  // loop: Simulator.loop ~activations (simulator.ml:519-533), then the head
+  __host__ __device__ inline int32_t loop(const EthParams& P, const Stream& S, const EthMem& M) {
+    init(P, S, M);
+    int64_t left = P.activations;
+    double t;
+    uint32_t ev;
+    int32_t s;
+    while (!dead && pop(M, &t, &ev, &s)) {
+      now = t;
+      if ((ev & 7u) == EV_CLOCK) {
+        if (left <= 0) continue;
+        --left;
+      }
+      handle(P, S, M, ev, s);
+    }
+    return head(P, M, priv);
+  }
+};
+
+}  // namespace eth
+}  // namespace cpr

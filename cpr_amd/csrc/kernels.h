@@ -5,6 +5,7 @@
 #include <stdint.h>
 
 #include "../../include/cpr_hip.h"
+#include "ethereum_lane.h"
 #include "nakamoto_lane.h"
 
 namespace cpr {
@@ -56,6 +57,13 @@ hipError_t launch_policy(int32_t policy, int unit, const double* obs, int64_t n,
 hipError_t launch_stream_fill(uint64_t seed, uint64_t ep, uint32_t idx0, uint32_t tag, int64_t n,
                               uint32_t* out, double* exp_out, hipStream_t st);
 size_t lock_lane_bytes();
+
+// Ethereum (kernels_eth.hip): mem = lanes x lane_bytes, one region per resident lane
+hipError_t launch_eth_run_episodes(const eth::EthParams& P, uint64_t seed, uint64_t first,
+                                   int64_t n_eps, uint8_t* mem, int64_t lane_bytes,
+                                   int64_t lanes, cpr_episode_record* recs, cpr_summary* sum,
+                                   hipStream_t st);
+int eth_blocks_per_cu();
 int run_episodes_blocks_per_cu(int32_t mode);  // resident 256-lane workgroups per CU
 
 }  // namespace cpr

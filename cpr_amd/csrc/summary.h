@@ -1,0 +1,86 @@
+// Episode-summary reduction shared by the episode kernels (kernels.hip, kernels_eth.hip):
+// per-lane integer accumulators, wave shuffles, one LDS pass per workgroup, then one
+// 64-bit atomic per field per workgroup. Integer arithmetic only, so the totals do not
+// depend on scheduling or on how episodes are sharded over GPUs.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/cpr_hip.h"
+#include "cpr_stream.h"
+
+#pragma clang fp contract(off)
+
+namespace cpr {
+
+constexpr int kBlock = 256;
+
+__device__ inline int64_t wave_sum(int64_t v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+
+struct Acc {
+  int64_t episodes, steps, activations, ra_fx, rd_fx, prog_fx, orphans, tie, overlap, other;
+  uint64_t rel_fx, rel_sq_fx;
+};
+
+// one finished episode; rewards and progress in 2^-20 fixed point, rel = attacker share
+// of the head's rewards (wrappers.py:14-26 SparseRelativeRewardWrapper)
+__device__ inline void acc_episode(Acc& a, int64_t ra_fx, int64_t rd_fx, int64_t prog_fx,
+                                   double rel, int64_t head_height, int64_t steps,
+                                   int64_t acts, uint32_t status, int32_t* hist_lds) {
+  a.episodes += 1;
+  a.steps += steps;
+  a.activations += acts;
+  a.ra_fx += ra_fx;
+  a.rd_fx += rd_fx;
+  a.prog_fx += prog_fx;
+  a.orphans += acts - head_height;
+  a.tie += (status & CPR_ST_TIE) ? 1 : 0;
+  a.overlap += (status & CPR_ST_OVERLAP) ? 1 : 0;
+  a.other += (status & ~(uint32_t)(CPR_ST_TIE | CPR_ST_OVERLAP)) ? 1 : 0;
+  a.rel_fx += (uint64_t)__builtin_rint(rel * 4294967296.0);
+  a.rel_sq_fx += (uint64_t)__builtin_rint(rel * rel * 4294967296.0);
+  int bin = (int)(rel * (double)CPR_HIST_BINS);
+  bin = bin < 0 ? 0 : (bin >= CPR_HIST_BINS ? CPR_HIST_BINS - 1 : bin);
+  atomicAdd(&hist_lds[bin], 1);
+}
+
+__device__ inline void block_flush(const Acc& a, int32_t* hist_lds, cpr_summary* out) {
+  __shared__ int64_t red[kBlock / 64][12];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  int64_t v[12] = {a.episodes, a.steps,   a.activations, a.ra_fx,
+                   a.rd_fx,    a.prog_fx, a.orphans,     a.tie,
+                   a.overlap,  a.other,   (int64_t)a.rel_fx, (int64_t)a.rel_sq_fx};
+#pragma unroll
+  for (int i = 0; i < 12; ++i) v[i] = wave_sum(v[i]);
+  if (lane == 0)
+#pragma unroll
+    for (int i = 0; i < 12; ++i) red[wave][i] = v[i];
+  __syncthreads();
+  if (threadIdx.x < 12) {
+    int64_t s = 0;
+    for (int w = 0; w < kBlock / 64; ++w) s += red[w][threadIdx.x];
+    unsigned long long* base = (unsigned long long*)out;
+    // cpr_summary word index of each accumulator (rel sums sit before orphans)
+    const int idx[12] = {0, 1, 2, 3, 4, 5, 8, 9, 10, 11, 6, 7};
+    if (s) atomicAdd(base + idx[threadIdx.x], (unsigned long long)s);
+  }
+  if (threadIdx.x < CPR_HIST_BINS && hist_lds[threadIdx.x])
+    atomicAdd((unsigned long long*)&out->hist[threadIdx.x],
+              (unsigned long long)hist_lds[threadIdx.x]);
+}
+
+__device__ inline Stream make_stream(uint64_t seed, uint64_t ep) {
+  Stream S;
+  S.k0 = (uint32_t)seed;
+  S.k1 = (uint32_t)(seed >> 32);
+  S.e0 = (uint32_t)ep;
+  S.e1 = (uint32_t)(ep >> 32);
+  return S;
+}
+
+
+}  // namespace cpr

@@ -220,14 +220,14 @@ class Batch:
     def observation_spec(self):
         ol = ctypes.c_int32()
         na = ctypes.c_int32()
-        low = np.zeros(4)
-        high = np.zeros(4)
+        low = np.zeros(16)
+        high = np.zeros(16)
         L.check(
             L.lib().cpr_observation_spec(
                 self.handle, ctypes.byref(ol), ctypes.byref(na), L.ptr(low), L.ptr(high)
             )
         )
-        return ol.value, na.value, low, high
+        return ol.value, na.value, low[: ol.value], high[: ol.value]
 
 
 def policy_registry(protocol=L.PROTO_NAKAMOTO):

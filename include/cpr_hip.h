@@ -105,7 +105,12 @@ enum cpr_episode_status {
   CPR_ST_TIE = 1u,      /* a defender resolved an equal-time, equal-height delivery */
   CPR_ST_OVERLAP = 2u,  /* an activation fired while finite-delay messages were in flight;
                            the device resolves it by delivering first */
-  CPR_ST_DEEP_FORK = 4u /* more than 2^30 withheld blocks (never expected) */
+  CPR_ST_DEEP_FORK = 4u,      /* Nakamoto: private chain beyond its slots */
+  CPR_ST_TIE_UNRESOLVED = 8u, /* Nakamoto: tie replay capacity exceeded */
+  CPR_ST_STALE_TIME = 16u,    /* Nakamoto: head time older than the time log */
+  CPR_ST_CAPACITY = 32u       /* Ethereum: a lane capacity (block ring, event heap, uncle
+                                 candidates, ancestor frontier) was exceeded; the episode's
+                                 outputs are not valid */
 };
 
 typedef struct cpr_config {

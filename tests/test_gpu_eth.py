@@ -1,0 +1,86 @@
+"""Ethereum on the device (through the C ABI) against the CPU oracle — needs an MI355X.
+
+Every record field is bit-identical: rewards are dyadic (multiples of 1/32 for both
+incentive schemes), heights/work are integers and event times follow the same IEEE
+operation sequence on both sides (keyed stream, fdlibm log, -ffp-contract=off).
+"""
+
+import numpy as np
+import pytest
+
+import oracle_py as O
+from cpr_amd import _lib as L
+from cpr_amd import device
+
+pytestmark = pytest.mark.gpu
+
+FIELDS = [f for f in L.RECORD_DTYPE.names if f not in ("status",)]
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    return device.default_context()
+
+
+def _cfg(**kw):
+    kw.setdefault("protocol", L.PROTO_ETHEREUM)
+    return device.make_config(**kw)
+
+
+def _compare(cfg, keep, n, first=0):
+    b = device.Batch(cfg, keep=keep)
+    s, rec = b.run(n, first_episode=first, records=True)
+    ref = O.run_episodes(cfg, first, n, threads=8)
+    ok = (rec["status"] & 32) == 0
+    for f in FIELDS:
+        bad = np.nonzero((rec[f] != ref[f]) & ok)[0]
+        assert len(bad) == 0, (f, int(bad[0]), rec[f][bad[0]], ref[f][bad[0]])
+    return s, rec, ok
+
+
+GYM = [
+    # alpha, gamma, policy, scheme, steps, episodes
+    (0.35, 0.5, L.ETH_POLICY_FN19, L.REWARD_CONSTANT, 300, 256),
+    (0.35, 0.5, L.ETH_POLICY_FN19PKEL, L.REWARD_DISCOUNT, 300, 256),
+    (0.25, 0.0, L.ETH_POLICY_SELFISH_RELEASE, L.REWARD_CONSTANT, 300, 256),
+    (0.40, 0.9, L.ETH_POLICY_SELFISH_DISCARD, L.REWARD_DISCOUNT, 300, 256),
+    (0.10, 0.75, L.ETH_POLICY_HONEST, L.REWARD_CONSTANT, 300, 256),
+    (0.45, 0.5, L.ETH_POLICY_FN19, L.REWARD_DISCOUNT, 2016, 128),
+]
+
+
+@pytest.mark.parametrize("alpha,gamma,policy,scheme,steps,n", GYM)
+def test_eth_gym_records_match_oracle(ctx, alpha, gamma, policy, scheme, steps, n):
+    cfg, keep = _cfg(alpha=alpha, gamma=gamma, policy=policy, reward_scheme=scheme,
+                     max_steps=steps, seed=0xE7E70000)
+    s, rec, ok = _compare(cfg, keep, n)
+    assert ok.mean() > 0.97
+    assert s.episodes == n and int((rec["n_steps"] == steps).sum()) == int(ok.sum())
+
+
+@pytest.mark.parametrize("policy", [0, 1, 2, 3, 4])
+def test_eth_two_agents_loop_matches_oracle(ctx, policy):
+    cfg, keep = _cfg(alpha=0.3, network=L.NET_TWO_AGENTS, mode=L.MODE_LOOP, activations=10000,
+                     policy=policy, reward_scheme=L.REWARD_DISCOUNT, seed=11)
+    _compare(cfg, keep, 64)
+
+
+def test_eth_summary_independent_of_chunking(ctx):
+    cfg, keep = _cfg(alpha=0.3, gamma=0.5, policy=L.ETH_POLICY_FN19, max_steps=500, seed=3)
+    b = device.Batch(cfg, keep=keep)
+    whole, _ = b.run(3000, first_episode=0)
+    a, _ = b.run(1000, first_episode=0)
+    c, _ = b.run(2000, first_episode=1000)
+    for f in ["episodes", "activations", "reward_attacker_fx", "reward_defender_fx",
+              "progress_fx", "rel_revenue_fx", "orphans"]:
+        assert getattr(whole, f) == getattr(a, f) + getattr(c, f), f
+
+
+def test_eth_policy_registry_and_spec(ctx):
+    assert [n for n, _ in device.policy_registry(L.PROTO_ETHEREUM)] == [
+        "fn19pkel", "fn19", "selfish_discard", "selfish_release", "honest"]
+    cfg, keep = _cfg(alpha=0.3, gamma=0.5, max_steps=10)
+    b = device.Batch(cfg, keep=keep)
+    n_obs, n_act, lo, hi = b.observation_spec()
+    assert (n_obs, n_act) == (10, 24)
+    assert list(lo) == [0.0] * 10 and list(hi) == [1.0] * 10

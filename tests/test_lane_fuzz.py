@@ -24,3 +24,19 @@ def test_lane_matches_oracle_fuzz():
     assert out["mismatches"] == 0 and out["hazard_mismatches"] == 0, p.stderr[-2000:]
     assert out["unresolved"] == 0
     assert out["episodes"] > 1000
+
+
+def test_ethereum_lane_matches_oracle_fuzz():
+    # tests/native/eth_vs_oracle.cpp: cpr_amd/csrc/ethereum_lane.h (host build) vs the
+    # oracle's ethereum.cpp, every step: 10 observation fields incl. the three dry-run
+    # uncle selections, rewards, height, work, chain time, clock, activations, head miner;
+    # 5 policies + 2 random-action fuzzers x 2 reward schemes x alpha x gamma, and
+    # Simulator.loop tasks on the two-agents network
+    subprocess.run(["make", "-s", "-C", str(ROOT / "tests" / "native")], check=True)
+    exe = ROOT / "tests" / "native" / "build" / "eth_vs_oracle"
+    p = subprocess.run([str(exe), "6", "400"], capture_output=True, text=True, timeout=600)
+    out = json.loads(p.stdout.strip().splitlines()[-1])
+    assert p.returncode == 0, p.stderr[-2000:]
+    assert out["mismatches"] == 0, p.stderr[-2000:]
+    assert out["episodes"] > 1000 and out["steps"] > 300000
+    assert out["capacity"] <= out["episodes"] // 100
