@@ -68,9 +68,9 @@ def test_eth_two_agents_loop_matches_oracle(ctx, policy):
 def test_eth_summary_independent_of_chunking(ctx):
     cfg, keep = _cfg(alpha=0.3, gamma=0.5, policy=L.ETH_POLICY_FN19, max_steps=500, seed=3)
     b = device.Batch(cfg, keep=keep)
-    whole, _ = b.run(3000, first_episode=0)
-    a, _ = b.run(1000, first_episode=0)
-    c, _ = b.run(2000, first_episode=1000)
+    whole = b.run(3000, first_episode=0)
+    a = b.run(1000, first_episode=0)
+    c = b.run(2000, first_episode=1000)
     for f in ["episodes", "activations", "reward_attacker_fx", "reward_defender_fx",
               "progress_fx", "rel_revenue_fx", "orphans"]:
         assert getattr(whole, f) == getattr(a, f) + getattr(c, f), f
