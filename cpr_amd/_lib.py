@@ -23,8 +23,15 @@ CPR_E_STATE = -5
 
 PROTO_NAKAMOTO = 0
 PROTO_ETHEREUM = 1
+PROTO_BK = 2
 REWARD_CONSTANT = 0
 REWARD_DISCOUNT = 1
+REWARD_BLOCK = 2
+BK_POLICY_HONEST = 0
+BK_POLICY_GET_AHEAD = 1
+BK_POLICY_MINOR_DELAY = 2
+BK_POLICY_AVOID_LOSS = 3
+BK_POLICY_TABLE = 4
 ETH_POLICY_HONEST = 0
 ETH_POLICY_SELFISH_RELEASE = 1
 ETH_POLICY_SELFISH_DISCARD = 2
@@ -70,6 +77,8 @@ class Config(ctypes.Structure):
         ("activations", ctypes.c_int64),
         ("seed", ctypes.c_uint64),
         ("n_lanes", ctypes.c_int64),
+        ("k", ctypes.c_int32),
+        ("reserved", ctypes.c_int32),
     ]
 
 

@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define CPR_ABI_VERSION 2
+#define CPR_ABI_VERSION 3
 
 typedef struct cpr_ctx cpr_ctx;
 typedef struct cpr_batch cpr_batch;
@@ -52,13 +52,33 @@ enum cpr_status {
 
 enum cpr_protocol {
   CPR_PROTO_NAKAMOTO = 0, /* nakamoto.ml + nakamoto_ssz.ml */
-  CPR_PROTO_ETHEREUM = 1  /* ethereum.ml Byzantium + ethereum_ssz.ml (cpr_protocols.ml:39-49) */
+  CPR_PROTO_ETHEREUM = 1, /* ethereum.ml Byzantium + ethereum_ssz.ml (cpr_protocols.ml:39-49) */
+  CPR_PROTO_BK = 2        /* bk.ml + bk_ssz.ml (cpr_protocols.ml:53-72), k = cpr_config.k */
 };
 
-/* incentive schemes (ethereum.ml:3,173-197) */
+/* incentive schemes (ethereum.ml:3,173-197; bk.ml:3,151-176) */
 enum cpr_reward_scheme {
-  CPR_REWARD_CONSTANT = 0, /* Ethereum `Constant` (whitepaper): uncle 15/16 */
-  CPR_REWARD_DISCOUNT = 1  /* Ethereum `Discount` (Byzantium): uncle (8 - dh) / 8 */
+  CPR_REWARD_CONSTANT = 0, /* Ethereum `Constant` (whitepaper): uncle 15/16;
+                              B_k `Constant`: 1 per confirmed vote to its miner */
+  CPR_REWARD_DISCOUNT = 1, /* Ethereum `Discount` (Byzantium): uncle (8 - dh) / 8 */
+  CPR_REWARD_BLOCK = 2     /* B_k `Block`: k to the block's signer (leader) */
+};
+
+/* policy ids of the bk_ssz attack space (bk_ssz.ml:346-415; "avoid-loss" is avoid_loss_alt) */
+enum cpr_bk_policy {
+  CPR_BK_POLICY_HONEST = 0,
+  CPR_BK_POLICY_GET_AHEAD = 1,
+  CPR_BK_POLICY_MINOR_DELAY = 2,
+  CPR_BK_POLICY_AVOID_LOSS = 3,
+  CPR_BK_POLICY_TABLE = 4 /* action = table[((((min(pub,D-1)*D + min(priv,D-1))*(k+1)
+                             + min(public_votes,k))*(k+1) + min(private_votes_inclusive,k))*3
+                             + event] with D = policy_table_dim */
+};
+
+/* ssz_tools.ml:230-263 Action8, Variants.to_rank */
+enum cpr_action8 {
+  CPR_ADOPT_PROLONG = 0, CPR_OVERRIDE_PROLONG = 1, CPR_MATCH_PROLONG = 2, CPR_WAIT_PROLONG = 3,
+  CPR_ADOPT_PROCEED = 4, CPR_OVERRIDE_PROCEED = 5, CPR_MATCH_PROCEED = 6, CPR_WAIT_PROCEED = 7
 };
 
 /* policy ids of the ethereum_ssz attack space (ethereum_ssz.ml:444-538) */
@@ -133,6 +153,8 @@ typedef struct cpr_config {
   int64_t activations;       /* LOOP mode: activations per episode */
   uint64_t seed;             /* keyed-stream seed */
   int64_t n_lanes;           /* lockstep lanes for cpr_reset/cpr_step; 0 = none */
+  int32_t k;                 /* B_k: votes per block (bk.ml:7), >= 1 */
+  int32_t reserved;
 } cpr_config;
 
 /* one finished episode; identical layout is produced by the CPU oracle */
@@ -145,7 +167,7 @@ typedef struct cpr_episode_record {
   int64_t n_steps;           /* episode_n_steps              engine.ml:236 */
   int64_t n_activations;     /* episode_n_activations        engine.ml:237 */
   int32_t head_height;
-  int32_t head_miner;        /* -1 = n/a (genesis) */
+  int32_t head_miner;        /* -1 = n/a (genesis); B_k: the head block's signer (leader) */
   uint32_t status;           /* enum cpr_episode_status bits */
   int32_t head_work;         /* Ethereum head work (ethereum.ml:93-97); 0 for Nakamoto */
 } cpr_episode_record;

@@ -231,6 +231,14 @@ int32_t KeyedSimRng::pow_bits(int serial) { return (int32_t)ks.pow_bits((uint32_
 
 double KeyedSimRng::link_delay(const Link& l, const Block* m) {
   const uint32_t kw = (uint32_t)m->share_k, off = (uint32_t)m->share_off;
+  if (serial_links) {
+    const double u = ks.msg_u((uint32_t)m->serial, (uint32_t)l.dest);
+    switch (l.kind) {
+      case D_CONST: return l.a;
+      case D_UNIFORM: return u * (l.b - l.a) + l.a;
+      case D_EXP: return -1. * l.a * cpr_log(u);
+    }
+  }
   switch (l.kind) {
     case D_CONST: return l.a;
     case D_UNIFORM: return ks.link_u(kw, off, (uint32_t)l.dest) * (l.b - l.a) + l.a;
@@ -282,6 +290,7 @@ void Sim::schedule_pow() {
 
 bool Sim::validity(const Block* b) const {
   if (proto == 1) return eth_validity(b);
+  if (proto == 2) return bk_validity(b, bk_k);
   if (!b->has_pow || b->parents.size() != 1) return false;
   return b->value.height == b->parents[0]->value.height + 1 && b->value.miner >= 0;
 }
@@ -289,6 +298,10 @@ bool Sim::validity(const Block* b) const {
 void Sim::reward(Block* x) const {
   if (proto == 1) {
     eth_reward(x, eth_scheme, x->rewards);
+    return;
+  }
+  if (proto == 2) {
+    bk_reward(x, bk_scheme, bk_k, x->rewards);
     return;
   }
   if (x->value.miner >= 0) x->rewards[x->value.miner] += 1.;
@@ -397,7 +410,7 @@ void Sim::handle_event(const Event& ev) {
       if (!visible(n, ev.blk)) throw std::runtime_error("assert: OnNode invisible");
       for (auto* p : ev.blk->parents)
         if (!visible(n, p)) throw std::runtime_error("assert: OnNode parent invisible");
-      if (ev.kind == K_NETWORK && n != 0) {
+      if (ev.kind == K_NETWORK && n != 0 && proto != 2) {
         // diagnostic: equal-height candidate delivered at the same instant as the current tip
         Block* cur = nodes[n]->preferred();
         if (cur && cur != ev.blk && cur->value.height == ev.blk->value.height &&

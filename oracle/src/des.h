@@ -31,13 +31,15 @@ struct Vis {
 };
 
 // block payload: Nakamoto {height; miner} (nakamoto.ml:8-12); Ethereum adds work
-// (ethereum.ml:69-73, always 0 for Nakamoto)
+// (ethereum.ml:69-73, always 0 for Nakamoto); B_k: kind 1 = Vote {height; id = miner},
+// kind 0 = Block {height} with miner -1 (bk.ml:26-35)
 struct NakData {
   int height = 0;
   int miner = -1;  // -1 = None
   int work = 0;
+  int kind = 0;
   bool operator==(const NakData& o) const {
-    return height == o.height && miner == o.miner && work == o.work;
+    return height == o.height && miner == o.miner && work == o.work && kind == o.kind;
   }
 };
 
@@ -62,6 +64,10 @@ struct Block {
 // max_uncles = 2) and the Constant / Discount reward functions (ethereum.ml:173-197)
 bool eth_validity(const Block* b);
 void eth_reward(const Block* x, int scheme, std::vector<double>& r);
+// B_k referee pieces (bk.cpp): validity (bk.ml:110-132), Constant / Block rewards
+// (bk.ml:151-176)
+bool bk_validity(const Block* b, int k);
+void bk_reward(const Block* x, int scheme, int k, std::vector<double>& r);
 
 struct Draft {
   std::vector<Block*> parents;
@@ -150,6 +156,7 @@ struct KeyedSimRng : SimRng {
   uint64_t t_att;
   int d;
   double ev;
+  bool serial_links = false;  // key link delays by (message serial, dest): TAG_MSG
   KeyedSimRng(uint64_t seed, uint64_t episode, const Network& net);
   int miner(int k) override;
   double act_delay(int j) override;
@@ -194,9 +201,11 @@ struct Sim {
   int n_nodes = 0;
   uint32_t diag = 0;
   int pending_finite_rx = 0;
-  // protocol of the referee: 0 = Nakamoto, 1 = Ethereum (Byzantium parameters)
+  // protocol of the referee: 0 = Nakamoto, 1 = Ethereum (Byzantium parameters), 2 = B_k
   int proto = 0;
   int eth_scheme = 0;  // Ethereum incentive scheme: 0 = Constant, 1 = Discount
+  int bk_k = 0;        // B_k votes per block
+  int bk_scheme = 0;   // B_k incentive scheme: 0 = Constant, 2 = Block
 
   Sim(const Network& net, SimRng* rng);
   void init(std::vector<std::unique_ptr<NodeImpl>> nodes_);
@@ -215,6 +224,8 @@ struct Sim {
   bool validity(const Block* b) const;
   void reward(Block* x) const;  // set_rewards (simulator.ml:377-388)
   double progress(const Block* b) const {
+    if (proto == 2)  // bk.ml:42-46
+      return (double)(b->value.height * bk_k + (b->value.kind == 1 ? 1 : 0));
     return proto == 1 ? (double)b->value.work : (double)b->value.height;
   }
   // nakamoto.ml:43-48 and ethereum.ml:159-162 (both: first maximum height)

@@ -13,6 +13,10 @@
 //           kw  = activations simulated when the message was shared (c_activations),
 //           off = position of the message in that action's recursive share order
 //   pow   : ctr = (ep_lo, ep_hi, serial, TAG_POW)  w0 & 0x3FFFFFFF
+//   msg   : ctr = (ep_lo, ep_hi, serial, TAG_MSG | dest>>1)  words (2*(dest&1), +1) -> u
+//           link delay of message `serial` to `dest`, used where one node shares several
+//           times per activation window (B_k: votes, proposals); a node shares a given
+//           vertex at most once (simulator.ml:404-415), so (serial, dest) is unique
 //
 // exponential(ev) = (-1 * ev) * cpr_log(u)   (same expression shape as distributions.ml:24)
 // uniform(lo,hi)  = u * (hi - lo) + lo       (distributions.ml:17)
@@ -31,6 +35,7 @@ namespace oracle {
 static const uint32_t TAG_ACT = 0u;
 static const uint32_t TAG_LINK = 0x10000000u;
 static const uint32_t TAG_POW = 0x20000000u;
+static const uint32_t TAG_MSG = 0x30000000u;
 
 struct Philox4x32 {
   static void block(const uint32_t ctr_in[4], const uint32_t key_in[2], uint32_t out[4]) {
@@ -159,6 +164,11 @@ struct KeyedStream {
   double link_u(uint32_t kw, uint32_t off, uint32_t dest) const {
     uint32_t w[4];
     block(kw, TAG_LINK | (off << 12) | (dest >> 1), w);
+    return (dest & 1) ? u53(w[2], w[3]) : u53(w[0], w[1]);
+  }
+  double msg_u(uint32_t serial, uint32_t dest) const {
+    uint32_t w[4];
+    block(serial, TAG_MSG | (dest >> 1), w);
     return (dest & 1) ? u53(w[2], w[3]) : u53(w[0], w[1]);
   }
   uint32_t pow_bits(uint32_t serial) const {

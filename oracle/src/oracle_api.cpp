@@ -11,6 +11,7 @@
 #include "../../include/cpr_hip.h"
 #include "des.h"
 #include "ethereum.h"
+#include "bk.h"
 #include "ocaml_sort.h"
 
 using namespace oracle;
@@ -362,9 +363,48 @@ static int run_eth_gym_episode(const cpr_config* c, uint64_t ep, cpr_episode_rec
   return 0;
 }
 
+static BkTable bk_table_of(const cpr_config* c) {
+  BkTable t;
+  if (c->protocol == CPR_PROTO_BK && c->policy == BKPOL_TABLE) {
+    t.dim = c->policy_table_dim;
+    t.k = c->k;
+    t.actions.assign(c->policy_table, c->policy_table + bk_table_size(t.dim, t.k));
+  }
+  return t;
+}
+
+static int run_bk_gym_episode(const cpr_config* c, const BkTable* tab, uint64_t ep,
+                              cpr_episode_record* rec) {
+  GymBk g(params_of(c), c->k, c->reward_scheme, 1, nullptr, c->seed, ep);
+  double obs[BK_OBS_LEN];
+  g.reset(obs);
+  bool done = false;
+  StepInfo info{};
+  while (!done) {
+    int a = bk_policy(c->policy, g.observe_int(), c->k, tab);
+    g.step(a, obs, &done, &info);
+  }
+  rec->reward_attacker = info.episode_reward_attacker;
+  rec->reward_defender = info.episode_reward_defender;
+  rec->progress = info.episode_progress;
+  rec->chain_time = info.episode_chain_time;
+  rec->sim_time = info.episode_sim_time;
+  rec->n_steps = info.episode_n_steps;
+  rec->n_activations = info.episode_n_activations;
+  rec->head_height = info.head_height;
+  rec->head_miner = info.head_miner;
+  rec->status = 0;
+  rec->head_work = 0;
+  return 0;
+}
+
 static int run_gym_episode(const cpr_config* c, const TablePolicy* tab, uint64_t ep,
                            cpr_episode_record* rec) {
   if (c->protocol == CPR_PROTO_ETHEREUM) return run_eth_gym_episode(c, ep, rec);
+  if (c->protocol == CPR_PROTO_BK) {
+    BkTable bt = bk_table_of(c);
+    return run_bk_gym_episode(c, &bt, ep, rec);
+  }
   GymNakamoto g(params_of(c), 1, nullptr, c->seed, ep);
   double obs[4];
   g.reset(obs);
@@ -397,6 +437,24 @@ static int run_loop_episode(const cpr_config* c, uint64_t ep, cpr_episode_record
   if (c->network != CPR_NET_TWO_AGENTS) {
     set_err("oracle loop mode: two-agents network only");
     return -2;
+  }
+  if (c->protocol == CPR_PROTO_BK) {
+    BkTable bt = bk_table_of(c);
+    BkLoopResult r;
+    bk_loop_task(Network::two_agents(c->activation_delay, c->alpha), 1, nullptr, c->seed, ep,
+                 c->k, c->reward_scheme, c->policy, &bt, (int)c->activations, &r);
+    rec->reward_attacker = r.rewards[0];
+    rec->reward_defender = r.rewards[1];
+    rec->progress = r.head_progress;
+    rec->chain_time = r.head_time;
+    rec->sim_time = 0.0;
+    rec->n_steps = 0;
+    rec->n_activations = r.activations[0] + r.activations[1];
+    rec->head_height = r.head_height;
+    rec->head_miner = r.head_signer;
+    rec->status = 0;
+    rec->head_work = 0;
+    return 0;
   }
   if (c->protocol == CPR_PROTO_ETHEREUM) {
     int32_t hw = 0;
@@ -432,6 +490,126 @@ static int run_loop_episode(const cpr_config* c, uint64_t ep, cpr_episode_record
   rec->status = 0;
   rec->head_work = 0;
   return 0;
+}
+
+// ---------------- B_k (bk.ml, bk_ssz.ml)
+int oracle_bk_policy(int policy, const int32_t obs[8], int k, const uint8_t* table, int dim) {
+  BkTable t;
+  if (policy == BKPOL_TABLE) {
+    t.dim = dim;
+    t.k = k;
+    t.actions.assign(table, table + bk_table_size(dim, k));
+  }
+  BkObs o{obs[0], obs[1], obs[2], obs[3], obs[4], obs[5], obs[6], obs[7]};
+  return bk_policy(policy, o, k, &t);
+}
+void oracle_bk_obs_to_floats(const int32_t obs[8], int unit, int k, double out[8]) {
+  BkObs o{obs[0], obs[1], obs[2], obs[3], obs[4], obs[5], obs[6], obs[7]};
+  bk_obs_to_floats(o, unit != 0, k, out);
+}
+void oracle_bk_obs_of_floats(const double in[8], int unit, int k, int32_t out[8]) {
+  BkObs o = bk_obs_of_floats(in, unit != 0, k);
+  const int32_t v[8] = {o.public_blocks,           o.private_blocks, o.diff_blocks,
+                        o.public_votes,            o.private_votes_inclusive,
+                        o.private_votes_exclusive, o.lead,           o.event};
+  memcpy(out, v, sizeof(v));
+}
+void oracle_bk_obs_range(int unit, double low[8], double high[8]) {
+  bk_obs_range(unit != 0, low, high);
+}
+void* oracle_bk_gym_new(const cpr_config* c, int rng_mode, void* ocaml_rng, uint64_t episode) {
+  try {
+    return new GymBk(params_of(c), c->k, c->reward_scheme, rng_mode, (OcamlRandom*)ocaml_rng,
+                     c->seed, episode);
+  } catch (std::exception& e) {
+    set_err(e.what());
+    return nullptr;
+  }
+}
+void oracle_bk_gym_free(void* g) { delete (GymBk*)g; }
+int oracle_bk_gym_reset(void* g, double obs[8]) {
+  try {
+    ((GymBk*)g)->reset(obs);
+    return 0;
+  } catch (std::exception& e) {
+    set_err(e.what());
+    return -1;
+  }
+}
+int oracle_bk_gym_obs_fields(void* g, int32_t out[8]) {
+  BkObs o = ((GymBk*)g)->observe_int();
+  const int32_t v[8] = {o.public_blocks,           o.private_blocks, o.diff_blocks,
+                        o.public_votes,            o.private_votes_inclusive,
+                        o.private_votes_exclusive, o.lead,           o.event};
+  memcpy(out, v, sizeof(v));
+  return 0;
+}
+// info_out: 12 doubles in engine.ml:226-237 order + head_height + head signer + n_vertices
+int oracle_bk_gym_step(void* g, int action, double obs[8], double* reward, int* done,
+                       double info_out[15]) {
+  try {
+    bool d = false;
+    StepInfo i;
+    GymBk* e = (GymBk*)g;
+    *reward = e->step(action, obs, &d, &i);
+    *done = d ? 1 : 0;
+    if (info_out) {
+      double v[15] = {i.step_reward_attacker,    i.step_reward_defender,
+                      i.step_progress,           i.step_chain_time,
+                      i.step_sim_time,           i.episode_reward_attacker,
+                      i.episode_reward_defender, i.episode_progress,
+                      i.episode_chain_time,      i.episode_sim_time,
+                      (double)i.episode_n_steps, (double)i.episode_n_activations,
+                      (double)i.head_height,     (double)i.head_miner,
+                      (double)e->sim->dag.size()};
+      memcpy(info_out, v, sizeof(v));
+    }
+    return 0;
+  } catch (std::exception& e) {
+    set_err(e.what());
+    return -1;
+  }
+}
+// Simulator.loop task for B_k. net_kind 0: two_agents(alpha); 1: symmetric_clique of n_nodes
+// with exponential(prop_ev) propagation delays (cpr_protocols.ml:200-210,478-485).
+// policy < 0: node 0 honest. rewards_out / acts_out: n_nodes entries.
+int oracle_bk_loop(int net_kind, int n_nodes, double alpha, double activation_delay,
+                   double prop_ev, int rng_mode, void* rng, uint64_t seed, uint64_t episode,
+                   int k, int scheme, int policy, int activations, double* rewards_out,
+                   int64_t* acts_out, double* head_time, double* head_progress,
+                   int32_t* head_height, int32_t* head_signer, int64_t* n_vertices) {
+  try {
+    Network net;
+    if (net_kind == 0) {
+      net = Network::two_agents(activation_delay, alpha);
+    } else {
+      net.flooding = false;
+      net.activation_delay = activation_delay;
+      net.nodes.resize(n_nodes);
+      for (int i = 0; i < n_nodes; ++i) {
+        net.nodes[i].compute = 1. / (double)n_nodes;
+        for (int j = 0; j < n_nodes - 1; ++j)
+          net.nodes[i].links.push_back(Link{j >= i ? j + 1 : j, D_EXP, prop_ev, 0.0});
+      }
+    }
+    BkTable t;
+    BkLoopResult r;
+    bk_loop_task(net, rng_mode, (OcamlRandom*)rng, seed, episode, k, scheme, policy, &t,
+                 activations, &r);
+    for (size_t i = 0; i < r.rewards.size(); ++i) {
+      rewards_out[i] = r.rewards[i];
+      acts_out[i] = r.activations[i];
+    }
+    *head_time = r.head_time;
+    *head_progress = r.head_progress;
+    *head_height = r.head_height;
+    *head_signer = r.head_signer;
+    *n_vertices = r.n_vertices;
+    return 0;
+  } catch (std::exception& e) {
+    set_err(e.what());
+    return -1;
+  }
 }
 
 // threads: number of worker threads (episode-parallel, like Parany workers)

@@ -369,3 +369,127 @@ def eth_two_agents_task(alpha, policy, activations, scheme=1, rng=None, seed=0, 
     return dict(activations=acts.tolist(), reward=rew.tolist(), head_time=ht.value,
                 head_progress=hp.value, head_height=hh.value, head_work=hw.value,
                 diag=dg.value)
+
+
+# ---------------------------------------------------------------- B_k
+
+BK_POLICIES = {"honest": 0, "get-ahead": 1, "minor-delay": 2, "avoid-loss": 3}
+BK_OBS_FIELDS = ["public_blocks", "private_blocks", "diff_blocks", "public_votes",
+                 "private_votes_inclusive", "private_votes_exclusive", "lead", "event"]
+
+
+def _bk_declare(L):
+    P = ctypes.POINTER
+    vp = ctypes.c_void_p
+    from cpr_amd import _lib as C
+
+    L.oracle_bk_policy.argtypes = [ctypes.c_int, vp, ctypes.c_int, vp, ctypes.c_int]
+    L.oracle_bk_obs_to_floats.argtypes = [vp, ctypes.c_int, ctypes.c_int, vp]
+    L.oracle_bk_obs_of_floats.argtypes = [vp, ctypes.c_int, ctypes.c_int, vp]
+    L.oracle_bk_obs_range.argtypes = [ctypes.c_int, vp, vp]
+    L.oracle_bk_gym_new.restype = vp
+    L.oracle_bk_gym_new.argtypes = [P(C.Config), ctypes.c_int, vp, ctypes.c_uint64]
+    L.oracle_bk_gym_free.argtypes = [vp]
+    L.oracle_bk_gym_reset.argtypes = [vp, vp]
+    L.oracle_bk_gym_obs_fields.argtypes = [vp, vp]
+    L.oracle_bk_gym_step.argtypes = [vp, ctypes.c_int, vp, P(ctypes.c_double), P(ctypes.c_int),
+                                     vp]
+    L.oracle_bk_loop.argtypes = [
+        ctypes.c_int, ctypes.c_int, ctypes.c_double, ctypes.c_double, ctypes.c_double,
+        ctypes.c_int, vp, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_int, ctypes.c_int,
+        ctypes.c_int, ctypes.c_int, vp, vp, P(ctypes.c_double), P(ctypes.c_double),
+        P(ctypes.c_int32), P(ctypes.c_int32), P(ctypes.c_int64),
+    ]
+
+
+def bk_lib():
+    L = lib()
+    if not getattr(L, "_bk_declared", False):
+        _bk_declare(L)
+        L._bk_declared = True
+    return L
+
+
+def bk_policy(policy, fields, k, table=None, dim=0):
+    o = np.ascontiguousarray(fields, dtype=np.int32)
+    if table is not None:
+        t = np.ascontiguousarray(table, dtype=np.uint8)
+        return bk_lib().oracle_bk_policy(policy, o.ctypes.data, k, t.ctypes.data, dim)
+    return bk_lib().oracle_bk_policy(BK_POLICIES.get(policy, policy), o.ctypes.data, k, None, 0)
+
+
+def bk_obs_to_floats(fields, unit, k):
+    o = np.ascontiguousarray(fields, dtype=np.int32)
+    out = np.zeros(8)
+    bk_lib().oracle_bk_obs_to_floats(o.ctypes.data, 1 if unit else 0, k, out.ctypes.data)
+    return out
+
+
+def bk_obs_of_floats(floats, unit, k):
+    f = np.ascontiguousarray(floats, dtype=np.float64)
+    out = np.zeros(8, dtype=np.int32)
+    bk_lib().oracle_bk_obs_of_floats(f.ctypes.data, 1 if unit else 0, k, out.ctypes.data)
+    return out
+
+
+def bk_obs_range(unit):
+    lo, hi = np.zeros(8), np.zeros(8)
+    bk_lib().oracle_bk_obs_range(1 if unit else 0, lo.ctypes.data, hi.ctypes.data)
+    return lo, hi
+
+
+class BkGymEnv:
+    """The oracle's engine.ml restatement for the bk_ssz attack space."""
+
+    INFO_KEYS = GymEnv.INFO_KEYS + ["n_vertices"]
+
+    def __init__(self, config, episode=0, ocaml_rng=None):
+        self.cfg = config
+        self.h = bk_lib().oracle_bk_gym_new(ctypes.byref(config), 0 if ocaml_rng else 1,
+                                            ocaml_rng.h if ocaml_rng else None, episode)
+        if not self.h:
+            raise ValueError(lib().oracle_last_error().decode())
+
+    def __del__(self):
+        try:
+            bk_lib().oracle_bk_gym_free(self.h)
+        except Exception:
+            pass
+
+    def reset(self):
+        obs = np.zeros(8)
+        check(bk_lib().oracle_bk_gym_reset(self.h, obs.ctypes.data))
+        return obs
+
+    def fields(self):
+        f = np.zeros(8, dtype=np.int32)
+        bk_lib().oracle_bk_gym_obs_fields(self.h, f.ctypes.data)
+        return f
+
+    def step(self, action):
+        obs = np.zeros(8)
+        r = ctypes.c_double()
+        d = ctypes.c_int()
+        info = np.zeros(15)
+        check(bk_lib().oracle_bk_gym_step(self.h, int(action), obs.ctypes.data, ctypes.byref(r),
+                                          ctypes.byref(d), info.ctypes.data))
+        return obs, r.value, bool(d.value), dict(zip(self.INFO_KEYS, info.tolist()))
+
+
+def bk_loop(k, activations, *, net="clique", n_nodes=3, alpha=0.5, activation_delay=1.0,
+            prop_ev=1.0, scheme=0, policy=-1, rng=None, seed=0, episode=0):
+    """Simulator.loop task for B_k; policy < 0 = all nodes honest."""
+    n = 2 if net == "two-agents" else n_nodes
+    rew = np.zeros(n)
+    acts = np.zeros(n, dtype=np.int64)
+    ht, hp = ctypes.c_double(), ctypes.c_double()
+    hh, hs, nv = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int64()
+    check(bk_lib().oracle_bk_loop(
+        0 if net == "two-agents" else 1, n, alpha, activation_delay, prop_ev,
+        0 if rng is not None else 1, rng.h if rng is not None else None, seed, episode, k,
+        scheme, BK_POLICIES.get(policy, policy), activations, rew.ctypes.data,
+        acts.ctypes.data, ctypes.byref(ht), ctypes.byref(hp), ctypes.byref(hh),
+        ctypes.byref(hs), ctypes.byref(nv)))
+    return dict(reward=rew.tolist(), activations=acts.tolist(), head_time=ht.value,
+                head_progress=hp.value, head_height=hh.value, head_signer=hs.value,
+                n_vertices=nv.value)
