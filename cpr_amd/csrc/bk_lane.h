@@ -1,0 +1,995 @@
+// B_k (parallel proof of work, bk.ml) with the bk_ssz attack space: one episode per lane,
+// as an exact per-lane discrete-event engine.
+//
+// B_k's honest nodes re-run quorum selection on every event they see (bk.ml:297-310):
+// the k smallest own votes, or the leader's smallest own vote plus the earliest-visible
+// foreign votes with larger hashes (bk.ml:233-279), ordered by the OCaml heap sort whose
+// tie order among equal visibility times is semantics (compare.ml:44-62). Fork choice
+// compares heights, confirming-vote counts in the node's view, leader hashes and
+// visibility times (bk.ml:217-231). All of that reads per-node visibility and time of
+// individual votes, so the lane replays the reference's event semantics itself, with the
+// skew-heap tie order of orderedQueue.ml:17-47, like the Ethereum lane.
+//
+// Per-lane memory (one contiguous region per resident lane):
+//   vtx    [cap_v] x 48 B   vertex ring (votes and blocks) indexed by serial & (cap_v-1);
+//                           a stale slot (serial mismatch) marks the lane CPR_ST_CAPACITY
+//   vis    [cap_v][n] u8    per node: kind (invisible/received/released/withheld) + got bit
+//   vt     [cap_v][n] f64   per node: visible_since (simulator.ml:291-294)
+//   quo    [cap_q][k+1] i32 block quorums (tag = block serial, then k vote serials by hash)
+//   drafts [cap_d][k+2] i32 outstanding Append drafts (tag, parent, k votes)
+//   heap   [cap_e] x 24 B   skew-heap nodes of the event queue
+//   tips   [n] i32          defenders' preferred blocks (Honest.state)
+//   scratch                 quorum candidates (keys, serials), share stack
+//
+// Reference map: simulator.ml:122-543 (engine), bk.ml:50-311 (referee, honest node),
+// bk_ssz.ml:148-401 (agent, policies), engine.ml:97-249 (gym step), network.ml
+// selfish_mining / two_agents (links), keyed stream (cpr_stream.h, TAG_MSG link delays).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "cpr_stream.h"
+
+#pragma clang fp contract(off)
+
+namespace cpr {
+namespace bk {
+
+constexpr uint32_t BST_CAPACITY = 32u;  // CPR_ST_CAPACITY
+
+enum : uint32_t { EV_CLOCK = 0, EV_DAG = 1, EV_TX = 2, EV_RX = 3, EV_ON = 4, EV_MV = 5, EV_MDV = 6 };
+enum : uint32_t { KD_APP = 0, KD_POW = 1, KD_NET = 2 };
+enum : uint8_t { V_INV = 0, V_RECV = 1, V_REL = 2, V_WH = 3, V_KIND = 3, V_GOT = 4 };
+enum : int32_t { VF_ALL = 0, VF_MINE = 1, VF_PUBLIC = 2 };
+
+__host__ __device__ inline uint32_t mkev(uint32_t ty, uint32_t node, uint32_t kind) {
+  return ty | (kind << 3) | (node << 5);
+}
+
+struct BVtx {
+  int32_t serial;
+  int32_t parent;  // block parent (votes and blocks); -1 = genesis
+  int32_t height;
+  int32_t vote;    // 1 = Vote, 0 = Block
+  int32_t who;     // vote: miner id; block: signer; -1 = genesis
+  int32_t pow;     // 30-bit hash bits (votes)
+  int32_t rew_att, rew_def;  // rewards of the precursor chain (units of 1)
+  int32_t nconf;   // blocks: confirming votes in the global view (Referee.winner)
+  int32_t qslot;   // blocks: quorum ring slot
+  double time;     // Simulator.timestamp = append time
+};
+static_assert(sizeof(BVtx) == 48, "BVtx layout");
+
+struct HNode {
+  double t;
+  uint32_t ev;
+  int32_t blk;
+  int32_t l, r;
+};
+static_assert(sizeof(HNode) == 24, "HNode layout");
+
+struct BkParams {
+  uint64_t t_att;
+  int32_t d, n;   // defenders, nodes
+  int32_t net;    // 0 selfish mining, 1 two agents
+  int32_t mode;   // 0 gym, 1 loop
+  int32_t policy, scheme, k;
+  int32_t cap_v, cap_q, cap_e, cap_d;
+  int32_t table_dim;
+  double ev, delta, dmax;
+  int64_t max_steps, activations;
+  double max_progress, max_time;
+  const uint8_t* table;  // device pointer (CPR_BK_POLICY_TABLE)
+};
+
+constexpr int32_t NQS = 128;     // quorum candidates per block and list
+constexpr int32_t NSTACK = 1024; // share stack
+
+struct BkMem {
+  BVtx* vtx;
+  uint8_t* vis;
+  double* vt;
+  int32_t* quo;
+  int32_t* drafts;
+  HNode* heap;
+  int32_t* tips;
+  uint64_t* skey;  // [2 * NQS]
+  int32_t* sval;   // [2 * NQS]
+  int32_t* stack;  // [NSTACK]
+};
+
+__host__ __device__ inline int64_t bk_align(int64_t x) { return (x + 127) / 128 * 128; }
+
+__host__ __device__ inline int64_t bk_lane_bytes(const BkParams& P) {
+  return bk_align((int64_t)P.cap_v * 48) + bk_align((int64_t)P.cap_v * P.n) +
+         bk_align((int64_t)P.cap_v * P.n * 8) + bk_align((int64_t)P.cap_q * (P.k + 1) * 4) +
+         bk_align((int64_t)P.cap_d * (P.k + 2) * 4) + bk_align((int64_t)P.cap_e * 24) +
+         bk_align((int64_t)P.n * 4) + bk_align(2 * NQS * 8) + bk_align(2 * NQS * 4) +
+         bk_align(NSTACK * 4);
+}
+
+__host__ __device__ inline BkMem bk_mem_at(uint8_t* base, const BkParams& P) {
+  BkMem M;
+  int64_t o = 0;
+  M.vtx = (BVtx*)(base + o);
+  o += bk_align((int64_t)P.cap_v * 48);
+  M.vis = base + o;
+  o += bk_align((int64_t)P.cap_v * P.n);
+  M.vt = (double*)(base + o);
+  o += bk_align((int64_t)P.cap_v * P.n * 8);
+  M.quo = (int32_t*)(base + o);
+  o += bk_align((int64_t)P.cap_q * (P.k + 1) * 4);
+  M.drafts = (int32_t*)(base + o);
+  o += bk_align((int64_t)P.cap_d * (P.k + 2) * 4);
+  M.heap = (HNode*)(base + o);
+  o += bk_align((int64_t)P.cap_e * 24);
+  M.tips = (int32_t*)(base + o);
+  o += bk_align((int64_t)P.n * 4);
+  M.skey = (uint64_t*)(base + o);
+  o += bk_align(2 * NQS * 8);
+  M.sval = (int32_t*)(base + o);
+  o += bk_align(2 * NQS * 4);
+  M.stack = (int32_t*)(base + o);
+  return M;
+}
+
+// ---- observation and policies (bk_ssz.ml:21-34, 346-401); Action8 ranks
+enum : int32_t { A_ADOPT_PROLONG = 0, A_OVERRIDE_PROLONG = 1, A_MATCH_PROLONG = 2,
+                 A_WAIT_PROLONG = 3, A_ADOPT_PROCEED = 4, A_OVERRIDE_PROCEED = 5,
+                 A_MATCH_PROCEED = 6, A_WAIT_PROCEED = 7 };
+
+struct BkObs {
+  int32_t public_blocks, private_blocks, diff_blocks, public_votes, private_votes_inclusive,
+      private_votes_exclusive, lead, event;  // event: 0 Append, 1 ProofOfWork, 2 Network
+};
+
+__host__ __device__ inline int32_t bk_table_index(const BkObs& o, int32_t D, int32_t k) {
+  auto cl = [](int32_t x, int32_t hi) { return x < 0 ? 0 : (x > hi ? hi : x); };
+  const int32_t K1 = k + 1;
+  return ((((cl(o.public_blocks, D - 1) * D + cl(o.private_blocks, D - 1)) * K1 +
+            cl(o.public_votes, k)) * K1 + cl(o.private_votes_inclusive, k)) * 3) + o.event;
+}
+
+__host__ __device__ inline int32_t bk_policy(const BkParams& P, const BkObs& o) {
+  const int32_t h = o.public_blocks, a = o.private_blocks;
+  switch (P.policy) {
+    case 0:  // honest
+      return h > a ? A_ADOPT_PROCEED : A_OVERRIDE_PROCEED;
+    case 1:  // get-ahead
+      return h > a ? A_ADOPT_PROCEED : (h < a ? A_OVERRIDE_PROCEED : A_WAIT_PROCEED);
+    case 2:  // minor-delay
+      return h > a ? A_ADOPT_PROCEED : (h == 0 ? A_WAIT_PROCEED : A_OVERRIDE_PROCEED);
+    case 3: {  // avoid-loss = avoid_loss_alt (bk_ssz.ml:391-401,411-414)
+      const int32_t hp = h * P.k + o.public_votes, ap = a * P.k + o.private_votes_inclusive;
+      if (h == 0) return A_WAIT_PROCEED;
+      if (h == 1 && hp == ap) return A_MATCH_PROCEED;
+      if (hp > ap) return A_ADOPT_PROCEED;
+      if (hp == ap - 1) return A_OVERRIDE_PROCEED;
+      if (h < a - 10) return A_OVERRIDE_PROCEED;
+      return A_WAIT_PROCEED;
+    }
+    default:  // table
+      return P.table[bk_table_index(o, P.table_dim, P.k)];
+  }
+}
+
+// OCaml stdlib Array.sort (ternary heap sort, not stable) on (key, value) pairs with
+// 64-bit keys (the ethereum lane has the int32 version; see oracle/src/ocaml_sort.h)
+__host__ __device__ inline void ocaml_heap_sort64(int32_t* v, uint64_t* k, int32_t l) {
+  if (l < 2) return;
+  auto maxson = [&](int32_t len, int32_t i) -> int32_t {
+    const int32_t i31 = i + i + i + 1;
+    int32_t x = i31;
+    if (i31 + 2 < len) {
+      if (k[i31] < k[i31 + 1]) x = i31 + 1;
+      if (k[x] < k[i31 + 2]) x = i31 + 2;
+      return x;
+    }
+    if (i31 + 1 < len && k[i31] < k[i31 + 1]) return i31 + 1;
+    if (i31 < len) return i31;
+    return -1;
+  };
+  for (int32_t i = (l + 1) / 3 - 1; i >= 0; --i) {
+    const uint64_t ek = k[i];
+    const int32_t ev = v[i];
+    int32_t p = i;
+    for (;;) {
+      const int32_t j = maxson(l, p);
+      if (j < 0 || !(k[j] > ek)) break;
+      k[p] = k[j];
+      v[p] = v[j];
+      p = j;
+    }
+    k[p] = ek;
+    v[p] = ev;
+  }
+  for (int32_t i = l - 1; i >= 2; --i) {
+    const uint64_t ek = k[i];
+    const int32_t ev = v[i];
+    k[i] = k[0];
+    v[i] = v[0];
+    int32_t p = 0;
+    for (;;) {
+      const int32_t j = maxson(i, p);
+      if (j < 0) break;
+      k[p] = k[j];
+      v[p] = v[j];
+      p = j;
+    }
+    for (;;) {
+      const int32_t father = (p - 1) / 3;
+      if (k[father] < ek) {
+        k[p] = k[father];
+        v[p] = v[father];
+        if (father > 0) {
+          p = father;
+          continue;
+        }
+        k[0] = ek;
+        v[0] = ev;
+        break;
+      }
+      k[p] = ek;
+      v[p] = ev;
+      break;
+    }
+  }
+  const uint64_t tk = k[0];
+  const int32_t tv = v[0];
+  k[0] = k[1];
+  v[0] = v[1];
+  k[1] = tk;
+  v[1] = tv;
+}
+
+// visibility times are finite and >= +0.0, so their IEEE bit patterns order like
+// OCaml's Float.compare on them
+__host__ __device__ inline uint64_t time_key(double t) { return bitsd(t); }
+
+struct BkLane {
+  double now;
+  int32_t c_act, newest, nblk, act0;
+  int32_t hroot, hfree, hused;
+  uint32_t status;
+  int32_t dead;  // capacity exceeded: 1 vertex ring, 2 event heap, 3 quorum list, 4 drafts,
+                 // 5 share stack, 6 queue drained, 7 quorum ring, 8 zero-time append loop
+  int32_t zt;    // appends since the last activation (loop-mode guard, see append_block)
+  int32_t dseq;  // Append drafts issued
+  // bk_ssz agent (BetweenActions + Observable)
+  int32_t pub, priv, pending;
+  int32_t o_pub, o_priv, o_common, o_event;
+  int64_t steps;
+
+  // ------------------------------------------------------------------ storage
+  __host__ __device__ inline void fail(int32_t why) {
+    status |= BST_CAPACITY;
+    if (!dead) dead = why;
+  }
+  __host__ __device__ inline BVtx& X(const BkParams& P, const BkMem& M, int32_t s) {
+    BVtx& b = M.vtx[s & (P.cap_v - 1)];
+    if (b.serial != s) fail(1);
+    return b;
+  }
+  __host__ __device__ inline uint8_t& V(const BkParams& P, const BkMem& M, int32_t s,
+                                        int32_t node) {
+    return M.vis[(int64_t)(s & (P.cap_v - 1)) * P.n + node];
+  }
+  __host__ __device__ inline double& VT(const BkParams& P, const BkMem& M, int32_t s,
+                                        int32_t node) {
+    return M.vt[(int64_t)(s & (P.cap_v - 1)) * P.n + node];
+  }
+  __host__ __device__ inline bool visible(const BkParams& P, const BkMem& M, int32_t s,
+                                          int32_t node) {
+    return (V(P, M, s, node) & V_KIND) != V_INV;
+  }
+  __host__ __device__ inline int32_t* Q(const BkParams& P, const BkMem& M, const BVtx& b) {
+    int32_t* q = M.quo + (int64_t)(b.qslot & (P.cap_q - 1)) * (P.k + 1);
+    if (q[0] != b.serial) fail(7);
+    return q + 1;
+  }
+  __host__ __device__ static inline bool keep(uint8_t v, int32_t vf) {
+    const uint8_t kd = v & V_KIND;
+    return vf == VF_ALL || (vf == VF_MINE ? (kd == V_WH || kd == V_REL)
+                                          : (kd == V_REL || kd == V_RECV));
+  }
+
+  // ------------------------------------------------------------------ event queue
+  // orderedQueue.ml:17-47 as an in-place skew heap. Events at +inf (messages that never
+  // arrive, gamma = 0) are stored too: every insertion swaps children along its path, so
+  // they shape the pop order of equal-time events even though they never pop in a gym
+  // episode (B_k is sensitive to that order: which same-instant Append lands first).
+  __host__ __device__ inline int32_t halloc(const BkParams& P, const BkMem& M) {
+    int32_t i;
+    if (hfree >= 0) {
+      i = hfree;
+      hfree = M.heap[i].l;
+    } else if (hused < P.cap_e) {
+      i = hused++;
+    } else {
+      fail(2);
+      return -1;
+    }
+    return i;
+  }
+  __host__ __device__ inline void push(const BkParams& P, const BkMem& M, double t, uint32_t ev,
+                                       int32_t blk) {
+    int32_t parent = -1, node = hroot;
+    for (;;) {
+      if (node < 0) {
+        const int32_t a = halloc(P, M);
+        if (a < 0) return;
+        HNode& h = M.heap[a];
+        h.t = t;
+        h.ev = ev;
+        h.blk = blk;
+        h.l = -1;
+        h.r = -1;
+        if (parent < 0)
+          hroot = a;
+        else
+          M.heap[parent].l = a;
+        return;
+      }
+      HNode& h = M.heap[node];
+      if (t < h.t) {
+        const double ot = h.t;
+        const uint32_t oe = h.ev;
+        const int32_t ob = h.blk;
+        h.t = t;
+        h.ev = ev;
+        h.blk = blk;
+        t = ot;
+        ev = oe;
+        blk = ob;
+      } else {
+        const int32_t tmp = h.l;
+        h.l = h.r;
+        h.r = tmp;
+      }
+      parent = node;
+      node = h.l;
+    }
+  }
+  __host__ __device__ inline bool pop(const BkMem& M, double* t, uint32_t* ev, int32_t* blk) {
+    if (hroot < 0) return false;
+    *t = M.heap[hroot].t;
+    *ev = M.heap[hroot].ev;
+    *blk = M.heap[hroot].blk;
+    int32_t parent = -1, side = 0, node = hroot;
+    for (;;) {
+      const int32_t l = M.heap[node].l, r = M.heap[node].r;
+      int32_t repl = -2;
+      if (r < 0)
+        repl = l;
+      else if (l < 0)
+        repl = r;
+      if (repl != -2) {
+        if (parent < 0)
+          hroot = repl;
+        else if (side == 0)
+          M.heap[parent].l = repl;
+        else
+          M.heap[parent].r = repl;
+        M.heap[node].l = hfree;
+        hfree = node;
+        return true;
+      }
+      const int32_t c = (M.heap[l].t <= M.heap[r].t) ? l : r;
+      M.heap[node].t = M.heap[c].t;
+      M.heap[node].ev = M.heap[c].ev;
+      M.heap[node].blk = M.heap[c].blk;
+      parent = node;
+      side = c == l ? 0 : 1;
+      node = c;
+    }
+  }
+  __host__ __device__ inline void push_now(const BkParams& P, const BkMem& M, uint32_t ev,
+                                           int32_t blk) {
+    push(P, M, now, ev, blk);
+  }
+
+  // ------------------------------------------------------------------ randomness
+  __host__ __device__ inline int32_t miner_of(const BkParams& P, const Stream& S, int32_t j) {
+    const Words4 w = S.block((uint32_t)j, TAG_ACT);
+    if ((uint64_t)w.w0 < P.t_att) return 0;
+    return 1 + (int32_t)(((uint64_t)w.w1 * (uint64_t)P.d) >> 32);
+  }
+  __host__ __device__ inline void schedule_pow(const BkParams& P, const Stream& S,
+                                               const BkMem& M) {
+    const Words4 w = S.block((uint32_t)c_act, TAG_ACT);
+    push(P, M, now + (-1.0 * P.ev) * cpr_log(u53(w.w2, w.w3)), mkev(EV_CLOCK, 0, KD_POW), -1);
+  }
+
+  // ------------------------------------------------------------------ DAG
+  __host__ __device__ inline void init_vertex(const BkParams& P, const BkMem& M, BVtx& b,
+                                              int32_t s) {
+    b.serial = s;
+    b.nconf = 0;
+    b.qslot = -1;
+    b.time = now;
+    for (int32_t j = 0; j < P.n; ++j) V(P, M, s, j) = V_INV;
+  }
+  // vote: simulator.ml:122-136 (pow = (bits, serial)), bk.ml:281-286 payload
+  __host__ __device__ inline int32_t append_vote(const BkParams& P, const Stream& S,
+                                                 const BkMem& M, int32_t node, int32_t parent) {
+    BVtx& p = X(P, M, parent);
+    const int32_t s = ++newest;
+    BVtx& b = M.vtx[s & (P.cap_v - 1)];
+    init_vertex(P, M, b, s);
+    b.parent = parent;
+    b.height = p.height;
+    b.vote = 1;
+    b.who = node;
+    b.pow = (int32_t)(S.block((uint32_t)s, TAG_POW).w0 & 0x3FFFFFFFu);
+    b.rew_att = p.rew_att;  // precursor = the block; votes carry no reward (bk.ml:151-176)
+    b.rew_def = p.rew_def;
+    p.nconf += 1;
+    return s;
+  }
+  // block from an Append draft (bk.ml:288-295), set_rewards (simulator.ml:377-388)
+  __host__ __device__ inline int32_t append_block(const BkParams& P, const BkMem& M,
+                                                  int32_t node, int32_t dseq_) {
+    const int32_t* dr = M.drafts + (int64_t)(dseq_ & (P.cap_d - 1)) * (P.k + 2);
+    if (dr[0] != dseq_) {
+      fail(4);
+      return 0;
+    }
+    // guard (not in the reference): in loop mode an attacker policy that keeps adopting
+    // re-proposes on the same block at the same instant forever (Simulator.loop has no
+    // step bound); stop such a lane after 4096 appends without an activation
+    if (P.mode == 1 && ++zt > 4096) {
+      fail(8);
+      return 0;
+    }
+    BVtx& p = X(P, M, dr[1]);
+    int32_t ra = p.rew_att, rd = p.rew_def;
+    const int32_t ph = p.height;
+    const int32_t s = ++newest;
+    const int32_t qs = nblk++;
+    int32_t* q = M.quo + (int64_t)(qs & (P.cap_q - 1)) * (P.k + 1);
+    q[0] = s;
+    for (int32_t i = 0; i < P.k; ++i) {
+      const int32_t v = dr[2 + i];
+      q[1 + i] = v;
+      if (P.scheme == 0) {  // Constant: 1 per confirmed vote to its miner
+        if (X(P, M, v).who == 0)
+          ++ra;
+        else
+          ++rd;
+      }
+    }
+    if (P.scheme != 0) {  // Block: k to the signer
+      if (node == 0)
+        ra += P.k;
+      else
+        rd += P.k;
+    }
+    BVtx& b = M.vtx[s & (P.cap_v - 1)];
+    init_vertex(P, M, b, s);
+    b.parent = dr[1];
+    b.height = ph + 1;
+    b.vote = 0;
+    b.who = node;
+    b.pow = 0;
+    b.rew_att = ra;
+    b.rew_def = rd;
+    b.qslot = qs;
+    return s;
+  }
+
+  // ------------------------------------------------------------------ honest node views
+  // pow hashes (bits, serial) as one ordered key; max_pow = all ones
+  __host__ __device__ static inline uint64_t pow_key(const BVtx& v) {
+    return ((uint64_t)(uint32_t)v.pow << 32) | (uint32_t)v.serial;
+  }
+  // Honest.leader_hash_exn (bk.ml:205-215): the block's first quorum vote
+  __host__ __device__ inline uint64_t leader_key(const BkParams& P, const BkMem& M, int32_t b) {
+    const BVtx& x = X(P, M, b);
+    if (x.parent < 0) return ~0ull;
+    return pow_key(X(P, M, Q(P, M, x)[0]));
+  }
+  // confirming votes of block b visible at `node` that pass `vf` (children scan, newest
+  // first: only vertices appended after b can be its children)
+  __host__ __device__ inline int32_t confirming(const BkParams& P, const BkMem& M, int32_t b,
+                                                int32_t node, int32_t vf) {
+    int32_t n = 0;
+    for (int32_t c = newest; c > b && !dead; --c) {
+      const uint8_t v = V(P, M, c, node);
+      if ((v & V_KIND) == V_INV || !keep(v, vf)) continue;
+      const BVtx& x = X(P, M, c);
+      n += (x.vote && x.parent == b) ? 1 : 0;
+    }
+    return n;
+  }
+  // bk.ml:217-226 (skip_eq; by height; by #votes; by neg leader hash; by neg visible_since)
+  __host__ __device__ inline int32_t compare_blocks(const BkParams& P, const BkMem& M,
+                                                    int32_t node, int32_t vf, int32_t a,
+                                                    int32_t b) {
+    if (a == b) return 0;
+    const int32_t ha = X(P, M, a).height, hb = X(P, M, b).height;
+    if (ha != hb) return ha < hb ? -1 : 1;
+    const int32_t ca = confirming(P, M, a, node, vf), cb = confirming(P, M, b, node, vf);
+    if (ca != cb) return ca < cb ? -1 : 1;
+    const uint64_t la = leader_key(P, M, a), lb = leader_key(P, M, b);
+    if (la != lb) return lb < la ? -1 : 1;
+    const double ta = VT(P, M, a, node), tb = VT(P, M, b, node);
+    return tb < ta ? -1 : (tb > ta ? 1 : 0);
+  }
+  __host__ __device__ inline int32_t update_head(const BkParams& P, const BkMem& M,
+                                                 int32_t node, int32_t vf, int32_t old,
+                                                 int32_t cand) {
+    return compare_blocks(P, M, node, vf, cand, old) > 0 ? cand : old;
+  }
+
+  // Honest.quorum + propose (bk.ml:233-295) at `node`; returns the draft sequence number
+  // (written to the draft ring) or -1
+  __host__ __device__ inline int32_t propose(const BkParams& P, const BkMem& M, int32_t node,
+                                             int32_t vf, int32_t b) {
+    uint64_t* mk = M.skey;        // mine: keys / serials, scan order (newest first)
+    int32_t* mv = M.sval;
+    uint64_t* tk = M.skey + NQS;  // theirs
+    int32_t* tv = M.sval + NQS;
+    int32_t nmine = 0, ntheirs = 0;
+    uint64_t my_hash = ~0ull;
+    for (int32_t c = newest; c > b && !dead; --c) {
+      const uint8_t v = V(P, M, c, node);
+      if ((v & V_KIND) == V_INV || !keep(v, vf)) continue;
+      const BVtx& x = X(P, M, c);
+      if (!x.vote || x.parent != b) continue;
+      const uint64_t key = pow_key(x);
+      if (x.who == node) {
+        if (nmine >= NQS) {
+          fail(3);
+          return -1;
+        }
+        my_hash = key < my_hash ? key : my_hash;
+        mk[nmine] = key;
+        mv[nmine++] = c;
+      } else {
+        if (ntheirs >= NQS) {
+          fail(3);
+          return -1;
+        }
+        tk[ntheirs] = key;
+        tv[ntheirs++] = c;
+      }
+    }
+    if (dead || nmine == 0 || nmine + ntheirs < P.k) return -1;  // fast path (bk.ml:254)
+    const int32_t seq = dseq++;
+    int32_t* dr = M.drafts + (int64_t)(seq & (P.cap_d - 1)) * (P.k + 2);
+    dr[0] = seq;
+    dr[1] = b;
+    int32_t* q = dr + 2;
+    int32_t nq = 0;
+    if (nmine >= P.k) {
+      // Compare.first (by compare_pow) k mine: the k smallest hashes (unique keys)
+      for (int32_t i = 0; i < nmine; ++i) {
+        int32_t rank = 0;
+        for (int32_t j = 0; j < nmine; ++j) rank += mk[j] < mk[i] ? 1 : 0;
+        if (rank < P.k) q[rank] = mv[i];
+      }
+      return seq;
+    }
+    // theirs with hash > my_hash, in children order (the list rebuilt by two prepending
+    // folds keeps it), then the k - nmine earliest visible by Array.sort on visible_since
+    int32_t n2 = 0;
+    for (int32_t i = 0; i < ntheirs; ++i) {
+      if (tk[i] > my_hash) {
+        tv[n2] = tv[i];
+        tk[n2] = time_key(VT(P, M, tv[i], node));
+        ++n2;
+      }
+    }
+    if (n2 < P.k - nmine) {
+      dseq--;  // no draft after all
+      return -1;
+    }
+    ocaml_heap_sort64(tv, tk, n2);
+    // mine @ first (k - nmine) theirs, then List.sort by pow hash (unique keys)
+    for (int32_t i = 0; i < nmine; ++i) q[nq++] = mv[i];
+    for (int32_t i = 0; i < P.k - nmine; ++i) q[nq++] = tv[i];
+    for (int32_t i = 1; i < nq; ++i) {
+      const int32_t s = q[i];
+      const uint64_t ks = pow_key(X(P, M, s));
+      int32_t j = i;
+      while (j > 0 && pow_key(X(P, M, q[j - 1])) > ks) {
+        q[j] = q[j - 1];
+        --j;
+      }
+      q[j] = s;
+    }
+    return seq;
+  }
+
+  // ------------------------------------------------------------------ actions
+  // Simulator.handle_action share part (simulator.ml:401-419): recursive release of
+  // withheld vertices, parents in order (block: parent block, then its quorum)
+  __host__ __device__ inline void share(const BkParams& P, const BkMem& M, int32_t node,
+                                        int32_t s0) {
+    int32_t* st = M.stack;
+    int32_t sp = 0;
+    st[sp++] = s0;
+    while (sp > 0 && !dead) {
+      const int32_t s = st[--sp];
+      uint8_t& v = V(P, M, s, node);
+      if ((v & V_KIND) != V_WH) continue;  // received / released: nothing
+      v = (uint8_t)((v & ~V_KIND) | V_REL);
+      push_now(P, M, mkev(EV_TX, node, KD_NET), s);
+      const BVtx& b = X(P, M, s);
+      if (b.parent < 0) continue;
+      const int32_t np = b.vote ? 1 : P.k + 1;
+      if (sp + np > NSTACK) {
+        fail(5);
+        return;
+      }
+      if (!b.vote) {
+        const int32_t* q = Q(P, M, b);
+        for (int32_t i = P.k - 1; i >= 0; --i) st[sp++] = q[i];
+      }
+      st[sp++] = b.parent;
+    }
+  }
+
+  // ------------------------------------------------------------------ agent (bk_ssz.ml)
+  __host__ __device__ inline void agent_init(int32_t root) {
+    pub = priv = root;
+    pending = -1;
+  }
+  __host__ __device__ inline int32_t last_block(const BkParams& P, const BkMem& M, int32_t x) {
+    const BVtx& b = X(P, M, x);
+    return b.vote ? b.parent : x;
+  }
+  // bk_ssz.ml:196-221; the pending share list is [block; votes of block], whose
+  // last_blocks all equal `block`, so folding update_head over it equals one update
+  __host__ __device__ inline void prepare(const BkParams& P, const BkMem& M, uint32_t kind,
+                                          int32_t x) {
+    int32_t p = pub;
+    if (pending >= 0) p = update_head(P, M, 0, VF_PUBLIC, p, pending);
+    int32_t q = priv;
+    if (kind == KD_APP) {
+      q = x;
+      o_event = 0;
+    } else if (kind == KD_POW) {
+      o_event = 1;
+    } else {
+      p = update_head(P, M, 0, VF_PUBLIC, p, last_block(P, M, x));
+      o_event = 2;
+    }
+    o_pub = p;
+    o_priv = q;
+    // Dagtools.common_ancestor over the vertex DAG; its last_block is the deepest common
+    // block of the two block chains
+    int32_t a = p, b = q;
+    while (a != b && !dead) {
+      const int32_t ha = X(P, M, a).height, hb = X(P, M, b).height;
+      if (ha >= hb) a = X(P, M, a).parent;
+      if (hb >= ha) b = X(P, M, b).parent;
+      if (a < 0 || b < 0) {
+        fail(1);
+        break;
+      }
+    }
+    o_common = a;
+  }
+  // bk_ssz.ml:225-263
+  __host__ __device__ inline BkObs observe(const BkParams& P, const BkMem& M) {
+    BkObs o;
+    const int32_t ca = X(P, M, o_common).height;
+    const int32_t ph = X(P, M, o_priv).height, qh = X(P, M, o_pub).height;
+    o.public_blocks = qh - ca;
+    o.private_blocks = ph - ca;
+    o.diff_blocks = ph - qh;
+    o.public_votes = confirming(P, M, o_pub, 0, VF_PUBLIC);
+    o.private_votes_inclusive = 0;
+    o.private_votes_exclusive = 0;
+    for (int32_t c = newest; c > o_priv && !dead; --c) {
+      const uint8_t v = V(P, M, c, 0);
+      if ((v & V_KIND) == V_INV) continue;
+      const BVtx& x = X(P, M, c);
+      if (!x.vote || x.parent != o_priv) continue;
+      ++o.private_votes_inclusive;
+      o.private_votes_exclusive += keep(v, VF_MINE) ? 1 : 0;
+    }
+    // `lead` compares the signature of the lowest-hash vote with my_id; votes are never
+    // signed (bk.ml:281-286), so it is always false in the reference
+    o.lead = 0;
+    o.event = o_event;
+    return o;
+  }
+  // bk_ssz.ml:265-331 (share + append through handle_action order: shares, then appends)
+  __host__ __device__ inline void apply(const BkParams& P, const BkMem& M, int32_t action) {
+    const int32_t kind = action & 3;  // 0 Adopt, 1 Override, 2 Match, 3 Wait
+    int32_t np = kind == 0 ? o_pub : o_priv;
+    int32_t rel = -1;
+    if (kind == 1 || kind == 2) {
+      int32_t height = X(P, M, o_pub).height;
+      int32_t nvotes = confirming(P, M, o_pub, 0, VF_PUBLIC);
+      if (kind == 1) {
+        if (nvotes >= P.k) {
+          height += 1;
+          nvotes = 0;
+        } else {
+          nvotes += 1;
+        }
+      }
+      int32_t block = o_priv;
+      while (!dead && X(P, M, block).height > height) block = X(P, M, block).parent;
+      if (nvotes >= P.k) {
+        for (int32_t c = newest; c > block && !dead; --c) {
+          if (!visible(P, M, c, 0)) continue;
+          const BVtx& x = X(P, M, c);
+          if (!x.vote && x.parent == block) {
+            block = c;  // newest visible child block (the attacker's proposal, if any)
+            nvotes = 0;
+            break;
+          }
+        }
+      }
+      // votes confirming `block` in children order; Compare.first by visible_since
+      uint64_t* vk = M.skey;
+      int32_t* vv = M.sval;
+      int32_t nv = 0;
+      for (int32_t c = newest; c > block && !dead; --c) {
+        if (!visible(P, M, c, 0)) continue;
+        const BVtx& x = X(P, M, c);
+        if (!x.vote || x.parent != block) continue;
+        if (nv >= 2 * NQS) {
+          fail(3);
+          break;
+        }
+        vk[nv] = time_key(VT(P, M, c, 0));
+        vv[nv++] = c;
+      }
+      int32_t take = nv;
+      if (nv >= nvotes) {
+        ocaml_heap_sort64(vv, vk, nv);
+        take = nvotes;
+      }
+      share(P, M, 0, block);
+      // share() reuses no scratch, so vv survives
+      for (int32_t i = 0; i < take && !dead; ++i) share(P, M, 0, vv[i]);
+      rel = block;
+    }
+    const int32_t d = propose(P, M, 0, action >= 4 ? VF_ALL : VF_MINE, np);
+    if (d >= 0) push_now(P, M, mkev(EV_DAG, 0, KD_APP), d);
+    pub = o_pub;
+    priv = np;
+    pending = rel;
+  }
+
+  // ------------------------------------------------------------------ engine
+  __host__ __device__ inline void init(const BkParams& P, const Stream& S, const BkMem& M) {
+    now = 0.0;
+    c_act = 0;
+    newest = 0;
+    nblk = 0;
+    act0 = 0;
+    hroot = -1;
+    hfree = -1;
+    hused = 0;
+    status = 0u;
+    dead = 0;
+    dseq = 0;
+    zt = 0;
+    steps = 0;
+    BVtx& r = M.vtx[0];
+    r.serial = 0;
+    r.parent = -1;
+    r.height = 0;
+    r.vote = 0;
+    r.who = -1;
+    r.pow = 0;
+    r.rew_att = r.rew_def = 0;
+    r.nconf = 0;
+    r.qslot = -1;
+    r.time = 0.0;
+    for (int32_t j = 0; j < P.n; ++j) {
+      V(P, M, 0, j) = V_RECV | V_GOT;
+      VT(P, M, 0, j) = 0.0;
+      M.tips[j] = 0;
+    }
+    agent_init(0);
+    schedule_pow(P, S, M);
+  }
+
+  // Honest.handler (bk.ml:297-310) at defender `node` for vertex x
+  __host__ __device__ inline void honest(const BkParams& P, const BkMem& M, int32_t node,
+                                         int32_t x) {
+    const int32_t b = last_block(P, M, x);
+    const int32_t d = propose(P, M, node, VF_ALL, b);
+    if ((V(P, M, x, node) & V_KIND) == V_WH) share(P, M, node, x);
+    M.tips[node] = update_head(P, M, node, VF_ALL, M.tips[node], b);
+    if (d >= 0) push_now(P, M, mkev(EV_DAG, node, KD_APP), d);
+  }
+
+  // one popped event that is not the attacker's gym interaction (simulator.ml:421-508)
+  __host__ __device__ inline void handle(const BkParams& P, const Stream& S, const BkMem& M,
+                                         uint32_t ev, int32_t s) {
+    const uint32_t ty = ev & 7u, kind = (ev >> 3) & 3u;
+    const int32_t node = (int32_t)(ev >> 5);
+    switch (ty) {
+      case EV_MV: {
+        uint8_t& v = V(P, M, s, node);
+        if ((v & V_KIND) != V_INV) break;
+        const BVtx& b = X(P, M, s);
+        bool ok = b.parent < 0 || visible(P, M, b.parent, node);
+        if (ok && !b.vote) {
+          const int32_t* q = Q(P, M, b);
+          for (int32_t i = 0; i < P.k && ok; ++i) ok = visible(P, M, q[i], node);
+        }
+        if (!ok) break;
+        v = (uint8_t)((v & ~V_KIND) | (kind == KD_NET ? V_RECV : V_WH));
+        VT(P, M, s, node) = now;
+        push_now(P, M, mkev(EV_ON, node, kind), s);
+        push_now(P, M, mkev(EV_MDV, node, kind), s);
+        break;
+      }
+      case EV_ON: {
+        if (node == 0) {
+          // loop mode: the attacker node's handler (bk_ssz.ml:334-343)
+          prepare(P, M, kind, s);
+          apply(P, M, bk_policy(P, observe(P, M)));
+          break;
+        }
+        honest(P, M, node, s);
+        break;
+      }
+      case EV_CLOCK: {
+        zt = 0;
+        const int32_t m = miner_of(P, S, c_act);
+        int32_t parent;
+        if (m == 0) {
+          ++act0;
+          parent = priv;  // gym: replaced at the Dag event (engine.ml:112-116)
+        } else {
+          parent = M.tips[m];
+        }
+        push_now(P, M, mkev(EV_DAG, m, KD_POW), parent);
+        ++c_act;
+        schedule_pow(P, S, M);
+        break;
+      }
+      case EV_DAG: {
+        const int32_t v = kind == KD_POW ? append_vote(P, S, M, node, s)
+                                         : append_block(P, M, node, s);
+        push_now(P, M, mkev(EV_MV, node, kind), v);
+        break;
+      }
+      case EV_TX: {
+        for (int32_t dst = 0; dst < P.n; ++dst) {
+          if (dst == node) continue;
+          double delay;
+          if (P.net == 1)
+            delay = 0.0;
+          else if (node == 0)
+            delay = S.msg_u((uint32_t)s, (uint32_t)dst) * (P.dmax - 0.0) + 0.0;
+          else
+            delay = dst == 0 ? 0.0 : P.delta;
+          push(P, M, now + delay, mkev(EV_RX, dst, KD_NET), s);
+        }
+        break;
+      }
+      case EV_RX: {
+        // simulator.ml:488-493: `now < received_at` with received_at = +inf until the
+        // first receipt, so a delivery at t = +inf (Simulator.loop draining gamma = 0
+        // messages) changes nothing
+        if (!(now < __builtin_inf())) break;
+        uint8_t& v = V(P, M, s, node);
+        if (!(v & V_GOT)) {
+          v |= V_GOT;
+          push_now(P, M, mkev(EV_MV, node, KD_NET), s);
+        }
+        break;
+      }
+      case EV_MDV: {
+        // children (newest first) already received at this node become visible: votes and
+        // blocks on block s, or blocks whose quorum holds vote s
+        const bool is_vote = X(P, M, s).vote != 0;
+        for (int32_t c = newest; c > s && !dead; --c) {
+          if (!(V(P, M, c, node) & V_GOT)) continue;
+          const BVtx& cb = X(P, M, c);
+          bool child = cb.parent == s;
+          if (!child && is_vote && !cb.vote) {
+            const int32_t* q = Q(P, M, cb);
+            for (int32_t i = 0; i < P.k; ++i) child |= q[i] == s;
+          }
+          if (child) push_now(P, M, mkev(EV_MV, node, KD_NET), c);
+        }
+        break;
+      }
+    }
+  }
+
+  // engine.ml:108-121
+  __host__ __device__ inline bool skip_to_interaction(const BkParams& P, const Stream& S,
+                                                      const BkMem& M, uint32_t* kind,
+                                                      int32_t* blk) {
+    double t;
+    uint32_t ev;
+    int32_t s;
+    while (!dead) {
+      if (!pop(M, &t, &ev, &s)) {
+        fail(6);
+        return false;
+      }
+      now = t;
+      const uint32_t ty = ev & 7u;
+      const int32_t node = (int32_t)(ev >> 5);
+      const uint32_t kd = (ev >> 3) & 3u;
+      if (ty == EV_ON && node == 0) {
+        *kind = kd;
+        *blk = s;
+        return true;
+      }
+      if (ty == EV_DAG && node == 0 && kd == KD_POW) {
+        const int32_t v = append_vote(P, S, M, 0, priv);
+        push_now(P, M, mkev(EV_MV, 0, KD_POW), v);
+        continue;
+      }
+      handle(P, S, M, ev, s);
+    }
+    return false;
+  }
+
+  // Referee.winner over [attacker preference; defenders' tips] (bk.ml:134-147): height,
+  // then confirming votes in the global view
+  __host__ __device__ inline int32_t head(const BkParams& P, const BkMem& M, int32_t att) {
+    int32_t h = att;
+    int32_t hh = X(P, M, att).height, hc = X(P, M, att).nconf;
+    for (int32_t j = 1; j < P.n; ++j) {
+      const int32_t t = M.tips[j];
+      if (t == h) continue;
+      const BVtx& x = X(P, M, t);
+      if (x.height > hh || (x.height == hh && x.nconf > hc)) {
+        h = t;
+        hh = x.height;
+        hc = x.nconf;
+      }
+    }
+    return h;
+  }
+
+  // gym: reset (engine.ml:122-170)
+  __host__ __device__ inline void gym_reset(const BkParams& P, const Stream& S, const BkMem& M) {
+    init(P, S, M);
+    uint32_t kind;
+    int32_t b;
+    if (skip_to_interaction(P, S, M, &kind, &b)) prepare(P, M, kind, b);
+  }
+
+  // gym: step (engine.ml:176-249); returns the head, sets *done
+  __host__ __device__ inline int32_t gym_step(const BkParams& P, const Stream& S,
+                                              const BkMem& M, int32_t action, bool* done) {
+    apply(P, M, action);
+    ++steps;
+    uint32_t kind;
+    int32_t b;
+    const int32_t att = priv;
+    if (skip_to_interaction(P, S, M, &kind, &b)) prepare(P, M, kind, b);
+    const int32_t hd = head(P, M, att);
+    const double progress = (double)(X(P, M, hd).height * P.k);
+    *done = dead || !(steps < P.max_steps && progress < P.max_progress && now < P.max_time);
+    return hd;
+  }
+
+  // loop: Simulator.loop ~activations (simulator.ml:519-533), then the head
+  __host__ __device__ inline int32_t loop(const BkParams& P, const Stream& S, const BkMem& M) {
+    init(P, S, M);
+    int64_t left = P.activations;
+    double t;
+    uint32_t ev;
+    int32_t s;
+    while (!dead && pop(M, &t, &ev, &s)) {
+      now = t;
+      if ((ev & 7u) == EV_CLOCK) {
+        if (left <= 0) continue;
+        --left;
+      }
+      handle(P, S, M, ev, s);
+    }
+    return head(P, M, priv);
+  }
+};
+
+}  // namespace bk
+}  // namespace cpr

@@ -65,6 +65,10 @@ struct cpr_batch {
   eth::EthParams EP;     // CPR_PROTO_ETHEREUM
   DevBuf eth_mem;        // lanes x eth_lane_bytes
   int64_t eth_bytes = 0;
+  bk::BkParams BP;       // CPR_PROTO_BK
+  DevBuf bk_mem;         // fused episodes: lanes x bk_bytes
+  DevBuf bk_lmem, bk_slots;  // lockstep lanes: n_lanes x bk_bytes, n_lanes slots
+  int64_t bk_bytes = 0;
   std::vector<uint8_t> table_host;
   DevBuf table_dev, tabs_dev;  // policy table; unit-observation tables
   DevBuf spill, tlog, replay, summary, records;
@@ -142,8 +146,11 @@ static int32_t pow2_at_least(int64_t x, int32_t cap) {
 // engine.ml:37-51 and network.ml:343-358 (messages kept verbatim)
 static int validate_eth(const cpr_config* c, eth::EthParams* P);
 
-static int validate(const cpr_config* c, NakParams* P, eth::EthParams* EP) {
+static int validate_bk(const cpr_config* c, bk::BkParams* P);
+
+static int validate(const cpr_config* c, NakParams* P, eth::EthParams* EP, bk::BkParams* BP) {
   if (c->protocol == CPR_PROTO_ETHEREUM) return validate_eth(c, EP);
+  if (c->protocol == CPR_PROTO_BK) return validate_bk(c, BP);
   if (c->protocol != CPR_PROTO_NAKAMOTO)
     return fail(CPR_E_UNSUPPORTED, "protocol not implemented on the device yet");
   if (std::isnan(c->activation_delay)) return fail(CPR_E_INVALID_ARG, "activation_delay cannot be NaN");
@@ -277,7 +284,95 @@ static int validate_eth(const cpr_config* c, eth::EthParams* P) {
   int32_t cb = 64;
   while (cb < span && cb < (1 << 15)) cb <<= 1;
   P->cap_b = cb;
-  P->cap_e = 64 + 512 * P->n;
+  // gamma = 0: messages at t = +inf stay in the skew heap (they shape its tie order)
+  P->cap_e = 64 + 512 * P->n +
+             (std::isfinite(P->dmax) ? 0 : (int32_t)(2 * P->d * std::min<int64_t>(span, 8192)));
+  return CPR_OK;
+}
+
+// B_k: engine.ml:37-51 checks shared with Nakamoto, network.ml:343-358, bk.ml k >= 1,
+// Constant / Block rewards, bk_ssz policies 0..3 or a table
+static int validate_bk(const cpr_config* c, bk::BkParams* P) {
+  if (std::isnan(c->activation_delay)) return fail(CPR_E_INVALID_ARG, "activation_delay cannot be NaN");
+  if (std::isnan(c->alpha)) return fail(CPR_E_INVALID_ARG, "alpha cannot be NaN");
+  if (std::isnan(c->gamma)) return fail(CPR_E_INVALID_ARG, "gamma cannot be NaN");
+  if (c->alpha < 0. || c->alpha > 1.) return fail(CPR_E_INVALID_ARG, "alpha < 0 || alpha > 1");
+  if (c->gamma < 0. || c->gamma > 1.) return fail(CPR_E_INVALID_ARG, "gamma < 0 || gamma > 1");
+  if (c->activation_delay <= 0.) return fail(CPR_E_INVALID_ARG, "activation_delay <= 0");
+  if (c->mode != CPR_MODE_GYM && c->mode != CPR_MODE_LOOP)
+    return fail(CPR_E_INVALID_ARG, "unknown mode");
+  if (c->k < 1) return fail(CPR_E_INVALID_ARG, "k must be positive");
+  if (c->k > 64) return fail(CPR_E_UNSUPPORTED, "device lanes support k <= 64");
+  if (c->reward_scheme != CPR_REWARD_CONSTANT && c->reward_scheme != CPR_REWARD_BLOCK)
+    return fail(CPR_E_INVALID_ARG, "'" + std::to_string(c->reward_scheme) +
+                                       "' is not a valid parameter choice, try 'block' or 'constant'");
+  if (c->policy < CPR_BK_POLICY_HONEST || c->policy > CPR_BK_POLICY_TABLE)
+    return fail(CPR_E_INVALID_ARG, "unknown policy");
+  memset(P, 0, sizeof(*P));
+  if (c->policy == CPR_BK_POLICY_TABLE) {
+    const int64_t D = c->policy_table_dim;
+    if (!c->policy_table || D <= 0 || D > 64)
+      return fail(CPR_E_INVALID_ARG, "policy table missing or dim out of range (1..64)");
+    const int64_t sz = D * D * (c->k + 1) * (c->k + 1) * 3;
+    for (int64_t i = 0; i < sz; i++)
+      if (c->policy_table[i] > 7) return fail(CPR_E_INVALID_ARG, "policy table action out of range");
+    P->table_dim = (int32_t)D;
+  }
+  P->ev = c->activation_delay;
+  P->t_att = alpha_threshold(c->alpha);
+  P->policy = c->policy;
+  P->scheme = c->reward_scheme;
+  P->mode = c->mode;
+  P->k = c->k;
+  if (c->network == CPR_NET_SELFISH_MINING) {
+    if (c->defenders < 1) return fail(CPR_E_INVALID_ARG, "defenders < 0");
+    if (c->defenders < 2) return fail(CPR_E_INVALID_ARG, "defenders must be at least 2");
+    if (c->defenders > 64)
+      return fail(CPR_E_UNSUPPORTED, "device lanes support at most 64 defenders");
+    const double dd = (double)c->defenders;
+    if (c->gamma > (dd - 1.) / dd)
+      return fail(CPR_E_INVALID_ARG, "gamma must not be greater ( (defenders - 1) / defenders )");
+    const double prop = c->propagation_delay > 0 ? c->propagation_delay : 1e-9;
+    P->d = c->defenders;
+    P->net = 0;
+    P->delta = prop;
+    P->dmax = (dd - 1.) / dd * prop / c->gamma;
+  } else if (c->network == CPR_NET_TWO_AGENTS) {
+    if (c->mode == CPR_MODE_GYM)
+      return fail(CPR_E_UNSUPPORTED, "the gym engine always uses the selfish-mining network");
+    P->d = 1;
+    P->net = 1;
+  } else {
+    return fail(CPR_E_INVALID_ARG, "unknown network");
+  }
+  P->n = P->d + 1;
+  int64_t span;
+  if (c->mode == CPR_MODE_GYM) {
+    const int64_t ms = c->max_steps > 0 ? c->max_steps : INT64_MAX;
+    P->max_steps = ms;
+    P->max_progress = c->max_progress > 0 ? c->max_progress : __builtin_inf();
+    P->max_time = c->max_time > 0 ? c->max_time : __builtin_inf();
+    span = ms < (1 << 20) ? ms + 2 : 8192;
+  } else {
+    if (c->activations <= 0) return fail(CPR_E_INVALID_ARG, "activations <= 0");
+    if (c->activations > (1 << 24)) return fail(CPR_E_UNSUPPORTED, "activations > 2^24");
+    P->max_steps = INT64_MAX;
+    P->activations = c->activations;
+    P->max_progress = __builtin_inf();
+    P->max_time = __builtin_inf();
+    span = c->activations * 2 + 2;  // votes + blocks
+  }
+  // vertex ring: a whole gym episode up to 2^16 vertices (longer runs flag
+  // CPR_ST_CAPACITY only if a fork outlives the ring)
+  int32_t cv = 64;
+  while (cv < span + 64 && cv < (1 << 16)) cv <<= 1;
+  P->cap_v = cv;
+  P->cap_q = cv / 2;
+  P->cap_d = 64;
+  P->cap_e = 256 + 1024 * P->n +
+             (std::isfinite(P->dmax) || P->net == 1
+                  ? 0
+                  : (int32_t)(2 * P->d * std::min<int64_t>(span, 8192)));
   return CPR_OK;
 }
 
@@ -285,9 +380,11 @@ int cpr_batch_create(cpr_ctx* ctx, const cpr_config* cfg, cpr_batch** out) {
   if (!ctx || !cfg || !out) return fail(CPR_E_INVALID_ARG, "NULL argument");
   NakParams P;
   eth::EthParams EP;
+  bk::BkParams BP;
   memset(&P, 0, sizeof(P));
   memset(&EP, 0, sizeof(EP));
-  int rc = validate(cfg, &P, &EP);
+  memset(&BP, 0, sizeof(BP));
+  int rc = validate(cfg, &P, &EP, &BP);
   if (rc) return rc;
   HIP_TRY(hipSetDevice(ctx->device));
   cpr_batch* b = new cpr_batch;
@@ -295,17 +392,26 @@ int cpr_batch_create(cpr_ctx* ctx, const cpr_config* cfg, cpr_batch** out) {
   b->cfg = *cfg;
   b->P = P;
   b->EP = EP;
+  b->BP = BP;
   b->eth_bytes = eth::eth_lane_bytes(EP.cap_b, EP.cap_e, EP.n);
+  if (cfg->protocol == CPR_PROTO_BK) b->bk_bytes = bk::bk_lane_bytes(BP);
   b->cfg.policy_table = nullptr;
-  if (cfg->policy == CPR_POLICY_TABLE) {
+  if (cfg->protocol == CPR_PROTO_BK && cfg->policy == CPR_BK_POLICY_TABLE) {
+    const size_t D = (size_t)cfg->policy_table_dim, K1 = (size_t)cfg->k + 1;
+    b->table_host.assign(cfg->policy_table, cfg->policy_table + D * D * K1 * K1 * 3);
+  } else if (cfg->protocol == CPR_PROTO_NAKAMOTO && cfg->policy == CPR_POLICY_TABLE) {
     const size_t nb = (size_t)cfg->policy_table_dim * cfg->policy_table_dim * 2;
     b->table_host.assign(cfg->policy_table, cfg->policy_table + nb);
   }
-  // unit-observation tables (ssz_tools.ml:487-491) evaluated with the host libm
-  std::vector<double> tabs(3 * (size_t)b->tab_n);
+  // unit-observation tables (ssz_tools.ml:487-491) evaluated with the host libm:
+  // [2/pi atan(i) | 0.5 + atan(i - N)/pi (2N) | 2/pi atan(i/k)], i < N
+  const double kscale = cfg->protocol == CPR_PROTO_BK ? (double)cfg->k : 1.0;
+  std::vector<double> tabs(4 * (size_t)b->tab_n);
   for (int i = 0; i < b->tab_n; i++) tabs[i] = 2. / M_PI * std::atan((double)i / 1.0);
   for (int i = 0; i < 2 * b->tab_n; i++)
     tabs[b->tab_n + i] = 0.5 + (1. / M_PI * std::atan((double)(i - b->tab_n) / 1.0));
+  for (int i = 0; i < b->tab_n; i++)
+    tabs[3 * b->tab_n + i] = 2. / M_PI * std::atan((double)i / kscale);
   hipError_t e = b->tabs_dev.ensure(tabs.size() * sizeof(double));
   if (e == hipSuccess)
     e = hipMemcpy(b->tabs_dev.p, tabs.data(), tabs.size() * sizeof(double), hipMemcpyHostToDevice);
@@ -320,6 +426,7 @@ int cpr_batch_create(cpr_ctx* ctx, const cpr_config* cfg, cpr_batch** out) {
     return fail(CPR_E_HIP, std::string("batch buffers: ") + hipGetErrorString(e));
   }
   b->P.table = (const uint8_t*)b->table_dev.p;
+  b->BP.table = (const uint8_t*)b->table_dev.p;
   *out = b;
   return CPR_OK;
 }
@@ -338,6 +445,9 @@ int cpr_batch_destroy(cpr_batch* b) {
   if (b->ev0) (void)hipEventDestroy(b->ev0);
   if (b->ev1) (void)hipEventDestroy(b->ev1);
   b->eth_mem.release();
+  b->bk_mem.release();
+  b->bk_lmem.release();
+  b->bk_slots.release();
   for (DevBuf* d : {&b->table_dev, &b->tabs_dev, &b->spill, &b->tlog, &b->replay, &b->summary,
                     &b->records, &b->lanes, &b->lring, &b->lspill, &b->ltlog, &b->lreplay,
                     &b->l_obs, &b->l_act, &b->l_rew, &b->l_done, &b->l_mask, &b->l_eps,
@@ -378,9 +488,30 @@ static int run_async_eth(cpr_batch* b, int64_t n, uint64_t first, cpr_summary* s
   return CPR_OK;
 }
 
+// B_k lanes: resident capacity bounded by a 32 GiB budget for the per-lane regions
+static int run_async_bk(cpr_batch* b, int64_t n, uint64_t first, cpr_summary* sum_dev,
+                        cpr_episode_record* rec_dev) {
+  const int64_t full = (int64_t)b->ctx->cus * bk_blocks_per_cu() * 256;
+  const int64_t budget = (int64_t)(32ll << 30) / b->bk_bytes;
+  int64_t lanes = std::min(full, std::max<int64_t>(256, budget));
+  lanes = std::min(lanes, ((n + 255) / 256) * 256);
+  lanes = std::max<int64_t>(256, (lanes / 256) * 256);
+  HIP_TRY(b->bk_mem.ensure((size_t)lanes * (size_t)b->bk_bytes));
+  if (!b->ev0) {
+    HIP_TRY(hipEventCreate(&b->ev0));
+    HIP_TRY(hipEventCreate(&b->ev1));
+  }
+  HIP_TRY(hipEventRecord(b->ev0, b->ctx->stream));
+  HIP_TRY(launch_bk_run_episodes(b->BP, b->cfg.seed, first, n, (uint8_t*)b->bk_mem.p,
+                                 b->bk_bytes, lanes, rec_dev, sum_dev, b->ctx->stream));
+  HIP_TRY(hipEventRecord(b->ev1, b->ctx->stream));
+  return CPR_OK;
+}
+
 static int run_async(cpr_batch* b, int64_t n, uint64_t first, cpr_summary* sum_dev,
                      cpr_episode_record* rec_dev) {
   if (b->cfg.protocol == CPR_PROTO_ETHEREUM) return run_async_eth(b, n, first, sum_dev, rec_dev);
+  if (b->cfg.protocol == CPR_PROTO_BK) return run_async_bk(b, n, first, sum_dev, rec_dev);
   const int64_t lanes = episode_lanes(b, n);
   if (lanes > b->lanes_alloc) {
     HIP_TRY(b->spill.ensure((size_t)lanes * b->P.cap * sizeof(int32_t)));
@@ -455,9 +586,38 @@ int cpr_run_episodes(cpr_batch* b, int64_t n, uint64_t first, cpr_summary* summa
 
 // ---------------------------------------------------------------- lockstep API
 
+static int obs_len_of(const cpr_config& c) {
+  return c.protocol == CPR_PROTO_BK ? 8 : (c.protocol == CPR_PROTO_ETHEREUM ? 10 : 4);
+}
+
+static int ensure_common_lockstep(cpr_batch* b, int obs_len) {
+  const int64_t n = b->cfg.n_lanes;
+  HIP_TRY(b->l_obs.ensure((size_t)n * obs_len * sizeof(double)));
+  HIP_TRY(b->l_act.ensure((size_t)n * sizeof(int32_t)));
+  HIP_TRY(b->l_rew.ensure((size_t)n * sizeof(double)));
+  HIP_TRY(b->l_done.ensure((size_t)n));
+  HIP_TRY(b->l_mask.ensure((size_t)n));
+  HIP_TRY(b->l_eps.ensure((size_t)n * sizeof(uint64_t)));
+  HIP_TRY(b->l_info.ensure((size_t)n * (7 * 8 + 2 * 4)));
+  return CPR_OK;
+}
+
+static int ensure_lockstep_bk(cpr_batch* b) {
+  const int64_t n = b->cfg.n_lanes;
+  if (n <= 0) return fail(CPR_E_STATE, "batch has no lockstep lanes (cfg.n_lanes = 0)");
+  if (b->cfg.mode != CPR_MODE_GYM) return fail(CPR_E_STATE, "lockstep lanes need CPR_MODE_GYM");
+  if (!b->bk_slots.p) {
+    HIP_TRY(b->bk_lmem.ensure((size_t)n * (size_t)b->bk_bytes));
+    HIP_TRY(b->bk_slots.ensure((size_t)n * bk_slot_bytes()));
+    HIP_TRY(hipMemsetAsync(b->bk_slots.p, 0, (size_t)n * bk_slot_bytes(), b->ctx->stream));
+  }
+  return ensure_common_lockstep(b, 8);
+}
+
 static int ensure_lockstep(cpr_batch* b) {
+  if (b->cfg.protocol == CPR_PROTO_BK) return ensure_lockstep_bk(b);
   if (b->cfg.protocol != CPR_PROTO_NAKAMOTO)
-    return fail(CPR_E_UNSUPPORTED, "lockstep lanes are implemented for Nakamoto only");
+    return fail(CPR_E_UNSUPPORTED, "lockstep lanes are implemented for Nakamoto and B_k");
   const int64_t n = b->cfg.n_lanes;
   if (n <= 0) return fail(CPR_E_STATE, "batch has no lockstep lanes (cfg.n_lanes = 0)");
   if (b->cfg.mode != CPR_MODE_GYM) return fail(CPR_E_STATE, "lockstep lanes need CPR_MODE_GYM");
@@ -508,10 +668,16 @@ int cpr_reset(cpr_batch* b, const uint8_t* mask, const uint64_t* eps, double* ob
     deps = (const uint64_t*)b->l_eps.p;
   }
   const double* tabs = (const double*)b->tabs_dev.p;
-  HIP_TRY(launch_reset(b->P, b->cfg.seed, lock_buffers(b), n, dmask, deps,
-                       b->cfg.unit_observation, tabs, tabs + b->tab_n, b->tab_n,
-                       (double*)b->l_obs.p, st));
-  HIP_TRY(hipMemcpyAsync(obs, b->l_obs.p, (size_t)n * 4 * sizeof(double), hipMemcpyDeviceToHost, st));
+  const int ol = obs_len_of(b->cfg);
+  if (b->cfg.protocol == CPR_PROTO_BK)
+    HIP_TRY(launch_bk_reset(b->BP, b->cfg.seed, (uint8_t*)b->bk_lmem.p, b->bk_bytes,
+                            b->bk_slots.p, n, dmask, deps, b->cfg.unit_observation, tabs,
+                            b->tab_n, (double*)b->l_obs.p, st));
+  else
+    HIP_TRY(launch_reset(b->P, b->cfg.seed, lock_buffers(b), n, dmask, deps,
+                         b->cfg.unit_observation, tabs, tabs + b->tab_n, b->tab_n,
+                         (double*)b->l_obs.p, st));
+  HIP_TRY(hipMemcpyAsync(obs, b->l_obs.p, (size_t)n * ol * sizeof(double), hipMemcpyDeviceToHost, st));
   HIP_TRY(hipStreamSynchronize(st));
   b->reset_done = true;
   return CPR_OK;
@@ -522,8 +688,10 @@ int cpr_step(cpr_batch* b, const int32_t* actions, double* obs, double* reward, 
   if (!b || !actions || !obs || !reward || !done) return fail(CPR_E_INVALID_ARG, "NULL argument");
   if (!b->reset_done) return fail(CPR_E_STATE, "step before reset");
   const int64_t n = b->cfg.n_lanes;
+  const int n_act = b->cfg.protocol == CPR_PROTO_BK ? 8 : 4;
+  const int ol = obs_len_of(b->cfg);
   for (int64_t i = 0; i < n; i++)
-    if (actions[i] < 0 || actions[i] > 3)
+    if (actions[i] < 0 || actions[i] >= n_act)
       return fail(CPR_E_INVALID_ARG, "Invalid_argument \"index out of bounds\" (action)");
   HIP_TRY(hipSetDevice(b->ctx->device));
   hipStream_t st = b->ctx->stream;
@@ -543,9 +711,14 @@ int cpr_step(cpr_batch* b, const int32_t* actions, double* obs, double* reward, 
   sb.hh = (int32_t*)(ib + 7 * n * 8);
   sb.hm = (int32_t*)(ib + 7 * n * 8 + n * 4);
   const double* tabs = (const double*)b->tabs_dev.p;
-  HIP_TRY(launch_step(b->P, b->cfg.seed, lock_buffers(b), n, (const int32_t*)b->l_act.p,
-                      b->cfg.unit_observation, tabs, tabs + b->tab_n, b->tab_n, sb, st));
-  HIP_TRY(hipMemcpyAsync(obs, sb.obs, (size_t)n * 32, hipMemcpyDeviceToHost, st));
+  if (b->cfg.protocol == CPR_PROTO_BK)
+    HIP_TRY(launch_bk_step(b->BP, b->cfg.seed, (uint8_t*)b->bk_lmem.p, b->bk_bytes,
+                           b->bk_slots.p, n, (const int32_t*)b->l_act.p,
+                           b->cfg.unit_observation, tabs, b->tab_n, sb, st));
+  else
+    HIP_TRY(launch_step(b->P, b->cfg.seed, lock_buffers(b), n, (const int32_t*)b->l_act.p,
+                        b->cfg.unit_observation, tabs, tabs + b->tab_n, b->tab_n, sb, st));
+  HIP_TRY(hipMemcpyAsync(obs, sb.obs, (size_t)n * ol * 8, hipMemcpyDeviceToHost, st));
   HIP_TRY(hipMemcpyAsync(reward, sb.reward, (size_t)n * 8, hipMemcpyDeviceToHost, st));
   HIP_TRY(hipMemcpyAsync(done, sb.done, (size_t)n, hipMemcpyDeviceToHost, st));
   if (info) {
@@ -567,16 +740,21 @@ int cpr_step(cpr_batch* b, const int32_t* actions, double* obs, double* reward, 
 
 int cpr_observe_fields(cpr_batch* b, int32_t* fields) {
   if (!b || !fields) return fail(CPR_E_INVALID_ARG, "NULL argument");
-  if (b->cfg.protocol != CPR_PROTO_NAKAMOTO)
-    return fail(CPR_E_UNSUPPORTED, "lockstep lanes are implemented for Nakamoto only");
+  if (b->cfg.protocol != CPR_PROTO_NAKAMOTO && b->cfg.protocol != CPR_PROTO_BK)
+    return fail(CPR_E_UNSUPPORTED, "lockstep lanes are implemented for Nakamoto and B_k");
   if (!b->reset_done) return fail(CPR_E_STATE, "observe before reset");
   const int64_t n = b->cfg.n_lanes;
   HIP_TRY(hipSetDevice(b->ctx->device));
   hipStream_t st = b->ctx->stream;
+  const size_t per = (size_t)obs_len_of(b->cfg) * 4;
   DevBuf tmp;
-  HIP_TRY(tmp.ensure((size_t)n * 16));
-  HIP_TRY(launch_observe_fields(b->lanes.p, n, (int32_t*)tmp.p, st));
-  HIP_TRY(hipMemcpyAsync(fields, tmp.p, (size_t)n * 16, hipMemcpyDeviceToHost, st));
+  HIP_TRY(tmp.ensure((size_t)n * per));
+  if (b->cfg.protocol == CPR_PROTO_BK)
+    HIP_TRY(launch_bk_observe_fields(b->BP, (uint8_t*)b->bk_lmem.p, b->bk_bytes, b->bk_slots.p,
+                                     n, (int32_t*)tmp.p, st));
+  else
+    HIP_TRY(launch_observe_fields(b->lanes.p, n, (int32_t*)tmp.p, st));
+  HIP_TRY(hipMemcpyAsync(fields, tmp.p, (size_t)n * per, hipMemcpyDeviceToHost, st));
   HIP_TRY(hipStreamSynchronize(st));
   tmp.release();
   return CPR_OK;
@@ -585,8 +763,26 @@ int cpr_observe_fields(cpr_batch* b, int32_t* fields) {
 int cpr_policy_actions(cpr_batch* b, int32_t policy, const double* obs, int64_t n,
                        int32_t* actions) {
   if (!b || !obs || !actions) return fail(CPR_E_INVALID_ARG, "NULL argument");
+  if (b->cfg.protocol == CPR_PROTO_BK) {
+    if (policy < 0 || policy > CPR_BK_POLICY_TABLE) return fail(CPR_E_INVALID_ARG, "unknown policy");
+    if (policy == CPR_BK_POLICY_TABLE && b->table_host.empty())
+      return fail(CPR_E_INVALID_ARG, "batch has no policy table");
+    if (n <= 0) return CPR_OK;
+    HIP_TRY(hipSetDevice(b->ctx->device));
+    hipStream_t st = b->ctx->stream;
+    DevBuf o, a;
+    HIP_TRY(o.ensure((size_t)n * 64));
+    HIP_TRY(a.ensure((size_t)n * 4));
+    HIP_TRY(hipMemcpyAsync(o.p, obs, (size_t)n * 64, hipMemcpyHostToDevice, st));
+    bk::BkParams P = b->BP;
+    P.policy = policy;
+    HIP_TRY(launch_bk_policy(P, b->cfg.unit_observation, (const double*)o.p, n, (int32_t*)a.p, st));
+    HIP_TRY(hipMemcpyAsync(actions, a.p, (size_t)n * 4, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    return CPR_OK;
+  }
   if (b->cfg.protocol != CPR_PROTO_NAKAMOTO)
-    return fail(CPR_E_UNSUPPORTED, "policy evaluation on encoded observations: Nakamoto only");
+    return fail(CPR_E_UNSUPPORTED, "policy evaluation on encoded observations: Nakamoto and B_k");
   if (policy < 0 || policy > CPR_POLICY_TABLE) return fail(CPR_E_INVALID_ARG, "unknown policy");
   if (policy == CPR_POLICY_TABLE && b->table_host.empty())
     return fail(CPR_E_INVALID_ARG, "batch has no policy table");
@@ -612,6 +808,21 @@ int cpr_observation_spec(cpr_batch* b, int32_t* obs_len, int32_t* n_actions, dou
                          double* high) {
   if (!b) return fail(CPR_E_INVALID_ARG, "NULL argument");
   const double inf = __builtin_inf();
+  if (b->cfg.protocol == CPR_PROTO_BK) {
+    // bk_ssz.ml:37-74 normalizers; ssz_tools.ml:64-74 ranges (raw Bool range is (0, 0))
+    if (obs_len) *obs_len = 8;
+    if (n_actions) *n_actions = 8;
+    for (int i = 0; i < 8; i++) {
+      double lo = 0.0, hi = 1.0;
+      if (!b->cfg.unit_observation) {
+        lo = i == 2 ? -inf : 0.0;
+        hi = i == 6 ? 0.0 : (i == 7 ? 2.0 : inf);
+      }
+      if (low) low[i] = lo;
+      if (high) high[i] = hi;
+    }
+    return CPR_OK;
+  }
   if (b->cfg.protocol == CPR_PROTO_ETHEREUM) {
     // ethereum_ssz.ml:47-80: 10 fields (diff_* signed, event discrete), 24 actions
     if (obs_len) *obs_len = 10;
@@ -658,8 +869,18 @@ static const int32_t kEthIds[5] = {CPR_ETH_POLICY_FN19PKEL, CPR_ETH_POLICY_FN19,
                                    CPR_ETH_POLICY_SELFISH_DISCARD,
                                    CPR_ETH_POLICY_SELFISH_RELEASE, CPR_ETH_POLICY_HONEST};
 
+// bk_ssz.ml:404-415, same reversal
+static const char* kBkNames[4] = {"avoid-loss", "minor-delay", "get-ahead", "honest"};
+static const int32_t kBkIds[4] = {CPR_BK_POLICY_AVOID_LOSS, CPR_BK_POLICY_MINOR_DELAY,
+                                  CPR_BK_POLICY_GET_AHEAD, CPR_BK_POLICY_HONEST};
+
 int cpr_policy_count(int32_t protocol) {
-  return protocol == CPR_PROTO_NAKAMOTO ? 4 : (protocol == CPR_PROTO_ETHEREUM ? 5 : 0);
+  switch (protocol) {
+    case CPR_PROTO_NAKAMOTO: return 4;
+    case CPR_PROTO_ETHEREUM: return 5;
+    case CPR_PROTO_BK: return 4;
+    default: return 0;
+  }
 }
 
 const char* cpr_policy_name(int32_t protocol, int32_t index, int32_t* policy_id) {
@@ -671,8 +892,59 @@ const char* cpr_policy_name(int32_t protocol, int32_t index, int32_t* policy_id)
     if (policy_id) *policy_id = kEthIds[index];
     return kEthNames[index];
   }
+  if (protocol == CPR_PROTO_BK) {
+    if (policy_id) *policy_id = kBkIds[index];
+    return kBkNames[index];
+  }
   if (policy_id) *policy_id = kIds[index];
   return kNames[index];
+}
+
+int cpr_rollout(cpr_batch* b, int64_t n_steps, double* obs_dev, double* reward_dev,
+                uint8_t* done_dev, cpr_summary* summary) {
+  if (!b || !summary) return fail(CPR_E_INVALID_ARG, "NULL argument");
+  if (b->cfg.protocol != CPR_PROTO_BK)
+    return fail(CPR_E_UNSUPPORTED, "cpr_rollout is implemented for B_k");
+  if (n_steps <= 0) return CPR_OK;
+  HIP_TRY(hipSetDevice(b->ctx->device));
+  int rc = ensure_lockstep(b);
+  if (rc) return rc;
+  hipStream_t st = b->ctx->stream;
+  HIP_TRY(b->summary.ensure(sizeof(cpr_summary)));
+  HIP_TRY(hipMemsetAsync(b->summary.p, 0, sizeof(cpr_summary), st));
+  if (!b->ev0) {
+    HIP_TRY(hipEventCreate(&b->ev0));
+    HIP_TRY(hipEventCreate(&b->ev1));
+  }
+  const double* tabs = (const double*)b->tabs_dev.p;
+  HIP_TRY(hipEventRecord(b->ev0, st));
+  HIP_TRY(launch_bk_rollout(b->BP, b->cfg.seed, (uint8_t*)b->bk_lmem.p, b->bk_bytes,
+                            b->bk_slots.p, b->cfg.n_lanes, n_steps, b->cfg.unit_observation,
+                            tabs, b->tab_n, obs_dev, reward_dev, done_dev,
+                            (cpr_summary*)b->summary.p, st));
+  HIP_TRY(hipEventRecord(b->ev1, st));
+  cpr_summary s;
+  HIP_TRY(hipMemcpyAsync(&s, b->summary.p, sizeof(s), hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  float ms = 0.f;
+  HIP_TRY(hipEventElapsedTime(&ms, b->ev0, b->ev1));
+  b->last_ms = ms;
+  b->last_acts = s.activations;
+  b->reset_done = true;
+  summary->episodes += s.episodes;
+  summary->steps += s.steps;
+  summary->activations += s.activations;
+  summary->reward_attacker_fx += s.reward_attacker_fx;
+  summary->reward_defender_fx += s.reward_defender_fx;
+  summary->progress_fx += s.progress_fx;
+  summary->rel_revenue_fx += s.rel_revenue_fx;
+  summary->rel_revenue_sq_fx += s.rel_revenue_sq_fx;
+  summary->orphans += s.orphans;
+  summary->status_tie += s.status_tie;
+  summary->status_overlap += s.status_overlap;
+  summary->status_other += s.status_other;
+  for (int i = 0; i < CPR_HIST_BINS; i++) summary->hist[i] += s.hist[i];
+  return CPR_OK;
 }
 
 int cpr_stream_fill(cpr_ctx* ctx, uint64_t seed, uint64_t ep, uint32_t idx0, uint32_t tag,

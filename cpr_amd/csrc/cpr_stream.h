@@ -9,6 +9,8 @@
 //                  w2,w3 -> u53 -> delay = (-1*ev) * cpr_log(u)
 //   link (shared at activation count kw, share position off, dest j) :
 //                  ctr = (ep, kw, TAG_LINK | off<<12 | j>>1), words 2*(j&1),+1 -> u53
+//   message (vertex serial s, dest j; B_k, where a node shares several times per
+//   activation window): ctr = (ep, s, TAG_MSG | j>>1), words 2*(j&1),+1 -> u53
 // cpr_log = fdlibm e_log.c (IEEE +,-,*,/ only) so device and host agree bit for bit;
 // this TU must be compiled with -ffp-contract=off.
 #pragma once
@@ -22,6 +24,7 @@ namespace cpr {
 constexpr uint32_t TAG_ACT = 0u;
 constexpr uint32_t TAG_LINK = 0x10000000u;
 constexpr uint32_t TAG_POW = 0x20000000u;
+constexpr uint32_t TAG_MSG = 0x30000000u;
 
 struct Words4 {
   uint32_t w0, w1, w2, w3;
@@ -123,6 +126,10 @@ struct Stream {
   // order, to node dest
   __host__ __device__ inline double link_u(uint32_t kw, uint32_t off, uint32_t dest) const {
     const Words4 w = block(kw, TAG_LINK | (off << 12) | (dest >> 1));
+    return (dest & 1u) ? u53(w.w2, w.w3) : u53(w.w0, w.w1);
+  }
+  __host__ __device__ inline double msg_u(uint32_t serial, uint32_t dest) const {
+    const Words4 w = block(serial, TAG_MSG | (dest >> 1));
     return (dest & 1u) ? u53(w.w2, w.w3) : u53(w.w0, w.w1);
   }
 };

@@ -197,8 +197,9 @@ struct EthLane {
   }
 
   // ------------------------------------------------------------------ event queue
-  // orderedQueue.ml:17-47 as an in-place skew heap (equal times: the earlier insertion
-  // pops first). Events at +inf (messages that never arrive, gamma = 0) are not stored.
+  // orderedQueue.ml:17-47 as an in-place skew heap. Events at +inf (messages that never
+  // arrive, gamma = 0) are stored too: every insertion swaps children along its path, so
+  // they shape the pop order of equal-time events although they never pop in the gym.
   __host__ __device__ inline int32_t halloc(const EthParams& P, const EthMem& M) {
     int32_t i;
     if (hfree >= 0) {
@@ -214,7 +215,6 @@ struct EthLane {
   }
   __host__ __device__ inline void push(const EthParams& P, const EthMem& M, double t,
                                        uint32_t ev, int32_t blk) {
-    if (!(t < __builtin_inf())) return;
     int32_t parent = -1, node = hroot;
     for (;;) {
       if (node < 0) {
@@ -771,6 +771,10 @@ struct EthLane {
         break;
       }
       case EV_RX: {
+        // simulator.ml:488-493: `now < received_at` with received_at = +inf until the
+        // first receipt, so a delivery at t = +inf (Simulator.loop draining gamma = 0
+        // messages) changes nothing
+        if (!(now < __builtin_inf())) break;
         uint8_t& v = V(P, M, s, node);
         if (!(v & V_GOT)) {
           v |= V_GOT;

@@ -5,6 +5,7 @@
 #include <stdint.h>
 
 #include "../../include/cpr_hip.h"
+#include "bk_lane.h"
 #include "ethereum_lane.h"
 #include "nakamoto_lane.h"
 
@@ -64,6 +65,27 @@ hipError_t launch_eth_run_episodes(const eth::EthParams& P, uint64_t seed, uint6
                                    int64_t lanes, cpr_episode_record* recs, cpr_summary* sum,
                                    hipStream_t st);
 int eth_blocks_per_cu();
+
+// B_k (kernels_bk.hip): mem = lanes x lane_bytes; lockstep slots = n x bk_slot_bytes()
+hipError_t launch_bk_run_episodes(const bk::BkParams& P, uint64_t seed, uint64_t first,
+                                  int64_t n_eps, uint8_t* mem, int64_t lane_bytes, int64_t lanes,
+                                  cpr_episode_record* recs, cpr_summary* sum, hipStream_t st);
+hipError_t launch_bk_reset(const bk::BkParams& P, uint64_t seed, uint8_t* mem, int64_t lane_bytes,
+                           void* slots, int64_t n, const uint8_t* mask, const uint64_t* eps,
+                           int unit, const double* tabs, int32_t tn, double* obs, hipStream_t st);
+hipError_t launch_bk_step(const bk::BkParams& P, uint64_t seed, uint8_t* mem, int64_t lane_bytes,
+                          void* slots, int64_t n, const int32_t* actions, int unit,
+                          const double* tabs, int32_t tn, const StepBuffers& b, hipStream_t st);
+hipError_t launch_bk_rollout(const bk::BkParams& P, uint64_t seed, uint8_t* mem,
+                             int64_t lane_bytes, void* slots, int64_t n, int64_t n_steps,
+                             int unit, const double* tabs, int32_t tn, double* obs,
+                             double* reward, uint8_t* done, cpr_summary* sum, hipStream_t st);
+hipError_t launch_bk_observe_fields(const bk::BkParams& P, uint8_t* mem, int64_t lane_bytes,
+                                    const void* slots, int64_t n, int32_t* f, hipStream_t st);
+hipError_t launch_bk_policy(const bk::BkParams& P, int unit, const double* obs, int64_t n,
+                            int32_t* actions, hipStream_t st);
+size_t bk_slot_bytes();
+int bk_blocks_per_cu();
 int run_episodes_blocks_per_cu(int32_t mode);  // resident 256-lane workgroups per CU
 
 }  // namespace cpr

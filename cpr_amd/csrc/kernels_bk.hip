@@ -1,0 +1,336 @@
+// B_k kernels for gfx950: one lane = one episode / gym env of the bk_ssz attack space,
+// driven by the exact per-lane event engine of bk_lane.h. Each lane owns one contiguous
+// HBM region (vertex ring, per-node visibility and times, quorums, drafts, event heap,
+// scratch) reused for every episode it runs.
+//
+//   k_bk_run_episodes  fused reset/(policy, step)* episodes, or Simulator.loop tasks
+//   k_bk_reset/k_bk_step  lockstep gym API (engine.ml reset / step) with host actions
+//   k_bk_rollout       lockstep rollout on the device: every lane takes n_steps steps with
+//                      the batch policy (built-in or table), auto-resetting finished
+//                      episodes like a gym VecEnv (BASELINE configs[4])
+#include <hip/hip_runtime.h>
+
+#include "../../include/cpr_hip.h"
+#include "bk_lane.h"
+#include "kernels.h"
+#include "summary.h"
+
+#pragma clang fp contract(off)
+
+namespace cpr {
+
+// engine.ml reward = Δ head.rewards[0]; episode ids of lane i in a rollout: i, i + n, ...
+struct BkSlot {
+  bk::BkLane L;
+  uint64_t ep;
+  double last_ra;
+  int32_t head;
+  int32_t live;
+};
+
+__device__ inline void bk_acc(Acc& acc, const bk::BkParams& P, const bk::BkLane& L,
+                              const bk::BVtx& h, int32_t* hist) {
+  const int32_t ra = h.rew_att, rd = h.rew_def;
+  const double rel = (ra + rd) != 0 ? (double)ra / (double)(ra + rd) : 0.0;
+  // orphans: activations (votes) not confirmed by the head's chain
+  acc_episode(acc, (int64_t)ra << 20, (int64_t)rd << 20, (int64_t)h.height * P.k << 20, rel,
+              (int64_t)h.height * P.k, L.steps, L.c_act, L.status, hist);
+}
+
+__global__ __launch_bounds__(kBlock) void k_bk_run_episodes(
+    bk::BkParams P, uint64_t seed, uint64_t first, int64_t n_eps, uint8_t* mem,
+    int64_t lane_bytes, cpr_episode_record* recs, cpr_summary* sum) {
+  __shared__ int32_t hist[CPR_HIST_BINS];
+  if (threadIdx.x < CPR_HIST_BINS) hist[threadIdx.x] = 0;
+  __syncthreads();
+  const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t nthreads = (int64_t)gridDim.x * blockDim.x;
+  const bk::BkMem M = bk::bk_mem_at(mem + tid * lane_bytes, P);
+  Acc acc = {};
+  bk::BkLane L;
+  for (int64_t e = tid; e < n_eps; e += nthreads) {
+    const uint64_t ep = first + (uint64_t)e;
+    const Stream S = make_stream(seed, ep);
+    int32_t hd;
+    if (P.mode == CPR_MODE_GYM) {
+      L.gym_reset(P, S, M);
+      bool done = L.dead != 0;
+      hd = 0;
+      while (!done) hd = L.gym_step(P, S, M, bk::bk_policy(P, L.observe(P, M)), &done);
+    } else {
+      hd = L.loop(P, S, M);
+    }
+    const bk::BVtx& h = L.X(P, M, hd);
+    bk_acc(acc, P, L, h, hist);
+    if (recs) {
+      cpr_episode_record r;
+      r.reward_attacker = (double)h.rew_att;
+      r.reward_defender = (double)h.rew_def;
+      r.progress = (double)(h.height * P.k);
+      r.chain_time = h.time;
+      r.sim_time = P.mode == CPR_MODE_GYM ? L.now : 0.0;
+      r.n_steps = L.steps;
+      r.n_activations = L.c_act;
+      r.head_height = h.height;
+      r.head_miner = h.who;
+      r.status = L.status;
+      r.head_work = 0;
+      recs[e] = r;
+    }
+  }
+  __syncthreads();
+  block_flush(acc, hist, sum);
+}
+
+// ssz_tools.ml:1-74 with bk_ssz.ml:37-48 normalizers; unit encodings use host-tabulated
+// libm values (tabs = [2/pi atan(i) | 0.5 + atan(i - N)/pi | 2/pi atan(i/k)], i < N)
+__device__ inline void bk_write_obs(const bk::BkObs& o, int unit, const double* tabs,
+                                    int32_t tn, int32_t k, double* out) {
+  const double pi = 3.141592653589793;
+  if (!unit) {
+    out[0] = (double)o.public_blocks;
+    out[1] = (double)o.private_blocks;
+    out[2] = (double)o.diff_blocks;
+    out[3] = (double)o.public_votes;
+    out[4] = (double)o.private_votes_inclusive;
+    out[5] = (double)o.private_votes_exclusive;
+    out[6] = o.lead ? 1.0 : 0.0;
+    out[7] = (double)o.event;
+    return;
+  }
+  auto nn1 = [&](int32_t x) { return x < tn ? tabs[x] : 2.0 / pi * atan((double)x / 1.0); };
+  auto nnk = [&](int32_t x) {
+    return x < tn ? tabs[3 * tn + x] : 2.0 / pi * atan((double)x / (double)k);
+  };
+  out[0] = nn1(o.public_blocks);
+  out[1] = nn1(o.private_blocks);
+  const int32_t d = o.diff_blocks;
+  out[2] = (d > -tn && d < tn) ? tabs[tn + d + tn] : 0.5 + (1.0 / pi * atan((double)d / 1.0));
+  out[3] = nnk(o.public_votes);
+  out[4] = nnk(o.private_votes_inclusive);
+  out[5] = nnk(o.private_votes_exclusive);
+  out[6] = o.lead ? 1.0 : 0.0;
+  out[7] = (double)o.event / 2.0;
+}
+
+__device__ inline void bk_slot_reset(const bk::BkParams& P, uint64_t seed, const bk::BkMem& M,
+                                     BkSlot& SL, uint64_t ep) {
+  SL.ep = ep;
+  SL.last_ra = 0.0;
+  SL.head = 0;
+  SL.live = 1;
+  SL.L.gym_reset(P, make_stream(seed, ep), M);
+}
+
+__global__ __launch_bounds__(kBlock) void k_bk_reset(bk::BkParams P, uint64_t seed,
+                                                      uint8_t* mem, int64_t lane_bytes,
+                                                      BkSlot* slots, int64_t n,
+                                                      const uint8_t* mask, const uint64_t* eps,
+                                                      int unit, const double* tabs, int32_t tn,
+                                                      double* obs) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const bk::BkMem M = bk::bk_mem_at(mem + i * lane_bytes, P);
+  BkSlot SL = slots[i];
+  if (mask == nullptr || mask[i]) bk_slot_reset(P, seed, M, SL, eps ? eps[i] : (uint64_t)i);
+  bk_write_obs(SL.L.observe(P, M), unit, tabs, tn, P.k, obs + 8 * i);
+  slots[i] = SL;
+}
+
+__global__ __launch_bounds__(kBlock) void k_bk_step(bk::BkParams P, uint64_t seed, uint8_t* mem,
+                                                     int64_t lane_bytes, BkSlot* slots,
+                                                     int64_t n, const int32_t* actions, int unit,
+                                                     const double* tabs, int32_t tn,
+                                                     StepBuffers out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const bk::BkMem M = bk::bk_mem_at(mem + i * lane_bytes, P);
+  BkSlot SL = slots[i];
+  const Stream S = make_stream(seed, SL.ep);
+  bool done = false;
+  const int32_t hd = SL.L.gym_step(P, S, M, actions[i], &done);
+  SL.head = hd;
+  const bk::BVtx& h = SL.L.X(P, M, hd);
+  const double ra = (double)h.rew_att;
+  out.reward[i] = ra - SL.last_ra;  // engine.ml:223
+  out.done[i] = done ? 1 : 0;
+  if (out.era) {
+    out.era[i] = ra;
+    out.erd[i] = (double)h.rew_def;
+    out.eprog[i] = (double)(h.height * P.k);
+    out.ect[i] = h.time;
+    out.est[i] = SL.L.now;
+    out.esteps[i] = SL.L.steps;
+    out.eacts[i] = SL.L.c_act;
+    out.hh[i] = h.height;
+    out.hm[i] = h.who;
+  }
+  SL.last_ra = ra;
+  bk_write_obs(SL.L.observe(P, M), unit, tabs, tn, P.k, out.obs + 8 * i);
+  slots[i] = SL;
+}
+
+// n_steps lockstep steps per lane with the batch's on-device policy; finished episodes are
+// summarised and the lane restarts with episode id ep + n (VecEnv auto-reset: the
+// observation written at a done step is the new episode's first observation).
+// summary.steps / .activations count every step / activation of the rollout; the other
+// summary fields cover the episodes that finished in it.
+__global__ __launch_bounds__(kBlock) void k_bk_rollout(bk::BkParams P, uint64_t seed,
+                                                        uint8_t* mem, int64_t lane_bytes,
+                                                        BkSlot* slots, int64_t n,
+                                                        int64_t n_steps, int unit,
+                                                        const double* tabs, int32_t tn,
+                                                        double* obs, double* reward,
+                                                        uint8_t* done_out, cpr_summary* sum) {
+  __shared__ int32_t hist[CPR_HIST_BINS];
+  if (threadIdx.x < CPR_HIST_BINS) hist[threadIdx.x] = 0;
+  __syncthreads();
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  Acc acc = {};
+  int64_t steps_all = 0, acts_all = 0;
+  if (i < n) {
+    const bk::BkMem M = bk::bk_mem_at(mem + i * lane_bytes, P);
+    BkSlot SL = slots[i];
+    if (!SL.live) {
+      bk_slot_reset(P, seed, M, SL, (uint64_t)i);
+      acts_all += SL.L.c_act;
+    }
+    Stream S = make_stream(seed, SL.ep);
+    for (int64_t t = 0; t < n_steps; ++t) {
+      const bk::BkObs o = SL.L.observe(P, M);
+      const int32_t c0 = SL.L.c_act;
+      bool done = false;
+      const int32_t hd = SL.L.gym_step(P, S, M, bk::bk_policy(P, o), &done);
+      acts_all += SL.L.c_act - c0;
+      ++steps_all;
+      const bk::BVtx& h = SL.L.X(P, M, hd);
+      const double ra = (double)h.rew_att;
+      const int64_t k = t * n + i;
+      if (reward) reward[k] = ra - SL.last_ra;
+      if (done_out) done_out[k] = done ? 1 : 0;
+      SL.last_ra = ra;
+      if (done) {
+        bk_acc(acc, P, SL.L, h, hist);
+        bk_slot_reset(P, seed, M, SL, SL.ep + (uint64_t)n);
+        acts_all += SL.L.c_act;
+        S = make_stream(seed, SL.ep);
+      }
+      if (obs) bk_write_obs(SL.L.observe(P, M), unit, tabs, tn, P.k, obs + 8 * k);
+    }
+    slots[i] = SL;
+  }
+  // rollout totals: all steps and activations (acc.steps/activations hold finished
+  // episodes only, so replace them before the block reduction)
+  acc.steps = steps_all;
+  acc.activations = acts_all;
+  __syncthreads();
+  block_flush(acc, hist, sum);
+}
+
+__global__ void k_bk_observe_fields(bk::BkParams P, uint8_t* mem, int64_t lane_bytes,
+                                    const BkSlot* slots, int64_t n, int32_t* f) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const bk::BkMem M = bk::bk_mem_at(mem + i * lane_bytes, P);
+  bk::BkLane L = slots[i].L;
+  const bk::BkObs o = L.observe(P, M);
+  int32_t* g = f + 8 * i;
+  g[0] = o.public_blocks;
+  g[1] = o.private_blocks;
+  g[2] = o.diff_blocks;
+  g[3] = o.public_votes;
+  g[4] = o.private_votes_inclusive;
+  g[5] = o.private_votes_exclusive;
+  g[6] = o.lead;
+  g[7] = o.event;
+}
+
+// engine.ml:258-261: decode (ssz_tools.ml:42-58 of_float) and apply the policy
+__global__ void k_bk_policy(bk::BkParams P, int unit, const double* obs, int64_t n,
+                            int32_t* actions) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const double* x = obs + 8 * i;
+  const double pi = 3.141592653589793;
+  int32_t v[8];
+  for (int j = 0; j < 8; ++j) {
+    if (j == 6) {
+      v[j] = x[j] >= 0.5 ? 1 : 0;
+    } else if (j == 7) {
+      v[j] = unit ? (int32_t)floor(x[j] * 2.0) : (int32_t)x[j];
+    } else if (!unit) {
+      v[j] = (int32_t)x[j];
+    } else {
+      const double scale = j >= 3 ? (double)P.k : 1.0;
+      v[j] = j == 2 ? (int32_t)__builtin_round(tan(pi * (x[j] - 0.5)) * scale)
+                    : (int32_t)__builtin_round(tan(pi / 2.0 * x[j]) * scale);
+    }
+  }
+  const bk::BkObs o{v[0], v[1], v[2], v[3], v[4], v[5], v[6], v[7]};
+  actions[i] = bk::bk_policy(P, o);
+}
+
+// ---------------------------------------------------------------- launchers
+
+static unsigned grid_of(int64_t n) { return (unsigned)((n + kBlock - 1) / kBlock); }
+
+hipError_t launch_bk_run_episodes(const bk::BkParams& P, uint64_t seed, uint64_t first,
+                                  int64_t n_eps, uint8_t* mem, int64_t lane_bytes, int64_t lanes,
+                                  cpr_episode_record* recs, cpr_summary* sum, hipStream_t st) {
+  hipLaunchKernelGGL(k_bk_run_episodes, dim3((unsigned)(lanes / kBlock)), dim3(kBlock), 0, st, P,
+                     seed, first, n_eps, mem, lane_bytes, recs, sum);
+  return hipGetLastError();
+}
+
+hipError_t launch_bk_reset(const bk::BkParams& P, uint64_t seed, uint8_t* mem, int64_t lane_bytes,
+                           void* slots, int64_t n, const uint8_t* mask, const uint64_t* eps,
+                           int unit, const double* tabs, int32_t tn, double* obs,
+                           hipStream_t st) {
+  hipLaunchKernelGGL(k_bk_reset, dim3(grid_of(n)), dim3(kBlock), 0, st, P, seed, mem, lane_bytes,
+                     (BkSlot*)slots, n, mask, eps, unit, tabs, tn, obs);
+  return hipGetLastError();
+}
+
+hipError_t launch_bk_step(const bk::BkParams& P, uint64_t seed, uint8_t* mem, int64_t lane_bytes,
+                          void* slots, int64_t n, const int32_t* actions, int unit,
+                          const double* tabs, int32_t tn, const StepBuffers& b, hipStream_t st) {
+  hipLaunchKernelGGL(k_bk_step, dim3(grid_of(n)), dim3(kBlock), 0, st, P, seed, mem, lane_bytes,
+                     (BkSlot*)slots, n, actions, unit, tabs, tn, b);
+  return hipGetLastError();
+}
+
+hipError_t launch_bk_rollout(const bk::BkParams& P, uint64_t seed, uint8_t* mem,
+                             int64_t lane_bytes, void* slots, int64_t n, int64_t n_steps,
+                             int unit, const double* tabs, int32_t tn, double* obs,
+                             double* reward, uint8_t* done, cpr_summary* sum, hipStream_t st) {
+  hipLaunchKernelGGL(k_bk_rollout, dim3(grid_of(n)), dim3(kBlock), 0, st, P, seed, mem,
+                     lane_bytes, (BkSlot*)slots, n, n_steps, unit, tabs, tn, obs, reward, done,
+                     sum);
+  return hipGetLastError();
+}
+
+hipError_t launch_bk_observe_fields(const bk::BkParams& P, uint8_t* mem, int64_t lane_bytes,
+                                    const void* slots, int64_t n, int32_t* f, hipStream_t st) {
+  hipLaunchKernelGGL(k_bk_observe_fields, dim3(grid_of(n)), dim3(kBlock), 0, st, P, mem,
+                     lane_bytes, (const BkSlot*)slots, n, f);
+  return hipGetLastError();
+}
+
+hipError_t launch_bk_policy(const bk::BkParams& P, int unit, const double* obs, int64_t n,
+                            int32_t* actions, hipStream_t st) {
+  hipLaunchKernelGGL(k_bk_policy, dim3(grid_of(n)), dim3(kBlock), 0, st, P, unit, obs, n,
+                     actions);
+  return hipGetLastError();
+}
+
+size_t bk_slot_bytes() { return sizeof(BkSlot); }
+
+int bk_blocks_per_cu() {
+  int blocks = 0;
+  hipError_t e =
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, k_bk_run_episodes, kBlock, 0);
+  if (e != hipSuccess || blocks <= 0) blocks = 2;
+  return blocks;
+}
+
+}  // namespace cpr

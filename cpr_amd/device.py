@@ -81,9 +81,13 @@ def make_config(
     table=None,
     protocol=L.PROTO_NAKAMOTO,
     reward_scheme=L.REWARD_CONSTANT,
+    k=8,
+    table_dim=None,
 ):
     """Build a cpr_config. ``defenders=None`` applies the gym's rule
-    d = max(2, ceil(1 / (1 - gamma))) (gym/ocaml/cpr_gym/envs.py:146-153)."""
+    d = max(2, ceil(1 / (1 - gamma))) (gym/ocaml/cpr_gym/envs.py:146-153).
+    B_k tables (protocol=PROTO_BK) hold dim*dim*(k+1)*(k+1)*3 actions
+    (include/cpr_hip.h CPR_BK_POLICY_TABLE)."""
     if defenders is None and network == L.NET_SELFISH_MINING:
         if gamma >= 1:
             raise ValueError("gamma must be smaller than 1")
@@ -106,8 +110,18 @@ def make_config(
     c.activations = int(activations)
     c.seed = int(seed) & ((1 << 64) - 1)
     c.n_lanes = int(n_lanes)
+    c.k = int(k)
     keep = None
-    if table is not None:
+    if table is not None and protocol == L.PROTO_BK:
+        keep = np.ascontiguousarray(table, dtype=np.uint8).ravel()
+        per = (k + 1) * (k + 1) * 3
+        dim = int(round((keep.size // per) ** 0.5)) if table_dim is None else int(table_dim)
+        if dim * dim * per != keep.size:
+            raise ValueError("B_k policy table must have dim*dim*(k+1)*(k+1)*3 entries")
+        c.policy = L.BK_POLICY_TABLE
+        c.policy_table = keep.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8))
+        c.policy_table_dim = dim
+    elif table is not None:
         keep = np.ascontiguousarray(table, dtype=np.uint8)
         dim = int(round((keep.size // 2) ** 0.5))
         if dim * dim * 2 != keep.size:
@@ -127,6 +141,7 @@ class Batch:
         L.check(L.lib().cpr_batch_create(self.ctx.handle, ctypes.byref(config), ctypes.byref(h)))
         self.handle = h
         self.n_lanes = int(config.n_lanes)
+        self.obs_len = self.observation_spec()[0]
 
     def close(self):
         if self.handle:
@@ -166,7 +181,7 @@ class Batch:
 
     # ---- lockstep gym lanes
     def reset(self, mask=None, episode_ids=None):
-        obs = np.zeros((self.n_lanes, 4), dtype=np.float64)
+        obs = np.zeros((self.n_lanes, self.obs_len), dtype=np.float64)
         m = None if mask is None else np.ascontiguousarray(mask, dtype=np.uint8)
         e = None if episode_ids is None else np.ascontiguousarray(episode_ids, dtype=np.uint64)
         L.check(L.lib().cpr_reset(self.handle, L.ptr(m), L.ptr(e), L.ptr(obs)))
@@ -175,7 +190,7 @@ class Batch:
     def step(self, actions, with_info=True):
         n = self.n_lanes
         a = np.ascontiguousarray(actions, dtype=np.int32)
-        obs = np.zeros((n, 4), dtype=np.float64)
+        obs = np.zeros((n, self.obs_len), dtype=np.float64)
         rew = np.zeros(n, dtype=np.float64)
         done = np.zeros(n, dtype=np.uint8)
         info = None
@@ -205,17 +220,31 @@ class Batch:
         return obs, rew, done.astype(bool), info
 
     def observe_fields(self):
-        f = np.zeros((self.n_lanes, 4), dtype=np.int32)
+        f = np.zeros((self.n_lanes, self.obs_len), dtype=np.int32)
         L.check(L.lib().cpr_observe_fields(self.handle, L.ptr(f)))
         return f
 
     def policy_actions(self, policy, obs):
         o = np.ascontiguousarray(np.atleast_2d(obs), dtype=np.float64)
-        if o.shape[1] != 4:
+        if o.shape[1] != self.obs_len:
             raise ValueError("invalid dimensions")
         out = np.zeros(o.shape[0], dtype=np.int32)
         L.check(L.lib().cpr_policy_actions(self.handle, policy, L.ptr(o), o.shape[0], L.ptr(out)))
         return out
+
+    def rollout(self, n_steps, obs=None, reward=None, done=None, summary=None):
+        """Device rollout (cpr_rollout): every lane takes n_steps steps with the batch
+        policy, auto-resetting finished episodes. Optional outputs are device tensors
+        (e.g. torch.cuda) of shape [n_steps, n_lanes, obs_len] f64, [n_steps, n_lanes] f64
+        and [n_steps, n_lanes] u8; only their data pointers cross the ABI."""
+        s = summary if summary is not None else L.Summary()
+
+        def dptr(t):
+            return None if t is None else ctypes.c_void_p(int(t.data_ptr()))
+
+        L.check(L.lib().cpr_rollout(self.handle, int(n_steps), dptr(obs), dptr(reward),
+                                    dptr(done), ctypes.byref(s)))
+        return s
 
     def observation_spec(self):
         ol = ctypes.c_int32()

@@ -239,8 +239,23 @@ int cpr_last_launch(cpr_batch* b, double* kernel_ms, int64_t* activations);
 int cpr_reset(cpr_batch* b, const uint8_t* mask, const uint64_t* episode_ids, double* obs);
 int cpr_step(cpr_batch* b, const int32_t* actions, double* obs, double* reward,
              uint8_t* done, cpr_step_info* info);
-/* integer observation fields of every lane (public, private, diff, event) */
+/* integer observation fields of every lane: Nakamoto (public, private, diff, event);
+ * B_k the 8 bk_ssz fields (bk_ssz.ml:22-34) */
 int cpr_observe_fields(cpr_batch* b, int32_t* fields);
+
+/* Lockstep rollout on the device (B_k): every one of cfg->n_lanes lanes takes n_steps
+ * steps with the batch policy (cfg->policy, built-in or table) evaluated on the device;
+ * a lane whose episode ends restarts at episode id (previous id + n_lanes), like a gym
+ * VecEnv auto-reset (the observation written at a done step is the new episode's first).
+ * Continues from the lanes' current state (a first call without cpr_reset starts lane i at
+ * episode i). Outputs are optional DEVICE pointers, step-major:
+ *   obs_dev [n_steps][n_lanes][obs_len] f64, reward_dev [n_steps][n_lanes] f64
+ *   (engine.ml:223), done_dev [n_steps][n_lanes] u8.
+ * summary (host, accumulated): steps / activations of the whole rollout, the other fields
+ * over the episodes that finished in it. Synchronous; cpr_last_launch times the kernel.
+ * Replaces SB3 SubprocVecEnv rollouts over cpr_gym envs (experiments/train/ppo.py:278-285). */
+int cpr_rollout(cpr_batch* b, int64_t n_steps, double* obs_dev, double* reward_dev,
+                uint8_t* done_dev, cpr_summary* summary);
 
 /* policy evaluated on encoded observations (host): obs n x obs_len -> actions n */
 int cpr_policy_actions(cpr_batch* b, int32_t policy, const double* obs, int64_t n,

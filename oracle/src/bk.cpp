@@ -580,6 +580,7 @@ void bk_loop_task(const Network& net, int rng_mode, OcamlRandom* r, uint64_t see
   sim.proto = 2;
   sim.bk_k = k;
   sim.bk_scheme = scheme;
+  sim.zt_limit = 4096;
   const int n = (int)net.nodes.size();
   std::vector<std::unique_ptr<NodeImpl>> nodes;
   BkSszAttackerNode* att = nullptr;

@@ -309,6 +309,8 @@ void Sim::reward(Block* x) const {
 
 // simulator.ml:122-136
 Block* Sim::raw_append(bool pow, int node, const Draft& d) {
+  if (zt_limit > 0 && ++zt_appends > zt_limit)
+    throw std::runtime_error("zero-time append loop: more appends between two activations than the guard allows");
   auto v = std::make_unique<Block>();
   v->serial = (int)dag.size();
   if (pow) {
@@ -423,6 +425,7 @@ void Sim::handle_event(const Event& ev) {
     }
     case EV_CLOCK: {
       if (pending_finite_rx > 0) diag |= DIAG_OVERLAP;
+      zt_appends = 0;
       int node_id = rng->miner(c_activations);
       Draft d = nodes[node_id]->puzzle_payload();
       int id = (int)drafts.size();

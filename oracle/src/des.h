@@ -205,6 +205,11 @@ struct Sim {
   int proto = 0;
   int eth_scheme = 0;  // Ethereum incentive scheme: 0 = Constant, 1 = Discount
   int bk_k = 0;        // B_k votes per block
+  // guard (not in the reference): appends allowed between two activations; 0 = no limit.
+  // A B_k attacker policy that keeps adopting re-proposes on the same block at the same
+  // instant forever, which Simulator.loop (no step bound) would never leave.
+  int zt_limit = 0;
+  int zt_appends = 0;
   int bk_scheme = 0;   // B_k incentive scheme: 0 = Constant, 2 = Block
 
   Sim(const Network& net, SimRng* rng);

@@ -1,0 +1,249 @@
+// TEST INFRASTRUCTURE ONLY. Differential fuzzer for the B_k lane
+// (cpr_amd/csrc/bk_lane.h, compiled here for the host) against the CPU oracle's
+// restatement (oracle/src/bk.cpp), step by step on the same keyed stream: all eight
+// observation fields and the step info after every step; loop-mode tasks on the
+// two-agents network compared at the end. Prints one JSON summary line; exit code 1 on
+// any mismatch. Usage: bk_vs_oracle [episodes per config] [steps] [k]
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../cpr_amd/csrc/bk_lane.h"
+#include "../../oracle/src/bk.h"
+
+using namespace cpr;
+
+static uint32_t mix(uint64_t a, uint64_t b) {
+  uint64_t x = a * 0x9E3779B97F4A7C15ull ^ (b + 0x632BE59BD9B4E019ull);
+  x ^= x >> 31;
+  x *= 0xD6E8FEB86659FD93ull;
+  x ^= x >> 32;
+  return (uint32_t)x;
+}
+
+struct Cfg {
+  double alpha, gamma;
+  int defenders;
+  int policy;  // 0..3 bk_ssz policies, 4 = table, 5 = random actions, 6 = random release-heavy
+  int scheme;  // 0 Constant, 2 Block
+  int steps;
+  int two_agents;
+  int k;
+};
+
+struct Counters {
+  long episodes = 0, mismatches = 0, capacity = 0, steps = 0;
+};
+
+static std::vector<uint8_t> g_table;
+static int g_dim = 4;
+
+static bk::BkParams params_of(const Cfg& cf) {
+  bk::BkParams P{};
+  P.t_att = oracle::alpha_threshold(cf.alpha);
+  P.d = cf.two_agents ? 1 : cf.defenders;
+  P.n = P.d + 1;
+  P.net = cf.two_agents ? 1 : 0;
+  P.mode = cf.two_agents ? 1 : 0;
+  P.policy = cf.policy < 5 ? cf.policy : 0;
+  P.scheme = cf.scheme;
+  P.k = cf.k;
+  P.cap_v = 64;
+  while (P.cap_v < cf.steps + 64) P.cap_v <<= 1;
+  P.cap_q = P.cap_v / 2;
+  P.cap_e = 256 + 1024 * P.n + (cf.gamma == 0.0 ? 2 * P.d * cf.steps : 0);
+  P.cap_d = 64;
+  P.table_dim = g_dim;
+  P.table = g_table.data();
+  P.ev = 1.0;
+  P.delta = 1e-9;
+  const double dd = cf.defenders;
+  P.dmax = (dd - 1.) / dd * 1e-9 / cf.gamma;
+  P.max_steps = cf.steps;
+  P.activations = cf.steps;
+  P.max_progress = __builtin_inf();
+  P.max_time = __builtin_inf();
+  return P;
+}
+
+static bool run_gym(const Cfg& cf, uint64_t seed, uint64_t ep, Counters& C, std::string& why) {
+  oracle::GymParams gp;
+  gp.alpha = cf.alpha;
+  gp.gamma = cf.gamma;
+  gp.defenders = cf.defenders;
+  gp.max_steps = cf.steps;
+  gp.unit_obs = false;
+  oracle::GymBk g(gp, cf.k, cf.scheme, 1, nullptr, seed, ep);
+  double obs[8];
+  g.reset(obs);
+  oracle::BkTable tab;
+  tab.dim = g_dim;
+  tab.k = cf.k;
+  tab.actions = g_table;
+
+  const bk::BkParams P = params_of(cf);
+  std::vector<uint8_t> mem(bk::bk_lane_bytes(P));
+  const bk::BkMem M = bk::bk_mem_at(mem.data(), P);
+  const Stream S{(uint32_t)seed, (uint32_t)(seed >> 32), (uint32_t)ep, (uint32_t)(ep >> 32)};
+  bk::BkLane L;
+  L.gym_reset(P, S, M);
+  char buf[700];
+  bool ok = true;
+  for (int s = 0;; s++) {
+    const oracle::BkObs o = g.observe_int();
+    if (L.dead) {
+      C.capacity++;
+      if (getenv("CAPDBG"))
+        fprintf(stderr, "capacity why %d a=%g g=%g pol=%d step %d newest %d hused %d\n", L.dead,
+                cf.alpha, cf.gamma, cf.policy, s, L.newest, L.hused);
+      return true;
+    }
+    const bk::BkObs e = L.observe(P, M);
+    const int ov[8] = {o.public_blocks, o.private_blocks, o.diff_blocks, o.public_votes,
+                       o.private_votes_inclusive, o.private_votes_exclusive, o.lead, o.event};
+    const int ev[8] = {e.public_blocks, e.private_blocks, e.diff_blocks, e.public_votes,
+                       e.private_votes_inclusive, e.private_votes_exclusive, e.lead, e.event};
+    if (memcmp(ov, ev, sizeof ov) != 0) {
+      snprintf(buf, sizeof buf,
+               "step %d obs oracle (%d %d %d %d %d %d %d %d) lane (%d %d %d %d %d %d %d %d)", s,
+               ov[0], ov[1], ov[2], ov[3], ov[4], ov[5], ov[6], ov[7], ev[0], ev[1], ev[2], ev[3],
+               ev[4], ev[5], ev[6], ev[7]);
+      why = buf;
+      ok = false;
+      break;
+    }
+    int act;
+    if (cf.policy < 5) {
+      act = oracle::bk_policy(cf.policy, o, cf.k, &tab);
+      const int la = bk::bk_policy(P, e);
+      if (la != act) {
+        snprintf(buf, sizeof buf, "step %d policy oracle %d lane %d", s, act, la);
+        why = buf;
+        ok = false;
+        break;
+      }
+    } else {
+      const uint32_t r = mix(ep, s);
+      act = (int)(r % 8);
+      if (cf.policy == 6 && (r >> 8) % 3 != 0) act = 4 + 1 + (int)((r >> 12) % 2);  // Override/Match
+    }
+    bool done = false;
+    oracle::StepInfo info{};
+
+    g.step(act, obs, &done, &info);
+
+    bool ldone = false;
+    const int32_t hd = L.gym_step(P, S, M, act, &ldone);
+    C.steps++;
+    if (L.dead) {
+      C.capacity++;
+      if (getenv("CAPDBG"))
+        fprintf(stderr, "capacity why %d a=%g g=%g pol=%d step %d newest %d hused %d\n", L.dead,
+                cf.alpha, cf.gamma, cf.policy, s, L.newest, L.hused);
+      return true;
+    }
+    const bk::BVtx& hb = L.X(P, M, hd);
+    const double ra = hb.rew_att, rd = hb.rew_def;
+    const double prog = (double)(hb.height * cf.k);
+    if (ra != info.episode_reward_attacker || rd != info.episode_reward_defender ||
+        hb.height != info.head_height || prog != info.episode_progress ||
+        hb.time != info.episode_chain_time || L.now != info.episode_sim_time ||
+        L.c_act != info.episode_n_activations || hb.who != info.head_miner || ldone != done ||
+        L.newest + 1 != (int)g.sim->dag.size()) {
+      snprintf(buf, sizeof buf,
+               "step %d head lane (ra %.1f rd %.1f h %d tm %.17g t %.17g k %d m %d done %d v %d) "
+               "oracle (ra %.1f rd %.1f h %d tm %.17g t %.17g k %ld m %d done %d v %d)",
+               s, ra, rd, hb.height, hb.time, L.now, L.c_act, hb.who, (int)ldone, L.newest + 1,
+               info.episode_reward_attacker, info.episode_reward_defender, info.head_height,
+               info.episode_chain_time, info.episode_sim_time, info.episode_n_activations,
+               info.head_miner, (int)done, (int)g.sim->dag.size());
+      why = buf;
+      ok = false;
+      break;
+    }
+    if (done) break;
+  }
+  C.episodes++;
+  if (!ok) C.mismatches++;
+  return ok;
+}
+
+static bool run_loop(const Cfg& cf, uint64_t seed, uint64_t ep, Counters& C, std::string& why) {
+  oracle::BkTable tab;
+  tab.dim = g_dim;
+  tab.k = cf.k;
+  tab.actions = g_table;
+  oracle::BkLoopResult r;
+  oracle::bk_loop_task(oracle::Network::two_agents(1.0, cf.alpha), 1, nullptr, seed, ep, cf.k,
+                       cf.scheme, cf.policy, &tab, cf.steps, &r);
+  const bk::BkParams P = params_of(cf);
+  std::vector<uint8_t> mem(bk::bk_lane_bytes(P));
+  const bk::BkMem M = bk::bk_mem_at(mem.data(), P);
+  const Stream S{(uint32_t)seed, (uint32_t)(seed >> 32), (uint32_t)ep, (uint32_t)(ep >> 32)};
+  bk::BkLane L;
+  const int32_t hd = L.loop(P, S, M);
+  if (L.dead) {
+    C.capacity++;
+    return true;
+  }
+  const bk::BVtx& hb = L.X(P, M, hd);
+  C.episodes++;
+  C.steps += cf.steps;
+  if (hb.rew_att != r.rewards[0] || hb.rew_def != r.rewards[1] || hb.height != r.head_height ||
+      hb.time != r.head_time || L.act0 != r.activations[0] ||
+      L.c_act != r.activations[0] + r.activations[1] || hb.who != r.head_signer ||
+      L.newest + 1 != r.n_vertices) {
+    char buf[400];
+    snprintf(buf, sizeof buf,
+             "loop lane (ra %d rd %d h %d tm %.17g a0 %d v %d) oracle (%.1f %.1f %d %.17g %ld %ld)",
+             hb.rew_att, hb.rew_def, hb.height, hb.time, L.act0, L.newest + 1, r.rewards[0],
+             r.rewards[1], r.head_height, r.head_time, (long)r.activations[0],
+             (long)r.n_vertices);
+    why = buf;
+    C.mismatches++;
+    return false;
+  }
+  return true;
+}
+
+int main(int argc, char** argv) {
+  const int eps = argc > 1 ? atoi(argv[1]) : 10;
+  const int steps = argc > 2 ? atoi(argv[2]) : 300;
+  const int k = argc > 3 ? atoi(argv[3]) : 8;
+  const uint64_t seed = 0xB0B00000ull + (uint64_t)k;
+  // a random table policy over (pub, priv, public votes, private votes, event)
+  g_table.resize((size_t)g_dim * g_dim * (k + 1) * (k + 1) * 3);
+  for (size_t i = 0; i < g_table.size(); ++i) g_table[i] = (uint8_t)(mix(7, i) % 8);
+  std::vector<Cfg> cfgs;
+  const double alphas[] = {0.1, 0.25, 0.33, 0.45};
+  const double gammas[] = {0.0, 0.5, 0.9};
+  for (double a : alphas)
+    for (double g : gammas) {
+      const int d = std::max(2, (int)std::ceil(1.0 / (1.0 - g)));
+      for (int pol : {0, 1, 2, 3, 4, 5, 6})
+        for (int sch : {0, 2}) cfgs.push_back(Cfg{a, g, d, pol, sch, steps, 0, k});
+    }
+  cfgs.push_back(Cfg{0.4, 0.75, 7, 6, 0, steps, 0, k});
+  cfgs.push_back(Cfg{0.33, 0.3, 4, 5, 0, steps, 0, k});
+  for (double a : alphas)
+    for (int pol : {0, 1, 2, 3}) cfgs.push_back(Cfg{a, 0, 1, pol, 0, steps * 2, 1, k});
+  Counters C;
+  int shown = 0;
+  for (auto& cf : cfgs)
+    for (int e = 0; e < eps; e++) {
+      std::string why;
+      const bool ok = cf.two_agents ? run_loop(cf, seed, e, C, why) : run_gym(cf, seed, e, C, why);
+      if (!ok && shown < 10) {
+        shown++;
+        fprintf(stderr, "MISMATCH alpha=%g gamma=%g d=%d pol=%d scheme=%d two=%d ep=%d: %s\n",
+                cf.alpha, cf.gamma, cf.defenders, cf.policy, cf.scheme, cf.two_agents, e,
+                why.c_str());
+      }
+    }
+  printf("{\"episodes\": %ld, \"steps\": %ld, \"mismatches\": %ld, \"capacity\": %ld}\n",
+         C.episodes, C.steps, C.mismatches, C.capacity);
+  return C.mismatches ? 1 : 0;
+}

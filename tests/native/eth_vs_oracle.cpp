@@ -48,7 +48,7 @@ static eth::EthParams params_of(const Cfg& cf) {
   P.scheme = cf.scheme;
   P.cap_b = 1;
   while (P.cap_b < cf.steps + 2) P.cap_b <<= 1;
-  P.cap_e = 64 + 512 * P.n;
+  P.cap_e = 64 + 512 * P.n + (cf.gamma == 0.0 ? 2 * P.d * cf.steps : 0);
   P.ev = 1.0;
   P.delta = 1e-9;
   const double dd = cf.defenders;

@@ -30,13 +30,16 @@ def test_library_exports_every_declared_symbol():
 
 def test_version_and_registry():
     lib = L.lib()
-    assert lib.cpr_abi_version() == 2
+    assert lib.cpr_abi_version() == 3
     assert lib.cpr_version().decode().startswith("cpr-hip")
     from cpr_amd import device
 
     # Collection.add prepends (collection.ml:13): reverse of nakamoto_ssz.ml:442-450
     assert [n for n, _ in device.policy_registry()] == [
         "sapirshtein-2016-sm1", "eyal-sirer-2014", "simple", "honest"]
+    # bk_ssz.ml:404-415, same reversal
+    assert [n for n, _ in device.policy_registry(L.PROTO_BK)] == [
+        "avoid-loss", "minor-delay", "get-ahead", "honest"]
 
 
 def test_struct_layouts_match_header(tmp_path):
@@ -44,12 +47,13 @@ def test_struct_layouts_match_header(tmp_path):
     src.write_text(
         '#include <stdio.h>\n#include <stddef.h>\n#include "cpr_hip.h"\n'
         'int main(){printf("%zu %zu %zu %zu %zu\\n", sizeof(cpr_config), sizeof(cpr_episode_record),'
-        ' sizeof(cpr_summary), sizeof(cpr_step_info), offsetof(cpr_config, seed));return 0;}\n')
+        ' sizeof(cpr_summary), sizeof(cpr_step_info), offsetof(cpr_config, seed));'
+        'printf("%zu\\n", offsetof(cpr_config, k));return 0;}\n')
     exe = tmp_path / "sz"
     subprocess.run(["gcc", "-I", str(ROOT / "include"), "-o", str(exe), str(src)], check=True)
     got = [int(x) for x in subprocess.run([str(exe)], capture_output=True, text=True).stdout.split()]
     want = [ctypes.sizeof(L.Config), ctypes.sizeof(L.EpisodeRecord), ctypes.sizeof(L.Summary),
-            ctypes.sizeof(L.StepInfo), L.Config.seed.offset]
+            ctypes.sizeof(L.StepInfo), L.Config.seed.offset, L.Config.k.offset]
     assert got == want
 
 

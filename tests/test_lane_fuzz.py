@@ -40,3 +40,20 @@ def test_ethereum_lane_matches_oracle_fuzz():
     assert out["mismatches"] == 0, p.stderr[-2000:]
     assert out["episodes"] > 1000 and out["steps"] > 300000
     assert out["capacity"] <= out["episodes"] // 100
+
+
+def test_bk_lane_matches_oracle_fuzz():
+    # tests/native/bk_vs_oracle.cpp: cpr_amd/csrc/bk_lane.h (host build) vs the oracle's
+    # bk.cpp, every step: the 8 bk_ssz observation fields, the policy action, rewards,
+    # height, chain time, clock, activations, head signer and the vertex count; 4 policies
+    # + a random table + 2 random-action fuzzers x 2 reward schemes x alpha x gamma, and
+    # Simulator.loop tasks on the two-agents network; k = 8 and k = 3
+    subprocess.run(["make", "-s", "-C", str(ROOT / "tests" / "native")], check=True)
+    exe = ROOT / "tests" / "native" / "build" / "bk_vs_oracle"
+    for k, steps in [("8", "400"), ("3", "250")]:
+        p = subprocess.run([str(exe), "4", steps, k], capture_output=True, text=True,
+                           timeout=600)
+        out = json.loads(p.stdout.strip().splitlines()[-1])
+        assert p.returncode == 0, p.stderr[-2000:]
+        assert out["mismatches"] == 0, p.stderr[-2000:]
+        assert out["episodes"] > 700 and out["capacity"] == 0
