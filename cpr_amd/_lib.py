@@ -230,7 +230,7 @@ def _declare(L):
     L.cpr_reset.argtypes = [vp, vp, vp, vp]
     L.cpr_step.argtypes = [vp, vp, vp, vp, vp, P(StepInfo)]
     L.cpr_observe_fields.argtypes = [vp, vp]
-    L.cpr_rollout.argtypes = [vp, ctypes.c_int64, vp, vp, vp, P(Summary)]
+    L.cpr_rollout.argtypes = [vp, ctypes.c_int64, vp, vp, vp, ctypes.c_int, P(Summary)]
     L.cpr_policy_actions.argtypes = [vp, ctypes.c_int32, vp, ctypes.c_int64, vp]
     L.cpr_observation_spec.argtypes = [vp, P(ctypes.c_int32), P(ctypes.c_int32), vp, vp]
     L.cpr_policy_count.argtypes = [ctypes.c_int32]

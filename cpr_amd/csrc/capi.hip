@@ -900,8 +900,8 @@ const char* cpr_policy_name(int32_t protocol, int32_t index, int32_t* policy_id)
   return kNames[index];
 }
 
-int cpr_rollout(cpr_batch* b, int64_t n_steps, double* obs_dev, double* reward_dev,
-                uint8_t* done_dev, cpr_summary* summary) {
+int cpr_rollout(cpr_batch* b, int64_t n_steps, double* obs, double* reward, uint8_t* done,
+                int outputs_on_device, cpr_summary* summary) {
   if (!b || !summary) return fail(CPR_E_INVALID_ARG, "NULL argument");
   if (b->cfg.protocol != CPR_PROTO_BK)
     return fail(CPR_E_UNSUPPORTED, "cpr_rollout is implemented for B_k");
@@ -916,6 +916,26 @@ int cpr_rollout(cpr_batch* b, int64_t n_steps, double* obs_dev, double* reward_d
     HIP_TRY(hipEventCreate(&b->ev0));
     HIP_TRY(hipEventCreate(&b->ev1));
   }
+  const int64_t cells = n_steps * b->cfg.n_lanes;
+  const int ol = obs_len_of(b->cfg);
+  double* obs_dev = obs;
+  double* reward_dev = reward;
+  uint8_t* done_dev = done;
+  DevBuf so, sr, sd;
+  if (!outputs_on_device) {
+    if (obs) {
+      HIP_TRY(so.ensure((size_t)cells * ol * 8));
+      obs_dev = (double*)so.p;
+    }
+    if (reward) {
+      HIP_TRY(sr.ensure((size_t)cells * 8));
+      reward_dev = (double*)sr.p;
+    }
+    if (done) {
+      HIP_TRY(sd.ensure((size_t)cells));
+      done_dev = (uint8_t*)sd.p;
+    }
+  }
   const double* tabs = (const double*)b->tabs_dev.p;
   HIP_TRY(hipEventRecord(b->ev0, st));
   HIP_TRY(launch_bk_rollout(b->BP, b->cfg.seed, (uint8_t*)b->bk_lmem.p, b->bk_bytes,
@@ -925,7 +945,15 @@ int cpr_rollout(cpr_batch* b, int64_t n_steps, double* obs_dev, double* reward_d
   HIP_TRY(hipEventRecord(b->ev1, st));
   cpr_summary s;
   HIP_TRY(hipMemcpyAsync(&s, b->summary.p, sizeof(s), hipMemcpyDeviceToHost, st));
+  if (!outputs_on_device) {
+    if (obs) HIP_TRY(hipMemcpyAsync(obs, obs_dev, (size_t)cells * ol * 8, hipMemcpyDeviceToHost, st));
+    if (reward) HIP_TRY(hipMemcpyAsync(reward, reward_dev, (size_t)cells * 8, hipMemcpyDeviceToHost, st));
+    if (done) HIP_TRY(hipMemcpyAsync(done, done_dev, (size_t)cells, hipMemcpyDeviceToHost, st));
+  }
   HIP_TRY(hipStreamSynchronize(st));
+  so.release();
+  sr.release();
+  sd.release();
   float ms = 0.f;
   HIP_TRY(hipEventElapsedTime(&ms, b->ev0, b->ev1));
   b->last_ms = ms;

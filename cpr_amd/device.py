@@ -232,19 +232,28 @@ class Batch:
         L.check(L.lib().cpr_policy_actions(self.handle, policy, L.ptr(o), o.shape[0], L.ptr(out)))
         return out
 
-    def rollout(self, n_steps, obs=None, reward=None, done=None, summary=None):
+    def rollout(self, n_steps, outputs=False, summary=None, device_outputs=None):
         """Device rollout (cpr_rollout): every lane takes n_steps steps with the batch
-        policy, auto-resetting finished episodes. Optional outputs are device tensors
-        (e.g. torch.cuda) of shape [n_steps, n_lanes, obs_len] f64, [n_steps, n_lanes] f64
-        and [n_steps, n_lanes] u8; only their data pointers cross the ABI."""
+        policy, auto-resetting finished episodes. ``outputs=True`` returns host arrays
+        obs [n_steps, n_lanes, obs_len], reward [n_steps, n_lanes], done [n_steps, n_lanes];
+        ``device_outputs=(obs_ptr, reward_ptr, done_ptr)`` writes to caller-owned device
+        memory instead. Returns the summary (and the arrays if requested)."""
         s = summary if summary is not None else L.Summary()
-
-        def dptr(t):
-            return None if t is None else ctypes.c_void_p(int(t.data_ptr()))
-
-        L.check(L.lib().cpr_rollout(self.handle, int(n_steps), dptr(obs), dptr(reward),
-                                    dptr(done), ctypes.byref(s)))
-        return s
+        n = self.n_lanes
+        if device_outputs is not None:
+            o, r, d = (None if x is None else ctypes.c_void_p(int(x)) for x in device_outputs)
+            L.check(L.lib().cpr_rollout(self.handle, int(n_steps), o, r, d, 1, ctypes.byref(s)))
+            return s
+        if not outputs:
+            L.check(L.lib().cpr_rollout(self.handle, int(n_steps), None, None, None, 0,
+                                        ctypes.byref(s)))
+            return s
+        obs = np.zeros((n_steps, n, self.obs_len))
+        rew = np.zeros((n_steps, n))
+        done = np.zeros((n_steps, n), dtype=np.uint8)
+        L.check(L.lib().cpr_rollout(self.handle, int(n_steps), L.ptr(obs), L.ptr(rew),
+                                    L.ptr(done), 0, ctypes.byref(s)))
+        return s, obs, rew, done.astype(bool)
 
     def observation_spec(self):
         ol = ctypes.c_int32()

@@ -248,14 +248,15 @@ int cpr_observe_fields(cpr_batch* b, int32_t* fields);
  * a lane whose episode ends restarts at episode id (previous id + n_lanes), like a gym
  * VecEnv auto-reset (the observation written at a done step is the new episode's first).
  * Continues from the lanes' current state (a first call without cpr_reset starts lane i at
- * episode i). Outputs are optional DEVICE pointers, step-major:
- *   obs_dev [n_steps][n_lanes][obs_len] f64, reward_dev [n_steps][n_lanes] f64
- *   (engine.ml:223), done_dev [n_steps][n_lanes] u8.
+ * episode i). Outputs are optional, step-major:
+ *   obs [n_steps][n_lanes][obs_len] f64, reward [n_steps][n_lanes] f64 (engine.ml:223),
+ *   done [n_steps][n_lanes] u8; device pointers if outputs_on_device != 0, else host
+ *   pointers (staged through library-owned device buffers).
  * summary (host, accumulated): steps / activations of the whole rollout, the other fields
  * over the episodes that finished in it. Synchronous; cpr_last_launch times the kernel.
  * Replaces SB3 SubprocVecEnv rollouts over cpr_gym envs (experiments/train/ppo.py:278-285). */
-int cpr_rollout(cpr_batch* b, int64_t n_steps, double* obs_dev, double* reward_dev,
-                uint8_t* done_dev, cpr_summary* summary);
+int cpr_rollout(cpr_batch* b, int64_t n_steps, double* obs, double* reward, uint8_t* done,
+                int outputs_on_device, cpr_summary* summary);
 
 /* policy evaluated on encoded observations (host): obs n x obs_len -> actions n */
 int cpr_policy_actions(cpr_batch* b, int32_t policy, const double* obs, int64_t n,
