@@ -24,6 +24,19 @@ CPR_E_STATE = -5
 PROTO_NAKAMOTO = 0
 PROTO_ETHEREUM = 1
 PROTO_BK = 2
+PROTO_TAILSTORM = 3
+REWARD_PUNISH = 3
+REWARD_HYBRID = 4
+SELECT_ALTRUISTIC = 0
+SELECT_HEURISTIC = 1
+SELECT_OPTIMAL = 2
+TS_POLICY_HONEST = 0
+TS_POLICY_GET_AHEAD = 1
+TS_POLICY_MINOR_DELAY = 2
+TS_POLICY_AVOID_LOSS = 3
+TS_POLICY_AVOID_LOSS_A = 4
+TS_POLICY_AVOID_LOSS_B = 5
+TS_POLICY_LONG_DELAY = 6
 REWARD_CONSTANT = 0
 REWARD_DISCOUNT = 1
 REWARD_BLOCK = 2
@@ -78,7 +91,7 @@ class Config(ctypes.Structure):
         ("seed", ctypes.c_uint64),
         ("n_lanes", ctypes.c_int64),
         ("k", ctypes.c_int32),
-        ("reserved", ctypes.c_int32),
+        ("subblock_selection", ctypes.c_int32),
     ]
 
 

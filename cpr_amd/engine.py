@@ -25,6 +25,21 @@ MAX_INT = (1 << 62) - 1  # OCaml max_int on 64-bit
 _ACTIONS = ["Adopt", "Override", "Match", "Wait"]  # nakamoto_ssz.ml:216-254
 _EVENTS = ["`ProofOfWork", "`Network"]  # ssz_tools.ml:527-531
 
+# per attack space: action names (Variants.to_name, rank order), observation record fields,
+# event values (ssz_tools.ml event_to_string)
+_ACTION8 = ["Adopt_Prolong", "Override_Prolong", "Match_Prolong", "Wait_Prolong",
+            "Adopt_Proceed", "Override_Proceed", "Match_Proceed", "Wait_Proceed"]  # ssz_tools.ml:230-263
+_SPACES = {
+    L.PROTO_NAKAMOTO: dict(actions=_ACTIONS, events=_EVENTS,
+                           fields=["public_blocks", "private_blocks", "diff_blocks", "event"],
+                           bools=()),
+    L.PROTO_BK: dict(actions=_ACTION8, events=["`Append", "`ProofOfWork", "`Network"],
+                     fields=["public_blocks", "private_blocks", "diff_blocks", "public_votes",
+                             "private_votes_inclusive", "private_votes_exclusive", "lead",
+                             "event"],
+                     bools=("lead",)),  # bk_ssz.ml:22-34,123-143
+}
+
 
 class InstantiatedEnv:
     """Stands in for the reference's "ocaml.instantiated_env" capsule."""
@@ -88,6 +103,9 @@ def create(
         seed = int(os.environ["CPR_SEED"]) if "CPR_SEED" in os.environ else \
             int.from_bytes(os.urandom(8), "little")
     cfg, keep = device.make_config(
+        protocol=proto.protocol_id,
+        k=proto.params.get("k", 8),
+        reward_scheme=proto.params.get("reward_scheme", L.REWARD_CONSTANT),
         alpha=p["alpha"],
         gamma=p["gamma"],
         defenders=p["defenders"],
@@ -120,9 +138,13 @@ def _miner_str(m):
     return "n/a" if m < 0 else str(m)
 
 
+def _space(ienv):
+    return _SPACES[ienv.proto.protocol_id]
+
+
 def step(ienv, action):
     a = int(action)
-    if a < 0 or a >= len(_ACTIONS):
+    if a < 0 or a >= len(_space(ienv)["actions"]):
         raise IndexError("index out of bounds")  # Action.of_int on table (nakamoto_ssz.ml:252)
     obs, rew, done, inf = ienv.batch.step(np.array([a], dtype=np.int32))
     ra = float(inf["episode_reward_attacker"][0])
@@ -145,10 +167,18 @@ def step(ienv, action):
         "episode_sim_time": st,
         "episode_n_steps": int(inf["episode_n_steps"][0]),
         "episode_n_activations": int(inf["episode_n_activations"][0]),
-        "protocol_family": "nakamoto",
-        "head_height": int(inf["head_height"][0]),
-        "head_miner": _miner_str(int(inf["head_miner"][0])),
     }
+    if ienv.proto.protocol_id == L.PROTO_BK:
+        # bk.ml:21-24 (Protocol.info), :53-58 (Referee.info of a block)
+        info["protocol_family"] = "bk"
+        info["protocol_k"] = ienv.proto.params["k"]
+        info["protocol_incentive_scheme"] = ienv.proto.params["reward"]
+        info["head_kind"] = "block"
+        info["head_height"] = int(inf["head_height"][0])
+    else:
+        info["protocol_family"] = "nakamoto"
+        info["head_height"] = int(inf["head_height"][0])
+        info["head_miner"] = _miner_str(int(inf["head_miner"][0]))
     ienv._last = (ra, rd, prog, ct, st)
     return obs[0].copy(), float(rew[0]), bool(done[0]), info
 
@@ -156,11 +186,12 @@ def step(ienv, action):
 def policies(ienv):
     """name -> callable(obs) -> int, in the reference's registry order."""
     out = {}
-    for name, pid in device.policy_registry():
+    n = len(_space(ienv)["fields"])
+    for name, pid in device.policy_registry(ienv.proto.protocol_id):
 
         def fn(obs, _pid=pid):
             o = np.asarray(obs, dtype=np.float64)
-            if o.shape != (4,):
+            if o.shape != (n,):
                 raise ValueError("invalid dimensions")
             return int(ienv.batch.policy_actions(_pid, o)[0])
 
@@ -181,20 +212,23 @@ def observation_high(ienv):
 
 
 def _observe_hum(ienv):
+    # Observation.to_string: "field: value" per record field (nakamoto_ssz.ml, bk_ssz.ml:123-143)
+    sp = _space(ienv)
     f = ienv.batch.observe_fields()[0]
-    return "\n".join(
-        [
-            f"public_blocks: {f[0]}",
-            f"private_blocks: {f[1]}",
-            f"diff_blocks: {f[2]}",
-            f"event: {_EVENTS[f[3]]}",
-        ]
-    )
+    lines = []
+    for name, v in zip(sp["fields"], f):
+        if name == "event":
+            lines.append(f"event: {sp['events'][v]}")
+        elif name in sp["bools"]:
+            lines.append(f"{name}: {'true' if v else 'false'}")
+        else:
+            lines.append(f"{name}: {v}")
+    return "\n".join(lines)
 
 
 def to_string(ienv):
     # engine.ml:250-257
-    actions = " | ".join(f"({i}) {a}" for i, a in enumerate(_ACTIONS))
+    actions = " | ".join(f"({i}) {a}" for i, a in enumerate(_space(ienv)["actions"]))
     return "%s; %s; α=%.2f attacker\n%s\nActions: %s" % (
         ienv.proto.description,
         ienv.proto.attack_info,

@@ -1,15 +1,19 @@
 """Drop-in for the reference's Python module ``protocols``
-(simulator/gym/cpr_gym_engine.ml:438-577): constructors returning protocol specs that
-``engine.create`` accepts. Only Nakamoto + SSZ'16 attack space runs on the device engine
-in this build; the other constructors exist with the reference's signatures and raise.
+(simulator/gym/cpr_gym_engine.ml:165-304): constructors returning protocol specs that
+``engine.create`` accepts. Nakamoto and B_k run as lockstep lanes on the device engine;
+the other constructors exist with the reference's signatures and raise.
 """
+
+from . import _lib as L
 
 
 class Protocol:
     """Stands in for the reference's "ocaml.protocol" capsule."""
 
-    def __init__(self, key, description, attack_info, unit_observation, **params):
+    def __init__(self, key, description, attack_info, unit_observation,
+                 protocol_id=L.PROTO_NAKAMOTO, **params):
         self.key = key
+        self.protocol_id = protocol_id
         self.description = description
         self.attack_info = attack_info
         self.unit_observation = bool(unit_observation)
@@ -37,7 +41,28 @@ def _not_on_device(name):
 
 
 ethereum = _not_on_device("ethereum")  # (reward, unit_observation)
-bk = _not_on_device("bk")  # (reward, k, unit_observation)
+
+
+def _option(choice, value):
+    # options.ml:56-77 of_string_exn: "'x' is not a valid parameter choice, try 'a' or 'b'"
+    if value in choice:
+        return value
+    quoted = [f"'{c}'" for c in choice]
+    alts = quoted[0] if len(quoted) == 1 else ", ".join(quoted[:-1]) + " or " + quoted[-1]
+    raise ValueError(f"'{value}' is not a valid parameter choice, try {alts}")
+
+
+def bk(reward, k, unit_observation):
+    """bk_ssz attack space over B_k (cpr_gym_engine.ml:193-206, cpr_protocols.ml:53-72)."""
+    reward = _option(["block", "constant"], reward)  # bk.ml:3 incentive_schemes
+    k = int(k)
+    if k < 1:
+        raise ValueError("k must be positive")
+    info = "SSZ'16-like attack space with %s observations" % ("unit" if unit_observation else "raw")
+    return Protocol(f"bk-{k}-{reward}", f"Bₖ with k={k} and {reward} rewards", info,
+                    unit_observation, protocol_id=L.PROTO_BK, k=k, reward=reward,
+                    reward_scheme=L.REWARD_BLOCK if reward == "block" else L.REWARD_CONSTANT)
+
 spar = _not_on_device("spar")
 stree = _not_on_device("stree")
 sdag = _not_on_device("sdag")

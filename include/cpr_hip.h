@@ -53,7 +53,9 @@ enum cpr_status {
 enum cpr_protocol {
   CPR_PROTO_NAKAMOTO = 0, /* nakamoto.ml + nakamoto_ssz.ml */
   CPR_PROTO_ETHEREUM = 1, /* ethereum.ml Byzantium + ethereum_ssz.ml (cpr_protocols.ml:39-49) */
-  CPR_PROTO_BK = 2        /* bk.ml + bk_ssz.ml (cpr_protocols.ml:53-72), k = cpr_config.k */
+  CPR_PROTO_BK = 2,       /* bk.ml + bk_ssz.ml (cpr_protocols.ml:53-72), k = cpr_config.k */
+  CPR_PROTO_TAILSTORM = 3 /* tailstorm.ml + tailstorm_ssz.ml (cpr_protocols.ml:153-175),
+                             k = cpr_config.k, selection = cpr_config.subblock_selection */
 };
 
 /* incentive schemes (ethereum.ml:3,173-197; bk.ml:3,151-176) */
@@ -61,7 +63,29 @@ enum cpr_reward_scheme {
   CPR_REWARD_CONSTANT = 0, /* Ethereum `Constant` (whitepaper): uncle 15/16;
                               B_k `Constant`: 1 per confirmed vote to its miner */
   CPR_REWARD_DISCOUNT = 1, /* Ethereum `Discount` (Byzantium): uncle (8 - dh) / 8 */
-  CPR_REWARD_BLOCK = 2     /* B_k `Block`: k to the block's signer (leader) */
+  CPR_REWARD_BLOCK = 2,    /* B_k `Block`: k to the block's signer (leader) */
+  CPR_REWARD_PUNISH = 3,   /* Tailstorm `Punish`: 1 per vote on the longest vote branch */
+  CPR_REWARD_HYBRID = 4    /* Tailstorm `Hybrid`: depth/k per vote on the longest branch;
+                              Tailstorm also takes CONSTANT (1 per vote) and DISCOUNT (depth/k
+                              per confirmed vote), tailstorm.ml:3,204-227 */
+};
+
+/* Tailstorm sub-block (quorum) selection, tailstorm.ml:4,262-507 */
+enum cpr_subblock_selection {
+  CPR_SELECT_ALTRUISTIC = 0,
+  CPR_SELECT_HEURISTIC = 1,
+  CPR_SELECT_OPTIMAL = 2 /* brute force over n-choose-k <= 100, else heuristic */
+};
+
+/* policy ids of the tailstorm_ssz attack space (tailstorm_ssz.ml:365-472) */
+enum cpr_tailstorm_policy {
+  CPR_TS_POLICY_HONEST = 0,
+  CPR_TS_POLICY_GET_AHEAD = 1,
+  CPR_TS_POLICY_MINOR_DELAY = 2,
+  CPR_TS_POLICY_AVOID_LOSS = 3,   /* avoid_loss_alt, registered as "avoid-loss" */
+  CPR_TS_POLICY_AVOID_LOSS_A = 4, /* avoid_loss */
+  CPR_TS_POLICY_AVOID_LOSS_B = 5, /* avoid_loss_alt2 */
+  CPR_TS_POLICY_LONG_DELAY = 6
 };
 
 /* policy ids of the bk_ssz attack space (bk_ssz.ml:346-415; "avoid-loss" is avoid_loss_alt) */
@@ -153,8 +177,8 @@ typedef struct cpr_config {
   int64_t activations;       /* LOOP mode: activations per episode */
   uint64_t seed;             /* keyed-stream seed */
   int64_t n_lanes;           /* lockstep lanes for cpr_reset/cpr_step; 0 = none */
-  int32_t k;                 /* B_k: votes per block (bk.ml:7), >= 1 */
-  int32_t reserved;
+  int32_t k;                 /* B_k / Tailstorm: votes per block (bk.ml:7), >= 1 */
+  int32_t subblock_selection;/* Tailstorm: enum cpr_subblock_selection */
 } cpr_config;
 
 /* one finished episode; identical layout is produced by the CPU oracle */

@@ -291,6 +291,7 @@ void Sim::schedule_pow() {
 bool Sim::validity(const Block* b) const {
   if (proto == 1) return eth_validity(b);
   if (proto == 2) return bk_validity(b, bk_k);
+  if (proto == 3) return ts_validity(b, bk_k);
   if (!b->has_pow || b->parents.size() != 1) return false;
   return b->value.height == b->parents[0]->value.height + 1 && b->value.miner >= 0;
 }
@@ -302,6 +303,10 @@ void Sim::reward(Block* x) const {
   }
   if (proto == 2) {
     bk_reward(x, bk_scheme, bk_k, x->rewards);
+    return;
+  }
+  if (proto == 3) {
+    ts_reward(x, bk_scheme, bk_k, x->rewards);
     return;
   }
   if (x->value.miner >= 0) x->rewards[x->value.miner] += 1.;
@@ -343,10 +348,17 @@ Block* Sim::append(bool pow, int node, const Draft& d) {
       candidates.assign(d.parents[0]->children_app.rbegin(), d.parents[0]->children_app.rend());
     for (auto* y : candidates) {
       if (!(y->value == d.data) || y->signature != -1) continue;
-      if (y->parents.size() != d.parents.size()) throw std::invalid_argument("List.for_all2");
+      // List.for_all2 (stdlib list.ml): false at the first unequal pair; raises
+      // Invalid_argument only if all compared pairs are equal and the lengths differ
       bool eq = true;
-      for (size_t i = 0; i < y->parents.size(); i++)
-        if (y->parents[i]->serial != d.parents[i]->serial) eq = false;
+      size_t i = 0;
+      for (; i < y->parents.size() && i < d.parents.size(); i++)
+        if (y->parents[i]->serial != d.parents[i]->serial) {
+          eq = false;
+          break;
+        }
+      if (eq && y->parents.size() != d.parents.size())
+        throw std::invalid_argument("List.for_all2");
       if (eq) return y;  // `Redundant
     }
   }
@@ -412,7 +424,7 @@ void Sim::handle_event(const Event& ev) {
       if (!visible(n, ev.blk)) throw std::runtime_error("assert: OnNode invisible");
       for (auto* p : ev.blk->parents)
         if (!visible(n, p)) throw std::runtime_error("assert: OnNode parent invisible");
-      if (ev.kind == K_NETWORK && n != 0 && proto != 2) {
+      if (ev.kind == K_NETWORK && n != 0 && proto < 2) {
         // diagnostic: equal-height candidate delivered at the same instant as the current tip
         Block* cur = nodes[n]->preferred();
         if (cur && cur != ev.blk && cur->value.height == ev.blk->value.height &&

@@ -68,6 +68,10 @@ void eth_reward(const Block* x, int scheme, std::vector<double>& r);
 // (bk.ml:151-176)
 bool bk_validity(const Block* b, int k);
 void bk_reward(const Block* x, int scheme, int k, std::vector<double>& r);
+// Tailstorm referee pieces (tailstorm.cpp): validity (tailstorm.ml:156-180), rewards
+// (tailstorm.ml:204-233)
+bool ts_validity(const Block* b, int k);
+void ts_reward(const Block* x, int scheme, int k, std::vector<double>& r);
 
 struct Draft {
   std::vector<Block*> parents;
@@ -201,7 +205,8 @@ struct Sim {
   int n_nodes = 0;
   uint32_t diag = 0;
   int pending_finite_rx = 0;
-  // protocol of the referee: 0 = Nakamoto, 1 = Ethereum (Byzantium parameters), 2 = B_k
+  // protocol of the referee: 0 = Nakamoto, 1 = Ethereum (Byzantium parameters), 2 = B_k,
+  // 3 = Tailstorm (bk_k = k, bk_scheme = the Tailstorm incentive scheme)
   int proto = 0;
   int eth_scheme = 0;  // Ethereum incentive scheme: 0 = Constant, 1 = Discount
   int bk_k = 0;        // B_k votes per block
@@ -231,6 +236,8 @@ struct Sim {
   double progress(const Block* b) const {
     if (proto == 2)  // bk.ml:42-46
       return (double)(b->value.height * bk_k + (b->value.kind == 1 ? 1 : 0));
+    if (proto == 3)  // tailstorm.ml:72: height * k + depth
+      return (double)(b->value.height * bk_k + (b->value.kind == 1 ? b->value.work : 0));
     return proto == 1 ? (double)b->value.work : (double)b->value.height;
   }
   // nakamoto.ml:43-48 and ethereum.ml:159-162 (both: first maximum height)

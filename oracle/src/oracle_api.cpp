@@ -12,6 +12,7 @@
 #include "des.h"
 #include "ethereum.h"
 #include "bk.h"
+#include "tailstorm.h"
 #include "ocaml_sort.h"
 
 using namespace oracle;
@@ -398,9 +399,35 @@ static int run_bk_gym_episode(const cpr_config* c, const BkTable* tab, uint64_t 
   return 0;
 }
 
+static int run_ts_gym_episode(const cpr_config* c, uint64_t ep, cpr_episode_record* rec) {
+  GymTailstorm g(params_of(c), c->k, c->reward_scheme, c->subblock_selection, 1, nullptr,
+                 c->seed, ep);
+  double obs[TS_OBS_LEN];
+  g.reset(obs);
+  bool done = false;
+  StepInfo info{};
+  while (!done) {
+    int a = ts_policy(c->policy, g.observe_int(), c->k);
+    g.step(a, obs, &done, &info);
+  }
+  rec->reward_attacker = info.episode_reward_attacker;
+  rec->reward_defender = info.episode_reward_defender;
+  rec->progress = info.episode_progress;
+  rec->chain_time = info.episode_chain_time;
+  rec->sim_time = info.episode_sim_time;
+  rec->n_steps = info.episode_n_steps;
+  rec->n_activations = info.episode_n_activations;
+  rec->head_height = info.head_height;
+  rec->head_miner = info.head_miner;
+  rec->status = 0;
+  rec->head_work = 0;
+  return 0;
+}
+
 static int run_gym_episode(const cpr_config* c, const TablePolicy* tab, uint64_t ep,
                            cpr_episode_record* rec) {
   if (c->protocol == CPR_PROTO_ETHEREUM) return run_eth_gym_episode(c, ep, rec);
+  if (c->protocol == CPR_PROTO_TAILSTORM) return run_ts_gym_episode(c, ep, rec);
   if (c->protocol == CPR_PROTO_BK) {
     BkTable bt = bk_table_of(c);
     return run_bk_gym_episode(c, &bt, ep, rec);
@@ -437,6 +464,24 @@ static int run_loop_episode(const cpr_config* c, uint64_t ep, cpr_episode_record
   if (c->network != CPR_NET_TWO_AGENTS) {
     set_err("oracle loop mode: two-agents network only");
     return -2;
+  }
+  if (c->protocol == CPR_PROTO_TAILSTORM) {
+    TsLoopResult r;
+    ts_loop_task(Network::two_agents(c->activation_delay, c->alpha), 1, nullptr, c->seed, ep,
+                 c->k, c->reward_scheme, c->subblock_selection, c->policy, (int)c->activations,
+                 &r);
+    rec->reward_attacker = r.rewards[0];
+    rec->reward_defender = r.rewards[1];
+    rec->progress = r.head_progress;
+    rec->chain_time = r.head_time;
+    rec->sim_time = 0.0;
+    rec->n_steps = 0;
+    rec->n_activations = r.activations[0] + r.activations[1];
+    rec->head_height = r.head_height;
+    rec->head_miner = -1;
+    rec->status = 0;
+    rec->head_work = 0;
+    return 0;
   }
   if (c->protocol == CPR_PROTO_BK) {
     BkTable bt = bk_table_of(c);
@@ -604,6 +649,125 @@ int oracle_bk_loop(int net_kind, int n_nodes, double alpha, double activation_de
     *head_progress = r.head_progress;
     *head_height = r.head_height;
     *head_signer = r.head_signer;
+    *n_vertices = r.n_vertices;
+    return 0;
+  } catch (std::exception& e) {
+    set_err(e.what());
+    return -1;
+  }
+}
+
+// ---------------- Tailstorm (tailstorm.ml, tailstorm_ssz.ml)
+int oracle_ts_policy(int policy, const int32_t obs[10], int k) {
+  TsObs o{obs[0], obs[1], obs[2], obs[3], obs[4], obs[5], obs[6], obs[7], obs[8], obs[9]};
+  return ts_policy(policy, o, k);
+}
+void oracle_ts_obs_to_floats(const int32_t obs[10], int unit, int k, double out[10]) {
+  TsObs o{obs[0], obs[1], obs[2], obs[3], obs[4], obs[5], obs[6], obs[7], obs[8], obs[9]};
+  ts_obs_to_floats(o, unit != 0, k, out);
+}
+void oracle_ts_obs_of_floats(const double in[10], int unit, int k, int32_t out[10]) {
+  TsObs o = ts_obs_of_floats(in, unit != 0, k);
+  const int32_t v[10] = {o.public_blocks,           o.private_blocks,
+                         o.diff_blocks,             o.public_votes,
+                         o.private_votes_inclusive, o.private_votes_exclusive,
+                         o.public_depth,            o.private_depth_inclusive,
+                         o.private_depth_exclusive, o.event};
+  memcpy(out, v, sizeof(v));
+}
+int64_t oracle_n_choose_k(int64_t n, int64_t k) {
+  try {
+    return ocaml_n_choose_k(n, k);
+  } catch (std::exception& e) {
+    set_err(e.what());
+    return -1;
+  }
+}
+void* oracle_ts_gym_new(const cpr_config* c, int rng_mode, void* ocaml_rng, uint64_t episode) {
+  try {
+    return new GymTailstorm(params_of(c), c->k, c->reward_scheme, c->subblock_selection,
+                            rng_mode, (OcamlRandom*)ocaml_rng, c->seed, episode);
+  } catch (std::exception& e) {
+    set_err(e.what());
+    return nullptr;
+  }
+}
+void oracle_ts_gym_free(void* g) { delete (GymTailstorm*)g; }
+int oracle_ts_gym_reset(void* g, double obs[10]) {
+  try {
+    ((GymTailstorm*)g)->reset(obs);
+    return 0;
+  } catch (std::exception& e) {
+    set_err(e.what());
+    return -1;
+  }
+}
+int oracle_ts_gym_obs_fields(void* g, int32_t out[10]) {
+  TsObs o = ((GymTailstorm*)g)->observe_int();
+  const int32_t v[10] = {o.public_blocks,           o.private_blocks,
+                         o.diff_blocks,             o.public_votes,
+                         o.private_votes_inclusive, o.private_votes_exclusive,
+                         o.public_depth,            o.private_depth_inclusive,
+                         o.private_depth_exclusive, o.event};
+  memcpy(out, v, sizeof(v));
+  return 0;
+}
+int oracle_ts_gym_step(void* g, int action, double obs[10], double* reward, int* done,
+                       double info_out[15]) {
+  try {
+    bool d = false;
+    StepInfo i;
+    GymTailstorm* e = (GymTailstorm*)g;
+    *reward = e->step(action, obs, &d, &i);
+    *done = d ? 1 : 0;
+    if (info_out) {
+      double v[15] = {i.step_reward_attacker,    i.step_reward_defender,
+                      i.step_progress,           i.step_chain_time,
+                      i.step_sim_time,           i.episode_reward_attacker,
+                      i.episode_reward_defender, i.episode_progress,
+                      i.episode_chain_time,      i.episode_sim_time,
+                      (double)i.episode_n_steps, (double)i.episode_n_activations,
+                      (double)i.head_height,     (double)i.head_miner,
+                      (double)e->sim->dag.size()};
+      memcpy(info_out, v, sizeof(v));
+    }
+    return 0;
+  } catch (std::exception& e) {
+    set_err(e.what());
+    return -1;
+  }
+}
+// Simulator.loop task for Tailstorm. net_kind 0: two_agents(alpha); 1: symmetric_clique of
+// n_nodes with exponential(prop_ev) delays. policy < 0: node 0 honest.
+int oracle_ts_loop(int net_kind, int n_nodes, double alpha, double activation_delay,
+                   double prop_ev, int rng_mode, void* rng, uint64_t seed, uint64_t episode,
+                   int k, int scheme, int selection, int policy, int activations,
+                   double* rewards_out, int64_t* acts_out, double* head_time,
+                   double* head_progress, int32_t* head_height, int64_t* n_vertices) {
+  try {
+    Network net;
+    if (net_kind == 0) {
+      net = Network::two_agents(activation_delay, alpha);
+    } else {
+      net.flooding = false;
+      net.activation_delay = activation_delay;
+      net.nodes.resize(n_nodes);
+      for (int i = 0; i < n_nodes; ++i) {
+        net.nodes[i].compute = 1. / (double)n_nodes;
+        for (int j = 0; j < n_nodes - 1; ++j)
+          net.nodes[i].links.push_back(Link{j >= i ? j + 1 : j, D_EXP, prop_ev, 0.0});
+      }
+    }
+    TsLoopResult r;
+    ts_loop_task(net, rng_mode, (OcamlRandom*)rng, seed, episode, k, scheme, selection, policy,
+                 activations, &r);
+    for (size_t i = 0; i < r.rewards.size(); ++i) {
+      rewards_out[i] = r.rewards[i];
+      acts_out[i] = r.activations[i];
+    }
+    *head_time = r.head_time;
+    *head_progress = r.head_progress;
+    *head_height = r.head_height;
     *n_vertices = r.n_vertices;
     return 0;
   } catch (std::exception& e) {

@@ -493,3 +493,119 @@ def bk_loop(k, activations, *, net="clique", n_nodes=3, alpha=0.5, activation_de
     return dict(reward=rew.tolist(), activations=acts.tolist(), head_time=ht.value,
                 head_progress=hp.value, head_height=hh.value, head_signer=hs.value,
                 n_vertices=nv.value)
+
+
+# ---------------------------------------------------------------- Tailstorm
+
+TS_POLICIES = {"honest": 0, "get-ahead": 1, "minor-delay": 2, "avoid-loss": 3,
+               "avoid-loss-a": 4, "avoid-loss-b": 5, "long-delay": 6}
+TS_SCHEMES = {"constant": 0, "discount": 1, "punish": 3, "hybrid": 4}
+TS_SELECTIONS = {"altruistic": 0, "heuristic": 1, "optimal": 2}
+
+
+def ts_lib():
+    L = lib()
+    if not getattr(L, "_ts_declared", False):
+        P = ctypes.POINTER
+        vp = ctypes.c_void_p
+        from cpr_amd import _lib as C
+
+        L.oracle_ts_policy.argtypes = [ctypes.c_int, vp, ctypes.c_int]
+        L.oracle_ts_obs_to_floats.argtypes = [vp, ctypes.c_int, ctypes.c_int, vp]
+        L.oracle_ts_obs_of_floats.argtypes = [vp, ctypes.c_int, ctypes.c_int, vp]
+        L.oracle_n_choose_k.argtypes = [ctypes.c_int64, ctypes.c_int64]
+        L.oracle_n_choose_k.restype = ctypes.c_int64
+        L.oracle_ts_gym_new.restype = vp
+        L.oracle_ts_gym_new.argtypes = [P(C.Config), ctypes.c_int, vp, ctypes.c_uint64]
+        L.oracle_ts_gym_free.argtypes = [vp]
+        L.oracle_ts_gym_reset.argtypes = [vp, vp]
+        L.oracle_ts_gym_obs_fields.argtypes = [vp, vp]
+        L.oracle_ts_gym_step.argtypes = [vp, ctypes.c_int, vp, P(ctypes.c_double),
+                                         P(ctypes.c_int), vp]
+        L.oracle_ts_loop.argtypes = [
+            ctypes.c_int, ctypes.c_int, ctypes.c_double, ctypes.c_double, ctypes.c_double,
+            ctypes.c_int, vp, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_int, ctypes.c_int,
+            ctypes.c_int, ctypes.c_int, ctypes.c_int, vp, vp, P(ctypes.c_double),
+            P(ctypes.c_double), P(ctypes.c_int32), P(ctypes.c_int64),
+        ]
+        L._ts_declared = True
+    return L
+
+
+def ts_policy(policy, fields, k):
+    o = np.ascontiguousarray(fields, dtype=np.int32)
+    return ts_lib().oracle_ts_policy(TS_POLICIES.get(policy, policy), o.ctypes.data, k)
+
+
+def ts_obs_to_floats(fields, unit, k):
+    o = np.ascontiguousarray(fields, dtype=np.int32)
+    out = np.zeros(10)
+    ts_lib().oracle_ts_obs_to_floats(o.ctypes.data, 1 if unit else 0, k, out.ctypes.data)
+    return out
+
+
+def ts_obs_of_floats(floats, unit, k):
+    f = np.ascontiguousarray(floats, dtype=np.float64)
+    out = np.zeros(10, dtype=np.int32)
+    ts_lib().oracle_ts_obs_of_floats(f.ctypes.data, 1 if unit else 0, k, out.ctypes.data)
+    return out
+
+
+def n_choose_k(n, k):
+    return ts_lib().oracle_n_choose_k(n, k)
+
+
+class TsGymEnv:
+    """The oracle's engine.ml restatement for the tailstorm_ssz attack space."""
+
+    INFO_KEYS = GymEnv.INFO_KEYS + ["n_vertices"]
+
+    def __init__(self, config, episode=0, ocaml_rng=None):
+        self.cfg = config
+        self.h = ts_lib().oracle_ts_gym_new(ctypes.byref(config), 0 if ocaml_rng else 1,
+                                            ocaml_rng.h if ocaml_rng else None, episode)
+        if not self.h:
+            raise ValueError(lib().oracle_last_error().decode())
+
+    def __del__(self):
+        try:
+            ts_lib().oracle_ts_gym_free(self.h)
+        except Exception:
+            pass
+
+    def reset(self):
+        obs = np.zeros(10)
+        check(ts_lib().oracle_ts_gym_reset(self.h, obs.ctypes.data))
+        return obs
+
+    def fields(self):
+        f = np.zeros(10, dtype=np.int32)
+        ts_lib().oracle_ts_gym_obs_fields(self.h, f.ctypes.data)
+        return f
+
+    def step(self, action):
+        obs = np.zeros(10)
+        r = ctypes.c_double()
+        d = ctypes.c_int()
+        info = np.zeros(15)
+        check(ts_lib().oracle_ts_gym_step(self.h, int(action), obs.ctypes.data, ctypes.byref(r),
+                                          ctypes.byref(d), info.ctypes.data))
+        return obs, r.value, bool(d.value), dict(zip(self.INFO_KEYS, info.tolist()))
+
+
+def ts_loop(k, activations, *, net="clique", n_nodes=3, alpha=0.5, activation_delay=1.0,
+            prop_ev=1.0, scheme="discount", selection="heuristic", policy=-1, rng=None, seed=0,
+            episode=0):
+    n = 2 if net == "two-agents" else n_nodes
+    rew = np.zeros(n)
+    acts = np.zeros(n, dtype=np.int64)
+    ht, hp = ctypes.c_double(), ctypes.c_double()
+    hh, nv = ctypes.c_int32(), ctypes.c_int64()
+    check(ts_lib().oracle_ts_loop(
+        0 if net == "two-agents" else 1, n, alpha, activation_delay, prop_ev,
+        0 if rng is not None else 1, rng.h if rng is not None else None, seed, episode, k,
+        TS_SCHEMES.get(scheme, scheme), TS_SELECTIONS.get(selection, selection),
+        TS_POLICIES.get(policy, policy), activations, rew.ctypes.data, acts.ctypes.data,
+        ctypes.byref(ht), ctypes.byref(hp), ctypes.byref(hh), ctypes.byref(nv)))
+    return dict(reward=rew.tolist(), activations=acts.tolist(), head_time=ht.value,
+                head_progress=hp.value, head_height=hh.value, n_vertices=nv.value)

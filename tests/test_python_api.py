@@ -126,3 +126,49 @@ def test_unsupported_protocol_is_loud():
     with pytest.raises(NotImplementedError):
         protocols.tailstorm(k=8, reward="discount", subblock_selection="heuristic",
                             unit_observation=True)
+
+
+def test_bk_protocol(capsys):
+    # gym/ocaml/test/test_protocols.py:105-127
+    env = envs.make("cpr_gym:core-v0",
+                    proto=protocols.bk(k=42, reward="constant", unit_observation=True),
+                    alpha=0.33, gamma=0.3, defenders=4, max_steps=10000)
+    env.render()
+    assert capsys.readouterr().out.splitlines()[0] == (
+        "Bₖ with k=42 and constant rewards; "
+        "SSZ'16-like attack space with unit observations; α=0.33 attacker")
+    obs = env.reset()
+    for _ in range(600):
+        obs, _, _, _ = env.step(env.policy(obs, "honest"))
+    obs = env.reset()
+    for _ in range(600):
+        obs, _, _, info = env.step(env.policy(obs, "minor-delay"))
+    assert info["protocol_k"] == 42
+    assert info["protocol_family"] == "bk" and info["head_kind"] == "block"
+    assert env.observation_space.contains(obs)
+    assert env.action_space.n == 8
+    assert list(env.policies()) == ["avoid-loss", "minor-delay", "get-ahead", "honest"]
+    env.render()
+    out = capsys.readouterr().out.splitlines()
+    assert out[-1].startswith("Actions: (0) Adopt_Prolong | (1) Override_Prolong")
+    assert out[7] == "lead: false" and out[8].startswith("event: `")
+    fuzz_episode(envs.make("core-v0", proto=protocols.bk(k=8, reward="block",
+                                                          unit_observation=False),
+                           max_steps=300))
+
+
+def test_bk_policies_and_errors():
+    # test_protocols.py:22-47
+    for gamma, d, pol in [(0.2, 2, "honest"), (0.5, 3, "minor-delay")]:
+        env = envs.make("core-v0", proto=protocols.bk(k=8, reward="constant",
+                                                      unit_observation=True),
+                        alpha=0.33, gamma=gamma, defenders=d, max_steps=10000)
+        obs = env.reset()
+        for _ in range(600):
+            obs, _, _, _ = env.step(env.policy(obs, pol))
+    with pytest.raises(ValueError, match="not a valid parameter choice, try 'block' or 'constant'"):
+        protocols.bk(k=8, reward="discount", unit_observation=True)
+    env = envs.make("cpr-v0", protocol="bk", protocol_args=dict(k=8, reward="constant"),
+                    episode_len=256)
+    _, r, done, info = run_episode(env, "avoid-loss")
+    assert done and info["episode_n_steps"] == 256 and r >= 0
