@@ -1,0 +1,1272 @@
+// Tailstorm (tailstorm.ml) with the tailstorm_ssz attack space: one episode per lane, as an
+// exact per-lane discrete-event engine (same skeleton as bk_lane.h).
+//
+// Tailstorm's votes form a tree under each summary; summaries are PoW-less, unsigned and
+// deterministic, so identical summaries appended by different nodes are deduplicated
+// (simulator.ml:139-159). Quorum selection (altruistic / heuristic / optimal,
+// tailstorm.ml:271-507) walks vote branches, the attacker's release walks the descendants
+// of the common ancestor in (DAG depth, serial) order (tailstorm_ssz.ml:292-314), and the
+// head is Compare.first over a heap sort (tailstorm.ml:191-194). The lane keeps per vote
+// its summary (last_summary) and parent, so a summary's vote tree is the set of votes whose
+// summary field names it, scanned from the vertex ring.
+//
+// Per-lane memory (one contiguous region per lane):
+//   vtx    [cap_v] x 64 B    vertex ring indexed by serial & (cap_v-1)
+//   vis    [cap_v][n] u8     per node: kind + got bit;  vt [cap_v][n] f64 visible_since
+//   quo    [cap_q][k+1] i32  summary quorums: tag (serial), leaves sorted by
+//                            compare_votes_in_block
+//   srew   [cap_q][2n] f64   per summary: cumulative rewards per node (set_rewards order),
+//                            and its own reward list summed per node (compare_blocks)
+//   drafts [cap_d][k+2] i32  outstanding summary drafts (tag, #leaves, leaves)
+//   heap   [cap_e] x 24 B    event queue (skew heap, +inf events kept)
+//   tips [n] i32, pend [NPEND] i32 (pending released messages), marks [cap_v] u8, scratch
+//
+// Reference map: simulator.ml:122-543, tailstorm.ml:86-609, tailstorm_ssz.ml:162-446,
+// combinatorics.ml:5-32, engine.ml:97-249.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "bk_lane.h"  // HNode, ocaml_heap_sort64, event/kind/visibility enums, time_key
+#include "cpr_stream.h"
+
+#pragma clang fp contract(off)
+
+namespace cpr {
+namespace ts {
+
+using bk::HNode;
+using bk::mkev;
+using bk::ocaml_heap_sort64;
+using bk::time_key;
+constexpr uint32_t EV_CLOCK = bk::EV_CLOCK, EV_DAG = bk::EV_DAG, EV_TX = bk::EV_TX,
+                   EV_RX = bk::EV_RX, EV_ON = bk::EV_ON, EV_MV = bk::EV_MV, EV_MDV = bk::EV_MDV;
+constexpr uint32_t KD_APP = bk::KD_APP, KD_POW = bk::KD_POW, KD_NET = bk::KD_NET;
+constexpr uint8_t V_INV = bk::V_INV, V_RECV = bk::V_RECV, V_REL = bk::V_REL, V_WH = bk::V_WH,
+                  V_KIND = bk::V_KIND, V_GOT = bk::V_GOT;
+
+constexpr uint32_t TST_CAPACITY = 32u;   // CPR_ST_CAPACITY
+constexpr uint32_t TST_REF_RAISES = 64u; // CPR_ST_REFERENCE_RAISES
+
+// vote filters: all, Honest.appended_by_me, public_visibility, public or in the release set
+enum : int32_t { VF_ALL = 0, VF_MINE = 1, VF_PUBLIC = 2, VF_PUBLIC_OR_MARKED = 3 };
+// incentive schemes (tailstorm.ml:3,221-227), ids as in cpr_reward_scheme
+enum : int32_t { SC_CONSTANT = 0, SC_DISCOUNT = 1, SC_PUNISH = 3, SC_HYBRID = 4 };
+enum : int32_t { SEL_ALTRUISTIC = 0, SEL_HEURISTIC = 1, SEL_OPTIMAL = 2 };
+
+struct TVtx {
+  int32_t serial;
+  int32_t parent;  // vote: its parent; summary: leaves[0] (precursor); genesis -1
+  int32_t height;
+  int32_t vote;    // 1 Vote, 0 Summary
+  int32_t who;     // vote miner; -1 summaries
+  int32_t depth;   // vote data depth; 0 summaries
+  int32_t pow;     // 30-bit hash bits (votes)
+  int32_t ddepth;  // Dag depth (dag.ml:28-35)
+  int32_t sum;     // vote: last_summary; summary: itself
+  int32_t nconf;   // summary: votes in its tree, global view (Referee.compare_summaries)
+  int32_t qslot;   // summary: quorum / reward slot; -1 genesis
+  int32_t nq;      // summary: number of leaves
+  double time;     // Simulator.timestamp = append time
+  int32_t _pad[2];
+};
+static_assert(sizeof(TVtx) == 64, "TVtx layout");
+
+struct TsParams {
+  uint64_t t_att;
+  int32_t d, n, net, mode;
+  int32_t policy, scheme, selection, k;
+  int32_t cap_v, cap_q, cap_e, cap_d;
+  double ev, delta, dmax;
+  int64_t max_steps, activations;
+  double max_progress, max_time;
+};
+
+constexpr int32_t NQS = 512;     // votes of one summary tree handled at once
+constexpr int32_t NSTACK = 1024; // share stack
+constexpr int32_t NPEND = 1024;  // pending released messages
+constexpr int32_t NFR = 64;      // common-ancestor frontier
+
+struct TsMem {
+  TVtx* vtx;
+  uint8_t* vis;
+  double* vt;
+  int32_t* quo;
+  double* srew;
+  int32_t* drafts;
+  HNode* heap;
+  int32_t* tips;
+  int32_t* pend;
+  uint8_t* marks;   // [cap_v]
+  int32_t* cand;    // [NQS] tree votes, ascending serial
+  int32_t* perm;    // [NQS] indices into cand in BlockSet order (Dag depth, serial)
+  int32_t* aux;     // [NQS] scratch indices
+  uint8_t* flag;    // [NQS]
+  uint8_t* flag2;   // [NQS]
+  uint64_t* key;    // [NQS] sort keys
+  int32_t* stack;   // [NSTACK]
+  int32_t* fr;      // [4 * NFR] two frontiers of (ddepth, serial)
+};
+
+__host__ __device__ inline int64_t ts_align(int64_t x) { return (x + 127) / 128 * 128; }
+
+__host__ __device__ inline int64_t ts_lane_bytes(const TsParams& P) {
+  return ts_align((int64_t)P.cap_v * 64) + ts_align((int64_t)P.cap_v * P.n) +
+         ts_align((int64_t)P.cap_v * P.n * 8) + ts_align((int64_t)P.cap_q * (P.k + 1) * 4) +
+         ts_align((int64_t)P.cap_q * 2 * P.n * 8) + ts_align((int64_t)P.cap_d * (P.k + 2) * 4) +
+         ts_align((int64_t)P.cap_e * 24) + ts_align((int64_t)P.n * 4) + ts_align(NPEND * 4) +
+         ts_align(P.cap_v) + 3 * ts_align(NQS * 4) + 2 * ts_align(NQS) + ts_align(NQS * 8) +
+         ts_align(NSTACK * 4) + ts_align(4 * NFR * 4);
+}
+
+__host__ __device__ inline TsMem ts_mem_at(uint8_t* base, const TsParams& P) {
+  TsMem M;
+  int64_t o = 0;
+  auto take = [&](int64_t bytes) {
+    uint8_t* p = base + o;
+    o += ts_align(bytes);
+    return p;
+  };
+  M.vtx = (TVtx*)take((int64_t)P.cap_v * 64);
+  M.vis = take((int64_t)P.cap_v * P.n);
+  M.vt = (double*)take((int64_t)P.cap_v * P.n * 8);
+  M.quo = (int32_t*)take((int64_t)P.cap_q * (P.k + 1) * 4);
+  M.srew = (double*)take((int64_t)P.cap_q * 2 * P.n * 8);
+  M.drafts = (int32_t*)take((int64_t)P.cap_d * (P.k + 2) * 4);
+  M.heap = (HNode*)take((int64_t)P.cap_e * 24);
+  M.tips = (int32_t*)take((int64_t)P.n * 4);
+  M.pend = (int32_t*)take(NPEND * 4);
+  M.marks = take(P.cap_v);
+  M.cand = (int32_t*)take(NQS * 4);
+  M.perm = (int32_t*)take(NQS * 4);
+  M.aux = (int32_t*)take(NQS * 4);
+  M.flag = take(NQS);
+  M.flag2 = take(NQS);
+  M.key = (uint64_t*)take(NQS * 8);
+  M.stack = (int32_t*)take(NSTACK * 4);
+  M.fr = (int32_t*)take(4 * NFR * 4);
+  return M;
+}
+
+// ---- observation and policies (tailstorm_ssz.ml:22-38, 365-446); Action8 ranks
+struct TsObs {
+  int32_t public_blocks, private_blocks, diff_blocks, public_votes, private_votes_inclusive,
+      private_votes_exclusive, public_depth, private_depth_inclusive, private_depth_exclusive,
+      event;  // 0 Append, 1 ProofOfWork, 2 Network
+};
+
+__host__ __device__ inline int32_t ts_policy(int32_t policy, int32_t k, const TsObs& o) {
+  const int32_t h = o.public_blocks, a = o.private_blocks;
+  const int32_t hp = h * k + o.public_votes, ap = a * k + o.private_votes_inclusive;
+  switch (policy) {
+    case 0: return h > a ? bk::A_ADOPT_PROCEED : bk::A_OVERRIDE_PROCEED;  // honest
+    case 1:  // get-ahead
+      return h > a ? bk::A_ADOPT_PROCEED
+                   : (h < a ? bk::A_OVERRIDE_PROCEED : bk::A_WAIT_PROCEED);
+    case 2:  // minor-delay
+      return h > a ? bk::A_ADOPT_PROCEED
+                   : (h == 0 ? bk::A_WAIT_PROCEED : bk::A_OVERRIDE_PROCEED);
+    case 4:  // avoid-loss-a = avoid_loss
+      if (a < h) return bk::A_ADOPT_PROCEED;
+      if (h == 0) return bk::A_WAIT_PROCEED;
+      if (o.private_votes_inclusive == 0 && a == h + 1) return bk::A_OVERRIDE_PROCEED;
+      if (h == a && o.private_votes_inclusive == o.public_votes + 1) return bk::A_OVERRIDE_PROCEED;
+      if (a - h > 10) return bk::A_OVERRIDE_PROCEED;
+      return bk::A_WAIT_PROCEED;
+    case 6:  // long-delay
+      if (h > a) return bk::A_ADOPT_PROCEED;
+      if (h == 0) return bk::A_WAIT_PROCEED;
+      if (h + 10 < a) return bk::A_OVERRIDE_PROCEED;
+      if (h * k + o.public_votes + 1 < a * k + o.private_votes_inclusive)
+        return bk::A_WAIT_PROCEED;
+      return bk::A_OVERRIDE_PROCEED;
+    default:  // 3 avoid-loss = avoid_loss_alt, 5 avoid-loss-b = avoid_loss_alt2
+      if (h == 0) return bk::A_WAIT_PROCEED;
+      if (h == 1 && hp == ap) return policy == 3 ? bk::A_MATCH_PROCEED : bk::A_OVERRIDE_PROCEED;
+      if (hp > ap) return bk::A_ADOPT_PROCEED;
+      if (hp == ap - 1) return bk::A_OVERRIDE_PROCEED;
+      if (h < a - 10) return bk::A_OVERRIDE_PROCEED;
+      return bk::A_WAIT_PROCEED;
+  }
+}
+
+// combinatorics.ml:5-17 in OCaml's 63-bit wrap-around arithmetic; *dz = Division_by_zero
+__host__ __device__ inline int64_t ocaml_nck(int64_t n, int64_t k, bool* dz) {
+  auto fact = [](int64_t m) {
+    int64_t x = 1;
+    for (int64_t i = 2; i <= m; ++i) {
+      uint64_t u = (uint64_t)x * (uint64_t)i;
+      x = ((int64_t)(u << 1)) >> 1;
+    }
+    return x;
+  };
+  const int64_t a = fact(n), b = fact(k), c = fact(n - k);
+  if (b == 0 || c == 0) {
+    *dz = true;
+    return 0;
+  }
+  return (a / b) / c;
+}
+
+struct TsLane {
+  double now;
+  int32_t c_act, newest, nsum, act0;
+  int32_t hroot, hfree, hused;
+  uint32_t status;
+  int32_t dead;  // 1 vertex ring, 2 heap, 3 tree list, 4 drafts, 5 stack, 6 drained, 7 quorum
+                 // ring, 8 zero-time loop, 9 pending list, 10 frontier, 11 reference raises,
+                 // 12 optimal-quorum brute-force budget
+  int32_t zt, dseq;
+  int32_t pub, priv, npend;
+  int32_t o_pub, o_priv, o_common, o_event;
+  int64_t steps;
+
+  // ------------------------------------------------------------------ storage
+  __host__ __device__ inline void fail(int32_t why) {
+    status |= why == 11 ? TST_REF_RAISES : TST_CAPACITY;
+    if (!dead) dead = why;
+  }
+  __host__ __device__ inline TVtx& X(const TsParams& P, const TsMem& M, int32_t s) {
+    TVtx& b = M.vtx[s & (P.cap_v - 1)];
+    if (b.serial != s) fail(1);
+    return b;
+  }
+  __host__ __device__ inline uint8_t& V(const TsParams& P, const TsMem& M, int32_t s,
+                                        int32_t node) {
+    return M.vis[(int64_t)(s & (P.cap_v - 1)) * P.n + node];
+  }
+  __host__ __device__ inline double& VT(const TsParams& P, const TsMem& M, int32_t s,
+                                        int32_t node) {
+    return M.vt[(int64_t)(s & (P.cap_v - 1)) * P.n + node];
+  }
+  __host__ __device__ inline bool visible(const TsParams& P, const TsMem& M, int32_t s,
+                                          int32_t node) {
+    return (V(P, M, s, node) & V_KIND) != V_INV;
+  }
+  __host__ __device__ inline uint8_t& MK(const TsParams& P, const TsMem& M, int32_t s) {
+    return M.marks[s & (P.cap_v - 1)];
+  }
+  __host__ __device__ inline int32_t* Q(const TsParams& P, const TsMem& M, const TVtx& b) {
+    int32_t* q = M.quo + (int64_t)(b.qslot & (P.cap_q - 1)) * (P.k + 1);
+    if (q[0] != b.serial) fail(7);
+    return q + 1;
+  }
+  // summary rewards: [0, n) cumulative, [n, 2n) own reward list summed per node
+  __host__ __device__ inline double* R(const TsParams& P, const TsMem& M, int32_t qslot) {
+    return M.srew + (int64_t)(qslot & (P.cap_q - 1)) * 2 * P.n;
+  }
+  __host__ __device__ static inline bool keep_kind(uint8_t v, int32_t vf, bool marked) {
+    const uint8_t kd = v & V_KIND;
+    switch (vf) {
+      case VF_MINE: return kd == V_WH || kd == V_REL;
+      case VF_PUBLIC: return kd == V_REL || kd == V_RECV;
+      case VF_PUBLIC_OR_MARKED: return kd == V_REL || kd == V_RECV || marked;
+      default: return true;
+    }
+  }
+
+  // ------------------------------------------------------------------ event queue
+  // orderedQueue.ml:17-47, in place; +inf events are stored (they shape the tie order)
+  __host__ __device__ inline int32_t halloc(const TsParams& P, const TsMem& M) {
+    int32_t i;
+    if (hfree >= 0) {
+      i = hfree;
+      hfree = M.heap[i].l;
+    } else if (hused < P.cap_e) {
+      i = hused++;
+    } else {
+      fail(2);
+      return -1;
+    }
+    return i;
+  }
+  __host__ __device__ inline void push(const TsParams& P, const TsMem& M, double t, uint32_t ev,
+                                       int32_t blk) {
+    int32_t parent = -1, node = hroot;
+    for (;;) {
+      if (node < 0) {
+        const int32_t a = halloc(P, M);
+        if (a < 0) return;
+        HNode& h = M.heap[a];
+        h.t = t;
+        h.ev = ev;
+        h.blk = blk;
+        h.l = -1;
+        h.r = -1;
+        if (parent < 0)
+          hroot = a;
+        else
+          M.heap[parent].l = a;
+        return;
+      }
+      HNode& h = M.heap[node];
+      if (t < h.t) {
+        const double ot = h.t;
+        const uint32_t oe = h.ev;
+        const int32_t ob = h.blk;
+        h.t = t;
+        h.ev = ev;
+        h.blk = blk;
+        t = ot;
+        ev = oe;
+        blk = ob;
+      } else {
+        const int32_t tmp = h.l;
+        h.l = h.r;
+        h.r = tmp;
+      }
+      parent = node;
+      node = h.l;
+    }
+  }
+  __host__ __device__ inline bool pop(const TsMem& M, double* t, uint32_t* ev, int32_t* blk) {
+    if (hroot < 0) return false;
+    *t = M.heap[hroot].t;
+    *ev = M.heap[hroot].ev;
+    *blk = M.heap[hroot].blk;
+    int32_t parent = -1, side = 0, node = hroot;
+    for (;;) {
+      const int32_t l = M.heap[node].l, r = M.heap[node].r;
+      int32_t repl = -2;
+      if (r < 0)
+        repl = l;
+      else if (l < 0)
+        repl = r;
+      if (repl != -2) {
+        if (parent < 0)
+          hroot = repl;
+        else if (side == 0)
+          M.heap[parent].l = repl;
+        else
+          M.heap[parent].r = repl;
+        M.heap[node].l = hfree;
+        hfree = node;
+        return true;
+      }
+      const int32_t c = (M.heap[l].t <= M.heap[r].t) ? l : r;
+      M.heap[node].t = M.heap[c].t;
+      M.heap[node].ev = M.heap[c].ev;
+      M.heap[node].blk = M.heap[c].blk;
+      parent = node;
+      side = c == l ? 0 : 1;
+      node = c;
+    }
+  }
+  __host__ __device__ inline void push_now(const TsParams& P, const TsMem& M, uint32_t ev,
+                                           int32_t blk) {
+    push(P, M, now, ev, blk);
+  }
+
+  // ------------------------------------------------------------------ randomness
+  __host__ __device__ inline int32_t miner_of(const TsParams& P, const Stream& S, int32_t j) {
+    const Words4 w = S.block((uint32_t)j, TAG_ACT);
+    if ((uint64_t)w.w0 < P.t_att) return 0;
+    return 1 + (int32_t)(((uint64_t)w.w1 * (uint64_t)P.d) >> 32);
+  }
+  __host__ __device__ inline void schedule_pow(const TsParams& P, const Stream& S,
+                                               const TsMem& M) {
+    const Words4 w = S.block((uint32_t)c_act, TAG_ACT);
+    push(P, M, now + (-1.0 * P.ev) * cpr_log(u53(w.w2, w.w3)), mkev(EV_CLOCK, 0, KD_POW), -1);
+  }
+
+  // ------------------------------------------------------------------ vote trees
+  __host__ __device__ static inline uint64_t pow_key(const TVtx& v) {
+    return ((uint64_t)(uint32_t)v.pow << 32) | (uint32_t)v.serial;
+  }
+  // compare_votes_in_block (tailstorm.ml:124-130): deeper first, then smaller pow
+  __host__ __device__ static inline bool vote_before(const TVtx& a, const TVtx& b) {
+    if (a.depth != b.depth) return a.depth > b.depth;
+    return pow_key(a) < pow_key(b);
+  }
+  __host__ __device__ inline int32_t index_of(const TsMem& M, int32_t n, int32_t s) {
+    int32_t lo = 0, hi = n - 1;
+    while (lo <= hi) {
+      const int32_t mid = (lo + hi) >> 1;
+      const int32_t v = M.cand[mid];
+      if (v == s) return mid;
+      if (v < s) lo = mid + 1; else hi = mid - 1;
+    }
+    return -1;
+  }
+  // votes of summary b's tree visible at `node` into cand[] (ascending serial): the
+  // expansion acc_votes children' (children' b) with children' = children |> filter vf when
+  // `restrict` (tailstorm.ml:509-535), else all of confirming_votes b; perm[] = BlockSet
+  // order (Dag depth, serial)
+  __host__ __device__ inline int32_t tree(const TsParams& P, const TsMem& M, int32_t b,
+                                          int32_t node, int32_t vf) {
+    int32_t n = 0;
+    for (int32_t c = b + 1; c <= newest && !dead; ++c) {
+      const uint8_t v = V(P, M, c, node);
+      if ((v & V_KIND) == V_INV) continue;
+      const TVtx& x = X(P, M, c);
+      if (!x.vote || x.sum != b) continue;
+      if (vf != VF_ALL) {
+        if (!keep_kind(v, vf, false)) continue;
+        if (x.parent != b && index_of(M, n, x.parent) < 0) continue;
+      }
+      if (n >= NQS) {
+        fail(3);
+        return 0;
+      }
+      M.cand[n++] = c;
+    }
+    // stable insertion by Dag depth (cand is serial-ascending)
+    for (int32_t i = 0; i < n; ++i) {
+      const int32_t dd = X(P, M, M.cand[i]).ddepth;
+      int32_t j = i;
+      while (j > 0 && X(P, M, M.cand[M.perm[j - 1]]).ddepth > dd) {
+        M.perm[j] = M.perm[j - 1];
+        --j;
+      }
+      M.perm[j] = i;
+    }
+    return n;
+  }
+  // votes of summary b's tree at `node` passing `vf` after expansion (compare_blocks,
+  // observe): count and max depth
+  __host__ __device__ inline int32_t count_post(const TsParams& P, const TsMem& M, int32_t b,
+                                                int32_t node, int32_t vf, int32_t* maxd) {
+    int32_t n = 0, d = 0;
+    for (int32_t c = b + 1; c <= newest && !dead; ++c) {
+      const uint8_t v = V(P, M, c, node);
+      if ((v & V_KIND) == V_INV) continue;
+      const TVtx& x = X(P, M, c);
+      if (!x.vote || x.sum != b) continue;
+      if (!keep_kind(v, vf, vf == VF_PUBLIC_OR_MARKED && MK(P, M, c))) continue;
+      ++n;
+      d = x.depth > d ? x.depth : d;
+    }
+    if (maxd) *maxd = d;
+    return n;
+  }
+  __host__ __device__ inline bool mine(const TsParams& P, const TsMem& M, int32_t s,
+                                       int32_t node) {
+    const uint8_t kd = V(P, M, s, node) & V_KIND;
+    return kd == V_WH || kd == V_REL;
+  }
+
+  // writes the draft's leaves (sorted by compare_votes_in_block) to q; returns #leaves or 0
+  __host__ __device__ inline int32_t heuristic(const TsParams& P, const TsMem& M, int32_t node,
+                                               int32_t n, int32_t* q) {
+    // flag = included
+    for (int32_t i = 0; i < n; ++i) M.flag[i] = 0;
+    int32_t need = P.k, nl = 0;
+    while (need > 0 && !dead) {
+      int32_t best = -1, bo = -1, bt = -1;
+      for (int32_t pi = 0; pi < n; ++pi) {
+        const int32_t i = M.perm[pi];
+        if (M.flag[i]) continue;
+        int32_t own = 0, tot = 0, s = M.cand[i];
+        for (;;) {
+          const int32_t j = index_of(M, n, s);
+          if (j < 0) break;
+          if (!M.flag[j]) {
+            ++tot;
+            own += mine(P, M, s, node) ? 1 : 0;
+          }
+          s = X(P, M, s).parent;
+        }
+        if (tot > need) continue;
+        if (own > bo || (own == bo && tot > bt)) {
+          best = i;
+          bo = own;
+          bt = tot;
+        }
+      }
+      if (best < 0) {  // `assert false` in the reference
+        fail(11);
+        return 0;
+      }
+      q[nl++] = M.cand[best];
+      int32_t s = M.cand[best];
+      for (;;) {
+        const int32_t j = index_of(M, n, s);
+        if (j < 0) break;
+        if (!M.flag[j]) {
+          M.flag[j] = 1;
+          --need;
+        }
+        s = X(P, M, s).parent;
+      }
+    }
+    return nl;
+  }
+  __host__ __device__ inline int32_t altruistic(const TsParams& P, const TsMem& M, int32_t node,
+                                                int32_t n, int32_t* q) {
+    // List.sort (stable) of BlockSet.elements by (neg depth, (own 0 | 1, visible_since))
+    for (int32_t pi = 0; pi < n; ++pi) M.aux[pi] = M.perm[pi];
+    auto before = [&](int32_t a, int32_t b) {  // strict "a sorts before b"
+      const TVtx& x = X(P, M, M.cand[a]);
+      const TVtx& y = X(P, M, M.cand[b]);
+      if (x.depth != y.depth) return x.depth > y.depth;
+      const int32_t ox = mine(P, M, x.serial, node) ? 0 : 1, oy = mine(P, M, y.serial, node) ? 0 : 1;
+      if (ox != oy) return ox < oy;
+      return VT(P, M, x.serial, node) < VT(P, M, y.serial, node);
+    };
+    for (int32_t i = 1; i < n; ++i) {
+      const int32_t v = M.aux[i];
+      int32_t j = i;
+      while (j > 0 && before(v, M.aux[j - 1])) {
+        M.aux[j] = M.aux[j - 1];
+        --j;
+      }
+      M.aux[j] = v;
+    }
+    for (int32_t i = 0; i < n; ++i) M.flag[i] = 0;  // acc
+    int32_t cnt = 0, nl = 0;
+    for (int32_t t = 0; t < n && cnt < P.k && !dead; ++t) {
+      const int32_t hd = M.aux[t];
+      int32_t nf = 0, s = M.cand[hd];
+      for (;;) {
+        const int32_t j = index_of(M, n, s);
+        if (j < 0) break;
+        nf += M.flag[j] ? 0 : 1;
+        s = X(P, M, s).parent;
+      }
+      if (cnt + nf > P.k || nf < 1) continue;
+      s = M.cand[hd];
+      for (;;) {
+        const int32_t j = index_of(M, n, s);
+        if (j < 0) break;
+        M.flag[j] = 1;
+        s = X(P, M, s).parent;
+      }
+      cnt += nf;
+      q[nl++] = M.cand[hd];
+    }
+    return cnt == P.k ? nl : 0;
+  }
+  // reward of a draft with these leaves for `node` (reward' folded over my entries)
+  __host__ __device__ inline double draft_reward(const TsParams& P, const TsMem& M, int32_t node,
+                                                 int32_t n, const int32_t* lv, int32_t nl) {
+    for (int32_t i = 0; i < n; ++i) M.flag2[i] = 0;
+    const bool punish = P.scheme == SC_PUNISH || P.scheme == SC_HYBRID;
+    const bool discount = P.scheme == SC_DISCOUNT || P.scheme == SC_HYBRID;
+    const int32_t upto = punish ? 1 : nl;
+    for (int32_t t = 0; t < upto; ++t) {
+      int32_t s = lv[t];
+      for (;;) {
+        const int32_t j = index_of(M, n, s);
+        if (j < 0) break;
+        M.flag2[j] = 1;
+        s = X(P, M, s).parent;
+      }
+    }
+    const double r = discount ? (double)X(P, M, lv[0]).depth / (double)P.k * 1.0 : 1.0;
+    double acc = 0.0;
+    for (int32_t i = 0; i < n; ++i)
+      if (M.flag2[i] && X(P, M, M.cand[i]).who == node) acc += r;
+    return acc;
+  }
+  __host__ __device__ inline int32_t optimal(const TsParams& P, const TsMem& M, int32_t node,
+                                             int32_t n, int32_t* q) {
+    bool dz = false;
+    const int64_t nck = ocaml_nck(n, P.k, &dz);
+    if (dz) {
+      fail(11);
+      return 0;
+    }
+    if (nck > 100) return heuristic(P, M, node, n, q);
+    if (n < P.k) return 0;
+    {  // brute-force budget (oracle/src/tailstorm.h TS_BRUTE_FORCE_BUDGET): the reference's
+       // overflowed n_choose_k can send it through millions of choices
+      int64_t kk = P.k < n - P.k ? P.k : n - P.k;
+      double r = 1.0;
+      for (int64_t i = 1; i <= kk; ++i) r = r * (double)(n - kk + i) / (double)i;
+      if (r > 100000.5) {
+        fail(12);
+        return 0;
+      }
+    }
+    // a = BlockSet order; pos[cand index] = position in a (M.aux)
+    for (int32_t pi = 0; pi < n; ++pi) M.aux[M.perm[pi]] = pi;
+    int32_t c[64];
+    for (int32_t t = 0; t < P.k; ++t) c[t] = t;
+    double best = -1.0;
+    int32_t nbest = 0;
+    int32_t lv[64];
+    for (;;) {
+      // leaves c (tailstorm.ml:442-481): reach (flag) and leave (flag2) over positions
+      for (int32_t i = 0; i < n; ++i) {
+        M.flag[i] = 0;
+        M.flag2[i] = 1;
+      }
+      bool ok = true;
+      for (int32_t t = 0; t < P.k && ok; ++t) {
+        const TVtx& x = X(P, M, M.cand[M.perm[c[t]]]);
+        const int32_t ji = index_of(M, n, x.parent);
+        if (ji >= 0) {  // vote parent (summary parents are filtered out)
+          const int32_t ip = M.aux[ji];
+          M.flag2[ip] = 0;
+          ok = M.flag[ip] != 0;
+        }
+        if (ok) M.flag[c[t]] = 1;
+      }
+      if (ok) {
+        int32_t nl = 0;
+        for (int32_t i = 0; i < n; ++i)
+          if (M.flag[i] && M.flag2[i]) lv[nl++] = M.cand[M.perm[i]];
+        for (int32_t i = 1; i < nl; ++i) {  // sort by compare_votes_in_block (unique keys)
+          const int32_t v = lv[i];
+          int32_t j = i;
+          while (j > 0 && vote_before(X(P, M, v), X(P, M, lv[j - 1]))) {
+            lv[j] = lv[j - 1];
+            --j;
+          }
+          lv[j] = v;
+        }
+        const double r = draft_reward(P, M, node, n, lv, nl);
+        if (r > best) {
+          best = r;
+          nbest = nl;
+          for (int32_t i = 0; i < nl; ++i) q[i] = lv[i];
+        }
+      }
+      // next combination in lexicographic order (iter_n_choose_k)
+      int32_t t = P.k - 1;
+      while (t >= 0 && c[t] == n - P.k + t) --t;
+      if (t < 0) break;
+      ++c[t];
+      for (int32_t u = t + 1; u < P.k; ++u) c[u] = c[u - 1] + 1;
+    }
+    if (nbest == 0) fail(11);  // "reward_optim_quorum: no choice"
+    return nbest;
+  }
+  // Honest.next_summary' (tailstorm.ml:530-535): draft seq or -1
+  __host__ __device__ inline int32_t next_summary(const TsParams& P, const TsMem& M,
+                                                  int32_t node, int32_t b, int32_t vf) {
+    const int32_t n = tree(P, M, b, node, vf);
+    if (dead || n < P.k) return -1;  // all three selections need k votes
+    const int32_t seq = dseq;
+    int32_t* dr = M.drafts + (int64_t)(seq & (P.cap_d - 1)) * (P.k + 2);
+    int32_t* q = dr + 2;
+    int32_t nl;
+    if (P.selection == SEL_ALTRUISTIC)
+      nl = altruistic(P, M, node, n, q);
+    else if (P.selection == SEL_OPTIMAL)
+      nl = optimal(P, M, node, n, q);
+    else
+      nl = heuristic(P, M, node, n, q);
+    if (nl <= 0 || dead) return -1;
+    if (P.selection != SEL_OPTIMAL || nl != 0) {
+      // leaves sorted by compare_votes_in_block (altruistic: by (neg depth, pow), same
+      // order since every vote has a pow)
+      for (int32_t i = 1; i < nl; ++i) {
+        const int32_t v = q[i];
+        int32_t j = i;
+        while (j > 0 && vote_before(X(P, M, v), X(P, M, q[j - 1]))) {
+          q[j] = q[j - 1];
+          --j;
+        }
+        q[j] = v;
+      }
+    }
+    dr[0] = seq;
+    dr[1] = nl;
+    ++dseq;
+    return seq;
+  }
+  // Honest.puzzle_payload (tailstorm.ml:509-528): parent of the next vote on summary b
+  __host__ __device__ inline int32_t payload_parent(const TsParams& P, const TsMem& M,
+                                                    int32_t node, int32_t b) {
+    int32_t best = b;
+    for (int32_t c = b + 1; c <= newest && !dead; ++c) {
+      if (!visible(P, M, c, node)) continue;
+      const TVtx& x = X(P, M, c);
+      if (!x.vote || x.sum != b) continue;
+      if (best == b || vote_before(x, X(P, M, best))) best = c;
+    }
+    return best;
+  }
+  // compare_blocks (tailstorm.ml:539-550) at `node`
+  __host__ __device__ inline int32_t compare_blocks(const TsParams& P, const TsMem& M,
+                                                    int32_t node, int32_t vf, int32_t a,
+                                                    int32_t b) {
+    if (a == b) return 0;
+    const TVtx& xa = X(P, M, a);
+    const TVtx& xb = X(P, M, b);
+    if (xa.height != xb.height) return xa.height < xb.height ? -1 : 1;
+    const int32_t ca = count_post(P, M, a, node, vf, nullptr);
+    const int32_t cb = count_post(P, M, b, node, vf, nullptr);
+    if (ca != cb) return ca < cb ? -1 : 1;
+    const double ra = xa.qslot < 0 ? 0.0 : R(P, M, xa.qslot)[P.n + node];
+    const double rb = xb.qslot < 0 ? 0.0 : R(P, M, xb.qslot)[P.n + node];
+    return ra < rb ? -1 : (ra > rb ? 1 : 0);
+  }
+  __host__ __device__ inline int32_t update_head(const TsParams& P, const TsMem& M, int32_t node,
+                                                 int32_t vf, int32_t old, int32_t cand) {
+    return compare_blocks(P, M, node, vf, cand, old) > 0 ? cand : old;
+  }
+  __host__ __device__ inline bool has_children(const TsParams& P, const TsMem& M, int32_t s,
+                                               int32_t node) {
+    // children of a summary are votes on it
+    for (int32_t c = newest; c > s && !dead; --c) {
+      if (!visible(P, M, c, node)) continue;
+      const TVtx& x = X(P, M, c);
+      if (x.vote && x.parent == s) return true;
+    }
+    return false;
+  }
+  // tailstorm.ml:557-563
+  __host__ __device__ inline bool feasible(const TsParams& P, const TsMem& M, int32_t node,
+                                           int32_t preferred, int32_t after) {
+    const int32_t ext = X(P, M, after).height + 1, cur = X(P, M, preferred).height;
+    return cur < ext || (cur == ext && !has_children(P, M, preferred, node));
+  }
+
+  // ------------------------------------------------------------------ DAG
+  __host__ __device__ inline void init_vertex(const TsParams& P, const TsMem& M, TVtx& b,
+                                              int32_t s) {
+    b.serial = s;
+    b.nconf = 0;
+    b.qslot = -1;
+    b.nq = 0;
+    b.time = now;
+    for (int32_t j = 0; j < P.n; ++j) V(P, M, s, j) = V_INV;
+  }
+  __host__ __device__ inline int32_t append_vote(const TsParams& P, const Stream& S,
+                                                 const TsMem& M, int32_t node, int32_t parent) {
+    TVtx& p = X(P, M, parent);
+    const int32_t s = ++newest;
+    TVtx& b = M.vtx[s & (P.cap_v - 1)];
+    init_vertex(P, M, b, s);
+    b.parent = parent;
+    b.height = p.height;
+    b.vote = 1;
+    b.who = node;
+    b.depth = (p.vote ? p.depth : 0) + 1;
+    b.pow = (int32_t)(S.block((uint32_t)s, TAG_POW).w0 & 0x3FFFFFFFu);
+    b.ddepth = p.ddepth + 1;
+    b.sum = p.vote ? p.sum : parent;
+    X(P, M, b.sum).nconf += 1;
+    return s;
+  }
+  // Dag(node, Append, draft): Simulator.append dedup (simulator.ml:139-159) or a fresh
+  // summary with set_rewards (simulator.ml:377-388, tailstorm.ml:204-227). Returns the
+  // vertex (existing or new).
+  __host__ __device__ inline int32_t append_summary(const TsParams& P, const TsMem& M,
+                                                    int32_t dseq_) {
+    const int32_t* dr = M.drafts + (int64_t)(dseq_ & (P.cap_d - 1)) * (P.k + 2);
+    if (dr[0] != dseq_) {
+      fail(4);
+      return 0;
+    }
+    const int32_t nl = dr[1];
+    const int32_t* lv = dr + 2;
+    const TVtx& l0 = X(P, M, lv[0]);
+    const int32_t prev = l0.sum;
+    const int32_t height = X(P, M, prev).height + 1;
+    // candidates: children of lv[0], newest first; only summaries can equal the draft
+    for (int32_t c = newest; c > lv[0] && !dead; --c) {
+      const TVtx& y = X(P, M, c);
+      if (y.vote || y.height != height || y.parent != lv[0]) continue;
+      const int32_t* yq = Q(P, M, y);
+      bool eq = true;
+      const int32_t m = y.nq < nl ? y.nq : nl;
+      for (int32_t i = 0; i < m && eq; ++i) eq = yq[i] == lv[i];
+      if (eq && y.nq != nl) {  // List.for_all2 raises Invalid_argument
+        fail(11);
+        return c;
+      }
+      if (eq) return c;  // `Redundant
+    }
+    if (P.mode == 1 && ++zt > 4096) {  // loop-mode guard, see bk_lane.h
+      fail(8);
+      return 0;
+    }
+    const int32_t s = ++newest;
+    const int32_t qs = nsum++;
+    int32_t* q = M.quo + (int64_t)(qs & (P.cap_q - 1)) * (P.k + 1);
+    q[0] = s;
+    int32_t dd = 0;
+    for (int32_t i = 0; i < nl; ++i) {
+      q[1 + i] = lv[i];
+      const int32_t d = X(P, M, lv[i]).ddepth;
+      dd = d > dd ? d : dd;
+    }
+    // rewards: cumulative of the precursor (leaf 0 -> ... -> previous summary), then r per
+    // vote of the confirmed set (or of leaf 0's branch for punish/hybrid)
+    double* rw = R(P, M, qs);
+    const TVtx& ps = X(P, M, prev);
+    for (int32_t j = 0; j < P.n; ++j) {
+      rw[j] = ps.qslot < 0 ? 0.0 : R(P, M, ps.qslot)[j];
+      rw[P.n + j] = 0.0;
+    }
+    const bool punish = P.scheme == SC_PUNISH || P.scheme == SC_HYBRID;
+    const bool discount = P.scheme == SC_DISCOUNT || P.scheme == SC_HYBRID;
+    const double r = discount ? (double)l0.depth / (double)P.k * 1.0 : 1.0;
+    // the confirmed set = union of the leaves' branches; mark to count each vote once
+    const int32_t upto = punish ? 1 : nl;
+    for (int32_t t = 0; t < upto; ++t) {
+      int32_t v = lv[t];
+      while (v != prev && !dead) {
+        MK(P, M, v) = 0;
+        v = X(P, M, v).parent;
+      }
+    }
+    for (int32_t t = 0; t < upto; ++t) {
+      int32_t v = lv[t];
+      while (v != prev && !dead) {
+        uint8_t& mk = MK(P, M, v);
+        if (!mk) {
+          mk = 1;
+          const int32_t w = X(P, M, v).who;
+          rw[w] += r;
+          rw[P.n + w] += r;
+        }
+        v = X(P, M, v).parent;
+      }
+    }
+    TVtx& b = M.vtx[s & (P.cap_v - 1)];
+    init_vertex(P, M, b, s);
+    b.parent = lv[0];
+    b.height = height;
+    b.vote = 0;
+    b.who = -1;
+    b.depth = 0;
+    b.pow = 0;
+    b.ddepth = dd + 1;
+    b.sum = s;
+    b.qslot = qs;
+    b.nq = nl;
+    return s;
+  }
+
+  // ------------------------------------------------------------------ actions
+  __host__ __device__ inline void share(const TsParams& P, const TsMem& M, int32_t node,
+                                        int32_t s0) {
+    int32_t* st = M.stack;
+    int32_t sp = 0;
+    st[sp++] = s0;
+    while (sp > 0 && !dead) {
+      const int32_t s = st[--sp];
+      uint8_t& v = V(P, M, s, node);
+      if ((v & V_KIND) != V_WH) continue;
+      v = (uint8_t)((v & ~V_KIND) | V_REL);
+      push_now(P, M, mkev(EV_TX, node, KD_NET), s);
+      const TVtx& b = X(P, M, s);
+      if (b.parent < 0) continue;
+      const int32_t np = b.vote ? 1 : b.nq;
+      if (sp + np > NSTACK) {
+        fail(5);
+        return;
+      }
+      if (b.vote) {
+        st[sp++] = b.parent;
+      } else {
+        const int32_t* q = Q(P, M, b);
+        for (int32_t i = b.nq - 1; i >= 0; --i) st[sp++] = q[i];
+      }
+    }
+  }
+
+  // Dagtools.common_ancestor (dagtools.ml:102-121) in the attacker's view: ancestors by
+  // descending (Dag depth, serial), set semantics
+  __host__ __device__ static inline uint64_t fr_key(int32_t dd, int32_t s) {
+    return ((uint64_t)(uint32_t)dd << 32) | (uint32_t)s;
+  }
+  __host__ __device__ inline void fr_insert(int32_t* q, int32_t* nq, int32_t s, int32_t dd) {
+    const uint64_t kk = fr_key(dd, s);
+    for (int32_t j = 0; j < *nq; ++j)
+      if (q[2 * j + 1] == s) return;
+    if (*nq >= NFR) {
+      fail(10);
+      return;
+    }
+    int32_t i = *nq;
+    while (i > 0 && fr_key(q[2 * (i - 1)], q[2 * (i - 1) + 1]) < kk) {
+      q[2 * i] = q[2 * (i - 1)];
+      q[2 * i + 1] = q[2 * (i - 1) + 1];
+      --i;
+    }
+    q[2 * i] = dd;
+    q[2 * i + 1] = s;
+    ++*nq;
+  }
+  __host__ __device__ inline int32_t fr_next(const TsParams& P, const TsMem& M, int32_t* q,
+                                             int32_t* nq) {
+    if (*nq == 0) return -1;
+    const int32_t s = q[1];
+    for (int32_t j = 1; j < *nq; ++j) {
+      q[2 * (j - 1)] = q[2 * j];
+      q[2 * (j - 1) + 1] = q[2 * j + 1];
+    }
+    --*nq;
+    const TVtx& b = X(P, M, s);
+    if (b.parent >= 0) {
+      if (b.vote) {
+        fr_insert(q, nq, b.parent, X(P, M, b.parent).ddepth);
+      } else {
+        const int32_t* lq = Q(P, M, b);
+        for (int32_t i = 0; i < b.nq; ++i) fr_insert(q, nq, lq[i], X(P, M, lq[i]).ddepth);
+      }
+    }
+    return s;
+  }
+  __host__ __device__ inline int32_t common_ancestor(const TsParams& P, const TsMem& M,
+                                                     int32_t a, int32_t b) {
+    int32_t* qa = M.fr;
+    int32_t* qb = M.fr + 2 * NFR;
+    int32_t na = 0, nb = 0;
+    fr_insert(qa, &na, a, X(P, M, a).ddepth);
+    fr_insert(qb, &nb, b, X(P, M, b).ddepth);
+    int32_t x = fr_next(P, M, qa, &na);
+    int32_t y = fr_next(P, M, qb, &nb);
+    while (x >= 0 && y >= 0 && !dead) {
+      if (x == y) return x;
+      const uint64_t kx = fr_key(X(P, M, x).ddepth, x), ky = fr_key(X(P, M, y).ddepth, y);
+      if (kx > ky)
+        x = fr_next(P, M, qa, &na);
+      else
+        y = fr_next(P, M, qb, &nb);
+    }
+    fail(10);
+    return 0;
+  }
+
+  // ------------------------------------------------------------------ agent
+  // tailstorm_ssz.ml:210-258
+  __host__ __device__ inline void prepare(const TsParams& P, const TsMem& M, uint32_t kind,
+                                          int32_t x) {
+    int32_t p = pub;
+    for (int32_t i = 0; i < npend && !dead; ++i)
+      p = update_head(P, M, 0, VF_PUBLIC, p, X(P, M, M.pend[i]).sum);
+    int32_t q = priv;
+    if (kind == KD_APP) {
+      q = update_head(P, M, 0, VF_ALL, priv, x);
+      o_event = 0;
+    } else if (kind == KD_POW) {
+      o_event = 1;
+    } else {
+      p = update_head(P, M, 0, VF_PUBLIC, p, X(P, M, x).sum);
+      o_event = 2;
+    }
+    o_pub = p;
+    o_priv = q;
+    o_common = common_ancestor(P, M, p, q);
+  }
+  // tailstorm_ssz.ml:262-290
+  __host__ __device__ inline TsObs observe(const TsParams& P, const TsMem& M) {
+    TsObs o;
+    o.public_votes = count_post(P, M, o_pub, 0, VF_PUBLIC, &o.public_depth);
+    o.private_votes_inclusive = count_post(P, M, o_priv, 0, VF_ALL, &o.private_depth_inclusive);
+    o.private_votes_exclusive = count_post(P, M, o_priv, 0, VF_MINE, &o.private_depth_exclusive);
+    const int32_t ca = X(P, M, o_common).height;
+    const int32_t ph = X(P, M, o_priv).height, qh = X(P, M, o_pub).height;
+    o.private_blocks = ph - ca;
+    o.public_blocks = qh - ca;
+    o.diff_blocks = ph - qh;
+    o.event = o_event;
+    return o;
+  }
+  // tailstorm_ssz.ml:292-350
+  __host__ __device__ inline void apply(const TsParams& P, const TsMem& M, int32_t action) {
+    const int32_t kind = action & 3;  // 0 Adopt, 1 Override, 2 Match, 3 Wait
+    npend = 0;
+    if (kind == 1 || kind == 2) {
+      // withheld descendants of common in view 0, ascending (Dag depth, serial)
+      const int32_t c0 = o_common;
+      for (int32_t s = c0; s <= newest; ++s) MK(P, M, s) = 0;
+      int32_t nw = 0;
+      for (int32_t s = c0; s <= newest && !dead; ++s) {
+        const uint8_t v = V(P, M, s, 0);
+        if ((v & V_KIND) == V_INV) continue;
+        const TVtx& x = X(P, M, s);
+        bool d = s == c0;
+        if (!d && x.parent >= 0) {
+          if (x.vote) {
+            d = x.parent >= c0 && MK(P, M, x.parent);
+          } else {
+            const int32_t* lq = Q(P, M, x);
+            for (int32_t i = 0; i < x.nq && !d; ++i) d = lq[i] >= c0 && MK(P, M, lq[i]);
+          }
+        }
+        if (!d) continue;
+        MK(P, M, s) = 1;
+        if ((v & V_KIND) == V_WH) {
+          if (nw >= NPEND) {
+            fail(9);
+            break;
+          }
+          M.pend[nw++] = s;
+        }
+      }
+      // sort by (Dag depth, serial): insertion sort on the (mostly sorted) list
+      for (int32_t i = 1; i < nw; ++i) {
+        const int32_t v = M.pend[i];
+        const uint64_t kv = fr_key(X(P, M, v).ddepth, v);
+        int32_t j = i;
+        while (j > 0 && fr_key(X(P, M, M.pend[j - 1]).ddepth, M.pend[j - 1]) > kv) {
+          M.pend[j] = M.pend[j - 1];
+          --j;
+        }
+        M.pend[j] = v;
+      }
+      // release search: marks now hold the release set
+      for (int32_t s = c0; s <= newest; ++s) MK(P, M, s) = 0;
+      int32_t take = nw;
+      for (int32_t i = 0; i < nw && !dead; ++i) {
+        const int32_t x = M.pend[i];
+        MK(P, M, x) = 1;
+        if (update_head(P, M, 0, VF_PUBLIC_OR_MARKED, o_pub, X(P, M, x).sum) == o_pub) {
+          take = kind == 1 ? i + 1 : i;
+          break;
+        }
+      }
+      npend = take;
+      for (int32_t i = 0; i < npend && !dead; ++i) share(P, M, 0, M.pend[i]);
+    }
+    const int32_t np = kind == 0 ? o_pub : o_priv;
+    // extend: replace the private tip if it has no confirmation, else advance it
+    int32_t extend = o_priv;
+    if (!has_children(P, M, o_priv, 0)) {
+      const TVtx& pr = X(P, M, o_priv);
+      if (pr.parent < 0) {  // List.hd [] on the genesis summary
+        fail(11);
+        return;
+      }
+      extend = X(P, M, pr.parent).sum;
+    }
+    const int32_t d = next_summary(P, M, 0, extend, action >= 4 ? VF_ALL : VF_MINE);
+    if (d >= 0) push_now(P, M, mkev(EV_DAG, 0, KD_APP), d);
+    pub = o_pub;
+    priv = np;
+  }
+
+  // ------------------------------------------------------------------ engine
+  __host__ __device__ inline void init(const TsParams& P, const Stream& S, const TsMem& M) {
+    now = 0.0;
+    c_act = 0;
+    newest = 0;
+    nsum = 0;
+    act0 = 0;
+    hroot = -1;
+    hfree = -1;
+    hused = 0;
+    status = 0u;
+    dead = 0;
+    zt = 0;
+    dseq = 0;
+    npend = 0;
+    steps = 0;
+    TVtx& r = M.vtx[0];
+    r.serial = 0;
+    r.parent = -1;
+    r.height = 0;
+    r.vote = 0;
+    r.who = -1;
+    r.depth = 0;
+    r.pow = 0;
+    r.ddepth = 1;  // dag.ml:29: fold max 0 [] + 1
+    r.sum = 0;
+    r.nconf = 0;
+    r.qslot = -1;
+    r.nq = 0;
+    r.time = 0.0;
+    for (int32_t j = 0; j < P.n; ++j) {
+      V(P, M, 0, j) = V_RECV | V_GOT;
+      VT(P, M, 0, j) = 0.0;
+      M.tips[j] = 0;
+    }
+    pub = priv = 0;
+    schedule_pow(P, S, M);
+  }
+
+  // Honest.handler (tailstorm.ml:565-608) at defender `node` for vertex x
+  __host__ __device__ inline void honest(const TsParams& P, const TsMem& M, int32_t node,
+                                         int32_t x) {
+    if ((V(P, M, x, node) & V_KIND) == V_WH) share(P, M, node, x);
+    const TVtx& b = X(P, M, x);
+    int32_t& tip = M.tips[node];
+    if (!b.vote) {
+      tip = update_head(P, M, node, VF_ALL, tip, x);
+      return;
+    }
+    const int32_t s = b.sum;
+    int32_t d = -1;
+    if (feasible(P, M, node, tip, s)) d = next_summary(P, M, node, s, VF_ALL);
+    tip = update_head(P, M, node, VF_ALL, tip, s);
+    if (d >= 0) push_now(P, M, mkev(EV_DAG, node, KD_APP), d);
+  }
+
+  __host__ __device__ inline void handle(const TsParams& P, const Stream& S, const TsMem& M,
+                                         uint32_t ev, int32_t s) {
+    const uint32_t ty = ev & 7u, kind = (ev >> 3) & 3u;
+    const int32_t node = (int32_t)(ev >> 5);
+    switch (ty) {
+      case EV_MV: {
+        uint8_t& v = V(P, M, s, node);
+        if ((v & V_KIND) != V_INV) break;
+        const TVtx& b = X(P, M, s);
+        bool ok = true;
+        if (b.parent >= 0) {
+          if (b.vote) {
+            ok = visible(P, M, b.parent, node);
+          } else {
+            const int32_t* q = Q(P, M, b);
+            for (int32_t i = 0; i < b.nq && ok; ++i) ok = visible(P, M, q[i], node);
+          }
+        }
+        if (!ok) break;
+        v = (uint8_t)((v & ~V_KIND) | (kind == KD_NET ? V_RECV : V_WH));
+        VT(P, M, s, node) = now;
+        push_now(P, M, mkev(EV_ON, node, kind), s);
+        push_now(P, M, mkev(EV_MDV, node, kind), s);
+        break;
+      }
+      case EV_ON: {
+        if (node == 0) {  // loop mode: the attacker node's handler (tailstorm_ssz.ml:353-362)
+          prepare(P, M, kind, s);
+          if (!dead) apply(P, M, ts_policy(P.policy, P.k, observe(P, M)));
+          break;
+        }
+        honest(P, M, node, s);
+        break;
+      }
+      case EV_CLOCK: {
+        zt = 0;
+        const int32_t m = miner_of(P, S, c_act);
+        int32_t parent;
+        if (m == 0) {
+          ++act0;
+          parent = payload_parent(P, M, 0, priv);  // gym: replaced at the Dag event
+        } else {
+          parent = payload_parent(P, M, m, M.tips[m]);
+        }
+        push_now(P, M, mkev(EV_DAG, m, KD_POW), parent);
+        ++c_act;
+        schedule_pow(P, S, M);
+        break;
+      }
+      case EV_DAG: {
+        const int32_t v = kind == KD_POW ? append_vote(P, S, M, node, s) : append_summary(P, M, s);
+        if (!dead) push_now(P, M, mkev(EV_MV, node, kind), v);
+        break;
+      }
+      case EV_TX: {
+        for (int32_t dst = 0; dst < P.n; ++dst) {
+          if (dst == node) continue;
+          double delay;
+          if (P.net == 1)
+            delay = 0.0;
+          else if (node == 0)
+            delay = S.msg_u((uint32_t)s, (uint32_t)dst) * (P.dmax - 0.0) + 0.0;
+          else
+            delay = dst == 0 ? 0.0 : P.delta;
+          push(P, M, now + delay, mkev(EV_RX, dst, KD_NET), s);
+        }
+        break;
+      }
+      case EV_RX: {
+        if (!(now < __builtin_inf())) break;  // see bk_lane.h
+        uint8_t& v = V(P, M, s, node);
+        if (!(v & V_GOT)) {
+          v |= V_GOT;
+          push_now(P, M, mkev(EV_MV, node, KD_NET), s);
+        }
+        break;
+      }
+      case EV_MDV: {
+        // children (newest first) already received here: votes on s, summaries holding s
+        const bool sv = X(P, M, s).vote != 0;
+        for (int32_t c = newest; c > s && !dead; --c) {
+          if (!(V(P, M, c, node) & V_GOT)) continue;
+          const TVtx& cb = X(P, M, c);
+          bool child = cb.vote && cb.parent == s;
+          if (!child && sv && !cb.vote && cb.qslot >= 0) {
+            const int32_t* q = Q(P, M, cb);
+            for (int32_t i = 0; i < cb.nq; ++i) child |= q[i] == s;
+          }
+          if (child) push_now(P, M, mkev(EV_MV, node, KD_NET), c);
+        }
+        break;
+      }
+    }
+  }
+
+  __host__ __device__ inline bool skip_to_interaction(const TsParams& P, const Stream& S,
+                                                      const TsMem& M, uint32_t* kind,
+                                                      int32_t* blk) {
+    double t;
+    uint32_t ev;
+    int32_t s;
+    while (!dead) {
+      if (!pop(M, &t, &ev, &s)) {
+        fail(6);
+        return false;
+      }
+      now = t;
+      const uint32_t ty = ev & 7u;
+      const int32_t node = (int32_t)(ev >> 5);
+      const uint32_t kd = (ev >> 3) & 3u;
+      if (ty == EV_ON && node == 0) {
+        *kind = kd;
+        *blk = s;
+        return true;
+      }
+      if (ty == EV_DAG && node == 0 && kd == KD_POW) {
+        const int32_t v = append_vote(P, S, M, 0, payload_parent(P, M, 0, priv));
+        push_now(P, M, mkev(EV_MV, 0, KD_POW), v);
+        continue;
+      }
+      handle(P, S, M, ev, s);
+    }
+    return false;
+  }
+
+  // Referee.winner (tailstorm.ml:191-194): Compare.first (neg compare_summaries) 1 over
+  // [attacker preference; defenders' tips], i.e. the first element after Array.sort
+  __host__ __device__ inline int32_t head(const TsParams& P, const TsMem& M, int32_t att) {
+    int32_t v[65];
+    uint64_t k[65];
+    for (int32_t j = 0; j < P.n; ++j) {
+      const int32_t s = j == 0 ? att : M.tips[j];
+      const TVtx& x = X(P, M, s);
+      v[j] = s;
+      k[j] = ~(((uint64_t)(uint32_t)x.height << 32) | (uint32_t)x.nconf);
+    }
+    ocaml_heap_sort64(v, k, P.n);
+    return v[0];
+  }
+
+  __host__ __device__ inline void gym_reset(const TsParams& P, const Stream& S, const TsMem& M) {
+    init(P, S, M);
+    uint32_t kind;
+    int32_t b;
+    if (skip_to_interaction(P, S, M, &kind, &b)) prepare(P, M, kind, b);
+  }
+
+  __host__ __device__ inline int32_t gym_step(const TsParams& P, const Stream& S,
+                                              const TsMem& M, int32_t action, bool* done) {
+    apply(P, M, action);
+    ++steps;
+    uint32_t kind;
+    int32_t b;
+    const int32_t att = priv;
+    if (!dead && skip_to_interaction(P, S, M, &kind, &b)) prepare(P, M, kind, b);
+    const int32_t hd = dead ? 0 : head(P, M, att);
+    const double progress = (double)(X(P, M, hd).height * P.k);
+    *done = dead || !(steps < P.max_steps && progress < P.max_progress && now < P.max_time);
+    return hd;
+  }
+
+  __host__ __device__ inline int32_t loop(const TsParams& P, const Stream& S, const TsMem& M) {
+    init(P, S, M);
+    int64_t left = P.activations;
+    double t;
+    uint32_t ev;
+    int32_t s;
+    while (!dead && pop(M, &t, &ev, &s)) {
+      now = t;
+      if ((ev & 7u) == EV_CLOCK) {
+        if (left <= 0) continue;
+        --left;
+      }
+      handle(P, S, M, ev, s);
+    }
+    return dead ? 0 : head(P, M, priv);
+  }
+};
+
+}  // namespace ts
+}  // namespace cpr

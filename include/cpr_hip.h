@@ -152,9 +152,14 @@ enum cpr_episode_status {
   CPR_ST_DEEP_FORK = 4u,      /* Nakamoto: private chain beyond its slots */
   CPR_ST_TIE_UNRESOLVED = 8u, /* Nakamoto: tie replay capacity exceeded */
   CPR_ST_STALE_TIME = 16u,    /* Nakamoto: head time older than the time log */
-  CPR_ST_CAPACITY = 32u       /* Ethereum: a lane capacity (block ring, event heap, uncle
-                                 candidates, ancestor frontier) was exceeded; the episode's
+  CPR_ST_CAPACITY = 32u,      /* event-engine lanes (Ethereum, B_k, Tailstorm): a lane
+                                 capacity (vertex ring, event heap, candidate lists, frontier,
+                                 Tailstorm brute-force budget) was exceeded; the episode's
                                  outputs are not valid */
+  CPR_ST_REFERENCE_RAISES = 64u /* Tailstorm: the reference raises an exception at this point
+                                 (List.for_all2 in summary dedup, Division_by_zero in
+                                 n_choose_k, assert false in heuristic_quorum); the episode
+                                 stops, outputs not valid */
 };
 
 typedef struct cpr_config {

@@ -36,6 +36,17 @@ int64_t ocaml_n_choose_k(int64_t n, int64_t k) {
   return (a / b) / c;
 }
 
+int64_t true_n_choose_k_saturated(int64_t n, int64_t k) {
+  if (k < 0 || n < k) return 0;
+  if (k > n - k) k = n - k;
+  __int128 r = 1;
+  for (int64_t i = 1; i <= k; ++i) {
+    r = r * (n - k + i) / i;
+    if (r > (__int128)INT64_MAX) return INT64_MAX;
+  }
+  return (int64_t)r;
+}
+
 // ---------------------------------------------------------------- referee
 
 // tailstorm.ml:124-130: smaller is better: deeper first, then smaller pow (default min_pow)
@@ -322,6 +333,7 @@ bool TsView::optimal(Block* b, const VFilter& vf, std::vector<Block*>* q) const 
   const int n = (int)a.size();
   if (ocaml_n_choose_k(n, k) > 100) return heuristic(b, vf, q);
   if (n < k) return false;
+  if (true_n_choose_k_saturated(n, k) > TS_BRUTE_FORCE_BUDGET) throw BudgetExceeded();
   auto index_of = [&](Block* x) {
     for (int i = 0; i < n; ++i)
       if (a[i] == x) return i;

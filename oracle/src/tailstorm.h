@@ -15,6 +15,7 @@
 #include <cstdint>
 #include <functional>
 #include <set>
+#include <stdexcept>
 
 #include "bk.h"
 #include "des.h"
@@ -43,6 +44,15 @@ TsObs ts_obs_of_floats(const double in[TS_OBS_LEN], bool unit, int k);
 
 // combinatorics.ml:5-17 with OCaml's 63-bit wrap-around integer arithmetic
 int64_t ocaml_n_choose_k(int64_t n, int64_t k);
+// For n >= 21 the reference's n_choose_k overflows and often returns <= 100, so the
+// optimal quorum brute-forces the true C(n, k) choices (e.g. 48 million for n = 38, k = 8).
+// Both engines stop such a search at this budget and flag the episode (not a semantic
+// difference: an episode either completes identically or is flagged on both sides).
+constexpr int64_t TS_BRUTE_FORCE_BUDGET = 100000;
+struct BudgetExceeded : std::runtime_error {
+  BudgetExceeded() : std::runtime_error("optimal quorum: brute-force budget exceeded") {}
+};
+int64_t true_n_choose_k_saturated(int64_t n, int64_t k);  // saturates at INT64_MAX
 
 struct DagCmp {
   bool operator()(const Block* a, const Block* b) const {
