@@ -69,6 +69,8 @@ struct cpr_batch {
   DevBuf bk_mem;         // fused episodes: lanes x bk_bytes
   DevBuf bk_lmem, bk_slots;  // lockstep lanes: n_lanes x bk_bytes, n_lanes slots
   int64_t bk_bytes = 0;
+  ts::TsParams TP;       // CPR_PROTO_TAILSTORM (shares bk_mem / bk_lmem / bk_slots)
+  bool is_ev = false;    // B_k or Tailstorm event-engine lanes
   std::vector<uint8_t> table_host;
   DevBuf table_dev, tabs_dev;  // policy table; unit-observation tables
   DevBuf spill, tlog, replay, summary, records;
@@ -147,10 +149,13 @@ static int32_t pow2_at_least(int64_t x, int32_t cap) {
 static int validate_eth(const cpr_config* c, eth::EthParams* P);
 
 static int validate_bk(const cpr_config* c, bk::BkParams* P);
+static int validate_ts(const cpr_config* c, ts::TsParams* P);
 
-static int validate(const cpr_config* c, NakParams* P, eth::EthParams* EP, bk::BkParams* BP) {
+static int validate(const cpr_config* c, NakParams* P, eth::EthParams* EP, bk::BkParams* BP,
+                    ts::TsParams* TP) {
   if (c->protocol == CPR_PROTO_ETHEREUM) return validate_eth(c, EP);
   if (c->protocol == CPR_PROTO_BK) return validate_bk(c, BP);
+  if (c->protocol == CPR_PROTO_TAILSTORM) return validate_ts(c, TP);
   if (c->protocol != CPR_PROTO_NAKAMOTO)
     return fail(CPR_E_UNSUPPORTED, "protocol not implemented on the device yet");
   if (std::isnan(c->activation_delay)) return fail(CPR_E_INVALID_ARG, "activation_delay cannot be NaN");
@@ -376,15 +381,73 @@ static int validate_bk(const cpr_config* c, bk::BkParams* P) {
   return CPR_OK;
 }
 
+// Tailstorm: engine.ml:37-51 checks, network.ml:343-358, tailstorm.ml k >= 1, the four
+// incentive schemes and three sub-block selections, tailstorm_ssz policies 0..6
+static int validate_ts(const cpr_config* c, ts::TsParams* P) {
+  // the B_k checks cover everything but the scheme, selection and policy ranges
+  cpr_config cb = *c;
+  cb.protocol = CPR_PROTO_BK;
+  cb.reward_scheme = CPR_REWARD_CONSTANT;
+  cb.policy = CPR_BK_POLICY_HONEST;
+  bk::BkParams B;
+  int rc = validate_bk(&cb, &B);
+  if (rc) return rc;
+  if (c->reward_scheme != CPR_REWARD_CONSTANT && c->reward_scheme != CPR_REWARD_DISCOUNT &&
+      c->reward_scheme != CPR_REWARD_PUNISH && c->reward_scheme != CPR_REWARD_HYBRID)
+    return fail(CPR_E_INVALID_ARG, "'" + std::to_string(c->reward_scheme) +
+                                       "' is not a valid parameter choice, try 'constant', "
+                                       "'discount', 'punish' or 'hybrid'");
+  if (c->subblock_selection < CPR_SELECT_ALTRUISTIC || c->subblock_selection > CPR_SELECT_OPTIMAL)
+    return fail(CPR_E_INVALID_ARG, "'" + std::to_string(c->subblock_selection) +
+                                       "' is not a valid parameter choice, try 'altruistic', "
+                                       "'heuristic' or 'optimal'");
+  if (c->policy < CPR_TS_POLICY_HONEST || c->policy > CPR_TS_POLICY_LONG_DELAY)
+    return fail(CPR_E_INVALID_ARG, "unknown policy");
+  memset(P, 0, sizeof(*P));
+  P->t_att = B.t_att;
+  P->d = B.d;
+  P->n = B.n;
+  P->net = B.net;
+  P->mode = B.mode;
+  P->policy = c->policy;
+  P->scheme = c->reward_scheme;
+  P->selection = c->subblock_selection;
+  P->k = c->k;
+  P->ev = B.ev;
+  P->delta = B.delta;
+  P->dmax = B.dmax;
+  P->max_steps = B.max_steps;
+  P->activations = B.activations;
+  P->max_progress = B.max_progress;
+  P->max_time = B.max_time;
+  // gym: one vertex per attacker interaction plus summaries; loop: ~ (1 + 1/k) per
+  // activation. Vertex ring covers the whole episode up to 2^16 vertices.
+  const int64_t span = c->mode == CPR_MODE_GYM
+                           ? (B.max_steps < (1 << 20) ? B.max_steps + 2 : 8192)
+                           : c->activations * 2 + 2;
+  int32_t cv = 64;
+  while (cv < span + 64 && cv < (1 << 16)) cv <<= 1;
+  P->cap_v = cv;
+  P->cap_q = cv / 2;
+  P->cap_d = 64;
+  P->cap_e = 256 + 1024 * P->n +
+             (std::isfinite(P->dmax) || P->net == 1
+                  ? 0
+                  : (int32_t)(2 * P->d * std::min<int64_t>(span, 8192)));
+  return CPR_OK;
+}
+
 int cpr_batch_create(cpr_ctx* ctx, const cpr_config* cfg, cpr_batch** out) {
   if (!ctx || !cfg || !out) return fail(CPR_E_INVALID_ARG, "NULL argument");
   NakParams P;
   eth::EthParams EP;
   bk::BkParams BP;
+  ts::TsParams TP;
   memset(&P, 0, sizeof(P));
   memset(&EP, 0, sizeof(EP));
   memset(&BP, 0, sizeof(BP));
-  int rc = validate(cfg, &P, &EP, &BP);
+  memset(&TP, 0, sizeof(TP));
+  int rc = validate(cfg, &P, &EP, &BP, &TP);
   if (rc) return rc;
   HIP_TRY(hipSetDevice(ctx->device));
   cpr_batch* b = new cpr_batch;
@@ -393,8 +456,11 @@ int cpr_batch_create(cpr_ctx* ctx, const cpr_config* cfg, cpr_batch** out) {
   b->P = P;
   b->EP = EP;
   b->BP = BP;
+  b->TP = TP;
   b->eth_bytes = eth::eth_lane_bytes(EP.cap_b, EP.cap_e, EP.n);
   if (cfg->protocol == CPR_PROTO_BK) b->bk_bytes = bk::bk_lane_bytes(BP);
+  if (cfg->protocol == CPR_PROTO_TAILSTORM) b->bk_bytes = ts::ts_lane_bytes(TP);
+  b->is_ev = cfg->protocol == CPR_PROTO_BK || cfg->protocol == CPR_PROTO_TAILSTORM;
   b->cfg.policy_table = nullptr;
   if (cfg->protocol == CPR_PROTO_BK && cfg->policy == CPR_BK_POLICY_TABLE) {
     const size_t D = (size_t)cfg->policy_table_dim, K1 = (size_t)cfg->k + 1;
@@ -405,7 +471,8 @@ int cpr_batch_create(cpr_ctx* ctx, const cpr_config* cfg, cpr_batch** out) {
   }
   // unit-observation tables (ssz_tools.ml:487-491) evaluated with the host libm:
   // [2/pi atan(i) | 0.5 + atan(i - N)/pi (2N) | 2/pi atan(i/k)], i < N
-  const double kscale = cfg->protocol == CPR_PROTO_BK ? (double)cfg->k : 1.0;
+  const double kscale =
+      (cfg->protocol == CPR_PROTO_BK || cfg->protocol == CPR_PROTO_TAILSTORM) ? (double)cfg->k : 1.0;
   std::vector<double> tabs(4 * (size_t)b->tab_n);
   for (int i = 0; i < b->tab_n; i++) tabs[i] = 2. / M_PI * std::atan((double)i / 1.0);
   for (int i = 0; i < 2 * b->tab_n; i++)
@@ -491,7 +558,8 @@ static int run_async_eth(cpr_batch* b, int64_t n, uint64_t first, cpr_summary* s
 // B_k lanes: resident capacity bounded by a 32 GiB budget for the per-lane regions
 static int run_async_bk(cpr_batch* b, int64_t n, uint64_t first, cpr_summary* sum_dev,
                         cpr_episode_record* rec_dev) {
-  const int64_t full = (int64_t)b->ctx->cus * bk_blocks_per_cu() * 256;
+  const bool tsp = b->cfg.protocol == CPR_PROTO_TAILSTORM;
+  const int64_t full = (int64_t)b->ctx->cus * (tsp ? ts_blocks_per_cu() : bk_blocks_per_cu()) * 256;
   const int64_t budget = (int64_t)(32ll << 30) / b->bk_bytes;
   int64_t lanes = std::min(full, std::max<int64_t>(256, budget));
   lanes = std::min(lanes, ((n + 255) / 256) * 256);
@@ -502,8 +570,12 @@ static int run_async_bk(cpr_batch* b, int64_t n, uint64_t first, cpr_summary* su
     HIP_TRY(hipEventCreate(&b->ev1));
   }
   HIP_TRY(hipEventRecord(b->ev0, b->ctx->stream));
-  HIP_TRY(launch_bk_run_episodes(b->BP, b->cfg.seed, first, n, (uint8_t*)b->bk_mem.p,
-                                 b->bk_bytes, lanes, rec_dev, sum_dev, b->ctx->stream));
+  if (tsp)
+    HIP_TRY(launch_ts_run_episodes(b->TP, b->cfg.seed, first, n, (uint8_t*)b->bk_mem.p,
+                                   b->bk_bytes, lanes, rec_dev, sum_dev, b->ctx->stream));
+  else
+    HIP_TRY(launch_bk_run_episodes(b->BP, b->cfg.seed, first, n, (uint8_t*)b->bk_mem.p,
+                                   b->bk_bytes, lanes, rec_dev, sum_dev, b->ctx->stream));
   HIP_TRY(hipEventRecord(b->ev1, b->ctx->stream));
   return CPR_OK;
 }
@@ -511,7 +583,7 @@ static int run_async_bk(cpr_batch* b, int64_t n, uint64_t first, cpr_summary* su
 static int run_async(cpr_batch* b, int64_t n, uint64_t first, cpr_summary* sum_dev,
                      cpr_episode_record* rec_dev) {
   if (b->cfg.protocol == CPR_PROTO_ETHEREUM) return run_async_eth(b, n, first, sum_dev, rec_dev);
-  if (b->cfg.protocol == CPR_PROTO_BK) return run_async_bk(b, n, first, sum_dev, rec_dev);
+  if (b->is_ev) return run_async_bk(b, n, first, sum_dev, rec_dev);
   const int64_t lanes = episode_lanes(b, n);
   if (lanes > b->lanes_alloc) {
     HIP_TRY(b->spill.ensure((size_t)lanes * b->P.cap * sizeof(int32_t)));
@@ -587,7 +659,12 @@ int cpr_run_episodes(cpr_batch* b, int64_t n, uint64_t first, cpr_summary* summa
 // ---------------------------------------------------------------- lockstep API
 
 static int obs_len_of(const cpr_config& c) {
-  return c.protocol == CPR_PROTO_BK ? 8 : (c.protocol == CPR_PROTO_ETHEREUM ? 10 : 4);
+  switch (c.protocol) {
+    case CPR_PROTO_BK: return 8;
+    case CPR_PROTO_ETHEREUM: return 10;
+    case CPR_PROTO_TAILSTORM: return 10;
+    default: return 4;
+  }
 }
 
 static int ensure_common_lockstep(cpr_batch* b, int obs_len) {
@@ -608,14 +685,15 @@ static int ensure_lockstep_bk(cpr_batch* b) {
   if (b->cfg.mode != CPR_MODE_GYM) return fail(CPR_E_STATE, "lockstep lanes need CPR_MODE_GYM");
   if (!b->bk_slots.p) {
     HIP_TRY(b->bk_lmem.ensure((size_t)n * (size_t)b->bk_bytes));
-    HIP_TRY(b->bk_slots.ensure((size_t)n * bk_slot_bytes()));
-    HIP_TRY(hipMemsetAsync(b->bk_slots.p, 0, (size_t)n * bk_slot_bytes(), b->ctx->stream));
+    const size_t sb = b->cfg.protocol == CPR_PROTO_TAILSTORM ? ts_slot_bytes() : bk_slot_bytes();
+    HIP_TRY(b->bk_slots.ensure((size_t)n * sb));
+    HIP_TRY(hipMemsetAsync(b->bk_slots.p, 0, (size_t)n * sb, b->ctx->stream));
   }
-  return ensure_common_lockstep(b, 8);
+  return ensure_common_lockstep(b, obs_len_of(b->cfg));
 }
 
 static int ensure_lockstep(cpr_batch* b) {
-  if (b->cfg.protocol == CPR_PROTO_BK) return ensure_lockstep_bk(b);
+  if (b->is_ev) return ensure_lockstep_bk(b);
   if (b->cfg.protocol != CPR_PROTO_NAKAMOTO)
     return fail(CPR_E_UNSUPPORTED, "lockstep lanes are implemented for Nakamoto and B_k");
   const int64_t n = b->cfg.n_lanes;
@@ -673,6 +751,10 @@ int cpr_reset(cpr_batch* b, const uint8_t* mask, const uint64_t* eps, double* ob
     HIP_TRY(launch_bk_reset(b->BP, b->cfg.seed, (uint8_t*)b->bk_lmem.p, b->bk_bytes,
                             b->bk_slots.p, n, dmask, deps, b->cfg.unit_observation, tabs,
                             b->tab_n, (double*)b->l_obs.p, st));
+  else if (b->cfg.protocol == CPR_PROTO_TAILSTORM)
+    HIP_TRY(launch_ts_reset(b->TP, b->cfg.seed, (uint8_t*)b->bk_lmem.p, b->bk_bytes,
+                            b->bk_slots.p, n, dmask, deps, b->cfg.unit_observation, tabs,
+                            b->tab_n, (double*)b->l_obs.p, st));
   else
     HIP_TRY(launch_reset(b->P, b->cfg.seed, lock_buffers(b), n, dmask, deps,
                          b->cfg.unit_observation, tabs, tabs + b->tab_n, b->tab_n,
@@ -688,7 +770,7 @@ int cpr_step(cpr_batch* b, const int32_t* actions, double* obs, double* reward, 
   if (!b || !actions || !obs || !reward || !done) return fail(CPR_E_INVALID_ARG, "NULL argument");
   if (!b->reset_done) return fail(CPR_E_STATE, "step before reset");
   const int64_t n = b->cfg.n_lanes;
-  const int n_act = b->cfg.protocol == CPR_PROTO_BK ? 8 : 4;
+  const int n_act = b->is_ev ? 8 : 4;
   const int ol = obs_len_of(b->cfg);
   for (int64_t i = 0; i < n; i++)
     if (actions[i] < 0 || actions[i] >= n_act)
@@ -713,6 +795,10 @@ int cpr_step(cpr_batch* b, const int32_t* actions, double* obs, double* reward, 
   const double* tabs = (const double*)b->tabs_dev.p;
   if (b->cfg.protocol == CPR_PROTO_BK)
     HIP_TRY(launch_bk_step(b->BP, b->cfg.seed, (uint8_t*)b->bk_lmem.p, b->bk_bytes,
+                           b->bk_slots.p, n, (const int32_t*)b->l_act.p,
+                           b->cfg.unit_observation, tabs, b->tab_n, sb, st));
+  else if (b->cfg.protocol == CPR_PROTO_TAILSTORM)
+    HIP_TRY(launch_ts_step(b->TP, b->cfg.seed, (uint8_t*)b->bk_lmem.p, b->bk_bytes,
                            b->bk_slots.p, n, (const int32_t*)b->l_act.p,
                            b->cfg.unit_observation, tabs, b->tab_n, sb, st));
   else
@@ -740,8 +826,8 @@ int cpr_step(cpr_batch* b, const int32_t* actions, double* obs, double* reward, 
 
 int cpr_observe_fields(cpr_batch* b, int32_t* fields) {
   if (!b || !fields) return fail(CPR_E_INVALID_ARG, "NULL argument");
-  if (b->cfg.protocol != CPR_PROTO_NAKAMOTO && b->cfg.protocol != CPR_PROTO_BK)
-    return fail(CPR_E_UNSUPPORTED, "lockstep lanes are implemented for Nakamoto and B_k");
+  if (b->cfg.protocol == CPR_PROTO_ETHEREUM)
+    return fail(CPR_E_UNSUPPORTED, "lockstep lanes are implemented for Nakamoto, B_k, Tailstorm");
   if (!b->reset_done) return fail(CPR_E_STATE, "observe before reset");
   const int64_t n = b->cfg.n_lanes;
   HIP_TRY(hipSetDevice(b->ctx->device));
@@ -751,6 +837,9 @@ int cpr_observe_fields(cpr_batch* b, int32_t* fields) {
   HIP_TRY(tmp.ensure((size_t)n * per));
   if (b->cfg.protocol == CPR_PROTO_BK)
     HIP_TRY(launch_bk_observe_fields(b->BP, (uint8_t*)b->bk_lmem.p, b->bk_bytes, b->bk_slots.p,
+                                     n, (int32_t*)tmp.p, st));
+  else if (b->cfg.protocol == CPR_PROTO_TAILSTORM)
+    HIP_TRY(launch_ts_observe_fields(b->TP, (uint8_t*)b->bk_lmem.p, b->bk_bytes, b->bk_slots.p,
                                      n, (int32_t*)tmp.p, st));
   else
     HIP_TRY(launch_observe_fields(b->lanes.p, n, (int32_t*)tmp.p, st));
@@ -763,6 +852,22 @@ int cpr_observe_fields(cpr_batch* b, int32_t* fields) {
 int cpr_policy_actions(cpr_batch* b, int32_t policy, const double* obs, int64_t n,
                        int32_t* actions) {
   if (!b || !obs || !actions) return fail(CPR_E_INVALID_ARG, "NULL argument");
+  if (b->cfg.protocol == CPR_PROTO_TAILSTORM) {
+    if (policy < 0 || policy > CPR_TS_POLICY_LONG_DELAY)
+      return fail(CPR_E_INVALID_ARG, "unknown policy");
+    if (n <= 0) return CPR_OK;
+    HIP_TRY(hipSetDevice(b->ctx->device));
+    hipStream_t st = b->ctx->stream;
+    DevBuf o, a;
+    HIP_TRY(o.ensure((size_t)n * 80));
+    HIP_TRY(a.ensure((size_t)n * 4));
+    HIP_TRY(hipMemcpyAsync(o.p, obs, (size_t)n * 80, hipMemcpyHostToDevice, st));
+    HIP_TRY(launch_ts_policy(policy, b->cfg.k, b->cfg.unit_observation, (const double*)o.p, n,
+                             (int32_t*)a.p, st));
+    HIP_TRY(hipMemcpyAsync(actions, a.p, (size_t)n * 4, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    return CPR_OK;
+  }
   if (b->cfg.protocol == CPR_PROTO_BK) {
     if (policy < 0 || policy > CPR_BK_POLICY_TABLE) return fail(CPR_E_INVALID_ARG, "unknown policy");
     if (policy == CPR_BK_POLICY_TABLE && b->table_host.empty())
@@ -808,6 +913,21 @@ int cpr_observation_spec(cpr_batch* b, int32_t* obs_len, int32_t* n_actions, dou
                          double* high) {
   if (!b) return fail(CPR_E_INVALID_ARG, "NULL argument");
   const double inf = __builtin_inf();
+  if (b->cfg.protocol == CPR_PROTO_TAILSTORM) {
+    // tailstorm_ssz.ml:41-79: 10 fields (diff signed, event discrete), Action8
+    if (obs_len) *obs_len = 10;
+    if (n_actions) *n_actions = 8;
+    for (int i = 0; i < 10; i++) {
+      double lo = 0.0, hi = 1.0;
+      if (!b->cfg.unit_observation) {
+        lo = i == 2 ? -inf : 0.0;
+        hi = i == 9 ? 2.0 : inf;
+      }
+      if (low) low[i] = lo;
+      if (high) high[i] = hi;
+    }
+    return CPR_OK;
+  }
   if (b->cfg.protocol == CPR_PROTO_BK) {
     // bk_ssz.ml:37-74 normalizers; ssz_tools.ml:64-74 ranges (raw Bool range is (0, 0))
     if (obs_len) *obs_len = 8;
@@ -874,11 +994,20 @@ static const char* kBkNames[4] = {"avoid-loss", "minor-delay", "get-ahead", "hon
 static const int32_t kBkIds[4] = {CPR_BK_POLICY_AVOID_LOSS, CPR_BK_POLICY_MINOR_DELAY,
                                   CPR_BK_POLICY_GET_AHEAD, CPR_BK_POLICY_HONEST};
 
+// tailstorm_ssz.ml:449-472, same reversal
+static const char* kTsNames[7] = {"long-delay", "avoid-loss-b", "avoid-loss-a", "avoid-loss",
+                                  "minor-delay", "get-ahead", "honest"};
+static const int32_t kTsIds[7] = {CPR_TS_POLICY_LONG_DELAY, CPR_TS_POLICY_AVOID_LOSS_B,
+                                  CPR_TS_POLICY_AVOID_LOSS_A, CPR_TS_POLICY_AVOID_LOSS,
+                                  CPR_TS_POLICY_MINOR_DELAY, CPR_TS_POLICY_GET_AHEAD,
+                                  CPR_TS_POLICY_HONEST};
+
 int cpr_policy_count(int32_t protocol) {
   switch (protocol) {
     case CPR_PROTO_NAKAMOTO: return 4;
     case CPR_PROTO_ETHEREUM: return 5;
     case CPR_PROTO_BK: return 4;
+    case CPR_PROTO_TAILSTORM: return 7;
     default: return 0;
   }
 }
@@ -896,6 +1025,10 @@ const char* cpr_policy_name(int32_t protocol, int32_t index, int32_t* policy_id)
     if (policy_id) *policy_id = kBkIds[index];
     return kBkNames[index];
   }
+  if (protocol == CPR_PROTO_TAILSTORM) {
+    if (policy_id) *policy_id = kTsIds[index];
+    return kTsNames[index];
+  }
   if (policy_id) *policy_id = kIds[index];
   return kNames[index];
 }
@@ -903,8 +1036,8 @@ const char* cpr_policy_name(int32_t protocol, int32_t index, int32_t* policy_id)
 int cpr_rollout(cpr_batch* b, int64_t n_steps, double* obs, double* reward, uint8_t* done,
                 int outputs_on_device, cpr_summary* summary) {
   if (!b || !summary) return fail(CPR_E_INVALID_ARG, "NULL argument");
-  if (b->cfg.protocol != CPR_PROTO_BK)
-    return fail(CPR_E_UNSUPPORTED, "cpr_rollout is implemented for B_k");
+  if (!b->is_ev)
+    return fail(CPR_E_UNSUPPORTED, "cpr_rollout is implemented for B_k and Tailstorm");
   if (n_steps <= 0) return CPR_OK;
   HIP_TRY(hipSetDevice(b->ctx->device));
   int rc = ensure_lockstep(b);
@@ -938,10 +1071,16 @@ int cpr_rollout(cpr_batch* b, int64_t n_steps, double* obs, double* reward, uint
   }
   const double* tabs = (const double*)b->tabs_dev.p;
   HIP_TRY(hipEventRecord(b->ev0, st));
-  HIP_TRY(launch_bk_rollout(b->BP, b->cfg.seed, (uint8_t*)b->bk_lmem.p, b->bk_bytes,
-                            b->bk_slots.p, b->cfg.n_lanes, n_steps, b->cfg.unit_observation,
-                            tabs, b->tab_n, obs_dev, reward_dev, done_dev,
-                            (cpr_summary*)b->summary.p, st));
+  if (b->cfg.protocol == CPR_PROTO_TAILSTORM)
+    HIP_TRY(launch_ts_rollout(b->TP, b->cfg.seed, (uint8_t*)b->bk_lmem.p, b->bk_bytes,
+                              b->bk_slots.p, b->cfg.n_lanes, n_steps, b->cfg.unit_observation,
+                              tabs, b->tab_n, obs_dev, reward_dev, done_dev,
+                              (cpr_summary*)b->summary.p, st));
+  else
+    HIP_TRY(launch_bk_rollout(b->BP, b->cfg.seed, (uint8_t*)b->bk_lmem.p, b->bk_bytes,
+                              b->bk_slots.p, b->cfg.n_lanes, n_steps, b->cfg.unit_observation,
+                              tabs, b->tab_n, obs_dev, reward_dev, done_dev,
+                              (cpr_summary*)b->summary.p, st));
   HIP_TRY(hipEventRecord(b->ev1, st));
   cpr_summary s;
   HIP_TRY(hipMemcpyAsync(&s, b->summary.p, sizeof(s), hipMemcpyDeviceToHost, st));

@@ -8,6 +8,7 @@
 #include "bk_lane.h"
 #include "ethereum_lane.h"
 #include "nakamoto_lane.h"
+#include "ts_lane.h"
 
 namespace cpr {
 
@@ -86,6 +87,27 @@ hipError_t launch_bk_policy(const bk::BkParams& P, int unit, const double* obs, 
                             int32_t* actions, hipStream_t st);
 size_t bk_slot_bytes();
 int bk_blocks_per_cu();
+
+// Tailstorm (kernels_ts.hip), same shapes as the B_k launchers
+hipError_t launch_ts_run_episodes(const ts::TsParams& P, uint64_t seed, uint64_t first,
+                                  int64_t n_eps, uint8_t* mem, int64_t lane_bytes, int64_t lanes,
+                                  cpr_episode_record* recs, cpr_summary* sum, hipStream_t st);
+hipError_t launch_ts_reset(const ts::TsParams& P, uint64_t seed, uint8_t* mem, int64_t lane_bytes,
+                           void* slots, int64_t n, const uint8_t* mask, const uint64_t* eps,
+                           int unit, const double* tabs, int32_t tn, double* obs, hipStream_t st);
+hipError_t launch_ts_step(const ts::TsParams& P, uint64_t seed, uint8_t* mem, int64_t lane_bytes,
+                          void* slots, int64_t n, const int32_t* actions, int unit,
+                          const double* tabs, int32_t tn, const StepBuffers& b, hipStream_t st);
+hipError_t launch_ts_rollout(const ts::TsParams& P, uint64_t seed, uint8_t* mem,
+                             int64_t lane_bytes, void* slots, int64_t n, int64_t n_steps,
+                             int unit, const double* tabs, int32_t tn, double* obs,
+                             double* reward, uint8_t* done, cpr_summary* sum, hipStream_t st);
+hipError_t launch_ts_observe_fields(const ts::TsParams& P, uint8_t* mem, int64_t lane_bytes,
+                                    const void* slots, int64_t n, int32_t* f, hipStream_t st);
+hipError_t launch_ts_policy(int32_t policy, int32_t k, int unit, const double* obs, int64_t n,
+                            int32_t* actions, hipStream_t st);
+size_t ts_slot_bytes();
+int ts_blocks_per_cu();
 int run_episodes_blocks_per_cu(int32_t mode);  // resident 256-lane workgroups per CU
 
 }  // namespace cpr

@@ -1,0 +1,323 @@
+// Tailstorm kernels for gfx950: one lane = one episode / gym env of the tailstorm_ssz
+// attack space, driven by the exact per-lane event engine of ts_lane.h (same launch
+// structure as kernels_bk.hip: fused episodes, lockstep reset/step, device rollout).
+#include <hip/hip_runtime.h>
+
+#include "../../include/cpr_hip.h"
+#include "kernels.h"
+#include "summary.h"
+#include "ts_lane.h"
+
+#pragma clang fp contract(off)
+
+namespace cpr {
+
+struct TsSlot {
+  ts::TsLane L;
+  uint64_t ep;
+  double last_ra;
+  int32_t live;
+};
+
+// head rewards: engine.ml:215-219 folds head.rewards left to right
+__device__ inline void ts_head_rewards(const ts::TsParams& P, ts::TsLane& L, const ts::TsMem& M,
+                                       int32_t hd, double* ra, double* rd) {
+  const ts::TVtx& h = L.X(P, M, hd);
+  *ra = 0.0;
+  *rd = 0.0;
+  if (h.qslot < 0) return;
+  const double* rw = L.R(P, M, h.qslot);
+  *ra = rw[0];
+  double s = 0.0;
+  for (int32_t j = 1; j < P.n; ++j) s += rw[j];
+  *rd = s;
+}
+
+__device__ inline void ts_acc(Acc& acc, const ts::TsParams& P, ts::TsLane& L,
+                              const ts::TsMem& M, int32_t hd, int32_t* hist) {
+  double ra, rd;
+  ts_head_rewards(P, L, M, hd, &ra, &rd);
+  const int32_t h = L.X(P, M, hd).height;
+  const double rel = (ra + rd) != 0.0 ? ra / (ra + rd) : 0.0;
+  acc_episode(acc, (int64_t)__builtin_rint(ra * 1048576.0), (int64_t)__builtin_rint(rd * 1048576.0),
+              (int64_t)h * P.k << 20, rel, (int64_t)h * P.k, L.steps, L.c_act, L.status, hist);
+}
+
+__global__ __launch_bounds__(kBlock) void k_ts_run_episodes(
+    ts::TsParams P, uint64_t seed, uint64_t first, int64_t n_eps, uint8_t* mem,
+    int64_t lane_bytes, cpr_episode_record* recs, cpr_summary* sum) {
+  __shared__ int32_t hist[CPR_HIST_BINS];
+  if (threadIdx.x < CPR_HIST_BINS) hist[threadIdx.x] = 0;
+  __syncthreads();
+  const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t nthreads = (int64_t)gridDim.x * blockDim.x;
+  const ts::TsMem M = ts::ts_mem_at(mem + tid * lane_bytes, P);
+  Acc acc = {};
+  ts::TsLane L;
+  for (int64_t e = tid; e < n_eps; e += nthreads) {
+    const uint64_t ep = first + (uint64_t)e;
+    const Stream S = make_stream(seed, ep);
+    int32_t hd;
+    if (P.mode == CPR_MODE_GYM) {
+      L.gym_reset(P, S, M);
+      bool done = L.dead != 0;
+      hd = 0;
+      while (!done) hd = L.gym_step(P, S, M, ts::ts_policy(P.policy, P.k, L.observe(P, M)), &done);
+    } else {
+      hd = L.loop(P, S, M);
+    }
+    ts_acc(acc, P, L, M, hd, hist);
+    if (recs) {
+      cpr_episode_record r;
+      ts_head_rewards(P, L, M, hd, &r.reward_attacker, &r.reward_defender);
+      const ts::TVtx& h = L.X(P, M, hd);
+      r.progress = (double)(h.height * P.k);
+      r.chain_time = h.time;
+      r.sim_time = P.mode == CPR_MODE_GYM ? L.now : 0.0;
+      r.n_steps = L.steps;
+      r.n_activations = L.c_act;
+      r.head_height = h.height;
+      r.head_miner = -1;
+      r.status = L.status;
+      r.head_work = 0;
+      recs[e] = r;
+    }
+  }
+  __syncthreads();
+  block_flush(acc, hist, sum);
+}
+
+// tailstorm_ssz.ml:41-55 normalizers; tabs as in kernels_bk.hip
+__device__ inline void ts_write_obs(const ts::TsObs& o, int unit, const double* tabs, int32_t tn,
+                                    int32_t k, double* out) {
+  const double pi = 3.141592653589793;
+  const int32_t v[10] = {o.public_blocks,           o.private_blocks,
+                         o.diff_blocks,             o.public_votes,
+                         o.private_votes_inclusive, o.private_votes_exclusive,
+                         o.public_depth,            o.private_depth_inclusive,
+                         o.private_depth_exclusive, o.event};
+  if (!unit) {
+    for (int i = 0; i < 10; ++i) out[i] = (double)v[i];
+    return;
+  }
+  for (int i = 0; i < 9; ++i) {
+    const int32_t x = v[i];
+    if (i == 2)
+      out[i] = (x > -tn && x < tn) ? tabs[tn + x + tn] : 0.5 + (1.0 / pi * atan((double)x / 1.0));
+    else if (i < 2)
+      out[i] = x < tn ? tabs[x] : 2.0 / pi * atan((double)x / 1.0);
+    else
+      out[i] = x < tn ? tabs[3 * tn + x] : 2.0 / pi * atan((double)x / (double)k);
+  }
+  out[9] = (double)v[9] / 2.0;
+}
+
+__device__ inline void ts_slot_reset(const ts::TsParams& P, uint64_t seed, const ts::TsMem& M,
+                                     TsSlot& SL, uint64_t ep) {
+  SL.ep = ep;
+  SL.last_ra = 0.0;
+  SL.live = 1;
+  SL.L.gym_reset(P, make_stream(seed, ep), M);
+}
+
+__global__ __launch_bounds__(kBlock) void k_ts_reset(ts::TsParams P, uint64_t seed, uint8_t* mem,
+                                                      int64_t lane_bytes, TsSlot* slots,
+                                                      int64_t n, const uint8_t* mask,
+                                                      const uint64_t* eps, int unit,
+                                                      const double* tabs, int32_t tn,
+                                                      double* obs) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const ts::TsMem M = ts::ts_mem_at(mem + i * lane_bytes, P);
+  TsSlot SL = slots[i];
+  if (mask == nullptr || mask[i]) ts_slot_reset(P, seed, M, SL, eps ? eps[i] : (uint64_t)i);
+  ts_write_obs(SL.L.observe(P, M), unit, tabs, tn, P.k, obs + 10 * i);
+  slots[i] = SL;
+}
+
+__global__ __launch_bounds__(kBlock) void k_ts_step(ts::TsParams P, uint64_t seed, uint8_t* mem,
+                                                     int64_t lane_bytes, TsSlot* slots,
+                                                     int64_t n, const int32_t* actions, int unit,
+                                                     const double* tabs, int32_t tn,
+                                                     StepBuffers out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const ts::TsMem M = ts::ts_mem_at(mem + i * lane_bytes, P);
+  TsSlot SL = slots[i];
+  const Stream S = make_stream(seed, SL.ep);
+  bool done = false;
+  const int32_t hd = SL.L.gym_step(P, S, M, actions[i], &done);
+  double ra, rd;
+  ts_head_rewards(P, SL.L, M, hd, &ra, &rd);
+  const ts::TVtx& h = SL.L.X(P, M, hd);
+  out.reward[i] = ra - SL.last_ra;
+  out.done[i] = done ? 1 : 0;
+  if (out.era) {
+    out.era[i] = ra;
+    out.erd[i] = rd;
+    out.eprog[i] = (double)(h.height * P.k);
+    out.ect[i] = h.time;
+    out.est[i] = SL.L.now;
+    out.esteps[i] = SL.L.steps;
+    out.eacts[i] = SL.L.c_act;
+    out.hh[i] = h.height;
+    out.hm[i] = -1;
+  }
+  SL.last_ra = ra;
+  ts_write_obs(SL.L.observe(P, M), unit, tabs, tn, P.k, out.obs + 10 * i);
+  slots[i] = SL;
+}
+
+// see k_bk_rollout
+__global__ __launch_bounds__(kBlock) void k_ts_rollout(ts::TsParams P, uint64_t seed,
+                                                        uint8_t* mem, int64_t lane_bytes,
+                                                        TsSlot* slots, int64_t n,
+                                                        int64_t n_steps, int unit,
+                                                        const double* tabs, int32_t tn,
+                                                        double* obs, double* reward,
+                                                        uint8_t* done_out, cpr_summary* sum) {
+  __shared__ int32_t hist[CPR_HIST_BINS];
+  if (threadIdx.x < CPR_HIST_BINS) hist[threadIdx.x] = 0;
+  __syncthreads();
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  Acc acc = {};
+  int64_t steps_all = 0, acts_all = 0;
+  if (i < n) {
+    const ts::TsMem M = ts::ts_mem_at(mem + i * lane_bytes, P);
+    TsSlot SL = slots[i];
+    if (!SL.live) {
+      ts_slot_reset(P, seed, M, SL, (uint64_t)i);
+      acts_all += SL.L.c_act;
+    }
+    Stream S = make_stream(seed, SL.ep);
+    for (int64_t t = 0; t < n_steps; ++t) {
+      const ts::TsObs o = SL.L.observe(P, M);
+      const int32_t c0 = SL.L.c_act;
+      bool done = false;
+      const int32_t hd = SL.L.gym_step(P, S, M, ts::ts_policy(P.policy, P.k, o), &done);
+      acts_all += SL.L.c_act - c0;
+      ++steps_all;
+      double ra, rd;
+      ts_head_rewards(P, SL.L, M, hd, &ra, &rd);
+      const int64_t kk = t * n + i;
+      if (reward) reward[kk] = ra - SL.last_ra;
+      if (done_out) done_out[kk] = done ? 1 : 0;
+      SL.last_ra = ra;
+      if (done) {
+        ts_acc(acc, P, SL.L, M, hd, hist);
+        ts_slot_reset(P, seed, M, SL, SL.ep + (uint64_t)n);
+        acts_all += SL.L.c_act;
+        S = make_stream(seed, SL.ep);
+      }
+      if (obs) ts_write_obs(SL.L.observe(P, M), unit, tabs, tn, P.k, obs + 10 * kk);
+    }
+    slots[i] = SL;
+  }
+  acc.steps = steps_all;
+  acc.activations = acts_all;
+  __syncthreads();
+  block_flush(acc, hist, sum);
+}
+
+__global__ void k_ts_observe_fields(ts::TsParams P, uint8_t* mem, int64_t lane_bytes,
+                                    const TsSlot* slots, int64_t n, int32_t* f) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const ts::TsMem M = ts::ts_mem_at(mem + i * lane_bytes, P);
+  ts::TsLane L = slots[i].L;
+  const ts::TsObs o = L.observe(P, M);
+  const int32_t v[10] = {o.public_blocks,           o.private_blocks,
+                         o.diff_blocks,             o.public_votes,
+                         o.private_votes_inclusive, o.private_votes_exclusive,
+                         o.public_depth,            o.private_depth_inclusive,
+                         o.private_depth_exclusive, o.event};
+  for (int j = 0; j < 10; ++j) f[10 * i + j] = v[j];
+}
+
+// engine.ml:258-261 on encoded observations (ssz_tools.ml:42-58 of_float)
+__global__ void k_ts_policy(int32_t policy, int32_t k, int unit, const double* obs, int64_t n,
+                            int32_t* actions) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const double* x = obs + 10 * i;
+  const double pi = 3.141592653589793;
+  int32_t v[10];
+  for (int j = 0; j < 10; ++j) {
+    if (j == 9) {
+      v[j] = unit ? (int32_t)floor(x[j] * 2.0) : (int32_t)x[j];
+    } else if (!unit) {
+      v[j] = (int32_t)x[j];
+    } else {
+      const double scale = j >= 3 ? (double)k : 1.0;
+      v[j] = j == 2 ? (int32_t)__builtin_round(tan(pi * (x[j] - 0.5)) * scale)
+                    : (int32_t)__builtin_round(tan(pi / 2.0 * x[j]) * scale);
+    }
+  }
+  const ts::TsObs o{v[0], v[1], v[2], v[3], v[4], v[5], v[6], v[7], v[8], v[9]};
+  actions[i] = ts::ts_policy(policy, k, o);
+}
+
+// ---------------------------------------------------------------- launchers
+
+static unsigned ts_grid(int64_t n) { return (unsigned)((n + kBlock - 1) / kBlock); }
+
+hipError_t launch_ts_run_episodes(const ts::TsParams& P, uint64_t seed, uint64_t first,
+                                  int64_t n_eps, uint8_t* mem, int64_t lane_bytes, int64_t lanes,
+                                  cpr_episode_record* recs, cpr_summary* sum, hipStream_t st) {
+  hipLaunchKernelGGL(k_ts_run_episodes, dim3((unsigned)(lanes / kBlock)), dim3(kBlock), 0, st, P,
+                     seed, first, n_eps, mem, lane_bytes, recs, sum);
+  return hipGetLastError();
+}
+
+hipError_t launch_ts_reset(const ts::TsParams& P, uint64_t seed, uint8_t* mem, int64_t lane_bytes,
+                           void* slots, int64_t n, const uint8_t* mask, const uint64_t* eps,
+                           int unit, const double* tabs, int32_t tn, double* obs,
+                           hipStream_t st) {
+  hipLaunchKernelGGL(k_ts_reset, dim3(ts_grid(n)), dim3(kBlock), 0, st, P, seed, mem, lane_bytes,
+                     (TsSlot*)slots, n, mask, eps, unit, tabs, tn, obs);
+  return hipGetLastError();
+}
+
+hipError_t launch_ts_step(const ts::TsParams& P, uint64_t seed, uint8_t* mem, int64_t lane_bytes,
+                          void* slots, int64_t n, const int32_t* actions, int unit,
+                          const double* tabs, int32_t tn, const StepBuffers& b, hipStream_t st) {
+  hipLaunchKernelGGL(k_ts_step, dim3(ts_grid(n)), dim3(kBlock), 0, st, P, seed, mem, lane_bytes,
+                     (TsSlot*)slots, n, actions, unit, tabs, tn, b);
+  return hipGetLastError();
+}
+
+hipError_t launch_ts_rollout(const ts::TsParams& P, uint64_t seed, uint8_t* mem,
+                             int64_t lane_bytes, void* slots, int64_t n, int64_t n_steps,
+                             int unit, const double* tabs, int32_t tn, double* obs,
+                             double* reward, uint8_t* done, cpr_summary* sum, hipStream_t st) {
+  hipLaunchKernelGGL(k_ts_rollout, dim3(ts_grid(n)), dim3(kBlock), 0, st, P, seed, mem,
+                     lane_bytes, (TsSlot*)slots, n, n_steps, unit, tabs, tn, obs, reward, done,
+                     sum);
+  return hipGetLastError();
+}
+
+hipError_t launch_ts_observe_fields(const ts::TsParams& P, uint8_t* mem, int64_t lane_bytes,
+                                    const void* slots, int64_t n, int32_t* f, hipStream_t st) {
+  hipLaunchKernelGGL(k_ts_observe_fields, dim3(ts_grid(n)), dim3(kBlock), 0, st, P, mem,
+                     lane_bytes, (const TsSlot*)slots, n, f);
+  return hipGetLastError();
+}
+
+hipError_t launch_ts_policy(int32_t policy, int32_t k, int unit, const double* obs, int64_t n,
+                            int32_t* actions, hipStream_t st) {
+  hipLaunchKernelGGL(k_ts_policy, dim3(ts_grid(n)), dim3(kBlock), 0, st, policy, k, unit, obs, n,
+                     actions);
+  return hipGetLastError();
+}
+
+size_t ts_slot_bytes() { return sizeof(TsSlot); }
+
+int ts_blocks_per_cu() {
+  int blocks = 0;
+  hipError_t e =
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, k_ts_run_episodes, kBlock, 0);
+  if (e != hipSuccess || blocks <= 0) blocks = 2;
+  return blocks;
+}
+
+}  // namespace cpr

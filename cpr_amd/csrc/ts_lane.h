@@ -580,11 +580,11 @@ struct TsLane {
     }
     // a = BlockSet order; pos[cand index] = position in a (M.aux)
     for (int32_t pi = 0; pi < n; ++pi) M.aux[M.perm[pi]] = pi;
-    int32_t c[64];
+    int32_t* c = M.stack;        // current choice (k <= 64); stack is free here
+    int32_t* lv = M.stack + 64;  // leaves of the choice
     for (int32_t t = 0; t < P.k; ++t) c[t] = t;
     double best = -1.0;
     int32_t nbest = 0;
-    int32_t lv[64];
     for (;;) {
       // leaves c (tailstorm.ml:442-481): reach (flag) and leave (flag2) over positions
       for (int32_t i = 0; i < n; ++i) {
@@ -1217,8 +1217,8 @@ struct TsLane {
   // Referee.winner (tailstorm.ml:191-194): Compare.first (neg compare_summaries) 1 over
   // [attacker preference; defenders' tips], i.e. the first element after Array.sort
   __host__ __device__ inline int32_t head(const TsParams& P, const TsMem& M, int32_t att) {
-    int32_t v[65];
-    uint64_t k[65];
+    int32_t* v = M.stack;  // n <= 65
+    uint64_t* k = M.key;
     for (int32_t j = 0; j < P.n; ++j) {
       const int32_t s = j == 0 ? att : M.tips[j];
       const TVtx& x = X(P, M, s);

@@ -83,6 +83,7 @@ def make_config(
     reward_scheme=L.REWARD_CONSTANT,
     k=8,
     table_dim=None,
+    subblock_selection=1,
 ):
     """Build a cpr_config. ``defenders=None`` applies the gym's rule
     d = max(2, ceil(1 / (1 - gamma))) (gym/ocaml/cpr_gym/envs.py:146-153).
@@ -111,6 +112,7 @@ def make_config(
     c.seed = int(seed) & ((1 << 64) - 1)
     c.n_lanes = int(n_lanes)
     c.k = int(k)
+    c.subblock_selection = int(subblock_selection)
     keep = None
     if table is not None and protocol == L.PROTO_BK:
         keep = np.ascontiguousarray(table, dtype=np.uint8).ravel()

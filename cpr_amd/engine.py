@@ -38,6 +38,13 @@ _SPACES = {
                              "private_votes_inclusive", "private_votes_exclusive", "lead",
                              "event"],
                      bools=("lead",)),  # bk_ssz.ml:22-34,123-143
+    L.PROTO_TAILSTORM: dict(actions=_ACTION8, events=["`Append", "`ProofOfWork", "`Network"],
+                            fields=["public_blocks", "private_blocks", "diff_blocks",
+                                    "public_votes", "private_votes_inclusive",
+                                    "private_votes_exclusive", "public_depth",
+                                    "private_depth_inclusive", "private_depth_exclusive",
+                                    "event"],
+                            bools=()),  # tailstorm_ssz.ml:22-38,136-157
 }
 
 
@@ -105,6 +112,7 @@ def create(
     cfg, keep = device.make_config(
         protocol=proto.protocol_id,
         k=proto.params.get("k", 8),
+        subblock_selection=proto.params.get("selection_id", 1),
         reward_scheme=proto.params.get("reward_scheme", L.REWARD_CONSTANT),
         alpha=p["alpha"],
         gamma=p["gamma"],
@@ -168,7 +176,15 @@ def step(ienv, action):
         "episode_n_steps": int(inf["episode_n_steps"][0]),
         "episode_n_activations": int(inf["episode_n_activations"][0]),
     }
-    if ienv.proto.protocol_id == L.PROTO_BK:
+    if ienv.proto.protocol_id == L.PROTO_TAILSTORM:
+        # tailstorm.ml:45-52 (Protocol.info), :89-94 (Referee.info of a summary)
+        info["protocol_family"] = "tailstorm"
+        info["protocol_k"] = ienv.proto.params["k"]
+        info["protocol_incentive_scheme"] = ienv.proto.params["reward"]
+        info["protocol_subblock_selection"] = ienv.proto.params["subblock_selection"]
+        info["head_kind"] = "summary"
+        info["head_height"] = int(inf["head_height"][0])
+    elif ienv.proto.protocol_id == L.PROTO_BK:
         # bk.ml:21-24 (Protocol.info), :53-58 (Referee.info of a block)
         info["protocol_family"] = "bk"
         info["protocol_k"] = ienv.proto.params["k"]

@@ -1,7 +1,7 @@
 """Drop-in for the reference's Python module ``protocols``
 (simulator/gym/cpr_gym_engine.ml:165-304): constructors returning protocol specs that
-``engine.create`` accepts. Nakamoto and B_k run as lockstep lanes on the device engine;
-the other constructors exist with the reference's signatures and raise.
+``engine.create`` accepts. Nakamoto, B_k and Tailstorm run as lockstep lanes on the device
+engine; the other constructors exist with the reference's signatures and raise.
 """
 
 from . import _lib as L
@@ -66,5 +66,24 @@ def bk(reward, k, unit_observation):
 spar = _not_on_device("spar")
 stree = _not_on_device("stree")
 sdag = _not_on_device("sdag")
-tailstorm = _not_on_device("tailstorm")  # (reward, k, subblock_selection, unit_observation)
+
+
+def tailstorm(reward, k, subblock_selection, unit_observation):
+    """tailstorm_ssz attack space (cpr_gym_engine.ml:245-265, cpr_protocols.ml:153-175)."""
+    reward = _option(["constant", "discount", "punish", "hybrid"], reward)  # tailstorm.ml:3
+    subblock_selection = _option(["altruistic", "heuristic", "optimal"], subblock_selection)
+    k = int(k)
+    if k < 1:
+        raise ValueError("k must be positive")
+    info = "SSZ'16-like attack space with %s observations" % ("unit" if unit_observation else "raw")
+    desc = (f"Tailstorm with k={k}, {reward} rewards, and {subblock_selection} "
+            "sub-block selection")  # tailstorm.ml:35-43
+    scheme = {"constant": L.REWARD_CONSTANT, "discount": L.REWARD_DISCOUNT,
+              "punish": L.REWARD_PUNISH, "hybrid": L.REWARD_HYBRID}[reward]
+    sel = {"altruistic": L.SELECT_ALTRUISTIC, "heuristic": L.SELECT_HEURISTIC,
+           "optimal": L.SELECT_OPTIMAL}[subblock_selection]
+    return Protocol(f"tailstorm-{k}-{reward}-{subblock_selection}", desc, info, unit_observation,
+                    protocol_id=L.PROTO_TAILSTORM, k=k, reward=reward, reward_scheme=scheme,
+                    subblock_selection=subblock_selection, selection_id=sel)
+
 tailstormjune = _not_on_device("tailstormjune")

@@ -1,0 +1,153 @@
+"""Tailstorm on the device (through the C ABI) against the CPU oracle — needs an MI355X.
+
+Every record field is bit-identical: per-node rewards are accumulated in the reference's
+fp64 order (set_rewards adds r per confirmed vote; the head's defender reward is the left
+fold over nodes), heights are integers and event times follow the same IEEE operation
+sequence on both sides. Episodes flagged CPR_ST_CAPACITY or CPR_ST_REFERENCE_RAISES are
+compared only for the flag (the oracle raises at the same point for the latter).
+"""
+
+import numpy as np
+import pytest
+
+import oracle_py as O
+from cpr_amd import _lib as L
+from cpr_amd import device
+
+pytestmark = pytest.mark.gpu
+
+FIELDS = [f for f in L.RECORD_DTYPE.names if f not in ("status",)]
+BAD = 32 | 64
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    return device.default_context()
+
+
+def _cfg(**kw):
+    kw.setdefault("protocol", L.PROTO_TAILSTORM)
+    kw.setdefault("k", 8)
+    kw.setdefault("reward_scheme", L.REWARD_DISCOUNT)
+    kw.setdefault("subblock_selection", L.SELECT_HEURISTIC)
+    return device.make_config(**kw)
+
+
+def _compare(cfg, keep, n, first=0):
+    b = device.Batch(cfg, keep=keep)
+    s, rec = b.run(n, first_episode=first, records=True)
+    ok = (rec["status"] & BAD) == 0
+    ref = O.run_episodes(cfg, first, n, threads=8)
+    for f in FIELDS:
+        bad = np.nonzero((rec[f] != ref[f]) & ok)[0]
+        assert len(bad) == 0, (f, int(bad[0]), rec[f][bad[0]], ref[f][bad[0]])
+    return s, rec, ok
+
+
+GYM = [
+    # alpha, gamma, policy, scheme, selection, k, steps, episodes
+    (0.33, 0.5, L.TS_POLICY_HONEST, L.REWARD_DISCOUNT, L.SELECT_HEURISTIC, 8, 2048, 128),
+    (0.33, 0.5, L.TS_POLICY_AVOID_LOSS, L.REWARD_DISCOUNT, L.SELECT_HEURISTIC, 8, 2048, 128),
+    (0.25, 0.0, L.TS_POLICY_GET_AHEAD, L.REWARD_CONSTANT, L.SELECT_ALTRUISTIC, 8, 600, 256),
+    (0.40, 0.9, L.TS_POLICY_LONG_DELAY, L.REWARD_HYBRID, L.SELECT_HEURISTIC, 8, 600, 256),
+    (0.33, 0.8, L.TS_POLICY_MINOR_DELAY, L.REWARD_PUNISH, L.SELECT_HEURISTIC, 13, 600, 64),
+    (0.30, 0.5, L.TS_POLICY_AVOID_LOSS_A, L.REWARD_CONSTANT, L.SELECT_OPTIMAL, 8, 400, 128),
+    (0.20, 0.5, L.TS_POLICY_AVOID_LOSS_B, L.REWARD_DISCOUNT, L.SELECT_HEURISTIC, 3, 600, 256),
+]
+
+
+@pytest.mark.parametrize("alpha,gamma,policy,scheme,sel,k,steps,n", GYM)
+def test_ts_gym_records_match_oracle(ctx, alpha, gamma, policy, scheme, sel, k, steps, n):
+    cfg, keep = _cfg(alpha=alpha, gamma=gamma, policy=policy, reward_scheme=scheme,
+                     subblock_selection=sel, k=k, max_steps=steps, seed=0x7A110000)
+    s, rec, ok = _compare(cfg, keep, n)
+    assert ok.mean() > 0.9
+    assert s.episodes == n and (rec["n_steps"][ok] == steps).all()
+
+
+@pytest.mark.parametrize("policy", [0, 1, 3, 6])
+def test_ts_two_agents_loop_matches_oracle(ctx, policy):
+    # BASELINE configs[3]: two agents, k = 8, discount, heuristic
+    cfg, keep = _cfg(alpha=0.33, network=L.NET_TWO_AGENTS, mode=L.MODE_LOOP, activations=10000,
+                     policy=policy, seed=11)
+    _, _, ok = _compare(cfg, keep, 64)
+    assert ok.all()
+
+
+def test_ts_lockstep_matches_oracle_step_by_step(ctx):
+    n, steps = 12, 200
+    cfg, keep = _cfg(alpha=0.33, gamma=0.5, max_steps=steps, seed=99, n_lanes=n)
+    b = device.Batch(cfg, keep=keep)
+    obs = b.reset()
+    envs = [O.TsGymEnv(cfg, episode=i) for i in range(n)]
+    assert np.array_equal(obs, np.array([e.reset() for e in envs]))
+    rnd = np.random.default_rng(0)
+    for t in range(steps):
+        acts = rnd.integers(0, 8, size=n).astype(np.int32)
+        acts[::2] = [O.ts_policy("avoid-loss", e.fields(), 8) for e in envs[::2]]
+        obs, rew, done, info = b.step(acts)
+        for i, e in enumerate(envs):
+            o, r, d, inf = e.step(int(acts[i]))
+            assert np.array_equal(obs[i], o), (t, i)
+            assert rew[i] == r and done[i] == d, (t, i)
+            for key in ["episode_reward_attacker", "episode_reward_defender",
+                        "episode_progress", "episode_chain_time", "episode_sim_time",
+                        "episode_n_steps", "episode_n_activations", "head_height"]:
+                assert info[key][i] == inf[key], (t, i, key)
+    assert done.all()
+
+
+def test_ts_policy_decoding(ctx):
+    n = 6
+    cfg, keep = _cfg(alpha=0.4, gamma=0.5, max_steps=200, seed=5, n_lanes=n)
+    b = device.Batch(cfg, keep=keep)
+    obs = b.reset()
+    envs = [O.TsGymEnv(cfg, episode=i) for i in range(n)]
+    for e in envs:
+        e.reset()
+    for t in range(80):
+        assert np.array_equal(b.observe_fields(), np.array([e.fields() for e in envs]))
+        for name, pid in device.policy_registry(L.PROTO_TAILSTORM):
+            assert b.policy_actions(pid, obs).tolist() == [
+                O.ts_policy(name, e.fields(), 8) for e in envs], name
+        acts = np.array([O.ts_policy("minor-delay", e.fields(), 8) for e in envs], np.int32)
+        obs, _, _, _ = b.step(acts, with_info=False)
+        for i, e in enumerate(envs):
+            e.step(int(acts[i]))
+
+
+def test_ts_rollout_matches_sequential_oracle_episodes(ctx):
+    n, T, ms = 16, 200, 60
+    cfg, keep = _cfg(alpha=0.33, gamma=0.5, policy=L.TS_POLICY_GET_AHEAD, max_steps=ms, seed=7,
+                     n_lanes=n)
+    b = device.Batch(cfg, keep=keep)
+    s, obs, rew, done = b.rollout(T, outputs=True)
+    assert s.steps == n * T
+    finished = 0
+    for i in range(n):
+        ep = i
+        e = O.TsGymEnv(cfg, episode=ep)
+        e.reset()
+        for t in range(T):
+            o, r, d, _ = e.step(O.ts_policy("get-ahead", e.fields(), 8))
+            assert rew[t, i] == r and done[t, i] == d, (i, t)
+            if d:
+                finished += 1
+                ep += n
+                e = O.TsGymEnv(cfg, episode=ep)
+                o = e.reset()
+            assert np.array_equal(obs[t, i], o), (i, t)
+    assert s.episodes == finished
+
+
+def test_ts_spec_registry_and_validation(ctx):
+    assert [x for x, _ in device.policy_registry(L.PROTO_TAILSTORM)] == [
+        "long-delay", "avoid-loss-b", "avoid-loss-a", "avoid-loss", "minor-delay", "get-ahead",
+        "honest"]
+    cfg, keep = _cfg(alpha=0.3, gamma=0.5, max_steps=10)
+    assert device.Batch(cfg, keep=keep).observation_spec()[:2] == (10, 8)
+    for bad in [dict(k=0), dict(reward_scheme=L.REWARD_BLOCK), dict(subblock_selection=5)]:
+        cfg, keep = _cfg(alpha=0.3, gamma=0.5, max_steps=10, **bad)
+        with pytest.raises(L.CprError) as e:
+            device.Batch(cfg, keep=keep)
+        assert e.value.code == L.CPR_E_INVALID_ARG

@@ -57,3 +57,21 @@ def test_bk_lane_matches_oracle_fuzz():
         assert p.returncode == 0, p.stderr[-2000:]
         assert out["mismatches"] == 0, p.stderr[-2000:]
         assert out["episodes"] > 700 and out["capacity"] == 0
+
+
+def test_tailstorm_lane_matches_oracle_fuzz():
+    # tests/native/ts_vs_oracle.cpp: cpr_amd/csrc/ts_lane.h (host build) vs the oracle's
+    # tailstorm.cpp, every step: 10 observation fields, the policy action, per-node fp64
+    # rewards, height, chain time, clock, activations and vertex count; 7 policies + 2
+    # random-action fuzzers x 4 reward schemes x alpha x gamma, plus Simulator.loop tasks;
+    # heuristic, altruistic and optimal sub-block selection. Episodes where the reference
+    # raises, or its optimal quorum would brute-force beyond the budget, must be flagged at
+    # the same step by both engines.
+    subprocess.run(["make", "-s", "-C", str(ROOT / "tests" / "native")], check=True)
+    exe = ROOT / "tests" / "native" / "build" / "ts_vs_oracle"
+    for args in [("3", "400", "8", "1"), ("2", "300", "8", "0"), ("2", "300", "3", "2")]:
+        p = subprocess.run([str(exe), *args], capture_output=True, text=True, timeout=600)
+        out = json.loads(p.stdout.strip().splitlines()[-1])
+        assert p.returncode == 0, p.stderr[-2000:]
+        assert out["mismatches"] == 0, p.stderr[-2000:]
+        assert out["episodes"] > 250 and out["capacity"] == 0

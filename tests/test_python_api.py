@@ -124,8 +124,7 @@ def test_registered_env_normalized_reward():
 
 def test_unsupported_protocol_is_loud():
     with pytest.raises(NotImplementedError):
-        protocols.tailstorm(k=8, reward="discount", subblock_selection="heuristic",
-                            unit_observation=True)
+        protocols.spar(k=8, reward="constant", unit_observation=True)
 
 
 def test_bk_protocol(capsys):
@@ -172,3 +171,38 @@ def test_bk_policies_and_errors():
                     episode_len=256)
     _, r, done, info = run_episode(env, "avoid-loss")
     assert done and info["episode_n_steps"] == 256 and r >= 0
+
+
+def test_tailstorm_protocol(capsys):
+    # gym/ocaml/test/test_protocols.py:230-261
+    env = envs.make("cpr_gym:core-v0",
+                    proto=protocols.tailstorm(k=13, reward="discount",
+                                              subblock_selection="heuristic",
+                                              unit_observation=True),
+                    alpha=0.33, gamma=0.8, defenders=5, max_steps=10000)
+    env.render()
+    assert capsys.readouterr().out.splitlines()[0] == (
+        "Tailstorm with k=13, discount rewards, and heuristic sub-block selection; "
+        "SSZ'16-like attack space with unit observations; α=0.33 attacker")
+    obs = env.reset()
+    for _ in range(600):
+        obs, _, _, _ = env.step(env.policy(obs, "honest"))
+    obs = env.reset()
+    for _ in range(600):
+        obs, _, _, info = env.step(env.policy(obs, "avoid-loss"))
+    assert info["protocol_k"] == 13 and info["head_kind"] == "summary"
+    assert env.observation_space.contains(obs)
+    assert list(env.policies()) == ["long-delay", "avoid-loss-b", "avoid-loss-a", "avoid-loss",
+                                    "minor-delay", "get-ahead", "honest"]
+
+
+def test_cpr_tailstorm_v0(capsys):
+    # gym/ocaml/test/test_envs.py:154-170
+    env = envs.make("cpr_gym:cpr-tailstorm-v0")
+    env.render()
+    assert capsys.readouterr().out.splitlines()[0] == (
+        "Tailstorm with k=8, discount rewards, and heuristic sub-block selection; "
+        "SSZ'16-like attack space with unit observations; α=0.45 attacker")
+    _, r, done, info = run_episode(env, "honest")
+    assert done and r >= 0
+    fuzz_episode(env)
