@@ -295,6 +295,11 @@ static int validate_eth(const cpr_config* c, eth::EthParams* P) {
   return CPR_OK;
 }
 
+// vertex-ring window of the B_k / Tailstorm lanes (see validate_bk)
+static constexpr int32_t kRingWindow = 4096;
+// HBM budget for the per-lane regions of the event-engine lanes (288 GB per MI355X)
+static constexpr int64_t kLaneBudget = 96ll << 30;
+
 // B_k: engine.ml:37-51 checks shared with Nakamoto, network.ml:343-358, bk.ml k >= 1,
 // Constant / Block rewards, bk_ssz policies 0..3 or a table
 static int validate_bk(const cpr_config* c, bk::BkParams* P) {
@@ -367,14 +372,15 @@ static int validate_bk(const cpr_config* c, bk::BkParams* P) {
     P->max_time = __builtin_inf();
     span = c->activations * 2 + 2;  // votes + blocks
   }
-  // vertex ring: a whole gym episode up to 2^16 vertices (longer runs flag
-  // CPR_ST_CAPACITY only if a fork outlives the ring)
+  // vertex ring: a window of at most 4096 vertices (a whole 2048-step gym episode); longer
+  // runs flag CPR_ST_CAPACITY only if something older than the window is read (a fork
+  // that outlives it). Small per-lane regions let the grid reach resident capacity.
   int32_t cv = 64;
-  while (cv < span + 64 && cv < (1 << 16)) cv <<= 1;
+  while (cv < span + 64 && cv < kRingWindow) cv <<= 1;
   P->cap_v = cv;
   P->cap_q = cv / 2;
   P->cap_d = 64;
-  P->cap_e = 256 + 1024 * P->n +
+  P->cap_e = 256 + 512 * P->n +
              (std::isfinite(P->dmax) || P->net == 1
                   ? 0
                   : (int32_t)(2 * P->d * std::min<int64_t>(span, 8192)));
@@ -426,11 +432,11 @@ static int validate_ts(const cpr_config* c, ts::TsParams* P) {
                            ? (B.max_steps < (1 << 20) ? B.max_steps + 2 : 8192)
                            : c->activations * 2 + 2;
   int32_t cv = 64;
-  while (cv < span + 64 && cv < (1 << 16)) cv <<= 1;
+  while (cv < span + 64 && cv < kRingWindow) cv <<= 1;
   P->cap_v = cv;
   P->cap_q = cv / 2;
   P->cap_d = 64;
-  P->cap_e = 256 + 1024 * P->n +
+  P->cap_e = 256 + 512 * P->n +
              (std::isfinite(P->dmax) || P->net == 1
                   ? 0
                   : (int32_t)(2 * P->d * std::min<int64_t>(span, 8192)));
@@ -560,7 +566,7 @@ static int run_async_bk(cpr_batch* b, int64_t n, uint64_t first, cpr_summary* su
                         cpr_episode_record* rec_dev) {
   const bool tsp = b->cfg.protocol == CPR_PROTO_TAILSTORM;
   const int64_t full = (int64_t)b->ctx->cus * (tsp ? ts_blocks_per_cu() : bk_blocks_per_cu()) * 256;
-  const int64_t budget = (int64_t)(32ll << 30) / b->bk_bytes;
+  const int64_t budget = kLaneBudget / b->bk_bytes;
   int64_t lanes = std::min(full, std::max<int64_t>(256, budget));
   lanes = std::min(lanes, ((n + 255) / 256) * 256);
   lanes = std::max<int64_t>(256, (lanes / 256) * 256);

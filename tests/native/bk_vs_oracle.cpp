@@ -4,6 +4,7 @@
 // observation fields and the step info after every step; loop-mode tasks on the
 // two-agents network compared at the end. Prints one JSON summary line; exit code 1 on
 // any mismatch. Usage: bk_vs_oracle [episodes per config] [steps] [k]
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -51,10 +52,12 @@ static bk::BkParams params_of(const Cfg& cf) {
   P.policy = cf.policy < 5 ? cf.policy : 0;
   P.scheme = cf.scheme;
   P.k = cf.k;
+  // same sizing rules as capi.hip validate_bk (4096-vertex window)
+  const int span = cf.two_agents ? 2 * cf.steps + 2 : cf.steps + 2;
   P.cap_v = 64;
-  while (P.cap_v < cf.steps + 64) P.cap_v <<= 1;
+  while (P.cap_v < span + 64 && P.cap_v < 4096) P.cap_v <<= 1;
   P.cap_q = P.cap_v / 2;
-  P.cap_e = 256 + 1024 * P.n + (cf.gamma == 0.0 ? 2 * P.d * cf.steps : 0);
+  P.cap_e = 256 + 512 * P.n + (cf.gamma == 0.0 && !cf.two_agents ? 2 * P.d * std::min(span, 8192) : 0);
   P.cap_d = 64;
   P.table_dim = g_dim;
   P.table = g_table.data();

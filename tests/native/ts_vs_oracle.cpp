@@ -6,6 +6,7 @@
 // (oracle exception) must be flagged CPR_ST_REFERENCE_RAISES by the lane at the same step.
 // Prints one JSON summary line; exit code 1 on any mismatch.
 // Usage: ts_vs_oracle [episodes per config] [steps] [k] [selection]
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -53,10 +54,12 @@ static ts::TsParams params_of(const Cfg& cf) {
   P.scheme = cf.scheme;
   P.selection = g_sel;
   P.k = cf.k;
+  // same sizing rules as capi.hip validate_ts (4096-vertex window)
+  const int span = cf.two_agents ? 2 * cf.steps + 2 : cf.steps + 2;
   P.cap_v = 64;
-  while (P.cap_v < 2 * cf.steps + 64) P.cap_v <<= 1;
+  while (P.cap_v < span + 64 && P.cap_v < 4096) P.cap_v <<= 1;
   P.cap_q = P.cap_v / 2;
-  P.cap_e = 256 + 1024 * P.n + (cf.gamma == 0.0 ? 2 * P.d * 2 * cf.steps : 0);
+  P.cap_e = 256 + 512 * P.n + (cf.gamma == 0.0 && !cf.two_agents ? 2 * P.d * std::min(span, 8192) : 0);
   P.cap_d = 64;
   P.ev = 1.0;
   P.delta = 1e-9;

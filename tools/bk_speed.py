@@ -9,7 +9,7 @@ import numpy as np
 from cpr_amd import _lib as L, device
 
 K = 8
-for pol, n in [(L.BK_POLICY_MINOR_DELAY, 65536), (L.BK_POLICY_HONEST, 65536)]:
+for pol, n in [(L.BK_POLICY_MINOR_DELAY, 262144), (L.BK_POLICY_HONEST, 262144)]:
     cfg, keep = device.make_config(alpha=0.33, gamma=0.5, policy=pol, k=K, max_steps=2048,
                                    seed=1, protocol=L.PROTO_BK)
     b = device.Batch(cfg, keep=keep)
@@ -36,9 +36,9 @@ for lanes, T in [(65536, 64), (65536, 256)]:
 
 # Tailstorm: BASELINE configs[3] (two agents, k=8, discount, heuristic, 10^4-activation
 # Simulator.loop tasks) and 2048-step gym episodes
-for pol, n in [(L.TS_POLICY_GET_AHEAD, 16384), (L.TS_POLICY_AVOID_LOSS, 16384)]:
+for pol, n in [(L.TS_POLICY_GET_AHEAD, 131072), (L.TS_POLICY_AVOID_LOSS, 131072)]:
     cfg, keep = device.make_config(alpha=0.33, network=L.NET_TWO_AGENTS, mode=L.MODE_LOOP,
-                                   activations=10000, policy=pol, k=8,
+                                   activations=2000, policy=pol, k=8,
                                    reward_scheme=L.REWARD_DISCOUNT,
                                    subblock_selection=L.SELECT_HEURISTIC, seed=3,
                                    protocol=L.PROTO_TAILSTORM)
@@ -54,7 +54,7 @@ cfg, keep = device.make_config(alpha=0.33, gamma=0.5, policy=L.TS_POLICY_AVOID_L
                                protocol=L.PROTO_TAILSTORM)
 b = device.Batch(cfg, keep=keep)
 b.run(1024)
-t = time.time(); s = b.run(65536); dt = time.time() - t
+t = time.time(); s = b.run(131072); dt = time.time() - t
 ms, acts = b.last_launch()
 print(f"tailstorm gym avoid-loss: {s.steps/dt:.3e} steps/s {s.activations/dt:.3e} act/s wall, "
       f"kernel {ms:.1f} ms; eps {s.episodes} other {s.status_other}", flush=True)
