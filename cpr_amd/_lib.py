@@ -65,6 +65,10 @@ ST_TIE = 1
 ST_OVERLAP = 2
 ST_DEEP_FORK = 4
 ST_TIE_UNRESOLVED = 8
+ST_STALE_TIME = 16
+ST_CAPACITY = 32
+ST_REFERENCE_RAISES = 64
+ST_TRACE_MISS = 128
 
 HIST_BINS = 64
 
@@ -190,6 +194,61 @@ class StepInfo(ctypes.Structure):
     ]
 
 
+class CTrace(ctypes.Structure):
+    _fields_ = [
+        ("n_episodes", ctypes.c_int64),
+        ("act_offset", ctypes.c_void_p),
+        ("act_miner", ctypes.c_void_p),
+        ("act_delay", ctypes.c_void_p),
+        ("pow_offset", ctypes.c_void_p),
+        ("pow_hash", ctypes.c_void_p),
+        ("link_offset", ctypes.c_void_p),
+        ("link_key", ctypes.c_void_p),
+        ("link_delay", ctypes.c_void_p),
+    ]
+
+
+class Trace:
+    """An exported activation/delay trace (cpr_trace, include/cpr_hip.h): CSR numpy arrays
+    over episodes. ``ctrace()`` gives the C struct (the arrays must outlive it)."""
+
+    ARRAYS = [
+        ("act_offset", np.int64), ("act_miner", np.int32), ("act_delay", np.float64),
+        ("pow_offset", np.int64), ("pow_hash", np.int32),
+        ("link_offset", np.int64), ("link_key", np.uint64), ("link_delay", np.float64),
+    ]
+
+    def __init__(self, **arrays):
+        for name, dt in self.ARRAYS:
+            setattr(self, name, np.ascontiguousarray(arrays[name], dtype=dt))
+        self.n_episodes = len(self.act_offset) - 1
+
+    def episode(self, e):
+        """Trace of episode e alone."""
+        a0, a1 = self.act_offset[e], self.act_offset[e + 1]
+        p0, p1 = self.pow_offset[e], self.pow_offset[e + 1]
+        l0, l1 = self.link_offset[e], self.link_offset[e + 1]
+        return Trace(act_offset=[0, a1 - a0], act_miner=self.act_miner[a0:a1],
+                     act_delay=self.act_delay[a0:a1], pow_offset=[0, p1 - p0],
+                     pow_hash=self.pow_hash[p0:p1], link_offset=[0, l1 - l0],
+                     link_key=self.link_key[l0:l1], link_delay=self.link_delay[l0:l1])
+
+    def save(self, path):
+        np.savez_compressed(path, **{n: getattr(self, n) for n, _ in self.ARRAYS})
+
+    @classmethod
+    def load(cls, path):
+        with np.load(path, allow_pickle=False) as z:
+            return cls(**{n: z[n] for n, _ in cls.ARRAYS})
+
+    def ctrace(self):
+        t = CTrace()
+        t.n_episodes = self.n_episodes
+        for name, _ in self.ARRAYS:
+            setattr(t, name, self.__dict__[name].ctypes.data)
+        return t
+
+
 # every symbol include/cpr_hip.h declares
 EXPORTS = [
     "cpr_version",
@@ -203,6 +262,7 @@ EXPORTS = [
     "cpr_run_episodes",
     "cpr_run_episodes_async",
     "cpr_synchronize",
+    "cpr_replay",
     "cpr_last_launch",
     "cpr_reset",
     "cpr_step",
@@ -239,6 +299,7 @@ def _declare(L):
     L.cpr_run_episodes.argtypes = [vp, ctypes.c_int64, ctypes.c_uint64, P(Summary), vp, ctypes.c_int]
     L.cpr_run_episodes_async.argtypes = [vp, ctypes.c_int64, ctypes.c_uint64, vp, vp]
     L.cpr_synchronize.argtypes = [vp]
+    L.cpr_replay.argtypes = [vp, P(CTrace), P(Summary), vp, ctypes.c_int]
     L.cpr_last_launch.argtypes = [vp, P(ctypes.c_double), P(ctypes.c_int64)]
     L.cpr_reset.argtypes = [vp, vp, vp, vp]
     L.cpr_step.argtypes = [vp, vp, vp, vp, vp, P(StepInfo)]

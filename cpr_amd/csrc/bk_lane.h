@@ -389,15 +389,14 @@ struct BkLane {
   }
 
   // ------------------------------------------------------------------ randomness
-  __host__ __device__ inline int32_t miner_of(const BkParams& P, const Stream& S, int32_t j) {
-    const Words4 w = S.block((uint32_t)j, TAG_ACT);
-    if ((uint64_t)w.w0 < P.t_att) return 0;
-    return 1 + (int32_t)(((uint64_t)w.w1 * (uint64_t)P.d) >> 32);
+  template <class St>
+  __host__ __device__ inline int32_t miner_of(const BkParams& P, const St& S, int32_t j) {
+    return S.miner((uint32_t)j, P.t_att, P.d);
   }
-  __host__ __device__ inline void schedule_pow(const BkParams& P, const Stream& S,
+  template <class St>
+  __host__ __device__ inline void schedule_pow(const BkParams& P, const St& S,
                                                const BkMem& M) {
-    const Words4 w = S.block((uint32_t)c_act, TAG_ACT);
-    push(P, M, now + (-1.0 * P.ev) * cpr_log(u53(w.w2, w.w3)), mkev(EV_CLOCK, 0, KD_POW), -1);
+    push(P, M, now + S.clock((uint32_t)c_act, P.ev), mkev(EV_CLOCK, 0, KD_POW), -1);
   }
 
   // ------------------------------------------------------------------ DAG
@@ -410,7 +409,8 @@ struct BkLane {
     for (int32_t j = 0; j < P.n; ++j) V(P, M, s, j) = V_INV;
   }
   // vote: simulator.ml:122-136 (pow = (bits, serial)), bk.ml:281-286 payload
-  __host__ __device__ inline int32_t append_vote(const BkParams& P, const Stream& S,
+  template <class St>
+  __host__ __device__ inline int32_t append_vote(const BkParams& P, const St& S,
                                                  const BkMem& M, int32_t node, int32_t parent) {
     BVtx& p = X(P, M, parent);
     const int32_t s = ++newest;
@@ -420,7 +420,7 @@ struct BkLane {
     b.height = p.height;
     b.vote = 1;
     b.who = node;
-    b.pow = (int32_t)(S.block((uint32_t)s, TAG_POW).w0 & 0x3FFFFFFFu);
+    b.pow = S.pow((uint32_t)s);
     b.rew_att = p.rew_att;  // precursor = the block; votes carry no reward (bk.ml:151-176)
     b.rew_def = p.rew_def;
     p.nconf += 1;
@@ -758,7 +758,8 @@ struct BkLane {
   }
 
   // ------------------------------------------------------------------ engine
-  __host__ __device__ inline void init(const BkParams& P, const Stream& S, const BkMem& M) {
+  template <class St>
+  __host__ __device__ inline void init(const BkParams& P, const St& S, const BkMem& M) {
     now = 0.0;
     c_act = 0;
     newest = 0;
@@ -803,7 +804,8 @@ struct BkLane {
   }
 
   // one popped event that is not the attacker's gym interaction (simulator.ml:421-508)
-  __host__ __device__ inline void handle(const BkParams& P, const Stream& S, const BkMem& M,
+  template <class St>
+  __host__ __device__ inline void handle(const BkParams& P, const St& S, const BkMem& M,
                                          uint32_t ev, int32_t s) {
     const uint32_t ty = ev & 7u, kind = (ev >> 3) & 3u;
     const int32_t node = (int32_t)(ev >> 5);
@@ -862,7 +864,7 @@ struct BkLane {
           if (P.net == 1)
             delay = 0.0;
           else if (node == 0)
-            delay = S.msg_u((uint32_t)s, (uint32_t)dst) * (P.dmax - 0.0) + 0.0;
+            delay = S.msg((uint32_t)s, (uint32_t)dst, P.dmax);
           else
             delay = dst == 0 ? 0.0 : P.delta;
           push(P, M, now + delay, mkev(EV_RX, dst, KD_NET), s);
@@ -901,7 +903,8 @@ struct BkLane {
   }
 
   // engine.ml:108-121
-  __host__ __device__ inline bool skip_to_interaction(const BkParams& P, const Stream& S,
+  template <class St>
+  __host__ __device__ inline bool skip_to_interaction(const BkParams& P, const St& S,
                                                       const BkMem& M, uint32_t* kind,
                                                       int32_t* blk) {
     double t;
@@ -950,7 +953,8 @@ struct BkLane {
   }
 
   // gym: reset (engine.ml:122-170)
-  __host__ __device__ inline void gym_reset(const BkParams& P, const Stream& S, const BkMem& M) {
+  template <class St>
+  __host__ __device__ inline void gym_reset(const BkParams& P, const St& S, const BkMem& M) {
     init(P, S, M);
     uint32_t kind;
     int32_t b;
@@ -958,7 +962,8 @@ struct BkLane {
   }
 
   // gym: step (engine.ml:176-249); returns the head, sets *done
-  __host__ __device__ inline int32_t gym_step(const BkParams& P, const Stream& S,
+  template <class St>
+  __host__ __device__ inline int32_t gym_step(const BkParams& P, const St& S,
                                               const BkMem& M, int32_t action, bool* done) {
     apply(P, M, action);
     ++steps;
@@ -973,7 +978,8 @@ struct BkLane {
   }
 
   // loop: Simulator.loop ~activations (simulator.ml:519-533), then the head
-  __host__ __device__ inline int32_t loop(const BkParams& P, const Stream& S, const BkMem& M) {
+  template <class St>
+  __host__ __device__ inline int32_t loop(const BkParams& P, const St& S, const BkMem& M) {
     init(P, S, M);
     int64_t left = P.activations;
     double t;

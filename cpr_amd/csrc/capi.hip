@@ -74,6 +74,7 @@ struct cpr_batch {
   std::vector<uint8_t> table_host;
   DevBuf table_dev, tabs_dev;  // policy table; unit-observation tables
   DevBuf spill, tlog, replay, summary, records;
+  DevBuf tr_off, tr_miner, tr_delay, tr_pow, tr_key, tr_ldelay;  // cpr_replay trace copy
   int64_t lanes_alloc = 0;
   // lockstep lanes
   DevBuf lanes, lring, lspill, ltlog, lreplay, l_obs, l_act, l_rew, l_done, l_mask, l_eps, l_info;
@@ -524,7 +525,8 @@ int cpr_batch_destroy(cpr_batch* b) {
   for (DevBuf* d : {&b->table_dev, &b->tabs_dev, &b->spill, &b->tlog, &b->replay, &b->summary,
                     &b->records, &b->lanes, &b->lring, &b->lspill, &b->ltlog, &b->lreplay,
                     &b->l_obs, &b->l_act, &b->l_rew, &b->l_done, &b->l_mask, &b->l_eps,
-                    &b->l_info})
+                    &b->l_info, &b->tr_off, &b->tr_miner, &b->tr_delay, &b->tr_pow,
+                    &b->tr_key, &b->tr_ldelay})
     d->release();
   delete b;
   return CPR_OK;
@@ -542,8 +544,8 @@ static int64_t episode_lanes(cpr_batch* b, int64_t n_eps) {
 }
 
 // Ethereum lanes: resident capacity bounded by a 32 GiB budget for the per-lane regions
-static int run_async_eth(cpr_batch* b, int64_t n, uint64_t first, cpr_summary* sum_dev,
-                         cpr_episode_record* rec_dev) {
+static int run_async_eth(cpr_batch* b, int64_t n, uint64_t first, const TraceSource* tr,
+                         cpr_summary* sum_dev, cpr_episode_record* rec_dev) {
   const int64_t full = (int64_t)b->ctx->cus * eth_blocks_per_cu() * 256;
   const int64_t budget = (int64_t)(32ll << 30) / b->eth_bytes;
   int64_t lanes = std::min(full, std::max<int64_t>(256, budget));
@@ -555,15 +557,19 @@ static int run_async_eth(cpr_batch* b, int64_t n, uint64_t first, cpr_summary* s
     HIP_TRY(hipEventCreate(&b->ev1));
   }
   HIP_TRY(hipEventRecord(b->ev0, b->ctx->stream));
-  HIP_TRY(launch_eth_run_episodes(b->EP, b->cfg.seed, first, n, (uint8_t*)b->eth_mem.p,
-                                  b->eth_bytes, lanes, rec_dev, sum_dev, b->ctx->stream));
+  if (tr)
+    HIP_TRY(launch_eth_replay_episodes(b->EP, *tr, n, (uint8_t*)b->eth_mem.p, b->eth_bytes,
+                                       lanes, rec_dev, sum_dev, b->ctx->stream));
+  else
+    HIP_TRY(launch_eth_run_episodes(b->EP, b->cfg.seed, first, n, (uint8_t*)b->eth_mem.p,
+                                    b->eth_bytes, lanes, rec_dev, sum_dev, b->ctx->stream));
   HIP_TRY(hipEventRecord(b->ev1, b->ctx->stream));
   return CPR_OK;
 }
 
 // B_k lanes: resident capacity bounded by a 32 GiB budget for the per-lane regions
-static int run_async_bk(cpr_batch* b, int64_t n, uint64_t first, cpr_summary* sum_dev,
-                        cpr_episode_record* rec_dev) {
+static int run_async_bk(cpr_batch* b, int64_t n, uint64_t first, const TraceSource* tr,
+                        cpr_summary* sum_dev, cpr_episode_record* rec_dev) {
   const bool tsp = b->cfg.protocol == CPR_PROTO_TAILSTORM;
   const int64_t full = (int64_t)b->ctx->cus * (tsp ? ts_blocks_per_cu() : bk_blocks_per_cu()) * 256;
   const int64_t budget = kLaneBudget / b->bk_bytes;
@@ -576,20 +582,28 @@ static int run_async_bk(cpr_batch* b, int64_t n, uint64_t first, cpr_summary* su
     HIP_TRY(hipEventCreate(&b->ev1));
   }
   HIP_TRY(hipEventRecord(b->ev0, b->ctx->stream));
-  if (tsp)
-    HIP_TRY(launch_ts_run_episodes(b->TP, b->cfg.seed, first, n, (uint8_t*)b->bk_mem.p,
-                                   b->bk_bytes, lanes, rec_dev, sum_dev, b->ctx->stream));
+  uint8_t* mem = (uint8_t*)b->bk_mem.p;
+  hipStream_t st = b->ctx->stream;
+  if (tsp && tr)
+    HIP_TRY(launch_ts_replay_episodes(b->TP, *tr, n, mem, b->bk_bytes, lanes, rec_dev, sum_dev, st));
+  else if (tsp)
+    HIP_TRY(launch_ts_run_episodes(b->TP, b->cfg.seed, first, n, mem, b->bk_bytes, lanes, rec_dev,
+                                   sum_dev, st));
+  else if (tr)
+    HIP_TRY(launch_bk_replay_episodes(b->BP, *tr, n, mem, b->bk_bytes, lanes, rec_dev, sum_dev, st));
   else
-    HIP_TRY(launch_bk_run_episodes(b->BP, b->cfg.seed, first, n, (uint8_t*)b->bk_mem.p,
-                                   b->bk_bytes, lanes, rec_dev, sum_dev, b->ctx->stream));
+    HIP_TRY(launch_bk_run_episodes(b->BP, b->cfg.seed, first, n, mem, b->bk_bytes, lanes, rec_dev,
+                                   sum_dev, st));
   HIP_TRY(hipEventRecord(b->ev1, b->ctx->stream));
   return CPR_OK;
 }
 
-static int run_async(cpr_batch* b, int64_t n, uint64_t first, cpr_summary* sum_dev,
-                     cpr_episode_record* rec_dev) {
-  if (b->cfg.protocol == CPR_PROTO_ETHEREUM) return run_async_eth(b, n, first, sum_dev, rec_dev);
-  if (b->is_ev) return run_async_bk(b, n, first, sum_dev, rec_dev);
+// tr == NULL: episodes [first, first + n) of the keyed stream; else trace episodes [0, n)
+static int run_async(cpr_batch* b, int64_t n, uint64_t first, const TraceSource* tr,
+                     cpr_summary* sum_dev, cpr_episode_record* rec_dev) {
+  if (b->cfg.protocol == CPR_PROTO_ETHEREUM)
+    return run_async_eth(b, n, first, tr, sum_dev, rec_dev);
+  if (b->is_ev) return run_async_bk(b, n, first, tr, sum_dev, rec_dev);
   const int64_t lanes = episode_lanes(b, n);
   if (lanes > b->lanes_alloc) {
     HIP_TRY(b->spill.ensure((size_t)lanes * b->P.cap * sizeof(int32_t)));
@@ -602,9 +616,15 @@ static int run_async(cpr_batch* b, int64_t n, uint64_t first, cpr_summary* sum_d
     HIP_TRY(hipEventCreate(&b->ev1));
   }
   HIP_TRY(hipEventRecord(b->ev0, b->ctx->stream));
-  HIP_TRY(launch_run_episodes(b->P, b->cfg.seed, first, n, b->cfg.mode, b->cfg.activations,
-                              (int32_t*)b->spill.p, (double*)b->tlog.p, (uint8_t*)b->replay.p,
-                              lanes, rec_dev, sum_dev, b->ctx->stream));
+  if (tr)
+    HIP_TRY(launch_replay_episodes(b->P, *tr, n, b->cfg.mode, b->cfg.activations,
+                                   (int32_t*)b->spill.p, (double*)b->tlog.p,
+                                   (uint8_t*)b->replay.p, lanes, rec_dev, sum_dev,
+                                   b->ctx->stream));
+  else
+    HIP_TRY(launch_run_episodes(b->P, b->cfg.seed, first, n, b->cfg.mode, b->cfg.activations,
+                                (int32_t*)b->spill.p, (double*)b->tlog.p, (uint8_t*)b->replay.p,
+                                lanes, rec_dev, sum_dev, b->ctx->stream));
   HIP_TRY(hipEventRecord(b->ev1, b->ctx->stream));
   return CPR_OK;
 }
@@ -614,14 +634,11 @@ int cpr_run_episodes_async(cpr_batch* b, int64_t n, uint64_t first, cpr_summary*
   if (!b || !sum_dev) return fail(CPR_E_INVALID_ARG, "NULL argument");
   if (n <= 0) return CPR_OK;
   HIP_TRY(hipSetDevice(b->ctx->device));
-  return run_async(b, n, first, sum_dev, rec_dev);
+  return run_async(b, n, first, nullptr, sum_dev, rec_dev);
 }
 
-int cpr_run_episodes(cpr_batch* b, int64_t n, uint64_t first, cpr_summary* summary,
-                     cpr_episode_record* records, int records_on_device) {
-  if (!b || !summary) return fail(CPR_E_INVALID_ARG, "NULL argument");
-  if (n <= 0) return CPR_OK;
-  HIP_TRY(hipSetDevice(b->ctx->device));
+static int run_sync(cpr_batch* b, int64_t n, uint64_t first, const TraceSource* tr,
+                    cpr_summary* summary, cpr_episode_record* records, int records_on_device) {
   hipStream_t st = b->ctx->stream;
   HIP_TRY(b->summary.ensure(sizeof(cpr_summary)));
   HIP_TRY(hipMemsetAsync(b->summary.p, 0, sizeof(cpr_summary), st));
@@ -634,7 +651,7 @@ int cpr_run_episodes(cpr_batch* b, int64_t n, uint64_t first, cpr_summary* summa
       rec_dev = (cpr_episode_record*)b->records.p;
     }
   }
-  int rc = run_async(b, n, first, (cpr_summary*)b->summary.p, rec_dev);
+  int rc = run_async(b, n, first, tr, (cpr_summary*)b->summary.p, rec_dev);
   if (rc) return rc;
   cpr_summary s;
   HIP_TRY(hipMemcpyAsync(&s, b->summary.p, sizeof(s), hipMemcpyDeviceToHost, st));
@@ -660,6 +677,99 @@ int cpr_run_episodes(cpr_batch* b, int64_t n, uint64_t first, cpr_summary* summa
   summary->status_other += s.status_other;
   for (int i = 0; i < CPR_HIST_BINS; i++) summary->hist[i] += s.hist[i];
   return CPR_OK;
+}
+
+int cpr_run_episodes(cpr_batch* b, int64_t n, uint64_t first, cpr_summary* summary,
+                     cpr_episode_record* records, int records_on_device) {
+  if (!b || !summary) return fail(CPR_E_INVALID_ARG, "NULL argument");
+  if (n <= 0) return CPR_OK;
+  HIP_TRY(hipSetDevice(b->ctx->device));
+  return run_sync(b, n, first, nullptr, summary, records, records_on_device);
+}
+
+// host-side checks of a trace before any of it reaches a lane: CSR offsets, miners within
+// the network, delays non-negative (not NaN), keys strictly ascending per episode
+static int check_trace(const cpr_batch* b, const cpr_trace* t) {
+  const int64_t E = t->n_episodes;
+  const int32_t nodes = b->cfg.network == CPR_NET_TWO_AGENTS ? 2 : b->cfg.defenders + 1;
+  const int64_t* offs[3] = {t->act_offset, t->pow_offset, t->link_offset};
+  const char* names[3] = {"act_offset", "pow_offset", "link_offset"};
+  for (int a = 0; a < 3; a++) {
+    const int64_t* o = offs[a];
+    const std::string nm = std::string("cpr_trace.") + names[a];
+    if (!o) return fail(CPR_E_INVALID_ARG, nm + " is NULL");
+    if (o[0] != 0) return fail(CPR_E_INVALID_ARG, nm + "[0] != 0");
+    for (int64_t e = 0; e < E; e++)
+      if (o[e + 1] < o[e] || o[e + 1] - o[e] > INT32_MAX)
+        return fail(CPR_E_INVALID_ARG, nm + " not monotone");
+  }
+  const int64_t na = t->act_offset[E], np = t->pow_offset[E], nl = t->link_offset[E];
+  if ((na && (!t->act_miner || !t->act_delay)) || (np && !t->pow_hash) ||
+      (nl && (!t->link_key || !t->link_delay)))
+    return fail(CPR_E_INVALID_ARG, "cpr_trace: NULL array with nonzero length");
+  for (int64_t i = 0; i < na; i++) {
+    if (t->act_miner[i] < 0 || t->act_miner[i] >= nodes)
+      return fail(CPR_E_INVALID_ARG, "cpr_trace.act_miner: node index out of range");
+    if (!(t->act_delay[i] >= 0.0))
+      return fail(CPR_E_INVALID_ARG, "cpr_trace.act_delay: negative or NaN delay");
+  }
+  for (int64_t i = 0; i < nl; i++)
+    if (!(t->link_delay[i] >= 0.0))
+      return fail(CPR_E_INVALID_ARG, "cpr_trace.link_delay: negative or NaN delay");
+  for (int64_t e = 0; e < E; e++)
+    for (int64_t i = t->link_offset[e] + 1; i < t->link_offset[e + 1]; i++)
+      if (t->link_key[i] <= t->link_key[i - 1])
+        return fail(CPR_E_INVALID_ARG, "cpr_trace.link_key: not strictly ascending");
+  return CPR_OK;
+}
+
+int cpr_replay(cpr_batch* b, const cpr_trace* t, cpr_summary* summary,
+               cpr_episode_record* records, int records_on_device) {
+  if (!b || !t || !summary) return fail(CPR_E_INVALID_ARG, "NULL argument");
+  if (t->n_episodes <= 0) return CPR_OK;
+  const int rc = check_trace(b, t);
+  if (rc) return rc;
+  HIP_TRY(hipSetDevice(b->ctx->device));
+  hipStream_t st = b->ctx->stream;
+  const int64_t E = t->n_episodes;
+  const int64_t na = t->act_offset[E], np = t->pow_offset[E], nl = t->link_offset[E];
+  const size_t ob = (size_t)(E + 1) * sizeof(int64_t);
+  // one device buffer holds the three offset arrays; empty arrays get 8 bytes
+  HIP_TRY(b->tr_off.ensure(3 * ob));
+  HIP_TRY(b->tr_miner.ensure(std::max<size_t>(8, (size_t)na * sizeof(int32_t))));
+  HIP_TRY(b->tr_delay.ensure(std::max<size_t>(8, (size_t)na * sizeof(double))));
+  HIP_TRY(b->tr_pow.ensure(std::max<size_t>(8, (size_t)np * sizeof(int32_t))));
+  HIP_TRY(b->tr_key.ensure(std::max<size_t>(8, (size_t)nl * sizeof(uint64_t))));
+  HIP_TRY(b->tr_ldelay.ensure(std::max<size_t>(8, (size_t)nl * sizeof(double))));
+  char* off = (char*)b->tr_off.p;
+  HIP_TRY(hipMemcpyAsync(off, t->act_offset, ob, hipMemcpyHostToDevice, st));
+  HIP_TRY(hipMemcpyAsync(off + ob, t->pow_offset, ob, hipMemcpyHostToDevice, st));
+  HIP_TRY(hipMemcpyAsync(off + 2 * ob, t->link_offset, ob, hipMemcpyHostToDevice, st));
+  if (na) {
+    HIP_TRY(hipMemcpyAsync(b->tr_miner.p, t->act_miner, na * sizeof(int32_t),
+                           hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(b->tr_delay.p, t->act_delay, na * sizeof(double),
+                           hipMemcpyHostToDevice, st));
+  }
+  if (np)
+    HIP_TRY(hipMemcpyAsync(b->tr_pow.p, t->pow_hash, np * sizeof(int32_t), hipMemcpyHostToDevice,
+                           st));
+  if (nl) {
+    HIP_TRY(hipMemcpyAsync(b->tr_key.p, t->link_key, nl * sizeof(uint64_t),
+                           hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(b->tr_ldelay.p, t->link_delay, nl * sizeof(double),
+                           hipMemcpyHostToDevice, st));
+  }
+  TraceSource src;
+  src.act_off = (const int64_t*)off;
+  src.pow_off = (const int64_t*)(off + ob);
+  src.link_off = (const int64_t*)(off + 2 * ob);
+  src.act_miner = (const int32_t*)b->tr_miner.p;
+  src.act_delay = (const double*)b->tr_delay.p;
+  src.pow_hash = (const int32_t*)b->tr_pow.p;
+  src.link_key = (const uint64_t*)b->tr_key.p;
+  src.link_delay = (const double*)b->tr_ldelay.p;
+  return run_sync(b, E, 0, &src, summary, records, records_on_device);
 }
 
 // ---------------------------------------------------------------- lockstep API

@@ -132,6 +132,107 @@ struct Stream {
     const Words4 w = block(serial, TAG_MSG | (dest >> 1));
     return (dest & 1u) ? u53(w.w2, w.w3) : u53(w.w0, w.w1);
   }
+
+  // ---- draws as the lanes consume them (the same interface as TraceStream)
+  // miner of activation j among [attacker] + d equal-weight defenders
+  __host__ __device__ inline int32_t miner(uint32_t j, uint64_t t_att, int32_t d) const {
+    const Words4 w = block(j, TAG_ACT);
+    if ((uint64_t)w.w0 < t_att) return 0;
+    return 1 + (int32_t)(((uint64_t)w.w1 * (uint64_t)d) >> 32);
+  }
+  // exponential delay of clock j (distributions.ml:120-127)
+  __host__ __device__ inline double clock(uint32_t j, double ev) const {
+    const Words4 w = block(j, TAG_ACT);
+    return (-1.0 * ev) * cpr_log(u53(w.w2, w.w3));
+  }
+  // both draws of activation j from one counter block
+  __host__ __device__ inline double act(uint32_t j, uint64_t t_att, int32_t d, double ev,
+                                        int32_t* miner_out) const {
+    const Words4 w = block(j, TAG_ACT);
+    *miner_out = (uint64_t)w.w0 < t_att ? 0 : 1 + (int32_t)(((uint64_t)w.w1 * (uint64_t)d) >> 32);
+    return (-1.0 * ev) * cpr_log(u53(w.w2, w.w3));
+  }
+  __host__ __device__ inline int32_t pow(uint32_t serial) const {
+    return (int32_t)(block(serial, TAG_POW).w0 & 0x3FFFFFFFu);
+  }
+  // U(0, dmax) link delays (network.ml:68-76)
+  __host__ __device__ inline double link(uint32_t kw, uint32_t off, uint32_t dest,
+                                         double dmax) const {
+    return link_u(kw, off, dest) * (dmax - 0.0) + 0.0;
+  }
+  __host__ __device__ inline double msg(uint32_t serial, uint32_t dest, double dmax) const {
+    return msg_u(serial, dest) * (dmax - 0.0) + 0.0;
+  }
+};
+
+// ---- replay of an exported activation/delay trace (cpr_replay)
+//
+// The same draws, read from a trace instead of computed: activation j's miner and clock
+// delay, the pow hash of vertex serial s, and message delays keyed by the coordinates of
+// the keyed stream (trace_link_key / trace_msg_key), sorted ascending per episode. A draw
+// the trace does not hold sets `miss` (the record gets CPR_ST_TRACE_MISS) and returns a
+// finite placeholder so the lane still terminates.
+__host__ __device__ inline uint64_t trace_link_key(uint32_t kw, uint32_t off, uint32_t dest) {
+  return ((uint64_t)kw << 32) | ((uint64_t)(off & 0xFFFFFu) << 12) | (uint64_t)(dest & 0xFFFu);
+}
+__host__ __device__ inline uint64_t trace_msg_key(uint32_t serial, uint32_t dest) {
+  return ((uint64_t)serial << 32) | (uint64_t)(dest & 0xFFFu);
+}
+
+struct TraceStream {
+  const int32_t* act_miner;  // [n_act]
+  const double* act_delay;   // [n_act]
+  const int32_t* pow_hash;   // [n_pow], by vertex serial
+  const uint64_t* key;       // [n_link], ascending
+  const double* delay;       // [n_link]
+  int32_t n_act, n_pow, n_link;
+  mutable uint32_t miss;
+
+  __host__ __device__ inline int32_t miner(uint32_t j, uint64_t, int32_t) const {
+    if (j < (uint32_t)n_act) return act_miner[j];
+    miss = 1u;
+    return 0;
+  }
+  __host__ __device__ inline double clock(uint32_t j, double) const {
+    if (j < (uint32_t)n_act) return act_delay[j];
+    miss = 1u;
+    return 1.0;
+  }
+  __host__ __device__ inline double act(uint32_t j, uint64_t, int32_t, double,
+                                        int32_t* miner_out) const {
+    if (j < (uint32_t)n_act) {
+      *miner_out = act_miner[j];
+      return act_delay[j];
+    }
+    miss = 1u;
+    *miner_out = 0;
+    return 1.0;
+  }
+  __host__ __device__ inline int32_t pow(uint32_t serial) const {
+    if (serial < (uint32_t)n_pow) return pow_hash[serial];
+    miss = 1u;
+    return 0;
+  }
+  __host__ __device__ inline double lookup(uint64_t k) const {
+    int32_t lo = 0, hi = n_link;
+    while (lo < hi) {
+      const int32_t mid = (lo + hi) >> 1;
+      if (key[mid] < k)
+        lo = mid + 1;
+      else
+        hi = mid;
+    }
+    if (lo < n_link && key[lo] == k) return delay[lo];
+    miss = 1u;
+    return 0.0;
+  }
+  __host__ __device__ inline double link(uint32_t kw, uint32_t off, uint32_t dest,
+                                         double) const {
+    return lookup(trace_link_key(kw, off, dest));
+  }
+  __host__ __device__ inline double msg(uint32_t serial, uint32_t dest, double) const {
+    return lookup(trace_msg_key(serial, dest));
+  }
 };
 
 }  // namespace cpr

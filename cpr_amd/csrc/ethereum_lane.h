@@ -291,16 +291,16 @@ struct EthLane {
   }
 
   // ------------------------------------------------------------------ randomness
-  __host__ __device__ inline int32_t miner_of(const EthParams& P, const Stream& S, int32_t k) {
-    const Words4 w = S.block((uint32_t)k, TAG_ACT);
-    if ((uint64_t)w.w0 < P.t_att) return 0;
-    return 1 + (int32_t)(((uint64_t)w.w1 * (uint64_t)P.d) >> 32);
+  template <class St>
+  __host__ __device__ inline int32_t miner_of(const EthParams& P, const St& S, int32_t k) {
+    return S.miner((uint32_t)k, P.t_att, P.d);
   }
-  __host__ __device__ inline double act_delay(const EthParams& P, const Stream& S, int32_t j) {
-    const Words4 w = S.block((uint32_t)j, TAG_ACT);
-    return (-1.0 * P.ev) * cpr_log(u53(w.w2, w.w3));
+  template <class St>
+  __host__ __device__ inline double act_delay(const EthParams& P, const St& S, int32_t j) {
+    return S.clock((uint32_t)j, P.ev);
   }
-  __host__ __device__ inline void schedule_pow(const EthParams& P, const Stream& S,
+  template <class St>
+  __host__ __device__ inline void schedule_pow(const EthParams& P, const St& S,
                                                const EthMem& M) {
     push(P, M, now + act_delay(P, S, c_act), mkev(EV_CLOCK, 0, KD_POW), -1);
   }
@@ -669,7 +669,8 @@ struct EthLane {
   }
 
   // ------------------------------------------------------------------ engine
-  __host__ __device__ inline void init(const EthParams& P, const Stream& S, const EthMem& M) {
+  template <class St>
+  __host__ __device__ inline void init(const EthParams& P, const St& S, const EthMem& M) {
     now = 0.0;
     c_act = 0;
     newest = 0;
@@ -701,7 +702,8 @@ struct EthLane {
   }
 
   // one popped event that is not the attacker's gym interaction (simulator.ml:421-508)
-  __host__ __device__ inline void handle(const EthParams& P, const Stream& S, const EthMem& M,
+  template <class St>
+  __host__ __device__ inline void handle(const EthParams& P, const St& S, const EthMem& M,
                                          uint32_t ev, int32_t s) {
     const uint32_t ty = ev & 7u, kind = (ev >> 3) & 3u;
     const int32_t node = (int32_t)(ev >> 5);
@@ -761,9 +763,7 @@ struct EthLane {
           if (P.net == 1)
             delay = 0.0;
           else if (node == 0)
-            delay = S.link_u((uint32_t)b.share_k, (uint32_t)b.share_off, (uint32_t)dst) *
-                        (P.dmax - 0.0) +
-                    0.0;
+            delay = S.link((uint32_t)b.share_k, (uint32_t)b.share_off, (uint32_t)dst, P.dmax);
           else
             delay = dst == 0 ? 0.0 : P.delta;
           push(P, M, now + delay, mkev(EV_RX, dst, KD_NET), s);
@@ -797,7 +797,8 @@ struct EthLane {
   }
 
   // engine.ml:108-121
-  __host__ __device__ inline bool skip_to_interaction(const EthParams& P, const Stream& S,
+  template <class St>
+  __host__ __device__ inline bool skip_to_interaction(const EthParams& P, const St& S,
                                                       const EthMem& M, uint32_t* kind,
                                                       int32_t* blk) {
     double t;
@@ -843,7 +844,8 @@ struct EthLane {
   }
 
   // gym: reset (engine.ml:122-170)
-  __host__ __device__ inline void gym_reset(const EthParams& P, const Stream& S,
+  template <class St>
+  __host__ __device__ inline void gym_reset(const EthParams& P, const St& S,
                                             const EthMem& M) {
     init(P, S, M);
     uint32_t kind;
@@ -852,7 +854,8 @@ struct EthLane {
   }
 
   // gym: step (engine.ml:176-249); returns the head, sets *done
-  __host__ __device__ inline int32_t gym_step(const EthParams& P, const Stream& S,
+  template <class St>
+  __host__ __device__ inline int32_t gym_step(const EthParams& P, const St& S,
                                               const EthMem& M, int32_t action, bool* done) {
     const int32_t sh = apply(P, M, action);
     if (sh >= 0) share(P, M, 0, sh);
@@ -868,7 +871,8 @@ struct EthLane {
   }
 
   // loop: Simulator.loop ~activations (simulator.ml:519-533), then the head
-  __host__ __device__ inline int32_t loop(const EthParams& P, const Stream& S, const EthMem& M) {
+  template <class St>
+  __host__ __device__ inline int32_t loop(const EthParams& P, const St& S, const EthMem& M) {
     init(P, S, M);
     int64_t left = P.activations;
     double t;

@@ -8,6 +8,7 @@
 #include "bk_lane.h"
 #include "ethereum_lane.h"
 #include "nakamoto_lane.h"
+#include "summary.h"
 #include "ts_lane.h"
 
 namespace cpr {
@@ -46,6 +47,11 @@ hipError_t launch_run_episodes(const NakParams& P, uint64_t seed, uint64_t first
                                int32_t mode, int64_t activations, int32_t* spill, double* tlog,
                                uint8_t* replay, int64_t lanes, cpr_episode_record* recs,
                                cpr_summary* sum, hipStream_t st);
+// the same fused kernel drawing from a device copy of a cpr_trace (cpr_replay)
+hipError_t launch_replay_episodes(const NakParams& P, const TraceSource& src, int64_t n_eps,
+                                  int32_t mode, int64_t activations, int32_t* spill,
+                                  double* tlog, uint8_t* replay, int64_t lanes,
+                                  cpr_episode_record* recs, cpr_summary* sum, hipStream_t st);
 hipError_t launch_reset(const NakParams& P, uint64_t seed, const LockBuffers& B, int64_t n,
                         const uint8_t* mask, const uint64_t* eps, int unit, const double* tab_nn,
                         const double* tab_sg, int32_t tab_n, double* obs, hipStream_t st);
@@ -65,12 +71,18 @@ hipError_t launch_eth_run_episodes(const eth::EthParams& P, uint64_t seed, uint6
                                    int64_t n_eps, uint8_t* mem, int64_t lane_bytes,
                                    int64_t lanes, cpr_episode_record* recs, cpr_summary* sum,
                                    hipStream_t st);
+hipError_t launch_eth_replay_episodes(const eth::EthParams& P, const TraceSource& src, int64_t n_eps,
+                                 uint8_t* mem, int64_t lane_bytes, int64_t lanes,
+                                 cpr_episode_record* recs, cpr_summary* sum, hipStream_t st);
 int eth_blocks_per_cu();
 
 // B_k (kernels_bk.hip): mem = lanes x lane_bytes; lockstep slots = n x bk_slot_bytes()
 hipError_t launch_bk_run_episodes(const bk::BkParams& P, uint64_t seed, uint64_t first,
                                   int64_t n_eps, uint8_t* mem, int64_t lane_bytes, int64_t lanes,
                                   cpr_episode_record* recs, cpr_summary* sum, hipStream_t st);
+hipError_t launch_bk_replay_episodes(const bk::BkParams& P, const TraceSource& src, int64_t n_eps,
+                                 uint8_t* mem, int64_t lane_bytes, int64_t lanes,
+                                 cpr_episode_record* recs, cpr_summary* sum, hipStream_t st);
 hipError_t launch_bk_reset(const bk::BkParams& P, uint64_t seed, uint8_t* mem, int64_t lane_bytes,
                            void* slots, int64_t n, const uint8_t* mask, const uint64_t* eps,
                            int unit, const double* tabs, int32_t tn, double* obs, hipStream_t st);
@@ -92,6 +104,9 @@ int bk_blocks_per_cu();
 hipError_t launch_ts_run_episodes(const ts::TsParams& P, uint64_t seed, uint64_t first,
                                   int64_t n_eps, uint8_t* mem, int64_t lane_bytes, int64_t lanes,
                                   cpr_episode_record* recs, cpr_summary* sum, hipStream_t st);
+hipError_t launch_ts_replay_episodes(const ts::TsParams& P, const TraceSource& src, int64_t n_eps,
+                                 uint8_t* mem, int64_t lane_bytes, int64_t lanes,
+                                 cpr_episode_record* recs, cpr_summary* sum, hipStream_t st);
 hipError_t launch_ts_reset(const ts::TsParams& P, uint64_t seed, uint8_t* mem, int64_t lane_bytes,
                            void* slots, int64_t n, const uint8_t* mask, const uint64_t* eps,
                            int unit, const double* tabs, int32_t tn, double* obs, hipStream_t st);

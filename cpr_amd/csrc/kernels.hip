@@ -27,7 +27,8 @@ __device__ inline void acc_add(Acc& a, const BRef& hd, int64_t steps, int64_t ac
 
 // One gym episode (engine.ml:164-249): reset = first activation up to the attacker's
 // interaction; step = apply, deliveries, next activation, observe; head at the end.
-__device__ inline BRef run_gym(NakLane& L, const NakParams& P, const Stream& S, const LaneMem& M,
+template <class St>
+__device__ inline BRef run_gym(NakLane& L, const NakParams& P, const St& S, const LaneMem& M,
                                int64_t* steps_out) {
   L.init();
   L.activate(P, S, M);
@@ -49,7 +50,8 @@ __device__ inline BRef run_gym(NakLane& L, const NakParams& P, const Stream& S, 
 
 // Simulator.loop ~activations with the SSZ attacker as node 0 (simulator.ml:519-533,
 // nakamoto_ssz.ml:362-372); all messages delivered before the head is taken.
-__device__ inline BRef run_loop(NakLane& L, const NakParams& P, const Stream& S, const LaneMem& M,
+template <class St>
+__device__ inline BRef run_loop(NakLane& L, const NakParams& P, const St& S, const LaneMem& M,
                                 int64_t activations) {
   L.init();
   for (int64_t i = 0; i < activations; ++i) {
@@ -60,9 +62,9 @@ __device__ inline BRef run_loop(NakLane& L, const NakParams& P, const Stream& S,
   return L.head(P, M);
 }
 
-template <int MODE>
+template <int MODE, class Src>
 __global__ __launch_bounds__(kBlock) void k_run_episodes(
-    NakParams P, uint64_t seed, uint64_t first, int64_t n_eps, int64_t activations,
+    NakParams P, Src src, int64_t n_eps, int64_t activations,
     int32_t* spill, double* tlog, uint8_t* replay, cpr_episode_record* recs, cpr_summary* sum) {
   __shared__ int32_t hist[CPR_HIST_BINS];
   __shared__ int32_t ring[RING * kBlock];
@@ -83,13 +85,13 @@ __global__ __launch_bounds__(kBlock) void k_run_episodes(
   Acc acc = {};
   NakLane L;
   for (int64_t e = tid; e < n_eps; e += nthreads) {
-    const uint64_t ep = first + (uint64_t)e;
-    const Stream S = make_stream(seed, ep);
+    const auto S = src.at(e);
     int64_t steps = 0;
     const BRef hd = MODE == CPR_MODE_GYM ? run_gym(L, P, S, M, &steps)
                                          : run_loop(L, P, S, M, activations);
     const double tm = L.time_of(M, hd);
-    acc_add(acc, hd, steps, L.k, L.status, hist);
+    const uint32_t status = L.status | Src::missed(S);
+    acc_add(acc, hd, steps, L.k, status, hist);
     if (recs) {
       cpr_episode_record r;
       r.reward_attacker = (double)hd.ra;
@@ -101,7 +103,7 @@ __global__ __launch_bounds__(kBlock) void k_run_episodes(
       r.n_activations = L.k;
       r.head_height = hd.h;
       r.head_miner = MODE == CPR_MODE_GYM ? miner_of(P, S, hd.k) : -1;
-      r.status = L.status;
+      r.status = status;
       r.head_work = 0;
       recs[e] = r;
     }
@@ -258,12 +260,27 @@ hipError_t launch_run_episodes(const NakParams& P, uint64_t seed, uint64_t first
                                uint8_t* replay, int64_t lanes, cpr_episode_record* recs,
                                cpr_summary* sum, hipStream_t st) {
   const unsigned blocks = (unsigned)(lanes / kBlock);
+  const SeedSource src{seed, first};
   if (mode == CPR_MODE_GYM)
-    hipLaunchKernelGGL(k_run_episodes<CPR_MODE_GYM>, dim3(blocks), dim3(kBlock), 0, st, P, seed,
-                       first, n_eps, activations, spill, tlog, replay, recs, sum);
+    hipLaunchKernelGGL((k_run_episodes<CPR_MODE_GYM, SeedSource>), dim3(blocks), dim3(kBlock), 0,
+                       st, P, src, n_eps, activations, spill, tlog, replay, recs, sum);
   else
-    hipLaunchKernelGGL(k_run_episodes<CPR_MODE_LOOP>, dim3(blocks), dim3(kBlock), 0, st, P, seed,
-                       first, n_eps, activations, spill, tlog, replay, recs, sum);
+    hipLaunchKernelGGL((k_run_episodes<CPR_MODE_LOOP, SeedSource>), dim3(blocks), dim3(kBlock), 0,
+                       st, P, src, n_eps, activations, spill, tlog, replay, recs, sum);
+  return hipGetLastError();
+}
+
+hipError_t launch_replay_episodes(const NakParams& P, const TraceSource& src, int64_t n_eps,
+                                  int32_t mode, int64_t activations, int32_t* spill,
+                                  double* tlog, uint8_t* replay, int64_t lanes,
+                                  cpr_episode_record* recs, cpr_summary* sum, hipStream_t st) {
+  const unsigned blocks = (unsigned)(lanes / kBlock);
+  if (mode == CPR_MODE_GYM)
+    hipLaunchKernelGGL((k_run_episodes<CPR_MODE_GYM, TraceSource>), dim3(blocks), dim3(kBlock), 0,
+                       st, P, src, n_eps, activations, spill, tlog, replay, recs, sum);
+  else
+    hipLaunchKernelGGL((k_run_episodes<CPR_MODE_LOOP, TraceSource>), dim3(blocks), dim3(kBlock),
+                       0, st, P, src, n_eps, activations, spill, tlog, replay, recs, sum);
   return hipGetLastError();
 }
 
@@ -314,9 +331,9 @@ int run_episodes_blocks_per_cu(int32_t mode) {
   int blocks = 0;
   hipError_t e = mode == CPR_MODE_GYM
                      ? hipOccupancyMaxActiveBlocksPerMultiprocessor(
-                           &blocks, k_run_episodes<CPR_MODE_GYM>, kBlock, 0)
+                           &blocks, k_run_episodes<CPR_MODE_GYM, SeedSource>, kBlock, 0)
                      : hipOccupancyMaxActiveBlocksPerMultiprocessor(
-                           &blocks, k_run_episodes<CPR_MODE_LOOP>, kBlock, 0);
+                           &blocks, k_run_episodes<CPR_MODE_LOOP, SeedSource>, kBlock, 0);
   if (e != hipSuccess || blocks <= 0) blocks = 2;
   return blocks;
 }

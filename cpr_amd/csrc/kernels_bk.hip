@@ -37,8 +37,9 @@ __device__ inline void bk_acc(Acc& acc, const bk::BkParams& P, const bk::BkLane&
               (int64_t)h.height * P.k, L.steps, L.c_act, L.status, hist);
 }
 
+template <class Src>
 __global__ __launch_bounds__(kBlock) void k_bk_run_episodes(
-    bk::BkParams P, uint64_t seed, uint64_t first, int64_t n_eps, uint8_t* mem,
+    bk::BkParams P, Src src, int64_t n_eps, uint8_t* mem,
     int64_t lane_bytes, cpr_episode_record* recs, cpr_summary* sum) {
   __shared__ int32_t hist[CPR_HIST_BINS];
   if (threadIdx.x < CPR_HIST_BINS) hist[threadIdx.x] = 0;
@@ -49,8 +50,7 @@ __global__ __launch_bounds__(kBlock) void k_bk_run_episodes(
   Acc acc = {};
   bk::BkLane L;
   for (int64_t e = tid; e < n_eps; e += nthreads) {
-    const uint64_t ep = first + (uint64_t)e;
-    const Stream S = make_stream(seed, ep);
+    const auto S = src.at(e);
     int32_t hd;
     if (P.mode == CPR_MODE_GYM) {
       L.gym_reset(P, S, M);
@@ -60,6 +60,7 @@ __global__ __launch_bounds__(kBlock) void k_bk_run_episodes(
     } else {
       hd = L.loop(P, S, M);
     }
+    L.status |= Src::missed(S);
     const bk::BVtx& h = L.X(P, M, hd);
     bk_acc(acc, P, L, h, hist);
     if (recs) {
@@ -277,8 +278,16 @@ static unsigned grid_of(int64_t n) { return (unsigned)((n + kBlock - 1) / kBlock
 hipError_t launch_bk_run_episodes(const bk::BkParams& P, uint64_t seed, uint64_t first,
                                   int64_t n_eps, uint8_t* mem, int64_t lane_bytes, int64_t lanes,
                                   cpr_episode_record* recs, cpr_summary* sum, hipStream_t st) {
-  hipLaunchKernelGGL(k_bk_run_episodes, dim3((unsigned)(lanes / kBlock)), dim3(kBlock), 0, st, P,
-                     seed, first, n_eps, mem, lane_bytes, recs, sum);
+  hipLaunchKernelGGL(k_bk_run_episodes<SeedSource>, dim3((unsigned)(lanes / kBlock)), dim3(kBlock), 0, st, P,
+                     SeedSource{seed, first}, n_eps, mem, lane_bytes, recs, sum);
+  return hipGetLastError();
+}
+
+hipError_t launch_bk_replay_episodes(const bk::BkParams& P, const TraceSource& src, int64_t n_eps,
+                                 uint8_t* mem, int64_t lane_bytes, int64_t lanes,
+                                 cpr_episode_record* recs, cpr_summary* sum, hipStream_t st) {
+  hipLaunchKernelGGL(k_bk_run_episodes<TraceSource>, dim3((unsigned)(lanes / kBlock)),
+                     dim3(kBlock), 0, st, P, src, n_eps, mem, lane_bytes, recs, sum);
   return hipGetLastError();
 }
 
@@ -328,7 +337,7 @@ size_t bk_slot_bytes() { return sizeof(BkSlot); }
 int bk_blocks_per_cu() {
   int blocks = 0;
   hipError_t e =
-      hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, k_bk_run_episodes, kBlock, 0);
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, k_bk_run_episodes<SeedSource>, kBlock, 0);
   if (e != hipSuccess || blocks <= 0) blocks = 2;
   return blocks;
 }

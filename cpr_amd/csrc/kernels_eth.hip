@@ -14,8 +14,9 @@
 
 namespace cpr {
 
+template <class Src>
 __global__ __launch_bounds__(kBlock) void k_eth_run_episodes(
-    eth::EthParams P, uint64_t seed, uint64_t first, int64_t n_eps, uint8_t* mem,
+    eth::EthParams P, Src src, int64_t n_eps, uint8_t* mem,
     int64_t lane_bytes, cpr_episode_record* recs, cpr_summary* sum) {
   __shared__ int32_t hist[CPR_HIST_BINS];
   if (threadIdx.x < CPR_HIST_BINS) hist[threadIdx.x] = 0;
@@ -26,8 +27,7 @@ __global__ __launch_bounds__(kBlock) void k_eth_run_episodes(
   Acc acc = {};
   eth::EthLane L;
   for (int64_t e = tid; e < n_eps; e += nthreads) {
-    const uint64_t ep = first + (uint64_t)e;
-    const Stream S = make_stream(seed, ep);
+    const auto S = src.at(e);
     int32_t hd;
     if (P.mode == CPR_MODE_GYM) {
       L.gym_reset(P, S, M);
@@ -40,6 +40,7 @@ __global__ __launch_bounds__(kBlock) void k_eth_run_episodes(
     } else {
       hd = L.loop(P, S, M);
     }
+    L.status |= Src::missed(S);
     const eth::EBlock& h = L.B(P, M, hd);
     const int32_t ra = h.rew_att, rd = h.rew_def;
     const double rel = (ra + rd) != 0 ? (double)ra / (double)(ra + rd) : 0.0;
@@ -70,15 +71,22 @@ hipError_t launch_eth_run_episodes(const eth::EthParams& P, uint64_t seed, uint6
                                    int64_t lanes, cpr_episode_record* recs, cpr_summary* sum,
                                    hipStream_t st) {
   const unsigned blocks = (unsigned)(lanes / kBlock);
-  hipLaunchKernelGGL(k_eth_run_episodes, dim3(blocks), dim3(kBlock), 0, st, P, seed, first,
-                     n_eps, mem, lane_bytes, recs, sum);
+  hipLaunchKernelGGL(k_eth_run_episodes<SeedSource>, dim3(blocks), dim3(kBlock), 0, st, P, SeedSource{seed, first}, n_eps, mem, lane_bytes, recs, sum);
+  return hipGetLastError();
+}
+
+hipError_t launch_eth_replay_episodes(const eth::EthParams& P, const TraceSource& src, int64_t n_eps,
+                                 uint8_t* mem, int64_t lane_bytes, int64_t lanes,
+                                 cpr_episode_record* recs, cpr_summary* sum, hipStream_t st) {
+  hipLaunchKernelGGL(k_eth_run_episodes<TraceSource>, dim3((unsigned)(lanes / kBlock)),
+                     dim3(kBlock), 0, st, P, src, n_eps, mem, lane_bytes, recs, sum);
   return hipGetLastError();
 }
 
 int eth_blocks_per_cu() {
   int blocks = 0;
   hipError_t e =
-      hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, k_eth_run_episodes, kBlock, 0);
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, k_eth_run_episodes<SeedSource>, kBlock, 0);
   if (e != hipSuccess || blocks <= 0) blocks = 2;
   return blocks;
 }

@@ -43,8 +43,9 @@ __device__ inline void ts_acc(Acc& acc, const ts::TsParams& P, ts::TsLane& L,
               (int64_t)h * P.k << 20, rel, (int64_t)h * P.k, L.steps, L.c_act, L.status, hist);
 }
 
+template <class Src>
 __global__ __launch_bounds__(kBlock) void k_ts_run_episodes(
-    ts::TsParams P, uint64_t seed, uint64_t first, int64_t n_eps, uint8_t* mem,
+    ts::TsParams P, Src src, int64_t n_eps, uint8_t* mem,
     int64_t lane_bytes, cpr_episode_record* recs, cpr_summary* sum) {
   __shared__ int32_t hist[CPR_HIST_BINS];
   if (threadIdx.x < CPR_HIST_BINS) hist[threadIdx.x] = 0;
@@ -55,8 +56,7 @@ __global__ __launch_bounds__(kBlock) void k_ts_run_episodes(
   Acc acc = {};
   ts::TsLane L;
   for (int64_t e = tid; e < n_eps; e += nthreads) {
-    const uint64_t ep = first + (uint64_t)e;
-    const Stream S = make_stream(seed, ep);
+    const auto S = src.at(e);
     int32_t hd;
     if (P.mode == CPR_MODE_GYM) {
       L.gym_reset(P, S, M);
@@ -66,6 +66,7 @@ __global__ __launch_bounds__(kBlock) void k_ts_run_episodes(
     } else {
       hd = L.loop(P, S, M);
     }
+    L.status |= Src::missed(S);
     ts_acc(acc, P, L, M, hd, hist);
     if (recs) {
       cpr_episode_record r;
@@ -264,8 +265,16 @@ static unsigned ts_grid(int64_t n) { return (unsigned)((n + kBlock - 1) / kBlock
 hipError_t launch_ts_run_episodes(const ts::TsParams& P, uint64_t seed, uint64_t first,
                                   int64_t n_eps, uint8_t* mem, int64_t lane_bytes, int64_t lanes,
                                   cpr_episode_record* recs, cpr_summary* sum, hipStream_t st) {
-  hipLaunchKernelGGL(k_ts_run_episodes, dim3((unsigned)(lanes / kBlock)), dim3(kBlock), 0, st, P,
-                     seed, first, n_eps, mem, lane_bytes, recs, sum);
+  hipLaunchKernelGGL(k_ts_run_episodes<SeedSource>, dim3((unsigned)(lanes / kBlock)), dim3(kBlock), 0, st, P,
+                     SeedSource{seed, first}, n_eps, mem, lane_bytes, recs, sum);
+  return hipGetLastError();
+}
+
+hipError_t launch_ts_replay_episodes(const ts::TsParams& P, const TraceSource& src, int64_t n_eps,
+                                 uint8_t* mem, int64_t lane_bytes, int64_t lanes,
+                                 cpr_episode_record* recs, cpr_summary* sum, hipStream_t st) {
+  hipLaunchKernelGGL(k_ts_run_episodes<TraceSource>, dim3((unsigned)(lanes / kBlock)),
+                     dim3(kBlock), 0, st, P, src, n_eps, mem, lane_bytes, recs, sum);
   return hipGetLastError();
 }
 
@@ -315,7 +324,7 @@ size_t ts_slot_bytes() { return sizeof(TsSlot); }
 int ts_blocks_per_cu() {
   int blocks = 0;
   hipError_t e =
-      hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, k_ts_run_episodes, kBlock, 0);
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, k_ts_run_episodes<SeedSource>, kBlock, 0);
   if (e != hipSuccess || blocks <= 0) blocks = 2;
   return blocks;
 }

@@ -239,7 +239,8 @@ struct SkewHeapLane {
 // at activation count kw, top first), the top one at the fresh block's height. Returns the
 // non-miner defenders that end on the released top (first received wins,
 // nakamoto.ml:85-89). *ok = false on capacity overflow.
-__host__ __device__ inline uint64_t tie_replay(const NakParams& P, const Stream& S,
+template <class St>
+__host__ __device__ inline uint64_t tie_replay(const NakParams& P, const St& S,
                                                const ReplayMem& M, int32_t miner, double t,
                                                int32_t rlo, int32_t rhi, int32_t kw, bool* ok) {
   const int32_t r = rhi - rlo + 1;
@@ -313,8 +314,7 @@ __host__ __device__ inline uint64_t tie_replay(const NakParams& P, const Stream&
         } else {
           const uint32_t off = (uint32_t)(r - x);  // share order: top first
           for (int32_t jj = 1; jj <= P.d; ++jj) {
-            const double u = S.link_u((uint32_t)kw, off, (uint32_t)jj);
-            H.push(now + (u * (P.dmax - 0.0) + 0.0), re_ev(RE_RX, jj, x));
+            H.push(now + S.link((uint32_t)kw, off, (uint32_t)jj, P.dmax), re_ev(RE_RX, jj, x));
           }
         }
         break;
@@ -385,15 +385,15 @@ struct NakLane {
 
   // latest finite arrival of the previous window (exact; only evaluated when the next
   // activation lands inside the conservative bound, ~1e-9 of activations in the gym)
+  template <class St>
   __host__ __device__ inline double window_last_arrival(const NakParams& P,
-                                                        const Stream& S) const {
+                                                        const St& S) const {
     double last = -__builtin_inf();
     if (w_hasb && P.d >= 2) last = w_t + P.delta;
     if (w_rhi >= w_rlo && P.arrive) {
       for (int32_t j = 1; j <= P.d; ++j)
         for (int32_t m = w_rlo; m <= w_rhi; ++m) {
-          const double u = S.link_u((uint32_t)w_kw, (uint32_t)(w_rhi - m), (uint32_t)j);
-          const double a = w_t + (u * (P.dmax - 0.0) + 0.0);
+          const double a = w_t + S.link((uint32_t)w_kw, (uint32_t)(w_rhi - m), (uint32_t)j, P.dmax);
           last = a > last ? a : last;
         }
     }
@@ -402,9 +402,10 @@ struct NakLane {
 
   // StochasticClock + Dag + the attacker's prepare (simulator.ml:465-480, engine.ml:108-121,
   // nakamoto_ssz.ml:291-318)
-  __host__ __device__ inline void activate(const NakParams& P, const Stream& S, const LaneMem& M) {
-    const Words4 w = S.block((uint32_t)k, TAG_ACT);
-    const double tn = t + (-1.0 * P.ev) * cpr_log(u53(w.w2, w.w3));
+  template <class St>
+  __host__ __device__ inline void activate(const NakParams& P, const St& S, const LaneMem& M) {
+    int32_t miner;
+    const double tn = t + S.act((uint32_t)k, P.t_att, P.d, P.ev, &miner);
     if (tn <= w_bound) {
       if (tn <= window_last_arrival(P, S)) status |= ST_OVERLAP;
     }
@@ -412,8 +413,6 @@ struct NakLane {
     M.tlog[(int64_t)(k & M.tmask) * M.tlog_stride] = tn;
     const int32_t ka = k;
     ++k;
-    int32_t miner = 0;
-    if ((uint64_t)w.w0 >= P.t_att) miner = 1 + (int32_t)(((uint64_t)w.w1 * (uint64_t)P.d) >> 32);
     wminer = miner;
     // deliver pending releases to the attacker's public model (strict >)
     if (pend >= 0 && p0.h + pend > pub.h) pub = chain_ref(M, pend);
@@ -495,7 +494,8 @@ struct NakLane {
 
   // deliveries of the window: the fresh defender block and the attacker's release reach
   // the defenders (simulator.ml:481-508 with update_head, nakamoto.ml:85-89)
-  __host__ __device__ inline void resolve(const NakParams& P, const Stream& S, const LaneMem& M) {
+  template <class St>
+  __host__ __device__ inline void resolve(const NakParams& P, const St& S, const LaneMem& M) {
     const bool released = rhi >= rlo && P.arrive;
     const uint64_t all = all_mask(P.d);
     double bound = -__builtin_inf();
@@ -516,8 +516,7 @@ struct NakLane {
             if (j == wminer) continue;
             double v = -__builtin_inf();
             for (int32_t m = rlo; m <= rhi; ++m) {
-              const double u = S.link_u((uint32_t)rkw, (uint32_t)(rhi - m), (uint32_t)j);
-              const double a = t + (u * (P.dmax - 0.0) + 0.0);
+              const double a = t + S.link((uint32_t)rkw, (uint32_t)(rhi - m), (uint32_t)j, P.dmax);
               v = a > v ? a : v;
             }
             if (v < tb) mask |= 1ull << (j - 1);
@@ -605,11 +604,10 @@ struct NakLane {
 };
 
 // miner of activation index ka (for head_miner of the record)
-__host__ __device__ inline int32_t miner_of(const NakParams& P, const Stream& S, int32_t ka) {
+template <class St>
+__host__ __device__ inline int32_t miner_of(const NakParams& P, const St& S, int32_t ka) {
   if (ka < 0) return -1;
-  const Words4 w = S.block((uint32_t)ka, TAG_ACT);
-  if ((uint64_t)w.w0 < P.t_att) return 0;
-  return 1 + (int32_t)(((uint64_t)w.w1 * (uint64_t)P.d) >> 32);
+  return S.miner((uint32_t)ka, P.t_att, P.d);
 }
 
 }  // namespace cpr

@@ -82,5 +82,42 @@ __device__ inline Stream make_stream(uint64_t seed, uint64_t ep) {
   return S;
 }
 
+// Where a fused episode kernel gets the draws of its e-th episode: the keyed stream of
+// episode first + e (cpr_run_episodes), or episode e of a device copy of a cpr_trace
+// (cpr_replay). missed() is the status bit a lane adds to its record.
+struct SeedSource {
+  uint64_t seed, first;
+  __device__ inline Stream at(int64_t e) const { return make_stream(seed, first + (uint64_t)e); }
+  __device__ static inline uint32_t missed(const Stream&) { return 0u; }
+};
+
+struct TraceSource {
+  const int64_t* act_off;
+  const int32_t* act_miner;
+  const double* act_delay;
+  const int64_t* pow_off;
+  const int32_t* pow_hash;
+  const int64_t* link_off;
+  const uint64_t* link_key;
+  const double* link_delay;
+  __device__ inline TraceStream at(int64_t e) const {
+    TraceStream S;
+    const int64_t a0 = act_off[e], p0 = pow_off[e], l0 = link_off[e];
+    S.act_miner = act_miner + a0;
+    S.act_delay = act_delay + a0;
+    S.n_act = (int32_t)(act_off[e + 1] - a0);
+    S.pow_hash = pow_hash + p0;
+    S.n_pow = (int32_t)(pow_off[e + 1] - p0);
+    S.key = link_key + l0;
+    S.delay = link_delay + l0;
+    S.n_link = (int32_t)(link_off[e + 1] - l0);
+    S.miss = 0u;
+    return S;
+  }
+  __device__ static inline uint32_t missed(const TraceStream& S) {
+    return S.miss ? (uint32_t)CPR_ST_TRACE_MISS : 0u;
+  }
+};
+
 
 }  // namespace cpr

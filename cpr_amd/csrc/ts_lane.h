@@ -358,15 +358,14 @@ struct TsLane {
   }
 
   // ------------------------------------------------------------------ randomness
-  __host__ __device__ inline int32_t miner_of(const TsParams& P, const Stream& S, int32_t j) {
-    const Words4 w = S.block((uint32_t)j, TAG_ACT);
-    if ((uint64_t)w.w0 < P.t_att) return 0;
-    return 1 + (int32_t)(((uint64_t)w.w1 * (uint64_t)P.d) >> 32);
+  template <class St>
+  __host__ __device__ inline int32_t miner_of(const TsParams& P, const St& S, int32_t j) {
+    return S.miner((uint32_t)j, P.t_att, P.d);
   }
-  __host__ __device__ inline void schedule_pow(const TsParams& P, const Stream& S,
+  template <class St>
+  __host__ __device__ inline void schedule_pow(const TsParams& P, const St& S,
                                                const TsMem& M) {
-    const Words4 w = S.block((uint32_t)c_act, TAG_ACT);
-    push(P, M, now + (-1.0 * P.ev) * cpr_log(u53(w.w2, w.w3)), mkev(EV_CLOCK, 0, KD_POW), -1);
+    push(P, M, now + S.clock((uint32_t)c_act, P.ev), mkev(EV_CLOCK, 0, KD_POW), -1);
   }
 
   // ------------------------------------------------------------------ vote trees
@@ -724,7 +723,8 @@ struct TsLane {
     b.time = now;
     for (int32_t j = 0; j < P.n; ++j) V(P, M, s, j) = V_INV;
   }
-  __host__ __device__ inline int32_t append_vote(const TsParams& P, const Stream& S,
+  template <class St>
+  __host__ __device__ inline int32_t append_vote(const TsParams& P, const St& S,
                                                  const TsMem& M, int32_t node, int32_t parent) {
     TVtx& p = X(P, M, parent);
     const int32_t s = ++newest;
@@ -735,7 +735,7 @@ struct TsLane {
     b.vote = 1;
     b.who = node;
     b.depth = (p.vote ? p.depth : 0) + 1;
-    b.pow = (int32_t)(S.block((uint32_t)s, TAG_POW).w0 & 0x3FFFFFFFu);
+    b.pow = S.pow((uint32_t)s);
     b.ddepth = p.ddepth + 1;
     b.sum = p.vote ? p.sum : parent;
     X(P, M, b.sum).nconf += 1;
@@ -1034,7 +1034,8 @@ struct TsLane {
   }
 
   // ------------------------------------------------------------------ engine
-  __host__ __device__ inline void init(const TsParams& P, const Stream& S, const TsMem& M) {
+  template <class St>
+  __host__ __device__ inline void init(const TsParams& P, const St& S, const TsMem& M) {
     now = 0.0;
     c_act = 0;
     newest = 0;
@@ -1089,7 +1090,8 @@ struct TsLane {
     if (d >= 0) push_now(P, M, mkev(EV_DAG, node, KD_APP), d);
   }
 
-  __host__ __device__ inline void handle(const TsParams& P, const Stream& S, const TsMem& M,
+  template <class St>
+  __host__ __device__ inline void handle(const TsParams& P, const St& S, const TsMem& M,
                                          uint32_t ev, int32_t s) {
     const uint32_t ty = ev & 7u, kind = (ev >> 3) & 3u;
     const int32_t node = (int32_t)(ev >> 5);
@@ -1150,7 +1152,7 @@ struct TsLane {
           if (P.net == 1)
             delay = 0.0;
           else if (node == 0)
-            delay = S.msg_u((uint32_t)s, (uint32_t)dst) * (P.dmax - 0.0) + 0.0;
+            delay = S.msg((uint32_t)s, (uint32_t)dst, P.dmax);
           else
             delay = dst == 0 ? 0.0 : P.delta;
           push(P, M, now + delay, mkev(EV_RX, dst, KD_NET), s);
@@ -1184,7 +1186,8 @@ struct TsLane {
     }
   }
 
-  __host__ __device__ inline bool skip_to_interaction(const TsParams& P, const Stream& S,
+  template <class St>
+  __host__ __device__ inline bool skip_to_interaction(const TsParams& P, const St& S,
                                                       const TsMem& M, uint32_t* kind,
                                                       int32_t* blk) {
     double t;
@@ -1229,14 +1232,16 @@ struct TsLane {
     return v[0];
   }
 
-  __host__ __device__ inline void gym_reset(const TsParams& P, const Stream& S, const TsMem& M) {
+  template <class St>
+  __host__ __device__ inline void gym_reset(const TsParams& P, const St& S, const TsMem& M) {
     init(P, S, M);
     uint32_t kind;
     int32_t b;
     if (skip_to_interaction(P, S, M, &kind, &b)) prepare(P, M, kind, b);
   }
 
-  __host__ __device__ inline int32_t gym_step(const TsParams& P, const Stream& S,
+  template <class St>
+  __host__ __device__ inline int32_t gym_step(const TsParams& P, const St& S,
                                               const TsMem& M, int32_t action, bool* done) {
     apply(P, M, action);
     ++steps;
@@ -1250,7 +1255,8 @@ struct TsLane {
     return hd;
   }
 
-  __host__ __device__ inline int32_t loop(const TsParams& P, const Stream& S, const TsMem& M) {
+  template <class St>
+  __host__ __device__ inline int32_t loop(const TsParams& P, const St& S, const TsMem& M) {
     init(P, S, M);
     int64_t left = P.activations;
     double t;

@@ -167,6 +167,15 @@ class Batch:
         )
         return (s, rec) if records else s
 
+    def replay(self, trace, records=True, summary=None):
+        """Replay an exported activation/delay trace (cpr_replay): record e is trace
+        episode e, run with this batch's protocol, mode and policy."""
+        s = summary if summary is not None else L.Summary()
+        rec = np.zeros(trace.n_episodes, dtype=L.RECORD_DTYPE) if records else None
+        ct = trace.ctrace()
+        L.check(L.lib().cpr_replay(self.handle, ctypes.byref(ct), ctypes.byref(s), L.ptr(rec), 0))
+        return (s, rec) if records else s
+
     def last_launch(self):
         """(kernel_ms, activations) of the last fused-episode launch (HIP events)."""
         ms = ctypes.c_double()

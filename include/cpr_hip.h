@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define CPR_ABI_VERSION 3
+#define CPR_ABI_VERSION 4
 
 typedef struct cpr_ctx cpr_ctx;
 typedef struct cpr_batch cpr_batch;
@@ -156,10 +156,13 @@ enum cpr_episode_status {
                                  capacity (vertex ring, event heap, candidate lists, frontier,
                                  Tailstorm brute-force budget) was exceeded; the episode's
                                  outputs are not valid */
-  CPR_ST_REFERENCE_RAISES = 64u /* Tailstorm: the reference raises an exception at this point
+  CPR_ST_REFERENCE_RAISES = 64u, /* Tailstorm: the reference raises an exception at this point
                                  (List.for_all2 in summary dedup, Division_by_zero in
                                  n_choose_k, assert false in heuristic_quorum); the episode
                                  stops, outputs not valid */
+  CPR_ST_TRACE_MISS = 128u      /* cpr_replay: the episode needed a draw its trace does not
+                                 hold (too few activations, a missing delay key); outputs
+                                 not valid */
 };
 
 typedef struct cpr_config {
@@ -233,6 +236,37 @@ typedef struct cpr_step_info {
   int32_t* head_miner;
 } cpr_step_info;
 
+/* An exported activation/delay trace: every random draw of n_episodes
+ * episodes, addressed by the coordinates of the keyed stream, so an episode replays
+ * bit-exactly on any engine that consumes the same draws. Arrays are CSR over episodes
+ * (x_offset has n_episodes + 1 entries, x_offset[0] = 0); all host pointers.
+ *   act_miner[j], act_delay[j]  activation j's miner (the alias sample over compute shares,
+ *                               distributions.ml:143-196 via simulator.ml:465-472) and the
+ *                               exponential delay drawn when clock j is scheduled
+ *                               (simulator.ml:170-173; j = 0 is the first clock)
+ *   pow_hash[s]                 30-bit Random.bits of vertex serial s (simulator.ml:123);
+ *                               B_k and Tailstorm only (may be empty otherwise)
+ *   link_key[i], link_delay[i]  message delays drawn at Network Tx (simulator.ml:481-487),
+ *                               keys ascending per episode:
+ *                               Nakamoto, Ethereum: (kw << 32) | (off << 12) | dest with
+ *                                 kw = activations when the share happened, off = the
+ *                                 message's position in that share's order
+ *                               B_k, Tailstorm: (serial << 32) | dest
+ * Traces come from the CPU oracle (tests/oracle_py.py export_traces; with the OCaml 4.12
+ * Random replica it records the reference's own stream) or from an instrumented OCaml
+ * Simulator. */
+typedef struct cpr_trace {
+  int64_t n_episodes;
+  const int64_t* act_offset;
+  const int32_t* act_miner;
+  const double* act_delay;
+  const int64_t* pow_offset;
+  const int32_t* pow_hash;
+  const int64_t* link_offset;
+  const uint64_t* link_key;
+  const double* link_delay;
+} cpr_trace;
+
 const char* cpr_version(void);
 int cpr_abi_version(void);
 const char* cpr_last_error(void);
@@ -257,6 +291,14 @@ int cpr_run_episodes(cpr_batch* b, int64_t n_episodes, uint64_t first_episode,
 int cpr_run_episodes_async(cpr_batch* b, int64_t n_episodes, uint64_t first_episode,
                            cpr_summary* summary_dev, cpr_episode_record* records_dev);
 int cpr_synchronize(cpr_ctx* ctx);
+/* Replay trace episodes [0, trace->n_episodes) on the device with the batch's protocol,
+ * mode and policy (fused episodes, like cpr_run_episodes, drawing from the trace instead
+ * of the keyed stream); records[e] is trace episode e. summary (host) is accumulated (+=).
+ * records: NULL or n_episodes records (device pointer if records_on_device != 0).
+ * Replaces nothing in the reference directly: it is the cross-engine check the north star
+ * asks for (same exported trace -> same per-episode outcomes). Synchronous. */
+int cpr_replay(cpr_batch* b, const cpr_trace* trace, cpr_summary* summary,
+               cpr_episode_record* records, int records_on_device);
 /* device time (HIP events on the context's stream) of the last episode-kernel launch of
  * this batch, and the activations it simulated (valid after cpr_run_episodes returns) */
 int cpr_last_launch(cpr_batch* b, double* kernel_ms, int64_t* activations);

@@ -475,10 +475,11 @@ Kind GymBk::skip_to_interaction(Block** blk) {
 
 static std::unique_ptr<SimRng> make_bk_rng(int rng_mode, OcamlRandom* oc, uint64_t seed,
                                            uint64_t ep, const Network& net) {
-  if (rng_mode == 0) return std::unique_ptr<SimRng>(new OcamlSimRng(oc, net));
+  if (rng_mode == 0)
+    return trace_wrap(std::unique_ptr<SimRng>(new OcamlSimRng(oc, net)), net, true);
   auto* r = new KeyedSimRng(seed, ep, net);
   r->serial_links = true;
-  return std::unique_ptr<SimRng>(r);
+  return trace_wrap(std::unique_ptr<SimRng>(r), net, true);
 }
 
 void GymBk::init() {

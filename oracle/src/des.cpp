@@ -247,6 +247,107 @@ double KeyedSimRng::link_delay(const Link& l, const Block* m) {
   return 0.0;
 }
 
+// ---------------------------------------------------------------- traces
+
+thread_local TraceHook g_trace;
+
+uint64_t trace_link_key(uint32_t kw, uint32_t off, uint32_t dest) {
+  return ((uint64_t)kw << 32) | ((uint64_t)(off & 0xFFFFFu) << 12) | (uint64_t)(dest & 0xFFFu);
+}
+uint64_t trace_msg_key(uint32_t serial, uint32_t dest) {
+  return ((uint64_t)serial << 32) | (uint64_t)(dest & 0xFFFu);
+}
+
+namespace {
+
+template <class T>
+void put(std::vector<T>& v, int i, T x, T fill) {
+  if ((int)v.size() <= i) v.resize(i + 1, fill);
+  v[i] = x;
+}
+
+uint64_t msg_key_of(const Link& l, const Block* m, bool serial_links) {
+  return serial_links ? trace_msg_key((uint32_t)m->serial, (uint32_t)l.dest)
+                      : trace_link_key((uint32_t)m->share_k, (uint32_t)m->share_off,
+                                       (uint32_t)l.dest);
+}
+
+// every draw of `inner`, logged by coordinate (a re-draw at the same coordinate, as when
+// the gym's reset runs Simulator.init twice, overwrites)
+struct RecordingSimRng : SimRng {
+  std::unique_ptr<SimRng> inner;
+  TraceBuf* buf;
+  bool serial_links;
+  int miner(int k) override {
+    const int m = inner->miner(k);
+    put<int32_t>(buf->miner, k, m, 0);
+    return m;
+  }
+  double act_delay(int j) override {
+    const double x = inner->act_delay(j);
+    put<double>(buf->delay, j, x, 0.0);
+    return x;
+  }
+  int32_t pow_bits(int serial) override {
+    const int32_t p = inner->pow_bits(serial);
+    put<int32_t>(buf->pow, serial, p, 0);
+    return p;
+  }
+  double link_delay(const Link& l, const Block* m) override {
+    const double x = inner->link_delay(l, m);
+    if (l.kind != D_CONST) buf->link[msg_key_of(l, m, serial_links)] = x;
+    return x;
+  }
+};
+
+struct ReplaySimRng : SimRng {
+  TraceBuf* buf;
+  bool serial_links;
+  int miner(int k) override {
+    if (k < (int)buf->miner.size()) return buf->miner[k];
+    buf->miss = 1;
+    return 0;
+  }
+  double act_delay(int j) override {
+    if (j < (int)buf->delay.size()) return buf->delay[j];
+    buf->miss = 1;
+    return 1.0;
+  }
+  int32_t pow_bits(int serial) override {
+    if (serial < (int)buf->pow.size()) return buf->pow[serial];
+    buf->miss = 1;
+    return 0;
+  }
+  double link_delay(const Link& l, const Block* m) override {
+    if (l.kind == D_CONST) return l.a;
+    auto it = buf->link.find(msg_key_of(l, m, serial_links));
+    if (it != buf->link.end()) return it->second;
+    buf->miss = 1;
+    return 0.0;
+  }
+};
+
+}  // namespace
+
+std::unique_ptr<SimRng> trace_wrap(std::unique_ptr<SimRng> inner, const Network& net,
+                                   bool serial_links) {
+  if (g_trace.mode == TRACE_RECORD) {
+    auto* r = new RecordingSimRng();
+    r->inner = g_trace.ocaml ? std::unique_ptr<SimRng>(new OcamlSimRng(g_trace.ocaml, net))
+                             : std::move(inner);
+    r->buf = g_trace.buf;
+    r->serial_links = serial_links;
+    return std::unique_ptr<SimRng>(r);
+  }
+  if (g_trace.mode == TRACE_REPLAY) {
+    auto* r = new ReplaySimRng();
+    r->buf = g_trace.buf;
+    r->serial_links = serial_links;
+    return std::unique_ptr<SimRng>(r);
+  }
+  return inner;
+}
+
 // ---------------------------------------------------------------- Simulator
 
 Sim::Sim(const Network& net_, SimRng* rng_) : net(net_), rng(rng_) {
@@ -793,6 +894,7 @@ void GymNakamoto::init() {
     rng.reset(new OcamlSimRng(ocaml, net));
   else
     rng.reset(new KeyedSimRng(seed, episode, net));
+  rng = trace_wrap(std::move(rng), net, false);
   sim.reset(new Sim(net, rng.get()));
   std::vector<std::unique_ptr<NodeImpl>> nodes;
   int n = (int)net.nodes.size();

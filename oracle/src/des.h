@@ -15,6 +15,7 @@
 // reference's recorded outputs) or the keyed Philox stream shared with the GPU.
 #pragma once
 #include <cstdint>
+#include <map>
 #include <memory>
 #include <string>
 #include <vector>
@@ -167,6 +168,32 @@ struct KeyedSimRng : SimRng {
   int32_t pow_bits(int serial) override;
   double link_delay(const Link& l, const Block* msg) override;
 };
+
+// ---- activation/delay traces (cpr_trace, include/cpr_hip.h)
+// One episode's draws addressed by keyed-stream coordinates: activation j's miner and
+// clock delay, vertex serial s's pow bits, message delays by link key (kw, off, dest) or,
+// for B_k / Tailstorm, by message key (serial, dest). Constant-delay links draw nothing.
+struct TraceBuf {
+  std::vector<int32_t> miner;
+  std::vector<double> delay;
+  std::vector<int32_t> pow;
+  std::map<uint64_t, double> link;
+  uint32_t miss = 0;  // replay: a draw the trace does not hold
+};
+enum { TRACE_OFF = 0, TRACE_RECORD = 1, TRACE_REPLAY = 2 };
+// per-thread hook consulted wherever an episode builds its SimRng: RECORD wraps the rng
+// (or, with `ocaml` set, an OcamlSimRng on that shared state) and logs every draw into
+// `buf`; REPLAY draws from `buf` instead
+struct TraceHook {
+  int mode = TRACE_OFF;
+  TraceBuf* buf = nullptr;
+  OcamlRandom* ocaml = nullptr;
+};
+extern thread_local TraceHook g_trace;
+uint64_t trace_link_key(uint32_t kw, uint32_t off, uint32_t dest);
+uint64_t trace_msg_key(uint32_t serial, uint32_t dest);
+std::unique_ptr<SimRng> trace_wrap(std::unique_ptr<SimRng> inner, const Network& net,
+                                   bool serial_links);
 
 struct Sim;
 

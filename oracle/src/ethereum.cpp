@@ -361,6 +361,7 @@ void GymEthereum::init() {
     rng.reset(new OcamlSimRng(ocaml, net));
   else
     rng.reset(new KeyedSimRng(seed, episode, net));
+  rng = trace_wrap(std::move(rng), net, false);
   sim.reset(new Sim(net, rng.get()));
   sim->proto = 1;
   sim->eth_scheme = scheme;
@@ -457,6 +458,7 @@ void eth_two_agents_task(int rng_mode, OcamlRandom* r, uint64_t seed, uint64_t e
     rng.reset(new OcamlSimRng(r, net));
   else
     rng.reset(new KeyedSimRng(seed, episode, net));
+  rng = trace_wrap(std::move(rng), net, false);
   Sim sim(net, rng.get());
   sim.proto = 1;
   sim.eth_scheme = scheme;

@@ -82,6 +82,7 @@ int oracle_two_agents_task(int rng_mode, void* rng, uint64_t seed, uint64_t epis
       r.reset(new OcamlSimRng((OcamlRandom*)rng, net));
     else
       r.reset(new KeyedSimRng(seed, episode, net));
+    r = trace_wrap(std::move(r), net, false);
     Sim sim(net, r.get());
     std::vector<std::unique_ptr<NodeImpl>> nodes;
     auto* att = new NakSszAttackerNode();
@@ -774,6 +775,121 @@ int oracle_ts_loop(int net_kind, int n_nodes, double alpha, double activation_de
     set_err(e.what());
     return -1;
   }
+}
+
+// ---------------- activation/delay traces (cpr_trace)
+// Record: run episodes [first, first + n) of config c in order on this thread with every
+// draw logged by keyed coordinate. rng_mode 1 draws from the keyed stream; rng_mode 0
+// from the OCaml Random state `rng`, carried from episode to episode like one Parany
+// worker (the reference's own stream). Returns a handle (NULL on error).
+struct TraceSet {
+  std::vector<TraceBuf> eps;
+};
+
+static TablePolicy table_of(const cpr_config* c) {
+  TablePolicy tab;
+  if (c->protocol == CPR_PROTO_NAKAMOTO && c->policy == POL_TABLE) {
+    tab.dim = c->policy_table_dim;
+    tab.actions.assign(c->policy_table, c->policy_table + tab.dim * tab.dim * 2);
+  }
+  return tab;
+}
+
+static int run_one(const cpr_config* c, const TablePolicy* tab, uint64_t ep,
+                   cpr_episode_record* rec) {
+  return c->mode == CPR_MODE_GYM ? run_gym_episode(c, tab, ep, rec) : run_loop_episode(c, ep, rec);
+}
+
+void* oracle_trace_record(const cpr_config* c, int rng_mode, void* rng, uint64_t first,
+                          int64_t n, cpr_episode_record* out) {
+  auto* ts = new TraceSet();
+  ts->eps.resize((size_t)n);
+  const TablePolicy tab = table_of(c);
+  int rc = 0;
+  try {
+    for (int64_t i = 0; i < n && rc == 0; i++) {
+      g_trace.mode = TRACE_RECORD;
+      g_trace.buf = &ts->eps[(size_t)i];
+      g_trace.ocaml = rng_mode == 0 ? (OcamlRandom*)rng : nullptr;
+      rc = run_one(c, &tab, first + (uint64_t)i, &out[i]);
+    }
+  } catch (std::exception& e) {
+    set_err(e.what());
+    rc = -1;
+  }
+  g_trace = TraceHook();
+  if (rc != 0) {
+    delete ts;
+    return nullptr;
+  }
+  return ts;
+}
+
+// totals: [0] activations, [1] pow hashes, [2] link delays over all episodes
+void oracle_trace_sizes(void* h, int64_t out[3]) {
+  const TraceSet* ts = (const TraceSet*)h;
+  out[0] = out[1] = out[2] = 0;
+  for (const TraceBuf& b : ts->eps) {
+    out[0] += (int64_t)b.delay.size();
+    out[1] += (int64_t)b.pow.size();
+    out[2] += (int64_t)b.link.size();
+  }
+}
+
+// CSR arrays of cpr_trace; activation arrays have one entry per act_delay draw (the last
+// clock of an episode is scheduled but never fires: its miner entry is 0)
+void oracle_trace_fill(void* h, int64_t* act_off, int32_t* miner, double* delay, int64_t* pow_off,
+                       int32_t* pow, int64_t* link_off, uint64_t* key, double* ldelay) {
+  const TraceSet* ts = (const TraceSet*)h;
+  int64_t a = 0, p = 0, l = 0;
+  act_off[0] = pow_off[0] = link_off[0] = 0;
+  for (size_t e = 0; e < ts->eps.size(); e++) {
+    const TraceBuf& b = ts->eps[e];
+    for (size_t j = 0; j < b.delay.size(); j++, a++) {
+      delay[a] = b.delay[j];
+      miner[a] = j < b.miner.size() ? b.miner[j] : 0;
+    }
+    for (size_t j = 0; j < b.pow.size(); j++) pow[p++] = b.pow[j];
+    for (const auto& kv : b.link) {
+      key[l] = kv.first;
+      ldelay[l++] = kv.second;
+    }
+    act_off[e + 1] = a;
+    pow_off[e + 1] = p;
+    link_off[e + 1] = l;
+  }
+}
+
+void oracle_trace_free(void* h) { delete (TraceSet*)h; }
+
+// Replay: trace episode e drives record out[e]; out[e].status gets CPR_ST_TRACE_MISS when
+// the episode needed a draw the trace lacks
+int oracle_trace_replay(const cpr_config* c, const cpr_trace* t, cpr_episode_record* out) {
+  const TablePolicy tab = table_of(c);
+  int rc = 0;
+  try {
+    for (int64_t e = 0; e < t->n_episodes && rc == 0; e++) {
+      TraceBuf b;
+      for (int64_t i = t->act_offset[e]; i < t->act_offset[e + 1]; i++) {
+        b.miner.push_back(t->act_miner[i]);
+        b.delay.push_back(t->act_delay[i]);
+      }
+      for (int64_t i = t->pow_offset[e]; i < t->pow_offset[e + 1]; i++)
+        b.pow.push_back(t->pow_hash[i]);
+      for (int64_t i = t->link_offset[e]; i < t->link_offset[e + 1]; i++)
+        b.link[t->link_key[i]] = t->link_delay[i];
+      g_trace.mode = TRACE_REPLAY;
+      g_trace.buf = &b;
+      g_trace.ocaml = nullptr;
+      rc = run_one(c, &tab, (uint64_t)e, &out[e]);
+      if (b.miss) out[e].status |= CPR_ST_TRACE_MISS;
+    }
+  } catch (std::exception& e) {
+    set_err(e.what());
+    rc = -1;
+  }
+  g_trace = TraceHook();
+  return rc;
 }
 
 // threads: number of worker threads (episode-parallel, like Parany workers)

@@ -67,6 +67,13 @@ def lib():
         L.oracle_gym_diag.restype = ctypes.c_uint32
         L.oracle_run_episodes.argtypes = [P(C.Config), ctypes.c_uint64, ctypes.c_int64, vp,
                                           ctypes.c_int]
+        L.oracle_trace_record.restype = vp
+        L.oracle_trace_record.argtypes = [P(C.Config), ctypes.c_int, vp, ctypes.c_uint64,
+                                          ctypes.c_int64, vp]
+        L.oracle_trace_sizes.argtypes = [vp, vp]
+        L.oracle_trace_fill.argtypes = [vp] + [vp] * 8
+        L.oracle_trace_free.argtypes = [vp]
+        L.oracle_trace_replay.argtypes = [P(C.Config), P(C.CTrace), vp]
         L.oracle_ocaml_sort_ints.argtypes = [vp, ctypes.c_int]
         L.oracle_ocaml_sort_pairs.argtypes = [vp, vp, ctypes.c_int]
         L.oracle_at_most_first_ints.argtypes = [vp, ctypes.c_int, ctypes.c_int]
@@ -237,6 +244,43 @@ def run_episodes(config, first, n, threads=1):
 
     rec = np.zeros(n, dtype=C.RECORD_DTYPE)
     check(lib().oracle_run_episodes(ctypes.byref(config), first, n, rec.ctypes.data, threads))
+    return rec
+
+
+def export_traces(config, first, n, rng=None):
+    """Run episodes [first, first + n) of `config` in the oracle, logging every draw:
+    returns (cpr_amd._lib.Trace, records). rng=None draws from the keyed stream; an
+    OcamlRandom draws from that OCaml 4.12 Random state, carried over the episodes in
+    order (the reference's own stream, as one Parany worker would)."""
+    from cpr_amd import _lib as C
+
+    rec = np.zeros(n, dtype=C.RECORD_DTYPE)
+    h = lib().oracle_trace_record(ctypes.byref(config), 0 if rng is not None else 1,
+                                  rng.h if rng is not None else None, first, n, rec.ctypes.data)
+    if not h:
+        raise RuntimeError(lib().oracle_last_error().decode())
+    try:
+        sz = np.zeros(3, dtype=np.int64)
+        lib().oracle_trace_sizes(h, sz.ctypes.data)
+        a = {
+            "act_offset": np.zeros(n + 1, np.int64), "act_miner": np.zeros(sz[0], np.int32),
+            "act_delay": np.zeros(sz[0], np.float64), "pow_offset": np.zeros(n + 1, np.int64),
+            "pow_hash": np.zeros(sz[1], np.int32), "link_offset": np.zeros(n + 1, np.int64),
+            "link_key": np.zeros(sz[2], np.uint64), "link_delay": np.zeros(sz[2], np.float64),
+        }
+        lib().oracle_trace_fill(h, *[a[k].ctypes.data for k, _ in C.Trace.ARRAYS])
+    finally:
+        lib().oracle_trace_free(h)
+    return C.Trace(**a), rec
+
+
+def replay(config, trace):
+    """The oracle driven by a trace instead of a generator; record e = trace episode e."""
+    from cpr_amd import _lib as C
+
+    rec = np.zeros(trace.n_episodes, dtype=C.RECORD_DTYPE)
+    ct = trace.ctrace()
+    check(lib().oracle_trace_replay(ctypes.byref(config), ctypes.byref(ct), rec.ctypes.data))
     return rec
 
 
