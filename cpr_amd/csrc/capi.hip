@@ -64,6 +64,7 @@ struct cpr_batch {
   NakParams P;
   eth::EthParams EP;     // CPR_PROTO_ETHEREUM
   DevBuf eth_mem;        // lanes x eth_lane_bytes
+  bool is_eth = false;   // Ethereum lockstep lanes share bk_lmem / bk_slots
   int64_t eth_bytes = 0;
   bk::BkParams BP;       // CPR_PROTO_BK
   DevBuf bk_mem;         // fused episodes: lanes x bk_bytes
@@ -468,6 +469,7 @@ int cpr_batch_create(cpr_ctx* ctx, const cpr_config* cfg, cpr_batch** out) {
   if (cfg->protocol == CPR_PROTO_BK) b->bk_bytes = bk::bk_lane_bytes(BP);
   if (cfg->protocol == CPR_PROTO_TAILSTORM) b->bk_bytes = ts::ts_lane_bytes(TP);
   b->is_ev = cfg->protocol == CPR_PROTO_BK || cfg->protocol == CPR_PROTO_TAILSTORM;
+  b->is_eth = cfg->protocol == CPR_PROTO_ETHEREUM;
   b->cfg.policy_table = nullptr;
   if (cfg->protocol == CPR_PROTO_BK && cfg->policy == CPR_BK_POLICY_TABLE) {
     const size_t D = (size_t)cfg->policy_table_dim, K1 = (size_t)cfg->k + 1;
@@ -795,13 +797,17 @@ static int ensure_common_lockstep(cpr_batch* b, int obs_len) {
   return CPR_OK;
 }
 
+// per-lane region bytes of the event-engine lockstep lanes (B_k, Tailstorm, Ethereum)
+static int64_t ev_lane_bytes(const cpr_batch* b) { return b->is_eth ? b->eth_bytes : b->bk_bytes; }
+
 static int ensure_lockstep_bk(cpr_batch* b) {
   const int64_t n = b->cfg.n_lanes;
   if (n <= 0) return fail(CPR_E_STATE, "batch has no lockstep lanes (cfg.n_lanes = 0)");
   if (b->cfg.mode != CPR_MODE_GYM) return fail(CPR_E_STATE, "lockstep lanes need CPR_MODE_GYM");
   if (!b->bk_slots.p) {
-    HIP_TRY(b->bk_lmem.ensure((size_t)n * (size_t)b->bk_bytes));
-    const size_t sb = b->cfg.protocol == CPR_PROTO_TAILSTORM ? ts_slot_bytes() : bk_slot_bytes();
+    HIP_TRY(b->bk_lmem.ensure((size_t)n * (size_t)ev_lane_bytes(b)));
+    const size_t sb = b->is_eth ? eth_slot_bytes()
+                      : b->cfg.protocol == CPR_PROTO_TAILSTORM ? ts_slot_bytes() : bk_slot_bytes();
     HIP_TRY(b->bk_slots.ensure((size_t)n * sb));
     HIP_TRY(hipMemsetAsync(b->bk_slots.p, 0, (size_t)n * sb, b->ctx->stream));
   }
@@ -809,9 +815,7 @@ static int ensure_lockstep_bk(cpr_batch* b) {
 }
 
 static int ensure_lockstep(cpr_batch* b) {
-  if (b->is_ev) return ensure_lockstep_bk(b);
-  if (b->cfg.protocol != CPR_PROTO_NAKAMOTO)
-    return fail(CPR_E_UNSUPPORTED, "lockstep lanes are implemented for Nakamoto and B_k");
+  if (b->is_ev || b->is_eth) return ensure_lockstep_bk(b);
   const int64_t n = b->cfg.n_lanes;
   if (n <= 0) return fail(CPR_E_STATE, "batch has no lockstep lanes (cfg.n_lanes = 0)");
   if (b->cfg.mode != CPR_MODE_GYM) return fail(CPR_E_STATE, "lockstep lanes need CPR_MODE_GYM");
@@ -863,7 +867,11 @@ int cpr_reset(cpr_batch* b, const uint8_t* mask, const uint64_t* eps, double* ob
   }
   const double* tabs = (const double*)b->tabs_dev.p;
   const int ol = obs_len_of(b->cfg);
-  if (b->cfg.protocol == CPR_PROTO_BK)
+  if (b->is_eth)
+    HIP_TRY(launch_eth_reset(b->EP, b->cfg.seed, (uint8_t*)b->bk_lmem.p, b->eth_bytes,
+                             b->bk_slots.p, n, dmask, deps, b->cfg.unit_observation, tabs,
+                             b->tab_n, (double*)b->l_obs.p, st));
+  else if (b->cfg.protocol == CPR_PROTO_BK)
     HIP_TRY(launch_bk_reset(b->BP, b->cfg.seed, (uint8_t*)b->bk_lmem.p, b->bk_bytes,
                             b->bk_slots.p, n, dmask, deps, b->cfg.unit_observation, tabs,
                             b->tab_n, (double*)b->l_obs.p, st));
@@ -886,7 +894,7 @@ int cpr_step(cpr_batch* b, const int32_t* actions, double* obs, double* reward, 
   if (!b || !actions || !obs || !reward || !done) return fail(CPR_E_INVALID_ARG, "NULL argument");
   if (!b->reset_done) return fail(CPR_E_STATE, "step before reset");
   const int64_t n = b->cfg.n_lanes;
-  const int n_act = b->is_ev ? 8 : 4;
+  const int n_act = b->is_eth ? 24 : b->is_ev ? 8 : 4;
   const int ol = obs_len_of(b->cfg);
   for (int64_t i = 0; i < n; i++)
     if (actions[i] < 0 || actions[i] >= n_act)
@@ -909,7 +917,11 @@ int cpr_step(cpr_batch* b, const int32_t* actions, double* obs, double* reward, 
   sb.hh = (int32_t*)(ib + 7 * n * 8);
   sb.hm = (int32_t*)(ib + 7 * n * 8 + n * 4);
   const double* tabs = (const double*)b->tabs_dev.p;
-  if (b->cfg.protocol == CPR_PROTO_BK)
+  if (b->is_eth)
+    HIP_TRY(launch_eth_step(b->EP, b->cfg.seed, (uint8_t*)b->bk_lmem.p, b->eth_bytes,
+                            b->bk_slots.p, n, (const int32_t*)b->l_act.p,
+                            b->cfg.unit_observation, tabs, b->tab_n, sb, st));
+  else if (b->cfg.protocol == CPR_PROTO_BK)
     HIP_TRY(launch_bk_step(b->BP, b->cfg.seed, (uint8_t*)b->bk_lmem.p, b->bk_bytes,
                            b->bk_slots.p, n, (const int32_t*)b->l_act.p,
                            b->cfg.unit_observation, tabs, b->tab_n, sb, st));
@@ -942,8 +954,6 @@ int cpr_step(cpr_batch* b, const int32_t* actions, double* obs, double* reward, 
 
 int cpr_observe_fields(cpr_batch* b, int32_t* fields) {
   if (!b || !fields) return fail(CPR_E_INVALID_ARG, "NULL argument");
-  if (b->cfg.protocol == CPR_PROTO_ETHEREUM)
-    return fail(CPR_E_UNSUPPORTED, "lockstep lanes are implemented for Nakamoto, B_k, Tailstorm");
   if (!b->reset_done) return fail(CPR_E_STATE, "observe before reset");
   const int64_t n = b->cfg.n_lanes;
   HIP_TRY(hipSetDevice(b->ctx->device));
@@ -951,7 +961,10 @@ int cpr_observe_fields(cpr_batch* b, int32_t* fields) {
   const size_t per = (size_t)obs_len_of(b->cfg) * 4;
   DevBuf tmp;
   HIP_TRY(tmp.ensure((size_t)n * per));
-  if (b->cfg.protocol == CPR_PROTO_BK)
+  if (b->is_eth)
+    HIP_TRY(launch_eth_observe_fields(b->EP, (uint8_t*)b->bk_lmem.p, b->eth_bytes, b->bk_slots.p,
+                                      n, (int32_t*)tmp.p, st));
+  else if (b->cfg.protocol == CPR_PROTO_BK)
     HIP_TRY(launch_bk_observe_fields(b->BP, (uint8_t*)b->bk_lmem.p, b->bk_bytes, b->bk_slots.p,
                                      n, (int32_t*)tmp.p, st));
   else if (b->cfg.protocol == CPR_PROTO_TAILSTORM)
@@ -1002,8 +1015,24 @@ int cpr_policy_actions(cpr_batch* b, int32_t policy, const double* obs, int64_t 
     HIP_TRY(hipStreamSynchronize(st));
     return CPR_OK;
   }
+  if (b->is_eth) {
+    if (policy < 0 || policy > CPR_ETH_POLICY_FN19PKEL)
+      return fail(CPR_E_INVALID_ARG, "unknown policy");
+    if (n <= 0) return CPR_OK;
+    HIP_TRY(hipSetDevice(b->ctx->device));
+    hipStream_t st = b->ctx->stream;
+    DevBuf o, a;
+    HIP_TRY(o.ensure((size_t)n * 80));
+    HIP_TRY(a.ensure((size_t)n * 4));
+    HIP_TRY(hipMemcpyAsync(o.p, obs, (size_t)n * 80, hipMemcpyHostToDevice, st));
+    HIP_TRY(launch_eth_policy(policy, b->cfg.unit_observation, (const double*)o.p, n,
+                              (int32_t*)a.p, st));
+    HIP_TRY(hipMemcpyAsync(actions, a.p, (size_t)n * 4, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    return CPR_OK;
+  }
   if (b->cfg.protocol != CPR_PROTO_NAKAMOTO)
-    return fail(CPR_E_UNSUPPORTED, "policy evaluation on encoded observations: Nakamoto and B_k");
+    return fail(CPR_E_UNSUPPORTED, "policy evaluation on encoded observations");
   if (policy < 0 || policy > CPR_POLICY_TABLE) return fail(CPR_E_INVALID_ARG, "unknown policy");
   if (policy == CPR_POLICY_TABLE && b->table_host.empty())
     return fail(CPR_E_INVALID_ARG, "batch has no policy table");
@@ -1152,8 +1181,8 @@ const char* cpr_policy_name(int32_t protocol, int32_t index, int32_t* policy_id)
 int cpr_rollout(cpr_batch* b, int64_t n_steps, double* obs, double* reward, uint8_t* done,
                 int outputs_on_device, cpr_summary* summary) {
   if (!b || !summary) return fail(CPR_E_INVALID_ARG, "NULL argument");
-  if (!b->is_ev)
-    return fail(CPR_E_UNSUPPORTED, "cpr_rollout is implemented for B_k and Tailstorm");
+  if (!b->is_ev && !b->is_eth)
+    return fail(CPR_E_UNSUPPORTED, "cpr_rollout is implemented for Ethereum, B_k and Tailstorm");
   if (n_steps <= 0) return CPR_OK;
   HIP_TRY(hipSetDevice(b->ctx->device));
   int rc = ensure_lockstep(b);
@@ -1187,7 +1216,12 @@ int cpr_rollout(cpr_batch* b, int64_t n_steps, double* obs, double* reward, uint
   }
   const double* tabs = (const double*)b->tabs_dev.p;
   HIP_TRY(hipEventRecord(b->ev0, st));
-  if (b->cfg.protocol == CPR_PROTO_TAILSTORM)
+  if (b->is_eth)
+    HIP_TRY(launch_eth_rollout(b->EP, b->cfg.seed, (uint8_t*)b->bk_lmem.p, b->eth_bytes,
+                               b->bk_slots.p, b->cfg.n_lanes, n_steps, b->cfg.unit_observation,
+                               tabs, b->tab_n, obs_dev, reward_dev, done_dev,
+                               (cpr_summary*)b->summary.p, st));
+  else if (b->cfg.protocol == CPR_PROTO_TAILSTORM)
     HIP_TRY(launch_ts_rollout(b->TP, b->cfg.seed, (uint8_t*)b->bk_lmem.p, b->bk_bytes,
                               b->bk_slots.p, b->cfg.n_lanes, n_steps, b->cfg.unit_observation,
                               tabs, b->tab_n, obs_dev, reward_dev, done_dev,

@@ -75,6 +75,24 @@ hipError_t launch_eth_replay_episodes(const eth::EthParams& P, const TraceSource
                                  uint8_t* mem, int64_t lane_bytes, int64_t lanes,
                                  cpr_episode_record* recs, cpr_summary* sum, hipStream_t st);
 int eth_blocks_per_cu();
+// Ethereum lockstep lanes: mem = n x lane_bytes; slots = n x eth_slot_bytes()
+hipError_t launch_eth_reset(const eth::EthParams& P, uint64_t seed, uint8_t* mem,
+                            int64_t lane_bytes, void* slots, int64_t n, const uint8_t* mask,
+                            const uint64_t* eps, int unit, const double* tabs, int32_t tn,
+                            double* obs, hipStream_t st);
+hipError_t launch_eth_step(const eth::EthParams& P, uint64_t seed, uint8_t* mem,
+                           int64_t lane_bytes, void* slots, int64_t n, const int32_t* actions,
+                           int unit, const double* tabs, int32_t tn, const StepBuffers& b,
+                           hipStream_t st);
+hipError_t launch_eth_rollout(const eth::EthParams& P, uint64_t seed, uint8_t* mem,
+                              int64_t lane_bytes, void* slots, int64_t n, int64_t n_steps,
+                              int unit, const double* tabs, int32_t tn, double* obs,
+                              double* reward, uint8_t* done, cpr_summary* sum, hipStream_t st);
+hipError_t launch_eth_observe_fields(const eth::EthParams& P, uint8_t* mem, int64_t lane_bytes,
+                                     const void* slots, int64_t n, int32_t* f, hipStream_t st);
+hipError_t launch_eth_policy(int32_t policy, int unit, const double* obs, int64_t n,
+                             int32_t* actions, hipStream_t st);
+size_t eth_slot_bytes();
 
 // B_k (kernels_bk.hip): mem = lanes x lane_bytes; lockstep slots = n x bk_slot_bytes()
 hipError_t launch_bk_run_episodes(const bk::BkParams& P, uint64_t seed, uint64_t first,

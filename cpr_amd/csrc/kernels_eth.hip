@@ -91,4 +91,252 @@ int eth_blocks_per_cu() {
   return blocks;
 }
 
+// ---------------------------------------------------------------- lockstep gym lanes
+// engine.ml reset/step with host actions (cpr_reset / cpr_step) and the on-device rollout,
+// one lane region of eth_lane_bytes per env; reward = Δ head.rewards[0] (engine.ml:223)
+struct EthSlot {
+  eth::EthLane L;
+  uint64_t ep;
+  double last_ra;
+  int32_t live;
+};
+
+// ethereum_ssz.ml:43-56 normalizers through ssz_tools.ml NormalizeObs.to_float; the unit
+// encodings use host-tabulated libm values (tabs = [2/pi atan(i) | 0.5 + atan(i - N)/pi],
+// i < N), the lanes' state decides the orphan fields with the three dry-run payloads
+__device__ inline void eth_write_obs(const eth::EthObs& o, int unit, const double* tabs,
+                                     int32_t tn, double* out) {
+  const int32_t v[10] = {o.public_height,  o.public_work,
+                         o.private_height, o.private_work,
+                         o.diff_height,    o.diff_work,
+                         o.public_orphans, o.private_orphans_inclusive,
+                         o.private_orphans_exclusive, o.event};
+  const double pi = 3.141592653589793;
+  for (int j = 0; j < 10; ++j) {
+    const int32_t x = v[j];
+    if (!unit || j == 9) {
+      out[j] = (double)x;
+    } else if (j == 4 || j == 5) {
+      out[j] = (x > -tn && x < tn) ? tabs[2 * tn + x] : 0.5 + (1.0 / pi * atan((double)x / 1.0));
+    } else {
+      out[j] = x < tn ? tabs[x] : 2.0 / pi * atan((double)x / 1.0);
+    }
+  }
+}
+
+__device__ inline void eth_slot_reset(const eth::EthParams& P, uint64_t seed, const eth::EthMem& M,
+                                      EthSlot& SL, uint64_t ep) {
+  SL.ep = ep;
+  SL.last_ra = 0.0;
+  SL.live = 1;
+  SL.L.gym_reset(P, make_stream(seed, ep), M);
+}
+
+__device__ inline eth::EthMem eth_lane_mem(const eth::EthParams& P, uint8_t* mem,
+                                           int64_t lane_bytes, int64_t i) {
+  return eth::eth_mem_at(mem + i * lane_bytes, P.cap_b, P.cap_e, P.n);
+}
+
+__global__ __launch_bounds__(kBlock) void k_eth_reset(eth::EthParams P, uint64_t seed,
+                                                       uint8_t* mem, int64_t lane_bytes,
+                                                       EthSlot* slots, int64_t n,
+                                                       const uint8_t* mask, const uint64_t* eps,
+                                                       int unit, const double* tabs, int32_t tn,
+                                                       double* obs) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const eth::EthMem M = eth_lane_mem(P, mem, lane_bytes, i);
+  EthSlot SL = slots[i];
+  if (mask == nullptr || mask[i]) eth_slot_reset(P, seed, M, SL, eps ? eps[i] : (uint64_t)i);
+  eth_write_obs(SL.L.observe(P, M, true), unit, tabs, tn, obs + 10 * i);
+  slots[i] = SL;
+}
+
+__device__ inline void eth_info(const eth::EthParams& P, const eth::EthMem& M, EthSlot& SL,
+                                int32_t hd, int64_t i, const StepBuffers& out) {
+  const eth::EBlock& h = SL.L.B(P, M, hd);
+  out.era[i] = (double)h.rew_att / 32.0;
+  out.erd[i] = (double)h.rew_def / 32.0;
+  out.eprog[i] = (double)h.work;
+  out.ect[i] = h.time;
+  out.est[i] = SL.L.now;
+  out.esteps[i] = SL.L.steps;
+  out.eacts[i] = SL.L.c_act;
+  out.hh[i] = h.height;
+  out.hm[i] = h.miner;
+}
+
+__global__ __launch_bounds__(kBlock) void k_eth_step(eth::EthParams P, uint64_t seed,
+                                                      uint8_t* mem, int64_t lane_bytes,
+                                                      EthSlot* slots, int64_t n,
+                                                      const int32_t* actions, int unit,
+                                                      const double* tabs, int32_t tn,
+                                                      StepBuffers out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const eth::EthMem M = eth_lane_mem(P, mem, lane_bytes, i);
+  EthSlot SL = slots[i];
+  bool done = false;
+  const int32_t hd = SL.L.gym_step(P, make_stream(seed, SL.ep), M, actions[i], &done);
+  const double ra = (double)SL.L.B(P, M, hd).rew_att / 32.0;
+  out.reward[i] = ra - SL.last_ra;  // engine.ml:223
+  out.done[i] = done ? 1 : 0;
+  if (out.era) eth_info(P, M, SL, hd, i, out);
+  SL.last_ra = ra;
+  eth_write_obs(SL.L.observe(P, M, true), unit, tabs, tn, out.obs + 10 * i);
+  slots[i] = SL;
+}
+
+// n_steps lockstep steps per lane with the batch policy on the device, VecEnv auto-reset
+// (episode id + n), as k_bk_rollout
+__global__ __launch_bounds__(kBlock) void k_eth_rollout(eth::EthParams P, uint64_t seed,
+                                                         uint8_t* mem, int64_t lane_bytes,
+                                                         EthSlot* slots, int64_t n,
+                                                         int64_t n_steps, int unit,
+                                                         const double* tabs, int32_t tn,
+                                                         double* obs, double* reward,
+                                                         uint8_t* done_out, cpr_summary* sum) {
+  __shared__ int32_t hist[CPR_HIST_BINS];
+  if (threadIdx.x < CPR_HIST_BINS) hist[threadIdx.x] = 0;
+  __syncthreads();
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  Acc acc = {};
+  int64_t steps_all = 0, acts_all = 0;
+  if (i < n) {
+    const eth::EthMem M = eth_lane_mem(P, mem, lane_bytes, i);
+    EthSlot SL = slots[i];
+    if (!SL.live) {
+      eth_slot_reset(P, seed, M, SL, (uint64_t)i);
+      acts_all += SL.L.c_act;
+    }
+    for (int64_t t = 0; t < n_steps; ++t) {
+      const eth::EthObs o = SL.L.observe(P, M, false);
+      const int32_t c0 = SL.L.c_act;
+      bool done = false;
+      const int32_t hd =
+          SL.L.gym_step(P, make_stream(seed, SL.ep), M, eth::eth_policy(P.policy, o), &done);
+      acts_all += SL.L.c_act - c0;
+      ++steps_all;
+      const eth::EBlock& h = SL.L.B(P, M, hd);
+      const double ra = (double)h.rew_att / 32.0;
+      const int64_t k = t * n + i;
+      if (reward) reward[k] = ra - SL.last_ra;
+      if (done_out) done_out[k] = done ? 1 : 0;
+      SL.last_ra = ra;
+      if (done) {
+        const int32_t a = h.rew_att, d = h.rew_def;
+        const double rel = (a + d) != 0 ? (double)a / (double)(a + d) : 0.0;
+        acc_episode(acc, (int64_t)a << 15, (int64_t)d << 15, (int64_t)h.work << 20, rel,
+                    h.height, SL.L.steps, SL.L.c_act, SL.L.status, hist);
+        eth_slot_reset(P, seed, M, SL, SL.ep + (uint64_t)n);
+        acts_all += SL.L.c_act;
+      }
+      if (obs) eth_write_obs(SL.L.observe(P, M, true), unit, tabs, tn, obs + 10 * k);
+    }
+    slots[i] = SL;
+  }
+  acc.steps = steps_all;
+  acc.activations = acts_all;
+  __syncthreads();
+  block_flush(acc, hist, sum);
+}
+
+__global__ void k_eth_observe_fields(eth::EthParams P, uint8_t* mem, int64_t lane_bytes,
+                                     const EthSlot* slots, int64_t n, int32_t* f) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const eth::EthMem M = eth_lane_mem(P, mem, lane_bytes, i);
+  eth::EthLane L = slots[i].L;
+  const eth::EthObs o = L.observe(P, M, true);
+  int32_t* g = f + 10 * i;
+  g[0] = o.public_height;
+  g[1] = o.public_work;
+  g[2] = o.private_height;
+  g[3] = o.private_work;
+  g[4] = o.diff_height;
+  g[5] = o.diff_work;
+  g[6] = o.public_orphans;
+  g[7] = o.private_orphans_inclusive;
+  g[8] = o.private_orphans_exclusive;
+  g[9] = o.event;
+}
+
+// engine.ml:258-261: decode (ssz_tools.ml NormalizeObs.of_float) and apply the policy
+__global__ void k_eth_policy(int32_t policy, int unit, const double* obs, int64_t n,
+                             int32_t* actions) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const double* x = obs + 10 * i;
+  const double pi = 3.141592653589793;
+  int32_t v[10];
+  for (int j = 0; j < 10; ++j) {
+    if (j == 9)
+      v[j] = (int32_t)floor(x[j] * 1.0);
+    else if (!unit)
+      v[j] = (int32_t)x[j];
+    else if (j == 4 || j == 5)
+      v[j] = (int32_t)__builtin_round(tan(pi * (x[j] - 0.5)) * 1.0);
+    else
+      v[j] = (int32_t)__builtin_round(tan(pi / 2.0 * x[j]) * 1.0);
+  }
+  eth::EthObs o;
+  o.public_height = v[0];
+  o.public_work = v[1];
+  o.private_height = v[2];
+  o.private_work = v[3];
+  o.diff_height = v[4];
+  o.diff_work = v[5];
+  o.public_orphans = v[6];
+  o.private_orphans_inclusive = v[7];
+  o.private_orphans_exclusive = v[8];
+  o.event = v[9];
+  actions[i] = eth::eth_policy(policy, o);
+}
+
+static unsigned eth_grid_of(int64_t n) { return (unsigned)((n + kBlock - 1) / kBlock); }
+
+hipError_t launch_eth_reset(const eth::EthParams& P, uint64_t seed, uint8_t* mem,
+                            int64_t lane_bytes, void* slots, int64_t n, const uint8_t* mask,
+                            const uint64_t* eps, int unit, const double* tabs, int32_t tn,
+                            double* obs, hipStream_t st) {
+  hipLaunchKernelGGL(k_eth_reset, dim3(eth_grid_of(n)), dim3(kBlock), 0, st, P, seed, mem,
+                     lane_bytes, (EthSlot*)slots, n, mask, eps, unit, tabs, tn, obs);
+  return hipGetLastError();
+}
+
+hipError_t launch_eth_step(const eth::EthParams& P, uint64_t seed, uint8_t* mem,
+                           int64_t lane_bytes, void* slots, int64_t n, const int32_t* actions,
+                           int unit, const double* tabs, int32_t tn, const StepBuffers& b,
+                           hipStream_t st) {
+  hipLaunchKernelGGL(k_eth_step, dim3(eth_grid_of(n)), dim3(kBlock), 0, st, P, seed, mem,
+                     lane_bytes, (EthSlot*)slots, n, actions, unit, tabs, tn, b);
+  return hipGetLastError();
+}
+
+hipError_t launch_eth_rollout(const eth::EthParams& P, uint64_t seed, uint8_t* mem,
+                              int64_t lane_bytes, void* slots, int64_t n, int64_t n_steps,
+                              int unit, const double* tabs, int32_t tn, double* obs,
+                              double* reward, uint8_t* done, cpr_summary* sum, hipStream_t st) {
+  hipLaunchKernelGGL(k_eth_rollout, dim3(eth_grid_of(n)), dim3(kBlock), 0, st, P, seed, mem,
+                     lane_bytes, (EthSlot*)slots, n, n_steps, unit, tabs, tn, obs, reward, done,
+                     sum);
+  return hipGetLastError();
+}
+
+hipError_t launch_eth_observe_fields(const eth::EthParams& P, uint8_t* mem, int64_t lane_bytes,
+                                     const void* slots, int64_t n, int32_t* f, hipStream_t st) {
+  hipLaunchKernelGGL(k_eth_observe_fields, dim3(eth_grid_of(n)), dim3(kBlock), 0, st, P, mem,
+                     lane_bytes, (const EthSlot*)slots, n, f);
+  return hipGetLastError();
+}
+
+hipError_t launch_eth_policy(int32_t policy, int unit, const double* obs, int64_t n,
+                             int32_t* actions, hipStream_t st) {
+  hipLaunchKernelGGL(k_eth_policy, dim3(eth_grid_of(n)), dim3(kBlock), 0, st, policy, unit, obs,
+                     n, actions);
+  return hipGetLastError();
+}
+
+size_t eth_slot_bytes() { return sizeof(EthSlot); }
+
 }  // namespace cpr

@@ -1,7 +1,7 @@
 """Drop-in for the reference's Python module ``engine`` (simulator/gym/cpr_gym_engine.ml:
 310-436): create / reset / step / policies / to_string / n_actions / observation_low /
 observation_high over one device lane each. The episode state lives on the GPU; every
-step is one launch of the lane state machine (cpr_amd/csrc/nakamoto_lane.h).
+step is one launch of the lane state machine (cpr_amd/csrc/*_lane.h).
 
 Randomness: the reference seeds OCaml's Random with ``self_init`` at import
 (cpr_gym_engine.ml:312), so it is not reproducible. Here each ``create`` draws a fresh
@@ -38,6 +38,17 @@ _SPACES = {
                              "private_votes_inclusive", "private_votes_exclusive", "lead",
                              "event"],
                      bools=("lead",)),  # bk_ssz.ml:22-34,123-143
+    # ethereum_ssz.ml:21-41,161-263: action i = (action_list[i / 4], uncles_list[i % 4])
+    L.PROTO_ETHEREUM: dict(
+        actions=[f"{a}, uncles {{own: {o}; foreign: {f}}}"
+                 for a in ["Adopt_discard", "Adopt_release", "Override", "Match", "Release1",
+                           "Wait"]
+                 for o in ("false", "true") for f in ("false", "true")],
+        events=_EVENTS,
+        fields=["public_height", "public_work", "private_height", "private_work",
+                "diff_height", "diff_work", "public_orphans", "private_orphans_inclusive",
+                "private_orphans_exclusive", "event"],
+        bools=()),
     L.PROTO_TAILSTORM: dict(actions=_ACTION8, events=["`Append", "`ProofOfWork", "`Network"],
                             fields=["public_blocks", "private_blocks", "diff_blocks",
                                     "public_votes", "private_votes_inclusive",
@@ -191,6 +202,14 @@ def step(ienv, action):
         info["protocol_incentive_scheme"] = ienv.proto.params["reward"]
         info["head_kind"] = "block"
         info["head_height"] = int(inf["head_height"][0])
+    elif ienv.proto.protocol_id == L.PROTO_ETHEREUM:
+        # ethereum.ml:57-63 (Protocol.info, Byzantium + scheme), :92-95 (Referee.info)
+        info["protocol_preference"] = "heaviest_chain"
+        info["protocol_progress"] = "work"
+        info["protocol_max_uncles"] = "2"
+        info["protocol_incentive_scheme"] = ienv.proto.params["reward"]
+        info["head_height"] = int(inf["head_height"][0])
+        info["head_work"] = int(round(prog))
     else:
         info["protocol_family"] = "nakamoto"
         info["head_height"] = int(inf["head_height"][0])

@@ -1,7 +1,8 @@
 """Drop-in for the reference's Python module ``protocols``
 (simulator/gym/cpr_gym_engine.ml:165-304): constructors returning protocol specs that
-``engine.create`` accepts. Nakamoto, B_k and Tailstorm run as lockstep lanes on the device
-engine; the other constructors exist with the reference's signatures and raise.
+``engine.create`` accepts. Nakamoto, Ethereum, B_k and Tailstorm run as lockstep lanes on the
+device engine; the other constructors (SPar, STree, SDag, TailstormJune: outside the north
+star) exist with the reference's signatures and raise.
 """
 
 from . import _lib as L
@@ -32,15 +33,12 @@ def nakamoto(unit_observation):
 def _not_on_device(name):
     def ctor(*args, **kwargs):
         raise NotImplementedError(
-            f"protocols.{name}: the device engine implements Nakamoto only in this build "
-            "(see DESIGN.md §8, next rows: Ethereum, B_k, Tailstorm)"
+            f"protocols.{name}: not implemented by the device engine (it covers Nakamoto, "
+            "Ethereum, B_k and Tailstorm; DESIGN.md §8)"
         )
 
     ctor.__name__ = name
     return ctor
-
-
-ethereum = _not_on_device("ethereum")  # (reward, unit_observation)
 
 
 def _option(choice, value):
@@ -50,6 +48,19 @@ def _option(choice, value):
     quoted = [f"'{c}'" for c in choice]
     alts = quoted[0] if len(quoted) == 1 else ", ".join(quoted[:-1]) + " or " + quoted[-1]
     raise ValueError(f"'{value}' is not a valid parameter choice, try {alts}")
+
+
+def ethereum(reward, unit_observation):
+    """ethereum_ssz attack space over Byzantium parameters with the chosen incentive scheme
+    (cpr_gym_engine.ml:180-192, cpr_protocols.ml:39-49, ethereum.ml:19-55)."""
+    reward = _option(["constant", "discount"], reward)  # ethereum.ml:3 incentive_schemes
+    info = "SSZ'16-like attack space with %s observations" % ("unit" if unit_observation else "raw")
+    # ethereum.ml:29-55: key / description over (preference, progress, max_uncles, scheme)
+    return Protocol(f"eth-heaviest_chain-work-2-{reward}",
+                    f"Ethereum with heaviest_chain-preference, work-progress, uncle cap 2, "
+                    f"and {reward}-rewards", info, unit_observation,
+                    protocol_id=L.PROTO_ETHEREUM, reward=reward,
+                    reward_scheme=L.REWARD_DISCOUNT if reward == "discount" else L.REWARD_CONSTANT)
 
 
 def bk(reward, k, unit_observation):

@@ -84,3 +84,83 @@ def test_eth_policy_registry_and_spec(ctx):
     n_obs, n_act, lo, hi = b.observation_spec()
     assert (n_obs, n_act) == (10, 24)
     assert list(lo) == [0.0] * 10 and list(hi) == [1.0] * 10
+
+
+# ---------------------------------------------------------------- lockstep gym lanes
+
+
+def test_eth_lockstep_matches_oracle_step_by_step(ctx):
+    # engine.ml reset/step over device lanes vs the oracle's engine, every output field;
+    # random actions over all 24 (action, uncle-rule) pairs plus a policy on every third lane
+    n, steps = 16, 250
+    for unit in (True, False):
+        cfg, keep = _cfg(alpha=0.35, gamma=0.5, max_steps=steps, seed=77, n_lanes=n,
+                         reward_scheme=L.REWARD_DISCOUNT, unit_observation=unit)
+        b = device.Batch(cfg, keep=keep)
+        obs = b.reset()
+        envs = [O.EthGymEnv(cfg, episode=i) for i in range(n)]
+        ref = np.array([e.reset() for e in envs])
+        assert np.array_equal(obs, ref)
+        rnd = np.random.default_rng(1)
+        for t in range(steps):
+            acts = rnd.integers(0, 24, size=n).astype(np.int32)
+            acts[::3] = [O.eth_policy("fn19", e.fields()) for e in envs[::3]]
+            obs, rew, done, info = b.step(acts)
+            for i, e in enumerate(envs):
+                o, r, d, inf = e.step(int(acts[i]))
+                assert np.array_equal(obs[i], o), (t, i, obs[i], o)
+                assert rew[i] == r and done[i] == d, (t, i)
+                for key in ["episode_reward_attacker", "episode_reward_defender",
+                            "episode_progress", "episode_chain_time", "episode_sim_time",
+                            "episode_n_steps", "episode_n_activations", "head_height",
+                            "head_miner"]:
+                    assert info[key][i] == inf[key], (t, i, key)
+        assert done.all()
+
+
+def test_eth_observe_fields_and_policy_decoding(ctx):
+    n = 8
+    for unit in (True, False):
+        cfg, keep = _cfg(alpha=0.4, gamma=0.5, max_steps=300, seed=6, n_lanes=n,
+                         unit_observation=unit)
+        b = device.Batch(cfg, keep=keep)
+        obs = b.reset()
+        envs = [O.EthGymEnv(cfg, episode=i) for i in range(n)]
+        for e in envs:
+            e.reset()
+        for t in range(100):
+            f = b.observe_fields()
+            assert np.array_equal(f, np.array([e.fields() for e in envs]))
+            for name, pid in device.policy_registry(L.PROTO_ETHEREUM):
+                dev = b.policy_actions(pid, obs)
+                assert dev.tolist() == [O.eth_policy(name, e.fields()) for e in envs], name
+            acts = np.array([O.eth_policy("selfish_release", e.fields()) for e in envs],
+                            np.int32)
+            obs, _, _, _ = b.step(acts, with_info=False)
+            for i, e in enumerate(envs):
+                e.step(int(acts[i]))
+
+
+def test_eth_rollout_matches_sequential_oracle_episodes(ctx):
+    n, T, ms = 32, 240, 60
+    cfg, keep = _cfg(alpha=0.3, gamma=0.5, policy=L.ETH_POLICY_FN19, max_steps=ms, seed=31,
+                     n_lanes=n)
+    b = device.Batch(cfg, keep=keep)
+    s, obs, rew, done = b.rollout(T, outputs=True)
+    assert s.steps == n * T
+    finished = 0
+    for i in range(n):
+        ep = i
+        e = O.EthGymEnv(cfg, episode=ep)
+        e.reset()
+        for t in range(T):
+            o, r, d, _ = e.step(O.eth_policy("fn19", e.fields()))
+            assert rew[t, i] == r and bool(done[t, i]) == d, (i, t)
+            if d:
+                finished += 1
+                ep += n
+                e = O.EthGymEnv(cfg, episode=ep)
+                o = e.reset()
+            assert np.array_equal(obs[t, i], o), (i, t)
+    assert s.episodes == finished
+    assert b.rollout(10).steps == n * 10

@@ -127,6 +127,40 @@ def test_unsupported_protocol_is_loud():
         protocols.spar(k=8, reward="constant", unit_observation=True)
 
 
+def test_ethereum_protocol(capsys):
+    # gym/ocaml/test/test_protocols.py:77-102
+    env = envs.make("cpr_gym:core-v0",
+                    proto=protocols.ethereum(reward="discount", unit_observation=True),
+                    alpha=0.13, gamma=0.9, defenders=10, max_steps=10000)
+    env.render()
+    assert capsys.readouterr().out.splitlines()[0] == (
+        "Ethereum with heaviest_chain-preference, work-progress, uncle cap 2, "
+        "and discount-rewards; "
+        "SSZ'16-like attack space with unit observations; α=0.13 attacker")
+    obs = env.reset()
+    for _ in range(600):
+        obs, _, _, _ = env.step(env.policy(obs, "honest"))
+    obs = env.reset()
+    for _ in range(600):
+        obs, _, _, info = env.step(env.policy(obs, "selfish_discard"))
+    assert env.observation_space.contains(obs)
+    assert env.action_space.n == 24
+    assert list(env.policies()) == ["fn19pkel", "fn19", "selfish_discard", "selfish_release",
+                                    "honest"]
+    assert info["protocol_incentive_scheme"] == "discount"
+    assert info["head_work"] == info["episode_progress"]
+    env.render()
+    out = capsys.readouterr().out.splitlines()
+    assert out[1].startswith("public_height: ") and out[10].startswith("event: `")
+    assert out[-1].startswith("Actions: (0) Adopt_discard, uncles {own: false; foreign: false}"
+                              " | (1) Adopt_discard, uncles {own: false; foreign: true}")
+    with pytest.raises(ValueError, match="try 'constant' or 'discount'"):
+        protocols.ethereum(reward="block", unit_observation=True)
+    fuzz_episode(envs.make("core-v0", proto=protocols.ethereum(reward="constant",
+                                                                unit_observation=False),
+                           max_steps=300))
+
+
 def test_bk_protocol(capsys):
     # gym/ocaml/test/test_protocols.py:105-127
     env = envs.make("cpr_gym:core-v0",
