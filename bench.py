@@ -14,6 +14,7 @@ Prints one JSON line (rank 0).
 """
 
 import argparse
+import ctypes
 import json
 import os
 import sys
@@ -68,7 +69,7 @@ def cpu_baseline(seconds, points):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--episodes", type=int, default=393216, help="per GPU per sweep point")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
@@ -92,33 +93,45 @@ def main():
         cfg, keep = device.make_config(alpha=a, gamma=g, max_steps=STEPS_PER_EPISODE, seed=SEED)
         batches.append(device.Batch(cfg, ctx=ctx, keep=keep))
     E = args.episodes
+    sbytes = ctypes.sizeof(L.Summary)
 
-    def one_step(step_idx, sums, launches):
+    def one_step(step_idx, sums_dev):
+        # every point's episodes submitted asynchronously on the library's streams (the
+        # flagged-episode re-runs go to its second stream); summaries accumulate on the
+        # device and are read after the synchronize that closes the timed region
         base = (step_idx * ws + rank) * E  # disjoint episode ids per rank and step
-        for i, b in enumerate(batches):
-            b.run(E, first_episode=base, summary=sums[i])
-            launches.append(b.last_launch())
+        for b, sd in zip(batches, sums_dev):
+            b.run_async(E, base, sd.data_ptr())
+
+    def read(sums_dev):
+        return [L.Summary.from_buffer_copy(sd.cpu().numpy().tobytes()) for sd in sums_dev]
+
+    def new_sums():
+        return [torch.zeros(sbytes // 8, dtype=torch.int64, device=tdev) for _ in points]
 
     for w in range(args.warmup):
-        one_step(10**6 + w, [L.Summary() for _ in points], [])
-    sums = [L.Summary() for _ in points]
-    launches = []
+        one_step(10**6 + w, new_sums())
+    ctx.synchronize()
+    sums_dev = new_sums()
     parallel.barrier(tdev)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for k in range(args.steps):
-        one_step(k, sums, launches)
+        one_step(k, sums_dev)
     ctx.synchronize()
     torch.cuda.synchronize()
     parallel.barrier(tdev)
     dt = parallel.allreduce_max(time.perf_counter() - t0, tdev)
+    sums = read(sums_dev)
     totals = [parallel.allreduce_summary(s, tdev) for s in sums]
     acts = sum(int(s.activations) for s in totals)
     episodes = sum(int(s.episodes) for s in totals)
 
-    # dominant kernel = k_run_episodes; achieved from HIP events on the library's stream
-    kms = np.array([m for m, _ in launches])
-    kacts = np.array([a for _, a in launches], dtype=np.float64)
+    # dominant kernel = k_run_episodes; achieved from HIP events recorded by the library
+    # around the last launch of every point, on the stream the kernel runs on; activations
+    # per launch = E episodes x (max_steps + 1) (every gym episode is exactly that long)
+    kms = np.array([b.last_launch()[0] for b in batches])
+    kacts = np.full(len(batches), float(E * (STEPS_PER_EPISODE + 1)))
     act_per_s_kernel = float(kacts.sum() / (kms.sum() / 1e3))
     achieved = act_per_s_kernel * OPS_PER_ACTIVATION / 1e12
     if rank == 0:

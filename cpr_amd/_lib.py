@@ -69,6 +69,7 @@ ST_STALE_TIME = 16
 ST_CAPACITY = 32
 ST_REFERENCE_RAISES = 64
 ST_TRACE_MISS = 128
+ST_EXACT_RERUN = 256
 
 HIST_BINS = 64
 

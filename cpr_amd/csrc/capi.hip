@@ -33,12 +33,6 @@ static int fail(int code, const std::string& msg) {
       return fail(CPR_E_HIP, std::string(#expr " failed: ") + hipGetErrorString(e_));   \
   } while (0)
 
-struct cpr_ctx {
-  int device;
-  hipStream_t stream;
-  int cus;
-};
-
 struct DevBuf {
   void* p = nullptr;
   size_t bytes = 0;
@@ -58,6 +52,18 @@ struct DevBuf {
   }
 };
 
+struct cpr_ctx {
+  int device;
+  hipStream_t stream;
+  int cus;
+  // Nakamoto episodes flagged by the closed-form lane wait here for their exact re-run
+  // (k_nak_exact_rerun), which runs at the next synchronization point, all of them in one
+  // launch: rq = [kRerunQueue] int64 entries + a uint32 counter; one RerunLaunch per
+  // episode-kernel launch since then
+  DevBuf rq, rtab, rmem;
+  std::vector<RerunLaunch> rlaunch, rlaunch_up;
+};
+
 struct cpr_batch {
   cpr_ctx* ctx;
   cpr_config cfg;
@@ -72,6 +78,11 @@ struct cpr_batch {
   int64_t bk_bytes = 0;
   ts::TsParams TP;       // CPR_PROTO_TAILSTORM (shares bk_mem / bk_lmem / bk_slots)
   bool is_ev = false;    // B_k or Tailstorm event-engine lanes
+  // Nakamoto fused episodes: exact re-runs of flagged episodes on the event engine
+  bool has_rerun = false;
+  eth::EthParams NEP;    // the Ethereum lane in Nakamoto mode
+  int64_t nak_bytes = 0;
+  bool async_launch = false;  // last launch came from cpr_run_episodes_async
   std::vector<uint8_t> table_host;
   DevBuf table_dev, tabs_dev;  // policy table; unit-observation tables
   DevBuf spill, tlog, replay, summary, records;
@@ -124,12 +135,20 @@ int cpr_ctx_destroy(cpr_ctx* c) {
   if (!c) return CPR_OK;
   (void)hipSetDevice(c->device);
   (void)hipStreamDestroy(c->stream);
+  (void)hipStreamSynchronize(c->stream);
+  c->rq.release();
+  c->rtab.release();
+  c->rmem.release();
   delete c;
   return CPR_OK;
 }
 
+static int flush_reruns(cpr_ctx* c);
+
 int cpr_synchronize(cpr_ctx* c) {
   HIP_TRY(hipSetDevice(c->device));
+  int rc = flush_reruns(c);
+  if (rc) return rc;
   HIP_TRY(hipStreamSynchronize(c->stream));
   return CPR_OK;
 }
@@ -503,12 +522,37 @@ int cpr_batch_create(cpr_ctx* ctx, const cpr_config* cfg, cpr_batch** out) {
   }
   b->P.table = (const uint8_t*)b->table_dev.p;
   b->BP.table = (const uint8_t*)b->table_dev.p;
+  if (cfg->protocol == CPR_PROTO_NAKAMOTO) {
+    // the same episode on the exact event engine: Ethereum lane, no uncles, nakamoto_ssz
+    // policy (validated above); configurations it cannot hold keep the lane's flags
+    cpr_config c2 = *cfg;
+    c2.protocol = CPR_PROTO_ETHEREUM;
+    c2.policy = CPR_ETH_POLICY_HONEST;
+    c2.reward_scheme = CPR_REWARD_CONSTANT;
+    const std::string keep_err = g_err;
+    if (validate_eth(&c2, &b->NEP) == CPR_OK) {
+      b->NEP.nak = 1;
+      b->NEP.policy = cfg->policy;
+      b->NEP.table = b->P.table;
+      b->NEP.table_dim = cfg->policy_table_dim;
+      b->nak_bytes = eth::eth_lane_bytes(b->NEP.cap_b, b->NEP.cap_e, b->NEP.n);
+      b->has_rerun = true;
+    }
+    g_err = keep_err;
+  }
   *out = b;
   return CPR_OK;
 }
 
 int cpr_last_launch(cpr_batch* b, double* kernel_ms, int64_t* activations) {
   if (!b) return fail(CPR_E_INVALID_ARG, "NULL argument");
+  if (b->async_launch) {  // cpr_run_episodes_async: the caller has synchronized
+    float ms = 0.f;
+    HIP_TRY(hipEventElapsedTime(&ms, b->ev0, b->ev1));
+    b->last_ms = ms;
+    b->last_acts = -1;  // not known without reading the caller's device summary
+    b->async_launch = false;
+  }
   if (kernel_ms) *kernel_ms = b->last_ms;
   if (activations) *activations = b->last_acts;
   return CPR_OK;
@@ -517,6 +561,8 @@ int cpr_last_launch(cpr_batch* b, double* kernel_ms, int64_t* activations) {
 int cpr_batch_destroy(cpr_batch* b) {
   if (!b) return CPR_OK;
   (void)hipSetDevice(b->ctx->device);
+  (void)hipStreamSynchronize(b->ctx->stream);
+  (void)flush_reruns(b->ctx);  // pending re-runs may read this batch's buffers
   (void)hipStreamSynchronize(b->ctx->stream);
   if (b->ev0) (void)hipEventDestroy(b->ev0);
   if (b->ev1) (void)hipEventDestroy(b->ev1);
@@ -536,6 +582,9 @@ int cpr_batch_destroy(cpr_batch* b) {
 
 // lanes per launch: exactly the resident capacity (occupancy API: workgroups per CU at
 // this kernel's register/LDS use x CUs x 256), bounded by a 16 GiB budget for per-lane HBM
+// exact Nakamoto re-runs: one-wave workgroups of the re-run kernel
+constexpr int64_t kRerunLanes = 512;
+
 static int64_t episode_lanes(cpr_batch* b, int64_t n_eps) {
   const int64_t full = (int64_t)b->ctx->cus * run_episodes_blocks_per_cu(b->cfg.mode) * 256;
   const int64_t budget = (int64_t)(16ll << 30) / episode_lane_bytes(b->P);
@@ -543,6 +592,30 @@ static int64_t episode_lanes(cpr_batch* b, int64_t n_eps) {
   const int64_t need = ((n_eps + 255) / 256) * 256;
   lanes = std::min(lanes, need);
   return std::max<int64_t>(256, (lanes / 256) * 256);
+}
+
+// Re-run every queued flagged Nakamoto episode of the launches since the last flush, in
+// one k_nak_exact_rerun launch on the context's stream (after those launches, before the
+// caller reads summaries or records), then empty the queue.
+static int flush_reruns(cpr_ctx* c) {
+  if (c->rlaunch.empty()) return CPR_OK;
+  int64_t lb = 0, rest = 0;
+  for (const RerunLaunch& r : c->rlaunch) {
+    lb = std::max(lb, r.lane_bytes);
+    rest = std::max(rest, eth::eth_rest_bytes(r.P.cap_b, r.P.cap_e, r.P.n));
+  }
+  c->rlaunch_up.swap(c->rlaunch);  // keeps the host table alive for the async copy
+  c->rlaunch.clear();
+  const size_t tb = c->rlaunch_up.size() * sizeof(RerunLaunch);
+  HIP_TRY(c->rtab.ensure(tb));
+  HIP_TRY(hipMemcpyAsync(c->rtab.p, c->rlaunch_up.data(), tb, hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(c->rmem.ensure((size_t)kRerunLanes * (size_t)lb));
+  uint32_t* qn = (uint32_t*)((char*)c->rq.p + (size_t)kRerunQueue * 8);
+  HIP_TRY(launch_nak_exact_rerun((const RerunLaunch*)c->rtab.p, (const int64_t*)c->rq.p, qn,
+                                 kRerunQueue, (uint8_t*)c->rmem.p, lb, rest, kRerunLanes,
+                                 c->stream));
+  HIP_TRY(hipMemsetAsync(qn, 0, 4, c->stream));
+  return CPR_OK;
 }
 
 // Ethereum lanes: resident capacity bounded by a 32 GiB budget for the per-lane regions
@@ -617,16 +690,45 @@ static int run_async(cpr_batch* b, int64_t n, uint64_t first, const TraceSource*
     HIP_TRY(hipEventCreate(&b->ev0));
     HIP_TRY(hipEventCreate(&b->ev1));
   }
+  int64_t* redo = nullptr;
+  uint32_t* redo_n = nullptr;
+  uint32_t launch_id = 0;
+  if (b->has_rerun) {
+    cpr_ctx* c = b->ctx;
+    if (c->rlaunch.size() >= kRerunMaxLaunches) {
+      int rc = flush_reruns(c);
+      if (rc) return rc;
+    }
+    if (!c->rq.p) {
+      HIP_TRY(c->rq.ensure((size_t)kRerunQueue * 8 + 64));
+      HIP_TRY(hipMemsetAsync((char*)c->rq.p + (size_t)kRerunQueue * 8, 0, 4, c->stream));
+    }
+    RerunLaunch rl;
+    memset(&rl, 0, sizeof(rl));
+    rl.P = b->NEP;
+    rl.seed = b->cfg.seed;
+    rl.first = first;
+    rl.is_trace = tr ? 1 : 0;
+    if (tr) rl.tr = *tr;
+    rl.recs = rec_dev;
+    rl.sum = sum_dev;
+    rl.lane_bytes = b->nak_bytes;
+    launch_id = (uint32_t)c->rlaunch.size();
+    c->rlaunch.push_back(rl);
+    redo = (int64_t*)c->rq.p;
+    redo_n = (uint32_t*)((char*)c->rq.p + (size_t)kRerunQueue * 8);
+  }
   HIP_TRY(hipEventRecord(b->ev0, b->ctx->stream));
   if (tr)
     HIP_TRY(launch_replay_episodes(b->P, *tr, n, b->cfg.mode, b->cfg.activations,
                                    (int32_t*)b->spill.p, (double*)b->tlog.p,
-                                   (uint8_t*)b->replay.p, lanes, rec_dev, sum_dev,
-                                   b->ctx->stream));
+                                   (uint8_t*)b->replay.p, lanes, rec_dev, sum_dev, redo, redo_n,
+                                   launch_id, kRerunQueue, b->ctx->stream));
   else
     HIP_TRY(launch_run_episodes(b->P, b->cfg.seed, first, n, b->cfg.mode, b->cfg.activations,
                                 (int32_t*)b->spill.p, (double*)b->tlog.p, (uint8_t*)b->replay.p,
-                                lanes, rec_dev, sum_dev, b->ctx->stream));
+                                lanes, rec_dev, sum_dev, redo, redo_n, launch_id, kRerunQueue,
+                                b->ctx->stream));
   HIP_TRY(hipEventRecord(b->ev1, b->ctx->stream));
   return CPR_OK;
 }
@@ -636,6 +738,7 @@ int cpr_run_episodes_async(cpr_batch* b, int64_t n, uint64_t first, cpr_summary*
   if (!b || !sum_dev) return fail(CPR_E_INVALID_ARG, "NULL argument");
   if (n <= 0) return CPR_OK;
   HIP_TRY(hipSetDevice(b->ctx->device));
+  b->async_launch = true;
   return run_async(b, n, first, nullptr, sum_dev, rec_dev);
 }
 
@@ -654,6 +757,8 @@ static int run_sync(cpr_batch* b, int64_t n, uint64_t first, const TraceSource* 
     }
   }
   int rc = run_async(b, n, first, tr, (cpr_summary*)b->summary.p, rec_dev);
+  if (rc) return rc;
+  rc = flush_reruns(b->ctx);
   if (rc) return rc;
   cpr_summary s;
   HIP_TRY(hipMemcpyAsync(&s, b->summary.p, sizeof(s), hipMemcpyDeviceToHost, st));

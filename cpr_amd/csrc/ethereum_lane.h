@@ -43,14 +43,16 @@ __host__ __device__ inline uint32_t mkev(uint32_t ty, uint32_t node, uint32_t ki
 
 struct EBlock {
   int32_t serial;
-  int32_t p[3];  // parent serials; p[0] = parent, p[1..] = uncles
+  int32_t p[3];  // parent serials; p[0] = parent, p[1..] = uncles (Nakamoto mode, no
+                 // uncles: p[1] = newest child, p[2] = next older sibling)
   int32_t np;
   int32_t height, work;
   int32_t miner;             // -1 = genesis
   int32_t rew_att, rew_def;  // cumulative rewards of the first-parent chain, units of 1/32
   int32_t share_k, share_off;
   double time;  // Simulator.timestamp = append time (the miner sees it first)
-  int32_t _pad[2];
+  int32_t jump;  // Nakamoto mode: skew-binary jump ancestor (O(log depth) ancestor walks)
+  int32_t _pad;
 };
 static_assert(sizeof(EBlock) == 64, "EBlock layout");
 
@@ -72,11 +74,18 @@ struct EthParams {
   double ev, delta, dmax;
   int64_t max_steps, activations;
   double max_progress, max_time;
+  // Nakamoto on this engine (exact re-runs of Nakamoto episodes): no
+  // uncles, so payloads, rewards (1 per block), work (= height) and the ethereum_ssz agent
+  // reduce to nakamoto.ml / nakamoto_ssz.ml; the nakamoto_ssz policy (or table) decides
+  int32_t nak, table_dim;
+  const uint8_t* table;
 };
 
 constexpr int32_t NCAND = 32, NQ = 32, NSTACK = 64;
 constexpr int32_t SCR_CAND = 0, SCR_KEY = 32, SCR_QA = 64, SCR_QB = 96, SCR_STACK = 128;
-constexpr int32_t SCR_INTS = 192;
+// per node: blocks received (V_GOT) but not yet visible, waiting for a parent
+constexpr int32_t SCR_PEND = 192;
+constexpr int32_t SCR_INTS = 192 + 72;
 
 struct EthMem {
   EBlock* blk;
@@ -93,6 +102,25 @@ __host__ __device__ inline int64_t eth_lane_bytes(int32_t cap_b, int32_t cap_e, 
          align128((int64_t)cap_e * 24) + align128((int64_t)n * 4) + align128(SCR_INTS * 4);
 }
 
+// bytes of the region after the block ring (visibility, heap, tips, scratch)
+__host__ __device__ inline int64_t eth_rest_bytes(int32_t cap_b, int32_t cap_e, int32_t n) {
+  return eth_lane_bytes(cap_b, cap_e, n) - align128((int64_t)cap_b * 64);
+}
+// block ring at blk, the rest at `rest` (e.g. LDS), same layout as eth_mem_at
+__host__ __device__ inline EthMem eth_mem_split(uint8_t* blk, uint8_t* rest, int32_t cap_b,
+                                                int32_t cap_e, int32_t n) {
+  EthMem M;
+  int64_t o = 0;
+  M.blk = (EBlock*)blk;
+  M.vis = rest + o;
+  o += align128((int64_t)cap_b * n);
+  M.heap = (HNode*)(rest + o);
+  o += align128((int64_t)cap_e * 24);
+  M.tips = (int32_t*)(rest + o);
+  o += align128((int64_t)n * 4);
+  M.scr = (int32_t*)(rest + o);
+  return M;
+}
 __host__ __device__ inline EthMem eth_mem_at(uint8_t* base, int32_t cap_b, int32_t cap_e,
                                              int32_t n) {
   EthMem M;
@@ -306,6 +334,38 @@ struct EthLane {
   }
 
   // ------------------------------------------------------------------ DAG
+  // Nakamoto mode (one parent per block): skew-binary jump pointers (Myers 1983). A
+  // block's jump is its parent's jump's jump when the parent's two jumps span equal height
+  // gaps, else its parent; a jump's height depends on the height alone, so ancestor-at-
+  // height and LCA queries take O(log depth) loads instead of the reference's O(depth)
+  // walks (dagtools.ml:102-121, ethereum_ssz.ml:407-414). Jumps whose slot in the ring was
+  // reused are not followed (the parent is).
+  __host__ __device__ inline bool resident(const EthParams& P, int32_t s) const {
+    return s >= 0 && newest - s < P.cap_b;
+  }
+  __host__ __device__ inline int32_t jump_for(const EthParams& P, const EthMem& M,
+                                              int32_t parent) {
+    const EBlock& pb = B(P, M, parent);
+    if (pb.np == 0 || !resident(P, pb.jump)) return parent;
+    const EBlock& jb = B(P, M, pb.jump);
+    if (jb.np == 0 || !resident(P, jb.jump)) return parent;
+    const int32_t jjh = B(P, M, jb.jump).height;
+    return (pb.height - jb.height == jb.height - jjh) ? jb.jump : parent;
+  }
+  // ancestor of x at height h <= height(x)
+  __host__ __device__ inline int32_t ancestor_at(const EthParams& P, const EthMem& M,
+                                                 int32_t x, int32_t h) {
+    while (!dead) {
+      const EBlock& b = B(P, M, x);
+      if (b.height <= h) return x;
+      if (resident(P, b.jump) && B(P, M, b.jump).height >= h)
+        x = b.jump;
+      else
+        x = b.p[0];
+    }
+    return x;
+  }
+
   // simulator.ml:233-332 (genesis) and 122-136 / 377-399 (append + set_rewards with
   // ethereum.ml:173-197; precursor = first parent)
   __host__ __device__ inline int32_t append(const EthParams& P, const EthMem& M, int32_t node,
@@ -340,6 +400,12 @@ struct EthLane {
     b.share_k = -1;
     b.share_off = 0;
     b.time = now;
+    b.jump = P.nak ? jump_for(P, M, d.p[0]) : d.p[0];
+    if (P.nak) {  // children list of the parent, newest first (dag.ml:32)
+      EBlock& par = B(P, M, d.p[0]);
+      b.p[2] = par.p[1];
+      par.p[1] = s;
+    }
     for (int32_t j = 0; j < P.n; ++j) V(P, M, s, j) = V_INV;
     return s;
   }
@@ -348,6 +414,16 @@ struct EthLane {
   __host__ __device__ inline Payload payload(const EthParams& P, const EthMem& M, int32_t view,
                                              int32_t tip, int32_t filter, int32_t f_own,
                                              int32_t f_foreign) {
+    if (P.nak) {  // Nakamoto: Honest.puzzle_payload (nakamoto.ml:77-81), one parent
+      const EBlock& t = B(P, M, tip);
+      Payload d;
+      d.p[0] = tip;
+      d.p[1] = d.p[2] = -1;
+      d.np = 1;
+      d.height = t.height + 1;
+      d.work = t.work + 1;
+      return d;
+    }
     int32_t* cand = M.scr + SCR_CAND;
     int32_t* key = M.scr + SCR_KEY;
     int32_t* ic = M.scr + SCR_QA;  // in-chain set (tip + parents of tip..gen5), <= 19
@@ -541,6 +617,30 @@ struct EthLane {
   }
   __host__ __device__ inline int32_t common_ancestor(const EthParams& P, const EthMem& M,
                                                      int32_t a, int32_t b) {
+    if (P.nak) {
+      // one parent per block: the frontier walk finds the lowest common ancestor of the
+      // two tree paths; equal heights first, then jump pairs that still differ (jumps of
+      // equal-height blocks have equal heights), else parents
+      const int32_t hx = B(P, M, a).height, hy = B(P, M, b).height;
+      int32_t x = ancestor_at(P, M, a, hy < hx ? hy : hx);
+      int32_t y = ancestor_at(P, M, b, hy < hx ? hy : hx);
+      while (x != y && !dead) {
+        const EBlock& bx = B(P, M, x);
+        const EBlock& by = B(P, M, y);
+        if (bx.np == 0 || by.np == 0) {
+          fail(4);
+          return 0;
+        }
+        if (bx.jump != by.jump && resident(P, bx.jump) && resident(P, by.jump)) {
+          x = bx.jump;
+          y = by.jump;
+        } else {
+          x = bx.p[0];
+          y = by.p[0];
+        }
+      }
+      return x;
+    }
     int32_t* qa = M.scr + SCR_QA;
     int32_t* qb = M.scr + SCR_QB;
     int32_t na = 0, nb = 0;
@@ -640,6 +740,7 @@ struct EthLane {
   __host__ __device__ inline int32_t apply(const EthParams& P, const EthMem& M, int32_t index) {
     const int32_t action = index >> 2;
     auto release_upto = [&](int32_t target) {
+      if (P.nak) return ancestor_at(P, M, o_priv, target < 0 ? 0 : target);
       int32_t b = o_priv;
       while (!dead) {
         const EBlock& x = B(P, M, b);
@@ -693,9 +794,11 @@ struct EthLane {
     r.share_k = -1;
     r.share_off = 0;
     r.time = 0.0;
+    r.jump = 0;
     for (int32_t j = 0; j < P.n; ++j) {
       V(P, M, 0, j) = V_RECV | V_GOT;
       M.tips[j] = 0;
+      M.scr[SCR_PEND + j] = 0;
     }
     agent_init(0);
     schedule_pow(P, S, M);
@@ -715,6 +818,7 @@ struct EthLane {
         bool ok = true;
         for (int32_t i = 0; i < b.np; ++i) ok &= visible(P, M, b.p[i], node);
         if (!ok) break;
+        if (v & V_GOT) --M.scr[SCR_PEND + node];
         v = (uint8_t)((v & ~V_KIND) | (kind == KD_NET ? V_RECV : V_WH));
         push_now(P, M, mkev(EV_ON, node, kind), s);
         push_now(P, M, mkev(EV_MDV, node, kind), s);
@@ -778,12 +882,20 @@ struct EthLane {
         uint8_t& v = V(P, M, s, node);
         if (!(v & V_GOT)) {
           v |= V_GOT;
+          if ((v & V_KIND) == V_INV) ++M.scr[SCR_PEND + node];
           push_now(P, M, mkev(EV_MV, node, KD_NET), s);
         }
         break;
       }
       case EV_MDV: {
-        // children (newest first) already received at this node become visible
+        // children (newest first) already received at this node become visible; none can
+        // be waiting when no received block is invisible here (the scan would find none)
+        if (M.scr[SCR_PEND + node] == 0) break;
+        if (P.nak) {  // the parent's children list, same order as the scan below
+          for (int32_t c = B(P, M, s).p[1]; c > s && !dead; c = B(P, M, c).p[2])
+            if (V(P, M, c, node) & V_GOT) push_now(P, M, mkev(EV_MV, node, KD_NET), c);
+          break;
+        }
         for (int32_t c = newest; c > s && !dead; --c) {
           if (!(V(P, M, c, node) & V_GOT)) continue;
           const EBlock& cb = B(P, M, c);

@@ -43,15 +43,20 @@ inline int64_t episode_lane_bytes(const NakParams& P) {
   return (int64_t)P.cap * 4 + (int64_t)P.tlog_len * 8 + REPLAY_BYTES;
 }
 
+// redo/redo_n (optional, device): flagged episodes are appended to that queue (entries
+// tagged with launch_id, at most redo_cap) instead of accumulated, for launch_nak_exact_rerun
 hipError_t launch_run_episodes(const NakParams& P, uint64_t seed, uint64_t first, int64_t n_eps,
                                int32_t mode, int64_t activations, int32_t* spill, double* tlog,
                                uint8_t* replay, int64_t lanes, cpr_episode_record* recs,
-                               cpr_summary* sum, hipStream_t st);
+                               cpr_summary* sum, int64_t* redo, uint32_t* redo_n,
+                               uint32_t launch_id, int64_t redo_cap, hipStream_t st);
 // the same fused kernel drawing from a device copy of a cpr_trace (cpr_replay)
 hipError_t launch_replay_episodes(const NakParams& P, const TraceSource& src, int64_t n_eps,
                                   int32_t mode, int64_t activations, int32_t* spill,
                                   double* tlog, uint8_t* replay, int64_t lanes,
-                                  cpr_episode_record* recs, cpr_summary* sum, hipStream_t st);
+                                  cpr_episode_record* recs, cpr_summary* sum, int64_t* redo,
+                                  uint32_t* redo_n, uint32_t launch_id, int64_t redo_cap,
+                                  hipStream_t st);
 hipError_t launch_reset(const NakParams& P, uint64_t seed, const LockBuffers& B, int64_t n,
                         const uint8_t* mask, const uint64_t* eps, int unit, const double* tab_nn,
                         const double* tab_sg, int32_t tab_n, double* obs, hipStream_t st);
@@ -93,6 +98,30 @@ hipError_t launch_eth_observe_fields(const eth::EthParams& P, uint8_t* mem, int6
 hipError_t launch_eth_policy(int32_t policy, int unit, const double* obs, int64_t n,
                              int32_t* actions, hipStream_t st);
 size_t eth_slot_bytes();
+// Exact re-runs of flagged Nakamoto episodes. Episode kernels append
+// queue entries (launch << 40) | (episode index << 8) | lane status bits; one RerunLaunch
+// per episode-kernel launch tells the re-run kernel where that launch's draws come from and
+// where its records and summary go.
+constexpr int64_t kRerunQueue = 1 << 22;       // queue entries per context
+constexpr size_t kRerunMaxLaunches = 1 << 20;  // launches per flush (< 2^23)
+
+struct RerunLaunch {
+  eth::EthParams P;  // the Ethereum lane in Nakamoto mode
+  uint64_t seed, first;
+  int32_t is_trace, _pad;
+  TraceSource tr;
+  cpr_episode_record* recs;
+  cpr_summary* sum;
+  int64_t lane_bytes;
+};
+
+// all queued re-runs (count on the device) in one launch of `lanes` one-wave workgroups,
+// each with a lane region of lane_bytes at mem + i x lane_bytes; lds_bytes (the largest
+// eth_rest_bytes of the launches; used if <= 64 KB) puts all but the block ring in LDS
+hipError_t launch_nak_exact_rerun(const RerunLaunch* launches, const int64_t* queue,
+                                  const uint32_t* queue_n, int64_t queue_cap, uint8_t* mem,
+                                  int64_t lane_bytes, int64_t lds_bytes, int64_t lanes,
+                                  hipStream_t st);
 
 // B_k (kernels_bk.hip): mem = lanes x lane_bytes; lockstep slots = n x bk_slot_bytes()
 hipError_t launch_bk_run_episodes(const bk::BkParams& P, uint64_t seed, uint64_t first,

@@ -62,10 +62,14 @@ __device__ inline BRef run_loop(NakLane& L, const NakParams& P, const St& S, con
   return L.head(P, M);
 }
 
+// lane status bits whose episodes the closed form cannot vouch for
+constexpr uint32_t kInexact = ST_OVERLAP | ST_DEEP_FORK | ST_TIE_UNRESOLVED | ST_STALE_TIME;
+
 template <int MODE, class Src>
 __global__ __launch_bounds__(kBlock) void k_run_episodes(
     NakParams P, Src src, int64_t n_eps, int64_t activations,
-    int32_t* spill, double* tlog, uint8_t* replay, cpr_episode_record* recs, cpr_summary* sum) {
+    int32_t* spill, double* tlog, uint8_t* replay, cpr_episode_record* recs, cpr_summary* sum,
+    int64_t* redo, uint32_t* redo_n, uint32_t launch_id, int64_t redo_cap) {
   __shared__ int32_t hist[CPR_HIST_BINS];
   __shared__ int32_t ring[RING * kBlock];
   if (threadIdx.x < CPR_HIST_BINS) hist[threadIdx.x] = 0;
@@ -91,7 +95,18 @@ __global__ __launch_bounds__(kBlock) void k_run_episodes(
                                          : run_loop(L, P, S, M, activations);
     const double tm = L.time_of(M, hd);
     const uint32_t status = L.status | Src::missed(S);
-    acc_add(acc, hd, steps, L.k, status, hist);
+    uint32_t st_out = status;
+    if (redo != nullptr && (status & kInexact) != 0u) {
+      // the closed form does not hold for this episode: hand it to the exact event engine
+      // (k_nak_exact_rerun), which writes its record and summary contribution
+      const uint32_t r = atomicAdd(redo_n, 1u);
+      if ((int64_t)r < redo_cap) {
+        redo[r] = ((int64_t)launch_id << 40) | (e << 8) | (int64_t)(status & 0xffu);
+        continue;
+      }
+      st_out |= CPR_ST_CAPACITY;  // queue full: the flagged outputs stay, marked invalid
+    }
+    acc_add(acc, hd, steps, L.k, st_out, hist);
     if (recs) {
       cpr_episode_record r;
       r.reward_attacker = (double)hd.ra;
@@ -103,7 +118,7 @@ __global__ __launch_bounds__(kBlock) void k_run_episodes(
       r.n_activations = L.k;
       r.head_height = hd.h;
       r.head_miner = MODE == CPR_MODE_GYM ? miner_of(P, S, hd.k) : -1;
-      r.status = status;
+      r.status = st_out;
       r.head_work = 0;
       recs[e] = r;
     }
@@ -258,29 +273,32 @@ __global__ void k_stream_fill(uint64_t seed, uint64_t ep, uint32_t idx0, uint32_
 hipError_t launch_run_episodes(const NakParams& P, uint64_t seed, uint64_t first, int64_t n_eps,
                                int32_t mode, int64_t activations, int32_t* spill, double* tlog,
                                uint8_t* replay, int64_t lanes, cpr_episode_record* recs,
-                               cpr_summary* sum, hipStream_t st) {
+                               cpr_summary* sum, int64_t* redo, uint32_t* redo_n,
+                               uint32_t launch_id, int64_t redo_cap, hipStream_t st) {
   const unsigned blocks = (unsigned)(lanes / kBlock);
   const SeedSource src{seed, first};
   if (mode == CPR_MODE_GYM)
     hipLaunchKernelGGL((k_run_episodes<CPR_MODE_GYM, SeedSource>), dim3(blocks), dim3(kBlock), 0,
-                       st, P, src, n_eps, activations, spill, tlog, replay, recs, sum);
+                       st, P, src, n_eps, activations, spill, tlog, replay, recs, sum, redo, redo_n, launch_id, redo_cap);
   else
     hipLaunchKernelGGL((k_run_episodes<CPR_MODE_LOOP, SeedSource>), dim3(blocks), dim3(kBlock), 0,
-                       st, P, src, n_eps, activations, spill, tlog, replay, recs, sum);
+                       st, P, src, n_eps, activations, spill, tlog, replay, recs, sum, redo, redo_n, launch_id, redo_cap);
   return hipGetLastError();
 }
 
 hipError_t launch_replay_episodes(const NakParams& P, const TraceSource& src, int64_t n_eps,
                                   int32_t mode, int64_t activations, int32_t* spill,
                                   double* tlog, uint8_t* replay, int64_t lanes,
-                                  cpr_episode_record* recs, cpr_summary* sum, hipStream_t st) {
+                                  cpr_episode_record* recs, cpr_summary* sum, int64_t* redo,
+                                  uint32_t* redo_n, uint32_t launch_id, int64_t redo_cap,
+                                  hipStream_t st) {
   const unsigned blocks = (unsigned)(lanes / kBlock);
   if (mode == CPR_MODE_GYM)
     hipLaunchKernelGGL((k_run_episodes<CPR_MODE_GYM, TraceSource>), dim3(blocks), dim3(kBlock), 0,
-                       st, P, src, n_eps, activations, spill, tlog, replay, recs, sum);
+                       st, P, src, n_eps, activations, spill, tlog, replay, recs, sum, redo, redo_n, launch_id, redo_cap);
   else
     hipLaunchKernelGGL((k_run_episodes<CPR_MODE_LOOP, TraceSource>), dim3(blocks), dim3(kBlock),
-                       0, st, P, src, n_eps, activations, spill, tlog, replay, recs, sum);
+                       0, st, P, src, n_eps, activations, spill, tlog, replay, recs, sum, redo, redo_n, launch_id, redo_cap);
   return hipGetLastError();
 }
 

@@ -14,6 +14,17 @@
 
 namespace cpr {
 
+// the lane's attack policy: ethereum_ssz (ethereum_ssz.ml:444-521), or in Nakamoto mode the
+// nakamoto_ssz policy / table (nakamoto_ssz.ml:374-440) mapped onto the same agent
+// (Adopt -> Adopt_discard; Override, Match, Wait unchanged; no uncles to choose)
+__device__ inline int32_t eth_lane_action(const eth::EthParams& P, const eth::EthObs& o) {
+  if (!P.nak) return eth::eth_policy(P.policy, o);
+  const int32_t a = nak_policy(P.policy, o.public_height, o.private_height, o.event, P.table,
+                               P.table_dim);
+  constexpr int32_t map[4] = {eth::A_ADOPT_DISCARD, eth::A_OVERRIDE, eth::A_MATCH, eth::A_WAIT};
+  return map[a & 3] * 4;
+}
+
 template <class Src>
 __global__ __launch_bounds__(kBlock) void k_eth_run_episodes(
     eth::EthParams P, Src src, int64_t n_eps, uint8_t* mem,
@@ -35,7 +46,7 @@ __global__ __launch_bounds__(kBlock) void k_eth_run_episodes(
       hd = 0;
       while (!done) {
         const eth::EthObs o = L.observe(P, M, false);
-        hd = L.gym_step(P, S, M, eth::eth_policy(P.policy, o), &done);
+        hd = L.gym_step(P, S, M, eth_lane_action(P, o), &done);
       }
     } else {
       hd = L.loop(P, S, M);
@@ -64,6 +75,120 @@ __global__ __launch_bounds__(kBlock) void k_eth_run_episodes(
   }
   __syncthreads();
   block_flush(acc, hist, sum);
+}
+
+// Exact re-run of the Nakamoto episodes the closed-form lane flagged.
+// Episode kernels queue (launch << 40) | (episode index << 8) | status bits instead of
+// accumulating such an episode; at the next synchronization point this kernel simulates
+// every queued episode again from its first draw on this event engine in Nakamoto mode
+// (P.nak), which follows every event of the reference's queue, so messages still in
+// flight at an activation are exact. Its record and summary contribution replace the
+// flagged ones; status keeps the lane's bits and adds CPR_ST_EXACT_RERUN.
+//
+// One episode per one-wave workgroup (lane 0 runs it: a re-run is one dependent chain, the
+// other lanes would only diverge); all queued episodes run concurrently. The summary is
+// updated with per-episode atomics (episodes of different launches go to different
+// summaries; there are ~1e-5 of them per episode kernel at the gym's delays).
+template <class St>
+__device__ inline int32_t nak_rerun_one(const eth::EthParams& P, const St& S,
+                                        const eth::EthMem& M, eth::EthLane& L) {
+  if (P.mode != CPR_MODE_GYM) return L.loop(P, S, M);
+  L.gym_reset(P, S, M);
+  bool done = L.dead != 0;
+  int32_t hd = 0;
+  while (!done) hd = L.gym_step(P, S, M, eth_lane_action(P, L.observe(P, M, false)), &done);
+  return hd;
+}
+
+__device__ inline void summary_add_episode(cpr_summary* out, int64_t ra, int64_t rd,
+                                           int64_t height, int64_t steps, int64_t acts,
+                                           uint32_t status) {
+  const double rel = (ra + rd) != 0 ? (double)ra / (double)(ra + rd) : 0.0;
+  auto add = [](int64_t* p, int64_t v) {
+    if (v) atomicAdd((unsigned long long*)p, (unsigned long long)v);
+  };
+  add(&out->episodes, 1);
+  add(&out->steps, steps);
+  add(&out->activations, acts);
+  add(&out->reward_attacker_fx, ra << 20);
+  add(&out->reward_defender_fx, rd << 20);
+  add(&out->progress_fx, height << 20);
+  add((int64_t*)&out->rel_revenue_fx, (int64_t)__builtin_rint(rel * 4294967296.0));
+  add((int64_t*)&out->rel_revenue_sq_fx, (int64_t)__builtin_rint(rel * rel * 4294967296.0));
+  add(&out->orphans, acts - height);
+  add(&out->status_tie, (status & CPR_ST_TIE) ? 1 : 0);
+  add(&out->status_overlap, (status & CPR_ST_OVERLAP) ? 1 : 0);
+  add(&out->status_other,
+      (status & ~(uint32_t)(CPR_ST_TIE | CPR_ST_OVERLAP | CPR_ST_EXACT_RERUN)) ? 1 : 0);
+  int bin = (int)(rel * (double)CPR_HIST_BINS);
+  bin = bin < 0 ? 0 : (bin >= CPR_HIST_BINS ? CPR_HIST_BINS - 1 : bin);
+  add(&out->hist[bin], 1);
+}
+
+__global__ __launch_bounds__(64) void k_nak_exact_rerun(const RerunLaunch* launches,
+                                                         const int64_t* queue,
+                                                         const uint32_t* queue_n,
+                                                         int64_t queue_cap, uint8_t* mem,
+                                                         int64_t lane_bytes, int lds) {
+  // the hot part of the lane region (visibility, event heap, scratch) in LDS when it fits
+  extern __shared__ __attribute__((aligned(128))) uint8_t lane_lds[];
+  if (threadIdx.x != 0) return;
+  int64_t nq = (int64_t)*queue_n;
+  nq = nq < queue_cap ? nq : queue_cap;
+  for (int64_t r = blockIdx.x; r < nq; r += gridDim.x) {
+    const int64_t q = queue[r];
+    const RerunLaunch& RL = launches[q >> 40];
+    const eth::EthParams P = RL.P;
+    const int64_t e = (q >> 8) & 0xffffffffll;
+    const uint32_t flags = (uint32_t)(q & 0xff);
+    uint8_t* base = mem + (int64_t)blockIdx.x * lane_bytes;
+    const eth::EthMem M = lds ? eth::eth_mem_split(base, lane_lds, P.cap_b, P.cap_e, P.n)
+                              : eth::eth_mem_at(base, P.cap_b, P.cap_e, P.n);
+    eth::EthLane L;
+    int32_t hd;
+    uint32_t miss = 0;
+    if (RL.is_trace) {
+      const auto S = RL.tr.at(e);
+      hd = nak_rerun_one(P, S, M, L);
+      miss = TraceSource::missed(S);
+    } else {
+      hd = nak_rerun_one(P, make_stream(RL.seed, RL.first + (uint64_t)e), M, L);
+    }
+    const uint32_t status = flags | L.status | miss | CPR_ST_EXACT_RERUN;
+    const eth::EBlock& h = L.B(P, M, hd);
+    const int32_t ra = h.rew_att / 32, rd = h.rew_def / 32;  // 1 per block
+    const int64_t steps = P.mode == CPR_MODE_GYM ? L.steps : 0;
+    // the summary counts the flags the re-run resolved as OVERLAP / TIE only
+    summary_add_episode(
+        RL.sum, ra, rd, h.height, steps, L.c_act,
+        status & ~(uint32_t)(CPR_ST_DEEP_FORK | CPR_ST_TIE_UNRESOLVED | CPR_ST_STALE_TIME));
+    if (RL.recs) {
+      cpr_episode_record rc;
+      rc.reward_attacker = (double)ra;
+      rc.reward_defender = (double)rd;
+      rc.progress = (double)h.height;
+      rc.chain_time = h.time;
+      rc.sim_time = P.mode == CPR_MODE_GYM ? L.now : 0.0;
+      rc.n_steps = steps;
+      rc.n_activations = L.c_act;
+      rc.head_height = h.height;
+      rc.head_miner = P.mode == CPR_MODE_GYM ? h.miner : -1;
+      rc.status = status;
+      rc.head_work = 0;
+      RL.recs[e] = rc;
+    }
+  }
+}
+
+hipError_t launch_nak_exact_rerun(const RerunLaunch* launches, const int64_t* queue,
+                                  const uint32_t* queue_n, int64_t queue_cap, uint8_t* mem,
+                                  int64_t lane_bytes, int64_t lds_bytes, int64_t lanes,
+                                  hipStream_t st) {
+  const int lds = lds_bytes > 0 && lds_bytes <= 64 * 1024 ? 1 : 0;
+  hipLaunchKernelGGL(k_nak_exact_rerun, dim3((unsigned)lanes), dim3(64),
+                     lds ? (size_t)lds_bytes : 0, st, launches, queue, queue_n, queue_cap, mem,
+                     lane_bytes, lds);
+  return hipGetLastError();
 }
 
 hipError_t launch_eth_run_episodes(const eth::EthParams& P, uint64_t seed, uint64_t first,
@@ -214,7 +339,7 @@ __global__ __launch_bounds__(kBlock) void k_eth_rollout(eth::EthParams P, uint64
       const int32_t c0 = SL.L.c_act;
       bool done = false;
       const int32_t hd =
-          SL.L.gym_step(P, make_stream(seed, SL.ep), M, eth::eth_policy(P.policy, o), &done);
+          SL.L.gym_step(P, make_stream(seed, SL.ep), M, eth_lane_action(P, o), &done);
       acts_all += SL.L.c_act - c0;
       ++steps_all;
       const eth::EBlock& h = SL.L.B(P, M, hd);

@@ -40,7 +40,7 @@ __device__ inline void acc_episode(Acc& a, int64_t ra_fx, int64_t rd_fx, int64_t
   a.orphans += acts - head_height;
   a.tie += (status & CPR_ST_TIE) ? 1 : 0;
   a.overlap += (status & CPR_ST_OVERLAP) ? 1 : 0;
-  a.other += (status & ~(uint32_t)(CPR_ST_TIE | CPR_ST_OVERLAP)) ? 1 : 0;
+  a.other += (status & ~(uint32_t)(CPR_ST_TIE | CPR_ST_OVERLAP | CPR_ST_EXACT_RERUN)) ? 1 : 0;
   a.rel_fx += (uint64_t)__builtin_rint(rel * 4294967296.0);
   a.rel_sq_fx += (uint64_t)__builtin_rint(rel * rel * 4294967296.0);
   int bin = (int)(rel * (double)CPR_HIST_BINS);

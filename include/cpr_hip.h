@@ -147,8 +147,8 @@ enum cpr_nakamoto_action { CPR_ADOPT = 0, CPR_OVERRIDE = 1, CPR_MATCH = 2, CPR_W
 enum cpr_episode_status {
   CPR_ST_OK = 0u,
   CPR_ST_TIE = 1u,      /* a defender resolved an equal-time, equal-height delivery */
-  CPR_ST_OVERLAP = 2u,  /* an activation fired while finite-delay messages were in flight;
-                           the device resolves it by delivering first */
+  CPR_ST_OVERLAP = 2u,  /* Nakamoto: an activation fired while finite-delay messages were in
+                           flight; the episode is re-run exactly (CPR_ST_EXACT_RERUN) */
   CPR_ST_DEEP_FORK = 4u,      /* Nakamoto: private chain beyond its slots */
   CPR_ST_TIE_UNRESOLVED = 8u, /* Nakamoto: tie replay capacity exceeded */
   CPR_ST_STALE_TIME = 16u,    /* Nakamoto: head time older than the time log */
@@ -160,9 +160,14 @@ enum cpr_episode_status {
                                  (List.for_all2 in summary dedup, Division_by_zero in
                                  n_choose_k, assert false in heuristic_quorum); the episode
                                  stops, outputs not valid */
-  CPR_ST_TRACE_MISS = 128u      /* cpr_replay: the episode needed a draw its trace does not
+  CPR_ST_TRACE_MISS = 128u,     /* cpr_replay: the episode needed a draw its trace does not
                                  hold (too few activations, a missing delay key); outputs
                                  not valid */
+  CPR_ST_EXACT_RERUN = 256u     /* Nakamoto fused episodes (cpr_run_episodes, cpr_replay): the
+                                 closed-form lane flagged the episode (OVERLAP, DEEP_FORK,
+                                 TIE_UNRESOLVED, STALE_TIME) and it was simulated again on the
+                                 exact event engine; its outputs are that
+                                 re-run's, and the lane's flags are kept beside this bit */
 };
 
 typedef struct cpr_config {
@@ -286,8 +291,10 @@ int cpr_batch_destroy(cpr_batch* b);
 int cpr_run_episodes(cpr_batch* b, int64_t n_episodes, uint64_t first_episode,
                      cpr_summary* summary, cpr_episode_record* records,
                      int records_on_device);
-/* Same, asynchronous on the context's stream; summary must be a device pointer to a
- * zeroed cpr_summary and records (optional) a device pointer. */
+/* Same, asynchronous on the context's streams; summary must be a device pointer to a
+ * zeroed cpr_summary and records (optional) a device pointer. Both are complete after
+ * cpr_synchronize (Nakamoto: exact re-runs of flagged episodes, CPR_ST_EXACT_RERUN, run on
+ * the context's second stream). */
 int cpr_run_episodes_async(cpr_batch* b, int64_t n_episodes, uint64_t first_episode,
                            cpr_summary* summary_dev, cpr_episode_record* records_dev);
 int cpr_synchronize(cpr_ctx* ctx);
@@ -300,7 +307,8 @@ int cpr_synchronize(cpr_ctx* ctx);
 int cpr_replay(cpr_batch* b, const cpr_trace* trace, cpr_summary* summary,
                cpr_episode_record* records, int records_on_device);
 /* device time (HIP events on the context's stream) of the last episode-kernel launch of
- * this batch, and the activations it simulated (valid after cpr_run_episodes returns) */
+ * this batch, and the activations it simulated (valid after cpr_run_episodes returns;
+ * after cpr_run_episodes_async + cpr_synchronize the time is valid and activations is -1) */
 int cpr_last_launch(cpr_batch* b, double* kernel_ms, int64_t* activations);
 
 /* Lockstep env API over cfg->n_lanes lanes (host pointers).

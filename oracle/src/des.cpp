@@ -866,7 +866,8 @@ GymNakamoto::GymNakamoto(const GymParams& p_, int mode, OcamlRandom* oc, uint64_
   std::string e = gym_params_error(p);
   if (!e.empty()) throw std::invalid_argument(e);
   // engine.ml:100-107
-  net = Network::selfish_mining(p.alpha, p.activation_delay, p.gamma, 1e-9, p.defenders);
+  net = Network::selfish_mining(p.alpha, p.activation_delay, p.gamma, p.propagation_delay,
+                                p.defenders);
 }
 
 // engine.ml:108-121

@@ -344,6 +344,9 @@ struct GymParams {
   double max_progress = 1.0 / 0.0;
   double max_time = 1.0 / 0.0;
   bool unit_obs = true;
+  // defender<->defender delay of Network.T.selfish_mining; the gym passes 1e-9
+  // (engine.ml:100-107), other values exercise overlapping delivery windows in tests
+  double propagation_delay = 1e-9;
 };
 
 struct StepInfo {

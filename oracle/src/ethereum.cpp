@@ -334,7 +334,8 @@ GymEthereum::GymEthereum(const GymParams& p_, int scheme_, int mode, OcamlRandom
     : p(p_), scheme(scheme_), rng_mode(mode), ocaml(oc), seed(seed_), episode(ep) {
   std::string e = gym_params_error(p);
   if (!e.empty()) throw std::invalid_argument(e);
-  net = Network::selfish_mining(p.alpha, p.activation_delay, p.gamma, 1e-9, p.defenders);
+  net = Network::selfish_mining(p.alpha, p.activation_delay, p.gamma, p.propagation_delay,
+                                p.defenders);
 }
 
 // engine.ml:108-121

@@ -674,7 +674,8 @@ GymTailstorm::GymTailstorm(const GymParams& p_, int k_, int scheme_, int selecti
   std::string e = gym_params_error(p);
   if (!e.empty()) throw std::invalid_argument(e);
   if (k < 1) throw std::invalid_argument("k must be positive");
-  net = Network::selfish_mining(p.alpha, p.activation_delay, p.gamma, 1e-9, p.defenders);
+  net = Network::selfish_mining(p.alpha, p.activation_delay, p.gamma, p.propagation_delay,
+                                p.defenders);
 }
 
 Kind GymTailstorm::skip_to_interaction(Block** blk) {

@@ -102,6 +102,51 @@ def test_tie_windows_replayed_exactly(ctx):
     assert int(((rec["status"] & L.ST_TIE_UNRESOLVED) != 0).sum()) == 0
 
 
+@pytest.mark.parametrize("alpha,policy,table", [(0.35, L.POLICY_SAPIRSHTEIN_2016_SM1, False),
+                                                (0.5, L.POLICY_SAPIRSHTEIN_2016_SM1, False),
+                                                (0.35, L.POLICY_EYAL_SIRER_2014, False),
+                                                (0.45, L.POLICY_TABLE, True)])
+def test_overlapping_windows_rerun_exactly(ctx, alpha, policy, table):
+    # Activations that fire while the previous window's messages are in flight: with the
+    # gym's 1e-9 propagation delay ~1e-9 of activations, here made common by a 0.05 delay
+    # (network.ml selfish_mining ~propagation_delay). The closed-form lane flags them and
+    # the library re-runs those episodes on the exact event engine (Nakamoto mode of the
+    # Ethereum lane); every record must equal the oracle's, which follows the reference's
+    # event queue, and the summary must equal the sum over the records.
+    tab = None
+    if table:
+        tab = np.random.default_rng(3).integers(0, 4, size=12 * 12 * 2).astype(np.uint8)
+    cfg, keep = device.make_config(alpha=alpha, gamma=0.5, policy=policy, max_steps=400,
+                                   seed=0x0E7, propagation_delay=0.05, table=tab)
+    b = device.Batch(cfg, ctx=ctx, keep=keep)
+    s, rec = b.run(768, first_episode=0, records=True)
+    ref = O.run_episodes(cfg, 0, 768, threads=8)
+    assert _records_equal(rec, ref) == {}
+    flagged = (rec["status"] & L.ST_OVERLAP) != 0
+    assert flagged.sum() > 100  # the case is actually exercised
+    assert ((rec["status"][flagged] & L.ST_EXACT_RERUN) != 0).all()
+    assert ((ref["status"][flagged] & L.ST_OVERLAP) != 0).all()
+    assert s.episodes == 768 and s.status_overlap == int(flagged.sum())
+    assert s.steps == int(rec["n_steps"].sum())
+    assert s.activations == int(rec["n_activations"].sum())
+    assert s.reward_attacker_fx == int((rec["reward_attacker"] * 2**20).sum())
+    assert s.orphans == int((rec["n_activations"] - rec["head_height"]).sum())
+    assert s.status_other == 0
+
+
+def test_gym_overlaps_at_the_reference_delay(ctx):
+    # at the gym's own 1e-9 delay overlaps are rare (~1 per 5e8 activations at gamma 0.5);
+    # whatever the device flags in 2^16 full episodes was re-run and matches the oracle
+    cfg, keep = device.make_config(alpha=0.45, gamma=0.5, policy=L.POLICY_SAPIRSHTEIN_2016_SM1,
+                                   max_steps=2016, seed=0x5EED0000)
+    b = device.Batch(cfg, ctx=ctx, keep=keep)
+    _, rec = b.run(1 << 16, first_episode=0, records=True)
+    idx = np.nonzero(rec["status"] & (L.ST_OVERLAP | L.ST_EXACT_RERUN))[0]
+    for e in idx[:8]:
+        ref = O.run_episodes(cfg, int(e), 1, threads=1)
+        assert _records_equal(rec[e:e + 1], ref) == {}, int(e)
+
+
 @pytest.mark.parametrize("policy", [0, 1, 2, 3])
 @pytest.mark.parametrize("alpha", [0.1, 0.33, 0.45])
 def test_loop_two_agents_bit_exact(ctx, alpha, policy):
