@@ -52,6 +52,7 @@ ETH_POLICY_FN19 = 3
 ETH_POLICY_FN19PKEL = 4
 NET_SELFISH_MINING = 0
 NET_TWO_AGENTS = 1
+NET_HONEST_CLIQUE = 2
 MODE_GYM = 0
 MODE_LOOP = 1
 
@@ -97,6 +98,8 @@ class Config(ctypes.Structure):
         ("n_lanes", ctypes.c_int64),
         ("k", ctypes.c_int32),
         ("subblock_selection", ctypes.c_int32),
+        ("delay_lo", ctypes.c_double),
+        ("delay_hi", ctypes.c_double),
     ]
 
 

@@ -71,6 +71,7 @@ struct cpr_batch {
   eth::EthParams EP;     // CPR_PROTO_ETHEREUM
   DevBuf eth_mem;        // lanes x eth_lane_bytes
   bool is_eth = false;   // Ethereum lockstep lanes share bk_lmem / bk_slots
+  bool nak_ev = false;   // Nakamoto on an honest clique: Ethereum lanes in Nakamoto mode (EP)
   int64_t eth_bytes = 0;
   bk::BkParams BP;       // CPR_PROTO_BK
   DevBuf bk_mem;         // fused episodes: lanes x bk_bytes
@@ -179,6 +180,17 @@ static int validate(const cpr_config* c, NakParams* P, eth::EthParams* EP, bk::B
   if (c->protocol == CPR_PROTO_TAILSTORM) return validate_ts(c, TP);
   if (c->protocol != CPR_PROTO_NAKAMOTO)
     return fail(CPR_E_UNSUPPORTED, "protocol not implemented on the device yet");
+  if (c->network == CPR_NET_HONEST_CLIQUE) {
+    // every node honest: the event engine in Nakamoto mode (no closed form for cliques)
+    cpr_config c2 = *c;
+    c2.protocol = CPR_PROTO_ETHEREUM;
+    c2.policy = CPR_ETH_POLICY_HONEST;
+    c2.reward_scheme = CPR_REWARD_CONSTANT;
+    const int rc = validate_eth(&c2, EP);
+    if (rc) return rc;
+    EP->nak = 1;
+    return CPR_OK;
+  }
   if (std::isnan(c->activation_delay)) return fail(CPR_E_INVALID_ARG, "activation_delay cannot be NaN");
   if (std::isnan(c->alpha)) return fail(CPR_E_INVALID_ARG, "alpha cannot be NaN");
   if (std::isnan(c->gamma)) return fail(CPR_E_INVALID_ARG, "gamma cannot be NaN");
@@ -285,6 +297,27 @@ static int validate_eth(const cpr_config* c, eth::EthParams* P) {
       return fail(CPR_E_UNSUPPORTED, "the gym engine always uses the selfish-mining network");
     P->d = 1;
     P->net = 1;
+  } else if (c->network == CPR_NET_HONEST_CLIQUE) {
+    // models.ml:3-28: n honest nodes with compute i + 1, uniform link delays
+    if (c->mode != CPR_MODE_LOOP)
+      return fail(CPR_E_UNSUPPORTED, "honest cliques run Simulator.loop tasks (CPR_MODE_LOOP)");
+    if (c->defenders < 2 || c->defenders > 64)
+      return fail(CPR_E_INVALID_ARG, "honest clique: 2..64 nodes (cfg.defenders)");
+    const bool dflt = c->delay_lo == 0. && c->delay_hi == 0.;
+    const double lo = dflt ? 0.5 : c->delay_lo, hi = dflt ? 1.5 : c->delay_hi;
+    if (!(lo >= 0.) || !(hi >= lo)) return fail(CPR_E_INVALID_ARG, "delay_lo/delay_hi");
+    P->d = c->defenders - 1;
+    P->net = 2;
+    P->lo = lo;
+    P->hi = hi;
+    // the keyed miner draw for weights 1..n, as the oracle's weight_thresholds
+    double total = 0.0, cum = 0.0;
+    for (int i = 0; i < c->defenders; ++i) total += (double)(i + 1);
+    for (int i = 0; i + 1 < c->defenders; ++i) {
+      cum += (double)(i + 1);
+      const double t = cum / total * 4294967296.0;
+      P->thr[i] = t <= 0.0 ? 0u : (t >= 4294967295.0 ? 4294967295u : (uint32_t)t);
+    }
   } else {
     return fail(CPR_E_INVALID_ARG, "unknown network");
   }
@@ -489,6 +522,7 @@ int cpr_batch_create(cpr_ctx* ctx, const cpr_config* cfg, cpr_batch** out) {
   if (cfg->protocol == CPR_PROTO_TAILSTORM) b->bk_bytes = ts::ts_lane_bytes(TP);
   b->is_ev = cfg->protocol == CPR_PROTO_BK || cfg->protocol == CPR_PROTO_TAILSTORM;
   b->is_eth = cfg->protocol == CPR_PROTO_ETHEREUM;
+  b->nak_ev = cfg->protocol == CPR_PROTO_NAKAMOTO && cfg->network == CPR_NET_HONEST_CLIQUE;
   b->cfg.policy_table = nullptr;
   if (cfg->protocol == CPR_PROTO_BK && cfg->policy == CPR_BK_POLICY_TABLE) {
     const size_t D = (size_t)cfg->policy_table_dim, K1 = (size_t)cfg->k + 1;
@@ -522,7 +556,7 @@ int cpr_batch_create(cpr_ctx* ctx, const cpr_config* cfg, cpr_batch** out) {
   }
   b->P.table = (const uint8_t*)b->table_dev.p;
   b->BP.table = (const uint8_t*)b->table_dev.p;
-  if (cfg->protocol == CPR_PROTO_NAKAMOTO) {
+  if (cfg->protocol == CPR_PROTO_NAKAMOTO && !b->nak_ev) {
     // the same episode on the exact event engine: Ethereum lane, no uncles, nakamoto_ssz
     // policy (validated above); configurations it cannot hold keep the lane's flags
     cpr_config c2 = *cfg;
@@ -676,7 +710,7 @@ static int run_async_bk(cpr_batch* b, int64_t n, uint64_t first, const TraceSour
 // tr == NULL: episodes [first, first + n) of the keyed stream; else trace episodes [0, n)
 static int run_async(cpr_batch* b, int64_t n, uint64_t first, const TraceSource* tr,
                      cpr_summary* sum_dev, cpr_episode_record* rec_dev) {
-  if (b->cfg.protocol == CPR_PROTO_ETHEREUM)
+  if (b->cfg.protocol == CPR_PROTO_ETHEREUM || b->nak_ev)
     return run_async_eth(b, n, first, tr, sum_dev, rec_dev);
   if (b->is_ev) return run_async_bk(b, n, first, tr, sum_dev, rec_dev);
   const int64_t lanes = episode_lanes(b, n);

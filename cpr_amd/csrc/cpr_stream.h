@@ -155,6 +155,19 @@ struct Stream {
   __host__ __device__ inline int32_t pow(uint32_t serial) const {
     return (int32_t)(block(serial, TAG_POW).w0 & 0x3FFFFFFFu);
   }
+  // miner of activation j for arbitrary compute weights (honest cliques): the first node
+  // i with w0 < thr[i] (thr: n - 1 cumulative thresholds, see cpr_weight_thresholds)
+  __host__ __device__ inline int32_t miner_w(uint32_t j, const uint32_t* thr, int32_t nthr) const {
+    const uint32_t w0 = block(j, TAG_ACT).w0;
+    int32_t i = 0;
+    while (i < nthr && w0 >= thr[i]) ++i;
+    return i;
+  }
+  // U(lo, hi) delay of the message shared at (kw, off) to dest (distributions.ml:114-118)
+  __host__ __device__ inline double link_unif(uint32_t kw, uint32_t off, uint32_t dest, double lo,
+                                              double hi) const {
+    return link_u(kw, off, dest) * (hi - lo) + lo;
+  }
   // U(0, dmax) link delays (network.ml:68-76)
   __host__ __device__ inline double link(uint32_t kw, uint32_t off, uint32_t dest,
                                          double dmax) const {
@@ -207,6 +220,13 @@ struct TraceStream {
     miss = 1u;
     *miner_out = 0;
     return 1.0;
+  }
+  __host__ __device__ inline int32_t miner_w(uint32_t j, const uint32_t*, int32_t) const {
+    return miner(j, 0, 0);
+  }
+  __host__ __device__ inline double link_unif(uint32_t kw, uint32_t off, uint32_t dest, double,
+                                              double) const {
+    return lookup(trace_link_key(kw, off, dest));
   }
   __host__ __device__ inline int32_t pow(uint32_t serial) const {
     if (serial < (uint32_t)n_pow) return pow_hash[serial];

@@ -67,7 +67,7 @@ static_assert(sizeof(HNode) == 24, "HNode layout");
 struct EthParams {
   uint64_t t_att;
   int32_t d, n;  // defenders, nodes
-  int32_t net;   // 0 selfish mining, 1 two agents
+  int32_t net;   // 0 selfish mining, 1 two agents, 2 honest clique (all nodes honest)
   int32_t mode;  // 0 gym, 1 loop
   int32_t policy, scheme;
   int32_t cap_b, cap_e;
@@ -79,6 +79,9 @@ struct EthParams {
   // reduce to nakamoto.ml / nakamoto_ssz.ml; the nakamoto_ssz policy (or table) decides
   int32_t nak, table_dim;
   const uint8_t* table;
+  // honest clique (net 2): keyed miner thresholds (n - 1) and uniform link delays
+  double lo, hi;
+  uint32_t thr[64];
 };
 
 constexpr int32_t NCAND = 32, NQ = 32, NSTACK = 64;
@@ -321,6 +324,7 @@ struct EthLane {
   // ------------------------------------------------------------------ randomness
   template <class St>
   __host__ __device__ inline int32_t miner_of(const EthParams& P, const St& S, int32_t k) {
+    if (P.net == 2) return S.miner_w((uint32_t)k, P.thr, P.n - 1);
     return S.miner((uint32_t)k, P.t_att, P.d);
   }
   template <class St>
@@ -825,7 +829,7 @@ struct EthLane {
         break;
       }
       case EV_ON: {
-        if (node == 0) {
+        if (node == 0 && P.net != 2) {
           // loop mode: the attacker node's handler (ethereum_ssz.ml:433-441)
           prepare(P, M, kind, s);
           const EthObs o = observe(P, M, false);
@@ -841,7 +845,7 @@ struct EthLane {
       }
       case EV_CLOCK: {
         const int32_t m = miner_of(P, S, c_act);
-        if (m == 0) {
+        if (m == 0 && P.net != 2) {
           ++act0;
           dr_node = 0;
           if (P.mode == 1) dr = payload(P, M, 0, priv, F_MINING, own, foreign);
@@ -864,7 +868,10 @@ struct EthLane {
         for (int32_t dst = 0; dst < P.n; ++dst) {
           if (dst == node) continue;
           double delay;
-          if (P.net == 1)
+          if (P.net == 2)  // models.ml:4 uniform propagation delays on every link
+            delay = S.link_unif((uint32_t)b.share_k, (uint32_t)b.share_off, (uint32_t)dst, P.lo,
+                                P.hi);
+          else if (P.net == 1)
             delay = 0.0;
           else if (node == 0)
             delay = S.link((uint32_t)b.share_k, (uint32_t)b.share_off, (uint32_t)dst, P.dmax);
@@ -998,7 +1005,7 @@ struct EthLane {
       }
       handle(P, S, M, ev, s);
     }
-    return head(P, M, priv);
+    return head(P, M, P.net == 2 ? M.tips[0] : priv);
   }
 };
 

@@ -24,6 +24,12 @@ __device__ inline void acc_add(Acc& a, const BRef& hd, int64_t steps, int64_t ac
   acc_episode(a, (int64_t)hd.ra << 20, (int64_t)(hd.h - hd.ra) << 20, (int64_t)hd.h << 20, rel,
               hd.h, steps, acts, status, hist_lds);
 }
+__device__ inline void acc_add(LdsAcc& a, const BRef& hd, int64_t steps, int64_t acts,
+                               uint32_t status, int32_t* hist_lds) {
+  const double rel = hd.h != 0 ? (double)hd.ra / (double)hd.h : 0.0;
+  a.episode((int64_t)hd.ra << 20, (int64_t)(hd.h - hd.ra) << 20, (int64_t)hd.h << 20, rel, hd.h,
+            steps, acts, status, hist_lds);
+}
 
 // One gym episode (engine.ml:164-249): reset = first activation up to the attacker's
 // interaction; step = apply, deliveries, next activation, observe; head at the end.
@@ -72,6 +78,9 @@ __global__ __launch_bounds__(kBlock) void k_run_episodes(
     int64_t* redo, uint32_t* redo_n, uint32_t launch_id, int64_t redo_cap) {
   __shared__ int32_t hist[CPR_HIST_BINS];
   __shared__ int32_t ring[RING * kBlock];
+  __shared__ unsigned long long acc_w[12];
+  LdsAcc acc{acc_w};
+  acc.init();
   if (threadIdx.x < CPR_HIST_BINS) hist[threadIdx.x] = 0;
   __syncthreads();
   const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -86,7 +95,6 @@ __global__ __launch_bounds__(kBlock) void k_run_episodes(
   M.tmask = P.tlog_len - 1;
   M.cap = P.cap;
   M.replay = ReplayMem::at(replay + tid * REPLAY_BYTES);
-  Acc acc = {};
   NakLane L;
   for (int64_t e = tid; e < n_eps; e += nthreads) {
     const auto S = src.at(e);
@@ -124,7 +132,7 @@ __global__ __launch_bounds__(kBlock) void k_run_episodes(
     }
   }
   __syncthreads();
-  block_flush(acc, hist, sum);
+  acc.flush(hist, sum);
 }
 
 // ---- lockstep gym lanes (engine.reset / engine.step over n lanes)

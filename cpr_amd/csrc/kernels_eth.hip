@@ -69,7 +69,7 @@ __global__ __launch_bounds__(kBlock) void k_eth_run_episodes(
       r.head_height = h.height;
       r.head_miner = P.mode == CPR_MODE_GYM ? h.miner : -1;
       r.status = L.status;
-      r.head_work = h.work;
+      r.head_work = P.nak ? 0 : h.work;
       recs[e] = r;
     }
   }

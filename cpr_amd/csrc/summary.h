@@ -73,6 +73,47 @@ __device__ inline void block_flush(const Acc& a, int32_t* hist_lds, cpr_summary*
               (unsigned long long)hist_lds[threadIdx.x]);
 }
 
+// Accumulators in LDS instead of registers (the Nakamoto lane's 24 VGPRs of int64 sums
+// would otherwise stay live through every activation): one ds atomic per field per
+// finished episode into the workgroup's 12 words, then one global atomic per field.
+// Word order is cpr_summary's.
+struct LdsAcc {
+  unsigned long long* w;  // 12 words in LDS
+  __device__ inline void init() {
+    if (threadIdx.x < 12) w[threadIdx.x] = 0ull;
+  }
+  __device__ inline void episode(int64_t ra_fx, int64_t rd_fx, int64_t prog_fx, double rel,
+                                 int64_t head_height, int64_t steps, int64_t acts,
+                                 uint32_t status, int32_t* hist_lds) {
+    auto add = [&](int i, int64_t v) {
+      if (v) atomicAdd(&w[i], (unsigned long long)v);
+    };
+    add(0, 1);
+    add(1, steps);
+    add(2, acts);
+    add(3, ra_fx);
+    add(4, rd_fx);
+    add(5, prog_fx);
+    add(6, (int64_t)__builtin_rint(rel * 4294967296.0));
+    add(7, (int64_t)__builtin_rint(rel * rel * 4294967296.0));
+    add(8, acts - head_height);
+    add(9, (status & CPR_ST_TIE) ? 1 : 0);
+    add(10, (status & CPR_ST_OVERLAP) ? 1 : 0);
+    add(11, (status & ~(uint32_t)(CPR_ST_TIE | CPR_ST_OVERLAP | CPR_ST_EXACT_RERUN)) ? 1 : 0);
+    int bin = (int)(rel * (double)CPR_HIST_BINS);
+    bin = bin < 0 ? 0 : (bin >= CPR_HIST_BINS ? CPR_HIST_BINS - 1 : bin);
+    atomicAdd(&hist_lds[bin], 1);
+  }
+  // after __syncthreads()
+  __device__ inline void flush(const int32_t* hist_lds, cpr_summary* out) const {
+    if (threadIdx.x < 12 && w[threadIdx.x])
+      atomicAdd((unsigned long long*)out + threadIdx.x, w[threadIdx.x]);
+    if (threadIdx.x < CPR_HIST_BINS && hist_lds[threadIdx.x])
+      atomicAdd((unsigned long long*)&out->hist[threadIdx.x],
+                (unsigned long long)hist_lds[threadIdx.x]);
+  }
+};
+
 __device__ inline Stream make_stream(uint64_t seed, uint64_t ep) {
   Stream S;
   S.k0 = (uint32_t)seed;

@@ -84,6 +84,8 @@ def make_config(
     k=8,
     table_dim=None,
     subblock_selection=1,
+    delay_lo=0.0,
+    delay_hi=0.0,
 ):
     """Build a cpr_config. ``defenders=None`` applies the gym's rule
     d = max(2, ceil(1 / (1 - gamma))) (gym/ocaml/cpr_gym/envs.py:146-153).
@@ -113,6 +115,8 @@ def make_config(
     c.n_lanes = int(n_lanes)
     c.k = int(k)
     c.subblock_selection = int(subblock_selection)
+    c.delay_lo = float(delay_lo)
+    c.delay_hi = float(delay_hi)
     keep = None
     if table is not None and protocol == L.PROTO_BK:
         keep = np.ascontiguousarray(table, dtype=np.uint8).ravel()

@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define CPR_ABI_VERSION 4
+#define CPR_ABI_VERSION 5
 
 typedef struct cpr_ctx cpr_ctx;
 typedef struct cpr_batch cpr_batch;
@@ -123,7 +123,11 @@ enum cpr_ethereum_action_rank {
 
 enum cpr_network {
   CPR_NET_SELFISH_MINING = 0, /* network.ml:343-387, as the gym builds it (engine.ml:100-107) */
-  CPR_NET_TWO_AGENTS = 1      /* network.ml:332-341 */
+  CPR_NET_TWO_AGENTS = 1,     /* network.ml:332-341 */
+  CPR_NET_HONEST_CLIQUE = 2   /* experiments/simulate/models.ml:3-28 honest_clique: `defenders`
+                                 = n honest nodes (2..64), node i has compute i + 1, every
+                                 link delay uniform [delay_lo, delay_hi), simple
+                                 dissemination; CPR_MODE_LOOP, Nakamoto or Ethereum */
 };
 
 enum cpr_mode {
@@ -192,6 +196,7 @@ typedef struct cpr_config {
   int64_t n_lanes;           /* lockstep lanes for cpr_reset/cpr_step; 0 = none */
   int32_t k;                 /* B_k / Tailstorm: votes per block (bk.ml:7), >= 1 */
   int32_t subblock_selection;/* Tailstorm: enum cpr_subblock_selection */
+  double delay_lo, delay_hi;  /* CPR_NET_HONEST_CLIQUE link delays; 0, 0 = 0.5, 1.5 (models.ml) */
 } cpr_config;
 
 /* one finished episode; identical layout is produced by the CPU oracle */

@@ -210,17 +210,27 @@ double OcamlSimRng::link_delay(const Link& l, const Block*) {
   return 0.0;
 }
 
-KeyedSimRng::KeyedSimRng(uint64_t seed, uint64_t episode, const Network& net)
+KeyedSimRng::KeyedSimRng(uint64_t seed, uint64_t episode, const Network& net,
+                         bool general_weights)
     : ks(seed, episode) {
   ev = net.activation_delay;
   d = (int)net.nodes.size() - 1;
   t_att = alpha_threshold(net.nodes[0].compute);
+  if (general_weights) {
+    std::vector<double> w;
+    for (const NetNode& x : net.nodes) w.push_back(x.compute);
+    thr = weight_thresholds(w);
+    return;
+  }
   for (int i = 2; i < (int)net.nodes.size(); i++)
     if (net.nodes[i].compute != net.nodes[1].compute)
       throw std::invalid_argument("keyed stream needs equal-weight defenders");
 }
 
-int KeyedSimRng::miner(int k) { return ks.miner((uint32_t)k, t_att, d); }
+int KeyedSimRng::miner(int k) {
+  if (!thr.empty()) return ks.miner_w((uint32_t)k, thr);
+  return ks.miner((uint32_t)k, t_att, d);
+}
 
 double KeyedSimRng::act_delay(int j) {
   double x = -1. * ev * cpr_log(ks.act_u((uint32_t)j));

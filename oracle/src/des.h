@@ -162,7 +162,8 @@ struct KeyedSimRng : SimRng {
   int d;
   double ev;
   bool serial_links = false;  // key link delays by (message serial, dest): TAG_MSG
-  KeyedSimRng(uint64_t seed, uint64_t episode, const Network& net);
+  std::vector<uint32_t> thr;  // general_weights: keyed miner thresholds (honest cliques)
+  KeyedSimRng(uint64_t seed, uint64_t episode, const Network& net, bool general_weights = false);
   int miner(int k) override;
   double act_delay(int j) override;
   int32_t pow_bits(int serial) override;

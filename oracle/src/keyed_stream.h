@@ -29,6 +29,7 @@
 #pragma once
 #include <cstdint>
 #include <cstring>
+#include <vector>
 
 namespace oracle {
 
@@ -136,6 +137,22 @@ static inline double cpr_log(double x) {
   return dk * ln2_hi - ((s * (f - R) - dk * ln2_lo) - f);
 }
 
+// cumulative compute thresholds of the keyed miner draw for arbitrary weights:
+// thr[i] = floor(sum_{j<=i} w_j / sum w * 2^32), i < n - 1 (fp64, clamped like the
+// attacker threshold); the device computes the same table on the host (capi.hip)
+inline std::vector<uint32_t> weight_thresholds(const std::vector<double>& w) {
+  double total = 0.0;
+  for (double x : w) total += x;
+  std::vector<uint32_t> thr;
+  double cum = 0.0;
+  for (size_t i = 0; i + 1 < w.size(); ++i) {
+    cum += w[i];
+    const double t = cum / total * 4294967296.0;
+    thr.push_back(t <= 0.0 ? 0u : (t >= 4294967295.0 ? 4294967295u : (uint32_t)t));
+  }
+  return thr;
+}
+
 struct KeyedStream {
   uint32_t key[2];
   uint32_t ep[2];
@@ -155,6 +172,15 @@ struct KeyedStream {
     block(j, TAG_ACT, w);
     if ((uint64_t)w[0] < t_att) return 0;
     return 1 + (int)(((uint64_t)w[1] * (uint64_t)d) >> 32);
+  }
+  // miner of activation j for arbitrary compute weights (honest cliques): the first node i
+  // with w0 < thr[i], thr = weight_thresholds(...) (n - 1 entries; the last node otherwise)
+  int miner_w(uint32_t j, const std::vector<uint32_t>& thr) const {
+    uint32_t w[4];
+    block(j, TAG_ACT, w);
+    int i = 0;
+    while (i < (int)thr.size() && w[0] >= thr[i]) ++i;
+    return i;
   }
   double act_u(uint32_t j) const {
     uint32_t w[4];

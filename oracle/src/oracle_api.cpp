@@ -71,6 +71,66 @@ void oracle_nak_obs_of_floats(const double in[4], int unit, int32_t out[4]) {
 // (experiments/simulate/models.ml:29-46, withholding.ml:90-108, csv_runner.ml:244-265)
 // rng_mode 0: OCaml Random state `rng` (carried over between calls like a Parany worker)
 // rng_mode 1: keyed stream (seed, episode)
+// Simulator.loop task on experiments/simulate/models.ml:3-28 honest_clique: n honest nodes,
+// compute i + 1, links to every other node with uniform [lo, hi) propagation delays,
+// simple dissemination. proto 0 Nakamoto, 1 Ethereum (Byzantium, scheme). Keyed mode uses
+// the general-weight miner draw (weight_thresholds). Outputs per node (n entries).
+int oracle_clique_task(int proto, int rng_mode, void* rng, uint64_t seed, uint64_t episode,
+                       int n, double activation_delay, double lo, double hi, int scheme,
+                       int activations, int64_t* acts_out, double* rewards_out,
+                       double* head_time, double* head_progress, int32_t* head_height,
+                       int32_t* head_miner, int32_t* head_work) {
+  try {
+    Network net;
+    net.flooding = false;
+    net.activation_delay = activation_delay;
+    net.nodes.resize(n);
+    for (int i = 0; i < n; ++i) {
+      net.nodes[i].compute = (double)(i + 1);
+      for (int j = 0; j < n - 1; ++j)
+        net.nodes[i].links.push_back(Link{j >= i ? j + 1 : j, D_UNIFORM, lo, hi});
+    }
+    std::unique_ptr<SimRng> r;
+    if (rng_mode == 0)
+      r.reset(new OcamlSimRng((OcamlRandom*)rng, net));
+    else
+      r.reset(new KeyedSimRng(seed, episode, net, true));
+    r = trace_wrap(std::move(r), net, false);
+    Sim sim(net, r.get());
+    std::vector<std::unique_ptr<NodeImpl>> nodes;
+    if (proto == 1) {
+      sim.proto = 1;
+      sim.eth_scheme = scheme;
+      for (int i = 0; i < n; ++i) nodes.emplace_back(new EthHonest());
+    } else {
+      for (int i = 0; i < n; ++i) nodes.emplace_back(new NakHonest());
+    }
+    sim.init(std::move(nodes));
+    Block* root = sim.roots.back();
+    for (int i = 0; i < n; ++i) {
+      if (proto == 1)
+        static_cast<EthHonest*>(sim.nodes[i].get())->state = root;
+      else
+        static_cast<NakHonest*>(sim.nodes[i].get())->state = root;
+    }
+    sim.loop(activations);
+    Block* h = sim.head();
+    for (int i = 0; i < n; i++) {
+      acts_out[i] = sim.activations[i];
+      rewards_out[i] = h->rewards[i];
+    }
+    *head_time = Sim::timestamp(h);
+    *head_progress = sim.progress(h);
+    *head_height = h->value.height;
+    *head_miner = h->value.miner;
+    *head_work = h->value.work;
+    return 0;
+  } catch (std::exception& e) {
+    set_err(e.what());
+    return -1;
+  }
+}
+
 int oracle_two_agents_task(int rng_mode, void* rng, uint64_t seed, uint64_t episode,
                            double alpha, int policy, int activations, int64_t acts_out[2],
                            double rewards_out[2], double* head_time, double* head_progress,
@@ -463,8 +523,36 @@ static int run_loop_episode(const cpr_config* c, uint64_t ep, cpr_episode_record
   double rew[2], ht, hp;
   int32_t hh;
   uint32_t diag = 0;
+  if (c->network == CPR_NET_HONEST_CLIQUE &&
+      (c->protocol == CPR_PROTO_NAKAMOTO || c->protocol == CPR_PROTO_ETHEREUM)) {
+    const int n = c->defenders;
+    const bool dflt = c->delay_lo == 0. && c->delay_hi == 0.;
+    std::vector<int64_t> a(n);
+    std::vector<double> r(n);
+    double ht, hp;
+    int32_t hh, hm, hw;
+    if (oracle_clique_task(c->protocol == CPR_PROTO_ETHEREUM ? 1 : 0, 1, nullptr, c->seed, ep, n,
+                           c->activation_delay, dflt ? 0.5 : c->delay_lo,
+                           dflt ? 1.5 : c->delay_hi, c->reward_scheme, (int)c->activations,
+                           a.data(), r.data(), &ht, &hp, &hh, &hm, &hw) != 0)
+      return -1;
+    rec->reward_attacker = r[0];
+    rec->reward_defender = 0.0;
+    rec->n_activations = 0;
+    for (int i = 1; i < n; ++i) rec->reward_defender += r[i];
+    for (int i = 0; i < n; ++i) rec->n_activations += a[i];
+    rec->progress = hp;
+    rec->chain_time = ht;
+    rec->sim_time = 0.0;
+    rec->n_steps = 0;
+    rec->head_height = hh;
+    rec->head_miner = -1;
+    rec->status = 0;
+    rec->head_work = c->protocol == CPR_PROTO_ETHEREUM ? hw : 0;
+    return 0;
+  }
   if (c->network != CPR_NET_TWO_AGENTS) {
-    set_err("oracle loop mode: two-agents network only");
+    set_err("oracle loop mode: two-agents network or honest clique only");
     return -2;
   }
   if (c->protocol == CPR_PROTO_TAILSTORM) {

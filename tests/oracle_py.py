@@ -57,6 +57,12 @@ def lib():
             ctypes.c_int, vp, vp, P(ctypes.c_double), P(ctypes.c_double), P(ctypes.c_int32),
             P(ctypes.c_uint32),
         ]
+        L.oracle_clique_task.argtypes = [
+            ctypes.c_int, ctypes.c_int, vp, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_int,
+            ctypes.c_double, ctypes.c_double, ctypes.c_double, ctypes.c_int, ctypes.c_int, vp,
+            vp, P(ctypes.c_double), P(ctypes.c_double), P(ctypes.c_int32), P(ctypes.c_int32),
+            P(ctypes.c_int32),
+        ]
         L.oracle_gym_new.restype = vp
         L.oracle_gym_new.argtypes = [P(C.Config), ctypes.c_int, vp, ctypes.c_uint64]
         L.oracle_gym_free.argtypes = [vp]
@@ -146,6 +152,27 @@ def two_agents_task(alpha, policy, activations, rng=None, seed=0, episode=0):
     )
     return dict(activations=acts.tolist(), reward=rew.tolist(), head_time=ht.value,
                 head_progress=hp.value, head_height=hh.value, diag=dg.value)
+
+
+def clique_task(protocol, n, activation_delay, activations, scheme=1, lo=0.5, hi=1.5, rng=None,
+                seed=0, episode=0):
+    """Simulator.loop task on models.ml:3-28 honest_clique (n honest nodes, compute i + 1,
+    uniform [lo, hi) link delays); protocol "nakamoto" or "ethereum" (Byzantium, scheme)."""
+    acts = np.zeros(n, dtype=np.int64)
+    rew = np.zeros(n, dtype=np.float64)
+    ht, hp = ctypes.c_double(), ctypes.c_double()
+    hh, hm, hw = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32()
+    check(
+        lib().oracle_clique_task(
+            1 if protocol == "ethereum" else 0, 0 if rng is not None else 1,
+            rng.h if rng is not None else None, seed, episode, n, activation_delay, lo, hi,
+            scheme, activations, acts.ctypes.data, rew.ctypes.data, ctypes.byref(ht),
+            ctypes.byref(hp), ctypes.byref(hh), ctypes.byref(hm), ctypes.byref(hw),
+        )
+    )
+    return dict(activations=acts.tolist(), reward=rew.tolist(), head_time=ht.value,
+                head_progress=hp.value, head_height=hh.value, head_miner=hm.value,
+                head_work=hw.value)
 
 
 def keyed_block(seed, episode, idx, tag):

@@ -1,0 +1,49 @@
+"""Honest cliques (experiments/simulate/models.ml:3-28) in the oracle, pinned by the
+reference's own recorded outputs: every Nakamoto and Ethereum row of data/honest_net.tsv
+(10 nodes, compute 1..10, uniform 0.5..1.5 delays, 10,000 activations; each task starts from
+OCaml's default Random state) reproduces bit for bit with the OCaml 4.12 Random replica —
+activations and reward of every node, head time to the TSV's 12 digits, head progress and
+height. Fixture: tests/golden/honest_net_clique.json (make_honest_net_fixture.py)."""
+
+import json
+import pathlib
+
+import numpy as np
+import pytest
+
+import oracle_py as O
+
+ROWS = json.loads((pathlib.Path(__file__).parent / "golden" / "honest_net_clique.json")
+                  .read_text())["rows"]
+
+
+def _scheme(row):
+    return 1 if row["incentive_scheme"] == "discount" else 0
+
+
+@pytest.mark.parametrize("row", ROWS, ids=[f"line{r['line']}" for r in ROWS])
+def test_honest_net_rows_exact(row):
+    out = O.clique_task(row["protocol"], row["nodes"], row["activation_delay"],
+                        row["activations"], scheme=_scheme(row), rng=O.OcamlRandom())
+    assert out["activations"] == row["activations_per_node"]
+    assert out["reward"] == row["reward"]
+    assert float("%.12g" % out["head_time"]) == float(row["head_time"])
+    assert out["head_progress"] == row["head_progress"]
+    assert out["head_height"] == row["head_height"]
+
+
+def test_keyed_clique_statistics_match_reference_rows():
+    # the keyed stream is a different random source for the same model: orphan rates and
+    # reward shares of 24 keyed tasks bracket the reference's rows
+    for row in [r for r in ROWS if r["activation_delay"] in (30.0, 600.0)]:
+        orph, share = [], []
+        for ep in range(24):
+            out = O.clique_task(row["protocol"], row["nodes"], row["activation_delay"],
+                                row["activations"], scheme=_scheme(row), seed=7, episode=ep)
+            orph.append(1 - out["head_height"] / row["activations"])
+            share.append(out["reward"][-1] / sum(out["reward"]))
+        ref_orph = 1 - row["head_height"] / row["activations"]
+        ref_share = row["reward"][-1] / sum(row["reward"])
+        for xs, ref in ((orph, ref_orph), (share, ref_share)):
+            m, sd = float(np.mean(xs)), float(np.std(xs, ddof=1))
+            assert abs(ref - m) <= 4 * sd + 1e-4, (row["line"], ref, m, sd)
