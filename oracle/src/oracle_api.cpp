@@ -718,13 +718,17 @@ int oracle_bk_loop(int net_kind, int n_nodes, double alpha, double activation_de
     if (net_kind == 0) {
       net = Network::two_agents(activation_delay, alpha);
     } else {
+      // 1: symmetric clique, exponential(prop_ev) delays; 2: models.ml:3-28 honest_clique
+      // (compute i + 1, uniform 0.5 .. 1.5 delays)
       net.flooding = false;
       net.activation_delay = activation_delay;
       net.nodes.resize(n_nodes);
       for (int i = 0; i < n_nodes; ++i) {
-        net.nodes[i].compute = 1. / (double)n_nodes;
+        net.nodes[i].compute = net_kind == 2 ? (double)(i + 1) : 1. / (double)n_nodes;
         for (int j = 0; j < n_nodes - 1; ++j)
-          net.nodes[i].links.push_back(Link{j >= i ? j + 1 : j, D_EXP, prop_ev, 0.0});
+          net.nodes[i].links.push_back(net_kind == 2
+                                           ? Link{j >= i ? j + 1 : j, D_UNIFORM, 0.5, 1.5}
+                                           : Link{j >= i ? j + 1 : j, D_EXP, prop_ev, 0.0});
       }
     }
     BkTable t;
@@ -839,13 +843,17 @@ int oracle_ts_loop(int net_kind, int n_nodes, double alpha, double activation_de
     if (net_kind == 0) {
       net = Network::two_agents(activation_delay, alpha);
     } else {
+      // 1: symmetric clique, exponential(prop_ev) delays; 2: models.ml:3-28 honest_clique
+      // (compute i + 1, uniform 0.5 .. 1.5 delays)
       net.flooding = false;
       net.activation_delay = activation_delay;
       net.nodes.resize(n_nodes);
       for (int i = 0; i < n_nodes; ++i) {
-        net.nodes[i].compute = 1. / (double)n_nodes;
+        net.nodes[i].compute = net_kind == 2 ? (double)(i + 1) : 1. / (double)n_nodes;
         for (int j = 0; j < n_nodes - 1; ++j)
-          net.nodes[i].links.push_back(Link{j >= i ? j + 1 : j, D_EXP, prop_ev, 0.0});
+          net.nodes[i].links.push_back(net_kind == 2
+                                           ? Link{j >= i ? j + 1 : j, D_UNIFORM, 0.5, 1.5}
+                                           : Link{j >= i ? j + 1 : j, D_EXP, prop_ev, 0.0});
       }
     }
     TsLoopResult r;

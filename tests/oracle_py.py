@@ -556,7 +556,8 @@ def bk_loop(k, activations, *, net="clique", n_nodes=3, alpha=0.5, activation_de
     ht, hp = ctypes.c_double(), ctypes.c_double()
     hh, hs, nv = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int64()
     check(bk_lib().oracle_bk_loop(
-        0 if net == "two-agents" else 1, n, alpha, activation_delay, prop_ev,
+        {"two-agents": 0, "clique": 1, "honest-clique": 2}[net], n, alpha, activation_delay,
+        prop_ev,
         0 if rng is not None else 1, rng.h if rng is not None else None, seed, episode, k,
         scheme, BK_POLICIES.get(policy, policy), activations, rew.ctypes.data,
         acts.ctypes.data, ctypes.byref(ht), ctypes.byref(hp), ctypes.byref(hh),
@@ -673,7 +674,8 @@ def ts_loop(k, activations, *, net="clique", n_nodes=3, alpha=0.5, activation_de
     ht, hp = ctypes.c_double(), ctypes.c_double()
     hh, nv = ctypes.c_int32(), ctypes.c_int64()
     check(ts_lib().oracle_ts_loop(
-        0 if net == "two-agents" else 1, n, alpha, activation_delay, prop_ev,
+        {"two-agents": 0, "clique": 1, "honest-clique": 2}[net], n, alpha, activation_delay,
+        prop_ev,
         0 if rng is not None else 1, rng.h if rng is not None else None, seed, episode, k,
         TS_SCHEMES.get(scheme, scheme), TS_SELECTIONS.get(selection, selection),
         TS_POLICIES.get(policy, policy), activations, rew.ctypes.data, acts.ctypes.data,
