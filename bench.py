@@ -22,6 +22,8 @@ import time
 
 import numpy as np
 
+HERE = os.path.dirname(os.path.abspath(__file__))
+
 ALPHAS = [0.05, 0.10, 0.15, 0.20, 0.25, 0.30, 0.35, 0.40, 0.45, 0.50]
 GAMMAS = [0.0, 0.5]
 STEPS_PER_EPISODE = 2016
@@ -64,6 +66,34 @@ def cpu_baseline(seconds, points):
                   f"({dt:.1f} s, {threads} threads, oracle/src/des.cpp event-driven DES)",
         "episodes_per_s": eps / dt,
     }
+
+
+# algorithmic HBM bytes per activation of k_run_episodes: the f64 activation-time log
+# store; episode outputs add ~0.02 B
+ALG_BYTES_PER_ACT = 8.0
+
+
+def pmc_traffic(episodes):
+    """HBM bytes per k_run_episodes launch from the newest committed rocprofv3 PMC summary
+    of this same bench command (tools/profile.sh -> tools/summarize_profile.py:
+    FETCH_SIZE x1024 x2 gfx950 correction + WRITE_SIZE x1024), or None when no summary
+    for this launch size exists."""
+    import glob
+
+    for path in sorted(glob.glob(os.path.join(HERE, "profiles", "*_pmc_summary.json")),
+                       reverse=True):
+        try:
+            d = json.load(open(path))
+        except (OSError, ValueError):
+            continue
+        if d.get("kernel") != "k_run_episodes" or d.get("episodes_per_dispatch") != episodes:
+            continue
+        rd = d.get("hbm_read_bytes_per_dispatch (FETCH_SIZE x1024 x2, gfx950 correction)")
+        wr = d.get("hbm_write_bytes_per_dispatch (WRITE_SIZE x1024)")
+        if rd is None or wr is None:
+            continue
+        return rd + wr, os.path.relpath(path, HERE)
+    return None, None
 
 
 def main():
@@ -131,6 +161,7 @@ def main():
     # around the last launch of every point, on the stream the kernel runs on; activations
     # per launch = E episodes x (max_steps + 1) (every gym episode is exactly that long)
     kms = np.array([b.last_launch()[0] for b in batches])
+    traffic, traffic_src = pmc_traffic(E)
     kacts = np.full(len(batches), float(E * (STEPS_PER_EPISODE + 1)))
     act_per_s_kernel = float(kacts.sum() / (kms.sum() / 1e3))
     achieved = act_per_s_kernel * OPS_PER_ACTIVATION / 1e12
@@ -171,7 +202,9 @@ def main():
                 "peak": VALU_PEAK_TOPS,
                 "unit": "Tops/s (VALU lane-ops, 40 ops/activation cost model)",
                 "frac": achieved / VALU_PEAK_TOPS,
-                "traffic": None,
+                "traffic": traffic,
+                "traffic_source": traffic_src,
+                "algorithmic_bytes_per_launch": ALG_BYTES_PER_ACT * E * (STEPS_PER_EPISODE + 1),
                 "kernel": "k_run_episodes",
                 "kernel_ms_mean": float(kms.mean()),
                 "kernel_activations_per_s": act_per_s_kernel,
