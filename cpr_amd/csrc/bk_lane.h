@@ -71,7 +71,7 @@ static_assert(sizeof(HNode) == 24, "HNode layout");
 struct BkParams {
   uint64_t t_att;
   int32_t d, n;   // defenders, nodes
-  int32_t net;    // 0 selfish mining, 1 two agents
+  int32_t net;    // 0 selfish mining, 1 two agents, 2 honest clique (all nodes honest)
   int32_t mode;   // 0 gym, 1 loop
   int32_t policy, scheme, k;
   int32_t cap_v, cap_q, cap_e, cap_d;
@@ -80,6 +80,9 @@ struct BkParams {
   int64_t max_steps, activations;
   double max_progress, max_time;
   const uint8_t* table;  // device pointer (CPR_BK_POLICY_TABLE)
+  // honest clique (net 2, models.ml:3-28): keyed miner thresholds (n - 1), U(lo, hi) links
+  double lo, hi;
+  uint32_t thr[64];
 };
 
 constexpr int32_t NQS = 128;     // quorum candidates per block and list
@@ -391,6 +394,7 @@ struct BkLane {
   // ------------------------------------------------------------------ randomness
   template <class St>
   __host__ __device__ inline int32_t miner_of(const BkParams& P, const St& S, int32_t j) {
+    if (P.net == 2) return S.miner_w((uint32_t)j, P.thr, P.n - 1);
     return S.miner((uint32_t)j, P.t_att, P.d);
   }
   template <class St>
@@ -827,7 +831,7 @@ struct BkLane {
         break;
       }
       case EV_ON: {
-        if (node == 0) {
+        if (node == 0 && P.net != 2) {
           // loop mode: the attacker node's handler (bk_ssz.ml:334-343)
           prepare(P, M, kind, s);
           apply(P, M, bk_policy(P, observe(P, M)));
@@ -840,7 +844,7 @@ struct BkLane {
         zt = 0;
         const int32_t m = miner_of(P, S, c_act);
         int32_t parent;
-        if (m == 0) {
+        if (m == 0 && P.net != 2) {
           ++act0;
           parent = priv;  // gym: replaced at the Dag event (engine.ml:112-116)
         } else {
@@ -861,7 +865,9 @@ struct BkLane {
         for (int32_t dst = 0; dst < P.n; ++dst) {
           if (dst == node) continue;
           double delay;
-          if (P.net == 1)
+          if (P.net == 2)  // models.ml:4 uniform propagation delays on every link
+            delay = S.msg_unif((uint32_t)s, (uint32_t)dst, P.lo, P.hi);
+          else if (P.net == 1)
             delay = 0.0;
           else if (node == 0)
             delay = S.msg((uint32_t)s, (uint32_t)dst, P.dmax);
@@ -993,7 +999,7 @@ struct BkLane {
       }
       handle(P, S, M, ev, s);
     }
-    return head(P, M, priv);
+    return head(P, M, P.net == 2 ? M.tips[0] : priv);
   }
 };
 

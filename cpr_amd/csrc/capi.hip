@@ -170,6 +170,18 @@ static int32_t pow2_at_least(int64_t x, int32_t cap) {
 // engine.ml:37-51 and network.ml:343-358 (messages kept verbatim)
 static int validate_eth(const cpr_config* c, eth::EthParams* P);
 
+// the keyed miner draw for compute weights 1..n (models.ml:3-28), as the oracle's
+// weight_thresholds: thr[i] = floor(sum_{j<=i} w_j / sum w * 2^32), i < n - 1
+static void clique_thresholds(int n, uint32_t* thr) {
+  double total = 0.0, cum = 0.0;
+  for (int i = 0; i < n; ++i) total += (double)(i + 1);
+  for (int i = 0; i + 1 < n; ++i) {
+    cum += (double)(i + 1);
+    const double t = cum / total * 4294967296.0;
+    thr[i] = t <= 0.0 ? 0u : (t >= 4294967295.0 ? 4294967295u : (uint32_t)t);
+  }
+}
+
 static int validate_bk(const cpr_config* c, bk::BkParams* P);
 static int validate_ts(const cpr_config* c, ts::TsParams* P);
 
@@ -310,14 +322,7 @@ static int validate_eth(const cpr_config* c, eth::EthParams* P) {
     P->net = 2;
     P->lo = lo;
     P->hi = hi;
-    // the keyed miner draw for weights 1..n, as the oracle's weight_thresholds
-    double total = 0.0, cum = 0.0;
-    for (int i = 0; i < c->defenders; ++i) total += (double)(i + 1);
-    for (int i = 0; i + 1 < c->defenders; ++i) {
-      cum += (double)(i + 1);
-      const double t = cum / total * 4294967296.0;
-      P->thr[i] = t <= 0.0 ? 0u : (t >= 4294967295.0 ? 4294967295u : (uint32_t)t);
-    }
+    clique_thresholds(c->defenders, P->thr);
   } else {
     return fail(CPR_E_INVALID_ARG, "unknown network");
   }
@@ -406,6 +411,21 @@ static int validate_bk(const cpr_config* c, bk::BkParams* P) {
       return fail(CPR_E_UNSUPPORTED, "the gym engine always uses the selfish-mining network");
     P->d = 1;
     P->net = 1;
+  } else if (c->network == CPR_NET_HONEST_CLIQUE) {
+    // models.ml:3-28: n honest nodes with compute i + 1, uniform link delays; node 0 runs
+    // the honest protocol too (the policy is ignored)
+    if (c->mode != CPR_MODE_LOOP)
+      return fail(CPR_E_UNSUPPORTED, "honest cliques run Simulator.loop tasks (CPR_MODE_LOOP)");
+    if (c->defenders < 2 || c->defenders > 64)
+      return fail(CPR_E_INVALID_ARG, "honest clique: 2..64 nodes (cfg.defenders)");
+    const bool dflt = c->delay_lo == 0. && c->delay_hi == 0.;
+    const double lo = dflt ? 0.5 : c->delay_lo, hi = dflt ? 1.5 : c->delay_hi;
+    if (!(lo >= 0.) || !(hi >= lo)) return fail(CPR_E_INVALID_ARG, "delay_lo/delay_hi");
+    P->d = c->defenders - 1;
+    P->net = 2;
+    P->lo = lo;
+    P->hi = hi;
+    clique_thresholds(c->defenders, P->thr);
   } else {
     return fail(CPR_E_INVALID_ARG, "unknown network");
   }
@@ -480,6 +500,9 @@ static int validate_ts(const cpr_config* c, ts::TsParams* P) {
   P->activations = B.activations;
   P->max_progress = B.max_progress;
   P->max_time = B.max_time;
+  P->lo = B.lo;
+  P->hi = B.hi;
+  memcpy(P->thr, B.thr, sizeof(P->thr));
   // gym: one vertex per attacker interaction plus summaries; loop: ~ (1 + 1/k) per
   // activation. Vertex ring covers the whole episode up to 2^16 vertices.
   const int64_t span = c->mode == CPR_MODE_GYM

@@ -176,6 +176,11 @@ struct Stream {
   __host__ __device__ inline double msg(uint32_t serial, uint32_t dest, double dmax) const {
     return msg_u(serial, dest) * (dmax - 0.0) + 0.0;
   }
+  // U(lo, hi) delay of message `serial` to dest (B_k / Tailstorm on honest cliques)
+  __host__ __device__ inline double msg_unif(uint32_t serial, uint32_t dest, double lo,
+                                             double hi) const {
+    return msg_u(serial, dest) * (hi - lo) + lo;
+  }
 };
 
 // ---- replay of an exported activation/delay trace (cpr_replay)
@@ -251,6 +256,10 @@ struct TraceStream {
     return lookup(trace_link_key(kw, off, dest));
   }
   __host__ __device__ inline double msg(uint32_t serial, uint32_t dest, double) const {
+    return lookup(trace_msg_key(serial, dest));
+  }
+  __host__ __device__ inline double msg_unif(uint32_t serial, uint32_t dest, double,
+                                             double) const {
     return lookup(trace_msg_key(serial, dest));
   }
 };

@@ -80,6 +80,9 @@ struct TsParams {
   double ev, delta, dmax;
   int64_t max_steps, activations;
   double max_progress, max_time;
+  // honest clique (net 2, models.ml:3-28): keyed miner thresholds (n - 1), U(lo, hi) links
+  double lo, hi;
+  uint32_t thr[64];
 };
 
 constexpr int32_t NQS = 512;     // votes of one summary tree handled at once
@@ -360,6 +363,7 @@ struct TsLane {
   // ------------------------------------------------------------------ randomness
   template <class St>
   __host__ __device__ inline int32_t miner_of(const TsParams& P, const St& S, int32_t j) {
+    if (P.net == 2) return S.miner_w((uint32_t)j, P.thr, P.n - 1);
     return S.miner((uint32_t)j, P.t_att, P.d);
   }
   template <class St>
@@ -1117,7 +1121,7 @@ struct TsLane {
         break;
       }
       case EV_ON: {
-        if (node == 0) {  // loop mode: the attacker node's handler (tailstorm_ssz.ml:353-362)
+        if (node == 0 && P.net != 2) {  // loop mode: the attacker's handler (tailstorm_ssz.ml:353-362)
           prepare(P, M, kind, s);
           if (!dead) apply(P, M, ts_policy(P.policy, P.k, observe(P, M)));
           break;
@@ -1129,7 +1133,7 @@ struct TsLane {
         zt = 0;
         const int32_t m = miner_of(P, S, c_act);
         int32_t parent;
-        if (m == 0) {
+        if (m == 0 && P.net != 2) {
           ++act0;
           parent = payload_parent(P, M, 0, priv);  // gym: replaced at the Dag event
         } else {
@@ -1149,7 +1153,9 @@ struct TsLane {
         for (int32_t dst = 0; dst < P.n; ++dst) {
           if (dst == node) continue;
           double delay;
-          if (P.net == 1)
+          if (P.net == 2)  // models.ml:4 uniform propagation delays on every link
+            delay = S.msg_unif((uint32_t)s, (uint32_t)dst, P.lo, P.hi);
+          else if (P.net == 1)
             delay = 0.0;
           else if (node == 0)
             delay = S.msg((uint32_t)s, (uint32_t)dst, P.dmax);
@@ -1270,7 +1276,7 @@ struct TsLane {
       }
       handle(P, S, M, ev, s);
     }
-    return dead ? 0 : head(P, M, priv);
+    return dead ? 0 : head(P, M, P.net == 2 ? M.tips[0] : priv);
   }
 };
 

@@ -478,7 +478,7 @@ static std::unique_ptr<SimRng> make_bk_rng(int rng_mode, OcamlRandom* oc, uint64
                                            uint64_t ep, const Network& net) {
   if (rng_mode == 0)
     return trace_wrap(std::unique_ptr<SimRng>(new OcamlSimRng(oc, net)), net, true);
-  auto* r = new KeyedSimRng(seed, ep, net);
+  auto* r = new KeyedSimRng(seed, ep, net, needs_general_weights(net));
   r->serial_links = true;
   return trace_wrap(std::unique_ptr<SimRng>(r), net, true);
 }

@@ -170,6 +170,14 @@ struct KeyedSimRng : SimRng {
   double link_delay(const Link& l, const Block* msg) override;
 };
 
+// keyed miner draw by general weights iff the defenders' compute differs (honest cliques
+// of models.ml:3-28); [attacker] + equal defenders keeps the two-threshold draw
+inline bool needs_general_weights(const Network& net) {
+  for (size_t i = 2; i < net.nodes.size(); ++i)
+    if (net.nodes[i].compute != net.nodes[1].compute) return true;
+  return false;
+}
+
 // ---- activation/delay traces (cpr_trace, include/cpr_hip.h)
 // One episode's draws addressed by keyed-stream coordinates: activation j's miner and
 // clock delay, vertex serial s's pow bits, message delays by link key (kw, off, dest) or,

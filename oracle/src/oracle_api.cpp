@@ -30,6 +30,8 @@ void* oracle_ocaml_rng_new(long seed) {
   return seed < 0 ? new OcamlRandom() : new OcamlRandom(seed);
 }
 void oracle_ocaml_rng_free(void* r) { delete (OcamlRandom*)r; }
+// an independent copy of the 55-word state (branching a Parany worker's stream)
+void* oracle_ocaml_rng_copy(void* r) { return new OcamlRandom(*(OcamlRandom*)r); }
 int32_t oracle_ocaml_rng_bits(void* r) { return ((OcamlRandom*)r)->bits(); }
 int32_t oracle_ocaml_rng_int(void* r, int32_t n) { return ((OcamlRandom*)r)->int_(n); }
 double oracle_ocaml_rng_float(void* r, double b) { return ((OcamlRandom*)r)->float_(b); }
@@ -518,6 +520,25 @@ static int run_gym_episode(const cpr_config* c, const TablePolicy* tab, uint64_t
   return 0;
 }
 
+// Networks of the B_k / Tailstorm loop tasks. 0: two_agents(alpha); 1: symmetric clique of
+// n_nodes with exponential(prop_ev) delays (cpr_protocols.ml:200-210,478-485); 2: models.ml:3-28
+// honest_clique (compute i + 1, uniform lo .. hi delays)
+static Network loop_net(int net_kind, int n_nodes, double alpha, double activation_delay,
+                        double prop_ev, double lo, double hi) {
+  if (net_kind == 0) return Network::two_agents(activation_delay, alpha);
+  Network net;
+  net.flooding = false;
+  net.activation_delay = activation_delay;
+  net.nodes.resize(n_nodes);
+  for (int i = 0; i < n_nodes; ++i) {
+    net.nodes[i].compute = net_kind == 2 ? (double)(i + 1) : 1. / (double)n_nodes;
+    for (int j = 0; j < n_nodes - 1; ++j)
+      net.nodes[i].links.push_back(net_kind == 2 ? Link{j >= i ? j + 1 : j, D_UNIFORM, lo, hi}
+                                                 : Link{j >= i ? j + 1 : j, D_EXP, prop_ev, 0.0});
+  }
+  return net;
+}
+
 static int run_loop_episode(const cpr_config* c, uint64_t ep, cpr_episode_record* rec) {
   int64_t acts[2];
   double rew[2], ht, hp;
@@ -549,6 +570,46 @@ static int run_loop_episode(const cpr_config* c, uint64_t ep, cpr_episode_record
     rec->head_miner = -1;
     rec->status = 0;
     rec->head_work = c->protocol == CPR_PROTO_ETHEREUM ? hw : 0;
+    return 0;
+  }
+  if (c->network == CPR_NET_HONEST_CLIQUE &&
+      (c->protocol == CPR_PROTO_BK || c->protocol == CPR_PROTO_TAILSTORM)) {
+    // every node honest (policy ignored), keyed stream
+    const bool dflt = c->delay_lo == 0. && c->delay_hi == 0.;
+    const Network net = loop_net(2, c->defenders, 0.0, c->activation_delay, 0.0,
+                                 dflt ? 0.5 : c->delay_lo, dflt ? 1.5 : c->delay_hi);
+    std::vector<double> rw;
+    std::vector<int64_t> ac;
+    if (c->protocol == CPR_PROTO_BK) {
+      BkLoopResult r;
+      bk_loop_task(net, 1, nullptr, c->seed, ep, c->k, c->reward_scheme, -1, nullptr,
+                   (int)c->activations, &r);
+      rw = r.rewards;
+      ac.assign(r.activations.begin(), r.activations.end());
+      rec->progress = r.head_progress;
+      rec->chain_time = r.head_time;
+      rec->head_height = r.head_height;
+      rec->head_miner = r.head_signer;
+    } else {
+      TsLoopResult r;
+      ts_loop_task(net, 1, nullptr, c->seed, ep, c->k, c->reward_scheme, c->subblock_selection,
+                   -1, (int)c->activations, &r);
+      rw = r.rewards;
+      ac.assign(r.activations.begin(), r.activations.end());
+      rec->progress = r.head_progress;
+      rec->chain_time = r.head_time;
+      rec->head_height = r.head_height;
+      rec->head_miner = -1;
+    }
+    rec->reward_attacker = rw[0];
+    rec->reward_defender = 0.0;
+    rec->n_activations = 0;
+    for (size_t i = 1; i < rw.size(); ++i) rec->reward_defender += rw[i];
+    for (int64_t a : ac) rec->n_activations += a;
+    rec->sim_time = 0.0;
+    rec->n_steps = 0;
+    rec->status = 0;
+    rec->head_work = 0;
     return 0;
   }
   if (c->network != CPR_NET_TWO_AGENTS) {
@@ -714,23 +775,7 @@ int oracle_bk_loop(int net_kind, int n_nodes, double alpha, double activation_de
                    int64_t* acts_out, double* head_time, double* head_progress,
                    int32_t* head_height, int32_t* head_signer, int64_t* n_vertices) {
   try {
-    Network net;
-    if (net_kind == 0) {
-      net = Network::two_agents(activation_delay, alpha);
-    } else {
-      // 1: symmetric clique, exponential(prop_ev) delays; 2: models.ml:3-28 honest_clique
-      // (compute i + 1, uniform 0.5 .. 1.5 delays)
-      net.flooding = false;
-      net.activation_delay = activation_delay;
-      net.nodes.resize(n_nodes);
-      for (int i = 0; i < n_nodes; ++i) {
-        net.nodes[i].compute = net_kind == 2 ? (double)(i + 1) : 1. / (double)n_nodes;
-        for (int j = 0; j < n_nodes - 1; ++j)
-          net.nodes[i].links.push_back(net_kind == 2
-                                           ? Link{j >= i ? j + 1 : j, D_UNIFORM, 0.5, 1.5}
-                                           : Link{j >= i ? j + 1 : j, D_EXP, prop_ev, 0.0});
-      }
-    }
+    const Network net = loop_net(net_kind, n_nodes, alpha, activation_delay, prop_ev, 0.5, 1.5);
     BkTable t;
     BkLoopResult r;
     bk_loop_task(net, rng_mode, (OcamlRandom*)rng, seed, episode, k, scheme, policy, &t,
@@ -839,23 +884,7 @@ int oracle_ts_loop(int net_kind, int n_nodes, double alpha, double activation_de
                    double* rewards_out, int64_t* acts_out, double* head_time,
                    double* head_progress, int32_t* head_height, int64_t* n_vertices) {
   try {
-    Network net;
-    if (net_kind == 0) {
-      net = Network::two_agents(activation_delay, alpha);
-    } else {
-      // 1: symmetric clique, exponential(prop_ev) delays; 2: models.ml:3-28 honest_clique
-      // (compute i + 1, uniform 0.5 .. 1.5 delays)
-      net.flooding = false;
-      net.activation_delay = activation_delay;
-      net.nodes.resize(n_nodes);
-      for (int i = 0; i < n_nodes; ++i) {
-        net.nodes[i].compute = net_kind == 2 ? (double)(i + 1) : 1. / (double)n_nodes;
-        for (int j = 0; j < n_nodes - 1; ++j)
-          net.nodes[i].links.push_back(net_kind == 2
-                                           ? Link{j >= i ? j + 1 : j, D_UNIFORM, 0.5, 1.5}
-                                           : Link{j >= i ? j + 1 : j, D_EXP, prop_ev, 0.0});
-      }
-    }
+    const Network net = loop_net(net_kind, n_nodes, alpha, activation_delay, prop_ev, 0.5, 1.5);
     TsLoopResult r;
     ts_loop_task(net, rng_mode, (OcamlRandom*)rng, seed, episode, k, scheme, selection, policy,
                  activations, &r);

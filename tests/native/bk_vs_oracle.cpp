@@ -31,8 +31,9 @@ struct Cfg {
   int policy;  // 0..3 bk_ssz policies, 4 = table, 5 = random actions, 6 = random release-heavy
   int scheme;  // 0 Constant, 2 Block
   int steps;
-  int two_agents;
+  int two_agents;  // 0 gym, 1 two-agents loop, 2 honest-clique loop (defenders = nodes)
   int k;
+  double ev = 1.0;
 };
 
 struct Counters {
@@ -45,10 +46,18 @@ static int g_dim = 4;
 static bk::BkParams params_of(const Cfg& cf) {
   bk::BkParams P{};
   P.t_att = oracle::alpha_threshold(cf.alpha);
-  P.d = cf.two_agents ? 1 : cf.defenders;
+  P.d = cf.two_agents == 2 ? cf.defenders - 1 : cf.two_agents ? 1 : cf.defenders;
   P.n = P.d + 1;
-  P.net = cf.two_agents ? 1 : 0;
+  P.net = cf.two_agents;
   P.mode = cf.two_agents ? 1 : 0;
+  if (cf.two_agents == 2) {  // models.ml:3-28 honest clique, as capi.hip validate_bk
+    std::vector<double> w;
+    for (int i = 0; i < P.n; ++i) w.push_back((double)(i + 1));
+    const std::vector<uint32_t> thr = oracle::weight_thresholds(w);
+    for (size_t i = 0; i < thr.size(); ++i) P.thr[i] = thr[i];
+    P.lo = 0.5;
+    P.hi = 1.5;
+  }
   P.policy = cf.policy < 5 ? cf.policy : 0;
   P.scheme = cf.scheme;
   P.k = cf.k;
@@ -61,7 +70,7 @@ static bk::BkParams params_of(const Cfg& cf) {
   P.cap_d = 64;
   P.table_dim = g_dim;
   P.table = g_table.data();
-  P.ev = 1.0;
+  P.ev = cf.ev;
   P.delta = 1e-9;
   const double dd = cf.defenders;
   P.dmax = (dd - 1.) / dd * 1e-9 / cf.gamma;
@@ -174,14 +183,33 @@ static bool run_gym(const Cfg& cf, uint64_t seed, uint64_t ep, Counters& C, std:
   return ok;
 }
 
+static constexpr int64_t L0_ANY = -1;
+
 static bool run_loop(const Cfg& cf, uint64_t seed, uint64_t ep, Counters& C, std::string& why) {
   oracle::BkTable tab;
   tab.dim = g_dim;
   tab.k = cf.k;
   tab.actions = g_table;
   oracle::BkLoopResult r;
-  oracle::bk_loop_task(oracle::Network::two_agents(1.0, cf.alpha), 1, nullptr, seed, ep, cf.k,
-                       cf.scheme, cf.policy, &tab, cf.steps, &r);
+  oracle::Network net = oracle::Network::two_agents(1.0, cf.alpha);
+  if (cf.two_agents == 2) {
+    net = oracle::Network{};
+    net.flooding = false;
+    net.activation_delay = cf.ev;
+    net.nodes.resize(cf.defenders);
+    for (int i = 0; i < cf.defenders; ++i) {
+      net.nodes[i].compute = (double)(i + 1);
+      for (int j = 0; j < cf.defenders - 1; ++j)
+        net.nodes[i].links.push_back(oracle::Link{j >= i ? j + 1 : j, oracle::D_UNIFORM, 0.5, 1.5});
+    }
+  }
+  oracle::bk_loop_task(net, 1, nullptr, seed, ep, cf.k, cf.scheme,
+                       cf.two_agents == 2 ? -1 : cf.policy, &tab, cf.steps, &r);
+  double rd = 0.0;
+  int64_t acts = 0;
+  for (size_t i = 1; i < r.rewards.size(); ++i) rd += r.rewards[i];
+  for (int64_t a : r.activations) acts += a;
+  const int64_t a0 = cf.two_agents == 2 ? L0_ANY : r.activations[0];
   const bk::BkParams P = params_of(cf);
   std::vector<uint8_t> mem(bk::bk_lane_bytes(P));
   const bk::BkMem M = bk::bk_mem_at(mem.data(), P);
@@ -195,9 +223,9 @@ static bool run_loop(const Cfg& cf, uint64_t seed, uint64_t ep, Counters& C, std
   const bk::BVtx& hb = L.X(P, M, hd);
   C.episodes++;
   C.steps += cf.steps;
-  if (hb.rew_att != r.rewards[0] || hb.rew_def != r.rewards[1] || hb.height != r.head_height ||
-      hb.time != r.head_time || L.act0 != r.activations[0] ||
-      L.c_act != r.activations[0] + r.activations[1] || hb.who != r.head_signer ||
+  if (hb.rew_att != r.rewards[0] || hb.rew_def != rd || hb.height != r.head_height ||
+      hb.time != r.head_time || (a0 != L0_ANY && L.act0 != a0) ||
+      L.c_act != acts || hb.who != r.head_signer ||
       L.newest + 1 != r.n_vertices) {
     char buf[400];
     snprintf(buf, sizeof buf,
@@ -233,6 +261,10 @@ int main(int argc, char** argv) {
   cfgs.push_back(Cfg{0.33, 0.3, 4, 5, 0, steps, 0, k});
   for (double a : alphas)
     for (int pol : {0, 1, 2, 3}) cfgs.push_back(Cfg{a, 0, 1, pol, 0, steps * 2, 1, k});
+  // honest cliques: n nodes, compute 1..n, U(0.5, 1.5) links, both reward schemes
+  for (int n : {3, 10})
+    for (double ev : {0.5, 2.0, 30.0})
+      for (int sch : {0, 2}) cfgs.push_back(Cfg{0, 0, n, 0, sch, steps * 2, 2, k, ev});
   Counters C;
   int shown = 0;
   for (auto& cf : cfgs)

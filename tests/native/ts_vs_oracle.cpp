@@ -33,8 +33,9 @@ struct Cfg {
   int policy;  // 0..6 tailstorm_ssz policies, 7 = random actions, 8 = random release-heavy
   int scheme;  // 0 Constant, 1 Discount, 3 Punish, 4 Hybrid
   int steps;
-  int two_agents;
+  int two_agents;  // 0 gym, 1 two-agents loop, 2 honest-clique loop (defenders = nodes)
   int k;
+  double ev = 1.0;
 };
 
 struct Counters {
@@ -46,10 +47,18 @@ static int g_sel = 1;
 static ts::TsParams params_of(const Cfg& cf) {
   ts::TsParams P{};
   P.t_att = oracle::alpha_threshold(cf.alpha);
-  P.d = cf.two_agents ? 1 : cf.defenders;
+  P.d = cf.two_agents == 2 ? cf.defenders - 1 : cf.two_agents ? 1 : cf.defenders;
   P.n = P.d + 1;
-  P.net = cf.two_agents ? 1 : 0;
+  P.net = cf.two_agents;
   P.mode = cf.two_agents ? 1 : 0;
+  if (cf.two_agents == 2) {  // models.ml:3-28 honest clique, as capi.hip validate_bk
+    std::vector<double> w;
+    for (int i = 0; i < P.n; ++i) w.push_back((double)(i + 1));
+    const std::vector<uint32_t> thr = oracle::weight_thresholds(w);
+    for (size_t i = 0; i < thr.size(); ++i) P.thr[i] = thr[i];
+    P.lo = 0.5;
+    P.hi = 1.5;
+  }
   P.policy = cf.policy < 7 ? cf.policy : 0;
   P.scheme = cf.scheme;
   P.selection = g_sel;
@@ -61,7 +70,7 @@ static ts::TsParams params_of(const Cfg& cf) {
   P.cap_q = P.cap_v / 2;
   P.cap_e = 256 + 512 * P.n + (cf.gamma == 0.0 && !cf.two_agents ? 2 * P.d * std::min(span, 8192) : 0);
   P.cap_d = 64;
-  P.ev = 1.0;
+  P.ev = cf.ev;
   P.delta = 1e-9;
   const double dd = cf.defenders;
   P.dmax = (dd - 1.) / dd * 1e-9 / cf.gamma;
@@ -237,8 +246,21 @@ static bool run_loop(const Cfg& cf, uint64_t seed, uint64_t ep, Counters& C, std
   bool raised = false;
   bool budget = false;
   try {
-    oracle::ts_loop_task(oracle::Network::two_agents(1.0, cf.alpha), 1, nullptr, seed, ep,
-                         cf.k, cf.scheme, g_sel, cf.policy, cf.steps, &r);
+    oracle::Network net = oracle::Network::two_agents(1.0, cf.alpha);
+    if (cf.two_agents == 2) {
+      net = oracle::Network{};
+      net.flooding = false;
+      net.activation_delay = cf.ev;
+      net.nodes.resize(cf.defenders);
+      for (int i = 0; i < cf.defenders; ++i) {
+        net.nodes[i].compute = (double)(i + 1);
+        for (int j = 0; j < cf.defenders - 1; ++j)
+          net.nodes[i].links.push_back(
+              oracle::Link{j >= i ? j + 1 : j, oracle::D_UNIFORM, 0.5, 1.5});
+      }
+    }
+    oracle::ts_loop_task(net, 1, nullptr, seed, ep, cf.k, cf.scheme, g_sel,
+                         cf.two_agents == 2 ? -1 : cf.policy, cf.steps, &r);
   } catch (oracle::BudgetExceeded&) {
     budget = true;
   } catch (std::exception&) {
@@ -279,9 +301,13 @@ static bool run_loop(const Cfg& cf, uint64_t seed, uint64_t ep, Counters& C, std
   const double* rw = L.R(P, M, hb.qslot);
   C.episodes++;
   C.steps += cf.steps;
-  if (rw[0] != r.rewards[0] || rw[1] != r.rewards[1] || hb.height != r.head_height ||
-      hb.time != r.head_time || L.act0 != r.activations[0] ||
-      L.c_act != r.activations[0] + r.activations[1] || L.newest + 1 != r.n_vertices) {
+  bool rw_ok = true;
+  int64_t acts = 0;
+  for (size_t j = 0; j < r.rewards.size(); ++j) rw_ok = rw_ok && rw[j] == r.rewards[j];
+  for (int64_t a : r.activations) acts += a;
+  if (!rw_ok || hb.height != r.head_height || hb.time != r.head_time ||
+      (cf.two_agents != 2 && L.act0 != r.activations[0]) || L.c_act != acts ||
+      L.newest + 1 != r.n_vertices) {
     char buf[400];
     snprintf(buf, sizeof buf,
              "loop lane (ra %.3f rd %.3f h %d tm %.17g a0 %d v %d) oracle (%.3f %.3f %d %.17g %ld %ld)",
@@ -314,6 +340,10 @@ int main(int argc, char** argv) {
   cfgs.push_back(Cfg{0.33, 0.3, 4, 7, 1, steps, 0, k});
   for (double a : alphas)
     for (int pol : {0, 1, 2, 3, 4, 5, 6}) cfgs.push_back(Cfg{a, 0, 1, pol, 1, steps * 2, 1, k});
+  // honest cliques: n nodes, compute 1..n, U(0.5, 1.5) links, all four reward schemes
+  for (int n : {3, 10})
+    for (double ev : {0.5, 2.0, 30.0})
+      for (int sch : {0, 1, 3, 4}) cfgs.push_back(Cfg{0, 0, n, 0, sch, steps * 2, 2, k, ev});
   Counters C;
   int shown = 0;
   for (auto& cf : cfgs)

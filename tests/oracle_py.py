@@ -38,6 +38,8 @@ def lib():
         L.oracle_ocaml_rng_new.restype = vp
         L.oracle_ocaml_rng_new.argtypes = [ctypes.c_long]
         L.oracle_ocaml_rng_free.argtypes = [vp]
+        L.oracle_ocaml_rng_copy.restype = vp
+        L.oracle_ocaml_rng_copy.argtypes = [vp]
         L.oracle_ocaml_rng_bits.argtypes = [vp]
         L.oracle_ocaml_rng_int.argtypes = [vp, ctypes.c_int32]
         L.oracle_ocaml_rng_float.argtypes = [vp, ctypes.c_double]
@@ -122,6 +124,11 @@ class OcamlRandom:
             lib().oracle_ocaml_rng_free(self.h)
         except Exception:
             pass
+
+    def copy(self):
+        c = OcamlRandom.__new__(OcamlRandom)
+        c.h = lib().oracle_ocaml_rng_copy(self.h)
+        return c
 
     def bits(self):
         return lib().oracle_ocaml_rng_bits(self.h)

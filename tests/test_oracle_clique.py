@@ -47,3 +47,47 @@ def test_keyed_clique_statistics_match_reference_rows():
         for xs, ref in ((orph, ref_orph), (share, ref_share)):
             m, sd = float(np.mean(xs)), float(np.std(xs, ddof=1))
             assert abs(ref - m) <= 4 * sd + 1e-4, (row["line"], ref, m, sd)
+
+
+# ---------------------------------------------------------------- Parany worker chains
+#
+# csv_runner.ml:105-131 runs honest_net.ml's tasks on forked Parany workers whose Random state
+# carries from task to task. make_honest_net_chains.py recovered, for 23 rows, the earlier rows
+# their worker ran first; replaying that chain from the default state reproduces the row bit
+# for bit — including 10 B_k (k = 1, 2) and 3 Tailstorm (k = 1) rows, both incentive schemes; the chains of
+# later rows pass through spar/stree tasks, which are out of scope).
+
+import importlib.util  # noqa: E402
+
+_spec = importlib.util.spec_from_file_location(
+    "make_honest_net_chains", pathlib.Path(__file__).parent / "golden" / "make_honest_net_chains.py")
+CH = importlib.util.module_from_spec(_spec)
+_spec.loader.exec_module(CH)
+CHAINS = json.loads((pathlib.Path(__file__).parent / "golden" / "honest_net_chains.json")
+                    .read_text())["rows"]
+BY_LINE = {r["line"]: r for r in CHAINS}
+
+
+def chained_rng(row):
+    """OCaml's default Random state advanced over the row's recovered worker chain."""
+    rng = O.OcamlRandom()
+    for ln in row["chain"]:
+        CH.run(BY_LINE[ln], rng)
+    return rng
+
+
+def test_chain_fixture_covers_bk_and_tailstorm():
+    protos = [r["protocol"] for r in CHAINS]
+    assert protos.count("bk") == 10 and protos.count("tailstorm") == 3
+    assert {r["incentive_scheme"] for r in CHAINS if r["protocol"] == "bk"} == {"block", "constant"}
+
+
+@pytest.mark.parametrize("row", [r for r in CHAINS if r["protocol"] in ("bk", "tailstorm")],
+                         ids=lambda r: f"line{r['line']}-{r['protocol']}")
+def test_honest_net_chained_rows_exact(row):
+    out = CH.run(row, chained_rng(row))
+    assert out["activations"] == row["activations_per_node"]
+    assert out["reward"] == row["reward"]
+    assert float("%.12g" % out["head_time"]) == float(row["head_time"])
+    assert out["head_progress"] == row["head_progress"]
+    assert out["head_height"] == row["head_height"]
