@@ -72,7 +72,7 @@ __device__ inline BRef run_loop(NakLane& L, const NakParams& P, const St& S, con
 constexpr uint32_t kInexact = ST_OVERLAP | ST_DEEP_FORK | ST_TIE_UNRESOLVED | ST_STALE_TIME;
 
 template <int MODE, class Src>
-__global__ __launch_bounds__(kBlock) void k_run_episodes(
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(MODE == 0 ? 5 : 4))) void k_run_episodes(
     NakParams P, Src src, int64_t n_eps, int64_t activations,
     int32_t* spill, double* tlog, uint8_t* replay, cpr_episode_record* recs, cpr_summary* sum,
     int64_t* redo, uint32_t* redo_n, uint32_t launch_id, int64_t redo_cap) {
