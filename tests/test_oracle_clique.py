@@ -91,3 +91,32 @@ def test_honest_net_chained_rows_exact(row):
     assert float("%.12g" % out["head_time"]) == float(row["head_time"])
     assert out["head_progress"] == row["head_progress"]
     assert out["head_height"] == row["head_height"]
+
+
+BKTS_ROWS = json.loads((pathlib.Path(__file__).parent / "golden" / "honest_net_bk_ts_rows.json")
+                       .read_text())["rows"]
+
+
+def test_keyed_bk_ts_cliques_bracket_reference_rows():
+    # the 24 B_k / Tailstorm rows (k = 4, 8, 16) whose worker states are unknown: orphan rate
+    # (1 - progress / activations) and the strongest node's reward share of each row lie
+    # within 4 sigma of 10 keyed oracle tasks of the same configuration
+    schemes = {"constant": 0, "block": 2, "discount": 1}
+    for row in BKTS_ROWS:
+        orph, share = [], []
+        for ep in range(10):
+            kw = dict(net="honest-clique", n_nodes=row["nodes"],
+                      activation_delay=row["activation_delay"],
+                      scheme=schemes[row["incentive_scheme"]], seed=7, episode=ep)
+            if row["protocol"] == "bk":
+                out = O.bk_loop(row["k"], row["activations"], **kw)
+            else:
+                out = O.ts_loop(row["k"], row["activations"],
+                                selection=O.TS_SELECTIONS[row["subblock_selection"]], **kw)
+            orph.append(1 - out["head_progress"] / row["activations"])
+            share.append(out["reward"][-1] / sum(out["reward"]))
+        ref_orph = 1 - row["head_progress"] / row["activations"]
+        ref_share = row["reward"][-1] / sum(row["reward"])
+        for xs, ref in ((orph, ref_orph), (share, ref_share)):
+            m, sd = float(np.mean(xs)), float(np.std(xs, ddof=1))
+            assert abs(ref - m) <= 4 * sd + 1e-4, (row["line"], ref, m, sd)
