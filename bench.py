@@ -92,8 +92,8 @@ def pmc_traffic(episodes):
         wr = d.get("hbm_write_bytes_per_dispatch (WRITE_SIZE x1024)")
         if rd is None or wr is None:
             continue
-        return rd + wr, os.path.relpath(path, HERE)
-    return None, None
+        return rd + wr, os.path.relpath(path, HERE), d.get("valu_wave_instr_per_activation")
+    return None, None, None
 
 
 def main():
@@ -161,7 +161,7 @@ def main():
     # around the last launch of every point, on the stream the kernel runs on; activations
     # per launch = E episodes x (max_steps + 1) (every gym episode is exactly that long)
     kms = np.array([b.last_launch()[0] for b in batches])
-    traffic, traffic_src = pmc_traffic(E)
+    traffic, traffic_src, valu_meas = pmc_traffic(E)
     kacts = np.full(len(batches), float(E * (STEPS_PER_EPISODE + 1)))
     act_per_s_kernel = float(kacts.sum() / (kms.sum() / 1e3))
     achieved = act_per_s_kernel * OPS_PER_ACTIVATION / 1e12
@@ -204,6 +204,10 @@ def main():
                 "frac": achieved / VALU_PEAK_TOPS,
                 "traffic": traffic,
                 "traffic_source": traffic_src,
+                # SQ_INSTS_VALU x 64 / activations from the same PMC summary: the VALU
+                # lane-instructions the kernel really issues per activation, beside the
+                # 40-op cost model `achieved` is priced at
+                "measured_valu_lane_ops_per_activation": valu_meas,
                 "algorithmic_bytes_per_launch": ALG_BYTES_PER_ACT * E * (STEPS_PER_EPISODE + 1),
                 "kernel": "k_run_episodes",
                 "kernel_ms_mean": float(kms.mean()),
