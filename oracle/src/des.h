@@ -170,9 +170,13 @@ struct KeyedSimRng : SimRng {
   double link_delay(const Link& l, const Block* msg) override;
 };
 
-// keyed miner draw by general weights iff the defenders' compute differs (honest cliques
-// of models.ml:3-28); [attacker] + equal defenders keeps the two-threshold draw
+// keyed miner draw by general weights iff the compute is not [alpha] + equal defenders
+// summing to 1 (honest cliques of models.ml:3-28: compute 1..n, also for n = 2); the
+// two-agents and symmetric-clique networks keep the two-threshold draw
 inline bool needs_general_weights(const Network& net) {
+  double total = 0.0;
+  for (const NetNode& x : net.nodes) total += x.compute;
+  if (total > 1.0 + 1e-9 || total < 1.0 - 1e-9) return true;
   for (size_t i = 2; i < net.nodes.size(); ++i)
     if (net.nodes[i].compute != net.nodes[1].compute) return true;
   return false;

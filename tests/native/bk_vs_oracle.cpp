@@ -262,8 +262,8 @@ int main(int argc, char** argv) {
   for (double a : alphas)
     for (int pol : {0, 1, 2, 3}) cfgs.push_back(Cfg{a, 0, 1, pol, 0, steps * 2, 1, k});
   // honest cliques: n nodes, compute 1..n, U(0.5, 1.5) links, both reward schemes
-  for (int n : {3, 10})
-    for (double ev : {0.5, 2.0, 30.0})
+  for (int n : {2, 3, 10})
+    for (double ev : {0.5, 2.0, 30.0, 600.0})
       for (int sch : {0, 2}) cfgs.push_back(Cfg{0, 0, n, 0, sch, steps * 2, 2, k, ev});
   Counters C;
   int shown = 0;

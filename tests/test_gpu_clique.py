@@ -93,7 +93,7 @@ def _cfg_bkts(protocol, n, ad, acts, k, scheme, selection=L.SELECT_HEURISTIC, se
     ("tailstorm", 8, L.REWARD_DISCOUNT, L.SELECT_HEURISTIC),
     ("tailstorm", 4, L.REWARD_CONSTANT, L.SELECT_OPTIMAL),
     ("tailstorm", 3, L.REWARD_HYBRID, L.SELECT_ALTRUISTIC)])
-@pytest.mark.parametrize("n,ad", [(10, 30.0), (10, 2.0), (3, 0.5)])
+@pytest.mark.parametrize("n,ad", [(10, 30.0), (10, 2.0), (3, 0.5), (2, 600.0)])
 def test_bk_ts_clique_records_match_oracle(ctx, protocol, k, scheme, selection, n, ad):
     cfg, keep = _cfg_bkts(protocol, n, ad, 1500, k, scheme, selection)
     b = device.Batch(cfg, ctx=ctx, keep=keep)
