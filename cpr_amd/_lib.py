@@ -71,6 +71,9 @@ ST_CAPACITY = 32
 ST_REFERENCE_RAISES = 64
 ST_TRACE_MISS = 128
 ST_EXACT_RERUN = 256
+ST_INVALID = ST_CAPACITY | ST_REFERENCE_RAISES | ST_TRACE_MISS  # include/cpr_hip.h
+ST_LOCKSTEP_INEXACT = ST_OVERLAP | ST_DEEP_FORK | ST_TIE_UNRESOLVED | ST_STALE_TIME
+ABI_VERSION = 6  # include/cpr_hip.h CPR_ABI_VERSION this module's structures follow
 
 HIST_BINS = 64
 
@@ -152,6 +155,7 @@ class Summary(ctypes.Structure):
         ("status_overlap", ctypes.c_int64),
         ("status_other", ctypes.c_int64),
         ("hist", ctypes.c_int64 * HIST_BINS),
+        ("invalid", ctypes.c_int64),
     ]
 
     FIELDS = [f for f, _ in _fields_ if f != "hist"]
@@ -195,6 +199,7 @@ class StepInfo(ctypes.Structure):
         ("episode_n_activations", ctypes.POINTER(ctypes.c_int64)),
         ("head_height", ctypes.POINTER(ctypes.c_int32)),
         ("head_miner", ctypes.POINTER(ctypes.c_int32)),
+        ("status", ctypes.POINTER(ctypes.c_uint32)),
     ]
 
 
@@ -330,6 +335,9 @@ def lib():
             )
         L = ctypes.CDLL(path)
         _declare(L)
+        if L.cpr_abi_version() != ABI_VERSION:
+            raise ImportError(f"{path} has ABI {L.cpr_abi_version()}, this module expects "
+                              f"{ABI_VERSION}; rebuild with __graft_entry__.build()")
         _lib = L
     return _lib
 

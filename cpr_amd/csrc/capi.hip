@@ -33,9 +33,15 @@ static int fail(int code, const std::string& msg) {
       return fail(CPR_E_HIP, std::string(#expr " failed: ") + hipGetErrorString(e_));   \
   } while (0)
 
+// device allocation owned by one object (freed on destruction, so every early return of
+// an entry point releases its scratch buffers); not copyable
 struct DevBuf {
   void* p = nullptr;
   size_t bytes = 0;
+  DevBuf() = default;
+  DevBuf(const DevBuf&) = delete;
+  DevBuf& operator=(const DevBuf&) = delete;
+  ~DevBuf() { release(); }
   hipError_t ensure(size_t n) {
     if (n <= bytes) return hipSuccess;
     if (p) (void)hipFree(p);
@@ -71,7 +77,8 @@ struct cpr_batch {
   eth::EthParams EP;     // CPR_PROTO_ETHEREUM
   DevBuf eth_mem;        // lanes x eth_lane_bytes
   bool is_eth = false;   // Ethereum lockstep lanes share bk_lmem / bk_slots
-  bool nak_ev = false;   // Nakamoto on an honest clique: Ethereum lanes in Nakamoto mode (EP)
+  bool nak_ev = false;   // Nakamoto on the event engine (nak_on_event_engine): Ethereum lanes
+                         // in Nakamoto mode (EP)
   int64_t eth_bytes = 0;
   bk::BkParams BP;       // CPR_PROTO_BK
   DevBuf bk_mem;         // fused episodes: lanes x bk_bytes
@@ -112,6 +119,8 @@ int cpr_device_count(int* out) {
   return CPR_OK;
 }
 
+static int flush_reruns(cpr_ctx* c);
+
 int cpr_ctx_create(int device, cpr_ctx** out) {
   if (!out) return fail(CPR_E_INVALID_ARG, "out is NULL");
   int n = 0;
@@ -135,16 +144,16 @@ int cpr_ctx_create(int device, cpr_ctx** out) {
 int cpr_ctx_destroy(cpr_ctx* c) {
   if (!c) return CPR_OK;
   (void)hipSetDevice(c->device);
-  (void)hipStreamDestroy(c->stream);
+  // pending work first: queued exact re-runs complete their callers' summaries and records
+  (void)flush_reruns(c);
   (void)hipStreamSynchronize(c->stream);
+  (void)hipStreamDestroy(c->stream);
   c->rq.release();
   c->rtab.release();
   c->rmem.release();
   delete c;
   return CPR_OK;
 }
-
-static int flush_reruns(cpr_ctx* c);
 
 int cpr_synchronize(cpr_ctx* c) {
   HIP_TRY(hipSetDevice(c->device));
@@ -185,6 +194,23 @@ static void clique_thresholds(int n, uint32_t* thr) {
 static int validate_bk(const cpr_config* c, bk::BkParams* P);
 static int validate_ts(const cpr_config* c, ts::TsParams* P);
 
+// Nakamoto configurations the closed-form lane does not cover run on the event engine:
+// honest cliques; Simulator.loop tasks on the selfish-mining network at gamma = 0 (messages
+// at t = +inf, drained after the last activation); and loop tasks whose message delays make
+// overlapping windows common (the withholding sweep's 1e-4 defender delay overlaps about
+// once per 10,000 activations, models.ml:54), which the closed-form lane would hand to
+// the same engine episode by episode anyway
+static bool nak_on_event_engine(const cpr_config* c) {
+  if (c->protocol != CPR_PROTO_NAKAMOTO) return false;
+  if (c->network == CPR_NET_HONEST_CLIQUE) return true;
+  if (c->network != CPR_NET_SELFISH_MINING || c->mode != CPR_MODE_LOOP) return false;
+  if (c->gamma == 0.0) return true;
+  const double prop = c->propagation_delay > 0 ? c->propagation_delay : 1e-9;
+  const double dd = (double)c->defenders;
+  const double span = std::max(prop, (dd - 1.) / dd * prop / c->gamma);
+  return !(span * (double)c->activations < 1e-3 * c->activation_delay);
+}
+
 static int validate(const cpr_config* c, NakParams* P, eth::EthParams* EP, bk::BkParams* BP,
                     ts::TsParams* TP) {
   if (c->protocol == CPR_PROTO_ETHEREUM) return validate_eth(c, EP);
@@ -219,6 +245,21 @@ static int validate(const cpr_config* c, NakParams* P, eth::EthParams* EP, bk::B
     for (int i = 0; i < c->policy_table_dim * c->policy_table_dim * 2; i++)
       if (c->policy_table[i] > 3) return fail(CPR_E_INVALID_ARG, "policy table action out of range");
   }
+  if (nak_on_event_engine(c)) {
+    // Simulator.loop on the selfish-mining network at gamma = 0: the attacker's messages
+    // arrive at t = +inf and the loop drains them after the last activation
+    // (simulator.ml:519-533); no closed form, so the event engine in Nakamoto mode runs it
+    cpr_config c2 = *c;
+    c2.protocol = CPR_PROTO_ETHEREUM;
+    c2.policy = CPR_ETH_POLICY_HONEST;
+    c2.reward_scheme = CPR_REWARD_CONSTANT;
+    const int rc = validate_eth(&c2, EP);
+    if (rc) return rc;
+    EP->nak = 1;
+    EP->policy = c->policy;
+    EP->table_dim = c->policy_table_dim;
+    return CPR_OK;
+  }
   memset(P, 0, sizeof(*P));
   P->ev = c->activation_delay;
   P->t_att = alpha_threshold(c->alpha);
@@ -237,9 +278,6 @@ static int validate(const cpr_config* c, NakParams* P, eth::EthParams* EP, bk::B
     P->delta = prop;
     P->dmax = (dd - 1.) / dd * prop / c->gamma;
     P->arrive = std::isfinite(P->dmax) ? 1 : 0;
-    if (c->mode == CPR_MODE_LOOP && !P->arrive)
-      return fail(CPR_E_UNSUPPORTED,
-                  "loop mode with gamma = 0 (messages delivered at t = inf) is not implemented");
   } else if (c->network == CPR_NET_TWO_AGENTS) {
     if (c->mode == CPR_MODE_GYM)
       return fail(CPR_E_UNSUPPORTED, "the gym engine always uses the selfish-mining network");
@@ -315,7 +353,7 @@ static int validate_eth(const cpr_config* c, eth::EthParams* P) {
       return fail(CPR_E_UNSUPPORTED, "honest cliques run Simulator.loop tasks (CPR_MODE_LOOP)");
     if (c->defenders < 2 || c->defenders > 64)
       return fail(CPR_E_INVALID_ARG, "honest clique: 2..64 nodes (cfg.defenders)");
-    const bool dflt = c->delay_lo == 0. && c->delay_hi == 0.;
+    const bool dflt = std::isnan(c->delay_lo) && std::isnan(c->delay_hi);  // NaN: models.ml default
     const double lo = dflt ? 0.5 : c->delay_lo, hi = dflt ? 1.5 : c->delay_hi;
     if (!(lo >= 0.) || !(hi >= lo)) return fail(CPR_E_INVALID_ARG, "delay_lo/delay_hi");
     P->d = c->defenders - 1;
@@ -348,9 +386,15 @@ static int validate_eth(const cpr_config* c, eth::EthParams* P) {
   int32_t cb = 64;
   while (cb < span && cb < (1 << 15)) cb <<= 1;
   P->cap_b = cb;
-  // gamma = 0: messages at t = +inf stay in the skew heap (they shape its tie order)
-  P->cap_e = 64 + 512 * P->n +
-             (std::isfinite(P->dmax) ? 0 : (int32_t)(2 * P->d * std::min<int64_t>(span, 8192)));
+  // gamma = 0: messages at t = +inf stay in the skew heap (they shape its tie order);
+  // Simulator.loop tasks on the selfish-mining network: a release shares every withheld
+  // block at once, d messages each, and loop tasks at alpha near 0.5 withhold thousands
+  int64_t extra = 0;
+  if (P->net == 0 && !std::isfinite(P->dmax))
+    extra = 2 * (int64_t)P->d * (P->mode == CPR_MODE_LOOP ? span : std::min<int64_t>(span, 8192));
+  else if (P->net == 0 && P->mode == CPR_MODE_LOOP)
+    extra = (int64_t)P->d * span;
+  P->cap_e = 64 + 512 * P->n + (int32_t)std::min<int64_t>(extra, 1 << 24);
   return CPR_OK;
 }
 
@@ -418,7 +462,7 @@ static int validate_bk(const cpr_config* c, bk::BkParams* P) {
       return fail(CPR_E_UNSUPPORTED, "honest cliques run Simulator.loop tasks (CPR_MODE_LOOP)");
     if (c->defenders < 2 || c->defenders > 64)
       return fail(CPR_E_INVALID_ARG, "honest clique: 2..64 nodes (cfg.defenders)");
-    const bool dflt = c->delay_lo == 0. && c->delay_hi == 0.;
+    const bool dflt = std::isnan(c->delay_lo) && std::isnan(c->delay_hi);  // NaN: models.ml default
     const double lo = dflt ? 0.5 : c->delay_lo, hi = dflt ? 1.5 : c->delay_hi;
     if (!(lo >= 0.) || !(hi >= lo)) return fail(CPR_E_INVALID_ARG, "delay_lo/delay_hi");
     P->d = c->defenders - 1;
@@ -545,7 +589,7 @@ int cpr_batch_create(cpr_ctx* ctx, const cpr_config* cfg, cpr_batch** out) {
   if (cfg->protocol == CPR_PROTO_TAILSTORM) b->bk_bytes = ts::ts_lane_bytes(TP);
   b->is_ev = cfg->protocol == CPR_PROTO_BK || cfg->protocol == CPR_PROTO_TAILSTORM;
   b->is_eth = cfg->protocol == CPR_PROTO_ETHEREUM;
-  b->nak_ev = cfg->protocol == CPR_PROTO_NAKAMOTO && cfg->network == CPR_NET_HONEST_CLIQUE;
+  b->nak_ev = nak_on_event_engine(cfg);
   b->cfg.policy_table = nullptr;
   if (cfg->protocol == CPR_PROTO_BK && cfg->policy == CPR_BK_POLICY_TABLE) {
     const size_t D = (size_t)cfg->policy_table_dim, K1 = (size_t)cfg->k + 1;
@@ -579,6 +623,7 @@ int cpr_batch_create(cpr_ctx* ctx, const cpr_config* cfg, cpr_batch** out) {
   }
   b->P.table = (const uint8_t*)b->table_dev.p;
   b->BP.table = (const uint8_t*)b->table_dev.p;
+  if (b->nak_ev) b->EP.table = (const uint8_t*)b->table_dev.p;
   if (cfg->protocol == CPR_PROTO_NAKAMOTO && !b->nak_ev) {
     // the same episode on the exact event engine: Ethereum lane, no uncles, nakamoto_ssz
     // policy (validated above); configurations it cannot hold keep the lane's flags
@@ -839,6 +884,7 @@ static int run_sync(cpr_batch* b, int64_t n, uint64_t first, const TraceSource* 
   summary->status_tie += s.status_tie;
   summary->status_overlap += s.status_overlap;
   summary->status_other += s.status_other;
+  summary->invalid += s.invalid;
   for (int i = 0; i < CPR_HIST_BINS; i++) summary->hist[i] += s.hist[i];
   return CPR_OK;
 }
@@ -855,7 +901,11 @@ int cpr_run_episodes(cpr_batch* b, int64_t n, uint64_t first, cpr_summary* summa
 // the network, delays non-negative (not NaN), keys strictly ascending per episode
 static int check_trace(const cpr_batch* b, const cpr_trace* t) {
   const int64_t E = t->n_episodes;
-  const int32_t nodes = b->cfg.network == CPR_NET_TWO_AGENTS ? 2 : b->cfg.defenders + 1;
+  // two agents: 2 nodes; honest clique: exactly `defenders` nodes; selfish mining: the
+  // attacker plus `defenders`
+  const int32_t nodes = b->cfg.network == CPR_NET_TWO_AGENTS      ? 2
+                        : b->cfg.network == CPR_NET_HONEST_CLIQUE ? b->cfg.defenders
+                                                                  : b->cfg.defenders + 1;
   const int64_t* offs[3] = {t->act_offset, t->pow_offset, t->link_offset};
   const char* names[3] = {"act_offset", "pow_offset", "link_offset"};
   for (int a = 0; a < 3; a++) {
@@ -955,7 +1005,7 @@ static int ensure_common_lockstep(cpr_batch* b, int obs_len) {
   HIP_TRY(b->l_done.ensure((size_t)n));
   HIP_TRY(b->l_mask.ensure((size_t)n));
   HIP_TRY(b->l_eps.ensure((size_t)n * sizeof(uint64_t)));
-  HIP_TRY(b->l_info.ensure((size_t)n * (7 * 8 + 2 * 4)));
+  HIP_TRY(b->l_info.ensure((size_t)n * (7 * 8 + 3 * 4)));
   return CPR_OK;
 }
 
@@ -992,7 +1042,7 @@ static int ensure_lockstep(cpr_batch* b) {
   HIP_TRY(b->l_done.ensure((size_t)n));
   HIP_TRY(b->l_mask.ensure((size_t)n));
   HIP_TRY(b->l_eps.ensure((size_t)n * sizeof(uint64_t)));
-  HIP_TRY(b->l_info.ensure((size_t)n * (7 * 8 + 2 * 4)));
+  HIP_TRY(b->l_info.ensure((size_t)n * (7 * 8 + 3 * 4)));
   return CPR_OK;
 }
 
@@ -1078,6 +1128,7 @@ int cpr_step(cpr_batch* b, const int32_t* actions, double* obs, double* reward, 
   sb.eacts = (int64_t*)(ib + 6 * n * 8);
   sb.hh = (int32_t*)(ib + 7 * n * 8);
   sb.hm = (int32_t*)(ib + 7 * n * 8 + n * 4);
+  sb.status = (uint32_t*)(ib + 7 * n * 8 + 2 * n * 4);
   const double* tabs = (const double*)b->tabs_dev.p;
   if (b->is_eth)
     HIP_TRY(launch_eth_step(b->EP, b->cfg.seed, (uint8_t*)b->bk_lmem.p, b->eth_bytes,
@@ -1106,7 +1157,7 @@ int cpr_step(cpr_batch* b, const int32_t* actions, double* obs, double* reward, 
               {info->episode_progress, sb.eprog, 8},       {info->episode_chain_time, sb.ect, 8},
               {info->episode_sim_time, sb.est, 8},         {info->episode_n_steps, sb.esteps, 8},
               {info->episode_n_activations, sb.eacts, 8},  {info->head_height, sb.hh, 4},
-              {info->head_miner, sb.hm, 4}};
+              {info->head_miner, sb.hm, 4},                {info->status, sb.status, 4}};
     for (auto& x : cp)
       if (x.dst) HIP_TRY(hipMemcpyAsync(x.dst, x.src, (size_t)n * x.sz, hipMemcpyDeviceToHost, st));
   }
@@ -1422,6 +1473,7 @@ int cpr_rollout(cpr_batch* b, int64_t n_steps, double* obs, double* reward, uint
   summary->status_tie += s.status_tie;
   summary->status_overlap += s.status_overlap;
   summary->status_other += s.status_other;
+  summary->invalid += s.invalid;
   for (int i = 0; i < CPR_HIST_BINS; i++) summary->hist[i] += s.hist[i];
   return CPR_OK;
 }

@@ -25,6 +25,7 @@
 #include <stdint.h>
 
 #include "cpr_stream.h"
+#include "nakamoto_lane.h"
 
 #pragma clang fp contract(off)
 
@@ -181,6 +182,18 @@ __host__ __device__ inline int32_t eth_policy(int32_t policy, const EthObs& o) {
       return a * 4 + (policy == 4 ? 2 : 3);
     }
   }
+}
+
+// the lane's attack policy: ethereum_ssz (ethereum_ssz.ml:444-521), or in Nakamoto mode the
+// nakamoto_ssz policy / table (nakamoto_ssz.ml:374-440) mapped onto the same agent
+// (Adopt -> Adopt_discard; Override, Match, Wait unchanged; no uncles to choose). Used by
+// the gym step and by the attacker's loop-mode handler alike.
+__host__ __device__ inline int32_t lane_action(const EthParams& P, const EthObs& o) {
+  if (!P.nak) return eth_policy(P.policy, o);
+  const int32_t a = nak_policy(P.policy, o.public_height, o.private_height, o.event, P.table,
+                               P.table_dim);
+  constexpr int32_t map[4] = {A_ADOPT_DISCARD, A_OVERRIDE, A_MATCH, A_WAIT};
+  return map[a & 3] * 4;
 }
 
 // uncle filters of Honest.puzzle_payload' callers
@@ -833,7 +846,7 @@ struct EthLane {
           // loop mode: the attacker node's handler (ethereum_ssz.ml:433-441)
           prepare(P, M, kind, s);
           const EthObs o = observe(P, M, false);
-          const int32_t sh = apply(P, M, eth_policy(P.policy, o));
+          const int32_t sh = apply(P, M, lane_action(P, o));
           if (sh >= 0) share(P, M, 0, sh);
           break;
         }

@@ -27,6 +27,7 @@ struct StepBuffers {
   int64_t* eacts;
   int32_t* hh;
   int32_t* hm;
+  uint32_t* status;  // per-lane cpr_episode_status bits of the current episode (always written)
 };
 
 // persistent per-lane memory of the lockstep lanes (device pointers)

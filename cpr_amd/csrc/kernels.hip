@@ -78,7 +78,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(MODE == 
     int64_t* redo, uint32_t* redo_n, uint32_t launch_id, int64_t redo_cap) {
   __shared__ int32_t hist[CPR_HIST_BINS];
   __shared__ int32_t ring[RING * kBlock];
-  __shared__ unsigned long long acc_w[12];
+  __shared__ unsigned long long acc_w[13];
   LdsAcc acc{acc_w};
   acc.init();
   if (threadIdx.x < CPR_HIST_BINS) hist[threadIdx.x] = 0;
@@ -222,6 +222,7 @@ __global__ __launch_bounds__(kBlock) void k_step(NakParams P, uint64_t seed, Loc
   const double ra = (double)hd.ra;
   out.reward[i] = ra - LL.last_ra;  // engine.ml:223
   out.done[i] = done ? 1 : 0;
+  out.status[i] = L.status;
   if (out.era) {
     out.era[i] = ra;
     out.erd[i] = (double)(hd.h - hd.ra);

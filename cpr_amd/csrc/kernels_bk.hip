@@ -155,6 +155,7 @@ __global__ __launch_bounds__(kBlock) void k_bk_step(bk::BkParams P, uint64_t see
   const double ra = (double)h.rew_att;
   out.reward[i] = ra - SL.last_ra;  // engine.ml:223
   out.done[i] = done ? 1 : 0;
+  out.status[i] = SL.L.status;
   if (out.era) {
     out.era[i] = ra;
     out.erd[i] = (double)h.rew_def;

@@ -14,16 +14,6 @@
 
 namespace cpr {
 
-// the lane's attack policy: ethereum_ssz (ethereum_ssz.ml:444-521), or in Nakamoto mode the
-// nakamoto_ssz policy / table (nakamoto_ssz.ml:374-440) mapped onto the same agent
-// (Adopt -> Adopt_discard; Override, Match, Wait unchanged; no uncles to choose)
-__device__ inline int32_t eth_lane_action(const eth::EthParams& P, const eth::EthObs& o) {
-  if (!P.nak) return eth::eth_policy(P.policy, o);
-  const int32_t a = nak_policy(P.policy, o.public_height, o.private_height, o.event, P.table,
-                               P.table_dim);
-  constexpr int32_t map[4] = {eth::A_ADOPT_DISCARD, eth::A_OVERRIDE, eth::A_MATCH, eth::A_WAIT};
-  return map[a & 3] * 4;
-}
 
 template <class Src>
 __global__ __launch_bounds__(kBlock) void k_eth_run_episodes(
@@ -46,7 +36,7 @@ __global__ __launch_bounds__(kBlock) void k_eth_run_episodes(
       hd = 0;
       while (!done) {
         const eth::EthObs o = L.observe(P, M, false);
-        hd = L.gym_step(P, S, M, eth_lane_action(P, o), &done);
+        hd = L.gym_step(P, S, M, eth::lane_action(P, o), &done);
       }
     } else {
       hd = L.loop(P, S, M);
@@ -96,7 +86,7 @@ __device__ inline int32_t nak_rerun_one(const eth::EthParams& P, const St& S,
   L.gym_reset(P, S, M);
   bool done = L.dead != 0;
   int32_t hd = 0;
-  while (!done) hd = L.gym_step(P, S, M, eth_lane_action(P, L.observe(P, M, false)), &done);
+  while (!done) hd = L.gym_step(P, S, M, eth::lane_action(P, L.observe(P, M, false)), &done);
   return hd;
 }
 
@@ -107,6 +97,12 @@ __device__ inline void summary_add_episode(cpr_summary* out, int64_t ra, int64_t
   auto add = [](int64_t* p, int64_t v) {
     if (v) atomicAdd((unsigned long long*)p, (unsigned long long)v);
   };
+  if (status & CPR_ST_INVALID) {  // outputs not valid: work counted, nothing else
+    add(&out->steps, steps);
+    add(&out->activations, acts);
+    add(&out->invalid, 1);
+    return;
+  }
   add(&out->episodes, 1);
   add(&out->steps, steps);
   add(&out->activations, acts);
@@ -306,6 +302,7 @@ __global__ __launch_bounds__(kBlock) void k_eth_step(eth::EthParams P, uint64_t 
   const double ra = (double)SL.L.B(P, M, hd).rew_att / 32.0;
   out.reward[i] = ra - SL.last_ra;  // engine.ml:223
   out.done[i] = done ? 1 : 0;
+  out.status[i] = SL.L.status;
   if (out.era) eth_info(P, M, SL, hd, i, out);
   SL.last_ra = ra;
   eth_write_obs(SL.L.observe(P, M, true), unit, tabs, tn, out.obs + 10 * i);
@@ -339,7 +336,7 @@ __global__ __launch_bounds__(kBlock) void k_eth_rollout(eth::EthParams P, uint64
       const int32_t c0 = SL.L.c_act;
       bool done = false;
       const int32_t hd =
-          SL.L.gym_step(P, make_stream(seed, SL.ep), M, eth_lane_action(P, o), &done);
+          SL.L.gym_step(P, make_stream(seed, SL.ep), M, eth::lane_action(P, o), &done);
       acts_all += SL.L.c_act - c0;
       ++steps_all;
       const eth::EBlock& h = SL.L.B(P, M, hd);

@@ -153,6 +153,7 @@ __global__ __launch_bounds__(kBlock) void k_ts_step(ts::TsParams P, uint64_t see
   const ts::TVtx& h = SL.L.X(P, M, hd);
   out.reward[i] = ra - SL.last_ra;
   out.done[i] = done ? 1 : 0;
+  out.status[i] = SL.L.status;
   if (out.era) {
     out.era[i] = ra;
     out.erd[i] = rd;

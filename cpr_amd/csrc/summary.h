@@ -24,13 +24,23 @@ __device__ inline int64_t wave_sum(int64_t v) {
 struct Acc {
   int64_t episodes, steps, activations, ra_fx, rd_fx, prog_fx, orphans, tie, overlap, other;
   uint64_t rel_fx, rel_sq_fx;
+  int64_t invalid;
 };
+
+// cpr_summary word index of `invalid` (after the histogram)
+constexpr int kInvalidWord = 12 + CPR_HIST_BINS;
 
 // one finished episode; rewards and progress in 2^-20 fixed point, rel = attacker share
 // of the head's rewards (wrappers.py:14-26 SparseRelativeRewardWrapper)
 __device__ inline void acc_episode(Acc& a, int64_t ra_fx, int64_t rd_fx, int64_t prog_fx,
                                    double rel, int64_t head_height, int64_t steps,
                                    int64_t acts, uint32_t status, int32_t* hist_lds) {
+  if (status & CPR_ST_INVALID) {  // outputs not valid: work counted, nothing else
+    a.steps += steps;
+    a.activations += acts;
+    a.invalid += 1;
+    return;
+  }
   a.episodes += 1;
   a.steps += steps;
   a.activations += acts;
@@ -49,23 +59,24 @@ __device__ inline void acc_episode(Acc& a, int64_t ra_fx, int64_t rd_fx, int64_t
 }
 
 __device__ inline void block_flush(const Acc& a, int32_t* hist_lds, cpr_summary* out) {
-  __shared__ int64_t red[kBlock / 64][12];
+  __shared__ int64_t red[kBlock / 64][13];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  int64_t v[12] = {a.episodes, a.steps,   a.activations, a.ra_fx,
+  int64_t v[13] = {a.episodes, a.steps,   a.activations, a.ra_fx,
                    a.rd_fx,    a.prog_fx, a.orphans,     a.tie,
-                   a.overlap,  a.other,   (int64_t)a.rel_fx, (int64_t)a.rel_sq_fx};
+                   a.overlap,  a.other,   (int64_t)a.rel_fx, (int64_t)a.rel_sq_fx,
+                   a.invalid};
 #pragma unroll
-  for (int i = 0; i < 12; ++i) v[i] = wave_sum(v[i]);
+  for (int i = 0; i < 13; ++i) v[i] = wave_sum(v[i]);
   if (lane == 0)
 #pragma unroll
-    for (int i = 0; i < 12; ++i) red[wave][i] = v[i];
+    for (int i = 0; i < 13; ++i) red[wave][i] = v[i];
   __syncthreads();
-  if (threadIdx.x < 12) {
+  if (threadIdx.x < 13) {
     int64_t s = 0;
     for (int w = 0; w < kBlock / 64; ++w) s += red[w][threadIdx.x];
     unsigned long long* base = (unsigned long long*)out;
     // cpr_summary word index of each accumulator (rel sums sit before orphans)
-    const int idx[12] = {0, 1, 2, 3, 4, 5, 8, 9, 10, 11, 6, 7};
+    const int idx[13] = {0, 1, 2, 3, 4, 5, 8, 9, 10, 11, 6, 7, kInvalidWord};
     if (s) atomicAdd(base + idx[threadIdx.x], (unsigned long long)s);
   }
   if (threadIdx.x < CPR_HIST_BINS && hist_lds[threadIdx.x])
@@ -78,9 +89,9 @@ __device__ inline void block_flush(const Acc& a, int32_t* hist_lds, cpr_summary*
 // finished episode into the workgroup's 12 words, then one global atomic per field.
 // Word order is cpr_summary's.
 struct LdsAcc {
-  unsigned long long* w;  // 12 words in LDS
+  unsigned long long* w;  // 13 words in LDS (word 12 = invalid)
   __device__ inline void init() {
-    if (threadIdx.x < 12) w[threadIdx.x] = 0ull;
+    if (threadIdx.x < 13) w[threadIdx.x] = 0ull;
   }
   __device__ inline void episode(int64_t ra_fx, int64_t rd_fx, int64_t prog_fx, double rel,
                                  int64_t head_height, int64_t steps, int64_t acts,
@@ -88,6 +99,12 @@ struct LdsAcc {
     auto add = [&](int i, int64_t v) {
       if (v) atomicAdd(&w[i], (unsigned long long)v);
     };
+    if (status & CPR_ST_INVALID) {  // outputs not valid: work counted, nothing else
+      add(1, steps);
+      add(2, acts);
+      add(12, 1);
+      return;
+    }
     add(0, 1);
     add(1, steps);
     add(2, acts);
@@ -106,8 +123,9 @@ struct LdsAcc {
   }
   // after __syncthreads()
   __device__ inline void flush(const int32_t* hist_lds, cpr_summary* out) const {
-    if (threadIdx.x < 12 && w[threadIdx.x])
-      atomicAdd((unsigned long long*)out + threadIdx.x, w[threadIdx.x]);
+    if (threadIdx.x < 13 && w[threadIdx.x])
+      atomicAdd((unsigned long long*)out + (threadIdx.x < 12 ? threadIdx.x : kInvalidWord),
+                w[threadIdx.x]);
     if (threadIdx.x < CPR_HIST_BINS && hist_lds[threadIdx.x])
       atomicAdd((unsigned long long*)&out->hist[threadIdx.x],
                 (unsigned long long)hist_lds[threadIdx.x]);

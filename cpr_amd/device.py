@@ -84,8 +84,8 @@ def make_config(
     k=8,
     table_dim=None,
     subblock_selection=1,
-    delay_lo=0.0,
-    delay_hi=0.0,
+    delay_lo=math.nan,
+    delay_hi=math.nan,
 ):
     """Build a cpr_config. ``defenders=None`` applies the gym's rule
     d = max(2, ceil(1 / (1 - gamma))) (gym/ocaml/cpr_gym/envs.py:146-153).
@@ -221,6 +221,7 @@ class Batch:
                 "episode_n_activations": np.zeros(n, dtype=np.int64),
                 "head_height": np.zeros(n, dtype=np.int32),
                 "head_miner": np.zeros(n, dtype=np.int32),
+                "status": np.zeros(n, dtype=np.uint32),
             }
             si = L.StepInfo()
             for k, v in info.items():

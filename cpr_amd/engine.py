@@ -166,6 +166,15 @@ def step(ienv, action):
     if a < 0 or a >= len(_space(ienv)["actions"]):
         raise IndexError("index out of bounds")  # Action.of_int on table (nakamoto_ssz.ml:252)
     obs, rew, done, inf = ienv.batch.step(np.array([a], dtype=np.int32))
+    status = int(inf["status"][0])
+    if status & L.ST_REFERENCE_RAISES:
+        # tailstorm.ml: List.for_all2 in summary dedup (simulator.ml:139-159),
+        # Division_by_zero in n_choose_k, assert false in heuristic_quorum
+        raise RuntimeError("the reference simulator raises an exception at this step "
+                           "(CPR_ST_REFERENCE_RAISES); the episode has no valid outcome")
+    if status & L.ST_CAPACITY:
+        raise RuntimeError("device lane capacity exceeded (CPR_ST_CAPACITY); the episode's "
+                           "outputs are not valid")
     ra = float(inf["episode_reward_attacker"][0])
     rd = float(inf["episode_reward_defender"][0])
     prog = float(inf["episode_progress"][0])
@@ -214,6 +223,10 @@ def step(ienv, action):
         info["protocol_family"] = "nakamoto"
         info["head_height"] = int(inf["head_height"][0])
         info["head_miner"] = _miner_str(int(inf["head_miner"][0]))
+    if status & L.ST_LOCKSTEP_INEXACT:
+        # Nakamoto lockstep lane outside its closed form (an activation inside a delivery
+        # window, a fork deeper than the lane's slots): outputs not exact; not a reference key
+        info["device_status"] = status
     ienv._last = (ra, rd, prog, ct, st)
     return obs[0].copy(), float(rew[0]), bool(done[0]), info
 

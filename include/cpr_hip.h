@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define CPR_ABI_VERSION 5
+#define CPR_ABI_VERSION 6
 
 typedef struct cpr_ctx cpr_ctx;
 typedef struct cpr_batch cpr_batch;
@@ -174,6 +174,14 @@ enum cpr_episode_status {
                                  re-run's, and the lane's flags are kept beside this bit */
 };
 
+/* status bits that make an episode's outputs invalid; such episodes never enter a
+ * summary's sums (cpr_summary.invalid counts them). A Nakamoto lockstep lane (cpr_step)
+ * whose status holds OVERLAP, DEEP_FORK, TIE_UNRESOLVED or STALE_TIME has inexact outputs
+ * too: live envs cannot be re-run, so the caller sees the bits in cpr_step_info.status. */
+#define CPR_ST_INVALID (CPR_ST_CAPACITY | CPR_ST_REFERENCE_RAISES | CPR_ST_TRACE_MISS)
+#define CPR_ST_LOCKSTEP_INEXACT \
+  (CPR_ST_OVERLAP | CPR_ST_DEEP_FORK | CPR_ST_TIE_UNRESOLVED | CPR_ST_STALE_TIME)
+
 typedef struct cpr_config {
   int32_t protocol;          /* enum cpr_protocol */
   int32_t network;           /* enum cpr_network */
@@ -196,7 +204,8 @@ typedef struct cpr_config {
   int64_t n_lanes;           /* lockstep lanes for cpr_reset/cpr_step; 0 = none */
   int32_t k;                 /* B_k / Tailstorm: votes per block (bk.ml:7), >= 1 */
   int32_t subblock_selection;/* Tailstorm: enum cpr_subblock_selection */
-  double delay_lo, delay_hi;  /* CPR_NET_HONEST_CLIQUE link delays; 0, 0 = 0.5, 1.5 (models.ml) */
+  double delay_lo, delay_hi;  /* CPR_NET_HONEST_CLIQUE link delays U[lo, hi); NaN, NaN = the
+                                 models.ml default 0.5, 1.5 (0, 0 is a real zero delay) */
 } cpr_config;
 
 /* one finished episode; identical layout is produced by the CPU oracle */
@@ -229,8 +238,10 @@ typedef struct cpr_summary {
   int64_t orphans;              /* activations - head height */
   int64_t status_tie;           /* episodes with CPR_ST_TIE */
   int64_t status_overlap;       /* episodes with CPR_ST_OVERLAP */
-  int64_t status_other;
+  int64_t status_other;         /* valid episodes with other status bits */
   int64_t hist[CPR_HIST_BINS];  /* relative revenue histogram, bin = floor(rel*64) */
+  int64_t invalid;              /* episodes with CPR_ST_INVALID bits: counted here and in
+                                   steps / activations only, never in episodes or any sum */
 } cpr_summary;
 
 /* lockstep info, structure of arrays, one entry per lane (engine.ml:224-241) */
@@ -244,6 +255,9 @@ typedef struct cpr_step_info {
   int64_t* episode_n_activations;
   int32_t* head_height;
   int32_t* head_miner;
+  uint32_t* status;  /* cpr_episode_status bits of the lane's episode (CPR_ST_INVALID: the
+                        reference would have raised / the lane's capacity was exceeded;
+                        CPR_ST_LOCKSTEP_INEXACT: Nakamoto outputs not exact) */
 } cpr_step_info;
 
 /* An exported activation/delay trace: every random draw of n_episodes

@@ -174,6 +174,55 @@ int oracle_two_agents_task(int rng_mode, void* rng, uint64_t seed, uint64_t epis
   }
 }
 
+// Simulator.loop task on experiments/simulate/models.ml:54-84 selfish_mining: node 0 the
+// nakamoto_ssz attacker (policy), `defenders` honest Nakamoto nodes, Network.T.selfish_mining
+// with activation delay 1 and defender message delay msg_delay (the withholding sweep's
+// gamma-* rows, withholding.ml:29-52). gamma = 0 keeps the attacker's messages at t = +inf;
+// Simulator.loop drains them after the last activation (simulator.ml:519-533). Outputs per
+// node (defenders + 1 entries).
+int oracle_sm_task(int rng_mode, void* rng, uint64_t seed, uint64_t episode, double alpha,
+                   double gamma, int defenders, double msg_delay, int policy, int activations,
+                   int64_t* acts_out, double* rewards_out, double* head_time,
+                   double* head_progress, int32_t* head_height, int32_t* head_miner,
+                   uint32_t* diag) {
+  try {
+    Network net = Network::selfish_mining(alpha, 1.0, gamma, msg_delay, defenders);
+    std::unique_ptr<SimRng> r;
+    if (rng_mode == 0)
+      r.reset(new OcamlSimRng((OcamlRandom*)rng, net));
+    else
+      r.reset(new KeyedSimRng(seed, episode, net));
+    r = trace_wrap(std::move(r), net, false);
+    Sim sim(net, r.get());
+    std::vector<std::unique_ptr<NodeImpl>> nodes;
+    auto* att = new NakSszAttackerNode();
+    att->policy = policy;
+    nodes.emplace_back(att);
+    for (int i = 0; i < defenders; ++i) nodes.emplace_back(new NakHonest());
+    sim.init(std::move(nodes));
+    Block* root = sim.roots.back();
+    att->agent.sim = &sim;
+    att->agent.my_id = 0;
+    att->agent.init(root);
+    for (int i = 1; i <= defenders; ++i) static_cast<NakHonest*>(sim.nodes[i].get())->state = root;
+    sim.loop(activations);
+    Block* h = sim.head();
+    for (int i = 0; i <= defenders; i++) {
+      acts_out[i] = sim.activations[i];
+      rewards_out[i] = h->rewards[i];
+    }
+    *head_time = Sim::timestamp(h);
+    *head_progress = (double)h->value.height;
+    *head_height = h->value.height;
+    *head_miner = h->value.miner;
+    if (diag) *diag = sim.diag;
+    return 0;
+  } catch (std::exception& e) {
+    set_err(e.what());
+    return -1;
+  }
+}
+
 // ---------------- gym env handle (engine.ml:97-273 for nakamoto_ssz)
 static GymParams params_of(const cpr_config* c) {
   GymParams p;
@@ -547,7 +596,7 @@ static int run_loop_episode(const cpr_config* c, uint64_t ep, cpr_episode_record
   if (c->network == CPR_NET_HONEST_CLIQUE &&
       (c->protocol == CPR_PROTO_NAKAMOTO || c->protocol == CPR_PROTO_ETHEREUM)) {
     const int n = c->defenders;
-    const bool dflt = c->delay_lo == 0. && c->delay_hi == 0.;
+    const bool dflt = std::isnan(c->delay_lo) && std::isnan(c->delay_hi);  // NaN: models.ml default
     std::vector<int64_t> a(n);
     std::vector<double> r(n);
     double ht, hp;
@@ -575,7 +624,7 @@ static int run_loop_episode(const cpr_config* c, uint64_t ep, cpr_episode_record
   if (c->network == CPR_NET_HONEST_CLIQUE &&
       (c->protocol == CPR_PROTO_BK || c->protocol == CPR_PROTO_TAILSTORM)) {
     // every node honest (policy ignored), keyed stream
-    const bool dflt = c->delay_lo == 0. && c->delay_hi == 0.;
+    const bool dflt = std::isnan(c->delay_lo) && std::isnan(c->delay_hi);  // NaN: models.ml default
     const Network net = loop_net(2, c->defenders, 0.0, c->activation_delay, 0.0,
                                  dflt ? 0.5 : c->delay_lo, dflt ? 1.5 : c->delay_hi);
     std::vector<double> rw;
@@ -612,8 +661,34 @@ static int run_loop_episode(const cpr_config* c, uint64_t ep, cpr_episode_record
     rec->head_work = 0;
     return 0;
   }
+  if (c->network == CPR_NET_SELFISH_MINING && c->protocol == CPR_PROTO_NAKAMOTO) {
+    const int n = c->defenders + 1;
+    std::vector<int64_t> a(n);
+    std::vector<double> r(n);
+    int32_t hm = -1;
+    if (oracle_sm_task(1, nullptr, c->seed, ep, c->alpha, c->gamma, c->defenders,
+                       c->propagation_delay > 0 ? c->propagation_delay : 1e-9, c->policy,
+                       (int)c->activations, a.data(), r.data(), &ht, &hp, &hh, &hm, &diag) != 0)
+      return -1;
+    rec->reward_attacker = r[0];
+    rec->reward_defender = 0.0;
+    rec->n_activations = 0;
+    for (int i = 1; i < n; ++i) rec->reward_defender += r[i];
+    for (int i = 0; i < n; ++i) rec->n_activations += a[i];
+    rec->progress = hp;
+    rec->chain_time = ht;
+    rec->sim_time = 0.0;
+    rec->n_steps = 0;
+    rec->head_height = hh;
+    rec->head_miner = -1;  // as every loop-mode record (oracle_sm_task reports the miner)
+    (void)hm;
+    rec->status = 0;
+    rec->head_work = 0;
+    return 0;
+  }
   if (c->network != CPR_NET_TWO_AGENTS) {
-    set_err("oracle loop mode: two-agents network or honest clique only");
+    set_err("oracle loop mode: two-agents network, selfish-mining network (Nakamoto) or "
+            "honest clique only");
     return -2;
   }
   if (c->protocol == CPR_PROTO_TAILSTORM) {

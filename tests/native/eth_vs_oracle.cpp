@@ -2,7 +2,10 @@
 // (cpr_amd/csrc/ethereum_lane.h, compiled here for the host) against the CPU oracle's
 // restatement (oracle/src/ethereum.cpp), step by step on the same keyed stream: all ten
 // observation fields (including the three dry-run uncle selections) and the step info
-// after every step; loop-mode tasks on the two-agents network compared at the end.
+// after every step; loop-mode tasks on the two-agents network compared at the end; and the
+// lane in Nakamoto mode (P.nak) running Simulator.loop tasks on the selfish-mining network
+// with a nakamoto_ssz attacker (the withholding sweep's gamma-* tasks, incl. gamma = 0)
+// against the oracle's oracle_sm_task.
 // Prints one JSON summary line; exit code 1 on any mismatch.
 #include <cmath>
 #include <cstdio>
@@ -30,8 +33,15 @@ struct Cfg {
   int policy;  // 0..4 ethereum_ssz policies, 5 = random actions, 6 = random biased to release
   int scheme;
   int steps;
-  int two_agents;
+  int two_agents;  // 2: Nakamoto-mode loop task on the selfish-mining network
+  double prop = 1e-9;
 };
+
+extern "C" int oracle_sm_task(int rng_mode, void* rng, uint64_t seed, uint64_t episode,
+                              double alpha, double gamma, int defenders, double msg_delay,
+                              int policy, int activations, int64_t* acts_out,
+                              double* rewards_out, double* head_time, double* head_progress,
+                              int32_t* head_height, int32_t* head_miner, uint32_t* diag);
 
 struct Counters {
   long episodes = 0, mismatches = 0, capacity = 0, steps = 0;
@@ -40,19 +50,21 @@ struct Counters {
 static eth::EthParams params_of(const Cfg& cf) {
   eth::EthParams P{};
   P.t_att = oracle::alpha_threshold(cf.alpha);
-  P.d = cf.two_agents ? 1 : cf.defenders;
+  P.d = cf.two_agents == 1 ? 1 : cf.defenders;
   P.n = P.d + 1;
-  P.net = cf.two_agents ? 1 : 0;
+  P.net = cf.two_agents == 1 ? 1 : 0;
   P.mode = cf.two_agents ? 1 : 0;
+  P.nak = cf.two_agents == 2 ? 1 : 0;
   P.policy = cf.policy < 5 ? cf.policy : 0;
   P.scheme = cf.scheme;
   P.cap_b = 1;
   while (P.cap_b < cf.steps + 2) P.cap_b <<= 1;
   P.cap_e = 64 + 512 * P.n + (cf.gamma == 0.0 ? 2 * P.d * cf.steps : 0);
+  if (cf.two_agents == 2 && cf.gamma != 0.0) P.cap_e += P.d * (cf.steps + 2);  // capi.hip
   P.ev = 1.0;
-  P.delta = 1e-9;
+  P.delta = cf.prop;
   const double dd = cf.defenders;
-  P.dmax = (dd - 1.) / dd * 1e-9 / cf.gamma;
+  P.dmax = (dd - 1.) / dd * cf.prop / cf.gamma;
   P.max_steps = cf.steps;
   P.activations = cf.steps;
   P.max_progress = __builtin_inf();
@@ -183,6 +195,49 @@ static bool run_loop(const Cfg& cf, uint64_t seed, uint64_t ep, Counters& C, std
   return true;
 }
 
+static bool run_sm_loop(const Cfg& cf, uint64_t seed, uint64_t ep, Counters& C,
+                        std::string& why) {
+  const int n = cf.defenders + 1;
+  std::vector<int64_t> acts(n);
+  std::vector<double> rew(n);
+  double ht, hp;
+  int32_t hh, hm;
+  uint32_t diag = 0;
+  if (oracle_sm_task(1, nullptr, seed, ep, cf.alpha, cf.gamma, cf.defenders, cf.prop, cf.policy,
+                     cf.steps, acts.data(), rew.data(), &ht, &hp, &hh, &hm, &diag) != 0) {
+    why = "oracle_sm_task failed";
+    C.mismatches++;
+    return false;
+  }
+  double rd = 0.0;
+  for (int i = 1; i < n; ++i) rd += rew[i];
+  const eth::EthParams P = params_of(cf);
+  std::vector<uint8_t> mem(eth::eth_lane_bytes(P.cap_b, P.cap_e, P.n));
+  const eth::EthMem M = eth::eth_mem_at(mem.data(), P.cap_b, P.cap_e, P.n);
+  const Stream S{(uint32_t)seed, (uint32_t)(seed >> 32), (uint32_t)ep, (uint32_t)(ep >> 32)};
+  eth::EthLane L;
+  const int32_t hd = L.loop(P, S, M);
+  if (L.dead) {
+    C.capacity++;
+    return true;
+  }
+  const eth::EBlock& hb = L.B(P, M, hd);
+  C.episodes++;
+  C.steps += cf.steps;
+  if (hb.rew_att / 32.0 != rew[0] || hb.rew_def / 32.0 != rd || hb.height != hh ||
+      hb.time != ht || L.act0 != acts[0]) {
+    char buf[400];
+    snprintf(buf, sizeof buf,
+             "sm loop lane (ra %.5f rd %.5f h %d tm %.17g a0 %d) oracle (%.5f %.5f %d %.17g %ld)",
+             hb.rew_att / 32.0, hb.rew_def / 32.0, hb.height, hb.time, L.act0, rew[0], rd, hh,
+             ht, (long)acts[0]);
+    why = buf;
+    C.mismatches++;
+    return false;
+  }
+  return true;
+}
+
 int main(int argc, char** argv) {
   const int eps = argc > 1 ? atoi(argv[1]) : 20;
   const int steps = argc > 2 ? atoi(argv[2]) : 200;
@@ -199,17 +254,29 @@ int main(int argc, char** argv) {
   cfgs.push_back(Cfg{0.4, 0.75, 7, 6, 1, steps, 0});
   for (double a : alphas)
     for (int pol : {0, 1, 2, 3, 4}) cfgs.push_back(Cfg{a, 0, 1, pol, 1, steps * 4, 1});
+  // withholding.ml:29-52 gamma-* tasks (defender message delay 1e-4, and a longer one that
+  // makes in-flight overlaps common), nakamoto_ssz policies 0..3
+  for (double a : {0.1, 0.25, 0.35, 0.45, 0.5})
+    for (double g : {0.0, 0.5, 0.75, 0.9})
+      for (int pol : {0, 1, 2, 3})
+        for (double prop : {1e-4, 0.05}) {
+          const int d = std::max(2, (int)std::ceil(1.0 / (1.0 - g)));
+          cfgs.push_back(Cfg{a, g, d, pol, 0, steps * 4, 2, prop});
+        }
   Counters C;
   int shown = 0;
   for (auto& cf : cfgs)
     for (int e = 0; e < eps; e++) {
       std::string why;
-      const bool ok = cf.two_agents ? run_loop(cf, seed, e, C, why) : run_gym(cf, seed, e, C, why);
+      const bool ok = cf.two_agents == 2   ? run_sm_loop(cf, seed, e, C, why)
+                      : cf.two_agents == 1 ? run_loop(cf, seed, e, C, why)
+                                           : run_gym(cf, seed, e, C, why);
       if (!ok && shown < 10) {
         shown++;
-        fprintf(stderr, "MISMATCH alpha=%g gamma=%g d=%d pol=%d scheme=%d two=%d ep=%d: %s\n",
-                cf.alpha, cf.gamma, cf.defenders, cf.policy, cf.scheme, cf.two_agents, e,
-                why.c_str());
+        fprintf(stderr,
+                "MISMATCH alpha=%g gamma=%g d=%d pol=%d scheme=%d net=%d prop=%g ep=%d: %s\n",
+                cf.alpha, cf.gamma, cf.defenders, cf.policy, cf.scheme, cf.two_agents, cf.prop,
+                e, why.c_str());
       }
     }
   printf("{\"episodes\": %ld, \"steps\": %ld, \"mismatches\": %ld, \"capacity\": %ld}\n",

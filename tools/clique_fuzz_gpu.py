@@ -34,7 +34,7 @@ for i in range(n_cfg):
                                    network=L.NET_HONEST_CLIQUE, mode=L.MODE_LOOP, protocol=proto,
                                    reward_scheme=sch, k=k, subblock_selection=sel,
                                    activation_delay=ad, activations=acts, seed=1000 + i, policy=0,
-                                   delay_lo=lo, delay_hi=hi if hi > 0 else 1e-300)
+                                   delay_lo=lo, delay_hi=hi)
     b = device.Batch(cfg, keep=keep)
     _, rec = b.run(32, records=True)
     ref = O.run_episodes(cfg, 0, 32, threads=8)
