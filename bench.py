@@ -32,45 +32,64 @@ VALU_PEAK_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12  # 256 CU x 4 SIMD32 x 32 lanes/clk
 SEED = 0x5EED0000
 
 
+def _host_cores():
+    """Cores this process may use: the affinity mask, capped by the job's CPU share when
+    the environment states one (the GPU box exports OMP_NUM_THREADS = its per-GPU share;
+    nproc there counts the whole machine)."""
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except AttributeError:
+        aff = os.cpu_count() or 1
+    share = os.environ.get("OMP_NUM_THREADS")
+    cores = min(aff, int(share)) if share and share.isdigit() and int(share) > 0 else aff
+    return max(1, cores), aff
+
+
 def cpu_baseline(seconds, points):
-    """The CPU oracle (faithful DES restatement) on the host cores, bounded sample."""
+    """The CPU oracle (faithful DES restatement, oracle/src/des.cpp) on the host: one run on
+    every core this job may use and one on a single core, each a bounded sample of the
+    same sweep points (all-core and single-process numbers)."""
     sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "tests"))
     import oracle_py
     from cpr_amd import device
 
-    try:
-        cores = len(os.sched_getaffinity(0))
-    except AttributeError:
-        cores = os.cpu_count() or 1
-    threads = max(1, min(16, cores))
-    per_point = 4 * threads
-    acts = 0
-    eps = 0
-    t0 = time.perf_counter()
-    i = 0
-    while time.perf_counter() - t0 < seconds:
-        alpha, gamma = points[i % len(points)]
-        cfg, _ = device.make_config(alpha=alpha, gamma=gamma, max_steps=STEPS_PER_EPISODE,
-                                    seed=SEED)
-        rec = oracle_py.run_episodes(cfg, 10**9 + i * per_point, per_point, threads=threads)
-        acts += int(rec["n_activations"].sum())
-        eps += per_point
-        i += 1
-    dt = time.perf_counter() - t0
+    cores, aff = _host_cores()
+
+    def sample(threads, budget, base):
+        per_point = 4 * threads
+        acts = eps = i = 0
+        t0 = time.perf_counter()
+        while time.perf_counter() - t0 < budget:
+            alpha, gamma = points[i % len(points)]
+            cfg, _ = device.make_config(alpha=alpha, gamma=gamma, max_steps=STEPS_PER_EPISODE,
+                                        seed=SEED)
+            rec = oracle_py.run_episodes(cfg, base + i * per_point, per_point, threads=threads)
+            acts += int(rec["n_activations"].sum())
+            eps += per_point
+            i += 1
+        return acts, eps, time.perf_counter() - t0
+
+    acts, eps, dt = sample(cores, seconds * 0.6, 10**9)
+    acts1, eps1, dt1 = sample(1, seconds * 0.4, 2 * 10**9)
     return {
         "value": acts / dt,
         "unit": "activations/s",
-        "cores": threads,
+        "cores": cores,
         "kind": "port",
         "sample": f"{eps} episodes x {STEPS_PER_EPISODE} steps of the same sweep points "
-                  f"({dt:.1f} s, {threads} threads, oracle/src/des.cpp event-driven DES)",
+                  f"({dt:.1f} s on {cores} threads; the host's affinity mask holds {aff} cores, "
+                  f"the job's CPU share is {cores}; oracle/src/des.cpp event-driven DES)",
         "episodes_per_s": eps / dt,
+        "single_core": {"value": acts1 / dt1, "unit": "activations/s", "cores": 1,
+                        "sample": f"{eps1} episodes ({dt1:.1f} s)"},
+        "affinity_cores": aff,
     }
 
 
-# algorithmic HBM bytes per activation of k_run_episodes: the f64 activation-time log
-# store (DESIGN.md §4.2); episode outputs add ~0.02 B
-ALG_BYTES_PER_ACT = 8.0
+# algorithmic HBM bytes of k_run_episodes (SURVEY.md §8d): the Monte-Carlo outputs,
+# ~48 B per episode (rewards, progress, status; the summary's share is negligible)
+ALG_BYTES_PER_EPISODE = 48.0
+HBM_PEAK_GBS = 8000.0
 
 
 def pmc_traffic(episodes):
@@ -208,7 +227,9 @@ def main():
                 # lane-instructions the kernel really issues per activation, beside the
                 # 40-op cost model `achieved` is priced at
                 "measured_valu_lane_ops_per_activation": valu_meas,
-                "algorithmic_bytes_per_launch": ALG_BYTES_PER_ACT * E * (STEPS_PER_EPISODE + 1),
+                "algorithmic_bytes_per_launch": ALG_BYTES_PER_EPISODE * E,
+                "hbm_frac_algorithmic": ALG_BYTES_PER_EPISODE * E / (kms.mean() / 1e3)
+                / (HBM_PEAK_GBS * 1e9),
                 "kernel": "k_run_episodes",
                 "kernel_ms_mean": float(kms.mean()),
                 "kernel_activations_per_s": act_per_s_kernel,

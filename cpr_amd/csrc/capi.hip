@@ -68,23 +68,35 @@ struct cpr_ctx {
   // episode-kernel launch since then
   DevBuf rq, rtab, rmem;
   std::vector<RerunLaunch> rlaunch, rlaunch_up;
+  // per-lane scratch regions of fused-episode launches (event-engine rings and heaps, the
+  // Nakamoto lane's spill / time log / tie-replay scratch), shared by every batch of the
+  // context: launches on the context's stream run in order, so one grow-only pool serves an
+  // alpha x gamma sweep of any number of batches
+  DevBuf pool;
 };
+
+// the context's scratch pool with at least `bytes`
+static hipError_t ctx_pool(cpr_ctx* c, size_t bytes, void** out) {
+  hipError_t e = c->pool.ensure(bytes);
+  *out = c->pool.p;
+  return e;
+}
+
+static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
 struct cpr_batch {
   cpr_ctx* ctx;
   cpr_config cfg;
   NakParams P;
   eth::EthParams EP;     // CPR_PROTO_ETHEREUM
-  DevBuf eth_mem;        // lanes x eth_lane_bytes
   bool is_eth = false;   // Ethereum lockstep lanes share bk_lmem / bk_slots
   bool nak_ev = false;   // Nakamoto on the event engine (nak_on_event_engine): Ethereum lanes
                          // in Nakamoto mode (EP)
   int64_t eth_bytes = 0;
   bk::BkParams BP;       // CPR_PROTO_BK
-  DevBuf bk_mem;         // fused episodes: lanes x bk_bytes
   DevBuf bk_lmem, bk_slots;  // lockstep lanes: n_lanes x bk_bytes, n_lanes slots
   int64_t bk_bytes = 0;
-  ts::TsParams TP;       // CPR_PROTO_TAILSTORM (shares bk_mem / bk_lmem / bk_slots)
+  ts::TsParams TP;       // CPR_PROTO_TAILSTORM (shares bk_lmem / bk_slots)
   bool is_ev = false;    // B_k or Tailstorm event-engine lanes
   // Nakamoto fused episodes: exact re-runs of flagged episodes on the event engine
   bool has_rerun = false;
@@ -93,9 +105,8 @@ struct cpr_batch {
   bool async_launch = false;  // last launch came from cpr_run_episodes_async
   std::vector<uint8_t> table_host;
   DevBuf table_dev, tabs_dev;  // policy table; unit-observation tables
-  DevBuf spill, tlog, replay, summary, records;
+  DevBuf summary, records;
   DevBuf tr_off, tr_miner, tr_delay, tr_pow, tr_key, tr_ldelay;  // cpr_replay trace copy
-  int64_t lanes_alloc = 0;
   // lockstep lanes
   DevBuf lanes, lring, lspill, ltlog, lreplay, l_obs, l_act, l_rew, l_done, l_mask, l_eps, l_info;
   bool reset_done = false;
@@ -668,11 +679,9 @@ int cpr_batch_destroy(cpr_batch* b) {
   (void)hipStreamSynchronize(b->ctx->stream);
   if (b->ev0) (void)hipEventDestroy(b->ev0);
   if (b->ev1) (void)hipEventDestroy(b->ev1);
-  b->eth_mem.release();
-  b->bk_mem.release();
   b->bk_lmem.release();
   b->bk_slots.release();
-  for (DevBuf* d : {&b->table_dev, &b->tabs_dev, &b->spill, &b->tlog, &b->replay, &b->summary,
+  for (DevBuf* d : {&b->table_dev, &b->tabs_dev, &b->summary,
                     &b->records, &b->lanes, &b->lring, &b->lspill, &b->ltlog, &b->lreplay,
                     &b->l_obs, &b->l_act, &b->l_rew, &b->l_done, &b->l_mask, &b->l_eps,
                     &b->l_info, &b->tr_off, &b->tr_miner, &b->tr_delay, &b->tr_pow,
@@ -728,17 +737,18 @@ static int run_async_eth(cpr_batch* b, int64_t n, uint64_t first, const TraceSou
   int64_t lanes = std::min(full, std::max<int64_t>(256, budget));
   lanes = std::min(lanes, ((n + 255) / 256) * 256);
   lanes = std::max<int64_t>(256, (lanes / 256) * 256);
-  HIP_TRY(b->eth_mem.ensure((size_t)lanes * (size_t)b->eth_bytes));
+  void* mem = nullptr;
+  HIP_TRY(ctx_pool(b->ctx, (size_t)lanes * (size_t)b->eth_bytes, &mem));
   if (!b->ev0) {
     HIP_TRY(hipEventCreate(&b->ev0));
     HIP_TRY(hipEventCreate(&b->ev1));
   }
   HIP_TRY(hipEventRecord(b->ev0, b->ctx->stream));
   if (tr)
-    HIP_TRY(launch_eth_replay_episodes(b->EP, *tr, n, (uint8_t*)b->eth_mem.p, b->eth_bytes,
+    HIP_TRY(launch_eth_replay_episodes(b->EP, *tr, n, (uint8_t*)mem, b->eth_bytes,
                                        lanes, rec_dev, sum_dev, b->ctx->stream));
   else
-    HIP_TRY(launch_eth_run_episodes(b->EP, b->cfg.seed, first, n, (uint8_t*)b->eth_mem.p,
+    HIP_TRY(launch_eth_run_episodes(b->EP, b->cfg.seed, first, n, (uint8_t*)mem,
                                     b->eth_bytes, lanes, rec_dev, sum_dev, b->ctx->stream));
   HIP_TRY(hipEventRecord(b->ev1, b->ctx->stream));
   return CPR_OK;
@@ -753,13 +763,14 @@ static int run_async_bk(cpr_batch* b, int64_t n, uint64_t first, const TraceSour
   int64_t lanes = std::min(full, std::max<int64_t>(256, budget));
   lanes = std::min(lanes, ((n + 255) / 256) * 256);
   lanes = std::max<int64_t>(256, (lanes / 256) * 256);
-  HIP_TRY(b->bk_mem.ensure((size_t)lanes * (size_t)b->bk_bytes));
+  void* pool = nullptr;
+  HIP_TRY(ctx_pool(b->ctx, (size_t)lanes * (size_t)b->bk_bytes, &pool));
   if (!b->ev0) {
     HIP_TRY(hipEventCreate(&b->ev0));
     HIP_TRY(hipEventCreate(&b->ev1));
   }
   HIP_TRY(hipEventRecord(b->ev0, b->ctx->stream));
-  uint8_t* mem = (uint8_t*)b->bk_mem.p;
+  uint8_t* mem = (uint8_t*)pool;
   hipStream_t st = b->ctx->stream;
   if (tsp && tr)
     HIP_TRY(launch_ts_replay_episodes(b->TP, *tr, n, mem, b->bk_bytes, lanes, rec_dev, sum_dev, st));
@@ -782,12 +793,14 @@ static int run_async(cpr_batch* b, int64_t n, uint64_t first, const TraceSource*
     return run_async_eth(b, n, first, tr, sum_dev, rec_dev);
   if (b->is_ev) return run_async_bk(b, n, first, tr, sum_dev, rec_dev);
   const int64_t lanes = episode_lanes(b, n);
-  if (lanes > b->lanes_alloc) {
-    HIP_TRY(b->spill.ensure((size_t)lanes * b->P.cap * sizeof(int32_t)));
-    HIP_TRY(b->tlog.ensure((size_t)lanes * b->P.tlog_len * sizeof(double)));
-    HIP_TRY(b->replay.ensure((size_t)lanes * REPLAY_BYTES));
-    b->lanes_alloc = lanes;
-  }
+  // spill [lane][cap] int32 | time log [slot][lane] f64 | tie-replay scratch [lane]
+  const size_t o_tlog = align256((size_t)lanes * b->P.cap * sizeof(int32_t));
+  const size_t o_replay = o_tlog + align256((size_t)lanes * b->P.tlog_len * sizeof(double));
+  void* pool = nullptr;
+  HIP_TRY(ctx_pool(b->ctx, o_replay + (size_t)lanes * REPLAY_BYTES, &pool));
+  int32_t* spill = (int32_t*)pool;
+  double* tlog = (double*)((char*)pool + o_tlog);
+  uint8_t* replay = (uint8_t*)pool + o_replay;
   if (!b->ev0) {
     HIP_TRY(hipEventCreate(&b->ev0));
     HIP_TRY(hipEventCreate(&b->ev1));
@@ -823,12 +836,11 @@ static int run_async(cpr_batch* b, int64_t n, uint64_t first, const TraceSource*
   HIP_TRY(hipEventRecord(b->ev0, b->ctx->stream));
   if (tr)
     HIP_TRY(launch_replay_episodes(b->P, *tr, n, b->cfg.mode, b->cfg.activations,
-                                   (int32_t*)b->spill.p, (double*)b->tlog.p,
-                                   (uint8_t*)b->replay.p, lanes, rec_dev, sum_dev, redo, redo_n,
+                                   spill, tlog, replay, lanes, rec_dev, sum_dev, redo, redo_n,
                                    launch_id, kRerunQueue, b->ctx->stream));
   else
     HIP_TRY(launch_run_episodes(b->P, b->cfg.seed, first, n, b->cfg.mode, b->cfg.activations,
-                                (int32_t*)b->spill.p, (double*)b->tlog.p, (uint8_t*)b->replay.p,
+                                spill, tlog, replay,
                                 lanes, rec_dev, sum_dev, redo, redo_n, launch_id, kRerunQueue,
                                 b->ctx->stream));
   HIP_TRY(hipEventRecord(b->ev1, b->ctx->stream));

@@ -512,16 +512,35 @@ static int run_bk_gym_episode(const cpr_config* c, const BkTable* tab, uint64_t 
   return 0;
 }
 
+// An episode in which the reference raises (List.for_all2 in summary dedup,
+// Division_by_zero in n_choose_k, assert false / assert in tailstorm.ml) ends with status
+// CPR_ST_REFERENCE_RAISES and zero outputs; one whose optimal quorum would brute-force past
+// the budget (tailstorm.ml:418-507, the device's limit) with CPR_ST_CAPACITY. The device
+// lane flags the same episodes (tests/native/ts_vs_oracle.cpp checks the step).
+static void flagged_record(cpr_episode_record* rec, uint32_t status) {
+  memset(rec, 0, sizeof(*rec));
+  rec->head_miner = -1;
+  rec->status = status;
+}
+
 static int run_ts_gym_episode(const cpr_config* c, uint64_t ep, cpr_episode_record* rec) {
   GymTailstorm g(params_of(c), c->k, c->reward_scheme, c->subblock_selection, 1, nullptr,
                  c->seed, ep);
   double obs[TS_OBS_LEN];
-  g.reset(obs);
   bool done = false;
   StepInfo info{};
-  while (!done) {
-    int a = ts_policy(c->policy, g.observe_int(), c->k);
-    g.step(a, obs, &done, &info);
+  try {
+    g.reset(obs);
+    while (!done) {
+      int a = ts_policy(c->policy, g.observe_int(), c->k);
+      g.step(a, obs, &done, &info);
+    }
+  } catch (BudgetExceeded&) {
+    flagged_record(rec, CPR_ST_CAPACITY);
+    return 0;
+  } catch (std::exception&) {
+    flagged_record(rec, CPR_ST_REFERENCE_RAISES);
+    return 0;
   }
   rec->reward_attacker = info.episode_reward_attacker;
   rec->reward_defender = info.episode_reward_defender;
@@ -641,8 +660,16 @@ static int run_loop_episode(const cpr_config* c, uint64_t ep, cpr_episode_record
       rec->head_miner = r.head_signer;
     } else {
       TsLoopResult r;
-      ts_loop_task(net, 1, nullptr, c->seed, ep, c->k, c->reward_scheme, c->subblock_selection,
-                   -1, (int)c->activations, &r);
+      try {
+        ts_loop_task(net, 1, nullptr, c->seed, ep, c->k, c->reward_scheme,
+                     c->subblock_selection, -1, (int)c->activations, &r);
+      } catch (BudgetExceeded&) {
+        flagged_record(rec, CPR_ST_CAPACITY);
+        return 0;
+      } catch (std::exception&) {
+        flagged_record(rec, CPR_ST_REFERENCE_RAISES);
+        return 0;
+      }
       rw = r.rewards;
       ac.assign(r.activations.begin(), r.activations.end());
       rec->progress = r.head_progress;
@@ -693,9 +720,17 @@ static int run_loop_episode(const cpr_config* c, uint64_t ep, cpr_episode_record
   }
   if (c->protocol == CPR_PROTO_TAILSTORM) {
     TsLoopResult r;
-    ts_loop_task(Network::two_agents(c->activation_delay, c->alpha), 1, nullptr, c->seed, ep,
-                 c->k, c->reward_scheme, c->subblock_selection, c->policy, (int)c->activations,
-                 &r);
+    try {
+      ts_loop_task(Network::two_agents(c->activation_delay, c->alpha), 1, nullptr, c->seed, ep,
+                   c->k, c->reward_scheme, c->subblock_selection, c->policy,
+                   (int)c->activations, &r);
+    } catch (BudgetExceeded&) {
+      flagged_record(rec, CPR_ST_CAPACITY);
+      return 0;
+    } catch (std::exception&) {
+      flagged_record(rec, CPR_ST_REFERENCE_RAISES);
+      return 0;
+    }
     rec->reward_attacker = r.rewards[0];
     rec->reward_defender = r.rewards[1];
     rec->progress = r.head_progress;
