@@ -8,7 +8,7 @@ episode), fused into one kernel launch per point; the batch summary is integer-e
 all-reduced once over RCCL. Weak scaling: E is per GPU.
 
 gamma = 1 is rejected by the reference (gym/ocaml/cpr_gym/envs.py:73-75,
-network.ml:351-354), so the sweep runs gamma in {0, 0.5}.
+network.ml:69-72), so the sweep runs gamma in {0, 0.5}.
 
 Prints one JSON line (rank 0).
 """

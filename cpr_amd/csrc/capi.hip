@@ -1,5 +1,5 @@
 // libcpr_hip C ABI (include/cpr_hip.h): host side. Validation mirrors the reference's
-// engine.ml:37-51 (Parameters.t) and network.ml:343-358 (selfish_mining) so invalid
+// engine.ml:37-51 (Parameters.t) and network.ml:61-76 (selfish_mining) so invalid
 // configurations fail with the same messages; all episode work runs on the device.
 #include <hip/hip_runtime.h>
 
@@ -187,7 +187,7 @@ static int32_t pow2_at_least(int64_t x, int32_t cap) {
   return p;
 }
 
-// engine.ml:37-51 and network.ml:343-358 (messages kept verbatim)
+// engine.ml:37-51 and network.ml:61-76 (messages kept verbatim)
 static int validate_eth(const cpr_config* c, eth::EthParams* P);
 
 // the keyed miner draw for compute weights 1..n (models.ml:3-28), as the oracle's
@@ -319,7 +319,7 @@ static int validate(const cpr_config* c, NakParams* P, eth::EthParams* EP, bk::B
   return CPR_OK;
 }
 
-// Ethereum: engine.ml:37-51 checks shared with Nakamoto, network.ml:343-358, ethereum_ssz
+// Ethereum: engine.ml:37-51 checks shared with Nakamoto, network.ml:61-76, ethereum_ssz
 // policies 0..4, Constant / Discount rewards
 static int validate_eth(const cpr_config* c, eth::EthParams* P) {
   if (std::isnan(c->activation_delay)) return fail(CPR_E_INVALID_ARG, "activation_delay cannot be NaN");
@@ -414,7 +414,7 @@ static constexpr int32_t kRingWindow = 4096;
 // HBM budget for the per-lane regions of the event-engine lanes (288 GB per MI355X)
 static constexpr int64_t kLaneBudget = 96ll << 30;
 
-// B_k: engine.ml:37-51 checks shared with Nakamoto, network.ml:343-358, bk.ml k >= 1,
+// B_k: engine.ml:37-51 checks shared with Nakamoto, network.ml:61-76, bk.ml k >= 1,
 // Constant / Block rewards, bk_ssz policies 0..3 or a table
 static int validate_bk(const cpr_config* c, bk::BkParams* P) {
   if (std::isnan(c->activation_delay)) return fail(CPR_E_INVALID_ARG, "activation_delay cannot be NaN");
@@ -516,7 +516,7 @@ static int validate_bk(const cpr_config* c, bk::BkParams* P) {
   return CPR_OK;
 }
 
-// Tailstorm: engine.ml:37-51 checks, network.ml:343-358, tailstorm.ml k >= 1, the four
+// Tailstorm: engine.ml:37-51 checks, network.ml:61-76, tailstorm.ml k >= 1, the four
 // incentive schemes and three sub-block selections, tailstorm_ssz policies 0..6
 static int validate_ts(const cpr_config* c, ts::TsParams* P) {
   // the B_k checks cover everything but the scheme, selection and policy ranges
@@ -609,7 +609,7 @@ int cpr_batch_create(cpr_ctx* ctx, const cpr_config* cfg, cpr_batch** out) {
     const size_t nb = (size_t)cfg->policy_table_dim * cfg->policy_table_dim * 2;
     b->table_host.assign(cfg->policy_table, cfg->policy_table + nb);
   }
-  // unit-observation tables (ssz_tools.ml:487-491) evaluated with the host libm:
+  // unit-observation tables (ssz_tools.ml:36-39) evaluated with the host libm:
   // [2/pi atan(i) | 0.5 + atan(i - N)/pi (2N) | 2/pi atan(i/k)], i < N
   const double kscale =
       (cfg->protocol == CPR_PROTO_BK || cfg->protocol == CPR_PROTO_TAILSTORM) ? (double)cfg->k : 1.0;
@@ -1278,7 +1278,7 @@ int cpr_policy_actions(cpr_batch* b, int32_t policy, const double* obs, int64_t 
   return CPR_OK;
 }
 
-// ssz_tools.ml:515-524 ranges; nakamoto_ssz.ml:143-161
+// ssz_tools.ml:64-73 ranges; nakamoto_ssz.ml:43-61
 int cpr_observation_spec(cpr_batch* b, int32_t* obs_len, int32_t* n_actions, double* low,
                          double* high) {
   if (!b) return fail(CPR_E_INVALID_ARG, "NULL argument");
@@ -1347,7 +1347,7 @@ int cpr_observation_spec(cpr_batch* b, int32_t* obs_len, int32_t* n_actions, dou
 }
 
 // Collection.add prepends (collection.ml:13): registry order is the reverse of the adds
-// in nakamoto_ssz.ml:442-450
+// in nakamoto_ssz.ml:342-350
 static const char* kNames[4] = {"sapirshtein-2016-sm1", "eyal-sirer-2014", "simple", "honest"};
 static const int32_t kIds[4] = {CPR_POLICY_SAPIRSHTEIN_2016_SM1, CPR_POLICY_EYAL_SIRER_2014,
                                 CPR_POLICY_SIMPLE, CPR_POLICY_HONEST};

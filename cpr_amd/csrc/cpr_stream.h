@@ -140,7 +140,7 @@ struct Stream {
     if ((uint64_t)w.w0 < t_att) return 0;
     return 1 + (int32_t)(((uint64_t)w.w1 * (uint64_t)d) >> 32);
   }
-  // exponential delay of clock j (distributions.ml:120-127)
+  // exponential delay of clock j (distributions.ml:22-29)
   __host__ __device__ inline double clock(uint32_t j, double ev) const {
     const Words4 w = block(j, TAG_ACT);
     return (-1.0 * ev) * cpr_log(u53(w.w2, w.w3));
@@ -163,7 +163,7 @@ struct Stream {
     while (i < nthr && w0 >= thr[i]) ++i;
     return i;
   }
-  // U(lo, hi) delay of the message shared at (kw, off) to dest (distributions.ml:114-118)
+  // U(lo, hi) delay of the message shared at (kw, off) to dest (distributions.ml:16-20)
   __host__ __device__ inline double link_unif(uint32_t kw, uint32_t off, uint32_t dest, double lo,
                                               double hi) const {
     return link_u(kw, off, dest) * (hi - lo) + lo;

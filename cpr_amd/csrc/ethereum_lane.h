@@ -185,7 +185,7 @@ __host__ __device__ inline int32_t eth_policy(int32_t policy, const EthObs& o) {
 }
 
 // the lane's attack policy: ethereum_ssz (ethereum_ssz.ml:444-521), or in Nakamoto mode the
-// nakamoto_ssz policy / table (nakamoto_ssz.ml:374-440) mapped onto the same agent
+// nakamoto_ssz policy / table (nakamoto_ssz.ml:274-340) mapped onto the same agent
 // (Adopt -> Adopt_discard; Override, Match, Wait unchanged; no uncles to choose). Used by
 // the gym step and by the attacker's loop-mode handler alike.
 __host__ __device__ inline int32_t lane_action(const EthParams& P, const EthObs& o) {

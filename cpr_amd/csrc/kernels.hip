@@ -55,7 +55,7 @@ __device__ inline BRef run_gym(NakLane& L, const NakParams& P, const St& S, cons
 }
 
 // Simulator.loop ~activations with the SSZ attacker as node 0 (simulator.ml:519-533,
-// nakamoto_ssz.ml:362-372); all messages delivered before the head is taken.
+// nakamoto_ssz.ml:262-272); all messages delivered before the head is taken.
 template <class St>
 __device__ inline BRef run_loop(NakLane& L, const NakParams& P, const St& S, const LaneMem& M,
                                 int64_t activations) {
@@ -165,7 +165,7 @@ __device__ inline void write_obs(const NakLane& L, int unit, const double* tab_n
   int32_t h, a, d, ev;
   L.observe(&h, &a, &d, &ev);
   if (unit) {
-    // ssz_tools.ml:480-491; host-tabulated (libm) for |x| < tab_n
+    // ssz_tools.ml:29-40; host-tabulated (libm) for |x| < tab_n
     o[0] = h < tab_n ? tab_nn[h] : 2.0 / 3.141592653589793 * atan((double)h / 1.0);
     o[1] = a < tab_n ? tab_nn[a] : 2.0 / 3.141592653589793 * atan((double)a / 1.0);
     o[2] = (d > -tab_n && d < tab_n) ? tab_sg[d + tab_n]
@@ -245,7 +245,7 @@ __global__ void k_observe_fields(const void* lanes, int64_t n, int32_t* f) {
   ((const LockLane*)lanes)[i].L.observe(f + 4 * i, f + 4 * i + 1, f + 4 * i + 2, f + 4 * i + 3);
 }
 
-// engine.ml:258-261: decode the observation (ssz_tools.ml:493-510), apply the policy
+// engine.ml:258-261: decode the observation (ssz_tools.ml:42-59), apply the policy
 __global__ void k_policy(int32_t policy, int unit, const double* obs, int64_t n,
                          const uint8_t* table, int32_t dim, int32_t* actions) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;

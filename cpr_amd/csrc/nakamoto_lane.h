@@ -7,9 +7,9 @@
 //
 // What the lane tracks, and the reference code it stands for:
 //   p0, n, rel      attacker private chain = p0 + n withheld/released blocks, released
-//                   prefix rel (nakamoto_ssz.ml:256-360, simulator.ml:401-419 share)
+//                   prefix rel (nakamoto_ssz.ml:156-260, simulator.ml:401-419 share)
 //   pub             attacker's model of the defender head (deliver_private_to_public,
-//                   nakamoto_ssz.ml:291-318), with its common-ancestor height `fork`
+//                   nakamoto_ssz.ml:191-218), with its common-ancestor height `fork`
 //   D, A, onA       defender tips: every defender holds D or A (bitmask); honest
 //                   update_head (nakamoto.ml:85-95) with first-received tie breaking
 //   b, wminer       the block of the activation the attacker is reacting to
@@ -83,8 +83,8 @@ struct NakParams {
   int32_t d;            // defenders
   int32_t arrive;       // attacker messages reach defenders (gamma > 0 or two-agents)
   double ev;            // activation delay (expected block interval)
-  double delta;         // defender -> defender delay (network.ml:375)
-  double dmax;          // attacker -> defender uniform [0, dmax) (network.ml:350-357)
+  double delta;         // defender -> defender delay (network.ml:93)
+  double dmax;          // attacker -> defender uniform [0, dmax) (network.ml:68-75)
   int64_t max_steps;
   double max_progress;
   double max_time;
@@ -99,7 +99,7 @@ __host__ __device__ inline uint64_t all_mask(int32_t d) {
   return d >= 64 ? ~0ull : ((1ull << d) - 1ull);
 }
 
-// nakamoto_ssz.ml:374-440 (policy registry: sapirshtein-2016-sm1, eyal-sirer-2014,
+// nakamoto_ssz.ml:274-340 (policy registry: sapirshtein-2016-sm1, eyal-sirer-2014,
 // simple, honest)
 __host__ __device__ inline int32_t nak_policy(int32_t policy, int32_t h, int32_t a, int32_t ev,
                                               const uint8_t* table, int32_t dim) {
@@ -401,7 +401,7 @@ struct NakLane {
   }
 
   // StochasticClock + Dag + the attacker's prepare (simulator.ml:465-480, engine.ml:108-121,
-  // nakamoto_ssz.ml:291-318)
+  // nakamoto_ssz.ml:191-218)
   template <class St>
   __host__ __device__ inline void activate(const NakParams& P, const St& S, const LaneMem& M) {
     int32_t miner;
@@ -450,7 +450,7 @@ struct NakLane {
     *ev = event;
   }
 
-  // Agent.apply (nakamoto_ssz.ml:332-359) + Simulator.handle_action share (:401-419)
+  // Agent.apply (nakamoto_ssz.ml:232-260) + Simulator.handle_action share (:401-419)
   __host__ __device__ inline void apply(int32_t action) {
     if (action == A_ADOPT) {
       const bool pub_on_chain = pub.fork == pub.h;

@@ -88,7 +88,7 @@ def make_config(
     delay_hi=math.nan,
 ):
     """Build a cpr_config. ``defenders=None`` applies the gym's rule
-    d = max(2, ceil(1 / (1 - gamma))) (gym/ocaml/cpr_gym/envs.py:146-153).
+    d = max(2, ceil(1 / (1 - gamma))) (gym/ocaml/cpr_gym/envs.py:70-76).
     B_k tables (protocol=PROTO_BK) hold dim*dim*(k+1)*(k+1)*3 actions
     (include/cpr_hip.h CPR_BK_POLICY_TABLE)."""
     if defenders is None and network == L.NET_SELFISH_MINING:
@@ -285,7 +285,7 @@ class Batch:
 
 
 def policy_registry(protocol=L.PROTO_NAKAMOTO):
-    """[(name, id)] in the reference's registry order (nakamoto_ssz.ml:442-450)."""
+    """[(name, id)] in the reference's registry order (nakamoto_ssz.ml:342-350)."""
     out = []
     for i in range(L.lib().cpr_policy_count(protocol)):
         pid = ctypes.c_int32()

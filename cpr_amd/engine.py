@@ -4,7 +4,7 @@ observation_high over one device lane each. The episode state lives on the GPU; 
 step is one launch of the lane state machine (cpr_amd/csrc/*_lane.h).
 
 Randomness: the reference seeds OCaml's Random with ``self_init`` at import
-(cpr_gym_engine.ml:312), so it is not reproducible. Here each ``create`` draws a fresh
+(cpr_gym_engine.ml:39), so it is not reproducible. Here each ``create`` draws a fresh
 64-bit seed from ``os.urandom`` unless ``seed=`` is passed (or CPR_SEED is set).
 """
 
@@ -22,8 +22,8 @@ cpr_lib_version = f"cpr_amd-{__version__}"
 
 MAX_INT = (1 << 62) - 1  # OCaml max_int on 64-bit
 
-_ACTIONS = ["Adopt", "Override", "Match", "Wait"]  # nakamoto_ssz.ml:216-254
-_EVENTS = ["`ProofOfWork", "`Network"]  # ssz_tools.ml:527-531
+_ACTIONS = ["Adopt", "Override", "Match", "Wait"]  # nakamoto_ssz.ml:116-154
+_EVENTS = ["`ProofOfWork", "`Network"]  # ssz_tools.ml:76-80
 
 # per attack space: action names (Variants.to_name, rank order), observation record fields,
 # event values (ssz_tools.ml event_to_string)
@@ -164,7 +164,7 @@ def _space(ienv):
 def step(ienv, action):
     a = int(action)
     if a < 0 or a >= len(_space(ienv)["actions"]):
-        raise IndexError("index out of bounds")  # Action.of_int on table (nakamoto_ssz.ml:252)
+        raise IndexError("index out of bounds")  # Action.of_int on table (nakamoto_ssz.ml:152)
     obs, rew, done, inf = ienv.batch.step(np.array([a], dtype=np.int32))
     status = int(inf["status"][0])
     if status & L.ST_REFERENCE_RAISES:

@@ -127,7 +127,7 @@ def env_fn(
     reward="sparse_relative",
     normalize_reward=True,
 ):
-    """envs.py:175-239: Core + AssumptionScheduleWrapper + reward wrapper (+ r/alpha)."""
+    """envs.py:99-163: Core + AssumptionScheduleWrapper + reward wrapper (+ r/alpha)."""
     ctor = getattr(protocols, protocol)
     args = dict(_protocol_args) if protocol_args is None else {**_protocol_args, **protocol_args}
     reward_wrappers = {
@@ -171,7 +171,7 @@ _registry = {
 
 
 def make(env_id, **kwargs):
-    """gym.make replacement for the ids registered by envs.py:172-267."""
+    """gym.make replacement for the ids registered by envs.py:166-191."""
     env_id = env_id.split(":")[-1]
     ctor, defaults = _registry[env_id]
     return ctor(**{**defaults, **kwargs})

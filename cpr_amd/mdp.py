@@ -2,7 +2,7 @@
 
 SURVEY.md §8f rank 4: the reference derives optimal withholding policies offline with its
 MDP toolbox — the Sapirshtein et al. (FC'16) Bitcoin model (`mdp/lib/models/fc16sapirshtein.py:
-21-205`), explored breadth-first into an explicit MDP (`mdp/lib/compiler.py:6-93`), mapped to
+21-205`), explored breadth-first into an explicit MDP (`mdp/lib/compiler.py:6-90`), mapped to
 a probabilistically terminating MDP (`mdp/lib/models/aft20barzur.py:244-300` `ptmdp`) and
 solved by value iteration (`mdp/lib/explicit_mdp.py:97-177`, used as in
 `mdp/sprint-0-explicit-mdps/util.py:6-14`). This module restates that pipeline (same state
@@ -72,7 +72,7 @@ class BitcoinSM:
 
 
 def compile_mdp(model):
-    """compiler.py:6-93: breadth-first exploration; state ids in discovery order, action ids
+    """compiler.py:6-90: breadth-first exploration; state ids in discovery order, action ids
     = positions in model.actions(state). Returns (states, tab) with
     tab[s][i] = [(dst, p, reward, progress), ...]."""
     ids, states, tab = {}, [], []
@@ -188,7 +188,7 @@ def policy_table(alpha, gamma, *, dim=None, maximum_fork_length=20, horizon=100,
     (a, h, RELEVANT) for event = Network (1) — the attacker's view after its own block or a
     defender's block; an active match (ACTIVE) is not observable by nakamoto_ssz and shares
     the ProofOfWork entry. States the MDP does not reach fall back to the other event's entry,
-    else to honest play (nakamoto_ssz.ml:374-381)."""
+    else to honest play (nakamoto_ssz.ml:275-284)."""
     model, states, vi = solve(alpha, gamma, maximum_fork_length=maximum_fork_length,
                               horizon=horizon, stop_delta=stop_delta)
     dim = maximum_fork_length + 1 if dim is None else dim

@@ -25,7 +25,7 @@ class Protocol:
 
 
 def nakamoto(unit_observation):
-    # nakamoto.ml:3-4 (key, description), nakamoto_ssz.ml:115-121 (attack-space info)
+    # nakamoto.ml:3-4 (key, description), nakamoto_ssz.ml:15-21 (attack-space info)
     info = "SSZ'16 attack space with %s observations" % ("unit" if unit_observation else "raw")
     return Protocol("nakamoto", "Nakamoto consensus", info, unit_observation)
 

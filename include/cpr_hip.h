@@ -7,7 +7,7 @@
  *
  * Reference interfaces each group of entry points replaces (file:line under the
  * pkel/cpr tree):
- *   cpr_version                    -> engine.cpr_lib_version   simulator/gym/cpr_gym_engine.ml:40
+ *   cpr_version                    -> engine.cpr_lib_version   simulator/gym/cpr_gym_engine.ml:41
  *   cpr_batch_create               -> engine.create + Engine.Parameters.t + Engine.of_module
  *                                      simulator/gym/cpr_gym_engine.ml:42-89,
  *                                      simulator/gym/engine.ml:37-51,97-107
@@ -17,12 +17,12 @@
  *                                                              cpr_gym_engine.ml:110-138, engine.ml:258-261
  *   cpr_observation_spec           -> engine.n_actions / observation_low / observation_high
  *                                                              cpr_gym_engine.ml:146-162
- *   cpr_policy_name                -> keys of engine.policies  nakamoto_ssz.ml:442-450
+ *   cpr_policy_name                -> keys of engine.policies  nakamoto_ssz.ml:342-350
  *   cpr_run_episodes               -> a Python loop of env.reset()/env.step(env.policy(obs))
  *                                      (experiments/rl-eval, gym/ocaml/test/test_benchmark.py:5-15)
  *                                      fused into one device launch per batch
  *   cpr_run_episodes (LOOP mode)   -> Simulator.loop ~activations + head
- *                                      simulator/lib/simulator.ml:519-543, csv_runner.ml:244-265
+ *                                      simulator/lib/simulator.ml:519-543, csv_runner.ml:56-98
  *   cpr_stream_fill                -> the randomness the reference draws from OCaml Random
  *                                      (distributions.ml:17,24,90,93; simulator.ml:123),
  *                                      re-specified as a keyed Philox stream
@@ -122,8 +122,8 @@ enum cpr_ethereum_action_rank {
 };
 
 enum cpr_network {
-  CPR_NET_SELFISH_MINING = 0, /* network.ml:343-387, as the gym builds it (engine.ml:100-107) */
-  CPR_NET_TWO_AGENTS = 1,     /* network.ml:332-341 */
+  CPR_NET_SELFISH_MINING = 0, /* network.ml:61-105, as the gym builds it (engine.ml:100-107) */
+  CPR_NET_TWO_AGENTS = 1,     /* network.ml:50-59 */
   CPR_NET_HONEST_CLIQUE = 2   /* experiments/simulate/models.ml:3-28 honest_clique: `defenders`
                                  = n honest nodes (2..64), node i has compute i + 1, every
                                  link delay uniform [delay_lo, delay_hi), simple
@@ -135,7 +135,7 @@ enum cpr_mode {
   CPR_MODE_LOOP = 1  /* episode = Simulator.loop ~activations (simulator.ml:519-533) */
 };
 
-/* policy ids of the nakamoto_ssz attack space, nakamoto_ssz.ml:374-450 */
+/* policy ids of the nakamoto_ssz attack space, nakamoto_ssz.ml:274-350 */
 enum cpr_policy {
   CPR_POLICY_HONEST = 0,
   CPR_POLICY_SIMPLE = 1,
@@ -144,7 +144,7 @@ enum cpr_policy {
   CPR_POLICY_TABLE = 4 /* action = table[(min(pub,D-1)*D + min(priv,D-1))*2 + event] */
 };
 
-/* nakamoto_ssz.ml:216-254, Variants.to_rank */
+/* nakamoto_ssz.ml:116-154, Variants.to_rank */
 enum cpr_nakamoto_action { CPR_ADOPT = 0, CPR_OVERRIDE = 1, CPR_MATCH = 2, CPR_WAIT = 3 };
 
 /* per-episode status bits */
@@ -265,7 +265,7 @@ typedef struct cpr_step_info {
  * bit-exactly on any engine that consumes the same draws. Arrays are CSR over episodes
  * (x_offset has n_episodes + 1 entries, x_offset[0] = 0); all host pointers.
  *   act_miner[j], act_delay[j]  activation j's miner (the alias sample over compute shares,
- *                               distributions.ml:143-196 via simulator.ml:465-472) and the
+ *                               distributions.ml:45-98 via simulator.ml:465-472) and the
  *                               exponential delay drawn when clock j is scheduled
  *                               (simulator.ml:170-173; j = 0 is the first clock)
  *   pow_hash[s]                 30-bit Random.bits of vertex serial s (simulator.ml:123);

@@ -137,7 +137,7 @@ Network Network::selfish_mining(double alpha, double activation_delay, double ga
 
 OcamlSimRng::OcamlSimRng(OcamlRandom* r_, const Network& net) : r(r_) {
   ev = net.activation_delay;
-  // distributions.ml:143-186 (Vose alias table)
+  // distributions.ml:45-88 (Vose alias table)
   int n = (int)net.nodes.size();
   double sum = 0.0;
   for (auto& x : net.nodes) {
@@ -715,7 +715,7 @@ Action DummyNode::handler(Kind, Block*) {
 
 // ---------------------------------------------------------------- SSZ attack space
 
-// nakamoto_ssz.ml:374-440
+// nakamoto_ssz.ml:274-340
 int nak_policy(int policy, const NakObs& o, const TablePolicy* table) {
   const int h = o.public_blocks, a = o.private_blocks;
   switch (policy) {
@@ -749,7 +749,7 @@ int nak_policy(int policy, const NakObs& o, const TablePolicy* table) {
   throw std::invalid_argument("unknown policy");
 }
 
-// ssz_tools.ml:480-491 (unit) and 462-469 (raw); field order nakamoto_ssz.ml:124-130
+// ssz_tools.ml:29-40 (unit) and 11-18 (raw); field order nakamoto_ssz.ml:24-30
 void nak_obs_to_floats(const NakObs& o, bool unit, double out[4]) {
   if (unit) {
     out[0] = 2. / M_PI * std::atan((double)o.public_blocks / 1.0);
@@ -766,7 +766,7 @@ void nak_obs_to_floats(const NakObs& o, bool unit, double out[4]) {
 
 static long ocaml_round_to_int(double x) { return (long)std::round(x); }
 
-// ssz_tools.ml:471-510
+// ssz_tools.ml:11-59
 NakObs nak_obs_of_floats(const double in[4], bool unit) {
   NakObs o;
   if (unit) {
@@ -790,7 +790,7 @@ Draft NakSszAgent::puzzle_payload() const {
   return d;
 }
 
-// nakamoto_ssz.ml:291-318
+// nakamoto_ssz.ml:191-218
 void NakSszAgent::prepare(Kind k, Block* x) {
   Block* p = pub;
   for (auto* m : pending)
@@ -813,13 +813,13 @@ void NakSszAgent::prepare(Kind k, Block* x) {
   if (!o_common) throw std::runtime_error("Option.get: no common ancestor");
 }
 
-// nakamoto_ssz.ml:320-330
+// nakamoto_ssz.ml:220-230
 NakObs NakSszAgent::observe() const {
   int ca = o_common->value.height, pr = o_priv->value.height, pu = o_pub->value.height;
   return NakObs{pu - ca, pr - ca, pr - pu, o_event};
 }
 
-// nakamoto_ssz.ml:332-359
+// nakamoto_ssz.ml:232-260
 Action NakSszAgent::apply(int action) {
   auto match_ = [&](int offset) {
     int h = o_pub->value.height + offset;

@@ -4,8 +4,8 @@
 // the OCaml discrete-event simulator of pkel/cpr function by function:
 //   OrderedQueue (skew heap)        simulator/lib/orderedQueue.ml:17-47
 //   Dag (vertices, children order)  simulator/lib/dag.ml:1-45
-//   Distributions (alias, exp, uni) simulator/lib/distributions.ml:110-196
-//   Network topologies              simulator/lib/network.ml:318-387
+//   Distributions (alias, exp, uni) simulator/lib/distributions.ml:12-98
+//   Network topologies              simulator/lib/network.ml:36-105
 //   Simulator (events, visibility)  simulator/lib/simulator.ml:122-543
 //   Dagtools.common_ancestor        simulator/lib/dagtools.ml:73-121
 //   Nakamoto referee / honest node  simulator/protocols/nakamoto.ml:19-96
@@ -127,9 +127,9 @@ struct Network {
   std::vector<NetNode> nodes;
   bool flooding = false;
   double activation_delay = 1.0;
-  // network.ml:332-341
+  // network.ml:50-59
   static Network two_agents(double activation_delay, double alpha);
-  // network.ml:343-387 (raises on defenders < 2 or gamma > (d-1)/d)
+  // network.ml:61-105 (raises on defenders < 2 or gamma > (d-1)/d)
   static Network selfish_mining(double alpha, double activation_delay, double gamma,
                                 double propagation_delay, int defenders);
 };
@@ -142,7 +142,7 @@ struct SimRng {
   virtual double link_delay(const Link& l, const Block* msg) = 0;
 };
 
-// OCaml Random: alias sampling exactly as distributions.ml:143-196
+// OCaml Random: alias sampling exactly as distributions.ml:45-98
 struct OcamlSimRng : SimRng {
   OcamlRandom* r;
   std::vector<double> p;
@@ -331,7 +331,7 @@ struct NakSszAgent {
   Action apply(int action);
 };
 
-// attacker as a simulator node (nakamoto_ssz.ml:362-372), used by Simulator.loop tasks
+// attacker as a simulator node (nakamoto_ssz.ml:262-272), used by Simulator.loop tasks
 struct NakSszAttackerNode : NodeImpl {
   NakSszAgent agent;
   int policy;

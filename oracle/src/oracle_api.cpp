@@ -70,7 +70,7 @@ void oracle_nak_obs_of_floats(const double in[4], int unit, int32_t out[4]) {
 }
 
 // ---------------- Simulator.loop task on the two-agents network with an SSZ attacker
-// (experiments/simulate/models.ml:29-46, withholding.ml:90-108, csv_runner.ml:244-265)
+// (experiments/simulate/models.ml:29-46, withholding.ml:6-27, csv_runner.ml:56-98)
 // rng_mode 0: OCaml Random state `rng` (carried over between calls like a Parany worker)
 // rng_mode 1: keyed stream (seed, episode)
 // Simulator.loop task on experiments/simulate/models.ml:3-28 honest_clique: n honest nodes,

@@ -144,7 +144,7 @@ POLICIES = {"honest": 0, "simple": 1, "eyal-sirer-2014": 2, "sapirshtein-2016-sm
 
 
 def two_agents_task(alpha, policy, activations, rng=None, seed=0, episode=0):
-    """Simulator.loop task (csv_runner.ml:244-265) on the two-agents network."""
+    """Simulator.loop task (csv_runner.ml:56-98) on the two-agents network."""
     acts = np.zeros(2, dtype=np.int64)
     rew = np.zeros(2, dtype=np.float64)
     ht, hp = ctypes.c_double(), ctypes.c_double()

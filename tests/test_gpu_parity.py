@@ -201,8 +201,8 @@ def test_policy_actions_decode(ctx):
 def test_invalid_configs_rejected(ctx):
     bad = [
         dict(alpha=1.5, gamma=0.5),  # engine.ml:42
-        dict(alpha=0.3, gamma=0.9, defenders=2),  # network.ml:351-354
-        dict(alpha=0.3, gamma=0.5, defenders=1),  # network.ml:345-346
+        dict(alpha=0.3, gamma=0.9, defenders=2),  # network.ml:69-72
+        dict(alpha=0.3, gamma=0.5, defenders=1),  # network.ml:63-64
         dict(alpha=float("nan"), gamma=0.5),
     ]
     for kw in bad:

@@ -34,7 +34,7 @@ def test_version_and_registry():
     assert lib.cpr_version().decode().startswith("cpr-hip")
     from cpr_amd import device
 
-    # Collection.add prepends (collection.ml:13): reverse of nakamoto_ssz.ml:442-450
+    # Collection.add prepends (collection.ml:13): reverse of nakamoto_ssz.ml:342-350
     assert [n for n, _ in device.policy_registry()] == [
         "sapirshtein-2016-sm1", "eyal-sirer-2014", "simple", "honest"]
     # bk_ssz.ml:404-415, same reversal
@@ -67,3 +67,31 @@ def test_no_device_raises_loudly(monkeypatch):
 
     with pytest.raises(Exception):
         device.Context(0)
+
+
+def _header_struct_fields(name):
+    text = HEADER.read_text()
+    body = re.search(r"typedef struct " + name + r" \{(.*?)\} " + name + ";", text, re.S).group(1)
+    body = re.sub(r"/\*.*?\*/", "", body, flags=re.S)
+    fields = []
+    for decl in body.split(";"):
+        decl = decl.strip()
+        if not decl:
+            continue
+        for part in re.sub(r"\[.*?\]", "", decl).split(","):
+            fields.append(re.findall(r"[A-Za-z_][A-Za-z_0-9]*", part)[-1])
+    return fields
+
+
+def test_ocaml_bindings_follow_the_header():
+    # integration/ocaml/cpr_hip.ml (not compiled here: no OCaml toolchain) must name every
+    # struct field in header order and bind every exported function
+    ml = (ROOT / "integration" / "ocaml" / "cpr_hip.ml").read_text()
+    for struct, var in [("cpr_config", "config"), ("cpr_episode_record", "record"),
+                        ("cpr_summary", "summary"), ("cpr_step_info", "step_info"),
+                        ("cpr_trace", "trace")]:
+        got = re.findall(r"field " + var + r' "([a-z_0-9]+)"', ml)
+        assert got == _header_struct_fields(struct), struct
+    bound = set(re.findall(r'foreign\s+"(cpr_[a-z_0-9]+)"', ml))
+    assert bound == set(_declared())
+    assert f"let abi_version = {L.ABI_VERSION}" in ml

@@ -4,7 +4,7 @@
   10,000 activations, OCaml Random carried over between tasks) — rewards per node,
   activations per node, head time (12 significant digits as written by
   string_of_float) and head progress must match exactly.
-* ssz_tools.ml:533-679 observation-encoding expect tests (unit and raw).
+* ssz_tools.ml:82-228 observation-encoding expect tests (unit and raw).
 * Philox4x32-10 known-answer vectors (Random123 kat_vectors) for the keyed stream.
 """
 
@@ -52,7 +52,7 @@ def test_ocaml_random_int_and_float_ranges():
     assert 0.45 < np.mean(fs) < 0.55
 
 
-# ssz_tools.ml:552-603 (unit) and :626-677 (raw), scale 1 as used by nakamoto_ssz.ml:135-138
+# ssz_tools.ml:101-152 (unit) and :175-226 (raw), scale 1 as used by nakamoto_ssz.ml:35-38
 @pytest.mark.parametrize(
     "fields,unit,expect",
     [
@@ -128,7 +128,7 @@ def test_keyed_stream_is_order_free():
     assert a.tolist() != b.tolist()
 
 
-# nakamoto_ssz.ml:374-440 spot checks (policy table of the reference)
+# nakamoto_ssz.ml:274-340 spot checks (policy table of the reference)
 @pytest.mark.parametrize(
     "policy,h,a,act",
     [
@@ -182,6 +182,6 @@ def test_gym_episode_accounting():
 
 
 def test_gym_gamma_one_rejected():
-    # network.ml:351-354 rejects gamma > (d-1)/d
+    # network.ml:69-72 rejects gamma > (d-1)/d
     with pytest.raises(ValueError):
         O.GymEnv(_cfg(alpha=0.3, gamma=1.0, defenders=2))

@@ -231,7 +231,7 @@ def test_tailstorm_protocol(capsys):
 
 
 def test_cpr_tailstorm_v0(capsys):
-    # gym/ocaml/test/test_envs.py:154-170
+    # gym/ocaml/test/test_envs.py:154-169
     env = envs.make("cpr_gym:cpr-tailstorm-v0")
     env.render()
     assert capsys.readouterr().out.splitlines()[0] == (
