@@ -31,6 +31,7 @@ SELECT_ALTRUISTIC = 0
 SELECT_HEURISTIC = 1
 SELECT_OPTIMAL = 2
 TS_POLICY_HONEST = 0
+TS_POLICY_TABLE = 7  # include/cpr_hip.h, the B_k table layout
 TS_POLICY_GET_AHEAD = 1
 TS_POLICY_MINOR_DELAY = 2
 TS_POLICY_AVOID_LOSS = 3
@@ -46,6 +47,7 @@ BK_POLICY_MINOR_DELAY = 2
 BK_POLICY_AVOID_LOSS = 3
 BK_POLICY_TABLE = 4
 ETH_POLICY_HONEST = 0
+ETH_POLICY_TABLE = 5  # include/cpr_hip.h: [(pub_h, priv_h) clamped to D][event]
 ETH_POLICY_SELFISH_RELEASE = 1
 ETH_POLICY_SELFISH_DISCARD = 2
 ETH_POLICY_FN19 = 3

@@ -106,9 +106,10 @@ struct cpr_batch {
   std::vector<uint8_t> table_host;
   DevBuf table_dev, tabs_dev;  // policy table; unit-observation tables
   DevBuf summary, records;
+  DevBuf pol_obs, pol_act;  // cpr_policy_actions staging, reused across calls
   DevBuf tr_off, tr_miner, tr_delay, tr_pow, tr_key, tr_ldelay;  // cpr_replay trace copy
   // lockstep lanes
-  DevBuf lanes, lring, lspill, ltlog, lreplay, l_obs, l_act, l_rew, l_done, l_mask, l_eps, l_info;
+  DevBuf lanes, lring, lspill, lreplay, l_obs, l_act, l_rew, l_done, l_mask, l_eps, l_info;
   bool reset_done = false;
   int32_t tab_n = 4096;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
@@ -179,12 +180,6 @@ static uint64_t alpha_threshold(double alpha) {
   if (t <= 0.0) return 0;
   if (t >= 4294967296.0) return 4294967296ull;
   return (uint64_t)t;
-}
-
-static int32_t pow2_at_least(int64_t x, int32_t cap) {
-  int32_t p = 64;
-  while (p < x && p < cap) p <<= 1;
-  return p;
 }
 
 // engine.ml:37-51 and network.ml:61-76 (messages kept verbatim)
@@ -315,7 +310,6 @@ static int validate(const cpr_config* c, NakParams* P, eth::EthParams* EP, bk::B
     span = c->activations + 2;
   }
   P->cap = (int32_t)(((std::min<int64_t>(span, 1 << 20) + 63) / 64) * 64);
-  P->tlog_len = pow2_at_least(span, 2048);
   return CPR_OK;
 }
 
@@ -330,11 +324,19 @@ static int validate_eth(const cpr_config* c, eth::EthParams* P) {
   if (c->activation_delay <= 0.) return fail(CPR_E_INVALID_ARG, "activation_delay <= 0");
   if (c->mode != CPR_MODE_GYM && c->mode != CPR_MODE_LOOP)
     return fail(CPR_E_INVALID_ARG, "unknown mode");
-  if (c->policy < CPR_ETH_POLICY_HONEST || c->policy > CPR_ETH_POLICY_FN19PKEL)
+  if (c->policy < CPR_ETH_POLICY_HONEST || c->policy > CPR_ETH_POLICY_TABLE)
     return fail(CPR_E_INVALID_ARG, "unknown policy");
   if (c->reward_scheme != CPR_REWARD_CONSTANT && c->reward_scheme != CPR_REWARD_DISCOUNT)
     return fail(CPR_E_INVALID_ARG, "unknown incentive scheme");
+  if (c->policy == CPR_ETH_POLICY_TABLE) {
+    const int64_t D = c->policy_table_dim;
+    if (!c->policy_table || D <= 0 || D > 64)
+      return fail(CPR_E_INVALID_ARG, "policy table missing or dim out of range (1..64)");
+    for (int64_t i = 0; i < D * D * 2; i++)
+      if (c->policy_table[i] > 23) return fail(CPR_E_INVALID_ARG, "policy table action out of range");
+  }
   memset(P, 0, sizeof(*P));
+  P->table_dim = c->policy == CPR_ETH_POLICY_TABLE ? c->policy_table_dim : 0;
   P->ev = c->activation_delay;
   P->t_att = alpha_threshold(c->alpha);
   P->policy = c->policy;
@@ -536,9 +538,18 @@ static int validate_ts(const cpr_config* c, ts::TsParams* P) {
     return fail(CPR_E_INVALID_ARG, "'" + std::to_string(c->subblock_selection) +
                                        "' is not a valid parameter choice, try 'altruistic', "
                                        "'heuristic' or 'optimal'");
-  if (c->policy < CPR_TS_POLICY_HONEST || c->policy > CPR_TS_POLICY_LONG_DELAY)
+  if (c->policy < CPR_TS_POLICY_HONEST || c->policy > CPR_TS_POLICY_TABLE)
     return fail(CPR_E_INVALID_ARG, "unknown policy");
+  if (c->policy == CPR_TS_POLICY_TABLE) {
+    const int64_t D = c->policy_table_dim;
+    if (!c->policy_table || D <= 0 || D > 64)
+      return fail(CPR_E_INVALID_ARG, "policy table missing or dim out of range (1..64)");
+    const int64_t sz = D * D * (c->k + 1) * (c->k + 1) * 3;
+    for (int64_t i = 0; i < sz; i++)
+      if (c->policy_table[i] > 7) return fail(CPR_E_INVALID_ARG, "policy table action out of range");
+  }
   memset(P, 0, sizeof(*P));
+  P->table_dim = c->policy == CPR_TS_POLICY_TABLE ? c->policy_table_dim : 0;
   P->t_att = B.t_att;
   P->d = B.d;
   P->n = B.n;
@@ -605,9 +616,13 @@ int cpr_batch_create(cpr_ctx* ctx, const cpr_config* cfg, cpr_batch** out) {
   if (cfg->protocol == CPR_PROTO_BK && cfg->policy == CPR_BK_POLICY_TABLE) {
     const size_t D = (size_t)cfg->policy_table_dim, K1 = (size_t)cfg->k + 1;
     b->table_host.assign(cfg->policy_table, cfg->policy_table + D * D * K1 * K1 * 3);
-  } else if (cfg->protocol == CPR_PROTO_NAKAMOTO && cfg->policy == CPR_POLICY_TABLE) {
+  } else if ((cfg->protocol == CPR_PROTO_NAKAMOTO && cfg->policy == CPR_POLICY_TABLE) ||
+             (cfg->protocol == CPR_PROTO_ETHEREUM && cfg->policy == CPR_ETH_POLICY_TABLE)) {
     const size_t nb = (size_t)cfg->policy_table_dim * cfg->policy_table_dim * 2;
     b->table_host.assign(cfg->policy_table, cfg->policy_table + nb);
+  } else if (cfg->protocol == CPR_PROTO_TAILSTORM && cfg->policy == CPR_TS_POLICY_TABLE) {
+    const size_t D = (size_t)cfg->policy_table_dim, K1 = (size_t)cfg->k + 1;
+    b->table_host.assign(cfg->policy_table, cfg->policy_table + D * D * K1 * K1 * 3);
   }
   // unit-observation tables (ssz_tools.ml:36-39) evaluated with the host libm:
   // [2/pi atan(i) | 0.5 + atan(i - N)/pi (2N) | 2/pi atan(i/k)], i < N
@@ -634,7 +649,8 @@ int cpr_batch_create(cpr_ctx* ctx, const cpr_config* cfg, cpr_batch** out) {
   }
   b->P.table = (const uint8_t*)b->table_dev.p;
   b->BP.table = (const uint8_t*)b->table_dev.p;
-  if (b->nak_ev) b->EP.table = (const uint8_t*)b->table_dev.p;
+  b->EP.table = (const uint8_t*)b->table_dev.p;  // Nakamoto-mode or ethereum_ssz table
+  b->TP.table = (const uint8_t*)b->table_dev.p;
   if (cfg->protocol == CPR_PROTO_NAKAMOTO && !b->nak_ev) {
     // the same episode on the exact event engine: Ethereum lane, no uncles, nakamoto_ssz
     // policy (validated above); configurations it cannot hold keep the lane's flags
@@ -682,7 +698,7 @@ int cpr_batch_destroy(cpr_batch* b) {
   b->bk_lmem.release();
   b->bk_slots.release();
   for (DevBuf* d : {&b->table_dev, &b->tabs_dev, &b->summary,
-                    &b->records, &b->lanes, &b->lring, &b->lspill, &b->ltlog, &b->lreplay,
+                    &b->records, &b->lanes, &b->lring, &b->lspill, &b->lreplay,
                     &b->l_obs, &b->l_act, &b->l_rew, &b->l_done, &b->l_mask, &b->l_eps,
                     &b->l_info, &b->tr_off, &b->tr_miner, &b->tr_delay, &b->tr_pow,
                     &b->tr_key, &b->tr_ldelay})
@@ -793,13 +809,11 @@ static int run_async(cpr_batch* b, int64_t n, uint64_t first, const TraceSource*
     return run_async_eth(b, n, first, tr, sum_dev, rec_dev);
   if (b->is_ev) return run_async_bk(b, n, first, tr, sum_dev, rec_dev);
   const int64_t lanes = episode_lanes(b, n);
-  // spill [lane][cap] int32 | time log [slot][lane] f64 | tie-replay scratch [lane]
-  const size_t o_tlog = align256((size_t)lanes * b->P.cap * sizeof(int32_t));
-  const size_t o_replay = o_tlog + align256((size_t)lanes * b->P.tlog_len * sizeof(double));
+  // spill [lane][cap] f64 mining times | tie-replay scratch [lane]
+  const size_t o_replay = align256((size_t)lanes * b->P.cap * sizeof(double));
   void* pool = nullptr;
   HIP_TRY(ctx_pool(b->ctx, o_replay + (size_t)lanes * REPLAY_BYTES, &pool));
-  int32_t* spill = (int32_t*)pool;
-  double* tlog = (double*)((char*)pool + o_tlog);
+  double* spill = (double*)pool;
   uint8_t* replay = (uint8_t*)pool + o_replay;
   if (!b->ev0) {
     HIP_TRY(hipEventCreate(&b->ev0));
@@ -836,11 +850,11 @@ static int run_async(cpr_batch* b, int64_t n, uint64_t first, const TraceSource*
   HIP_TRY(hipEventRecord(b->ev0, b->ctx->stream));
   if (tr)
     HIP_TRY(launch_replay_episodes(b->P, *tr, n, b->cfg.mode, b->cfg.activations,
-                                   spill, tlog, replay, lanes, rec_dev, sum_dev, redo, redo_n,
+                                   spill, replay, lanes, rec_dev, sum_dev, redo, redo_n,
                                    launch_id, kRerunQueue, b->ctx->stream));
   else
     HIP_TRY(launch_run_episodes(b->P, b->cfg.seed, first, n, b->cfg.mode, b->cfg.activations,
-                                spill, tlog, replay,
+                                spill, replay,
                                 lanes, rec_dev, sum_dev, redo, redo_n, launch_id, kRerunQueue,
                                 b->ctx->stream));
   HIP_TRY(hipEventRecord(b->ev1, b->ctx->stream));
@@ -1044,9 +1058,8 @@ static int ensure_lockstep(cpr_batch* b) {
   if (n <= 0) return fail(CPR_E_STATE, "batch has no lockstep lanes (cfg.n_lanes = 0)");
   if (b->cfg.mode != CPR_MODE_GYM) return fail(CPR_E_STATE, "lockstep lanes need CPR_MODE_GYM");
   HIP_TRY(b->lanes.ensure((size_t)n * lock_lane_bytes()));
-  HIP_TRY(b->lring.ensure((size_t)n * RING * sizeof(int32_t)));
-  HIP_TRY(b->lspill.ensure((size_t)n * b->P.cap * sizeof(int32_t)));
-  HIP_TRY(b->ltlog.ensure((size_t)n * b->P.tlog_len * sizeof(double)));
+  HIP_TRY(b->lring.ensure((size_t)n * RING * sizeof(double)));
+  HIP_TRY(b->lspill.ensure((size_t)n * b->P.cap * sizeof(double)));
   HIP_TRY(b->lreplay.ensure((size_t)n * REPLAY_BYTES));
   HIP_TRY(b->l_obs.ensure((size_t)n * 4 * sizeof(double)));
   HIP_TRY(b->l_act.ensure((size_t)n * sizeof(int32_t)));
@@ -1061,9 +1074,8 @@ static int ensure_lockstep(cpr_batch* b) {
 static LockBuffers lock_buffers(cpr_batch* b) {
   LockBuffers B;
   B.lanes = b->lanes.p;
-  B.ring = (int32_t*)b->lring.p;
-  B.spill = (int32_t*)b->lspill.p;
-  B.tlog = (double*)b->ltlog.p;
+  B.ring = (double*)b->lring.p;
+  B.spill = (double*)b->lspill.p;
   B.replay = (uint8_t*)b->lreplay.p;
   return B;
 }
@@ -1207,16 +1219,20 @@ int cpr_policy_actions(cpr_batch* b, int32_t policy, const double* obs, int64_t 
                        int32_t* actions) {
   if (!b || !obs || !actions) return fail(CPR_E_INVALID_ARG, "NULL argument");
   if (b->cfg.protocol == CPR_PROTO_TAILSTORM) {
-    if (policy < 0 || policy > CPR_TS_POLICY_LONG_DELAY)
+    if (policy < 0 || policy > CPR_TS_POLICY_TABLE)
       return fail(CPR_E_INVALID_ARG, "unknown policy");
+    if (policy == CPR_TS_POLICY_TABLE && b->table_host.empty())
+      return fail(CPR_E_INVALID_ARG, "batch has no policy table");
     if (n <= 0) return CPR_OK;
     HIP_TRY(hipSetDevice(b->ctx->device));
     hipStream_t st = b->ctx->stream;
-    DevBuf o, a;
+    DevBuf& o = b->pol_obs;
+    DevBuf& a = b->pol_act;
     HIP_TRY(o.ensure((size_t)n * 80));
     HIP_TRY(a.ensure((size_t)n * 4));
     HIP_TRY(hipMemcpyAsync(o.p, obs, (size_t)n * 80, hipMemcpyHostToDevice, st));
     HIP_TRY(launch_ts_policy(policy, b->cfg.k, b->cfg.unit_observation, (const double*)o.p, n,
+                             (const uint8_t*)b->table_dev.p, b->cfg.policy_table_dim,
                              (int32_t*)a.p, st));
     HIP_TRY(hipMemcpyAsync(actions, a.p, (size_t)n * 4, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
@@ -1229,7 +1245,8 @@ int cpr_policy_actions(cpr_batch* b, int32_t policy, const double* obs, int64_t 
     if (n <= 0) return CPR_OK;
     HIP_TRY(hipSetDevice(b->ctx->device));
     hipStream_t st = b->ctx->stream;
-    DevBuf o, a;
+    DevBuf& o = b->pol_obs;
+    DevBuf& a = b->pol_act;
     HIP_TRY(o.ensure((size_t)n * 64));
     HIP_TRY(a.ensure((size_t)n * 4));
     HIP_TRY(hipMemcpyAsync(o.p, obs, (size_t)n * 64, hipMemcpyHostToDevice, st));
@@ -1241,16 +1258,20 @@ int cpr_policy_actions(cpr_batch* b, int32_t policy, const double* obs, int64_t 
     return CPR_OK;
   }
   if (b->is_eth) {
-    if (policy < 0 || policy > CPR_ETH_POLICY_FN19PKEL)
+    if (policy < 0 || policy > CPR_ETH_POLICY_TABLE)
       return fail(CPR_E_INVALID_ARG, "unknown policy");
+    if (policy == CPR_ETH_POLICY_TABLE && b->table_host.empty())
+      return fail(CPR_E_INVALID_ARG, "batch has no policy table");
     if (n <= 0) return CPR_OK;
     HIP_TRY(hipSetDevice(b->ctx->device));
     hipStream_t st = b->ctx->stream;
-    DevBuf o, a;
+    DevBuf& o = b->pol_obs;
+    DevBuf& a = b->pol_act;
     HIP_TRY(o.ensure((size_t)n * 80));
     HIP_TRY(a.ensure((size_t)n * 4));
     HIP_TRY(hipMemcpyAsync(o.p, obs, (size_t)n * 80, hipMemcpyHostToDevice, st));
     HIP_TRY(launch_eth_policy(policy, b->cfg.unit_observation, (const double*)o.p, n,
+                              (const uint8_t*)b->table_dev.p, b->cfg.policy_table_dim,
                               (int32_t*)a.p, st));
     HIP_TRY(hipMemcpyAsync(actions, a.p, (size_t)n * 4, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
@@ -1264,7 +1285,8 @@ int cpr_policy_actions(cpr_batch* b, int32_t policy, const double* obs, int64_t 
   if (n <= 0) return CPR_OK;
   HIP_TRY(hipSetDevice(b->ctx->device));
   hipStream_t st = b->ctx->stream;
-  DevBuf o, a;
+  DevBuf& o = b->pol_obs;
+  DevBuf& a = b->pol_act;
   HIP_TRY(o.ensure((size_t)n * 32));
   HIP_TRY(a.ensure((size_t)n * 4));
   HIP_TRY(hipMemcpyAsync(o.p, obs, (size_t)n * 32, hipMemcpyHostToDevice, st));
@@ -1273,8 +1295,6 @@ int cpr_policy_actions(cpr_batch* b, int32_t policy, const double* obs, int64_t 
                         st));
   HIP_TRY(hipMemcpyAsync(actions, a.p, (size_t)n * 4, hipMemcpyDeviceToHost, st));
   HIP_TRY(hipStreamSynchronize(st));
-  o.release();
-  a.release();
   return CPR_OK;
 }
 

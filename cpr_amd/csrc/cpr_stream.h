@@ -30,14 +30,23 @@ struct Words4 {
   uint32_t w0, w1, w2, w3;
 };
 
+// a ^ b ^ c in one VALU instruction on gfx950 (v_bitop3_b32, truth table 0x96)
+__host__ __device__ inline uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+#else
+  return a ^ b ^ c;
+#endif
+}
+
 __host__ __device__ inline Words4 philox4x32_10(uint32_t c0, uint32_t c1, uint32_t c2,
                                                 uint32_t c3, uint32_t k0, uint32_t k1) {
 #pragma unroll
   for (int r = 0; r < 10; ++r) {
     const uint64_t p0 = (uint64_t)0xD2511F53u * c0;
     const uint64_t p1 = (uint64_t)0xCD9E8D57u * c2;
-    const uint32_t n0 = (uint32_t)(p1 >> 32) ^ c1 ^ k0;
-    const uint32_t n2 = (uint32_t)(p0 >> 32) ^ c3 ^ k1;
+    const uint32_t n0 = xor3((uint32_t)(p1 >> 32), c1, k0);
+    const uint32_t n2 = xor3((uint32_t)(p0 >> 32), c3, k1);
     c1 = (uint32_t)p1;
     c3 = (uint32_t)p0;
     c0 = n0;
@@ -86,7 +95,7 @@ __host__ __device__ inline double cpr_log(double x) {
   k += (i >> 20);
   const double f = x - 1.0;
   double dk, R;
-  if ((0x000fffff & (2 + hx)) < 3) {
+  if ((0x000fffff & (2 + hx)) < 3) {  // |f| < 2^-20 (rare)
     if (f == 0.0) {
       if (k == 0) return 0.0;
       dk = (double)k;
@@ -107,13 +116,14 @@ __host__ __device__ inline double cpr_log(double x) {
   const double t2 = z * (Lg1 + w * (Lg3 + w * (Lg5 + w * Lg7)));
   i |= j;
   R = t2 + t1;
-  if (i > 0) {
-    const double hfsq = 0.5 * f * f;
-    if (k == 0) return f - (hfsq - s * (hfsq + R));
-    return dk * ln2_hi - ((hfsq - (s * (hfsq + R) + dk * ln2_lo)) - f);
-  }
-  if (k == 0) return f - s * (f - R);
-  return dk * ln2_hi - ((s * (f - R) - dk * ln2_lo) - f);
+  // fdlibm's four tails as one select: its k == 0 forms equal the general forms at dk = 0
+  // bit for bit (0 * c = +0, y + 0 = y, and fl(y - f) = -fl(f - y) under round to nearest),
+  // so lanes of a wave no longer split over four branches (tests/test_oracle_kat.py checks
+  // this against the oracle's line-by-line fdlibm)
+  const double hfsq = 0.5 * f * f;
+  const double lo = dk * ln2_lo;
+  const double tail = i > 0 ? hfsq - (s * (hfsq + R) + lo) : s * (f - R) - lo;
+  return dk * ln2_hi - (tail - f);
 }
 
 struct Stream {

@@ -184,12 +184,26 @@ __host__ __device__ inline int32_t eth_policy(int32_t policy, const EthObs& o) {
   }
 }
 
-// the lane's attack policy: ethereum_ssz (ethereum_ssz.ml:444-521), or in Nakamoto mode the
+// table-driven ethereum_ssz policy (include/cpr_hip.h CPR_ETH_POLICY_TABLE): action =
+// table[(min(public_height, D-1) * D + min(private_height, D-1)) * 2 + event], 0..23
+constexpr int32_t ETH_POLICY_TABLE = 5;
+__host__ __device__ inline int32_t eth_table_index(const EthObs& o, int32_t D) {
+  auto cl = [](int32_t x, int32_t hi) { return x < 0 ? 0 : (x > hi ? hi : x); };
+  return (cl(o.public_height, D - 1) * D + cl(o.private_height, D - 1)) * 2 + o.event;
+}
+__host__ __device__ inline int32_t eth_policy_t(int32_t policy, const EthObs& o,
+                                                const uint8_t* table, int32_t dim) {
+  if (policy == ETH_POLICY_TABLE) return (int32_t)table[eth_table_index(o, dim)];
+  return eth_policy(policy, o);
+}
+
+// the lane's attack policy: ethereum_ssz (ethereum_ssz.ml:444-521) or its table, or in
+// Nakamoto mode the
 // nakamoto_ssz policy / table (nakamoto_ssz.ml:274-340) mapped onto the same agent
 // (Adopt -> Adopt_discard; Override, Match, Wait unchanged; no uncles to choose). Used by
 // the gym step and by the attacker's loop-mode handler alike.
 __host__ __device__ inline int32_t lane_action(const EthParams& P, const EthObs& o) {
-  if (!P.nak) return eth_policy(P.policy, o);
+  if (!P.nak) return eth_policy_t(P.policy, o, P.table, P.table_dim);
   const int32_t a = nak_policy(P.policy, o.public_height, o.private_height, o.event, P.table,
                                P.table_dim);
   constexpr int32_t map[4] = {A_ADOPT_DISCARD, A_OVERRIDE, A_MATCH, A_WAIT};

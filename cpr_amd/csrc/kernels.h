@@ -33,28 +33,27 @@ struct StepBuffers {
 // persistent per-lane memory of the lockstep lanes (device pointers)
 struct LockBuffers {
   void* lanes;      // LockLane[n]
-  int32_t* ring;    // [RING][n]
-  int32_t* spill;   // [n][cap]
-  double* tlog;     // [tlog_len][n]
+  double* ring;     // [RING][n] mining times of the private chain's last RING blocks
+  double* spill;    // [n][cap]
   uint8_t* replay;  // [n][REPLAY_BYTES]
 };
 
 // per-lane bytes the fused kernel needs in HBM besides LDS
 inline int64_t episode_lane_bytes(const NakParams& P) {
-  return (int64_t)P.cap * 4 + (int64_t)P.tlog_len * 8 + REPLAY_BYTES;
+  return (int64_t)P.cap * 8 + REPLAY_BYTES;
 }
 
 // redo/redo_n (optional, device): flagged episodes are appended to that queue (entries
 // tagged with launch_id, at most redo_cap) instead of accumulated, for launch_nak_exact_rerun
 hipError_t launch_run_episodes(const NakParams& P, uint64_t seed, uint64_t first, int64_t n_eps,
-                               int32_t mode, int64_t activations, int32_t* spill, double* tlog,
+                               int32_t mode, int64_t activations, double* spill,
                                uint8_t* replay, int64_t lanes, cpr_episode_record* recs,
                                cpr_summary* sum, int64_t* redo, uint32_t* redo_n,
                                uint32_t launch_id, int64_t redo_cap, hipStream_t st);
 // the same fused kernel drawing from a device copy of a cpr_trace (cpr_replay)
 hipError_t launch_replay_episodes(const NakParams& P, const TraceSource& src, int64_t n_eps,
-                                  int32_t mode, int64_t activations, int32_t* spill,
-                                  double* tlog, uint8_t* replay, int64_t lanes,
+                                  int32_t mode, int64_t activations, double* spill,
+                                  uint8_t* replay, int64_t lanes,
                                   cpr_episode_record* recs, cpr_summary* sum, int64_t* redo,
                                   uint32_t* redo_n, uint32_t launch_id, int64_t redo_cap,
                                   hipStream_t st);
@@ -97,7 +96,8 @@ hipError_t launch_eth_rollout(const eth::EthParams& P, uint64_t seed, uint8_t* m
 hipError_t launch_eth_observe_fields(const eth::EthParams& P, uint8_t* mem, int64_t lane_bytes,
                                      const void* slots, int64_t n, int32_t* f, hipStream_t st);
 hipError_t launch_eth_policy(int32_t policy, int unit, const double* obs, int64_t n,
-                             int32_t* actions, hipStream_t st);
+                             const uint8_t* table, int32_t dim, int32_t* actions,
+                             hipStream_t st);
 size_t eth_slot_bytes();
 // Exact re-runs of flagged Nakamoto episodes. Episode kernels append
 // queue entries (launch << 40) | (episode index << 8) | lane status bits; one RerunLaunch
@@ -168,7 +168,8 @@ hipError_t launch_ts_rollout(const ts::TsParams& P, uint64_t seed, uint8_t* mem,
 hipError_t launch_ts_observe_fields(const ts::TsParams& P, uint8_t* mem, int64_t lane_bytes,
                                     const void* slots, int64_t n, int32_t* f, hipStream_t st);
 hipError_t launch_ts_policy(int32_t policy, int32_t k, int unit, const double* obs, int64_t n,
-                            int32_t* actions, hipStream_t st);
+                            const uint8_t* table, int32_t dim, int32_t* actions,
+                            hipStream_t st);
 size_t ts_slot_bytes();
 int ts_blocks_per_cu();
 int run_episodes_blocks_per_cu(int32_t mode);  // resident 256-lane workgroups per CU

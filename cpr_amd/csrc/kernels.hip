@@ -1,9 +1,9 @@
 // HIP kernels for gfx950 (MI355X): one lane = one independent episode / gym env.
 //
 // Work is integer/branch (VALU) bound; nothing is a contraction, so no MFMA. Per-lane
-// state lives in VGPRs; the last 16 private-chain blocks live in LDS (16 KB per
-// workgroup), deeper ones spill to HBM, and every activation time goes to a [k][lane] log
-// (one coalesced 512 B store per wave and activation, read back only for the head).
+// state lives in VGPRs; the mining times of the last 16 private-chain blocks live in LDS
+// (32 KB per workgroup), deeper ones spill to HBM; every other block the lane can name
+// carries its own mining time, so an activation stores nothing to HBM.
 // Episode outcomes are reduced wave-wide with shuffles, then per workgroup in LDS, then
 // one 64-bit atomic per field per workgroup, all in integer arithmetic so totals are
 // independent of scheduling and of how episodes are sharded over GPUs.
@@ -33,7 +33,7 @@ __device__ inline void acc_add(LdsAcc& a, const BRef& hd, int64_t steps, int64_t
 
 // One gym episode (engine.ml:164-249): reset = first activation up to the attacker's
 // interaction; step = apply, deliveries, next activation, observe; head at the end.
-template <class St>
+template <int POL, class St>
 __device__ inline BRef run_gym(NakLane& L, const NakParams& P, const St& S, const LaneMem& M,
                                int64_t* steps_out) {
   L.init();
@@ -41,7 +41,7 @@ __device__ inline BRef run_gym(NakLane& L, const NakParams& P, const St& S, cons
   const bool check_prog = P.max_progress < __builtin_inf();
   int64_t steps = 0;
   for (;;) {
-    const int32_t a = L.policy_action(P);
+    const int32_t a = L.policy_action<POL>(P);
     L.apply(a);
     L.resolve(P, S, M);
     L.activate(P, S, M);
@@ -56,13 +56,13 @@ __device__ inline BRef run_gym(NakLane& L, const NakParams& P, const St& S, cons
 
 // Simulator.loop ~activations with the SSZ attacker as node 0 (simulator.ml:519-533,
 // nakamoto_ssz.ml:262-272); all messages delivered before the head is taken.
-template <class St>
+template <int POL, class St>
 __device__ inline BRef run_loop(NakLane& L, const NakParams& P, const St& S, const LaneMem& M,
                                 int64_t activations) {
   L.init();
   for (int64_t i = 0; i < activations; ++i) {
     L.activate(P, S, M);
-    L.apply(L.policy_action(P));
+    L.apply(L.policy_action<POL>(P));
     L.resolve(P, S, M);
   }
   return L.head(P, M);
@@ -71,13 +71,14 @@ __device__ inline BRef run_loop(NakLane& L, const NakParams& P, const St& S, con
 // lane status bits whose episodes the closed form cannot vouch for
 constexpr uint32_t kInexact = ST_OVERLAP | ST_DEEP_FORK | ST_TIE_UNRESOLVED | ST_STALE_TIME;
 
-template <int MODE, class Src>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(MODE == 0 ? 5 : 4))) void k_run_episodes(
+// POL: nakamoto_ssz policy fixed at compile time (P_HONEST .. P_SM1), or -1 for P.policy
+template <int MODE, class Src, int POL>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) void k_run_episodes(
     NakParams P, Src src, int64_t n_eps, int64_t activations,
-    int32_t* spill, double* tlog, uint8_t* replay, cpr_episode_record* recs, cpr_summary* sum,
+    double* spill, uint8_t* replay, cpr_episode_record* recs, cpr_summary* sum,
     int64_t* redo, uint32_t* redo_n, uint32_t launch_id, int64_t redo_cap) {
   __shared__ int32_t hist[CPR_HIST_BINS];
-  __shared__ int32_t ring[RING * kBlock];
+  __shared__ double ring[RING * kBlock];
   __shared__ unsigned long long acc_w[13];
   LdsAcc acc{acc_w};
   acc.init();
@@ -90,17 +91,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(MODE == 
   M.ring_stride = kBlock;
   M.spill = spill + tid * P.cap;
   M.spill_stride = 1;
-  M.tlog = tlog + tid;
-  M.tlog_stride = nthreads;
-  M.tmask = P.tlog_len - 1;
   M.cap = P.cap;
   M.replay = ReplayMem::at(replay + tid * REPLAY_BYTES);
   NakLane L;
   for (int64_t e = tid; e < n_eps; e += nthreads) {
     const auto S = src.at(e);
     int64_t steps = 0;
-    const BRef hd = MODE == CPR_MODE_GYM ? run_gym(L, P, S, M, &steps)
-                                         : run_loop(L, P, S, M, activations);
+    const BRef hd = MODE == CPR_MODE_GYM ? run_gym<POL>(L, P, S, M, &steps)
+                                         : run_loop<POL>(L, P, S, M, activations);
     const double tm = L.time_of(M, hd);
     const uint32_t status = L.status | Src::missed(S);
     uint32_t st_out = status;
@@ -152,9 +150,6 @@ __device__ inline LaneMem lock_mem(const NakParams& P, const LockBuffers& B, int
   M.ring_stride = n;
   M.spill = B.spill + i * P.cap;
   M.spill_stride = 1;
-  M.tlog = B.tlog + i;
-  M.tlog_stride = n;
-  M.tmask = P.tlog_len - 1;
   M.cap = P.cap;
   M.replay = ReplayMem::at(B.replay + i * REPLAY_BYTES);
   return M;
@@ -280,34 +275,44 @@ __global__ void k_stream_fill(uint64_t seed, uint64_t ep, uint32_t idx0, uint32_
 // ---------------------------------------------------------------- launchers
 
 hipError_t launch_run_episodes(const NakParams& P, uint64_t seed, uint64_t first, int64_t n_eps,
-                               int32_t mode, int64_t activations, int32_t* spill, double* tlog,
+                               int32_t mode, int64_t activations, double* spill,
                                uint8_t* replay, int64_t lanes, cpr_episode_record* recs,
                                cpr_summary* sum, int64_t* redo, uint32_t* redo_n,
                                uint32_t launch_id, int64_t redo_cap, hipStream_t st) {
   const unsigned blocks = (unsigned)(lanes / kBlock);
   const SeedSource src{seed, first};
-  if (mode == CPR_MODE_GYM)
-    hipLaunchKernelGGL((k_run_episodes<CPR_MODE_GYM, SeedSource>), dim3(blocks), dim3(kBlock), 0,
-                       st, P, src, n_eps, activations, spill, tlog, replay, recs, sum, redo, redo_n, launch_id, redo_cap);
-  else
-    hipLaunchKernelGGL((k_run_episodes<CPR_MODE_LOOP, SeedSource>), dim3(blocks), dim3(kBlock), 0,
-                       st, P, src, n_eps, activations, spill, tlog, replay, recs, sum, redo, redo_n, launch_id, redo_cap);
+#define CPR_LAUNCH(MODE, POL)                                                                    \
+  hipLaunchKernelGGL((k_run_episodes<MODE, SeedSource, POL>), dim3(blocks), dim3(kBlock), 0, st, \
+                     P, src, n_eps, activations, spill, replay, recs, sum, redo, redo_n,         \
+                     launch_id, redo_cap)
+  if (mode == CPR_MODE_GYM) {
+    switch (P.policy) {  // the built-in policies get their own specialisation
+      case P_HONEST: CPR_LAUNCH(CPR_MODE_GYM, P_HONEST); break;
+      case P_SIMPLE: CPR_LAUNCH(CPR_MODE_GYM, P_SIMPLE); break;
+      case P_ES2014: CPR_LAUNCH(CPR_MODE_GYM, P_ES2014); break;
+      case P_SM1: CPR_LAUNCH(CPR_MODE_GYM, P_SM1); break;
+      default: CPR_LAUNCH(CPR_MODE_GYM, -1);
+    }
+  } else {
+    CPR_LAUNCH(CPR_MODE_LOOP, -1);
+  }
+#undef CPR_LAUNCH
   return hipGetLastError();
 }
 
 hipError_t launch_replay_episodes(const NakParams& P, const TraceSource& src, int64_t n_eps,
-                                  int32_t mode, int64_t activations, int32_t* spill,
-                                  double* tlog, uint8_t* replay, int64_t lanes,
+                                  int32_t mode, int64_t activations, double* spill,
+                                  uint8_t* replay, int64_t lanes,
                                   cpr_episode_record* recs, cpr_summary* sum, int64_t* redo,
                                   uint32_t* redo_n, uint32_t launch_id, int64_t redo_cap,
                                   hipStream_t st) {
   const unsigned blocks = (unsigned)(lanes / kBlock);
   if (mode == CPR_MODE_GYM)
-    hipLaunchKernelGGL((k_run_episodes<CPR_MODE_GYM, TraceSource>), dim3(blocks), dim3(kBlock), 0,
-                       st, P, src, n_eps, activations, spill, tlog, replay, recs, sum, redo, redo_n, launch_id, redo_cap);
+    hipLaunchKernelGGL((k_run_episodes<CPR_MODE_GYM, TraceSource, -1>), dim3(blocks), dim3(kBlock), 0,
+                       st, P, src, n_eps, activations, spill, replay, recs, sum, redo, redo_n, launch_id, redo_cap);
   else
-    hipLaunchKernelGGL((k_run_episodes<CPR_MODE_LOOP, TraceSource>), dim3(blocks), dim3(kBlock),
-                       0, st, P, src, n_eps, activations, spill, tlog, replay, recs, sum, redo, redo_n, launch_id, redo_cap);
+    hipLaunchKernelGGL((k_run_episodes<CPR_MODE_LOOP, TraceSource, -1>), dim3(blocks), dim3(kBlock),
+                       0, st, P, src, n_eps, activations, spill, replay, recs, sum, redo, redo_n, launch_id, redo_cap);
   return hipGetLastError();
 }
 
@@ -358,9 +363,9 @@ int run_episodes_blocks_per_cu(int32_t mode) {
   int blocks = 0;
   hipError_t e = mode == CPR_MODE_GYM
                      ? hipOccupancyMaxActiveBlocksPerMultiprocessor(
-                           &blocks, k_run_episodes<CPR_MODE_GYM, SeedSource>, kBlock, 0)
+                           &blocks, k_run_episodes<CPR_MODE_GYM, SeedSource, -1>, kBlock, 0)
                      : hipOccupancyMaxActiveBlocksPerMultiprocessor(
-                           &blocks, k_run_episodes<CPR_MODE_LOOP, SeedSource>, kBlock, 0);
+                           &blocks, k_run_episodes<CPR_MODE_LOOP, SeedSource, -1>, kBlock, 0);
   if (e != hipSuccess || blocks <= 0) blocks = 2;
   return blocks;
 }

@@ -385,7 +385,7 @@ __global__ void k_eth_observe_fields(eth::EthParams P, uint8_t* mem, int64_t lan
 
 // engine.ml:258-261: decode (ssz_tools.ml NormalizeObs.of_float) and apply the policy
 __global__ void k_eth_policy(int32_t policy, int unit, const double* obs, int64_t n,
-                             int32_t* actions) {
+                             const uint8_t* table, int32_t dim, int32_t* actions) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const double* x = obs + 10 * i;
@@ -412,7 +412,7 @@ __global__ void k_eth_policy(int32_t policy, int unit, const double* obs, int64_
   o.private_orphans_inclusive = v[7];
   o.private_orphans_exclusive = v[8];
   o.event = v[9];
-  actions[i] = eth::eth_policy(policy, o);
+  actions[i] = eth::eth_policy_t(policy, o, table, dim);
 }
 
 static unsigned eth_grid_of(int64_t n) { return (unsigned)((n + kBlock - 1) / kBlock); }
@@ -453,9 +453,10 @@ hipError_t launch_eth_observe_fields(const eth::EthParams& P, uint8_t* mem, int6
 }
 
 hipError_t launch_eth_policy(int32_t policy, int unit, const double* obs, int64_t n,
-                             int32_t* actions, hipStream_t st) {
+                             const uint8_t* table, int32_t dim, int32_t* actions,
+                             hipStream_t st) {
   hipLaunchKernelGGL(k_eth_policy, dim3(eth_grid_of(n)), dim3(kBlock), 0, st, policy, unit, obs,
-                     n, actions);
+                     n, table, dim, actions);
   return hipGetLastError();
 }
 

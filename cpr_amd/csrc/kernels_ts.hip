@@ -62,7 +62,7 @@ __global__ __launch_bounds__(kBlock) void k_ts_run_episodes(
       L.gym_reset(P, S, M);
       bool done = L.dead != 0;
       hd = 0;
-      while (!done) hd = L.gym_step(P, S, M, ts::ts_policy(P.policy, P.k, L.observe(P, M)), &done);
+      while (!done) hd = L.gym_step(P, S, M, ts::ts_policy_p(P, L.observe(P, M)), &done);
     } else {
       hd = L.loop(P, S, M);
     }
@@ -196,7 +196,7 @@ __global__ __launch_bounds__(kBlock) void k_ts_rollout(ts::TsParams P, uint64_t 
       const ts::TsObs o = SL.L.observe(P, M);
       const int32_t c0 = SL.L.c_act;
       bool done = false;
-      const int32_t hd = SL.L.gym_step(P, S, M, ts::ts_policy(P.policy, P.k, o), &done);
+      const int32_t hd = SL.L.gym_step(P, S, M, ts::ts_policy_p(P, o), &done);
       acts_all += SL.L.c_act - c0;
       ++steps_all;
       double ra, rd;
@@ -238,7 +238,7 @@ __global__ void k_ts_observe_fields(ts::TsParams P, uint8_t* mem, int64_t lane_b
 
 // engine.ml:258-261 on encoded observations (ssz_tools.ml:42-58 of_float)
 __global__ void k_ts_policy(int32_t policy, int32_t k, int unit, const double* obs, int64_t n,
-                            int32_t* actions) {
+                            const uint8_t* table, int32_t dim, int32_t* actions) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const double* x = obs + 10 * i;
@@ -256,7 +256,7 @@ __global__ void k_ts_policy(int32_t policy, int32_t k, int unit, const double* o
     }
   }
   const ts::TsObs o{v[0], v[1], v[2], v[3], v[4], v[5], v[6], v[7], v[8], v[9]};
-  actions[i] = ts::ts_policy(policy, k, o);
+  actions[i] = ts::ts_policy_t(policy, k, o, table, dim);
 }
 
 // ---------------------------------------------------------------- launchers
@@ -314,9 +314,10 @@ hipError_t launch_ts_observe_fields(const ts::TsParams& P, uint8_t* mem, int64_t
 }
 
 hipError_t launch_ts_policy(int32_t policy, int32_t k, int unit, const double* obs, int64_t n,
-                            int32_t* actions, hipStream_t st) {
+                            const uint8_t* table, int32_t dim, int32_t* actions,
+                            hipStream_t st) {
   hipLaunchKernelGGL(k_ts_policy, dim3(ts_grid(n)), dim3(kBlock), 0, st, policy, k, unit, obs, n,
-                     actions);
+                     table, dim, actions);
   return hipGetLastError();
 }
 

@@ -17,9 +17,9 @@
 //   BRef.fork       height of the block's common ancestor with the private chain
 //                   (Dagtools.common_ancestor, dagtools.ml:102-121)
 //
-// Per-lane memory (LaneMem): the private chain's mining activations in a 16-slot ring
-// (LDS in the fused kernel) with a global spill for deeper chains, and the time of every
-// activation in a coalesced [k][lane] log that is read only for the final head.
+// Per-lane memory (LaneMem): the private chain's mining times in a 16-slot ring (LDS in
+// the fused kernel) with a global spill for deeper chains. Every other block the lane can
+// name carries its mining time in its BRef, so the head's chain time needs no log.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -63,19 +63,22 @@ struct ReplayMem {
 };
 
 struct LaneMem {
-  int32_t* ring;      // ring[(m & (RING-1)) * ring_stride]: mining activation of chain block m
-  int32_t* spill;     // spill[m * spill_stride], m < cap: chain blocks evicted from the ring
-  double* tlog;       // tlog[(k & tmask) * tlog_stride]: time of activation k
-  int64_t ring_stride, spill_stride, tlog_stride;
-  int32_t tmask, cap;
+  double* ring;       // ring[(m & (RING-1)) * ring_stride]: mining time of chain block m
+  double* spill;      // spill[m * spill_stride], m < cap: chain blocks evicted from the ring
+  int64_t ring_stride, spill_stride;
+  int32_t cap;
   ReplayMem replay;
 };
+
+constexpr int32_t K_GENESIS = -1, K_PRIVATE = -2;
 
 struct BRef {
   int32_t h;     // height (nakamoto.ml:11-14)
   int32_t ra;    // attacker blocks on the chain up to here
-  int32_t k;     // activation that mined it (DAG serial - 1); -1 = genesis
+  int32_t k;     // activation that mined it (DAG serial - 1); K_GENESIS; K_PRIVATE for the
+                 // attacker's private-chain blocks (mined by node 0, named by chain index)
   int32_t fork;  // height of the common ancestor with the attacker's private chain
+  double tm;     // mining time = Simulator.timestamp for these networks (simulator.ml:14-21)
 };
 
 struct NakParams {
@@ -92,7 +95,6 @@ struct NakParams {
   int32_t table_dim;
   const uint8_t* table;
   int32_t cap;          // spill slots per lane
-  int32_t tlog_len;     // time-log slots per lane (power of two)
 };
 
 __host__ __device__ inline uint64_t all_mask(int32_t d) {
@@ -354,12 +356,12 @@ struct NakLane {
   double w_t, w_bound;
   int32_t w_rlo, w_rhi, w_hasb, w_kw;
 
-  __host__ __device__ inline int32_t chain_k(const LaneMem& M, int32_t m) const {
+  __host__ __device__ inline double chain_t(const LaneMem& M, int32_t m) const {
     // two loads in their own address spaces (ds_read, then a rare global load) rather than
     // a select of pointers, which would compile to a generic flat load
-    int32_t v = M.ring[(int64_t)(m & (RING - 1)) * M.ring_stride];
+    double v = M.ring[(m & (RING - 1)) * M.ring_stride];
     // volatile: stops the compiler from sinking both loads into one generic (flat) load
-    if (m <= n - RING) v = *(volatile const int32_t*)&M.spill[(int64_t)m * M.spill_stride];
+    if (m <= n - RING) v = *(volatile const double*)&M.spill[(int64_t)m * M.spill_stride];
     return v;
   }
 
@@ -368,14 +370,15 @@ struct NakLane {
     BRef r;
     r.h = p0.h + m;
     r.ra = p0.ra + m;
-    r.k = chain_k(M, m);
+    r.k = K_PRIVATE;
     r.fork = r.h;
+    r.tm = chain_t(M, m);
     return r;
   }
 
   __host__ __device__ inline void init() {
     BRef g;
-    g.h = 0; g.ra = 0; g.k = -1; g.fork = 0;
+    g.h = 0; g.ra = 0; g.k = K_GENESIS; g.fork = 0; g.tm = 0.0;
     p0 = pub = D = A = b = g;
     t = 0.0;
     k = 0; n = 0; rel = 0; n_ba = 0; pend = -1; wminer = 0; event = 0;
@@ -410,7 +413,6 @@ struct NakLane {
       if (tn <= window_last_arrival(P, S)) status |= ST_OVERLAP;
     }
     t = tn;
-    M.tlog[(int64_t)(k & M.tmask) * M.tlog_stride] = tn;
     const int32_t ka = k;
     ++k;
     wminer = miner;
@@ -422,9 +424,9 @@ struct NakLane {
         status |= ST_DEEP_FORK;
         m = M.cap - 1;
       }
-      int32_t* slot = M.ring + (int64_t)(m & (RING - 1)) * M.ring_stride;
+      double* slot = M.ring + (m & (RING - 1)) * M.ring_stride;
       if (m > RING) M.spill[(int64_t)(m - RING) * M.spill_stride] = *slot;  // evict
-      *slot = ka;
+      *slot = tn;
       n = m;
       event = 0;
     } else {
@@ -433,6 +435,7 @@ struct NakLane {
       b.ra = par.ra;
       b.k = ka;
       b.fork = par.fork;
+      b.tm = tn;
       if (b.h > pub.h) pub = b;
       event = 1;
     }
@@ -590,22 +593,22 @@ struct NakLane {
   }
 
   // Simulator.timestamp of a block = its mining time for these networks
-  __host__ __device__ inline double time_of(const LaneMem& M, const BRef& x) {
-    if (x.k < 0) return 0.0;
-    if (k - x.k > M.tmask + 1) status |= ST_STALE_TIME;  // slot already reused
-    return M.tlog[(int64_t)(x.k & M.tmask) * M.tlog_stride];
-  }
+  __host__ __device__ inline double time_of(const LaneMem&, const BRef& x) const { return x.tm; }
 
+  // POL >= 0: the policy fixed at compile time (the fused kernel's specialisations), so
+  // the policy switch and its table operands disappear from the activation loop
+  template <int POL = -1>
   __host__ __device__ inline int32_t policy_action(const NakParams& P) const {
     int32_t h, a, dd, ev;
     observe(&h, &a, &dd, &ev);
-    return nak_policy(P.policy, h, a, ev, P.table, P.table_dim);
+    return nak_policy(POL >= 0 ? POL : P.policy, h, a, ev, P.table, P.table_dim);
   }
 };
 
 // miner of activation index ka (for head_miner of the record)
 template <class St>
 __host__ __device__ inline int32_t miner_of(const NakParams& P, const St& S, int32_t ka) {
+  if (ka == K_PRIVATE) return 0;
   if (ka < 0) return -1;
   return S.miner((uint32_t)ka, P.t_att, P.d);
 }

@@ -83,6 +83,9 @@ struct TsParams {
   // honest clique (net 2, models.ml:3-28): keyed miner thresholds (n - 1), U(lo, hi) links
   double lo, hi;
   uint32_t thr[64];
+  // table-driven policy (policy == TS_POLICY_TABLE): device table, dimension D
+  const uint8_t* table;
+  int32_t table_dim;
 };
 
 constexpr int32_t NQS = 512;     // votes of one summary tree handled at once
@@ -191,6 +194,25 @@ __host__ __device__ inline int32_t ts_policy(int32_t policy, int32_t k, const Ts
       if (h < a - 10) return bk::A_OVERRIDE_PROCEED;
       return bk::A_WAIT_PROCEED;
   }
+}
+
+// table-driven tailstorm_ssz policy (include/cpr_hip.h CPR_TS_POLICY_TABLE), the B_k
+// layout: table[((((min(pub,D-1)*D + min(priv,D-1))*(k+1) + min(public_votes,k))*(k+1)
+// + min(private_votes_inclusive,k))*3 + event], Action8
+constexpr int32_t TS_POLICY_TABLE = 7;
+__host__ __device__ inline int32_t ts_table_index(const TsObs& o, int32_t D, int32_t k) {
+  auto cl = [](int32_t x, int32_t hi) { return x < 0 ? 0 : (x > hi ? hi : x); };
+  const int32_t K1 = k + 1;
+  return ((((cl(o.public_blocks, D - 1) * D + cl(o.private_blocks, D - 1)) * K1 +
+            cl(o.public_votes, k)) * K1 + cl(o.private_votes_inclusive, k)) * 3) + o.event;
+}
+__host__ __device__ inline int32_t ts_policy_t(int32_t policy, int32_t k, const TsObs& o,
+                                               const uint8_t* table, int32_t dim) {
+  if (policy == TS_POLICY_TABLE) return (int32_t)table[ts_table_index(o, dim, k)];
+  return ts_policy(policy, k, o);
+}
+__host__ __device__ inline int32_t ts_policy_p(const TsParams& P, const TsObs& o) {
+  return ts_policy_t(P.policy, P.k, o, P.table, P.table_dim);
 }
 
 // combinatorics.ml:5-17 in OCaml's 63-bit wrap-around arithmetic; *dz = Division_by_zero
@@ -1123,7 +1145,7 @@ struct TsLane {
       case EV_ON: {
         if (node == 0 && P.net != 2) {  // loop mode: the attacker's handler (tailstorm_ssz.ml:353-362)
           prepare(P, M, kind, s);
-          if (!dead) apply(P, M, ts_policy(P.policy, P.k, observe(P, M)));
+          if (!dead) apply(P, M, ts_policy_p(P, observe(P, M)));
           break;
         }
         honest(P, M, node, s);

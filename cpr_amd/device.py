@@ -118,13 +118,22 @@ def make_config(
     c.delay_lo = float(delay_lo)
     c.delay_hi = float(delay_hi)
     keep = None
-    if table is not None and protocol == L.PROTO_BK:
+    if table is not None and protocol in (L.PROTO_BK, L.PROTO_TAILSTORM):
         keep = np.ascontiguousarray(table, dtype=np.uint8).ravel()
         per = (k + 1) * (k + 1) * 3
         dim = int(round((keep.size // per) ** 0.5)) if table_dim is None else int(table_dim)
         if dim * dim * per != keep.size:
-            raise ValueError("B_k policy table must have dim*dim*(k+1)*(k+1)*3 entries")
-        c.policy = L.BK_POLICY_TABLE
+            raise ValueError("B_k / Tailstorm policy table must have dim*dim*(k+1)*(k+1)*3 "
+                             "entries")
+        c.policy = L.BK_POLICY_TABLE if protocol == L.PROTO_BK else L.TS_POLICY_TABLE
+        c.policy_table = keep.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8))
+        c.policy_table_dim = dim
+    elif table is not None and protocol == L.PROTO_ETHEREUM:
+        keep = np.ascontiguousarray(table, dtype=np.uint8).ravel()
+        dim = int(round((keep.size // 2) ** 0.5))
+        if dim * dim * 2 != keep.size:
+            raise ValueError("Ethereum policy table must have dim*dim*2 entries")
+        c.policy = L.ETH_POLICY_TABLE
         c.policy_table = keep.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8))
         c.policy_table_dim = dim
     elif table is not None:

@@ -85,7 +85,10 @@ enum cpr_tailstorm_policy {
   CPR_TS_POLICY_AVOID_LOSS = 3,   /* avoid_loss_alt, registered as "avoid-loss" */
   CPR_TS_POLICY_AVOID_LOSS_A = 4, /* avoid_loss */
   CPR_TS_POLICY_AVOID_LOSS_B = 5, /* avoid_loss_alt2 */
-  CPR_TS_POLICY_LONG_DELAY = 6
+  CPR_TS_POLICY_LONG_DELAY = 6,
+  CPR_TS_POLICY_TABLE = 7 /* Action8 = table[((((min(pub,D-1)*D + min(priv,D-1))*(k+1)
+                             + min(public_votes,k))*(k+1) + min(private_votes_inclusive,k))*3
+                             + event] with D = policy_table_dim (the B_k layout) */
 };
 
 /* policy ids of the bk_ssz attack space (bk_ssz.ml:346-415; "avoid-loss" is avoid_loss_alt) */
@@ -111,7 +114,9 @@ enum cpr_ethereum_policy {
   CPR_ETH_POLICY_SELFISH_RELEASE = 1,
   CPR_ETH_POLICY_SELFISH_DISCARD = 2,
   CPR_ETH_POLICY_FN19 = 3,
-  CPR_ETH_POLICY_FN19PKEL = 4
+  CPR_ETH_POLICY_FN19PKEL = 4,
+  CPR_ETH_POLICY_TABLE = 5 /* action (0..23) = table[(min(public_height,D-1)*D
+                              + min(private_height,D-1))*2 + event], D = policy_table_dim */
 };
 
 /* ethereum_ssz.ml:161-277: action = rank * 4 + own * 2 + foreign, rank in
@@ -187,7 +192,7 @@ typedef struct cpr_config {
   int32_t network;           /* enum cpr_network */
   int32_t mode;              /* enum cpr_mode */
   int32_t policy;            /* enum cpr_policy; for cpr_step lanes the caller acts */
-  const uint8_t* policy_table; /* host pointer, dim*dim*2 actions (CPR_POLICY_TABLE) */
+  const uint8_t* policy_table; /* host pointer: the *_POLICY_TABLE of the protocol */
   int32_t policy_table_dim;
   int32_t unit_observation;  /* ssz_tools.ml NormalizeObs ~unit */
   double alpha;              /* attacker compute, [0,1] */

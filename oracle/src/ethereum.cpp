@@ -248,7 +248,14 @@ Action EthSszAgent::apply(int index) {
 
 Action EthSszAttackerNode::handler(Kind k, Block* b) {
   agent.prepare(k, b);
-  return agent.apply(eth_policy(policy, agent.observe()));
+  return agent.apply(eth_policy(policy, agent.observe(), table));
+}
+
+int eth_policy(int policy, const EthObs& o, const EthTable* t) {
+  if (policy != ETH_POL_TABLE) return eth_policy(policy, o);
+  auto cl = [](int x, int hi) { return x < 0 ? 0 : (x > hi ? hi : x); };
+  const int D = t->dim;
+  return t->actions[(cl(o.public_height, D - 1) * D + cl(o.private_height, D - 1)) * 2 + o.event];
 }
 
 // ethereum_ssz.ml:444-521
@@ -452,7 +459,7 @@ double GymEthereum::step(int action, double obs[ETH_OBS_LEN], bool* done, StepIn
 
 void eth_two_agents_task(int rng_mode, OcamlRandom* r, uint64_t seed, uint64_t episode,
                          double alpha, int scheme, int policy, int activations,
-                         EthLoopResult* out) {
+                         EthLoopResult* out, const EthTable* table) {
   Network net = Network::two_agents(1.0, alpha);
   std::unique_ptr<SimRng> rng;
   if (rng_mode == 0)
@@ -466,6 +473,7 @@ void eth_two_agents_task(int rng_mode, OcamlRandom* r, uint64_t seed, uint64_t e
   std::vector<std::unique_ptr<NodeImpl>> nodes;
   auto* att = new EthSszAttackerNode();
   att->policy = policy;
+  att->table = table;
   nodes.emplace_back(att);
   nodes.emplace_back(new EthHonest());
   sim.init(std::move(nodes));

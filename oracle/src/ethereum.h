@@ -33,6 +33,14 @@ struct EthObs {
 constexpr int ETH_OBS_LEN = 10;
 
 int eth_policy(int policy, const EthObs& o);
+// table-driven policy (include/cpr_hip.h CPR_ETH_POLICY_TABLE): action =
+// table[(min(public_height, D-1) * D + min(private_height, D-1)) * 2 + event]
+constexpr int ETH_POL_TABLE = 5;
+struct EthTable {
+  int dim = 0;
+  std::vector<uint8_t> actions;
+};
+int eth_policy(int policy, const EthObs& o, const EthTable* table);
 void eth_obs_to_floats(const EthObs& o, bool unit, double out[ETH_OBS_LEN]);
 EthObs eth_obs_of_floats(const double in[ETH_OBS_LEN], bool unit);
 
@@ -79,6 +87,7 @@ struct EthSszAgent {
 struct EthSszAttackerNode : NodeImpl {
   EthSszAgent agent;
   int policy = 0;
+  const EthTable* table = nullptr;
   Draft puzzle_payload() override { return agent.puzzle_payload(); }
   Action handler(Kind k, Block* b) override;
   Block* preferred() override { return agent.priv; }
@@ -119,6 +128,6 @@ struct EthLoopResult {
 };
 void eth_two_agents_task(int rng_mode, OcamlRandom* r, uint64_t seed, uint64_t episode,
                          double alpha, int scheme, int policy, int activations,
-                         EthLoopResult* out);
+                         EthLoopResult* out, const EthTable* table = nullptr);
 
 }  // namespace oracle

@@ -21,6 +21,25 @@ static thread_local std::string g_err;
 
 static void set_err(const char* what) { g_err = what; }
 
+static EthTable eth_table_of(const cpr_config* c) {
+  EthTable t;
+  if (c->policy == ETH_POL_TABLE && c->policy_table) {
+    t.dim = c->policy_table_dim;
+    t.actions.assign(c->policy_table, c->policy_table + (size_t)t.dim * t.dim * 2);
+  }
+  return t;
+}
+static TsTable ts_table_of(const cpr_config* c) {
+  TsTable t;
+  if (c->policy == TS_POL_TABLE && c->policy_table) {
+    t.dim = c->policy_table_dim;
+    const size_t K1 = (size_t)c->k + 1;
+    t.actions.assign(c->policy_table, c->policy_table + (size_t)t.dim * t.dim * K1 * K1 * 3);
+  }
+  return t;
+}
+
+
 extern "C" {
 
 const char* oracle_last_error() { return g_err.c_str(); }
@@ -354,9 +373,14 @@ int oracle_eth_dag_mine(void* dp, int parent, const int32_t* uncles, int n_uncle
 }
 
 // ---------------- ethereum_ssz policies / observation encoding
-int oracle_eth_policy(int policy, const int32_t obs[10]) {
+int oracle_eth_policy(int policy, const int32_t obs[10], const uint8_t* table, int dim) {
   EthObs o{obs[0], obs[1], obs[2], obs[3], obs[4], obs[5], obs[6], obs[7], obs[8], obs[9]};
-  return eth_policy(policy, o);
+  EthTable t;
+  if (policy == ETH_POL_TABLE) {
+    t.dim = dim;
+    t.actions.assign(table, table + (size_t)dim * dim * 2);
+  }
+  return eth_policy(policy, o, &t);
 }
 void oracle_eth_obs_to_floats(const int32_t obs[10], int unit, double out[10]) {
   EthObs o{obs[0], obs[1], obs[2], obs[3], obs[4], obs[5], obs[6], obs[7], obs[8], obs[9]};
@@ -426,6 +450,9 @@ int oracle_eth_gym_step(void* g, int action, double obs[10], double* reward, int
 }
 uint32_t oracle_eth_gym_diag(void* g) { return ((GymEthereum*)g)->sim->diag; }
 
+// the table of a CPR_ETH_POLICY_TABLE loop task (set per call by run_loop_episode)
+static thread_local const EthTable* g_eth_table = nullptr;
+
 int oracle_eth_two_agents_task(int rng_mode, void* rng, uint64_t seed, uint64_t episode,
                                double alpha, int scheme, int policy, int activations,
                                int64_t acts_out[2], double rewards_out[2], double* head_time,
@@ -434,7 +461,7 @@ int oracle_eth_two_agents_task(int rng_mode, void* rng, uint64_t seed, uint64_t 
   try {
     EthLoopResult r;
     eth_two_agents_task(rng_mode, (OcamlRandom*)rng, seed, episode, alpha, scheme, policy,
-                        activations, &r);
+                        activations, &r, g_eth_table);
     for (int i = 0; i < 2; i++) {
       acts_out[i] = r.activations[i];
       rewards_out[i] = r.rewards[i];
@@ -453,13 +480,14 @@ int oracle_eth_two_agents_task(int rng_mode, void* rng, uint64_t seed, uint64_t 
 
 // ---------------- batch of full episodes (keyed stream), the CPU baseline workload
 static int run_eth_gym_episode(const cpr_config* c, uint64_t ep, cpr_episode_record* rec) {
+  const EthTable et = eth_table_of(c);
   GymEthereum g(params_of(c), c->reward_scheme, 1, nullptr, c->seed, ep);
   double obs[10];
   g.reset(obs);
   bool done = false;
   StepInfo info{};
   while (!done) {
-    int a = eth_policy(c->policy, g.observe_int());
+    int a = eth_policy(c->policy, g.observe_int(), &et);
     g.step(a, obs, &done, &info);
   }
   rec->reward_attacker = info.episode_reward_attacker;
@@ -524,6 +552,7 @@ static void flagged_record(cpr_episode_record* rec, uint32_t status) {
 }
 
 static int run_ts_gym_episode(const cpr_config* c, uint64_t ep, cpr_episode_record* rec) {
+  const TsTable tt = ts_table_of(c);
   GymTailstorm g(params_of(c), c->k, c->reward_scheme, c->subblock_selection, 1, nullptr,
                  c->seed, ep);
   double obs[TS_OBS_LEN];
@@ -532,7 +561,7 @@ static int run_ts_gym_episode(const cpr_config* c, uint64_t ep, cpr_episode_reco
   try {
     g.reset(obs);
     while (!done) {
-      int a = ts_policy(c->policy, g.observe_int(), c->k);
+      int a = ts_policy(c->policy, g.observe_int(), c->k, &tt);
       g.step(a, obs, &done, &info);
     }
   } catch (BudgetExceeded&) {
@@ -721,9 +750,10 @@ static int run_loop_episode(const cpr_config* c, uint64_t ep, cpr_episode_record
   if (c->protocol == CPR_PROTO_TAILSTORM) {
     TsLoopResult r;
     try {
+      const TsTable tt = ts_table_of(c);
       ts_loop_task(Network::two_agents(c->activation_delay, c->alpha), 1, nullptr, c->seed, ep,
                    c->k, c->reward_scheme, c->subblock_selection, c->policy,
-                   (int)c->activations, &r);
+                   (int)c->activations, &r, &tt);
     } catch (BudgetExceeded&) {
       flagged_record(rec, CPR_ST_CAPACITY);
       return 0;
@@ -764,10 +794,13 @@ static int run_loop_episode(const cpr_config* c, uint64_t ep, cpr_episode_record
   }
   if (c->protocol == CPR_PROTO_ETHEREUM) {
     int32_t hw = 0;
-    if (oracle_eth_two_agents_task(1, nullptr, c->seed, ep, c->alpha, c->reward_scheme,
-                                   c->policy, (int)c->activations, acts, rew, &ht, &hp, &hh,
-                                   &hw, &diag) != 0)
-      return -1;
+    const EthTable et = eth_table_of(c);
+    g_eth_table = &et;
+    const int rc = oracle_eth_two_agents_task(1, nullptr, c->seed, ep, c->alpha,
+                                              c->reward_scheme, c->policy, (int)c->activations,
+                                              acts, rew, &ht, &hp, &hh, &hw, &diag);
+    g_eth_table = nullptr;
+    if (rc != 0) return -1;
     rec->reward_attacker = rew[0];
     rec->reward_defender = rew[1];
     rec->progress = hp;
@@ -907,9 +940,15 @@ int oracle_bk_loop(int net_kind, int n_nodes, double alpha, double activation_de
 }
 
 // ---------------- Tailstorm (tailstorm.ml, tailstorm_ssz.ml)
-int oracle_ts_policy(int policy, const int32_t obs[10], int k) {
+int oracle_ts_policy(int policy, const int32_t obs[10], int k, const uint8_t* table, int dim) {
   TsObs o{obs[0], obs[1], obs[2], obs[3], obs[4], obs[5], obs[6], obs[7], obs[8], obs[9]};
-  return ts_policy(policy, o, k);
+  TsTable t;
+  if (policy == TS_POL_TABLE) {
+    t.dim = dim;
+    const size_t K1 = (size_t)k + 1;
+    t.actions.assign(table, table + (size_t)dim * dim * K1 * K1 * 3);
+  }
+  return ts_policy(policy, o, k, &t);
 }
 void oracle_ts_obs_to_floats(const int32_t obs[10], int unit, int k, double out[10]) {
   TsObs o{obs[0], obs[1], obs[2], obs[3], obs[4], obs[5], obs[6], obs[7], obs[8], obs[9]};

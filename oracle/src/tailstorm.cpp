@@ -662,7 +662,16 @@ Action TsSszAgent::apply(int action) {
 
 Action TsSszAttackerNode::handler(Kind kd, Block* b) {
   agent.prepare(kd, b);
-  return agent.apply(ts_policy(policy, agent.observe(), agent.k));
+  return agent.apply(ts_policy(policy, agent.observe(), agent.k, table));
+}
+
+int ts_policy(int policy, const TsObs& o, int k, const TsTable* t) {
+  if (policy != TS_POL_TABLE) return ts_policy(policy, o, k);
+  auto cl = [](int x, int hi) { return x < 0 ? 0 : (x > hi ? hi : x); };
+  const int D = t->dim, K1 = k + 1;
+  return t->actions[((((cl(o.public_blocks, D - 1) * D + cl(o.private_blocks, D - 1)) * K1 +
+                       cl(o.public_votes, k)) * K1 + cl(o.private_votes_inclusive, k)) * 3) +
+                    o.event];
 }
 
 // ---------------------------------------------------------------- gym engine
@@ -807,7 +816,7 @@ double GymTailstorm::step(int action, double obs[TS_OBS_LEN], bool* done, StepIn
 
 void ts_loop_task(const Network& net, int rng_mode, OcamlRandom* r, uint64_t seed,
                   uint64_t episode, int k, int scheme, int selection, int policy,
-                  int activations, TsLoopResult* out) {
+                  int activations, TsLoopResult* out, const TsTable* table) {
   std::unique_ptr<SimRng> rng = make_ts_rng(rng_mode, r, seed, episode, net);
   Sim sim(net, rng.get());
   setup_sim(sim, k, scheme);
@@ -819,6 +828,7 @@ void ts_loop_task(const Network& net, int rng_mode, OcamlRandom* r, uint64_t see
     if (i == 0 && policy >= 0) {
       att = new TsSszAttackerNode();
       att->policy = policy;
+      att->table = table;
       nodes.emplace_back(att);
     } else {
       auto* h = new TsHonest();

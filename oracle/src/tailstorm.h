@@ -39,6 +39,13 @@ struct TsObs {
 constexpr int TS_OBS_LEN = 10;
 
 int ts_policy(int policy, const TsObs& o, int k);
+// table-driven policy (include/cpr_hip.h CPR_TS_POLICY_TABLE, the B_k table layout)
+constexpr int TS_POL_TABLE = 7;
+struct TsTable {
+  int dim = 0;
+  std::vector<uint8_t> actions;
+};
+int ts_policy(int policy, const TsObs& o, int k, const TsTable* table);
 void ts_obs_to_floats(const TsObs& o, bool unit, int k, double out[TS_OBS_LEN]);
 TsObs ts_obs_of_floats(const double in[TS_OBS_LEN], bool unit, int k);
 
@@ -133,6 +140,7 @@ struct TsSszAgent {
 struct TsSszAttackerNode : NodeImpl {
   TsSszAgent agent;
   int policy = 0;
+  const TsTable* table = nullptr;
   Draft puzzle_payload() override { return agent.puzzle_payload(); }
   Action handler(Kind k, Block* b) override;
   Block* preferred() override { return agent.priv; }
@@ -172,6 +180,6 @@ struct TsLoopResult {
 };
 void ts_loop_task(const Network& net, int rng_mode, OcamlRandom* r, uint64_t seed,
                   uint64_t episode, int k, int scheme, int selection, int policy,
-                  int activations, TsLoopResult* out);
+                  int activations, TsLoopResult* out, const TsTable* table = nullptr);
 
 }  // namespace oracle

@@ -30,7 +30,8 @@ static uint32_t mix(uint64_t a, uint64_t b) {
 struct Cfg {
   double alpha, gamma;
   int defenders;
-  int policy;  // 0..4 ethereum_ssz policies, 5 = random actions, 6 = random biased to release
+  int policy;  // 0..4 ethereum_ssz policies, 5 = random actions, 6 = random biased to release,
+               // 9 = a random table (CPR_ETH_POLICY_TABLE, loop tasks)
   int scheme;
   int steps;
   int two_agents;  // 2: Nakamoto-mode loop task on the selfish-mining network
@@ -47,6 +48,21 @@ struct Counters {
   long episodes = 0, mismatches = 0, capacity = 0, steps = 0;
 };
 
+// a random ethereum_ssz table (dim 6): the oracle's EthTable and the lane read the same bytes
+static const oracle::EthTable& g_table() {
+  static oracle::EthTable t;
+  if (t.dim == 0) {
+    t.dim = 6;
+    uint64_t x = 0xE7AB1E00u;
+    t.actions.resize((size_t)t.dim * t.dim * 2);
+    for (auto& a : t.actions) {
+      x = x * 6364136223846793005ull + 1442695040888963407ull;
+      a = (uint8_t)((x >> 33) % 24);
+    }
+  }
+  return t;
+}
+
 static eth::EthParams params_of(const Cfg& cf) {
   eth::EthParams P{};
   P.t_att = oracle::alpha_threshold(cf.alpha);
@@ -55,7 +71,11 @@ static eth::EthParams params_of(const Cfg& cf) {
   P.net = cf.two_agents == 1 ? 1 : 0;
   P.mode = cf.two_agents ? 1 : 0;
   P.nak = cf.two_agents == 2 ? 1 : 0;
-  P.policy = cf.policy < 5 ? cf.policy : 0;
+  P.policy = cf.policy < 5 ? cf.policy : (cf.policy == 9 ? eth::ETH_POLICY_TABLE : 0);
+  if (cf.policy == 9) {
+    P.table = g_table().actions.data();
+    P.table_dim = g_table().dim;
+  }
   P.scheme = cf.scheme;
   P.cap_b = 1;
   while (P.cap_b < cf.steps + 2) P.cap_b <<= 1;
@@ -164,8 +184,9 @@ static bool run_gym(const Cfg& cf, uint64_t seed, uint64_t ep, Counters& C, std:
 
 static bool run_loop(const Cfg& cf, uint64_t seed, uint64_t ep, Counters& C, std::string& why) {
   oracle::EthLoopResult r;
-  oracle::eth_two_agents_task(1, nullptr, seed, ep, cf.alpha, cf.scheme, cf.policy, cf.steps,
-                              &r);
+  oracle::eth_two_agents_task(1, nullptr, seed, ep, cf.alpha, cf.scheme,
+                              cf.policy == 9 ? oracle::ETH_POL_TABLE : cf.policy, cf.steps, &r,
+                              &g_table());
   const eth::EthParams P = params_of(cf);
   std::vector<uint8_t> mem(eth::eth_lane_bytes(P.cap_b, P.cap_e, P.n));
   const eth::EthMem M = eth::eth_mem_at(mem.data(), P.cap_b, P.cap_e, P.n);
@@ -253,7 +274,7 @@ int main(int argc, char** argv) {
     }
   cfgs.push_back(Cfg{0.4, 0.75, 7, 6, 1, steps, 0});
   for (double a : alphas)
-    for (int pol : {0, 1, 2, 3, 4}) cfgs.push_back(Cfg{a, 0, 1, pol, 1, steps * 4, 1});
+    for (int pol : {0, 1, 2, 3, 4, 9}) cfgs.push_back(Cfg{a, 0, 1, pol, 1, steps * 4, 1});
   // withholding.ml:29-52 gamma-* tasks (defender message delay 1e-4, and a longer one that
   // makes in-flight overlaps common), nakamoto_ssz policies 0..3
   for (double a : {0.1, 0.25, 0.35, 0.45, 0.5})

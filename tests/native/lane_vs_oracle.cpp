@@ -31,20 +31,16 @@ struct Cfg {
   int two_agents;  // loop mode on the two-agents network
 };
 
-// host stand-in for the kernel's per-lane memory (ring, spill, time log, replay scratch)
+// host stand-in for the kernel's per-lane memory (ring, spill, replay scratch)
 struct HostMem {
-  std::vector<int32_t> ring, spill;
-  std::vector<double> tlog;
+  std::vector<double> ring, spill;
   std::vector<uint8_t> replay;
-  explicit HostMem(const NakParams& P)
-      : ring(RING), spill(P.cap), tlog(P.tlog_len), replay(REPLAY_BYTES) {}
+  explicit HostMem(const NakParams& P) : ring(RING), spill(P.cap), replay(REPLAY_BYTES) {}
   LaneMem lane() {
     LaneMem M;
     M.ring = ring.data();
     M.spill = spill.data();
-    M.tlog = tlog.data();
-    M.ring_stride = M.spill_stride = M.tlog_stride = 1;
-    M.tmask = (int32_t)tlog.size() - 1;
+    M.ring_stride = M.spill_stride = 1;
     M.cap = (int32_t)spill.size();
     M.replay = ReplayMem::at(replay.data());
     return M;
@@ -83,7 +79,6 @@ static bool run_gym(const Cfg& cf, uint64_t seed, uint64_t ep, Counters& C, std:
   P.max_time = __builtin_inf();
   P.policy = cf.policy < 4 ? cf.policy : 0;
   P.cap = cf.steps + 64;
-  P.tlog_len = 1 << 20;
   HostMem mem(P);
   const LaneMem M = mem.lane();
   Stream S{(uint32_t)seed, (uint32_t)(seed >> 32), (uint32_t)ep, (uint32_t)(ep >> 32)};
@@ -166,7 +161,6 @@ static bool run_loop(const Cfg& cf, uint64_t seed, uint64_t ep, Counters& C, std
   P.max_progress = __builtin_inf();
   P.max_time = __builtin_inf();
   P.cap = cf.steps + 64;
-  P.tlog_len = 1 << 20;
   HostMem mem(P);
   const LaneMem M = mem.lane();
   Stream S{(uint32_t)seed, (uint32_t)(seed >> 32), (uint32_t)ep, (uint32_t)(ep >> 32)};

@@ -30,7 +30,8 @@ static uint32_t mix(uint64_t a, uint64_t b) {
 struct Cfg {
   double alpha, gamma;
   int defenders;
-  int policy;  // 0..6 tailstorm_ssz policies, 7 = random actions, 8 = random release-heavy
+  int policy;  // 0..6 tailstorm_ssz policies, 7 = random actions, 8 = random release-heavy,
+               // 9 = a random table (CPR_TS_POLICY_TABLE, loop tasks)
   int scheme;  // 0 Constant, 1 Discount, 3 Punish, 4 Hybrid
   int steps;
   int two_agents;  // 0 gym, 1 two-agents loop, 2 honest-clique loop (defenders = nodes)
@@ -43,6 +44,22 @@ struct Counters {
 };
 
 static int g_sel = 1;
+
+// one random table per k (dim 5): the oracle's TsTable and the lane read the same bytes
+static const oracle::TsTable& g_table(int k) {
+  static std::vector<oracle::TsTable> tabs(65);
+  oracle::TsTable& t = tabs[k];
+  if (t.dim == 0) {
+    t.dim = 5;
+    uint64_t x = 0x7AB1E000u + (uint64_t)k;
+    t.actions.resize((size_t)t.dim * t.dim * (k + 1) * (k + 1) * 3);
+    for (auto& a : t.actions) {
+      x = x * 6364136223846793005ull + 1442695040888963407ull;
+      a = (uint8_t)((x >> 33) % 8);
+    }
+  }
+  return t;
+}
 
 static ts::TsParams params_of(const Cfg& cf) {
   ts::TsParams P{};
@@ -59,7 +76,11 @@ static ts::TsParams params_of(const Cfg& cf) {
     P.lo = 0.5;
     P.hi = 1.5;
   }
-  P.policy = cf.policy < 7 ? cf.policy : 0;
+  P.policy = cf.policy < 7 ? cf.policy : (cf.policy == 9 ? ts::TS_POLICY_TABLE : 0);
+  if (cf.policy == 9) {
+    P.table = g_table(cf.k).actions.data();
+    P.table_dim = g_table(cf.k).dim;
+  }
   P.scheme = cf.scheme;
   P.selection = g_sel;
   P.k = cf.k;
@@ -260,7 +281,8 @@ static bool run_loop(const Cfg& cf, uint64_t seed, uint64_t ep, Counters& C, std
       }
     }
     oracle::ts_loop_task(net, 1, nullptr, seed, ep, cf.k, cf.scheme, g_sel,
-                         cf.two_agents == 2 ? -1 : cf.policy, cf.steps, &r);
+                         cf.two_agents == 2 ? -1 : (cf.policy == 9 ? oracle::TS_POL_TABLE : cf.policy),
+                         cf.steps, &r, &g_table(cf.k));
   } catch (oracle::BudgetExceeded&) {
     budget = true;
   } catch (std::exception&) {
@@ -339,7 +361,7 @@ int main(int argc, char** argv) {
   cfgs.push_back(Cfg{0.4, 0.75, 7, 8, 1, steps, 0, k});
   cfgs.push_back(Cfg{0.33, 0.3, 4, 7, 1, steps, 0, k});
   for (double a : alphas)
-    for (int pol : {0, 1, 2, 3, 4, 5, 6}) cfgs.push_back(Cfg{a, 0, 1, pol, 1, steps * 2, 1, k});
+    for (int pol : {0, 1, 2, 3, 4, 5, 6, 9}) cfgs.push_back(Cfg{a, 0, 1, pol, 1, steps * 2, 1, k});
   // honest cliques: n nodes, compute 1..n, U(0.5, 1.5) links, all four reward schemes
   for (int n : {2, 3, 10})
     for (double ev : {0.5, 2.0, 30.0, 600.0})

@@ -89,7 +89,7 @@ def lib():
         L.oracle_eth_dag_new.argtypes = [ctypes.c_int, ctypes.c_int]
         L.oracle_eth_dag_free.argtypes = [vp]
         L.oracle_eth_dag_mine.argtypes = [vp, ctypes.c_int, vp, ctypes.c_int, P(ctypes.c_int32)]
-        L.oracle_eth_policy.argtypes = [ctypes.c_int, vp]
+        L.oracle_eth_policy.argtypes = [ctypes.c_int, vp, vp, ctypes.c_int]
         L.oracle_eth_obs_to_floats.argtypes = [vp, ctypes.c_int, vp]
         L.oracle_eth_obs_of_floats.argtypes = [vp, ctypes.c_int, vp]
         L.oracle_eth_gym_new.restype = vp
@@ -370,9 +370,14 @@ class EthDag:
         return out.value, bool(ok)
 
 
-def eth_policy(policy, fields):
+def eth_policy(policy, fields, table=None):
+    """ethereum_ssz policy by name or id; policy 5 (CPR_ETH_POLICY_TABLE) reads `table`
+    (dim x dim x 2 actions)."""
     o = np.ascontiguousarray(fields, dtype=np.int32)
-    return lib().oracle_eth_policy(ETH_POLICIES.get(policy, policy), o.ctypes.data)
+    t = None if table is None else np.ascontiguousarray(table, dtype=np.uint8).ravel()
+    dim = 0 if t is None else int(round((t.size // 2) ** 0.5))
+    return lib().oracle_eth_policy(ETH_POLICIES.get(policy, policy), o.ctypes.data,
+                                   None if t is None else t.ctypes.data, dim)
 
 
 def eth_obs_to_floats(fields, unit):
@@ -589,7 +594,7 @@ def ts_lib():
         vp = ctypes.c_void_p
         from cpr_amd import _lib as C
 
-        L.oracle_ts_policy.argtypes = [ctypes.c_int, vp, ctypes.c_int]
+        L.oracle_ts_policy.argtypes = [ctypes.c_int, vp, ctypes.c_int, vp, ctypes.c_int]
         L.oracle_ts_obs_to_floats.argtypes = [vp, ctypes.c_int, ctypes.c_int, vp]
         L.oracle_ts_obs_of_floats.argtypes = [vp, ctypes.c_int, ctypes.c_int, vp]
         L.oracle_n_choose_k.argtypes = [ctypes.c_int64, ctypes.c_int64]
@@ -611,9 +616,14 @@ def ts_lib():
     return L
 
 
-def ts_policy(policy, fields, k):
+def ts_policy(policy, fields, k, table=None):
+    """tailstorm_ssz policy by name or id; policy 7 (CPR_TS_POLICY_TABLE) reads `table`
+    (dim x dim x (k+1) x (k+1) x 3 actions)."""
     o = np.ascontiguousarray(fields, dtype=np.int32)
-    return ts_lib().oracle_ts_policy(TS_POLICIES.get(policy, policy), o.ctypes.data, k)
+    t = None if table is None else np.ascontiguousarray(table, dtype=np.uint8).ravel()
+    dim = 0 if t is None else int(round((t.size // (3 * (k + 1) ** 2)) ** 0.5))
+    return ts_lib().oracle_ts_policy(TS_POLICIES.get(policy, policy), o.ctypes.data, k,
+                                     None if t is None else t.ctypes.data, dim)
 
 
 def ts_obs_to_floats(fields, unit, k):

@@ -166,3 +166,47 @@ def test_eth_rollout_matches_sequential_oracle_episodes(ctx):
             assert np.array_equal(obs[t, i], o), (i, t)
     assert s.episodes == finished
     assert b.rollout(10).steps == n * 10
+
+
+# ---- table-driven ethereum_ssz policy (CPR_ETH_POLICY_TABLE)
+
+def _eth_table(dim=6, seed=3):
+    return np.random.default_rng(seed).integers(0, 24, size=dim * dim * 2).astype(np.uint8)
+
+
+@pytest.mark.parametrize("mode", ["gym", "loop"])
+def test_eth_table_policy_matches_oracle(ctx, mode):
+    table = _eth_table()
+    if mode == "gym":
+        cfg, keep = _cfg(alpha=0.35, gamma=0.5, table=table, reward_scheme=L.REWARD_CONSTANT,
+                         max_steps=400, seed=0x7AB1E)
+    else:
+        cfg, keep = _cfg(alpha=0.35, network=L.NET_TWO_AGENTS, mode=L.MODE_LOOP,
+                         activations=3000, table=table, reward_scheme=L.REWARD_DISCOUNT,
+                         seed=0x7AB1E)
+    assert cfg.policy == L.ETH_POLICY_TABLE
+    s, rec, ok = _compare(cfg, keep, 256)
+    assert s.episodes == 256
+
+
+def test_eth_table_policy_decoding_and_rollout(ctx):
+    table = _eth_table(dim=4, seed=9)
+    n, T, ms = 12, 120, 40
+    cfg, keep = _cfg(alpha=0.3, gamma=0.5, table=table, max_steps=ms, seed=21, n_lanes=n)
+    b = device.Batch(cfg, keep=keep)
+    obs = b.reset()
+    fields = b.observe_fields()
+    assert b.policy_actions(L.ETH_POLICY_TABLE, obs).tolist() == [
+        O.eth_policy(L.ETH_POLICY_TABLE, f, table=table) for f in fields]
+    b2 = device.Batch(cfg, keep=keep)
+    s, _, rew, done = b2.rollout(T, outputs=True)
+    for i in range(4):
+        e, ep = O.EthGymEnv(cfg, episode=i), i
+        e.reset()
+        for t in range(T):
+            _, r, d, _ = e.step(O.eth_policy(L.ETH_POLICY_TABLE, e.fields(), table=table))
+            assert rew[t, i] == r and done[t, i] == d, (i, t)
+            if d:
+                ep += n
+                e = O.EthGymEnv(cfg, episode=ep)
+                e.reset()

@@ -161,3 +161,47 @@ def test_ts_spec_registry_and_validation(ctx):
         with pytest.raises(L.CprError) as e:
             device.Batch(cfg, keep=keep)
         assert e.value.code == L.CPR_E_INVALID_ARG
+
+
+# ---- table-driven tailstorm_ssz policy (CPR_TS_POLICY_TABLE)
+
+def _ts_table(k, dim=5, seed=4):
+    return np.random.default_rng(seed).integers(0, 8, size=dim * dim * (k + 1) ** 2 * 3).astype(
+        np.uint8)
+
+
+@pytest.mark.parametrize("mode", ["gym", "loop"])
+def test_ts_table_policy_matches_oracle(ctx, mode):
+    k = 8
+    table = _ts_table(k)
+    if mode == "gym":
+        cfg, keep = _cfg(alpha=0.33, gamma=0.5, table=table, k=k, max_steps=400, seed=0x7AB1E)
+    else:
+        cfg, keep = _cfg(alpha=0.33, network=L.NET_TWO_AGENTS, mode=L.MODE_LOOP,
+                         activations=3000, table=table, k=k, seed=0x7AB1E)
+    assert cfg.policy == L.TS_POLICY_TABLE
+    _compare(cfg, keep, 128)
+
+
+def test_ts_table_policy_decoding_and_rollout(ctx):
+    k = 4
+    table = _ts_table(k, dim=4, seed=11)
+    n, T, ms = 12, 120, 40
+    cfg, keep = _cfg(alpha=0.3, gamma=0.5, table=table, k=k, max_steps=ms, seed=22, n_lanes=n)
+    b = device.Batch(cfg, keep=keep)
+    obs = b.reset()
+    fields = b.observe_fields()
+    assert b.policy_actions(L.TS_POLICY_TABLE, obs).tolist() == [
+        O.ts_policy(L.TS_POLICY_TABLE, f, k, table=table) for f in fields]
+    b2 = device.Batch(cfg, keep=keep)
+    s, _, rew, done = b2.rollout(T, outputs=True)
+    for i in range(4):
+        e, ep = O.TsGymEnv(cfg, episode=i), i
+        e.reset()
+        for t in range(T):
+            _, r, d, _ = e.step(O.ts_policy(L.TS_POLICY_TABLE, e.fields(), k, table=table))
+            assert rew[t, i] == r and done[t, i] == d, (i, t)
+            if d:
+                ep += n
+                e = O.TsGymEnv(cfg, episode=ep)
+                e.reset()

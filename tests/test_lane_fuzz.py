@@ -77,3 +77,17 @@ def test_tailstorm_lane_matches_oracle_fuzz():
         assert p.returncode == 0, p.stderr[-2000:]
         assert out["mismatches"] == 0, p.stderr[-2000:]
         assert out["episodes"] > 250 and out["capacity"] == 0
+
+
+def test_device_log_and_philox_match_oracle():
+    # tests/native/log_vs_oracle.cpp: the device's cpr_log (branch-free fdlibm tails) and
+    # Philox4x32-10 (gfx950 v_bitop3 xors) compiled for the host, bit for bit against the
+    # oracle's line-by-line fdlibm and keyed blocks: 2e7 uniform inputs plus 480k inputs
+    # near 1, near powers of two and subnormal
+    subprocess.run(["make", "-s", "-C", str(ROOT / "tests" / "native")], check=True)
+    exe = ROOT / "tests" / "native" / "build" / "log_vs_oracle"
+    p = subprocess.run([str(exe), "20000000"], capture_output=True, text=True, timeout=600)
+    out = json.loads(p.stdout.strip().splitlines()[-1])
+    assert p.returncode == 0, p.stderr[-2000:]
+    assert out["log_mismatches"] == 0 and out["philox_mismatches"] == 0
+    assert out["checked"] > 20_000_000
