@@ -64,6 +64,11 @@ POLICY_EYAL_SIRER_2014 = 2
 POLICY_SAPIRSHTEIN_2016_SM1 = 3
 POLICY_TABLE = 4
 
+PROTO_FC16 = 4  # gym/rust/src/fc16.rs abstract model (fused episodes)
+FC16_POLICY_HONEST = 0
+FC16_POLICY_SM1 = 1
+FC16_POLICY_TABLE = 2
+FC16_WAIT, FC16_ADOPT, FC16_OVERRIDE, FC16_MATCH = 0, 1, 2, 3
 ST_TIE = 1
 ST_OVERLAP = 2
 ST_DEEP_FORK = 4
@@ -105,6 +110,7 @@ class Config(ctypes.Structure):
         ("subblock_selection", ctypes.c_int32),
         ("delay_lo", ctypes.c_double),
         ("delay_hi", ctypes.c_double),
+        ("horizon", ctypes.c_double),
     ]
 
 

@@ -97,6 +97,7 @@ struct cpr_batch {
   DevBuf bk_lmem, bk_slots;  // lockstep lanes: n_lanes x bk_bytes, n_lanes slots
   int64_t bk_bytes = 0;
   ts::TsParams TP;       // CPR_PROTO_TAILSTORM (shares bk_lmem / bk_slots)
+  fc16::Fc16Params FP;   // CPR_PROTO_FC16
   bool is_ev = false;    // B_k or Tailstorm event-engine lanes
   // Nakamoto fused episodes: exact re-runs of flagged episodes on the event engine
   bool has_rerun = false;
@@ -215,6 +216,34 @@ static bool nak_on_event_engine(const cpr_config* c) {
   const double dd = (double)c->defenders;
   const double span = std::max(prop, (dd - 1.) / dd * prop / c->gamma);
   return !(span * (double)c->activations < 1e-3 * c->activation_delay);
+}
+
+// FC'16 abstract model (fc16.rs:141-158 FC16SSZwPT::new: Bernoulli(alpha), Bernoulli(gamma),
+// Bernoulli(1 / horizon) reject probabilities outside [0, 1])
+static int validate_fc16(const cpr_config* c, fc16::Fc16Params* P) {
+  if (std::isnan(c->alpha) || c->alpha < 0. || c->alpha > 1.)
+    return fail(CPR_E_INVALID_ARG, "alpha < 0 || alpha > 1");
+  if (std::isnan(c->gamma) || c->gamma < 0. || c->gamma > 1.)
+    return fail(CPR_E_INVALID_ARG, "gamma < 0 || gamma > 1");
+  if (!(c->horizon >= 1.)) return fail(CPR_E_INVALID_ARG, "horizon must be >= 1");
+  if (c->mode != CPR_MODE_GYM) return fail(CPR_E_UNSUPPORTED, "FC16 runs gym episodes");
+  if (c->policy < CPR_FC16_POLICY_HONEST || c->policy > CPR_FC16_POLICY_TABLE)
+    return fail(CPR_E_INVALID_ARG, "unknown policy");
+  memset(P, 0, sizeof(*P));
+  if (c->policy == CPR_FC16_POLICY_TABLE) {
+    const int64_t D = c->policy_table_dim;
+    if (!c->policy_table || D <= 0 || D > 256)
+      return fail(CPR_E_INVALID_ARG, "policy table missing or dim out of range (1..256)");
+    for (int64_t i = 0; i < D * D * 3; i++)
+      if (c->policy_table[i] > 3) return fail(CPR_E_INVALID_ARG, "policy table action out of range");
+    P->table_dim = (int32_t)D;
+  }
+  P->t_alpha = alpha_threshold(c->alpha);
+  P->t_gamma = alpha_threshold(c->gamma);
+  P->t_term = alpha_threshold(1.0 / c->horizon);
+  P->max_steps = c->max_steps > 0 ? c->max_steps : (int64_t)1 << 30;
+  P->policy = c->policy;
+  return CPR_OK;
 }
 
 static int validate(const cpr_config* c, NakParams* P, eth::EthParams* EP, bk::BkParams* BP,
@@ -596,7 +625,10 @@ int cpr_batch_create(cpr_ctx* ctx, const cpr_config* cfg, cpr_batch** out) {
   memset(&EP, 0, sizeof(EP));
   memset(&BP, 0, sizeof(BP));
   memset(&TP, 0, sizeof(TP));
-  int rc = validate(cfg, &P, &EP, &BP, &TP);
+  fc16::Fc16Params FP;
+  memset(&FP, 0, sizeof(FP));
+  int rc = cfg->protocol == CPR_PROTO_FC16 ? validate_fc16(cfg, &FP)
+                                           : validate(cfg, &P, &EP, &BP, &TP);
   if (rc) return rc;
   HIP_TRY(hipSetDevice(ctx->device));
   cpr_batch* b = new cpr_batch;
@@ -606,6 +638,7 @@ int cpr_batch_create(cpr_ctx* ctx, const cpr_config* cfg, cpr_batch** out) {
   b->EP = EP;
   b->BP = BP;
   b->TP = TP;
+  b->FP = FP;
   b->eth_bytes = eth::eth_lane_bytes(EP.cap_b, EP.cap_e, EP.n);
   if (cfg->protocol == CPR_PROTO_BK) b->bk_bytes = bk::bk_lane_bytes(BP);
   if (cfg->protocol == CPR_PROTO_TAILSTORM) b->bk_bytes = ts::ts_lane_bytes(TP);
@@ -620,6 +653,9 @@ int cpr_batch_create(cpr_ctx* ctx, const cpr_config* cfg, cpr_batch** out) {
              (cfg->protocol == CPR_PROTO_ETHEREUM && cfg->policy == CPR_ETH_POLICY_TABLE)) {
     const size_t nb = (size_t)cfg->policy_table_dim * cfg->policy_table_dim * 2;
     b->table_host.assign(cfg->policy_table, cfg->policy_table + nb);
+  } else if (cfg->protocol == CPR_PROTO_FC16 && cfg->policy == CPR_FC16_POLICY_TABLE) {
+    const size_t D = (size_t)cfg->policy_table_dim;
+    b->table_host.assign(cfg->policy_table, cfg->policy_table + D * D * 3);
   } else if (cfg->protocol == CPR_PROTO_TAILSTORM && cfg->policy == CPR_TS_POLICY_TABLE) {
     const size_t D = (size_t)cfg->policy_table_dim, K1 = (size_t)cfg->k + 1;
     b->table_host.assign(cfg->policy_table, cfg->policy_table + D * D * K1 * K1 * 3);
@@ -651,6 +687,7 @@ int cpr_batch_create(cpr_ctx* ctx, const cpr_config* cfg, cpr_batch** out) {
   b->BP.table = (const uint8_t*)b->table_dev.p;
   b->EP.table = (const uint8_t*)b->table_dev.p;  // Nakamoto-mode or ethereum_ssz table
   b->TP.table = (const uint8_t*)b->table_dev.p;
+  b->FP.table = (const uint8_t*)b->table_dev.p;
   if (cfg->protocol == CPR_PROTO_NAKAMOTO && !b->nak_ev) {
     // the same episode on the exact event engine: Ethereum lane, no uncles, nakamoto_ssz
     // policy (validated above); configurations it cannot hold keep the lane's flags
@@ -803,8 +840,26 @@ static int run_async_bk(cpr_batch* b, int64_t n, uint64_t first, const TraceSour
 }
 
 // tr == NULL: episodes [first, first + n) of the keyed stream; else trace episodes [0, n)
+// FC16 abstract-model episodes: grid-stride over n, a few resident workgroups per CU
+static int run_async_fc16(cpr_batch* b, int64_t n, uint64_t first, const TraceSource* tr,
+                          cpr_summary* sum_dev, cpr_episode_record* rec_dev) {
+  if (tr) return fail(CPR_E_UNSUPPORTED, "FC16 episodes have no trace format");
+  int64_t lanes = std::min<int64_t>((int64_t)b->ctx->cus * 8 * 256, ((n + 255) / 256) * 256);
+  lanes = std::max<int64_t>(256, lanes);
+  if (!b->ev0) {
+    HIP_TRY(hipEventCreate(&b->ev0));
+    HIP_TRY(hipEventCreate(&b->ev1));
+  }
+  HIP_TRY(hipEventRecord(b->ev0, b->ctx->stream));
+  HIP_TRY(launch_fc16_episodes(b->FP, b->cfg.seed, first, n, lanes, rec_dev, sum_dev,
+                               b->ctx->stream));
+  HIP_TRY(hipEventRecord(b->ev1, b->ctx->stream));
+  return CPR_OK;
+}
+
 static int run_async(cpr_batch* b, int64_t n, uint64_t first, const TraceSource* tr,
                      cpr_summary* sum_dev, cpr_episode_record* rec_dev) {
+  if (b->cfg.protocol == CPR_PROTO_FC16) return run_async_fc16(b, n, first, tr, sum_dev, rec_dev);
   if (b->cfg.protocol == CPR_PROTO_ETHEREUM || b->nak_ev)
     return run_async_eth(b, n, first, tr, sum_dev, rec_dev);
   if (b->is_ev) return run_async_bk(b, n, first, tr, sum_dev, rec_dev);
@@ -1082,6 +1137,8 @@ static LockBuffers lock_buffers(cpr_batch* b) {
 
 int cpr_reset(cpr_batch* b, const uint8_t* mask, const uint64_t* eps, double* obs) {
   if (!b || !obs) return fail(CPR_E_INVALID_ARG, "NULL argument");
+  if (b->cfg.protocol == CPR_PROTO_FC16)
+    return fail(CPR_E_UNSUPPORTED, "FC16 runs fused episodes (cpr_run_episodes) only");
   HIP_TRY(hipSetDevice(b->ctx->device));
   int rc = ensure_lockstep(b);
   if (rc) return rc;
@@ -1303,6 +1360,16 @@ int cpr_observation_spec(cpr_batch* b, int32_t* obs_len, int32_t* n_actions, dou
                          double* high) {
   if (!b) return fail(CPR_E_INVALID_ARG, "NULL argument");
   const double inf = __builtin_inf();
+  if (b->cfg.protocol == CPR_PROTO_FC16) {
+    // fc16.rs:61-73: (a, h, fork index) each mapped x -> x / (1 + x); at most 4 actions
+    if (obs_len) *obs_len = 3;
+    if (n_actions) *n_actions = 4;
+    for (int i = 0; i < 3; i++) {
+      if (low) low[i] = 0.0;
+      if (high) high[i] = 1.0;
+    }
+    return CPR_OK;
+  }
   if (b->cfg.protocol == CPR_PROTO_TAILSTORM) {
     // tailstorm_ssz.ml:41-79: 10 fields (diff signed, event discrete), Action8
     if (obs_len) *obs_len = 10;

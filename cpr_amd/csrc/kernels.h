@@ -8,6 +8,7 @@
 #include "bk_lane.h"
 #include "ethereum_lane.h"
 #include "nakamoto_lane.h"
+#include "fc16_lane.h"
 #include "summary.h"
 #include "ts_lane.h"
 
@@ -173,5 +174,10 @@ hipError_t launch_ts_policy(int32_t policy, int32_t k, int unit, const double* o
 size_t ts_slot_bytes();
 int ts_blocks_per_cu();
 int run_episodes_blocks_per_cu(int32_t mode);  // resident 256-lane workgroups per CU
+
+// FC'16 abstract-model episodes (fc16_lane.h), lanes = multiple of kBlock
+hipError_t launch_fc16_episodes(const fc16::Fc16Params& P, uint64_t seed, uint64_t first,
+                                int64_t n_eps, int64_t lanes, cpr_episode_record* recs,
+                                cpr_summary* sum, hipStream_t st);
 
 }  // namespace cpr

@@ -86,6 +86,7 @@ def make_config(
     subblock_selection=1,
     delay_lo=math.nan,
     delay_hi=math.nan,
+    horizon=100.0,
 ):
     """Build a cpr_config. ``defenders=None`` applies the gym's rule
     d = max(2, ceil(1 / (1 - gamma))) (gym/ocaml/cpr_gym/envs.py:70-76).
@@ -117,6 +118,7 @@ def make_config(
     c.subblock_selection = int(subblock_selection)
     c.delay_lo = float(delay_lo)
     c.delay_hi = float(delay_hi)
+    c.horizon = float(horizon)
     keep = None
     if table is not None and protocol in (L.PROTO_BK, L.PROTO_TAILSTORM):
         keep = np.ascontiguousarray(table, dtype=np.uint8).ravel()
@@ -126,6 +128,14 @@ def make_config(
             raise ValueError("B_k / Tailstorm policy table must have dim*dim*(k+1)*(k+1)*3 "
                              "entries")
         c.policy = L.BK_POLICY_TABLE if protocol == L.PROTO_BK else L.TS_POLICY_TABLE
+        c.policy_table = keep.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8))
+        c.policy_table_dim = dim
+    elif table is not None and protocol == L.PROTO_FC16:
+        keep = np.ascontiguousarray(table, dtype=np.uint8).ravel()
+        dim = int(round((keep.size // 3) ** 0.5))
+        if dim * dim * 3 != keep.size:
+            raise ValueError("FC16 policy table must have dim*dim*3 entries")
+        c.policy = L.FC16_POLICY_TABLE
         c.policy_table = keep.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8))
         c.policy_table_dim = dim
     elif table is not None and protocol == L.PROTO_ETHEREUM:

@@ -207,3 +207,99 @@ def policy_table(alpha, gamma, *, dim=None, maximum_fork_length=20, horizon=100,
                     x = honest
                 table[h, a, ev] = x
     return table.ravel()
+
+
+# ---- the FC'16 abstract-model kernel (gym/rust/src/fc16.rs, cpr_amd/csrc/fc16_lane.h)
+
+FC16_WAIT, FC16_ADOPT, FC16_OVERRIDE, FC16_MATCH = 0, 1, 2, 3  # fc16.rs:19-25 names
+_FC16_NAME = {WAIT: FC16_WAIT, ADOPT: FC16_ADOPT, OVERRIDE: FC16_OVERRIDE, MATCH: FC16_MATCH}
+
+
+def fc16_table(alpha, gamma, *, dim=None, maximum_fork_length=20, horizon=100,
+               stop_delta=1e-6):
+    """A `CPR_FC16_POLICY_TABLE` (entry (a, h, fork) = an action name) from the solved
+    SSZ'16 MDP: the MDP's action where it defines one, honest play elsewhere."""
+    model, states, vi = solve(alpha, gamma, maximum_fork_length=maximum_fork_length,
+                              horizon=horizon, stop_delta=stop_delta)
+    dim = maximum_fork_length + 1 if dim is None else dim
+    act = {}
+    for sid, s in enumerate(states):
+        acts = model.actions(s)
+        if acts:
+            act[s] = _FC16_NAME[acts[int(vi["vi_policy"][sid])]]
+    table = np.zeros((dim, dim, 3), np.uint8)
+    for a in range(dim):
+        for h in range(dim):
+            honest = FC16_OVERRIDE if a > h else (FC16_ADOPT if h > a else FC16_WAIT)
+            for fork in (IRRELEVANT, RELEVANT, ACTIVE):
+                table[a, h, fork] = act.get((a, h, fork), honest)
+    return table.ravel()
+
+
+def _fc16_threshold(p):
+    t = p * 4294967296.0
+    return 0 if t <= 0 else (4294967296 if t >= 4294967296.0 else int(t))
+
+
+def fc16_policy_value(alpha, gamma, horizon, table, *, max_states=200_000):
+    """Exact expected episode reward and progress of the device's FC16 lane under a table
+    policy: the Markov chain of fc16.rs's transitions (a successful match adds reward h and
+    progress 0, fc16.rs:109-110; the reward of the step that terminates is kept, fc16.rs:
+    174-199) with the lane's draw probabilities (thresholds / 2^32), solved exactly over
+    the states the policy reaches. Returns (E[reward], E[progress])."""
+    pa = _fc16_threshold(alpha) / 4294967296.0
+    pg = _fc16_threshold(gamma) / 4294967296.0
+    pt = _fc16_threshold(1.0 / horizon) / 4294967296.0
+    table = np.asarray(table, np.uint8).ravel()
+    dim = int(round((table.size // 3) ** 0.5))
+
+    def action(s):
+        a, h, fork = s
+        x = int(table[(min(a, dim - 1) * dim + min(h, dim - 1)) * 3 + fork])
+        if (x == FC16_OVERRIDE and not a > h) or (x == FC16_MATCH and not a >= h):
+            x = FC16_WAIT
+        return x
+
+    def transitions(s):
+        a, h, fork = s
+        x = action(s)
+        if x == FC16_ADOPT:
+            return [((1, 0, IRRELEVANT), pa, 0, h), ((0, 1, IRRELEVANT), 1 - pa, 0, h)]
+        if x == FC16_OVERRIDE:
+            return [((a - h, 0, IRRELEVANT), pa, h + 1, h + 1),
+                    ((a - h - 1, 1, RELEVANT), 1 - pa, h + 1, h + 1)]
+        if x == FC16_MATCH or fork == ACTIVE:
+            return [((a + 1, h, ACTIVE), pa, 0, 0), ((a - h, 1, RELEVANT), (1 - pa) * pg, h, 0),
+                    ((a, h + 1, RELEVANT), (1 - pa) * (1 - pg), 0, 0)]
+        return [((a + 1, h, IRRELEVANT), pa, 0, 0), ((a, h + 1, RELEVANT), 1 - pa, 0, 0)]
+
+    starts = [(1, 0, IRRELEVANT), (0, 1, IRRELEVANT)]
+    ids, order, queue = {}, [], deque(starts)
+    for s in starts:
+        ids[s] = len(order)
+        order.append(s)
+    tr = []
+    while queue:
+        s = queue.popleft()
+        row = transitions(s)
+        tr.append(row)
+        for d, _p, _r, _g in row:
+            if d not in ids:
+                if len(order) >= max_states:
+                    raise ValueError("the policy reaches more than max_states states")
+                ids[d] = len(order)
+                order.append(d)
+                queue.append(d)
+    n = len(order)
+    m = np.eye(n)
+    rhs_r = np.zeros(n)
+    rhs_g = np.zeros(n)
+    for s_id, row in enumerate(tr):
+        for d, p, r, g in row:
+            cont = (1.0 - pt) ** g  # no termination draw fires over g units of progress
+            m[s_id, ids[d]] -= p * cont
+            rhs_r[s_id] += p * r
+            rhs_g[s_id] += p * g
+    v_r = np.linalg.solve(m, rhs_r)
+    v_g = np.linalg.solve(m, rhs_g)
+    return (pa * v_r[0] + (1 - pa) * v_r[1], pa * v_g[0] + (1 - pa) * v_g[1])

@@ -54,9 +54,19 @@ enum cpr_protocol {
   CPR_PROTO_NAKAMOTO = 0, /* nakamoto.ml + nakamoto_ssz.ml */
   CPR_PROTO_ETHEREUM = 1, /* ethereum.ml Byzantium + ethereum_ssz.ml (cpr_protocols.ml:39-49) */
   CPR_PROTO_BK = 2,       /* bk.ml + bk_ssz.ml (cpr_protocols.ml:53-72), k = cpr_config.k */
-  CPR_PROTO_TAILSTORM = 3 /* tailstorm.ml + tailstorm_ssz.ml (cpr_protocols.ml:153-175),
+  CPR_PROTO_TAILSTORM = 3, /* tailstorm.ml + tailstorm_ssz.ml (cpr_protocols.ml:153-175),
                              k = cpr_config.k, selection = cpr_config.subblock_selection */
+  CPR_PROTO_FC16 = 4       /* the FC'16 abstract selfish-mining model with probabilistic
+                             termination, gym/rust/src/fc16.rs FC16SSZwPT: alpha, gamma,
+                             horizon, policy = enum cpr_fc16_policy; fused episodes only
+                             (cpr_run_episodes); max_steps caps an episode (CPR_ST_CAPACITY) */
 };
+
+/* policies of the FC16 model (fc16_lane.h); a table maps (a, h, fork) to an action name
+ * CPR_FC16_WAIT .. CPR_FC16_MATCH: table[(min(a,D-1)*D + min(h,D-1))*3 + fork],
+ * fork 0 irrelevant, 1 relevant, 2 active (fc16.rs:7-11) */
+enum cpr_fc16_policy { CPR_FC16_POLICY_HONEST = 0, CPR_FC16_POLICY_SM1 = 1, CPR_FC16_POLICY_TABLE = 2 };
+enum cpr_fc16_action { CPR_FC16_WAIT = 0, CPR_FC16_ADOPT = 1, CPR_FC16_OVERRIDE = 2, CPR_FC16_MATCH = 3 };
 
 /* incentive schemes (ethereum.ml:3,173-197; bk.ml:3,151-176) */
 enum cpr_reward_scheme {
@@ -211,6 +221,7 @@ typedef struct cpr_config {
   int32_t subblock_selection;/* Tailstorm: enum cpr_subblock_selection */
   double delay_lo, delay_hi;  /* CPR_NET_HONEST_CLIQUE link delays U[lo, hi); NaN, NaN = the
                                  models.ml default 0.5, 1.5 (0, 0 is a real zero delay) */
+  double horizon;             /* CPR_PROTO_FC16: expected progress before termination, >= 1 */
 } cpr_config;
 
 /* one finished episode; identical layout is produced by the CPU oracle */

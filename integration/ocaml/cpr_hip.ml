@@ -25,6 +25,7 @@ let proto_nakamoto = 0l
 let proto_ethereum = 1l
 let proto_bk = 2l
 let proto_tailstorm = 3l
+let proto_fc16 = 4l
 let net_selfish_mining = 0l
 let net_two_agents = 1l
 let net_honest_clique = 2l
@@ -81,6 +82,7 @@ let c_k = field config "k" int32_t
 let c_subblock_selection = field config "subblock_selection" int32_t
 let c_delay_lo = field config "delay_lo" double
 let c_delay_hi = field config "delay_hi" double
+let c_horizon = field config "horizon" double
 let () = seal config
 
 (* ---- cpr_episode_record *)

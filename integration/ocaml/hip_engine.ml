@@ -127,6 +127,7 @@ let of_module ?(device = 0) ?seed (Intf.AttackSpace (module M)) (p : Engine.Para
   setf cfg H.c_subblock_selection spec.selection;
   setf cfg H.c_delay_lo Float.nan;
   setf cfg H.c_delay_hi Float.nan;
+  setf cfg H.c_horizon 100.;
   let new_instance () =
     let c = allocate (ptr H.ctx) (from_voidp H.ctx null) in
     H.check (H.ctx_create device c);

@@ -699,3 +699,84 @@ def ts_loop(k, activations, *, net="clique", n_nodes=3, alpha=0.5, activation_de
         ctypes.byref(ht), ctypes.byref(hp), ctypes.byref(hh), ctypes.byref(nv)))
     return dict(reward=rew.tolist(), activations=acts.tolist(), head_time=ht.value,
                 head_progress=hp.value, head_height=hh.value, n_vertices=nv.value)
+
+
+# ---------------- FC'16 abstract model (gym/rust/src/fc16.rs), pure Python (small cases)
+
+FC16_TAG = 0x40000000
+FC16_WAIT, FC16_ADOPT, FC16_OVERRIDE, FC16_MATCH = 0, 1, 2, 3
+FC16_IRRELEVANT, FC16_RELEVANT, FC16_ACTIVE = 0, 1, 2
+
+
+def _thr(p):
+    t = p * 4294967296.0
+    return 0 if t <= 0 else (4294967296 if t >= 4294967296.0 else int(t))
+
+
+def fc16_policy(policy, a, h, fork, table=None, dim=0):
+    """honest / sapirshtein-2016-sm1 on (h, a) / a (a, h, fork) table of action names."""
+    if policy == 0:
+        return FC16_OVERRIDE if a > h else (FC16_ADOPT if h > a else FC16_WAIT)
+    if policy == 1:
+        if h > a:
+            return FC16_ADOPT
+        if h == 1 and a == 1:
+            return FC16_MATCH
+        if h == a - 1 and h >= 1:
+            return FC16_OVERRIDE
+        return FC16_WAIT
+    return int(table[(min(a, dim - 1) * dim + min(h, dim - 1)) * 3 + fork])
+
+
+def fc16_episode(seed, episode, alpha, gamma, horizon, policy, table=None, max_steps=1 << 30):
+    """One episode of FC16SSZwPT (fc16.rs:74-190) on the keyed stream of fc16_lane.h:
+    returns (reward, progress, steps, truncated). The offered actions are [Wait, Adopt,
+    Override if a > h, Match if a >= h]; a named action not offered acts as Wait."""
+    ta, tg, tt = _thr(alpha), _thr(gamma), _thr(1.0 / horizon)
+    dim = 0 if table is None else int(round((len(table) // 3) ** 0.5))
+    if int(keyed_block(seed, episode, 0, FC16_TAG | 1)[0]) < ta:
+        a, h = 1, 0
+    else:
+        a, h = 0, 1
+    fork, reward, progress, steps = FC16_IRRELEVANT, 0, 0, 0
+    j = 0
+    while True:
+        if j >= max_steps:
+            return reward, progress, steps, True
+        act = fc16_policy(policy, a, h, fork, table, dim)
+        if (act == FC16_OVERRIDE and not a > h) or (act == FC16_MATCH and not a >= h):
+            act = FC16_WAIT
+        w = keyed_block(seed, episode, j, FC16_TAG)
+        mining = int(w[0]) < ta
+        r = g = 0
+        if act == FC16_ADOPT:  # fc16.rs:131-137
+            a, h, fork, g = (1, 0, FC16_IRRELEVANT, h) if mining else (0, 1, FC16_IRRELEVANT, h)
+        elif act == FC16_OVERRIDE:  # fc16.rs:116-129
+            r = g = h + 1
+            a, h, fork = (a - h, 0, FC16_IRRELEVANT) if mining else (a - h - 1, 1, FC16_RELEVANT)
+        elif act == FC16_MATCH or fork == FC16_ACTIVE:  # fc16.rs:103-114
+            if mining:
+                a, fork = a + 1, FC16_ACTIVE
+            elif int(w[1]) < tg:
+                r = h
+                a, h, fork = a - h, 1, FC16_RELEVANT
+            else:
+                h, fork = h + 1, FC16_RELEVANT
+        else:  # fc16.rs:94-101
+            if mining:
+                a, fork = a + 1, FC16_IRRELEVANT
+            else:
+                h, fork = h + 1, FC16_RELEVANT
+        reward += r
+        progress += g
+        steps += 1
+        term = False
+        for i in range(g):  # fc16.rs:178-186, one Bernoulli(1/horizon) per unit of progress
+            if i % 4 == 0:
+                t = keyed_block(seed, episode, j, FC16_TAG | 0x100000 | (i >> 2))
+            if int(t[i % 4]) < tt:
+                term = True
+                break
+        if term:
+            return reward, progress, steps, False
+        j += 1
