@@ -183,3 +183,82 @@ def test_bk_spec_registry_and_validation(ctx):
         with pytest.raises(L.CprError) as e:
             device.Batch(cfg, keep=keep)
         assert e.value.code == L.CPR_E_INVALID_ARG
+
+
+class _HipBuffer:
+    """Device memory through the HIP runtime (ctypes), for rollout outputs too large to
+    stage through the host."""
+
+    def __init__(self, nbytes):
+        import ctypes
+
+        self.hip = ctypes.CDLL("libamdhip64.so")
+        self.p = ctypes.c_void_p()
+        assert self.hip.hipMalloc(ctypes.byref(self.p), ctypes.c_size_t(nbytes)) == 0
+        self.nbytes = nbytes
+
+    def rows(self, dtype, shape, lanes):
+        """host copy of columns `lanes` of a [T][n] row-major device array"""
+        import ctypes
+
+        T, n = shape
+        item = np.dtype(dtype).itemsize
+        out = np.zeros((T, len(lanes)), dtype)
+        host = np.zeros(n, dtype)
+        for t in range(T):
+            src = ctypes.c_void_p(self.p.value + t * n * item)
+            assert self.hip.hipMemcpy(host.ctypes.data_as(ctypes.c_void_p), src,
+                                      ctypes.c_size_t(n * item), 2) == 0  # DeviceToHost
+            out[t] = host[lanes]
+        return out
+
+    def free(self):
+        self.hip.hipFree(self.p)
+
+
+def test_configs4_full_size_table_rollout(ctx):
+    # BASELINE configs[4]: 65,536 lockstep B_k k=8 envs (bk(k=8, reward="constant") +
+    # bk_ssz, alpha .33, gamma .5, d = 2) stepped by an on-device table policy for 2048-step
+    # episodes (experiments/train/configs/bk-8.yaml:7-8, ppo.py:278-285); T = 2,200 steps so
+    # every lane finishes its first episode and auto-resets
+    n, T, ms, K, D = 65536, 2200, 2048, 8, 4
+    table = np.random.default_rng(41).integers(0, 8, size=D * D * (K + 1) ** 2 * 3).astype(
+        np.uint8)
+    cfg, keep = _cfg(alpha=0.33, gamma=0.5, table=table, k=K, max_steps=ms, seed=4,
+                     n_lanes=n)
+    b = device.Batch(cfg, keep=keep)
+    rew = _HipBuffer(T * n * 8)
+    done = _HipBuffer(T * n)
+    try:
+        s = b.rollout(T, device_outputs=(None, rew.p.value, done.p.value))
+        assert s.steps == n * T and s.invalid == 0
+        assert s.episodes >= n  # every lane finished at least one 2048-step episode
+        assert s.activations > s.steps * 0.5
+        # sampled lanes, bit for bit against sequential oracle episodes (auto-reset ids
+        # lane, lane + n, ...)
+        lanes = [0, 1, 777, 40000, n - 1]
+        r = rew.rows(np.float64, (T, n), lanes)
+        d = done.rows(np.uint8, (T, n), lanes)
+        for c, i in enumerate(lanes):
+            ep = i
+            e = O.BkGymEnv(cfg, episode=ep)
+            e.reset()
+            ret = 0.0
+            for t in range(T):
+                _, rr, dd, info = e.step(O.bk_policy(L.BK_POLICY_TABLE, e.fields(), K,
+                                                     table=table, dim=D))
+                assert r[t, c] == rr and bool(d[t, c]) == dd, (i, t)
+                ret += rr
+                if dd:
+                    # reward conservation: the step rewards sum to the episode's reward
+                    assert ret == info["episode_reward_attacker"], (i, t)
+                    assert info["episode_n_steps"] == ms
+                    ep += n
+                    e = O.BkGymEnv(cfg, episode=ep)
+                    e.reset()
+                    ret = 0.0
+        print(f"configs[4]: {s.steps} env-steps, {s.activations} activations, "
+              f"{s.episodes} finished episodes")
+    finally:
+        rew.free()
+        done.free()

@@ -247,3 +247,20 @@ def test_full_size_properties(ctx):
     # are within 2e-3 of the stationary value (finite-horizon start/end effects)
     m = s1.rel_revenue_fx / 2**32 / n
     assert abs(m - 0.384615) < 2e-3, m
+
+
+def test_configs0_honest_episodes_match_oracle(ctx):
+    # BASELINE configs[0]: cpr-nakamoto-v0 honest policy, alpha 0.33, gamma 0.5 (d = 2),
+    # 2016-step episodes (2017 activations), every record field against the oracle
+    cfg, keep = device.make_config(alpha=0.33, gamma=0.5, policy=L.POLICY_HONEST,
+                                   max_steps=2016, seed=0x5EED0000)
+    b = device.Batch(cfg, ctx=ctx, keep=keep)
+    s, rec = b.run(2048, records=True)
+    ref = O.run_episodes(cfg, 0, 2048, threads=8)
+    assert _records_equal(rec, ref) == {}
+    assert (rec["n_activations"] == 2017).all() and s.episodes == 2048
+    # honest play: the head chain is every block but the 1e-9-delay races' orphans, and
+    # the attacker's share is alpha (normalised reward ~ 1)
+    assert (rec["progress"] >= 2010).all()
+    share = rec["reward_attacker"].sum() / rec["progress"].sum()
+    assert abs(share - 0.33) < 0.005
