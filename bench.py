@@ -123,6 +123,9 @@ def main():
     ap.add_argument("--episodes", type=int, default=393216, help="per GPU per sweep point")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
+                    help="collective backend (nccl = RCCL; gloo only for the one-GPU "
+                         "multi-rank test, tests/test_gpu_distributed.py)")
     args = ap.parse_args()
 
     import torch
@@ -130,12 +133,15 @@ def main():
     from cpr_amd import _lib as L
     from cpr_amd import device, parallel
 
-    rank, ws, local = parallel.init("nccl")
+    rank, ws, local = parallel.init(args.backend)
     if ws != args.gpus and rank == 0:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE={ws}", file=sys.stderr)
-    torch.cuda.set_device(local)
-    tdev = torch.device("cuda", local)
-    ctx = device.Context(local)
+    # one GPU per rank; under gloo several ranks may share one GPU (rank-sharing test)
+    gpu = local if args.backend == "nccl" else local % max(1, torch.cuda.device_count())
+    torch.cuda.set_device(gpu)
+    tdev = torch.device("cuda", gpu)
+    cdev = tdev if args.backend == "nccl" else None  # where collectives' tensors live
+    ctx = device.Context(gpu)
     points = [(a, g) for g in GAMMAS for a in ALPHAS]
     batches = []
     for a, g in points:
@@ -162,17 +168,17 @@ def main():
         one_step(10**6 + w, new_sums())
     ctx.synchronize()
     sums_dev = new_sums()
-    parallel.barrier(tdev)
+    parallel.barrier(cdev)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for k in range(args.steps):
         one_step(k, sums_dev)
     ctx.synchronize()
     torch.cuda.synchronize()
-    parallel.barrier(tdev)
-    dt = parallel.allreduce_max(time.perf_counter() - t0, tdev)
+    parallel.barrier(cdev)
+    dt = parallel.allreduce_max(time.perf_counter() - t0, cdev)
     sums = read(sums_dev)
-    totals = [parallel.allreduce_summary(s, tdev) for s in sums]
+    totals = [parallel.allreduce_summary(s, cdev) for s in sums]
     acts = sum(int(s.activations) for s in totals)
     episodes = sum(int(s.episodes) for s in totals)
 
@@ -212,7 +218,8 @@ def main():
                 "episodes_per_point_per_gpu": E,
                 "points": len(points),
                 "activations_per_episode": STEPS_PER_EPISODE + 1,
-                "parallelism": f"dp{ws} (episode shards, 1 RCCL all-reduce of the summary)",
+                "parallelism": f"dp{ws} (episode shards, 1 {'RCCL' if args.backend == 'nccl' else 'gloo'} "
+                               f"all-reduce of the summary)",
             },
             "episodes_per_s": episodes / dt,
             "roofline": {
