@@ -80,7 +80,7 @@ ST_TRACE_MISS = 128
 ST_EXACT_RERUN = 256
 ST_INVALID = ST_CAPACITY | ST_REFERENCE_RAISES | ST_TRACE_MISS  # include/cpr_hip.h
 ST_LOCKSTEP_INEXACT = ST_OVERLAP | ST_DEEP_FORK | ST_TIE_UNRESOLVED | ST_STALE_TIME
-ABI_VERSION = 6  # include/cpr_hip.h CPR_ABI_VERSION this module's structures follow
+ABI_VERSION = 7  # include/cpr_hip.h CPR_ABI_VERSION this module's structures follow
 
 HIST_BINS = 64
 
@@ -280,6 +280,7 @@ EXPORTS = [
     "cpr_run_episodes_async",
     "cpr_synchronize",
     "cpr_replay",
+    "cpr_node_outputs",
     "cpr_last_launch",
     "cpr_reset",
     "cpr_step",
@@ -317,6 +318,8 @@ def _declare(L):
     L.cpr_run_episodes_async.argtypes = [vp, ctypes.c_int64, ctypes.c_uint64, vp, vp]
     L.cpr_synchronize.argtypes = [vp]
     L.cpr_replay.argtypes = [vp, P(CTrace), P(Summary), vp, ctypes.c_int]
+    L.cpr_node_outputs.argtypes = [vp, ctypes.c_int64, ctypes.c_uint64, vp, ctypes.c_int32, vp,
+                                   vp, vp]
     L.cpr_last_launch.argtypes = [vp, P(ctypes.c_double), P(ctypes.c_int64)]
     L.cpr_reset.argtypes = [vp, vp, vp, vp]
     L.cpr_step.argtypes = [vp, vp, vp, vp, vp, P(StepInfo)]

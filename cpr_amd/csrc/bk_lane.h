@@ -99,6 +99,11 @@ struct BkMem {
   uint64_t* skey;  // [2 * NQS]
   int32_t* sval;   // [2 * NQS]
   int32_t* stack;  // [NSTACK]
+  // per-node outputs (cpr_node_outputs), else null: activations per node, and per block
+  // quorum slot the cumulative rewards of every node along the block chain (the
+  // reference's per-vertex reward arrays, simulator.ml:377-388); genesis = zeros
+  int64_t* nact = nullptr;
+  int32_t* nrew = nullptr;
 };
 
 __host__ __device__ inline int64_t bk_align(int64_t x) { return (x + 127) / 128 * 128; }
@@ -134,6 +139,15 @@ __host__ __device__ inline BkMem bk_mem_at(uint8_t* base, const BkParams& P) {
   o += bk_align(2 * NQS * 4);
   M.stack = (int32_t*)(base + o);
   return M;
+}
+
+// per-node output region of one lane: activations [n] i64 | rewards [cap_q][n] i32
+__host__ __device__ inline int64_t bk_node_bytes(const BkParams& P) {
+  return bk_align((int64_t)P.n * 8) + bk_align((int64_t)P.cap_q * P.n * 4);
+}
+__host__ __device__ inline void bk_node_mem(BkMem& M, uint8_t* base, const BkParams& P) {
+  M.nact = (int64_t*)base;
+  M.nrew = (int32_t*)(base + bk_align((int64_t)P.n * 8));
 }
 
 // ---- observation and policies (bk_ssz.ml:21-34, 346-401); Action8 ranks
@@ -468,6 +482,15 @@ struct BkLane {
       else
         rd += P.k;
     }
+    if (M.nrew) {  // set_rewards per node: the precursor block's array plus this block's
+      int32_t* br = M.nrew + (int64_t)(qs & (P.cap_q - 1)) * P.n;
+      const int32_t* pr = p.qslot < 0 ? nullptr : M.nrew + (int64_t)(p.qslot & (P.cap_q - 1)) * P.n;
+      for (int32_t j = 0; j < P.n; ++j) br[j] = pr ? pr[j] : 0;
+      if (P.scheme == 0)
+        for (int32_t i = 0; i < P.k; ++i) br[X(P, M, dr[2 + i]).who] += 1;
+      else
+        br[node] += P.k;
+    }
     BVtx& b = M.vtx[s & (P.cap_v - 1)];
     init_vertex(P, M, b, s);
     b.parent = dr[1];
@@ -792,6 +815,7 @@ struct BkLane {
       V(P, M, 0, j) = V_RECV | V_GOT;
       VT(P, M, 0, j) = 0.0;
       M.tips[j] = 0;
+      if (M.nact) M.nact[j] = 0;
     }
     agent_init(0);
     schedule_pow(P, S, M);
@@ -851,6 +875,7 @@ struct BkLane {
           parent = M.tips[m];
         }
         push_now(P, M, mkev(EV_DAG, m, KD_POW), parent);
+        if (M.nact) ++M.nact[m];
         ++c_act;
         schedule_pow(P, S, M);
         break;

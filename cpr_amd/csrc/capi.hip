@@ -1018,13 +1018,8 @@ static int check_trace(const cpr_batch* b, const cpr_trace* t) {
   return CPR_OK;
 }
 
-int cpr_replay(cpr_batch* b, const cpr_trace* t, cpr_summary* summary,
-               cpr_episode_record* records, int records_on_device) {
-  if (!b || !t || !summary) return fail(CPR_E_INVALID_ARG, "NULL argument");
-  if (t->n_episodes <= 0) return CPR_OK;
-  const int rc = check_trace(b, t);
-  if (rc) return rc;
-  HIP_TRY(hipSetDevice(b->ctx->device));
+// copy a checked trace into the batch's trace buffers (on the context's stream)
+static int upload_trace(cpr_batch* b, const cpr_trace* t, TraceSource* out) {
   hipStream_t st = b->ctx->stream;
   const int64_t E = t->n_episodes;
   const int64_t na = t->act_offset[E], np = t->pow_offset[E], nl = t->link_offset[E];
@@ -1064,7 +1059,117 @@ int cpr_replay(cpr_batch* b, const cpr_trace* t, cpr_summary* summary,
   src.pow_hash = (const int32_t*)b->tr_pow.p;
   src.link_key = (const uint64_t*)b->tr_key.p;
   src.link_delay = (const double*)b->tr_ldelay.p;
-  return run_sync(b, E, 0, &src, summary, records, records_on_device);
+  *out = src;
+  return CPR_OK;
+}
+
+int cpr_replay(cpr_batch* b, const cpr_trace* t, cpr_summary* summary,
+               cpr_episode_record* records, int records_on_device) {
+  if (!b || !t || !summary) return fail(CPR_E_INVALID_ARG, "NULL argument");
+  if (t->n_episodes <= 0) return CPR_OK;
+  int rc = check_trace(b, t);
+  if (rc) return rc;
+  HIP_TRY(hipSetDevice(b->ctx->device));
+  TraceSource src;
+  rc = upload_trace(b, t, &src);
+  if (rc) return rc;
+  return run_sync(b, t->n_episodes, 0, &src, summary, records, records_on_device);
+}
+
+static int32_t network_nodes(const cpr_config& c) {
+  return c.network == CPR_NET_TWO_AGENTS      ? 2
+         : c.network == CPR_NET_HONEST_CLIQUE ? c.defenders
+                                               : c.defenders + 1;
+}
+
+// Per-node outputs (csv_runner.ml:74-79): the episodes run once more on the exact event
+// engine with a second per-lane region holding activations per node and per-block reward
+// arrays; Nakamoto configurations of the closed-form lane use the Nakamoto-mode engine of
+// the exact re-runs (same episodes, bit for bit)
+int cpr_node_outputs(cpr_batch* b, int64_t n, uint64_t first, const cpr_trace* trace,
+                     int32_t n_nodes, cpr_episode_record* records, int64_t* node_activations,
+                     double* node_rewards) {
+  if (!b || !node_activations || !node_rewards) return fail(CPR_E_INVALID_ARG, "NULL argument");
+  if (b->cfg.protocol == CPR_PROTO_FC16)
+    return fail(CPR_E_UNSUPPORTED, "FC16 episodes have no network nodes");
+  if (n_nodes != network_nodes(b->cfg))
+    return fail(CPR_E_INVALID_ARG, "n_nodes must equal the network's node count");
+  const bool nak_fused = b->cfg.protocol == CPR_PROTO_NAKAMOTO && !b->nak_ev;
+  if (nak_fused && !b->has_rerun)
+    return fail(CPR_E_UNSUPPORTED, "configuration beyond the exact event engine's capacity");
+  int rc;
+  TraceSource src;
+  if (trace) {
+    rc = check_trace(b, trace);
+    if (rc) return rc;
+    n = trace->n_episodes;
+    first = 0;
+  }
+  if (n <= 0) return CPR_OK;
+  HIP_TRY(hipSetDevice(b->ctx->device));
+  if (trace) {
+    rc = upload_trace(b, trace, &src);
+    if (rc) return rc;
+  }
+  hipStream_t st = b->ctx->stream;
+  const bool eth = b->cfg.protocol == CPR_PROTO_ETHEREUM || b->cfg.protocol == CPR_PROTO_NAKAMOTO;
+  const bool tsp = b->cfg.protocol == CPR_PROTO_TAILSTORM;
+  const eth::EthParams& EP = nak_fused ? b->NEP : b->EP;
+  const int64_t lane_bytes = eth ? eth::eth_lane_bytes(EP.cap_b, EP.cap_e, EP.n) : b->bk_bytes;
+  const int64_t node_bytes = eth ? eth::eth_node_bytes(EP.cap_b, EP.n)
+                             : tsp ? ts::ts_align((int64_t)b->TP.n * 8)
+                                   : bk::bk_node_bytes(b->BP);
+  const int64_t per_cu = eth ? eth_blocks_per_cu() : (tsp ? ts_blocks_per_cu() : bk_blocks_per_cu());
+  const int64_t full = (int64_t)b->ctx->cus * per_cu * 256;
+  const int64_t budget = kLaneBudget / (lane_bytes + node_bytes);
+  int64_t lanes = std::min(full, std::max<int64_t>(256, budget));
+  lanes = std::min(lanes, ((n + 255) / 256) * 256);
+  lanes = std::max<int64_t>(256, (lanes / 256) * 256);
+  void* pool = nullptr;
+  const size_t o_node = align256((size_t)lanes * (size_t)lane_bytes);
+  HIP_TRY(ctx_pool(b->ctx, o_node + (size_t)lanes * (size_t)node_bytes, &pool));
+  DevBuf out, sum;
+  const size_t rows = (size_t)n * (size_t)n_nodes;
+  const size_t o_rew = align256(rows * 8), o_hm = o_rew + align256(rows * 8),
+               o_rec = o_hm + align256((size_t)n * 4);
+  HIP_TRY(out.ensure(o_rec + (size_t)n * sizeof(cpr_episode_record)));
+  HIP_TRY(sum.ensure(sizeof(cpr_summary)));
+  HIP_TRY(hipMemsetAsync(sum.p, 0, sizeof(cpr_summary), st));
+  NodeOut no;
+  no.mem = (uint8_t*)pool + o_node;
+  no.lane_bytes = node_bytes;
+  no.acts = (int64_t*)out.p;
+  no.rews = (double*)((char*)out.p + o_rew);
+  no.head_miner = (int32_t*)((char*)out.p + o_hm);
+  cpr_episode_record* rec = (cpr_episode_record*)((char*)out.p + o_rec);
+  cpr_summary* sd = (cpr_summary*)sum.p;
+  uint8_t* mem = (uint8_t*)pool;
+  if (eth && trace)
+    HIP_TRY(launch_eth_replay_episodes(EP, src, n, mem, lane_bytes, lanes, rec, sd, st, no));
+  else if (eth)
+    HIP_TRY(launch_eth_run_episodes(EP, b->cfg.seed, first, n, mem, lane_bytes, lanes, rec, sd,
+                                    st, no));
+  else if (tsp && trace)
+    HIP_TRY(launch_ts_replay_episodes(b->TP, src, n, mem, lane_bytes, lanes, rec, sd, st, no));
+  else if (tsp)
+    HIP_TRY(launch_ts_run_episodes(b->TP, b->cfg.seed, first, n, mem, lane_bytes, lanes, rec, sd,
+                                   st, no));
+  else if (trace)
+    HIP_TRY(launch_bk_replay_episodes(b->BP, src, n, mem, lane_bytes, lanes, rec, sd, st, no));
+  else
+    HIP_TRY(launch_bk_run_episodes(b->BP, b->cfg.seed, first, n, mem, lane_bytes, lanes, rec, sd,
+                                   st, no));
+  std::vector<int32_t> hm((size_t)n);
+  HIP_TRY(hipMemcpyAsync(node_activations, no.acts, rows * 8, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipMemcpyAsync(node_rewards, no.rews, rows * 8, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipMemcpyAsync(hm.data(), no.head_miner, (size_t)n * 4, hipMemcpyDeviceToHost, st));
+  if (records)
+    HIP_TRY(hipMemcpyAsync(records, rec, (size_t)n * sizeof(cpr_episode_record),
+                           hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  if (records)
+    for (int64_t e = 0; e < n; e++) records[e].head_miner = hm[(size_t)e];
+  return CPR_OK;
 }
 
 // ---------------------------------------------------------------- lockstep API

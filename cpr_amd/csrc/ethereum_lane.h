@@ -97,6 +97,11 @@ struct EthMem {
   HNode* heap;
   int32_t* tips;
   int32_t* scr;
+  // per-node outputs (cpr_node_outputs), else null: activations per node, and per block
+  // slot the cumulative rewards of every node along the first-parent chain (the
+  // reference's per-vertex reward arrays, simulator.ml:377-388), units of 1/32
+  int64_t* nact = nullptr;
+  int32_t* nrew = nullptr;
 };
 
 __host__ __device__ inline int64_t align128(int64_t x) { return (x + 127) / 128 * 128; }
@@ -104,6 +109,15 @@ __host__ __device__ inline int64_t align128(int64_t x) { return (x + 127) / 128 
 __host__ __device__ inline int64_t eth_lane_bytes(int32_t cap_b, int32_t cap_e, int32_t n) {
   return align128((int64_t)cap_b * 64) + align128((int64_t)cap_b * n) +
          align128((int64_t)cap_e * 24) + align128((int64_t)n * 4) + align128(SCR_INTS * 4);
+}
+
+// per-node output region of one lane: activations [n] i64 | rewards [cap_b][n] i32
+__host__ __device__ inline int64_t eth_node_bytes(int32_t cap_b, int32_t n) {
+  return align128((int64_t)n * 8) + align128((int64_t)cap_b * n * 4);
+}
+__host__ __device__ inline void eth_node_mem(EthMem& M, uint8_t* base, int32_t n) {
+  M.nact = (int64_t*)base;
+  M.nrew = (int32_t*)(base + align128((int64_t)n * 8));
 }
 
 // bytes of the region after the block ring (visibility, heap, tips, scratch)
@@ -417,6 +431,16 @@ struct EthLane {
         rd += amt;
     }
     const int32_t s = ++newest;
+    if (M.nrew) {  // set_rewards per node: the precursor's array plus this block's list
+      const int32_t* pr = M.nrew + (int64_t)(d.p[0] & (P.cap_b - 1)) * P.n;
+      int32_t* br = M.nrew + (int64_t)(s & (P.cap_b - 1)) * P.n;
+      for (int32_t j = 0; j < P.n; ++j) br[j] = pr[j];
+      br[node] += 32 + nu;
+      for (int32_t i = 1; i < d.np; ++i) {
+        const EBlock& u = B(P, M, d.p[i]);
+        if (u.miner >= 0) br[u.miner] += P.scheme == 0 ? 30 : 4 * (8 - (d.height - u.height));
+      }
+    }
     EBlock& b = M.blk[s & (P.cap_b - 1)];
     b.serial = s;
     b.p[0] = d.p[0];
@@ -830,6 +854,8 @@ struct EthLane {
       V(P, M, 0, j) = V_RECV | V_GOT;
       M.tips[j] = 0;
       M.scr[SCR_PEND + j] = 0;
+      if (M.nact) M.nact[j] = 0;
+      if (M.nrew) M.nrew[j] = 0;  // genesis rewards, slot 0
     }
     agent_init(0);
     schedule_pow(P, S, M);
@@ -881,6 +907,7 @@ struct EthLane {
           dr = payload(P, M, m, M.tips[m], F_ALL, 0, 0);
         }
         push_now(P, M, mkev(EV_DAG, m, KD_POW), -1);
+        if (M.nact) ++M.nact[m];
         ++c_act;
         schedule_pow(P, S, M);
         break;

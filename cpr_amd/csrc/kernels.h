@@ -72,14 +72,27 @@ hipError_t launch_stream_fill(uint64_t seed, uint64_t ep, uint32_t idx0, uint32_
                               uint32_t* out, double* exp_out, hipStream_t st);
 size_t lock_lane_bytes();
 
+// Per-node outputs of the event-engine episode kernels (cpr_node_outputs): a second
+// per-lane region (activations per node, per-block reward arrays) and the [episode][node]
+// output rows; mem == nullptr disables them
+struct NodeOut {
+  uint8_t* mem = nullptr;
+  int64_t lane_bytes = 0;
+  int64_t* acts = nullptr;   // [n_eps][n]
+  double* rews = nullptr;    // [n_eps][n]
+  int32_t* head_miner = nullptr;  // [n_eps] miner of the head block (-1 genesis / summary)
+};
+
 // Ethereum (kernels_eth.hip): mem = lanes x lane_bytes, one region per resident lane
 hipError_t launch_eth_run_episodes(const eth::EthParams& P, uint64_t seed, uint64_t first,
                                    int64_t n_eps, uint8_t* mem, int64_t lane_bytes,
                                    int64_t lanes, cpr_episode_record* recs, cpr_summary* sum,
-                                   hipStream_t st);
+                                   hipStream_t st,
+                                   const NodeOut& no = NodeOut());
 hipError_t launch_eth_replay_episodes(const eth::EthParams& P, const TraceSource& src, int64_t n_eps,
                                  uint8_t* mem, int64_t lane_bytes, int64_t lanes,
-                                 cpr_episode_record* recs, cpr_summary* sum, hipStream_t st);
+                                 cpr_episode_record* recs, cpr_summary* sum, hipStream_t st,
+                                   const NodeOut& no = NodeOut());
 int eth_blocks_per_cu();
 // Ethereum lockstep lanes: mem = n x lane_bytes; slots = n x eth_slot_bytes()
 hipError_t launch_eth_reset(const eth::EthParams& P, uint64_t seed, uint8_t* mem,
@@ -128,10 +141,12 @@ hipError_t launch_nak_exact_rerun(const RerunLaunch* launches, const int64_t* qu
 // B_k (kernels_bk.hip): mem = lanes x lane_bytes; lockstep slots = n x bk_slot_bytes()
 hipError_t launch_bk_run_episodes(const bk::BkParams& P, uint64_t seed, uint64_t first,
                                   int64_t n_eps, uint8_t* mem, int64_t lane_bytes, int64_t lanes,
-                                  cpr_episode_record* recs, cpr_summary* sum, hipStream_t st);
+                                  cpr_episode_record* recs, cpr_summary* sum, hipStream_t st,
+                                   const NodeOut& no = NodeOut());
 hipError_t launch_bk_replay_episodes(const bk::BkParams& P, const TraceSource& src, int64_t n_eps,
                                  uint8_t* mem, int64_t lane_bytes, int64_t lanes,
-                                 cpr_episode_record* recs, cpr_summary* sum, hipStream_t st);
+                                 cpr_episode_record* recs, cpr_summary* sum, hipStream_t st,
+                                   const NodeOut& no = NodeOut());
 hipError_t launch_bk_reset(const bk::BkParams& P, uint64_t seed, uint8_t* mem, int64_t lane_bytes,
                            void* slots, int64_t n, const uint8_t* mask, const uint64_t* eps,
                            int unit, const double* tabs, int32_t tn, double* obs, hipStream_t st);
@@ -152,10 +167,12 @@ int bk_blocks_per_cu();
 // Tailstorm (kernels_ts.hip), same shapes as the B_k launchers
 hipError_t launch_ts_run_episodes(const ts::TsParams& P, uint64_t seed, uint64_t first,
                                   int64_t n_eps, uint8_t* mem, int64_t lane_bytes, int64_t lanes,
-                                  cpr_episode_record* recs, cpr_summary* sum, hipStream_t st);
+                                  cpr_episode_record* recs, cpr_summary* sum, hipStream_t st,
+                                   const NodeOut& no = NodeOut());
 hipError_t launch_ts_replay_episodes(const ts::TsParams& P, const TraceSource& src, int64_t n_eps,
                                  uint8_t* mem, int64_t lane_bytes, int64_t lanes,
-                                 cpr_episode_record* recs, cpr_summary* sum, hipStream_t st);
+                                 cpr_episode_record* recs, cpr_summary* sum, hipStream_t st,
+                                   const NodeOut& no = NodeOut());
 hipError_t launch_ts_reset(const ts::TsParams& P, uint64_t seed, uint8_t* mem, int64_t lane_bytes,
                            void* slots, int64_t n, const uint8_t* mask, const uint64_t* eps,
                            int unit, const double* tabs, int32_t tn, double* obs, hipStream_t st);

@@ -40,13 +40,14 @@ __device__ inline void bk_acc(Acc& acc, const bk::BkParams& P, const bk::BkLane&
 template <class Src>
 __global__ __launch_bounds__(kBlock) void k_bk_run_episodes(
     bk::BkParams P, Src src, int64_t n_eps, uint8_t* mem,
-    int64_t lane_bytes, cpr_episode_record* recs, cpr_summary* sum) {
+    int64_t lane_bytes, cpr_episode_record* recs, cpr_summary* sum, NodeOut no) {
   __shared__ int32_t hist[CPR_HIST_BINS];
   if (threadIdx.x < CPR_HIST_BINS) hist[threadIdx.x] = 0;
   __syncthreads();
   const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t nthreads = (int64_t)gridDim.x * blockDim.x;
-  const bk::BkMem M = bk::bk_mem_at(mem + tid * lane_bytes, P);
+  bk::BkMem M = bk::bk_mem_at(mem + tid * lane_bytes, P);
+  if (no.mem) bk::bk_node_mem(M, no.mem + tid * no.lane_bytes, P);
   Acc acc = {};
   bk::BkLane L;
   for (int64_t e = tid; e < n_eps; e += nthreads) {
@@ -77,6 +78,15 @@ __global__ __launch_bounds__(kBlock) void k_bk_run_episodes(
       r.status = L.status;
       r.head_work = 0;
       recs[e] = r;
+    }
+    if (no.acts) {  // csv_runner.ml:74-79: sim.activations and (Dag.data head).rewards
+      const int32_t* hr =
+          h.qslot < 0 ? nullptr : M.nrew + (int64_t)(h.qslot & (P.cap_q - 1)) * P.n;
+      for (int32_t j = 0; j < P.n; ++j) {
+        no.acts[e * P.n + j] = M.nact[j];
+        no.rews[e * P.n + j] = hr ? (double)hr[j] : 0.0;
+      }
+      no.head_miner[e] = h.who;
     }
   }
   __syncthreads();
@@ -278,17 +288,19 @@ static unsigned grid_of(int64_t n) { return (unsigned)((n + kBlock - 1) / kBlock
 
 hipError_t launch_bk_run_episodes(const bk::BkParams& P, uint64_t seed, uint64_t first,
                                   int64_t n_eps, uint8_t* mem, int64_t lane_bytes, int64_t lanes,
-                                  cpr_episode_record* recs, cpr_summary* sum, hipStream_t st) {
+                                  cpr_episode_record* recs, cpr_summary* sum, hipStream_t st,
+                                  const NodeOut& no) {
   hipLaunchKernelGGL(k_bk_run_episodes<SeedSource>, dim3((unsigned)(lanes / kBlock)), dim3(kBlock), 0, st, P,
-                     SeedSource{seed, first}, n_eps, mem, lane_bytes, recs, sum);
+                     SeedSource{seed, first}, n_eps, mem, lane_bytes, recs, sum, no);
   return hipGetLastError();
 }
 
 hipError_t launch_bk_replay_episodes(const bk::BkParams& P, const TraceSource& src, int64_t n_eps,
                                  uint8_t* mem, int64_t lane_bytes, int64_t lanes,
-                                 cpr_episode_record* recs, cpr_summary* sum, hipStream_t st) {
+                                 cpr_episode_record* recs, cpr_summary* sum, hipStream_t st,
+                                  const NodeOut& no) {
   hipLaunchKernelGGL(k_bk_run_episodes<TraceSource>, dim3((unsigned)(lanes / kBlock)),
-                     dim3(kBlock), 0, st, P, src, n_eps, mem, lane_bytes, recs, sum);
+                     dim3(kBlock), 0, st, P, src, n_eps, mem, lane_bytes, recs, sum, no);
   return hipGetLastError();
 }
 

@@ -18,13 +18,14 @@ namespace cpr {
 template <class Src>
 __global__ __launch_bounds__(kBlock) void k_eth_run_episodes(
     eth::EthParams P, Src src, int64_t n_eps, uint8_t* mem,
-    int64_t lane_bytes, cpr_episode_record* recs, cpr_summary* sum) {
+    int64_t lane_bytes, cpr_episode_record* recs, cpr_summary* sum, NodeOut no) {
   __shared__ int32_t hist[CPR_HIST_BINS];
   if (threadIdx.x < CPR_HIST_BINS) hist[threadIdx.x] = 0;
   __syncthreads();
   const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t nthreads = (int64_t)gridDim.x * blockDim.x;
-  const eth::EthMem M = eth::eth_mem_at(mem + tid * lane_bytes, P.cap_b, P.cap_e, P.n);
+  eth::EthMem M = eth::eth_mem_at(mem + tid * lane_bytes, P.cap_b, P.cap_e, P.n);
+  if (no.mem) eth::eth_node_mem(M, no.mem + tid * no.lane_bytes, P.n);
   Acc acc = {};
   eth::EthLane L;
   for (int64_t e = tid; e < n_eps; e += nthreads) {
@@ -61,6 +62,14 @@ __global__ __launch_bounds__(kBlock) void k_eth_run_episodes(
       r.status = L.status;
       r.head_work = P.nak ? 0 : h.work;
       recs[e] = r;
+    }
+    if (no.acts) {  // csv_runner.ml:74-79: sim.activations and (Dag.data head).rewards
+      const int32_t* hr = M.nrew + (int64_t)(hd & (P.cap_b - 1)) * P.n;
+      for (int32_t j = 0; j < P.n; ++j) {
+        no.acts[e * P.n + j] = M.nact[j];
+        no.rews[e * P.n + j] = (double)hr[j] / 32.0;
+      }
+      no.head_miner[e] = h.miner;
     }
   }
   __syncthreads();
@@ -190,17 +199,19 @@ hipError_t launch_nak_exact_rerun(const RerunLaunch* launches, const int64_t* qu
 hipError_t launch_eth_run_episodes(const eth::EthParams& P, uint64_t seed, uint64_t first,
                                    int64_t n_eps, uint8_t* mem, int64_t lane_bytes,
                                    int64_t lanes, cpr_episode_record* recs, cpr_summary* sum,
-                                   hipStream_t st) {
+                                   hipStream_t st, const NodeOut& no) {
   const unsigned blocks = (unsigned)(lanes / kBlock);
-  hipLaunchKernelGGL(k_eth_run_episodes<SeedSource>, dim3(blocks), dim3(kBlock), 0, st, P, SeedSource{seed, first}, n_eps, mem, lane_bytes, recs, sum);
+  hipLaunchKernelGGL(k_eth_run_episodes<SeedSource>, dim3(blocks), dim3(kBlock), 0, st, P,
+                     SeedSource{seed, first}, n_eps, mem, lane_bytes, recs, sum, no);
   return hipGetLastError();
 }
 
 hipError_t launch_eth_replay_episodes(const eth::EthParams& P, const TraceSource& src, int64_t n_eps,
                                  uint8_t* mem, int64_t lane_bytes, int64_t lanes,
-                                 cpr_episode_record* recs, cpr_summary* sum, hipStream_t st) {
+                                 cpr_episode_record* recs, cpr_summary* sum, hipStream_t st,
+                                 const NodeOut& no) {
   hipLaunchKernelGGL(k_eth_run_episodes<TraceSource>, dim3((unsigned)(lanes / kBlock)),
-                     dim3(kBlock), 0, st, P, src, n_eps, mem, lane_bytes, recs, sum);
+                     dim3(kBlock), 0, st, P, src, n_eps, mem, lane_bytes, recs, sum, no);
   return hipGetLastError();
 }
 

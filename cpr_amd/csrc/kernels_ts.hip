@@ -46,13 +46,14 @@ __device__ inline void ts_acc(Acc& acc, const ts::TsParams& P, ts::TsLane& L,
 template <class Src>
 __global__ __launch_bounds__(kBlock) void k_ts_run_episodes(
     ts::TsParams P, Src src, int64_t n_eps, uint8_t* mem,
-    int64_t lane_bytes, cpr_episode_record* recs, cpr_summary* sum) {
+    int64_t lane_bytes, cpr_episode_record* recs, cpr_summary* sum, NodeOut no) {
   __shared__ int32_t hist[CPR_HIST_BINS];
   if (threadIdx.x < CPR_HIST_BINS) hist[threadIdx.x] = 0;
   __syncthreads();
   const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t nthreads = (int64_t)gridDim.x * blockDim.x;
-  const ts::TsMem M = ts::ts_mem_at(mem + tid * lane_bytes, P);
+  ts::TsMem M = ts::ts_mem_at(mem + tid * lane_bytes, P);
+  if (no.mem) M.nact = (int64_t*)(no.mem + tid * no.lane_bytes);
   Acc acc = {};
   ts::TsLane L;
   for (int64_t e = tid; e < n_eps; e += nthreads) {
@@ -82,6 +83,15 @@ __global__ __launch_bounds__(kBlock) void k_ts_run_episodes(
       r.status = L.status;
       r.head_work = 0;
       recs[e] = r;
+    }
+    if (no.acts) {  // csv_runner.ml:74-79: sim.activations and (Dag.data head).rewards
+      const ts::TVtx& h = L.X(P, M, hd);
+      const double* hr = h.qslot < 0 ? nullptr : L.R(P, M, h.qslot);
+      for (int32_t j = 0; j < P.n; ++j) {
+        no.acts[e * P.n + j] = M.nact[j];
+        no.rews[e * P.n + j] = hr ? hr[j] : 0.0;
+      }
+      no.head_miner[e] = -1;  // summaries have no miner (tailstorm.ml info: kind, height)
     }
   }
   __syncthreads();
@@ -265,17 +275,19 @@ static unsigned ts_grid(int64_t n) { return (unsigned)((n + kBlock - 1) / kBlock
 
 hipError_t launch_ts_run_episodes(const ts::TsParams& P, uint64_t seed, uint64_t first,
                                   int64_t n_eps, uint8_t* mem, int64_t lane_bytes, int64_t lanes,
-                                  cpr_episode_record* recs, cpr_summary* sum, hipStream_t st) {
+                                  cpr_episode_record* recs, cpr_summary* sum, hipStream_t st,
+                                  const NodeOut& no) {
   hipLaunchKernelGGL(k_ts_run_episodes<SeedSource>, dim3((unsigned)(lanes / kBlock)), dim3(kBlock), 0, st, P,
-                     SeedSource{seed, first}, n_eps, mem, lane_bytes, recs, sum);
+                     SeedSource{seed, first}, n_eps, mem, lane_bytes, recs, sum, no);
   return hipGetLastError();
 }
 
 hipError_t launch_ts_replay_episodes(const ts::TsParams& P, const TraceSource& src, int64_t n_eps,
                                  uint8_t* mem, int64_t lane_bytes, int64_t lanes,
-                                 cpr_episode_record* recs, cpr_summary* sum, hipStream_t st) {
+                                 cpr_episode_record* recs, cpr_summary* sum, hipStream_t st,
+                                  const NodeOut& no) {
   hipLaunchKernelGGL(k_ts_run_episodes<TraceSource>, dim3((unsigned)(lanes / kBlock)),
-                     dim3(kBlock), 0, st, P, src, n_eps, mem, lane_bytes, recs, sum);
+                     dim3(kBlock), 0, st, P, src, n_eps, mem, lane_bytes, recs, sum, no);
   return hipGetLastError();
 }
 

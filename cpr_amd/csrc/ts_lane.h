@@ -112,6 +112,7 @@ struct TsMem {
   uint64_t* key;    // [NQS] sort keys
   int32_t* stack;   // [NSTACK]
   int32_t* fr;      // [4 * NFR] two frontiers of (ddepth, serial)
+  int64_t* nact = nullptr;  // per-node activations (cpr_node_outputs), else null
 };
 
 __host__ __device__ inline int64_t ts_align(int64_t x) { return (x + 127) / 128 * 128; }
@@ -1094,6 +1095,7 @@ struct TsLane {
       V(P, M, 0, j) = V_RECV | V_GOT;
       VT(P, M, 0, j) = 0.0;
       M.tips[j] = 0;
+      if (M.nact) M.nact[j] = 0;
     }
     pub = priv = 0;
     schedule_pow(P, S, M);
@@ -1162,6 +1164,7 @@ struct TsLane {
           parent = payload_parent(P, M, m, M.tips[m]);
         }
         push_now(P, M, mkev(EV_DAG, m, KD_POW), parent);
+        if (M.nact) ++M.nact[m];
         ++c_act;
         schedule_pow(P, S, M);
         break;

@@ -199,6 +199,30 @@ class Batch:
         L.check(L.lib().cpr_replay(self.handle, ctypes.byref(ct), ctypes.byref(s), L.ptr(rec), 0))
         return (s, rec) if records else s
 
+    @property
+    def n_nodes(self):
+        """Nodes of the batch's network: 2, defenders + 1 (attacker first) or the clique."""
+        c = self.config
+        if c.network == L.NET_TWO_AGENTS:
+            return 2
+        return int(c.defenders) if c.network == L.NET_HONEST_CLIQUE else int(c.defenders) + 1
+
+    def node_outputs(self, n_episodes=0, first_episode=0, trace=None):
+        """Per-node outputs (cpr_node_outputs): (records, activations [n, n_nodes] int64,
+        rewards [n, n_nodes] f64) of keyed episodes [first, first + n) or of a trace; the
+        `activations` / `reward` columns of a csv_runner.ml row."""
+        if trace is not None:
+            n_episodes = trace.n_episodes
+        nn = self.n_nodes
+        rec = np.zeros(n_episodes, dtype=L.RECORD_DTYPE)
+        acts = np.zeros((n_episodes, nn), dtype=np.int64)
+        rews = np.zeros((n_episodes, nn), dtype=np.float64)
+        ct = trace.ctrace() if trace is not None else None
+        L.check(L.lib().cpr_node_outputs(
+            self.handle, n_episodes, first_episode, ctypes.byref(ct) if ct is not None else None,
+            nn, L.ptr(rec), L.ptr(acts), L.ptr(rews)))
+        return rec, acts, rews
+
     def last_launch(self):
         """(kernel_ms, activations) of the last fused-episode launch (HIP events)."""
         ms = ctypes.c_double()

@@ -23,6 +23,9 @@
  *                                      fused into one device launch per batch
  *   cpr_run_episodes (LOOP mode)   -> Simulator.loop ~activations + head
  *                                      simulator/lib/simulator.ml:519-543, csv_runner.ml:56-98
+ *   cpr_node_outputs               -> the per-node `activations` / `reward` columns of a
+ *                                      csv_runner.ml:74-79 row (Simulator state.activations,
+ *                                      (Dag.data head).rewards, simulator.ml:377-388)
  *   cpr_stream_fill                -> the randomness the reference draws from OCaml Random
  *                                      (distributions.ml:17,24,90,93; simulator.ml:123),
  *                                      re-specified as a keyed Philox stream
@@ -36,7 +39,7 @@
 extern "C" {
 #endif
 
-#define CPR_ABI_VERSION 6
+#define CPR_ABI_VERSION 7
 
 typedef struct cpr_ctx cpr_ctx;
 typedef struct cpr_batch cpr_batch;
@@ -341,6 +344,20 @@ int cpr_synchronize(cpr_ctx* ctx);
  * asks for (same exported trace -> same per-episode outcomes). Synchronous. */
 int cpr_replay(cpr_batch* b, const cpr_trace* trace, cpr_summary* summary,
                cpr_episode_record* records, int records_on_device);
+/* Per-node outputs of episodes: activations per node and the head's reward array, one row
+ * of n_nodes per episode (node 0 = the attacker on selfish-mining / two-agents networks;
+ * n_nodes must be the network's node count: 2, defenders + 1, or defenders for cliques).
+ * trace == NULL: keyed-stream episodes [first_episode, first_episode + n_episodes); else
+ * trace episodes [0, trace->n_episodes) (n_episodes / first_episode ignored). The episodes
+ * run on the exact event engine (Nakamoto configurations of the closed-form lane: the
+ * Nakamoto-mode engine of its exact re-runs), so results equal cpr_run_episodes /
+ * cpr_replay bit for bit. Host buffers: node_activations and node_rewards
+ * [n_episodes][n_nodes]; records (optional) [n_episodes] as cpr_run_episodes, except that
+ * head_miner is the head block's miner in LOOP mode too (nakamoto.ml:22-27 head info;
+ * -1 genesis, Tailstorm summaries). Not for FC16. Synchronous. */
+int cpr_node_outputs(cpr_batch* b, int64_t n_episodes, uint64_t first_episode,
+                     const cpr_trace* trace, int32_t n_nodes, cpr_episode_record* records,
+                     int64_t* node_activations, double* node_rewards);
 /* device time (HIP events on the context's stream) of the last episode-kernel launch of
  * this batch, and the activations it simulated (valid after cpr_run_episodes returns;
  * after cpr_run_episodes_async + cpr_synchronize the time is valid and activations is -1) */

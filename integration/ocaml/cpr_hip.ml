@@ -1,4 +1,4 @@
-(* OCaml ctypes bindings of libcpr_hip (include/cpr_hip.h, CPR_ABI_VERSION 6).
+(* OCaml ctypes bindings of libcpr_hip (include/cpr_hip.h, CPR_ABI_VERSION 7).
 
    For a host that has OCaml: dropped next to the reference's gym engine
    (simulator/gym/), it lets Hip_engine.of_module (hip_engine.ml) stand in for
@@ -12,7 +12,7 @@
 open Ctypes
 open Foreign
 
-let abi_version = 6
+let abi_version = 7
 
 (* ---- status codes and enums (cpr_status, cpr_protocol, cpr_network, cpr_mode) *)
 let ok = 0
@@ -188,6 +188,13 @@ let replay =
   foreign
     "cpr_replay"
     (ptr batch @-> ptr trace @-> ptr summary @-> ptr record @-> int @-> returning int)
+;;
+
+let node_outputs =
+  foreign
+    "cpr_node_outputs"
+    (ptr batch @-> int64_t @-> uint64_t @-> ptr trace @-> int32_t @-> ptr record
+    @-> ptr int64_t @-> ptr double @-> returning int)
 ;;
 
 let last_launch =

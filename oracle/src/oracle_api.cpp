@@ -636,6 +636,27 @@ static Network loop_net(int net_kind, int n_nodes, double alpha, double activati
   return net;
 }
 
+// Per-node outputs of a loop task (csv_runner.ml:74-79 `activations` / `reward` columns):
+// run_loop_episode copies its per-node vectors here when a caller set the sink
+// (oracle_node_outputs); head_miner -2 = not reported
+struct NodeSink {
+  int64_t* acts = nullptr;
+  double* rews = nullptr;
+  int32_t* head_miner = nullptr;
+  int n = 0;
+};
+static thread_local NodeSink g_sink;
+
+static void sink_nodes(const int64_t* a, const double* r, int n, int32_t hm) {
+  if (!g_sink.acts) return;
+  if (n != g_sink.n) throw std::runtime_error("node outputs: node count mismatch");
+  for (int i = 0; i < n; ++i) {
+    g_sink.acts[i] = a[i];
+    g_sink.rews[i] = r[i];
+  }
+  *g_sink.head_miner = hm;
+}
+
 static int run_loop_episode(const cpr_config* c, uint64_t ep, cpr_episode_record* rec) {
   int64_t acts[2];
   double rew[2], ht, hp;
@@ -654,6 +675,7 @@ static int run_loop_episode(const cpr_config* c, uint64_t ep, cpr_episode_record
                            dflt ? 1.5 : c->delay_hi, c->reward_scheme, (int)c->activations,
                            a.data(), r.data(), &ht, &hp, &hh, &hm, &hw) != 0)
       return -1;
+    sink_nodes(a.data(), r.data(), n, c->protocol == CPR_PROTO_ETHEREUM ? -2 : hm);
     rec->reward_attacker = r[0];
     rec->reward_defender = 0.0;
     rec->n_activations = 0;
@@ -687,6 +709,7 @@ static int run_loop_episode(const cpr_config* c, uint64_t ep, cpr_episode_record
       rec->chain_time = r.head_time;
       rec->head_height = r.head_height;
       rec->head_miner = r.head_signer;
+      sink_nodes(ac.data(), rw.data(), (int)rw.size(), r.head_signer);
     } else {
       TsLoopResult r;
       try {
@@ -705,6 +728,7 @@ static int run_loop_episode(const cpr_config* c, uint64_t ep, cpr_episode_record
       rec->chain_time = r.head_time;
       rec->head_height = r.head_height;
       rec->head_miner = -1;
+      sink_nodes(ac.data(), rw.data(), (int)rw.size(), -1);
     }
     rec->reward_attacker = rw[0];
     rec->reward_defender = 0.0;
@@ -726,6 +750,7 @@ static int run_loop_episode(const cpr_config* c, uint64_t ep, cpr_episode_record
                        c->propagation_delay > 0 ? c->propagation_delay : 1e-9, c->policy,
                        (int)c->activations, a.data(), r.data(), &ht, &hp, &hh, &hm, &diag) != 0)
       return -1;
+    sink_nodes(a.data(), r.data(), n, hm);
     rec->reward_attacker = r[0];
     rec->reward_defender = 0.0;
     rec->n_activations = 0;
@@ -761,6 +786,10 @@ static int run_loop_episode(const cpr_config* c, uint64_t ep, cpr_episode_record
       flagged_record(rec, CPR_ST_REFERENCE_RAISES);
       return 0;
     }
+    {
+      const int64_t a2[2] = {r.activations[0], r.activations[1]};
+      sink_nodes(a2, r.rewards.data(), 2, -1);
+    }
     rec->reward_attacker = r.rewards[0];
     rec->reward_defender = r.rewards[1];
     rec->progress = r.head_progress;
@@ -779,6 +808,10 @@ static int run_loop_episode(const cpr_config* c, uint64_t ep, cpr_episode_record
     BkLoopResult r;
     bk_loop_task(Network::two_agents(c->activation_delay, c->alpha), 1, nullptr, c->seed, ep,
                  c->k, c->reward_scheme, c->policy, &bt, (int)c->activations, &r);
+    {
+      const int64_t a2[2] = {r.activations[0], r.activations[1]};
+      sink_nodes(a2, r.rewards.data(), 2, r.head_signer);
+    }
     rec->reward_attacker = r.rewards[0];
     rec->reward_defender = r.rewards[1];
     rec->progress = r.head_progress;
@@ -801,6 +834,7 @@ static int run_loop_episode(const cpr_config* c, uint64_t ep, cpr_episode_record
                                               acts, rew, &ht, &hp, &hh, &hw, &diag);
     g_eth_table = nullptr;
     if (rc != 0) return -1;
+    sink_nodes(acts, rew, 2, -2);
     rec->reward_attacker = rew[0];
     rec->reward_defender = rew[1];
     rec->progress = hp;
@@ -817,6 +851,7 @@ static int run_loop_episode(const cpr_config* c, uint64_t ep, cpr_episode_record
   if (oracle_two_agents_task(1, nullptr, c->seed, ep, c->alpha, c->policy,
                              (int)c->activations, acts, rew, &ht, &hp, &hh, &diag) != 0)
     return -1;
+  sink_nodes(acts, rew, 2, -2);
   rec->reward_attacker = rew[0];
   rec->reward_defender = rew[1];
   rec->progress = hp;
@@ -1164,6 +1199,56 @@ int oracle_trace_replay(const cpr_config* c, const cpr_trace* t, cpr_episode_rec
     rc = -1;
   }
   g_trace = TraceHook();
+  return rc;
+}
+
+// Per-node outputs of loop tasks (cpr_node_outputs' oracle): keyed episodes [first, first+n)
+// or, with t != NULL, trace episodes; rows of n_nodes; head_miner -2 where the task does
+// not report it
+int oracle_node_outputs(const cpr_config* c, uint64_t first, int64_t n, const cpr_trace* t,
+                        int n_nodes, cpr_episode_record* out, int64_t* acts, double* rews,
+                        int32_t* head_miner) {
+  if (c->mode != CPR_MODE_LOOP) {
+    set_err("oracle node outputs: loop mode only");
+    return -2;
+  }
+  if (t) n = t->n_episodes;
+  int rc = 0;
+  try {
+    for (int64_t e = 0; e < n && rc == 0; e++) {
+      g_sink.acts = acts + e * n_nodes;
+      g_sink.rews = rews + e * n_nodes;
+      g_sink.head_miner = head_miner + e;
+      g_sink.n = n_nodes;
+      head_miner[e] = -2;
+      for (int i = 0; i < n_nodes; ++i) {
+        g_sink.acts[i] = 0;
+        g_sink.rews[i] = 0.0;
+      }
+      if (t) {
+        cpr_trace one = *t;  // episode e of the trace as a one-episode trace
+        int64_t offs[3][2] = {{0, t->act_offset[e + 1] - t->act_offset[e]},
+                              {0, t->pow_offset[e + 1] - t->pow_offset[e]},
+                              {0, t->link_offset[e + 1] - t->link_offset[e]}};
+        one.n_episodes = 1;
+        one.act_offset = offs[0];
+        one.pow_offset = offs[1];
+        one.link_offset = offs[2];
+        one.act_miner = t->act_miner + t->act_offset[e];
+        one.act_delay = t->act_delay + t->act_offset[e];
+        one.pow_hash = t->pow_hash + t->pow_offset[e];
+        one.link_key = t->link_key + t->link_offset[e];
+        one.link_delay = t->link_delay + t->link_offset[e];
+        rc = oracle_trace_replay(c, &one, &out[e]);
+      } else {
+        rc = run_loop_episode(c, first + (uint64_t)e, &out[e]);
+      }
+    }
+  } catch (std::exception& ex) {
+    set_err(ex.what());
+    rc = -1;
+  }
+  g_sink = NodeSink();
   return rc;
 }
 

@@ -82,6 +82,8 @@ def lib():
         L.oracle_trace_fill.argtypes = [vp] + [vp] * 8
         L.oracle_trace_free.argtypes = [vp]
         L.oracle_trace_replay.argtypes = [P(C.Config), P(C.CTrace), vp]
+        L.oracle_node_outputs.argtypes = [P(C.Config), ctypes.c_uint64, ctypes.c_int64, vp,
+                                          ctypes.c_int, vp, vp, vp, vp]
         L.oracle_ocaml_sort_ints.argtypes = [vp, ctypes.c_int]
         L.oracle_ocaml_sort_pairs.argtypes = [vp, vp, ctypes.c_int]
         L.oracle_at_most_first_ints.argtypes = [vp, ctypes.c_int, ctypes.c_int]
@@ -316,6 +318,25 @@ def replay(config, trace):
     ct = trace.ctrace()
     check(lib().oracle_trace_replay(ctypes.byref(config), ctypes.byref(ct), rec.ctypes.data))
     return rec
+
+
+def node_outputs(config, n_nodes, first=0, n=0, trace=None):
+    """Per-node outputs of loop tasks (the oracle side of cpr_node_outputs): (records,
+    activations [n, n_nodes], rewards [n, n_nodes], head_miner [n], -2 = not reported)."""
+    from cpr_amd import _lib as C
+
+    if trace is not None:
+        n = trace.n_episodes
+    rec = np.zeros(n, dtype=C.RECORD_DTYPE)
+    acts = np.zeros((n, n_nodes), dtype=np.int64)
+    rews = np.zeros((n, n_nodes), dtype=np.float64)
+    hm = np.zeros(n, dtype=np.int32)
+    ct = trace.ctrace() if trace is not None else None
+    check(lib().oracle_node_outputs(ctypes.byref(config), first, n,
+                                    ctypes.byref(ct) if ct is not None else None, n_nodes,
+                                    rec.ctypes.data, acts.ctypes.data, rews.ctypes.data,
+                                    hm.ctypes.data))
+    return rec, acts, rews, hm
 
 
 # ---------------------------------------------------------------- OCaml Array.sort
