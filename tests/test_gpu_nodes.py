@@ -169,3 +169,56 @@ def test_chained_honest_net_rows_per_node(ctx, row):
     assert not (rec["status"] & L.ST_TRACE_MISS).any()
     assert acts[0].tolist() == row["activations_per_node"]
     assert rews[0].tolist() == row["reward"]
+
+
+# ---------------------------------------------------------------- TSV rows (csv_runner)
+
+TSV_LINES = sorted(int(k) for k in json.loads((GOLDEN / "honest_net_tsv_lines.json")
+                                               .read_text())["rows"])
+
+
+@pytest.mark.parametrize("line", TSV_LINES)
+def test_device_rows_reproduce_reference_text(ctx, line):
+    # data/honest_net.tsv text, every column but version / machine_duration_s, from the
+    # device's per-node outputs of the row's replayed OCaml Random draws
+    from test_csv_runner import CHAINS, SKIP, TSV, _fields, _task
+    from test_oracle_clique import chained_rng
+
+    from cpr_amd import csv_runner as C
+
+    row = CHAINS[line]
+    task = _task(row)
+    cfg, keep = C.config_of(task, seed=11)
+    trace, _ = O.export_traces(cfg, 0, 1, rng=chained_rng(row))
+    b = device.Batch(cfg, ctx=ctx, keep=keep)
+    rec, acts, rews = b.node_outputs(trace=trace)
+    got = _fields(C.result_row(task, rec[0], acts[0], rews[0], 0.0), TSV["header"])
+    for col, g, r in zip(TSV["header"], got, TSV["rows"][str(line)]):
+        if col not in SKIP:
+            assert g == r, (line, col, g, r)
+
+
+def test_csv_runner_end_to_end(ctx, tmp_path):
+    from cpr_amd import csv_runner as C
+
+    tasks = C.honest_net_tasks(2000)[::7] + C.withholding_tasks(2000)[::37]
+    rows = C.run(tasks, ctx=ctx, seed=3)
+    out = tmp_path / "rows.tsv"
+    C.save_rows_as_tsv(out, rows)
+    lines = out.read_text().rstrip("\n").split("\n")
+    header = lines[0].split("\t")
+    assert len(lines) == len(tasks) + 1
+    errors = 0
+    for t, ln in zip(tasks, lines[1:]):
+        d = dict(zip(header, ln.split("\t")))
+        assert d["network"] == t.network.key and d["number_activations"] == "2000"
+        if d.get("error"):
+            errors += 1
+            continue
+        acts = [int(x) for x in d["activations"].split("|")]
+        rews = [float(x) for x in d["reward"].split("|")]
+        assert len(acts) == len(rews) == len(t.network.compute)
+        assert sum(acts) == 2000
+        assert float(d["head_progress"]) > 0 and float(d["head_time"]) > 0
+    assert errors <= len(tasks) // 20, errors
+    print(f"{len(tasks)} tasks, {errors} error rows")
