@@ -55,6 +55,7 @@ ETH_POLICY_FN19PKEL = 4
 NET_SELFISH_MINING = 0
 NET_TWO_AGENTS = 1
 NET_HONEST_CLIQUE = 2
+NET_EXP_CLIQUE = 3  # include/cpr_hip.h: attacker + `defenders`, exponential link delays
 MODE_GYM = 0
 MODE_LOOP = 1
 

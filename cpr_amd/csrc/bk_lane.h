@@ -71,7 +71,8 @@ static_assert(sizeof(HNode) == 24, "HNode layout");
 struct BkParams {
   uint64_t t_att;
   int32_t d, n;   // defenders, nodes
-  int32_t net;    // 0 selfish mining, 1 two agents, 2 honest clique (all nodes honest)
+  int32_t net;    // 0 selfish mining, 1 two agents, 2 honest clique (all nodes honest),
+                  // 3 exponential-delay clique (node 0 attacker; delta = mean link delay)
   int32_t mode;   // 0 gym, 1 loop
   int32_t policy, scheme, k;
   int32_t cap_v, cap_q, cap_e, cap_d;
@@ -892,6 +893,8 @@ struct BkLane {
           double delay;
           if (P.net == 2)  // models.ml:4 uniform propagation delays on every link
             delay = S.msg_unif((uint32_t)s, (uint32_t)dst, P.lo, P.hi);
+          else if (P.net == 3)  // cpr_protocols.ml:481-483 exponential delays on every link
+            delay = S.msg_exp((uint32_t)s, (uint32_t)dst, P.delta);
           else if (P.net == 1)
             delay = 0.0;
           else if (node == 0)

@@ -191,6 +191,11 @@ struct Stream {
                                              double hi) const {
     return msg_u(serial, dest) * (hi - lo) + lo;
   }
+  // exponential(ev) delay of message `serial` to dest (distributions.ml:22-29; B_k /
+  // Tailstorm on exponential-delay cliques)
+  __host__ __device__ inline double msg_exp(uint32_t serial, uint32_t dest, double ev) const {
+    return (-1.0 * ev) * cpr_log(msg_u(serial, dest));
+  }
 };
 
 // ---- replay of an exported activation/delay trace (cpr_replay)
@@ -270,6 +275,9 @@ struct TraceStream {
   }
   __host__ __device__ inline double msg_unif(uint32_t serial, uint32_t dest, double,
                                              double) const {
+    return lookup(trace_msg_key(serial, dest));
+  }
+  __host__ __device__ inline double msg_exp(uint32_t serial, uint32_t dest, double) const {
     return lookup(trace_msg_key(serial, dest));
   }
 };

@@ -1180,6 +1180,8 @@ struct TsLane {
           double delay;
           if (P.net == 2)  // models.ml:4 uniform propagation delays on every link
             delay = S.msg_unif((uint32_t)s, (uint32_t)dst, P.lo, P.hi);
+          else if (P.net == 3)  // cpr_protocols.ml:481-483 exponential delays on every link
+            delay = S.msg_exp((uint32_t)s, (uint32_t)dst, P.delta);
           else if (P.net == 1)
             delay = 0.0;
           else if (node == 0)

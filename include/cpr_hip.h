@@ -142,10 +142,15 @@ enum cpr_ethereum_action_rank {
 enum cpr_network {
   CPR_NET_SELFISH_MINING = 0, /* network.ml:61-105, as the gym builds it (engine.ml:100-107) */
   CPR_NET_TWO_AGENTS = 1,     /* network.ml:50-59 */
-  CPR_NET_HONEST_CLIQUE = 2   /* experiments/simulate/models.ml:3-28 honest_clique: `defenders`
+  CPR_NET_HONEST_CLIQUE = 2,  /* experiments/simulate/models.ml:3-28 honest_clique: `defenders`
                                  = n honest nodes (2..64), node i has compute i + 1, every
                                  link delay uniform [delay_lo, delay_hi), simple
                                  dissemination; CPR_MODE_LOOP, Nakamoto or Ethereum */
+  CPR_NET_EXP_CLIQUE = 3      /* Network.T.symmetric_clique with exponential propagation
+                                 (cpr_protocols.ml:200-210,478-485): node 0 (the attacker,
+                                 running cfg.policy) plus `defenders` honest nodes (1..63),
+                                 equal compute, every link delay exponential with mean
+                                 propagation_delay; CPR_MODE_LOOP, B_k or Tailstorm */
 };
 
 enum cpr_mode {

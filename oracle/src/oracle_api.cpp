@@ -767,6 +767,58 @@ static int run_loop_episode(const cpr_config* c, uint64_t ep, cpr_episode_record
     rec->head_work = 0;
     return 0;
   }
+  if (c->network == CPR_NET_EXP_CLIQUE &&
+      (c->protocol == CPR_PROTO_BK || c->protocol == CPR_PROTO_TAILSTORM)) {
+    // symmetric clique, exponential(propagation_delay) links, node 0 runs the policy
+    // (cpr_protocols.ml:200-210,478-485), keyed stream
+    const Network net = loop_net(1, c->defenders + 1, 0.0, c->activation_delay,
+                                 c->propagation_delay, 0.0, 0.0);
+    std::vector<double> rw;
+    std::vector<int64_t> ac;
+    if (c->protocol == CPR_PROTO_BK) {
+      BkTable bt = bk_table_of(c);
+      BkLoopResult r;
+      bk_loop_task(net, 1, nullptr, c->seed, ep, c->k, c->reward_scheme, c->policy, &bt,
+                   (int)c->activations, &r);
+      rw = r.rewards;
+      ac.assign(r.activations.begin(), r.activations.end());
+      rec->progress = r.head_progress;
+      rec->chain_time = r.head_time;
+      rec->head_height = r.head_height;
+      rec->head_miner = r.head_signer;
+      sink_nodes(ac.data(), rw.data(), (int)rw.size(), r.head_signer);
+    } else {
+      TsLoopResult r;
+      try {
+        const TsTable tt = ts_table_of(c);
+        ts_loop_task(net, 1, nullptr, c->seed, ep, c->k, c->reward_scheme,
+                     c->subblock_selection, c->policy, (int)c->activations, &r, &tt);
+      } catch (BudgetExceeded&) {
+        flagged_record(rec, CPR_ST_CAPACITY);
+        return 0;
+      } catch (std::exception&) {
+        flagged_record(rec, CPR_ST_REFERENCE_RAISES);
+        return 0;
+      }
+      rw = r.rewards;
+      ac.assign(r.activations.begin(), r.activations.end());
+      rec->progress = r.head_progress;
+      rec->chain_time = r.head_time;
+      rec->head_height = r.head_height;
+      rec->head_miner = -1;
+      sink_nodes(ac.data(), rw.data(), (int)rw.size(), -1);
+    }
+    rec->reward_attacker = rw[0];
+    rec->reward_defender = 0.0;
+    rec->n_activations = 0;
+    for (size_t i = 1; i < rw.size(); ++i) rec->reward_defender += rw[i];
+    for (int64_t a : ac) rec->n_activations += a;
+    rec->sim_time = 0.0;
+    rec->n_steps = 0;
+    rec->status = 0;
+    rec->head_work = 0;
+    return 0;
+  }
   if (c->network != CPR_NET_TWO_AGENTS) {
     set_err("oracle loop mode: two-agents network, selfish-mining network (Nakamoto) or "
             "honest clique only");

@@ -1,0 +1,118 @@
+"""Exponential-delay cliques with an attacker (CPR_NET_EXP_CLIQUE) on the device — needs an
+MI355X.
+
+BASELINE configs[3] — Tailstorm k=8, discount rewards, a withholding attack on a 2-miner
+network with exponential delays — and the B_k / Tailstorm network of the reference's
+policy tests (cpr_protocols.ml:478-485: Network.T.symmetric_clique of 3 nodes, activation
+delay 100, exponential(1) propagation, node 0 patched with the attack space's policy):
+every record and per-node row bit-identical to the oracle on the keyed stream, and the
+reference's own orphan-rate limits (cpr_protocols.ml:554-617, honest policy, 1000
+activations, orphan rate <= 0.01) met.
+"""
+
+import numpy as np
+import pytest
+
+import oracle_py as O
+from cpr_amd import _lib as L
+from cpr_amd import device
+
+pytestmark = pytest.mark.gpu
+
+FIELDS = [f for f in L.RECORD_DTYPE.names if f != "status"]
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    return device.default_context()
+
+
+def exp_clique(protocol, defenders, policy, activations, k=8, scheme=L.REWARD_DISCOUNT,
+               sel=L.SELECT_HEURISTIC, ad=1.0, prop=1.0, seed=31):
+    return device.make_config(alpha=0.0, gamma=0.0, network=L.NET_EXP_CLIQUE, mode=L.MODE_LOOP,
+                              defenders=defenders, protocol=protocol, k=k, policy=policy,
+                              reward_scheme=scheme, subblock_selection=sel, activation_delay=ad,
+                              propagation_delay=prop, activations=activations, seed=seed)
+
+
+CASES = {
+    # configs[3]: attacker + 1 defender, exponential delays, each withholding policy
+    "cfg3-avoid-loss-ad1": (L.PROTO_TAILSTORM, 1, L.TS_POLICY_AVOID_LOSS, 2000, {}),
+    "cfg3-get-ahead-ad10": (L.PROTO_TAILSTORM, 1, L.TS_POLICY_GET_AHEAD, 2000, dict(ad=10.0)),
+    "cfg3-long-delay-ad2": (L.PROTO_TAILSTORM, 1, L.TS_POLICY_LONG_DELAY, 2000, dict(ad=2.0)),
+    "cfg3-minor-delay-optimal": (L.PROTO_TAILSTORM, 1, L.TS_POLICY_MINOR_DELAY, 1500,
+                                 dict(ad=5.0, sel=L.SELECT_OPTIMAL)),
+    "ts-3nodes-avoid-loss-a": (L.PROTO_TAILSTORM, 2, L.TS_POLICY_AVOID_LOSS_A, 1500,
+                               dict(ad=3.0, scheme=L.REWARD_CONSTANT)),
+    "bk-2miners-avoid-loss": (L.PROTO_BK, 1, L.BK_POLICY_AVOID_LOSS, 2000,
+                              dict(scheme=L.REWARD_CONSTANT, ad=2.0)),
+    "bk-4nodes-get-ahead": (L.PROTO_BK, 3, L.BK_POLICY_GET_AHEAD, 2000,
+                            dict(k=4, scheme=L.REWARD_BLOCK, ad=10.0)),
+}
+
+
+@pytest.mark.parametrize("case", list(CASES))
+def test_exp_clique_records_match_oracle(ctx, case):
+    proto, d, pol, acts, kw = CASES[case]
+    cfg, keep = exp_clique(proto, d, pol, acts, **kw)
+    b = device.Batch(cfg, ctx=ctx, keep=keep)
+    n = 64
+    s, rec = b.run(n, records=True)
+    ref = O.run_episodes(cfg, 0, n, threads=8)
+    for f in FIELDS:
+        bad = np.nonzero(rec[f] != ref[f])[0]
+        assert len(bad) == 0, (case, f, int(bad[0]), rec[f][bad[0]], ref[f][bad[0]])
+    inv = (rec["status"] & L.ST_INVALID) != 0
+    assert np.array_equal(inv, (ref["status"] & L.ST_INVALID) != 0)
+    assert inv.mean() < 0.05, (case, inv.mean())
+    assert s.episodes + s.invalid == n
+    # per-node rows (attacker first) equal the oracle's
+    rec2, a, r = b.node_outputs(n)
+    _, oa, orw, _ = O.node_outputs(cfg, d + 1, first=0, n=n)
+    ok = ~inv
+    assert np.array_equal(a[ok], oa[ok]) and np.array_equal(r[ok], orw[ok]), case
+    print(f"{case}: attacker share {rec['reward_attacker'][ok].sum() / (rec['reward_attacker'][ok] + rec['reward_defender'][ok]).sum():.4f}, "
+          f"invalid {int(inv.sum())}")
+
+
+@pytest.mark.parametrize("proto,k,scheme,sel", [
+    (L.PROTO_BK, 8, L.REWARD_BLOCK, 0),                                  # bk8/ssz/honest
+    (L.PROTO_TAILSTORM, 8, L.REWARD_CONSTANT, L.SELECT_OPTIMAL),         # tailstorm8constant
+    (L.PROTO_TAILSTORM, 8, L.REWARD_DISCOUNT, L.SELECT_HEURISTIC),       # tailstorm8discount
+])
+def test_reference_policy_test_orphan_limit(ctx, proto, k, scheme, sel):
+    # cpr_protocols.ml:478-520 `test ~policy:"honest" ~orphan_rate_limit:0.01`: 3-node
+    # symmetric clique, activation delay 100, exponential(1) propagation, 1000 activations
+    pol = L.BK_POLICY_HONEST if proto == L.PROTO_BK else L.TS_POLICY_HONEST
+    cfg, keep = exp_clique(proto, 2, pol, 1000, k=k, scheme=scheme, sel=sel, ad=100.0, seed=7)
+    b = device.Batch(cfg, ctx=ctx, keep=keep)
+    n = 4096
+    _, rec = b.run(n, records=True)
+    assert not (rec["status"] & L.ST_INVALID).any()
+    orphan = (1000.0 - rec["progress"]) / 1000.0
+    # the reference checks one episode; over 4096 keyed episodes the limit holds on
+    # average and for the bulk of them (the votes not yet confirmed when the loop stops,
+    # up to k - 1 of 1000, are counted as orphans too)
+    assert orphan.mean() <= 0.01, orphan.mean()
+    assert (orphan <= 0.01).mean() > 0.9, (orphan <= 0.01).mean()
+    ref = O.run_episodes(cfg, 0, 32, threads=8)
+    for f in FIELDS:
+        assert np.array_equal(rec[f][:32], ref[f]), f
+
+
+def test_exp_clique_rejections(ctx):
+    cases = [
+        (dict(mode=L.MODE_GYM, max_steps=100), "selfish-mining"),
+        (dict(defenders=0), "defenders"),
+        (dict(propagation_delay=0.0), "propagation_delay"),
+        (dict(protocol=L.PROTO_NAKAMOTO, policy=0), "network"),
+        (dict(protocol=L.PROTO_ETHEREUM, policy=0), "network"),
+    ]
+    for kw, msg in cases:
+        base = dict(alpha=0.0, gamma=0.0, network=L.NET_EXP_CLIQUE, mode=L.MODE_LOOP, defenders=1,
+                    protocol=L.PROTO_TAILSTORM, policy=0, propagation_delay=1.0,
+                    activations=100)
+        base.update(kw)
+        cfg, keep = device.make_config(**base)
+        with pytest.raises(L.CprError, match=msg):
+            device.Batch(cfg, ctx=ctx, keep=keep)
