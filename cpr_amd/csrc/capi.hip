@@ -403,19 +403,6 @@ static int validate_eth(const cpr_config* c, eth::EthParams* P) {
     P->lo = lo;
     P->hi = hi;
     clique_thresholds(c->defenders, P->thr);
-  } else if (c->network == CPR_NET_EXP_CLIQUE) {
-    // cpr_protocols.ml:478-485: symmetric clique, exponential link delays, node 0 runs the
-    // attack policy; the oracle's keyed draw for equal compute 1/n (attacker threshold)
-    if (c->mode != CPR_MODE_LOOP)
-      return fail(CPR_E_UNSUPPORTED, "the gym engine always uses the selfish-mining network");
-    if (c->defenders < 1 || c->defenders > 63)
-      return fail(CPR_E_INVALID_ARG, "exponential clique: 1..63 defenders");
-    if (!(c->propagation_delay > 0.) || !std::isfinite(c->propagation_delay))
-      return fail(CPR_E_INVALID_ARG, "exponential clique: propagation_delay must be positive");
-    P->d = c->defenders;
-    P->net = 3;
-    P->delta = c->propagation_delay;
-    P->t_att = alpha_threshold(1.0 / (double)(c->defenders + 1));
   } else {
     return fail(CPR_E_INVALID_ARG, "unknown network");
   }
@@ -525,6 +512,19 @@ static int validate_bk(const cpr_config* c, bk::BkParams* P) {
     P->lo = lo;
     P->hi = hi;
     clique_thresholds(c->defenders, P->thr);
+  } else if (c->network == CPR_NET_EXP_CLIQUE) {
+    // cpr_protocols.ml:478-485: symmetric clique, exponential link delays, node 0 runs the
+    // attack policy; the oracle's keyed draw for equal compute 1/n (attacker threshold)
+    if (c->mode != CPR_MODE_LOOP)
+      return fail(CPR_E_UNSUPPORTED, "the gym engine always uses the selfish-mining network");
+    if (c->defenders < 1 || c->defenders > 63)
+      return fail(CPR_E_INVALID_ARG, "exponential clique: 1..63 defenders");
+    if (!(c->propagation_delay > 0.) || !std::isfinite(c->propagation_delay))
+      return fail(CPR_E_INVALID_ARG, "exponential clique: propagation_delay must be positive");
+    P->d = c->defenders;
+    P->net = 3;
+    P->delta = c->propagation_delay;
+    P->t_att = alpha_threshold(1.0 / (double)(c->defenders + 1));
   } else {
     return fail(CPR_E_INVALID_ARG, "unknown network");
   }

@@ -34,9 +34,11 @@ struct Cfg {
                // 9 = a random table (CPR_TS_POLICY_TABLE, loop tasks)
   int scheme;  // 0 Constant, 1 Discount, 3 Punish, 4 Hybrid
   int steps;
-  int two_agents;  // 0 gym, 1 two-agents loop, 2 honest-clique loop (defenders = nodes)
+  int two_agents;  // 0 gym, 1 two-agents loop, 2 honest-clique loop (defenders = nodes),
+                   // 3 exponential-delay clique loop (attacker + defenders, mean delay prop)
   int k;
   double ev = 1.0;
+  double prop = 1.0;
 };
 
 struct Counters {
@@ -64,7 +66,10 @@ static const oracle::TsTable& g_table(int k) {
 static ts::TsParams params_of(const Cfg& cf) {
   ts::TsParams P{};
   P.t_att = oracle::alpha_threshold(cf.alpha);
-  P.d = cf.two_agents == 2 ? cf.defenders - 1 : cf.two_agents ? 1 : cf.defenders;
+  P.d = cf.two_agents == 2 ? cf.defenders - 1
+        : cf.two_agents == 3 ? cf.defenders
+        : cf.two_agents    ? 1
+                           : cf.defenders;
   P.n = P.d + 1;
   P.net = cf.two_agents;
   P.mode = cf.two_agents ? 1 : 0;
@@ -90,11 +95,17 @@ static ts::TsParams params_of(const Cfg& cf) {
   while (P.cap_v < span + 64 && P.cap_v < 4096) P.cap_v <<= 1;
   P.cap_q = P.cap_v / 2;
   P.cap_e = 256 + 512 * P.n + (cf.gamma == 0.0 && !cf.two_agents ? 2 * P.d * std::min(span, 8192) : 0);
+  if (cf.two_agents == 3) P.cap_e = 256 + 512 * P.n;
   P.cap_d = 64;
   P.ev = cf.ev;
   P.delta = 1e-9;
   const double dd = cf.defenders;
   P.dmax = (dd - 1.) / dd * 1e-9 / cf.gamma;
+  if (cf.two_agents == 3) {  // as capi.hip validate_bk for CPR_NET_EXP_CLIQUE
+    P.delta = cf.prop;
+    P.dmax = 0.0;
+    P.t_att = oracle::alpha_threshold(1.0 / (double)(cf.defenders + 1));
+  }
   P.max_steps = cf.steps;
   P.activations = cf.steps;
   P.max_progress = __builtin_inf();
@@ -279,6 +290,17 @@ static bool run_loop(const Cfg& cf, uint64_t seed, uint64_t ep, Counters& C, std
           net.nodes[i].links.push_back(
               oracle::Link{j >= i ? j + 1 : j, oracle::D_UNIFORM, 0.5, 1.5});
       }
+    } else if (cf.two_agents == 3) {  // cpr_protocols.ml:478-485, as oracle_api.cpp loop_net
+      const int n = cf.defenders + 1;
+      net = oracle::Network{};
+      net.flooding = false;
+      net.activation_delay = cf.ev;
+      net.nodes.resize(n);
+      for (int i = 0; i < n; ++i) {
+        net.nodes[i].compute = 1. / (double)n;
+        for (int j = 0; j < n - 1; ++j)
+          net.nodes[i].links.push_back(oracle::Link{j >= i ? j + 1 : j, oracle::D_EXP, cf.prop, 0.0});
+      }
     }
     oracle::ts_loop_task(net, 1, nullptr, seed, ep, cf.k, cf.scheme, g_sel,
                          cf.two_agents == 2 ? -1 : (cf.policy == 9 ? oracle::TS_POL_TABLE : cf.policy),
@@ -350,6 +372,24 @@ int main(int argc, char** argv) {
   g_sel = argc > 4 ? atoi(argv[4]) : 1;
   const uint64_t seed = 0x7A110000ull + (uint64_t)k * 16 + (uint64_t)g_sel;
   std::vector<Cfg> cfgs;
+  if (const char* one = getenv("TSCASE")) {
+    // one exponential-clique case: "defenders,policy,scheme,ev,prop,activations,seed,first,n"
+    int d, pol, sch, acts, first, n;
+    double ev, prop;
+    unsigned long long sd;
+    if (sscanf(one, "%d,%d,%d,%lf,%lf,%d,%llu,%d,%d", &d, &pol, &sch, &ev, &prop, &acts, &sd, &first,
+               &n) != 9)
+      return 2;
+    Cfg cf{0, 0, d, pol, sch, acts, 3, k, ev, prop};
+    Counters C;
+    for (int e = first; e < first + n; e++) {
+      std::string why;
+      if (!run_loop(cf, sd, e, C, why)) fprintf(stderr, "MISMATCH ep=%d: %s\n", e, why.c_str());
+    }
+    printf("{\"episodes\": %ld, \"mismatches\": %ld, \"capacity\": %ld, \"raises\": %ld}\n",
+           C.episodes, C.mismatches, C.capacity, C.raises);
+    return C.mismatches ? 1 : 0;
+  }
   const double alphas[] = {0.1, 0.25, 0.33, 0.45};
   const double gammas[] = {0.0, 0.5, 0.9};
   for (double a : alphas)
@@ -366,6 +406,10 @@ int main(int argc, char** argv) {
   for (int n : {2, 3, 10})
     for (double ev : {0.5, 2.0, 30.0, 600.0})
       for (int sch : {0, 1, 3, 4}) cfgs.push_back(Cfg{0, 0, n, 0, sch, steps * 2, 2, k, ev});
+  // exponential-delay cliques with the attacker as node 0 (configs[3] and its 3-node form)
+  for (int d : {1, 2})
+    for (double ev : {1.0, 10.0})
+      for (int pol : {0, 1, 2, 3, 9}) cfgs.push_back(Cfg{0, 0, d, pol, 1, steps * 2, 3, k, ev, 1.0});
   Counters C;
   int shown = 0;
   for (auto& cf : cfgs)

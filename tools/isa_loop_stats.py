@@ -1,0 +1,106 @@
+"""Static instruction mix of the activation loop of a fused-episode kernel.
+
+Compiles one translation unit to gfx950 assembly (hipcc -S, same flags as the build),
+finds the kernel, and counts the instructions of every basic block whose innermost loop
+is the activation loop (the depth-2 loop: depth 1 is the grid-stride episode loop),
+plus those of loops nested in it, separately. Used to compare layouts of the Nakamoto
+lane without a GPU; the PMC-measured SQ_INSTS_VALU per activation is the real figure.
+
+usage: python tools/isa_loop_stats.py [kernels.hip] [kernel-substring] [-D...]
+"""
+import collections
+import pathlib
+import re
+import subprocess
+import sys
+
+ROOT = pathlib.Path(__file__).resolve().parent.parent
+
+
+def compile_asm(src, defines):
+    out = pathlib.Path("/tmp") / (pathlib.Path(src).stem + ".s")
+    cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17",
+           "-ffp-contract=off", f"-I{ROOT / 'include'}", "--cuda-device-only", "-S",
+           *defines, str(src), "-o", str(out)]
+    subprocess.run(cmd, check=True, stderr=subprocess.DEVNULL)
+    return out.read_text().split("\n")
+
+
+def kernel_meta(lines, name):
+    meta = {}
+    for i, l in enumerate(lines):
+        if l.strip() == f".name:           {name}":
+            for l2 in lines[i - 12:i + 12]:
+                m = re.match(r"\s+\.(sgpr_count|vgpr_count|sgpr_spill_count|vgpr_spill_count|"
+                             r"private_segment_fixed_size):\s+(\d+)", l2)
+                if m:
+                    meta[m.group(1)] = int(m.group(2))
+    return meta
+
+
+def kernel_lines(lines, sub):
+    starts = [i for i, l in enumerate(lines) if re.match(r"^_Z\S+:", l)]
+    for j, s in enumerate(starts):
+        if sub in lines[s]:
+            e = starts[j + 1] if j + 1 < len(starts) else len(lines)
+            return lines[s:e], lines[s].split(":")[0]
+    raise SystemExit(f"kernel {sub!r} not found")
+
+
+def main():
+    args = [a for a in sys.argv[1:] if not a.startswith("-D")]
+    defines = [a for a in sys.argv[1:] if a.startswith("-D")]
+    src = args[0] if args else str(ROOT / "cpr_amd" / "csrc" / "kernels.hip")
+    sub = args[1] if len(args) > 1 else "k_run_episodesILi0ENS_10SeedSourceELi3E"
+    all_lines = compile_asm(src, defines)
+    lines, name = kernel_lines(all_lines, sub)
+    meta = kernel_meta(all_lines, name)
+    # basic blocks: (label, annotation comments, instructions)
+    blocks = []
+    for l in lines:
+        m = re.match(r"^(\.L(BB\d+_\d+):|; %bb\.\d+:)(.*)$", l)
+        if m:
+            blocks.append([m.group(2), m.group(3), []])
+            continue
+        t = l.strip()
+        if not blocks:
+            continue
+        if t.startswith(";") and not blocks[-1][2]:
+            blocks[-1][1] += " " + t
+            continue
+        if not t or t.startswith(";") or t.startswith("."):
+            continue
+        blocks[-1][2].append(t.split()[0])
+    depth = {}
+    for lab, ann, _ in blocks:
+        m = re.search(r"This Loop Header: Depth=(\d+)", ann)
+        if m:
+            depth[lab] = int(m.group(1))
+    hdr2 = [h for h, d in depth.items() if d == 2]
+    body = collections.Counter()
+    nested = collections.Counter()
+    for lab, ann, ins in blocks:
+        if lab in depth:
+            loop = lab
+        else:
+            m = re.search(r"in Loop: Header=(BB\d+_\d+)", ann)
+            loop = m.group(1) if m else None
+        tgt = body if loop in hdr2 else (nested if depth.get(loop, 0) > 2 else None)
+        if tgt is not None:
+            tgt.update(ins)
+    v = sum(c for o, c in body.items() if o.startswith("v_"))
+    s = sum(c for o, c in body.items() if o.startswith("s_"))
+    mov = sum(c for o, c in body.items() if o.startswith("v_mov"))
+    lane = sum(c for o, c in body.items() if "lane" in o and o.startswith("v_"))
+    f64 = sum(c for o, c in body.items() if o.startswith("v_") and "f64" in o)
+    print(f"{name}\n activation-loop body: VALU {v} (v_mov {mov}, readlane/writelane {lane}, "
+          f"f64 {f64}), SALU {s}, LDS {sum(c for o, c in body.items() if o.startswith('ds_'))}")
+    nv = sum(c for o, c in nested.items() if o.startswith("v_"))
+    print(f" registers: {meta}")
+    print(f" nested loops inside it: VALU {nv}")
+    for o, c in body.most_common(25):
+        print(f"   {c:4d} {o}")
+
+
+if __name__ == "__main__":
+    main()
