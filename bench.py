@@ -8,7 +8,10 @@ episode), fused into one kernel launch per point; the batch summary is integer-e
 all-reduced once over RCCL. Weak scaling: E is per GPU.
 
 gamma = 1 is rejected by the reference (gym/ocaml/cpr_gym/envs.py:73-75,
-network.ml:69-72), so the sweep runs gamma in {0, 0.5}.
+network.ml:69-72), so the timed sweep runs gamma in {0, 0.5}; the gamma = 1 column runs
+after it, untimed for `value`, in the flagged abstract-gamma mode (CPR_NET_ABSTRACT_GAMMA,
+include/cpr_hip.h) and is reported separately ("abstract_gamma_1") beside the Eyal-Sirer
+closed form.
 
 Prints one JSON line (rank 0).
 """
@@ -43,6 +46,12 @@ def _host_cores():
     share = os.environ.get("OMP_NUM_THREADS")
     cores = min(aff, int(share)) if share and share.isdigit() and int(share) > 0 else aff
     return max(1, cores), aff
+
+
+def es14(alpha, gamma):
+    """Eyal & Sirer (FC'14) relative revenue of selfish mining (alpha < 1/2)."""
+    a, g = alpha, gamma
+    return (a * (1 - a) ** 2 * (4 * a + g * (1 - 2 * a)) - a ** 3) / (1 - a * (1 + (2 - a) * a))
 
 
 def cpu_baseline(seconds, points):
@@ -186,6 +195,25 @@ def main():
     # around the last launch of every point, on the stream the kernel runs on; activations
     # per launch = E episodes x (max_steps + 1) (every gym episode is exactly that long)
     kms = np.array([b.last_launch()[0] for b in batches])
+
+    # configs[1]'s gamma = 1 column in the flagged abstract-gamma mode, after the timed
+    # region: same kernel, zero delays, match races decided by gamma coins; its own clock
+    abatches = []
+    for a in ALPHAS:
+        cfg, keep = device.make_config(alpha=a, gamma=1.0, network=L.NET_ABSTRACT_GAMMA,
+                                       defenders=2, max_steps=STEPS_PER_EPISODE, seed=SEED)
+        abatches.append(device.Batch(cfg, ctx=ctx, keep=keep))
+    asums = new_sums()
+    parallel.barrier(cdev)
+    torch.cuda.synchronize()
+    ta = time.perf_counter()
+    for b, sd in zip(abatches, asums):
+        b.run_async(E, rank * E, sd.data_ptr())
+    ctx.synchronize()
+    torch.cuda.synchronize()
+    parallel.barrier(cdev)
+    dta = parallel.allreduce_max(time.perf_counter() - ta, cdev)
+    atotals = [parallel.allreduce_summary(s, cdev) for s in read(asums[:len(abatches)])]
     traffic, traffic_src, valu_meas = pmc_traffic(E)
     kacts = np.full(len(batches), float(E * (STEPS_PER_EPISODE + 1)))
     act_per_s_kernel = float(kacts.sum() / (kms.sum() / 1e3))
@@ -243,11 +271,24 @@ def main():
             },
             "status": {"tie_episodes": ties, "overlap_episodes": overlaps, "other": other},
             "sweep_mean_rel_revenue": sweep,
+            "abstract_gamma_1": {
+                "mode": "FLAGGED abstract-gamma (CPR_NET_ABSTRACT_GAMMA): not the reference's "
+                        "network, which rejects gamma = 1; zero delays, 2 defenders, a match "
+                        "race goes to the attacker's release at every defender (coin < 1)",
+                "activations_per_s": sum(int(s.activations) for s in atotals) / dta,
+                "episodes_per_point": E * ws,
+                "mean_rel_revenue_vs_es14": {
+                    f"{a:.2f}": [round(parallel.summary_stats(s)["mean"], 6),
+                                 round(parallel.summary_stats(s)["stderr"], 6),
+                                 round(es14(a, 1.0), 6) if a < 0.5 else None]
+                    for a, s in zip(ALPHAS, atotals)},
+                "invalid_episodes": sum(int(s.invalid) for s in atotals),
+            },
         }
         if not args.no_cpu and ws == 1:
             out["cpu_baseline"] = cpu_baseline(args.cpu_seconds, points)
         print(json.dumps(out), flush=True)
-    for b in batches:
+    for b in batches + abatches:
         b.close()
     ctx.close()
     if ws > 1:

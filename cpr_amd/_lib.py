@@ -56,6 +56,7 @@ NET_SELFISH_MINING = 0
 NET_TWO_AGENTS = 1
 NET_HONEST_CLIQUE = 2
 NET_EXP_CLIQUE = 3  # include/cpr_hip.h: attacker + `defenders`, exponential link delays
+NET_ABSTRACT_GAMMA = 4  # FLAGGED abstract-gamma mode (include/cpr_hip.h), gamma in [0, 1]
 MODE_GYM = 0
 MODE_LOOP = 1
 
@@ -81,7 +82,7 @@ ST_TRACE_MISS = 128
 ST_EXACT_RERUN = 256
 ST_INVALID = ST_CAPACITY | ST_REFERENCE_RAISES | ST_TRACE_MISS  # include/cpr_hip.h
 ST_LOCKSTEP_INEXACT = ST_OVERLAP | ST_DEEP_FORK | ST_TIE_UNRESOLVED | ST_STALE_TIME
-ABI_VERSION = 7  # include/cpr_hip.h CPR_ABI_VERSION this module's structures follow
+ABI_VERSION = 8  # include/cpr_hip.h CPR_ABI_VERSION this module's structures follow
 
 HIST_BINS = 64
 

@@ -320,6 +320,18 @@ static int validate(const cpr_config* c, NakParams* P, eth::EthParams* EP, bk::B
     P->delta = 0.0;
     P->dmax = 0.0;
     P->arrive = 1;
+  } else if (c->network == CPR_NET_ABSTRACT_GAMMA) {
+    // flagged abstract-gamma mode (include/cpr_hip.h): zero delays, coin-decided races
+    if (c->mode != CPR_MODE_GYM)
+      return fail(CPR_E_UNSUPPORTED, "the abstract-gamma mode runs gym episodes");
+    if (c->defenders < 1 || c->defenders > 64)
+      return fail(CPR_E_INVALID_ARG, "abstract gamma: 1..64 defenders");
+    P->d = c->defenders;
+    P->delta = 0.0;
+    P->dmax = 0.0;
+    P->arrive = 1;
+    P->abstract_g = 1;
+    P->gamma = c->gamma;
   } else {
     return fail(CPR_E_INVALID_ARG, "unknown network");
   }
@@ -1079,6 +1091,8 @@ static int upload_trace(cpr_batch* b, const cpr_trace* t, TraceSource* out) {
 int cpr_replay(cpr_batch* b, const cpr_trace* t, cpr_summary* summary,
                cpr_episode_record* records, int records_on_device) {
   if (!b || !t || !summary) return fail(CPR_E_INVALID_ARG, "NULL argument");
+  if (b->cfg.network == CPR_NET_ABSTRACT_GAMMA)
+    return fail(CPR_E_UNSUPPORTED, "the abstract-gamma mode has no trace replay");
   if (t->n_episodes <= 0) return CPR_OK;
   int rc = check_trace(b, t);
   if (rc) return rc;
@@ -1105,6 +1119,8 @@ int cpr_node_outputs(cpr_batch* b, int64_t n, uint64_t first, const cpr_trace* t
   if (!b || !node_activations || !node_rewards) return fail(CPR_E_INVALID_ARG, "NULL argument");
   if (b->cfg.protocol == CPR_PROTO_FC16)
     return fail(CPR_E_UNSUPPORTED, "FC16 episodes have no network nodes");
+  if (b->cfg.network == CPR_NET_ABSTRACT_GAMMA)
+    return fail(CPR_E_UNSUPPORTED, "the abstract-gamma mode has no exact event engine");
   if (n_nodes != network_nodes(b->cfg))
     return fail(CPR_E_INVALID_ARG, "n_nodes must equal the network's node count");
   const bool nak_fused = b->cfg.protocol == CPR_PROTO_NAKAMOTO && !b->nak_ev;

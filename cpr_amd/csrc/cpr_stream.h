@@ -53,6 +53,13 @@ __host__ __device__ inline Words4 philox4x32_10(uint32_t c0, uint32_t c1, uint32
     c2 = n2;
     k0 += 0x9E3779B9u;
     k1 += 0xBB67AE85u;
+    // recompute the round keys with SALU adds in every call instead of holding twenty
+    // SGPRs across the activation loop (which spills other uniforms to VGPR lanes); only
+    // in translation units whose kernels take one seed for the whole grid
+    // (CPR_UNIFORM_SEED), since the barrier pins the keys to SGPRs
+#if defined(__HIP_DEVICE_COMPILE__) && defined(CPR_UNIFORM_SEED)
+    asm volatile("" : "+s"(k0), "+s"(k1));
+#endif
   }
   return Words4{c0, c1, c2, c3};
 }
@@ -74,6 +81,23 @@ __host__ __device__ inline double cpr_log(double x) {
   const double Lg3 = dbits(0x3FD2492494229359ull), Lg4 = dbits(0x3FCC71C51D8E78AFull);
   const double Lg5 = dbits(0x3FC7466496CB03DEull), Lg6 = dbits(0x3FC39A09D078C69Full);
   const double Lg7 = dbits(0x3FC2F112DF3E5244ull);
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(CPR_NO_CONST_BARRIER)
+  // materialise the constants at each use instead of keeping ten SGPR pairs live across
+  // the activation loop (which spills other uniforms to VGPR lanes)
+  double c_[10] = {ln2_hi, ln2_lo, Lg1, Lg2, Lg3, Lg4, Lg5, Lg6, Lg7, two54};
+#pragma unroll
+  for (int q = 0; q < 10; ++q) asm volatile("" : "+s"(c_[q]));
+#define ln2_hi c_[0]
+#define ln2_lo c_[1]
+#define Lg1 c_[2]
+#define Lg2 c_[3]
+#define Lg3 c_[4]
+#define Lg4 c_[5]
+#define Lg5 c_[6]
+#define Lg6 c_[7]
+#define Lg7 c_[8]
+#define two54 c_[9]
+#endif
   uint64_t ux = bitsd(x);
   int32_t hx = (int32_t)(ux >> 32);
   const uint32_t lx = (uint32_t)ux;
@@ -124,6 +148,18 @@ __host__ __device__ inline double cpr_log(double x) {
   const double lo = dk * ln2_lo;
   const double tail = i > 0 ? hfsq - (s * (hfsq + R) + lo) : s * (f - R) - lo;
   return dk * ln2_hi - (tail - f);
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(CPR_NO_CONST_BARRIER)
+#undef ln2_hi
+#undef ln2_lo
+#undef Lg1
+#undef Lg2
+#undef Lg3
+#undef Lg4
+#undef Lg5
+#undef Lg6
+#undef Lg7
+#undef two54
+#endif
 }
 
 struct Stream {

@@ -7,6 +7,8 @@
 // Episode outcomes are reduced wave-wide with shuffles, then per workgroup in LDS, then
 // one 64-bit atomic per field per workgroup, all in integer arithmetic so totals are
 // independent of scheduling and of how episodes are sharded over GPUs.
+// every kernel of this file takes one seed for the whole grid (cpr_stream.h)
+#define CPR_UNIFORM_SEED 1
 #include <hip/hip_runtime.h>
 
 #include "../../include/cpr_hip.h"
@@ -34,12 +36,24 @@ __device__ inline void acc_add(LdsAcc& a, const BRef& hd, int64_t steps, int64_t
 // One gym episode (engine.ml:164-249): reset = first activation up to the attacker's
 // interaction; step = apply, deliveries, next activation, observe; head at the end.
 template <int POL, class St>
-__device__ inline BRef run_gym(NakLane& L, const NakParams& P, const St& S, const LaneMem& M,
+__device__ inline CPR_AI BRef run_gym(NakLane& L, const NakParams& P, const St& S, const LaneMem& M,
                                int64_t* steps_out) {
   L.init();
   L.activate(P, S, M);
   const bool check_prog = P.max_progress < __builtin_inf();
   int64_t steps = 0;
+  if (!check_prog && !(P.max_time < __builtin_inf())) {
+    // only max_steps ends the episode: the trip count is the same in every lane of the
+    // wave, so the loop exit is uniform and no lane state is merged at a divergent exit
+    do {
+      L.apply(L.policy_action<POL>(P));
+      L.resolve(P, S, M);
+      L.activate(P, S, M);
+      ++steps;
+    } while (steps < P.max_steps);
+    *steps_out = steps;
+    return L.head(P, M);
+  }
   for (;;) {
     const int32_t a = L.policy_action<POL>(P);
     L.apply(a);
@@ -57,7 +71,7 @@ __device__ inline BRef run_gym(NakLane& L, const NakParams& P, const St& S, cons
 // Simulator.loop ~activations with the SSZ attacker as node 0 (simulator.ml:519-533,
 // nakamoto_ssz.ml:262-272); all messages delivered before the head is taken.
 template <int POL, class St>
-__device__ inline BRef run_loop(NakLane& L, const NakParams& P, const St& S, const LaneMem& M,
+__device__ inline CPR_AI BRef run_loop(NakLane& L, const NakParams& P, const St& S, const LaneMem& M,
                                 int64_t activations) {
   L.init();
   for (int64_t i = 0; i < activations; ++i) {
@@ -102,7 +116,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
     const double tm = L.time_of(M, hd);
     const uint32_t status = L.status | Src::missed(S);
     uint32_t st_out = status;
-    if (redo != nullptr && (status & kInexact) != 0u) {
+    if (redo != nullptr && !P.abstract_g && (status & kInexact) != 0u) {
       // the closed form does not hold for this episode: hand it to the exact event engine
       // (k_nak_exact_rerun), which writes its record and summary contribution
       const uint32_t r = atomicAdd(redo_n, 1u);
@@ -111,6 +125,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
         continue;
       }
       st_out |= CPR_ST_CAPACITY;  // queue full: the flagged outputs stay, marked invalid
+    } else if (P.abstract_g && (status & kInexact) != 0u) {
+      st_out |= CPR_ST_CAPACITY;  // the exact event engine has no abstract-gamma mode
     }
     acc_add(acc, hd, steps, L.k, st_out, hist);
     if (recs) {

@@ -30,6 +30,11 @@
 
 namespace cpr {
 
+// Lane methods are inlined into the kernel before any optimisation: optimised on their own,
+// `c ? this->x.f : this->y.f` becomes a load from a selected field address, which keeps
+// the whole lane struct in scratch memory once inlined.
+#define CPR_AI __attribute__((always_inline))
+
 enum : int32_t { A_ADOPT = 0, A_OVERRIDE = 1, A_MATCH = 2, A_WAIT = 3 };
 enum : int32_t { P_HONEST = 0, P_SIMPLE = 1, P_ES2014 = 2, P_SM1 = 3, P_TABLE = 4 };
 enum : uint32_t {
@@ -81,6 +86,16 @@ struct BRef {
   double tm;     // mining time = Simulator.timestamp for these networks (simulator.ml:14-21)
 };
 
+// dst := c ? src : dst, field by field (a whole-struct conditional copy would make the
+// compiler select between the two objects' addresses and put them in scratch memory)
+__host__ __device__ inline CPR_AI void sel(BRef& dst, bool c, const BRef& src) {
+  dst.h = c ? src.h : dst.h;
+  dst.ra = c ? src.ra : dst.ra;
+  dst.k = c ? src.k : dst.k;
+  dst.fork = c ? src.fork : dst.fork;
+  dst.tm = c ? src.tm : dst.tm;
+}
+
 struct NakParams {
   uint64_t t_att;       // floor(alpha * 2^32)
   int32_t d;            // defenders
@@ -95,15 +110,17 @@ struct NakParams {
   int32_t table_dim;
   const uint8_t* table;
   int32_t cap;          // spill slots per lane
+  int32_t abstract_g;   // CPR_NET_ABSTRACT_GAMMA: match races decided by per-defender coins
+  double gamma;         //   U(k, 0, j) < gamma (zero delays otherwise)
 };
 
-__host__ __device__ inline uint64_t all_mask(int32_t d) {
+__host__ __device__ inline CPR_AI uint64_t all_mask(int32_t d) {
   return d >= 64 ? ~0ull : ((1ull << d) - 1ull);
 }
 
 // nakamoto_ssz.ml:274-340 (policy registry: sapirshtein-2016-sm1, eyal-sirer-2014,
 // simple, honest)
-__host__ __device__ inline int32_t nak_policy(int32_t policy, int32_t h, int32_t a, int32_t ev,
+__host__ __device__ inline CPR_AI int32_t nak_policy(int32_t policy, int32_t h, int32_t a, int32_t ev,
                                               const uint8_t* table, int32_t dim) {
   switch (policy) {
     case P_HONEST:
@@ -142,7 +159,7 @@ __host__ __device__ inline int32_t nak_policy(int32_t policy, int32_t h, int32_t
 
 enum : int32_t { RE_SC = 0, RE_SC2 = 1, RE_DAG = 2, RE_MV = 3, RE_ON = 4, RE_MDV = 5, RE_TX = 6, RE_RX = 7 };
 
-__host__ __device__ inline int32_t re_ev(int32_t ty, int32_t node, int32_t x) {
+__host__ __device__ inline CPR_AI int32_t re_ev(int32_t ty, int32_t node, int32_t x) {
   return ty | (node << 3) | (x << 11);
 }
 
@@ -150,7 +167,7 @@ struct SkewHeapLane {
   ReplayNode* n;
   int32_t root, freeh, used;
   bool ok;
-  __host__ __device__ inline int32_t alloc(double t, int32_t ev) {
+  __host__ __device__ inline CPR_AI int32_t alloc(double t, int32_t ev) {
     int32_t i;
     if (freeh >= 0) {
       i = freeh;
@@ -168,7 +185,7 @@ struct SkewHeapLane {
     return i;
   }
   // orderedQueue.ml:17-26, iterative: new equal-time elements sink below existing ones
-  __host__ __device__ inline void push(double t, int32_t ev) {
+  __host__ __device__ inline CPR_AI void push(double t, int32_t ev) {
     int32_t parent = -1;
     int32_t node = root;
     for (;;) {
@@ -197,7 +214,7 @@ struct SkewHeapLane {
     }
   }
   // orderedQueue.ml:28-47 (ties prefer the left subtree)
-  __host__ __device__ inline bool pop(double* t, int32_t* ev) {
+  __host__ __device__ inline CPR_AI bool pop(double* t, int32_t* ev) {
     if (root < 0) return false;
     *t = n[root].t;
     *ev = n[root].ev;
@@ -242,7 +259,7 @@ struct SkewHeapLane {
 // non-miner defenders that end on the released top (first received wins,
 // nakamoto.ml:85-89). *ok = false on capacity overflow.
 template <class St>
-__host__ __device__ inline uint64_t tie_replay(const NakParams& P, const St& S,
+__host__ __device__ inline CPR_AI uint64_t tie_replay(const NakParams& P, const St& S,
                                                const ReplayMem& M, int32_t miner, double t,
                                                int32_t rlo, int32_t rhi, int32_t kw, bool* ok) {
   const int32_t r = rhi - rlo + 1;
@@ -339,24 +356,24 @@ __host__ __device__ inline uint64_t tie_replay(const NakParams& P, const St& S,
 
 struct NakLane {
   double t;          // time of the latest activation (clock.now at the interaction)
-  int32_t k;         // activations so far (clock.c_activations)
+  int32_t k;         // activations so far (clock.c_activations); the same in every lane of
+                     // a wave, so the keyed-stream counter and release keys stay uniform
   int32_t n;         // private blocks above p0 (observable state)
   int32_t rel;       // released prefix of the private chain
   int32_t n_ba;      // private length of the BetweenActions state (attacker's preferred)
   int32_t pend;      // pending private->public message: chain index, -1 = none
   int32_t wminer;    // miner of the current window's activation (0 = attacker)
   int32_t event;     // observation event: 0 ProofOfWork, 1 Network
-  int32_t rlo, rhi;  // chain indices released by the last action
-  int32_t rkw;       // activation count when they were shared (keyed-stream coordinate)
+  int32_t rlo, rhi;  // chain indices released in the current window (shared at count k);
+                     // kept until the next activation, whose overlap check reads them
   uint32_t status;
   BRef p0, pub, D, A, b;
   uint64_t onA;      // bit j-1: defender j prefers A (else D)
   int32_t lca_da;    // height of LCA(D, A)
-  // previous window, for the exact overlap check of the next activation
-  double w_t, w_bound;
-  int32_t w_rlo, w_rhi, w_hasb, w_kw;
+  int32_t w_hasb;    // the window resolved last delivered a defender block
+  double w_bound;    // conservative bound on that window's latest arrival
 
-  __host__ __device__ inline double chain_t(const LaneMem& M, int32_t m) const {
+  __host__ __device__ inline CPR_AI double chain_t(const LaneMem& M, int32_t m) const {
     // two loads in their own address spaces (ds_read, then a rare global load) rather than
     // a select of pointers, which would compile to a generic flat load
     double v = M.ring[(m & (RING - 1)) * M.ring_stride];
@@ -365,38 +382,41 @@ struct NakLane {
     return v;
   }
 
-  __host__ __device__ inline BRef chain_ref(const LaneMem& M, int32_t m) const {
-    if (m <= 0) return p0;
+  // chain block m (m >= 1) of the private chain; p0 for m <= 0
+  __host__ __device__ inline CPR_AI BRef chain_ref(const LaneMem& M, int32_t m) const {
     BRef r;
-    r.h = p0.h + m;
-    r.ra = p0.ra + m;
-    r.k = K_PRIVATE;
-    r.fork = r.h;
-    r.tm = chain_t(M, m);
+    const bool above = m > 0;
+    const int32_t mm = above ? m : 0;
+    r.h = p0.h + mm;
+    r.ra = p0.ra + mm;
+    r.k = above ? K_PRIVATE : p0.k;
+    r.fork = r.h;  // p0.fork == p0.h always (apply sets it on Adopt)
+    r.tm = above ? chain_t(M, m) : p0.tm;
     return r;
   }
 
-  __host__ __device__ inline void init() {
+  __host__ __device__ inline CPR_AI void init() {
     BRef g;
     g.h = 0; g.ra = 0; g.k = K_GENESIS; g.fork = 0; g.tm = 0.0;
     p0 = pub = D = A = b = g;
     t = 0.0;
     k = 0; n = 0; rel = 0; n_ba = 0; pend = -1; wminer = 0; event = 0;
-    rlo = 1; rhi = 0; rkw = 0; status = 0u; onA = 0ull; lca_da = 0;
-    w_t = 0.0; w_bound = -__builtin_inf(); w_rlo = 1; w_rhi = 0; w_hasb = 0; w_kw = 0;
+    rlo = 1; rhi = 0; status = 0u; onA = 0ull; lca_da = 0;
+    w_hasb = 0; w_bound = -__builtin_inf();
   }
 
-  // latest finite arrival of the previous window (exact; only evaluated when the next
-  // activation lands inside the conservative bound, ~1e-9 of activations in the gym)
+  // latest finite arrival of the window resolved last (exact; only evaluated when the next
+  // activation lands inside the conservative bound, ~1e-9 of activations in the gym). Its
+  // coordinates are still live: t and k are the window's, rlo/rhi its release.
   template <class St>
-  __host__ __device__ inline double window_last_arrival(const NakParams& P,
+  __host__ __device__ inline CPR_AI double window_last_arrival(const NakParams& P,
                                                         const St& S) const {
     double last = -__builtin_inf();
-    if (w_hasb && P.d >= 2) last = w_t + P.delta;
-    if (w_rhi >= w_rlo && P.arrive) {
+    if (w_hasb && P.d >= 2) last = t + P.delta;
+    if (rhi >= rlo && P.arrive) {
       for (int32_t j = 1; j <= P.d; ++j)
-        for (int32_t m = w_rlo; m <= w_rhi; ++m) {
-          const double a = w_t + S.link((uint32_t)w_kw, (uint32_t)(w_rhi - m), (uint32_t)j, P.dmax);
+        for (int32_t m = rlo; m <= rhi; ++m) {
+          const double a = t + S.link((uint32_t)k, (uint32_t)(rhi - m), (uint32_t)j, P.dmax);
           last = a > last ? a : last;
         }
     }
@@ -404,9 +424,10 @@ struct NakLane {
   }
 
   // StochasticClock + Dag + the attacker's prepare (simulator.ml:465-480, engine.ml:108-121,
-  // nakamoto_ssz.ml:191-218)
+  // nakamoto_ssz.ml:191-218). Written as selects: the lanes of a wave take different
+  // sides of every decision, so both sides run anyway and the merges cost no copies.
   template <class St>
-  __host__ __device__ inline void activate(const NakParams& P, const St& S, const LaneMem& M) {
+  __host__ __device__ inline CPR_AI void activate(const NakParams& P, const St& S, const LaneMem& M) {
     int32_t miner;
     const double tn = t + S.act((uint32_t)k, P.t_att, P.d, P.ev, &miner);
     if (tn <= w_bound) {
@@ -416,9 +437,12 @@ struct NakLane {
     const int32_t ka = k;
     ++k;
     wminer = miner;
-    // deliver pending releases to the attacker's public model (strict >)
-    if (pend >= 0 && p0.h + pend > pub.h) pub = chain_ref(M, pend);
-    if (miner == 0) {
+    rlo = 1;
+    rhi = 0;
+    // deliver the pending release to the attacker's public model (strict >)
+    sel(pub, pend >= 0 && p0.h + pend > pub.h, chain_ref(M, pend));
+    const bool att = miner == 0;
+    if (att) {
       int32_t m = n + 1;
       if (m >= M.cap) {
         status |= ST_DEEP_FORK;
@@ -428,22 +452,19 @@ struct NakLane {
       if (m > RING) M.spill[(int64_t)(m - RING) * M.spill_stride] = *slot;  // evict
       *slot = tn;
       n = m;
-      event = 0;
-    } else {
-      const BRef par = ((onA >> (miner - 1)) & 1ull) ? A : D;
-      b.h = par.h + 1;
-      b.ra = par.ra;
-      b.k = ka;
-      b.fork = par.fork;
-      b.tm = tn;
-      if (b.h > pub.h) pub = b;
-      event = 1;
     }
-    rlo = 1;
-    rhi = 0;
+    // the defender block (its fields are meaningless when the attacker mined)
+    const bool par_a = ((onA >> ((miner - 1) & 63)) & 1ull) != 0ull;
+    b.h = (par_a ? A.h : D.h) + 1;
+    b.ra = par_a ? A.ra : D.ra;
+    b.fork = par_a ? A.fork : D.fork;
+    b.k = ka;
+    b.tm = tn;
+    sel(pub, !att && b.h > pub.h, b);
+    event = att ? 0 : 1;
   }
 
-  __host__ __device__ inline void observe(int32_t* pub_blocks, int32_t* priv_blocks,
+  __host__ __device__ inline CPR_AI void observe(int32_t* pub_blocks, int32_t* priv_blocks,
                                           int32_t* diff_blocks, int32_t* ev) const {
     const int32_t ca = pub.fork;
     const int32_t ph = p0.h + n;
@@ -453,152 +474,129 @@ struct NakLane {
     *ev = event;
   }
 
-  // Agent.apply (nakamoto_ssz.ml:232-260) + Simulator.handle_action share (:401-419)
-  __host__ __device__ inline void apply(int32_t action) {
-    if (action == A_ADOPT) {
-      const bool pub_on_chain = pub.fork == pub.h;
-      if (wminer != 0 && pub.k == b.k) {
-        b.fork = b.h;  // new private chain = ancestry of the fresh defender block
-      } else if (pub_on_chain) {
-        const int32_t hp = pub.h;
-        D.fork = D.fork < hp ? D.fork : hp;
-        A.fork = A.fork < hp ? A.fork : hp;
-        b.fork = b.fork < hp ? b.fork : hp;
-      } else {  // pub is the off-chain defender tip D
-        D.fork = D.h;
-        A.fork = lca_da;
-      }
-      p0 = pub;
-      p0.fork = p0.h;
-      pub.fork = pub.h;
-      n = 0;
-      rel = 0;
-      pend = -1;
-      n_ba = 0;
-      return;
-    }
-    if (action == A_MATCH || action == A_OVERRIDE) {
-      const int32_t target = pub.h + (action == A_OVERRIDE ? 1 : 0);
-      int32_t mf = target - p0.h;
-      mf = mf < 0 ? 0 : (mf > n ? n : mf);
-      if (mf > rel) {
-        rlo = rel + 1;
-        rhi = mf;
-        rkw = k;
-        rel = mf;
-      }
-      pend = mf;
-      n_ba = n;
-      return;
-    }
-    pend = -1;  // Wait (and any out-of-range action is rejected by the host)
-    n_ba = n;
+  // Agent.apply (nakamoto_ssz.ml:232-260) + Simulator.handle_action share (:401-419).
+  // Adopt: private := public (forks of the defender tips move to the new base); Match /
+  // Override: release up to the public height (+1); Wait (and any out-of-range action,
+  // rejected by the host) shares nothing.
+  __host__ __device__ inline CPR_AI void apply(int32_t action) {
+    const bool adopt = action == A_ADOPT;
+    const bool relx = action == A_MATCH || action == A_OVERRIDE;
+    const int32_t hp = pub.h;
+    const bool fresh = wminer != 0 && pub.k == b.k;  // pub is this window's defender block
+    const bool onch = pub.fork == hp;                // pub lies on the private chain
+    const int32_t bf = fresh ? b.h : (onch ? (b.fork < hp ? b.fork : hp) : b.fork);
+    const int32_t df = fresh ? D.fork : (onch ? (D.fork < hp ? D.fork : hp) : D.h);
+    const int32_t af = fresh ? A.fork : (onch ? (A.fork < hp ? A.fork : hp) : lca_da);
+    const int32_t target = hp + (action == A_OVERRIDE ? 1 : 0);
+    int32_t mf = target - p0.h;
+    mf = mf < 0 ? 0 : (mf > n ? n : mf);
+    const bool newrel = relx && mf > rel;
+    rlo = newrel ? rel + 1 : rlo;
+    rhi = newrel ? mf : rhi;
+    rel = adopt ? 0 : (newrel ? mf : rel);
+    pend = relx ? mf : -1;
+    n_ba = adopt ? 0 : n;
+    n = adopt ? 0 : n;
+    b.fork = adopt ? bf : b.fork;
+    D.fork = adopt ? df : D.fork;
+    A.fork = adopt ? af : A.fork;
+    BRef np = pub;  // value copy: the select below picks values, not field addresses
+    np.fork = hp;
+    sel(p0, adopt, np);
+    pub.fork = adopt ? hp : pub.fork;
   }
 
   // deliveries of the window: the fresh defender block and the attacker's release reach
   // the defenders (simulator.ml:481-508 with update_head, nakamoto.ml:85-89)
   template <class St>
-  __host__ __device__ inline void resolve(const NakParams& P, const St& S, const LaneMem& M) {
+  __host__ __device__ inline CPR_AI void resolve(const NakParams& P, const St& S, const LaneMem& M) {
     const bool released = rhi >= rlo && P.arrive;
     const uint64_t all = all_mask(P.d);
-    double bound = -__builtin_inf();
-    if (wminer != 0) {
-      if (P.d >= 2) bound = t + P.delta;
-      if (released) {
-        const int32_t xh = p0.h + rhi;
-        if (xh > b.h) {
-          A = chain_ref(M, rhi);
-          onA = all;
-          lca_da = b.fork;
-        } else if (xh == b.h) {
-          // race at every defender except the miner: first visible wins
-          const double tb = t + P.delta;
-          uint64_t mask = 0ull;
-          bool tie = false;
-          for (int32_t j = 1; j <= P.d; ++j) {
-            if (j == wminer) continue;
-            double v = -__builtin_inf();
-            for (int32_t m = rlo; m <= rhi; ++m) {
-              const double a = t + S.link((uint32_t)rkw, (uint32_t)(rhi - m), (uint32_t)j, P.dmax);
-              v = a > v ? a : v;
-            }
-            if (v < tb) mask |= 1ull << (j - 1);
-            tie |= v == tb;
-          }
-          if (tie) {
-            // same instant at some defender: the queue order decides
-            status |= ST_TIE;
-            bool ok = false;
-            const uint64_t exact = tie_replay(P, S, M.replay, wminer, t, rlo, rhi, rkw, &ok);
-            if (ok)
-              mask = exact;
-            else
-              status |= ST_TIE_UNRESOLVED;
-          }
-          A = chain_ref(M, rhi);
-          onA = mask;
-          lca_da = b.fork;
-        } else {
-          onA = 0ull;
+    const bool dm = wminer != 0;
+    const int32_t xh = p0.h + rhi;
+    const int32_t hs = onA ? A.h : D.h;
+    const int32_t lca_new = dm ? b.fork : D.fork;  // read before the race block splits this
+    const bool newA = released && (dm ? xh >= b.h : xh > hs);
+    uint64_t mask = all;
+    if (released && dm && xh == b.h && P.abstract_g) {
+      // flagged abstract-gamma mode: each defender, the miner included, mines on the
+      // released block iff its coin falls below gamma (Eyal-Sirer'14's gamma)
+      mask = 0ull;
+      for (int32_t j = 1; j <= P.d; ++j)
+        mask |= S.link((uint32_t)k, 0u, (uint32_t)j, 1.0) < P.gamma ? 1ull << (j - 1) : 0ull;
+    } else if (released && dm && xh == b.h) {
+      // race at every defender except the miner: first visible wins. One link draw per
+      // (non-miner defender, released block); the defender index is per lane.
+      const double tb = t + P.delta;
+      mask = 0ull;
+      bool tie = false;
+      for (int32_t i = 0; i < P.d - 1; ++i) {
+        const int32_t j = i + (i + 1 >= wminer ? 2 : 1);
+        double v = -__builtin_inf();
+        for (int32_t m = rlo; m <= rhi; ++m) {
+          const double a = t + S.link((uint32_t)k, (uint32_t)(rhi - m), (uint32_t)j, P.dmax);
+          v = a > v ? a : v;
         }
-        D = b;
-      } else {
-        D = b;
-        onA = 0ull;
+        mask |= v < tb ? 1ull << (j - 1) : 0ull;
+        tie |= v == tb;
       }
-    } else if (released) {
-      const int32_t hs = onA ? A.h : D.h;
-      if (p0.h + rhi > hs) {
-        lca_da = D.fork;
-        A = chain_ref(M, rhi);
-        onA = all;
+      if (tie) {
+        // same instant at some defender: the queue order decides
+        status |= ST_TIE;
+        bool ok = false;
+        const uint64_t exact = tie_replay(P, S, M.replay, wminer, t, rlo, rhi, k, &ok);
+        if (ok)
+          mask = exact;
+        else
+          status |= ST_TIE_UNRESOLVED;
       }
     }
+    sel(A, newA, chain_ref(M, rhi));
+    lca_da = newA ? lca_new : lca_da;
+    onA = dm ? (newA ? mask : 0ull) : (newA ? all : onA);
+    sel(D, dm, b);
+    double bound = dm && P.d >= 2 ? t + P.delta : -__builtin_inf();
     if (released) {
       const double ub = t + (P.dmax - 0.0);
       bound = ub > bound ? ub : bound;
     }
-    w_t = t;
     w_bound = bound;
-    w_rlo = rlo;
-    w_rhi = released ? rhi : 0;
-    w_kw = rkw;
-    w_hasb = wminer != 0;
+    w_hasb = dm ? 1 : 0;
     wminer = 0;
-    rlo = 1;
-    rhi = 0;
   }
 
   // Ref.winner over [attacker preferred; defender tips 1..d] (engine.ml:195-206,
   // nakamoto.ml:43-48): first maximal height, attacker listed first
-  __host__ __device__ inline BRef head(const NakParams& P, const LaneMem& M) const {
+  __host__ __device__ inline CPR_AI BRef head(const NakParams& P, const LaneMem& M) const {
     BRef best = chain_ref(M, n_ba);
     const uint64_t all = all_mask(P.d);
     const uint64_t mb = wminer ? (1ull << (wminer - 1)) : 0ull;
     const uint64_t ma = onA & ~mb;
     const uint64_t md = all & ~onA & ~mb;
-    int32_t bh = -1, bj = 1 << 30;
-    BRef cand = best;
-    if (wminer) { bh = b.h; bj = wminer; cand = b; }
-    if (ma) {
-      const int32_t j = 1 + __builtin_ctzll(ma);
-      if (A.h > bh || (A.h == bh && j < bj)) { bh = A.h; bj = j; cand = A; }
-    }
-    if (md) {
-      const int32_t j = 1 + __builtin_ctzll(md);
-      if (D.h > bh || (D.h == bh && j < bj)) { bh = D.h; bj = j; cand = D; }
-    }
-    if (bh > best.h) best = cand;
+    // candidates in node order: the miner of b holds b, the first defender on A holds A,
+    // the first on D holds D; the first maximal height wins (fold keeps earlier on ties)
+    const int32_t ja = ma ? 1 + __builtin_ctzll(ma) : (1 << 30);
+    const int32_t jd = md ? 1 + __builtin_ctzll(md) : (1 << 30);
+    int32_t bh = wminer ? b.h : -1, bj = wminer ? wminer : (1 << 30);
+    BRef cand = b;
+    const bool ta = ma && (A.h > bh || (A.h == bh && ja < bj));
+    sel(cand, ta, A);
+    bh = ta ? A.h : bh;
+    bj = ta ? ja : bj;
+    const bool td = md && (D.h > bh || (D.h == bh && jd < bj));
+    sel(cand, td, D);
+    bh = td ? D.h : bh;
+    sel(best, bh > best.h, cand);
     return best;
   }
 
   // Simulator.timestamp of a block = its mining time for these networks
-  __host__ __device__ inline double time_of(const LaneMem&, const BRef& x) const { return x.tm; }
+  __host__ __device__ inline CPR_AI double time_of(const LaneMem&, const BRef& x) const { return x.tm; }
 
   // POL >= 0: the policy fixed at compile time (the fused kernel's specialisations), so
   // the policy switch and its table operands disappear from the activation loop
   template <int POL = -1>
-  __host__ __device__ inline int32_t policy_action(const NakParams& P) const {
+  __host__ __device__ inline CPR_AI int32_t policy_action(const NakParams& P) const {
     int32_t h, a, dd, ev;
     observe(&h, &a, &dd, &ev);
     return nak_policy(POL >= 0 ? POL : P.policy, h, a, ev, P.table, P.table_dim);
@@ -607,7 +605,7 @@ struct NakLane {
 
 // miner of activation index ka (for head_miner of the record)
 template <class St>
-__host__ __device__ inline int32_t miner_of(const NakParams& P, const St& S, int32_t ka) {
+__host__ __device__ inline CPR_AI int32_t miner_of(const NakParams& P, const St& S, int32_t ka) {
   if (ka == K_PRIVATE) return 0;
   if (ka < 0) return -1;
   return S.miner((uint32_t)ka, P.t_att, P.d);

@@ -88,8 +88,9 @@ struct TsParams {
   int32_t table_dim;
 };
 
-constexpr int32_t NQS = 2048;    // votes of one summary tree handled at once (a withheld
-                                  // tree on configs[3] exceeded 512)
+constexpr int32_t NQS = 512;     // votes of one summary tree handled at once; a larger
+                                  // withheld tree flags CPR_ST_CAPACITY (its quadratic
+                                  // tree scans would stall the wave for minutes)
 constexpr int32_t NSTACK = 1024; // share stack
 constexpr int32_t NPEND = 1024;  // pending released messages
 constexpr int32_t NFR = 64;      // common-ancestor frontier

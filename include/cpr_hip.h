@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define CPR_ABI_VERSION 7
+#define CPR_ABI_VERSION 8
 
 typedef struct cpr_ctx cpr_ctx;
 typedef struct cpr_batch cpr_batch;
@@ -146,11 +146,20 @@ enum cpr_network {
                                  = n honest nodes (2..64), node i has compute i + 1, every
                                  link delay uniform [delay_lo, delay_hi), simple
                                  dissemination; CPR_MODE_LOOP, Nakamoto or Ethereum */
-  CPR_NET_EXP_CLIQUE = 3      /* Network.T.symmetric_clique with exponential propagation
+  CPR_NET_EXP_CLIQUE = 3,     /* Network.T.symmetric_clique with exponential propagation
                                  (cpr_protocols.ml:200-210,478-485): node 0 (the attacker,
                                  running cfg.policy) plus `defenders` honest nodes (1..63),
                                  equal compute, every link delay exponential with mean
                                  propagation_delay; CPR_MODE_LOOP, B_k or Tailstorm */
+  CPR_NET_ABSTRACT_GAMMA = 4  /* FLAGGED abstract-gamma mode (not a network
+                                 of the reference, which rejects gamma = 1, envs.py:73-75):
+                                 the gym's attacker + `defenders` equal-compute honest nodes
+                                 with zero propagation delays, where a release that ties the
+                                 window's fresh defender block wins at each defender, its
+                                 miner included, iff that defender's coin
+                                 U(k, 0, j) < gamma (Eyal-Sirer'14 gamma, exact for any
+                                 gamma in [0, 1]); every other tie keeps the first-received
+                                 block. Nakamoto, CPR_MODE_GYM; no replay, no node outputs */
 };
 
 enum cpr_mode {

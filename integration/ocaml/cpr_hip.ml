@@ -1,4 +1,4 @@
-(* OCaml ctypes bindings of libcpr_hip (include/cpr_hip.h, CPR_ABI_VERSION 7).
+(* OCaml ctypes bindings of libcpr_hip (include/cpr_hip.h, CPR_ABI_VERSION 8).
 
    For a host that has OCaml: dropped next to the reference's gym engine
    (simulator/gym/), it lets Hip_engine.of_module (hip_engine.ml) stand in for
@@ -12,7 +12,7 @@
 open Ctypes
 open Foreign
 
-let abi_version = 7
+let abi_version = 8
 
 (* ---- status codes and enums (cpr_status, cpr_protocol, cpr_network, cpr_mode) *)
 let ok = 0
@@ -29,6 +29,8 @@ let proto_fc16 = 4l
 let net_selfish_mining = 0l
 let net_two_agents = 1l
 let net_honest_clique = 2l
+let net_exp_clique = 3l
+let net_abstract_gamma = 4l (* flagged abstract-gamma mode, not a reference network *)
 let mode_gym = 0l
 let mode_loop = 1l
 

@@ -308,6 +308,7 @@ struct RecordingSimRng : SimRng {
     if (l.kind != D_CONST) buf->link[msg_key_of(l, m, serial_links)] = x;
     return x;
   }
+  double coin(int kw, int j) override { return inner->coin(kw, j); }
 };
 
 struct ReplaySimRng : SimRng {
@@ -693,7 +694,16 @@ Action NakHonest::handler(Kind k, Block* v) {
   switch (k) {
     case K_APPEND: throw std::runtime_error("not implemented");
     case K_NETWORK:
-      if (v->value.height > state->value.height) state = v;
+      if (v->value.height > state->value.height) {
+        state = v;
+      } else if (abstract_gamma >= 0.0 && v != state && v->value.height == state->value.height) {
+        // abstract-gamma match race: the attacker's release against the defender block
+        // mined at this very instant, in either arrival order; the coin decides
+        Block* att = v->value.miner == 0 ? v : (state->value.miner == 0 ? state : nullptr);
+        Block* def = att == v ? state : v;
+        if (att && def->value.miner >= 1 && def->vis[def->value.miner].time == sim->now)
+          state = sim->rng->coin(att->share_k, id) < abstract_gamma ? att : def;
+      }
       return a;
     case K_POW:
       state = v;
@@ -875,6 +885,18 @@ GymNakamoto::GymNakamoto(const GymParams& p_, int mode, OcamlRandom* oc, uint64_
     : p(p_), rng_mode(mode), ocaml(oc), seed(seed_), episode(ep) {
   std::string e = gym_params_error(p);
   if (!e.empty()) throw std::invalid_argument(e);
+  if (p.abstract_gamma) {
+    // flagged abstract-gamma mode: the gym's nodes and compute, every link delay zero
+    net = Network{};
+    net.activation_delay = p.activation_delay;
+    net.nodes.resize(p.defenders + 1);
+    net.nodes[0].compute = p.alpha;
+    for (int i = 1; i <= p.defenders; ++i) net.nodes[i].compute = (1. - p.alpha) / p.defenders;
+    for (int i = 0; i <= p.defenders; ++i)
+      for (int j = 0; j <= p.defenders; ++j)
+        if (j != i) net.nodes[i].links.push_back(Link{j, D_CONST, 0.0, 0.0});
+    return;
+  }
   // engine.ml:100-107
   net = Network::selfish_mining(p.alpha, p.activation_delay, p.gamma, p.propagation_delay,
                                 p.defenders);
@@ -923,8 +945,11 @@ void GymNakamoto::init() {
     for (int i = 0; i < n; i++) {
       if (i == 0)
         static_cast<DummyNode*>(sim->nodes[0].get())->state = root;
-      else
-        static_cast<NakHonest*>(sim->nodes[i].get())->state = root;
+      else {
+        auto* h = static_cast<NakHonest*>(sim->nodes[i].get());
+        h->state = root;
+        if (p.abstract_gamma) h->abstract_gamma = p.gamma;
+      }
     }
   }
   agent = NakSszAgent();

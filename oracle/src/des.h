@@ -17,6 +17,7 @@
 #include <cstdint>
 #include <map>
 #include <memory>
+#include <stdexcept>
 #include <string>
 #include <vector>
 
@@ -140,6 +141,13 @@ struct SimRng {
   virtual double act_delay(int j) = 0;
   virtual int32_t pow_bits(int serial) = 0;
   virtual double link_delay(const Link& l, const Block* msg) = 0;
+  // abstract-gamma coin of defender j for the release shared at activation count kw
+  // (CPR_NET_ABSTRACT_GAMMA; keyed stream only)
+  virtual double coin(int kw, int j) {
+    (void)kw;
+    (void)j;
+    throw std::runtime_error("abstract-gamma coins need the keyed stream");
+  }
 };
 
 // OCaml Random: alias sampling exactly as distributions.ml:45-98
@@ -168,6 +176,7 @@ struct KeyedSimRng : SimRng {
   double act_delay(int j) override;
   int32_t pow_bits(int serial) override;
   double link_delay(const Link& l, const Block* msg) override;
+  double coin(int kw, int j) override { return ks.link_u((uint32_t)kw, 0u, (uint32_t)j); }
 };
 
 // keyed miner draw by general weights iff the compute is not [alpha] + equal defenders
@@ -290,6 +299,9 @@ Block* common_ancestor(const Sim& sim, int view, Block* a, Block* b);
 
 struct NakHonest : NodeImpl {
   Block* state = nullptr;
+  // CPR_NET_ABSTRACT_GAMMA (not the reference; a flagged mode of the build): a release by
+  // node 0 that ties a defender block mined at this instant wins iff coin < abstract_gamma
+  double abstract_gamma = -1.0;
   Draft puzzle_payload() override;
   Action handler(Kind k, Block* b) override;
   Block* preferred() override { return state; }
@@ -360,6 +372,9 @@ struct GymParams {
   // defender<->defender delay of Network.T.selfish_mining; the gym passes 1e-9
   // (engine.ml:100-107), other values exercise overlapping delivery windows in tests
   double propagation_delay = 1e-9;
+  // flagged abstract-gamma mode (include/cpr_hip.h CPR_NET_ABSTRACT_GAMMA): zero delays,
+  // match races decided by per-defender coins < gamma
+  bool abstract_gamma = false;
 };
 
 struct StepInfo {

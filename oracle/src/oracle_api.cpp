@@ -254,6 +254,7 @@ static GymParams params_of(const cpr_config* c) {
   p.max_time = c->max_time > 0 ? c->max_time : 1.0 / 0.0;
   p.unit_obs = c->unit_observation != 0;
   if (c->propagation_delay > 0) p.propagation_delay = c->propagation_delay;
+  p.abstract_gamma = c->network == CPR_NET_ABSTRACT_GAMMA;
   return p;
 }
 

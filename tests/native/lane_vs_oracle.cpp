@@ -28,7 +28,8 @@ struct Cfg {
   int defenders;
   int policy;  // 0..3, 5 = random actions, 6 = random with bias to match
   int steps;
-  int two_agents;  // loop mode on the two-agents network
+  int two_agents;  // 1: loop mode on the two-agents network; 2: gym episodes in the flagged
+                   // abstract-gamma mode (CPR_NET_ABSTRACT_GAMMA)
 };
 
 // host stand-in for the kernel's per-lane memory (ring, spill, replay scratch)
@@ -62,6 +63,7 @@ static bool run_gym(const Cfg& cf, uint64_t seed, uint64_t ep, Counters& C, std:
   gp.defenders = cf.defenders;
   gp.max_steps = cf.steps;
   gp.unit_obs = false;
+  gp.abstract_gamma = cf.two_agents == 2;
   oracle::GymNakamoto g(gp, 1, nullptr, seed, ep);
   double obs[4];
   g.reset(obs);
@@ -74,6 +76,13 @@ static bool run_gym(const Cfg& cf, uint64_t seed, uint64_t ep, Counters& C, std:
   const double dd = cf.defenders;
   P.dmax = (dd - 1.) / dd * 1e-9 / cf.gamma;
   P.arrive = std::isfinite(P.dmax) ? 1 : 0;
+  if (cf.two_agents == 2) {  // as capi.hip validate for CPR_NET_ABSTRACT_GAMMA
+    P.delta = 0.0;
+    P.dmax = 0.0;
+    P.arrive = 1;
+    P.abstract_g = 1;
+    P.gamma = cf.gamma;
+  }
   P.max_steps = cf.steps;
   P.max_progress = __builtin_inf();
   P.max_time = __builtin_inf();
@@ -203,12 +212,17 @@ int main(int argc, char** argv) {
   cfgs.push_back(Cfg{0.3, 0.7, 5, 5, steps, 0});
   for (double a : alphas)
     for (int pol : {0, 1, 2, 3}) cfgs.push_back(Cfg{a, 0, 1, pol, steps * 4, 1});
+  // flagged abstract-gamma mode: gamma 0 .. 1 incl. the reference-rejected gamma = 1
+  for (double a : alphas)
+    for (double g : {0.0, 0.5, 0.9, 1.0})
+      for (int d : {1, 2, 5})
+        for (int pol : {2, 3, 6}) cfgs.push_back(Cfg{a, g, d, pol, steps, 2});
   Counters C;
   int shown = 0;
   for (auto& cf : cfgs)
     for (int e = 0; e < eps; e++) {
       std::string why;
-      bool ok = cf.two_agents ? run_loop(cf, seed, e, C, why) : run_gym(cf, seed, e, C, why);
+      bool ok = cf.two_agents == 1 ? run_loop(cf, seed, e, C, why) : run_gym(cf, seed, e, C, why);
       if (!ok && shown < 12) {
         shown++;
         fprintf(stderr, "MISMATCH alpha=%g gamma=%g d=%d pol=%d two=%d ep=%d: %s\n", cf.alpha,

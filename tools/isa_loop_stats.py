@@ -77,7 +77,7 @@ def main():
         if m:
             depth[lab] = int(m.group(1))
     hdr2 = [h for h, d in depth.items() if d == 2]
-    body = collections.Counter()
+    per = {h: collections.Counter() for h in hdr2}
     nested = collections.Counter()
     for lab, ann, ins in blocks:
         if lab in depth:
@@ -85,9 +85,19 @@ def main():
         else:
             m = re.search(r"in Loop: Header=(BB\d+_\d+)", ann)
             loop = m.group(1) if m else None
-        tgt = body if loop in hdr2 else (nested if depth.get(loop, 0) > 2 else None)
-        if tgt is not None:
-            tgt.update(ins)
+        if loop in per:
+            per[loop].update(ins)
+        elif loop is not None and depth.get(loop, 0) > 2:
+            nested.update(ins)
+    # the activation loop: the depth-2 loop with the most Philox multiplies (several
+    # depth-2 loops exist when run_gym has a uniform and a general variant; report the
+    # largest, which the bench's configuration runs)
+    for h, c in sorted(per.items(), key=lambda x: -sum(v for o, v in x[1].items()
+                                                       if o.startswith("v_"))):
+        print(f" depth-2 loop {h}: VALU {sum(v for o, v in c.items() if o.startswith('v_'))}")
+    # the first depth-2 loop in block order is run_gym's uniform-trip-count loop (the
+    # configuration the bench runs: only max_steps ends an episode)
+    body = per[hdr2[0]] if hdr2 else collections.Counter()
     v = sum(c for o, c in body.items() if o.startswith("v_"))
     s = sum(c for o, c in body.items() if o.startswith("s_"))
     mov = sum(c for o, c in body.items() if o.startswith("v_mov"))
