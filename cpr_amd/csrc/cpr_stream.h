@@ -130,7 +130,20 @@ __host__ __device__ inline double cpr_log(double x) {
     dk = (double)k;
     return dk * ln2_hi - ((R - dk * ln2_lo) - f);
   }
+#if defined(__HIP_DEVICE_COMPILE__)
+  // f / (2 + f) as the compiler's own IEEE division expansion minus v_div_scale and
+  // v_div_fixup: here f in [sqrt(2)/2 - 1, sqrt(2) - 1) and 2 + f in [1.7, 2.5), so
+  // div_scale would return its operands unchanged (vcc = 0, div_fmas = fma) and div_fixup
+  // its quotient: the same bits, three instructions fewer
+  const double dd2 = 2.0 + f;
+  double rr = __builtin_amdgcn_rcp(dd2);
+  rr = __builtin_fma(rr, __builtin_fma(-dd2, rr, 1.0), rr);
+  rr = __builtin_fma(rr, __builtin_fma(-dd2, rr, 1.0), rr);
+  const double qq = f * rr;
+  const double s = __builtin_fma(__builtin_fma(-dd2, qq, f), rr, qq);
+#else
   const double s = f / (2.0 + f);
+#endif
   dk = (double)k;
   const double z = s * s;
   i = hx - 0x6147a;

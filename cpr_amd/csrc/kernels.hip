@@ -47,7 +47,7 @@ __device__ inline CPR_AI BRef run_gym(NakLane& L, const NakParams& P, const St& 
     // wave, so the loop exit is uniform and no lane state is merged at a divergent exit
     do {
       L.apply(L.policy_action<POL>(P));
-      L.resolve(P, S, M);
+      L.resolve<St, POL >= 0 ? 0 : -1>(P, S, M);
       L.activate(P, S, M);
       ++steps;
     } while (steps < P.max_steps);
@@ -57,7 +57,7 @@ __device__ inline CPR_AI BRef run_gym(NakLane& L, const NakParams& P, const St& 
   for (;;) {
     const int32_t a = L.policy_action<POL>(P);
     L.apply(a);
-    L.resolve(P, S, M);
+    L.resolve<St, POL >= 0 ? 0 : -1>(P, S, M);
     L.activate(P, S, M);
     ++steps;
     bool go = steps < P.max_steps && L.t < P.max_time;
@@ -85,7 +85,8 @@ __device__ inline CPR_AI BRef run_loop(NakLane& L, const NakParams& P, const St&
 // lane status bits whose episodes the closed form cannot vouch for
 constexpr uint32_t kInexact = ST_OVERLAP | ST_DEEP_FORK | ST_TIE_UNRESOLVED | ST_STALE_TIME;
 
-// POL: nakamoto_ssz policy fixed at compile time (P_HONEST .. P_SM1), or -1 for P.policy
+// POL: nakamoto_ssz policy fixed at compile time (P_HONEST .. P_SM1; these kernels never
+// run the abstract-gamma mode), or -1 for P.policy (and P.abstract_g)
 template <int MODE, class Src, int POL>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) void k_run_episodes(
     NakParams P, Src src, int64_t n_eps, int64_t activations,
@@ -301,7 +302,9 @@ hipError_t launch_run_episodes(const NakParams& P, uint64_t seed, uint64_t first
   hipLaunchKernelGGL((k_run_episodes<MODE, SeedSource, POL>), dim3(blocks), dim3(kBlock), 0, st, \
                      P, src, n_eps, activations, spill, replay, recs, sum, redo, redo_n,         \
                      launch_id, redo_cap)
-  if (mode == CPR_MODE_GYM) {
+  if (mode == CPR_MODE_GYM && P.abstract_g) {
+    CPR_LAUNCH(CPR_MODE_GYM, -1);  // flagged abstract-gamma mode: the generic kernel
+  } else if (mode == CPR_MODE_GYM) {
     switch (P.policy) {  // the built-in policies get their own specialisation
       case P_HONEST: CPR_LAUNCH(CPR_MODE_GYM, P_HONEST); break;
       case P_SIMPLE: CPR_LAUNCH(CPR_MODE_GYM, P_SIMPLE); break;

@@ -508,7 +508,8 @@ struct NakLane {
 
   // deliveries of the window: the fresh defender block and the attacker's release reach
   // the defenders (simulator.ml:481-508 with update_head, nakamoto.ml:85-89)
-  template <class St>
+  // AG: the abstract-gamma rule fixed at compile time (0 off, 1 on) or read from P (-1)
+  template <class St, int AG = -1>
   __host__ __device__ inline CPR_AI void resolve(const NakParams& P, const St& S, const LaneMem& M) {
     const bool released = rhi >= rlo && P.arrive;
     const uint64_t all = all_mask(P.d);
@@ -518,7 +519,8 @@ struct NakLane {
     const int32_t lca_new = dm ? b.fork : D.fork;  // read before the race block splits this
     const bool newA = released && (dm ? xh >= b.h : xh > hs);
     uint64_t mask = all;
-    if (released && dm && xh == b.h && P.abstract_g) {
+    const bool abstract_g = AG >= 0 ? AG != 0 : P.abstract_g != 0;
+    if (released && dm && xh == b.h && abstract_g) {
       // flagged abstract-gamma mode: each defender, the miner included, mines on the
       // released block iff its coin falls below gamma (Eyal-Sirer'14's gamma)
       mask = 0ull;

@@ -1,0 +1,65 @@
+"""Timing probes for k_run_episodes (not product code): build libcpr_hip variants whose
+kernels.hip translation unit has one cost centre replaced by a trivial stand-in, so one
+GPU call can time each (tools/nak_probe_ab.sh). The stand-ins break the keyed stream, so
+the variants' results are meaningless; only their kernel times are read.
+
+  cheap_rng : Philox4x32-10 -> two multiply-xorshift rounds
+  cheap_log : fdlibm cpr_log -> (x - 1) (a negative number, so delays stay positive)
+  cheap_both: both
+  base      : the tree as it is
+
+usage: python tools/nak_probe_variants.py   (writes build/var/<name>.so)
+"""
+import pathlib
+import shutil
+import subprocess
+import sys
+
+ROOT = pathlib.Path(__file__).resolve().parent.parent
+CSRC = ROOT / "cpr_amd" / "csrc"
+OUT = ROOT / "build" / "var"
+
+PHILOX_OLD = "#pragma unroll\n  for (int r = 0; r < 10; ++r) {"
+PHILOX_NEW = """#if 1  // probe: cheap stand-in
+  {
+    uint32_t h = c0 * 0x9E3779B9u ^ c1 * 0x85EBCA6Bu ^ c2 * 0xC2B2AE35u ^ c3 ^ k0 ^ k1;
+    h ^= h >> 15; h *= 0x2C1B3C6Du; h ^= h >> 12;
+    return Words4{h, h * 0x297A2D39u, h ^ 0x5BD1E995u, (h >> 7) * 0x68E31DA4u};
+  }
+#endif
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {"""
+LOG_OLD = "__host__ __device__ inline double cpr_log(double x) {"
+LOG_NEW = LOG_OLD + "\n  return x - 1.0;  // probe: cheap stand-in"
+
+
+def variant(name, rng, log):
+    d = ROOT / "cpr_amd" / ("csrc_probe_" + name)  # same depth: ../../include resolves
+    if d.exists():
+        shutil.rmtree(d)
+    shutil.copytree(CSRC, d)
+    st = (d / "cpr_stream.h").read_text()
+    if rng:
+        assert PHILOX_OLD in st
+        st = st.replace(PHILOX_OLD, PHILOX_NEW, 1)
+    if log:
+        assert LOG_OLD in st
+        st = st.replace(LOG_OLD, LOG_NEW, 1)
+    (d / "cpr_stream.h").write_text(st)
+    obj = OUT / f"kernels_{name}.o"
+    subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17",
+                    "-ffp-contract=off", "-fPIC", f"-I{ROOT / 'include'}", "-c",
+                    str(d / "kernels.hip"), "-o", str(obj)], check=True)
+    objs = [str(obj)] + [str(p) for p in sorted((ROOT / "build" / "hip").glob("*.o"))
+                         if p.name != "kernels.hip.o"]
+    subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-shared", "-fPIC", *objs,
+                    "-o", str(OUT / f"{name}.so")], check=True)
+    shutil.rmtree(d)
+
+
+if __name__ == "__main__":
+    OUT.mkdir(parents=True, exist_ok=True)
+    names = sys.argv[1:] or ["base", "cheap_rng", "cheap_log", "cheap_both"]
+    for n in names:
+        variant(n, "rng" in n or "both" in n, "log" in n or "both" in n)
+        print("built", OUT / f"{n}.so")
