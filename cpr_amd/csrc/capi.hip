@@ -209,7 +209,7 @@ static int validate_ts(const cpr_config* c, ts::TsParams* P);
 // the same engine episode by episode anyway
 static bool nak_on_event_engine(const cpr_config* c) {
   if (c->protocol != CPR_PROTO_NAKAMOTO) return false;
-  if (c->network == CPR_NET_HONEST_CLIQUE) return true;
+  if (c->network == CPR_NET_HONEST_CLIQUE || c->network == CPR_NET_EXP_CLIQUE) return true;
   if (c->network != CPR_NET_SELFISH_MINING || c->mode != CPR_MODE_LOOP) return false;
   if (c->gamma == 0.0) return true;
   const double prop = c->propagation_delay > 0 ? c->propagation_delay : 1e-9;
@@ -415,6 +415,20 @@ static int validate_eth(const cpr_config* c, eth::EthParams* P) {
     P->lo = lo;
     P->hi = hi;
     clique_thresholds(c->defenders, P->thr);
+  } else if (c->network == CPR_NET_EXP_CLIQUE) {
+    // cpr_protocols.ml:478-485: symmetric clique, exponential link delays, node 0 runs the
+    // attack policy (ethereum_ssz, or nakamoto_ssz in Nakamoto mode); keyed equal-weight
+    // miner draw (attacker threshold 1/n)
+    if (c->mode != CPR_MODE_LOOP)
+      return fail(CPR_E_UNSUPPORTED, "the gym engine always uses the selfish-mining network");
+    if (c->defenders < 1 || c->defenders > 63)
+      return fail(CPR_E_INVALID_ARG, "exponential clique: 1..63 defenders");
+    if (!(c->propagation_delay > 0.) || !std::isfinite(c->propagation_delay))
+      return fail(CPR_E_INVALID_ARG, "exponential clique: propagation_delay must be positive");
+    P->d = c->defenders;
+    P->net = 3;
+    P->delta = c->propagation_delay;
+    P->t_att = alpha_threshold(1.0 / (double)(c->defenders + 1));
   } else {
     return fail(CPR_E_INVALID_ARG, "unknown network");
   }

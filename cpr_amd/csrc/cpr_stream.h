@@ -1,4 +1,4 @@
-// Keyed random stream v1, device side.
+// Keyed random stream v2, device side.
 //
 // Every draw of the reference (OCaml Random, distributions.ml:17,24,90,93 and
 // simulator.ml:123) is re-addressed by semantic coordinates so one GPU lane can produce
@@ -11,11 +11,13 @@
 //                  ctr = (ep, kw, TAG_LINK | off<<12 | j>>1), words 2*(j&1),+1 -> u53
 //   message (vertex serial s, dest j; B_k, where a node shares several times per
 //   activation window): ctr = (ep, s, TAG_MSG | j>>1), words 2*(j&1),+1 -> u53
-// cpr_log = fdlibm e_log.c (IEEE +,-,*,/ only) so device and host agree bit for bit;
-// this TU must be compiled with -ffp-contract=off.
+// cpr_log = the keyed stream v2 table log (IEEE +, *, fma only) so device and host agree
+// bit for bit; this TU must be compiled with -ffp-contract=off.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+
+#include <cmath>
 
 #pragma clang fp contract(off)
 
@@ -72,107 +74,58 @@ __host__ __device__ inline double u53(uint32_t a, uint32_t b) {
 __host__ __device__ inline double dbits(uint64_t b) { return __builtin_bit_cast(double, b); }
 __host__ __device__ inline uint64_t bitsd(double d) { return __builtin_bit_cast(uint64_t, d); }
 
-// fdlibm __ieee754_log; domain used here: [0, 1)
-__host__ __device__ inline double cpr_log(double x) {
-  const double ln2_hi = dbits(0x3fe62e42fee00000ull);
-  const double ln2_lo = dbits(0x3dea39ef35793c76ull);
-  const double two54 = dbits(0x4350000000000000ull);
-  const double Lg1 = dbits(0x3FE5555555555593ull), Lg2 = dbits(0x3FD999999997FA04ull);
-  const double Lg3 = dbits(0x3FD2492494229359ull), Lg4 = dbits(0x3FCC71C51D8E78AFull);
-  const double Lg5 = dbits(0x3FC7466496CB03DEull), Lg6 = dbits(0x3FC39A09D078C69Full);
-  const double Lg7 = dbits(0x3FC2F112DF3E5244ull);
-#if defined(__HIP_DEVICE_COMPILE__) && !defined(CPR_NO_CONST_BARRIER)
-  // materialise the constants at each use instead of keeping ten SGPR pairs live across
-  // the activation loop (which spills other uniforms to VGPR lanes)
-  double c_[10] = {ln2_hi, ln2_lo, Lg1, Lg2, Lg3, Lg4, Lg5, Lg6, Lg7, two54};
-#pragma unroll
-  for (int q = 0; q < 10; ++q) asm volatile("" : "+s"(c_[q]));
-#define ln2_hi c_[0]
-#define ln2_lo c_[1]
-#define Lg1 c_[2]
-#define Lg2 c_[3]
-#define Lg3 c_[4]
-#define Lg4 c_[5]
-#define Lg5 c_[6]
-#define Lg6 c_[7]
-#define Lg7 c_[8]
-#define two54 c_[9]
-#endif
-  uint64_t ux = bitsd(x);
-  int32_t hx = (int32_t)(ux >> 32);
-  const uint32_t lx = (uint32_t)ux;
-  int32_t k = 0;
-  if (hx < 0x00100000) {
-    if (((hx & 0x7fffffff) | (int32_t)lx) == 0) return -__builtin_inf();
-    if (hx < 0) return __builtin_nan("");
-    k -= 54;
-    x *= two54;
-    ux = bitsd(x);
-    hx = (int32_t)(ux >> 32);
-  }
-  if (hx >= 0x7ff00000) return x + x;
-  k += (hx >> 20) - 1023;
-  hx &= 0x000fffff;
-  int32_t i = (hx + 0x95f64) & 0x100000;
-  ux = ((uint64_t)(uint32_t)(hx | (i ^ 0x3ff00000)) << 32) | (ux & 0xffffffffull);
-  x = dbits(ux);
-  k += (i >> 20);
-  const double f = x - 1.0;
-  double dk, R;
-  if ((0x000fffff & (2 + hx)) < 3) {  // |f| < 2^-20 (rare)
-    if (f == 0.0) {
-      if (k == 0) return 0.0;
-      dk = (double)k;
-      return dk * ln2_hi + dk * ln2_lo;
-    }
-    R = f * f * (0.5 - 0.33333333333333333 * f);
-    if (k == 0) return f - R;
-    dk = (double)k;
-    return dk * ln2_hi - ((R - dk * ln2_lo) - f);
-  }
+// keyed stream v2 log: x in [0, 1) (the stream's 53-bit uniforms).
+// x = 2^e * xr with xr in [sqrt(2)/2, sqrt(2)); bucket i of xr (i = hi << 7 | top 7
+// mantissa bits) gives INV_C ~ 1/c_i and T = -log(INV_C) as a double-double
+// (tools/gen_logtab.py); log x = e ln2 + T + log1p(r), r = fma(xr, INV_C, -1) (|r| <= 2^-7,
+// exact where c_i = 1), log1p as its degree-8 Taylor polynomial. Only IEEE +, *, fma and
+// exact bit moves, so the oracle's restatement (oracle/src/keyed_stream.h) is bit-identical;
+// at most 1-2 ulp from the true log. Replaces v1's fdlibm e_log.c: a quarter of the f64
+// work and no division (tools/nak_probe_ab.sh: the log was 23% of k_run_episodes).
+struct LogEnt {
+  uint64_t inv_c, t_hi, t_lo, pad;
+};
 #if defined(__HIP_DEVICE_COMPILE__)
-  // f / (2 + f) as the compiler's own IEEE division expansion minus v_div_scale and
-  // v_div_fixup: here f in [sqrt(2)/2 - 1, sqrt(2) - 1) and 2 + f in [1.7, 2.5), so
-  // div_scale would return its operands unchanged (vcc = 0, div_fmas = fma) and div_fixup
-  // its quotient: the same bits, three instructions fewer
-  const double dd2 = 2.0 + f;
-  double rr = __builtin_amdgcn_rcp(dd2);
-  rr = __builtin_fma(rr, __builtin_fma(-dd2, rr, 1.0), rr);
-  rr = __builtin_fma(rr, __builtin_fma(-dd2, rr, 1.0), rr);
-  const double qq = f * rr;
-  const double s = __builtin_fma(__builtin_fma(-dd2, qq, f), rr, qq);
+__constant__ static const LogEnt kLogTab[256] = {
+#include "cpr_logtab.inc"
+};
 #else
-  const double s = f / (2.0 + f);
+static const LogEnt kLogTab[256] = {
+#include "cpr_logtab.inc"
+};
 #endif
-  dk = (double)k;
-  const double z = s * s;
-  i = hx - 0x6147a;
-  const double w = z * z;
-  const int32_t j = 0x6b851 - hx;
-  const double t1 = w * (Lg2 + w * (Lg4 + w * Lg6));
-  const double t2 = z * (Lg1 + w * (Lg3 + w * (Lg5 + w * Lg7)));
-  i |= j;
-  R = t2 + t1;
-  // fdlibm's four tails as one select: its k == 0 forms equal the general forms at dk = 0
-  // bit for bit (0 * c = +0, y + 0 = y, and fl(y - f) = -fl(f - y) under round to nearest),
-  // so lanes of a wave no longer split over four branches (tests/test_oracle_kat.py checks
-  // this against the oracle's line-by-line fdlibm)
-  const double hfsq = 0.5 * f * f;
-  const double lo = dk * ln2_lo;
-  const double tail = i > 0 ? hfsq - (s * (hfsq + R) + lo) : s * (f - R) - lo;
-  return dk * ln2_hi - (tail - f);
-#if defined(__HIP_DEVICE_COMPILE__) && !defined(CPR_NO_CONST_BARRIER)
-#undef ln2_hi
-#undef ln2_lo
-#undef Lg1
-#undef Lg2
-#undef Lg3
-#undef Lg4
-#undef Lg5
-#undef Lg6
-#undef Lg7
-#undef two54
+
+__host__ __device__ inline double cpr_fma(double a, double b, double c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_fma(a, b, c);
+#else
+  return std::fma(a, b, c);
 #endif
+}
+
+__host__ __device__ inline double cpr_log(double x) {
+  const double ln2_hi = dbits(0x3fe62e42fee00000ull);  // 32 trailing zeros: e * ln2_hi exact
+  const double ln2_lo = dbits(0x3dea39ef35793c76ull);
+  const uint64_t ux = bitsd(x);
+  const uint64_t mant = ux & 0x000FFFFFFFFFFFFFull;
+  const uint32_t hi = mant >= 0x6A09E667F3BCDull ? 1u : 0u;  // xr >= sqrt(2): halve it
+  const int32_t e = (int32_t)(ux >> 52) - 1023 + (int32_t)hi;
+  const double xr = dbits(((uint64_t)(1023u - hi) << 52) | mant);
+  const LogEnt E = kLogTab[(hi << 7) | (uint32_t)(mant >> 45)];
+  const double r = cpr_fma(xr, dbits(E.inv_c), -1.0);
+  double q = -0.125;
+  q = cpr_fma(r, q, 1.0 / 7.0);
+  q = cpr_fma(r, q, -1.0 / 6.0);
+  q = cpr_fma(r, q, 0.2);
+  q = cpr_fma(r, q, -0.25);
+  q = cpr_fma(r, q, 1.0 / 3.0);
+  q = cpr_fma(r, q, -0.5);
+  const double p = cpr_fma(r * r, q, r);
+  const double de = (double)e;
+  const double a = cpr_fma(de, ln2_hi, dbits(E.t_hi));
+  const double b = cpr_fma(de, ln2_lo, dbits(E.t_lo));
+  const double y = (a + p) + b;
+  return x == 0.0 ? -__builtin_inf() : y;  // x = 0: exponential draw +inf
 }
 
 struct Stream {
@@ -239,6 +192,12 @@ struct Stream {
   __host__ __device__ inline double msg_unif(uint32_t serial, uint32_t dest, double lo,
                                              double hi) const {
     return msg_u(serial, dest) * (hi - lo) + lo;
+  }
+  // exponential(ev) delay of the message shared at (kw, off) to dest (distributions.ml:
+  // 22-29; Nakamoto / Ethereum on exponential-delay cliques)
+  __host__ __device__ inline double link_exp(uint32_t kw, uint32_t off, uint32_t dest,
+                                             double ev) const {
+    return (-1.0 * ev) * cpr_log(link_u(kw, off, dest));
   }
   // exponential(ev) delay of message `serial` to dest (distributions.ml:22-29; B_k /
   // Tailstorm on exponential-delay cliques)
@@ -328,6 +287,10 @@ struct TraceStream {
   }
   __host__ __device__ inline double msg_exp(uint32_t serial, uint32_t dest, double) const {
     return lookup(trace_msg_key(serial, dest));
+  }
+  __host__ __device__ inline double link_exp(uint32_t kw, uint32_t off, uint32_t dest,
+                                             double) const {
+    return lookup(trace_link_key(kw, off, dest));
   }
 };
 

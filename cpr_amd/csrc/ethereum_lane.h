@@ -68,7 +68,8 @@ static_assert(sizeof(HNode) == 24, "HNode layout");
 struct EthParams {
   uint64_t t_att;
   int32_t d, n;  // defenders, nodes
-  int32_t net;   // 0 selfish mining, 1 two agents, 2 honest clique (all nodes honest)
+  int32_t net;   // 0 selfish mining, 1 two agents, 2 honest clique (all nodes honest),
+                 // 3 exponential-delay clique (node 0 attacker; delta = mean link delay)
   int32_t mode;  // 0 gym, 1 loop
   int32_t policy, scheme;
   int32_t cap_b, cap_e;
@@ -925,6 +926,9 @@ struct EthLane {
           if (P.net == 2)  // models.ml:4 uniform propagation delays on every link
             delay = S.link_unif((uint32_t)b.share_k, (uint32_t)b.share_off, (uint32_t)dst, P.lo,
                                 P.hi);
+          else if (P.net == 3)  // cpr_protocols.ml:481-483 exponential delays on every link
+            delay = S.link_exp((uint32_t)b.share_k, (uint32_t)b.share_off, (uint32_t)dst,
+                               P.delta);
           else if (P.net == 1)
             delay = 0.0;
           else if (node == 0)

@@ -150,7 +150,8 @@ enum cpr_network {
                                  (cpr_protocols.ml:200-210,478-485): node 0 (the attacker,
                                  running cfg.policy) plus `defenders` honest nodes (1..63),
                                  equal compute, every link delay exponential with mean
-                                 propagation_delay; CPR_MODE_LOOP, B_k or Tailstorm */
+                                 propagation_delay; CPR_MODE_LOOP, every protocol
+                                 (Nakamoto on the exact event engine in Nakamoto mode) */
   CPR_NET_ABSTRACT_GAMMA = 4  /* FLAGGED abstract-gamma mode (not a network
                                  of the reference, which rejects gamma = 1, envs.py:73-75):
                                  the gym's attacker + `defenders` equal-compute honest nodes

@@ -1,4 +1,4 @@
-// TEST INFRASTRUCTURE ONLY — CPU oracle side of the "cpr keyed stream v1".
+// TEST INFRASTRUCTURE ONLY — CPU oracle side of the "cpr keyed stream v2".
 //
 // The reference draws every random number from one sequential OCaml `Random` stream
 // (distributions.ml:17,24,90,93; simulator.ml:123), which makes results depend on the
@@ -22,11 +22,12 @@
 // uniform(lo,hi)  = u * (hi - lo) + lo       (distributions.ml:17)
 // miner           = 0 if w0 < floor(alpha * 2^32) else 1 + ((w1 * d) >> 32)
 //
-// cpr_log is fdlibm's e_log.c algorithm (only IEEE +,-,*,/), so the GPU and the CPU
-// oracle compute bit-identical event times. This file is an independent restatement of
+// cpr_log is the v2 table-driven log (only IEEE +, *, fma and bit moves; v1 used fdlibm's
+// e_log.c), so the GPU and the CPU oracle compute bit-identical event times. This file is an independent restatement of
 // the same specification the HIP code implements (cpr_amd/csrc/cpr_stream.h); the two
 // are cross-checked draw-by-draw in tests/test_gpu_parity.py.
 #pragma once
+#include <cmath>
 #include <cstdint>
 #include <cstring>
 #include <vector>
@@ -74,67 +75,37 @@ static inline uint64_t double_to_bits(double d) {
   return b;
 }
 
-// fdlibm __ieee754_log (e_log.c), restated. Input domain used by the stream: [0, 1).
+// keyed stream v2 log, restated: x in [0, 1) is 2^e * xr, xr in [sqrt(2)/2, sqrt(2));
+// bucket i = (xr < 1) << 7 | top 7 mantissa bits of x selects INV_C ~ 1/c_i and
+// T = -log(INV_C) = T_HI + T_LO (keyed_logtab.inc, from tools/gen_logtab.py);
+// log x = e ln2 + T + log1p(r), r = fma(xr, INV_C, -1), log1p by its Taylor polynomial
+// through r^8, summed as ((e ln2_hi + T_HI) + p) + (e ln2_lo + T_LO).
+struct KeyedLogEntry {
+  uint64_t inv_c, t_hi, t_lo, pad;
+};
+static const KeyedLogEntry kKeyedLog[256] = {
+#include "keyed_logtab.inc"
+};
+
 static inline double cpr_log(double x) {
+  if (x == 0.0) return -1.0 / 0.0;
   const double ln2_hi = bits_to_double(0x3fe62e42fee00000ull);
   const double ln2_lo = bits_to_double(0x3dea39ef35793c76ull);
-  const double two54 = bits_to_double(0x4350000000000000ull);
-  const double Lg1 = bits_to_double(0x3FE5555555555593ull);
-  const double Lg2 = bits_to_double(0x3FD999999997FA04ull);
-  const double Lg3 = bits_to_double(0x3FD2492494229359ull);
-  const double Lg4 = bits_to_double(0x3FCC71C51D8E78AFull);
-  const double Lg5 = bits_to_double(0x3FC7466496CB03DEull);
-  const double Lg6 = bits_to_double(0x3FC39A09D078C69Full);
-  const double Lg7 = bits_to_double(0x3FC2F112DF3E5244ull);
-  uint64_t ux = double_to_bits(x);
-  int32_t hx = (int32_t)(ux >> 32);
-  uint32_t lx = (uint32_t)ux;
-  int32_t k = 0;
-  if (hx < 0x00100000) {
-    if (((hx & 0x7fffffff) | lx) == 0) return -1.0 / 0.0;
-    if (hx < 0) return (x - x) / 0.0;
-    k -= 54;
-    x *= two54;
-    ux = double_to_bits(x);
-    hx = (int32_t)(ux >> 32);
-  }
-  if (hx >= 0x7ff00000) return x + x;
-  k += (hx >> 20) - 1023;
-  hx &= 0x000fffff;
-  int32_t i = (hx + 0x95f64) & 0x100000;
-  ux = ((uint64_t)(uint32_t)(hx | (i ^ 0x3ff00000)) << 32) | (ux & 0xffffffffull);
-  x = bits_to_double(ux);
-  k += (i >> 20);
-  double f = x - 1.0;
-  double dk, R;
-  if ((0x000fffff & (2 + hx)) < 3) {
-    if (f == 0.0) {
-      if (k == 0) return 0.0;
-      dk = (double)k;
-      return dk * ln2_hi + dk * ln2_lo;
-    }
-    R = f * f * (0.5 - 0.33333333333333333 * f);
-    if (k == 0) return f - R;
-    dk = (double)k;
-    return dk * ln2_hi - ((R - dk * ln2_lo) - f);
-  }
-  double s = f / (2.0 + f);
-  dk = (double)k;
-  double z = s * s;
-  i = hx - 0x6147a;
-  double w = z * z;
-  int32_t j = 0x6b851 - hx;
-  double t1 = w * (Lg2 + w * (Lg4 + w * Lg6));
-  double t2 = z * (Lg1 + w * (Lg3 + w * (Lg5 + w * Lg7)));
-  i |= j;
-  R = t2 + t1;
-  if (i > 0) {
-    double hfsq = 0.5 * f * f;
-    if (k == 0) return f - (hfsq - s * (hfsq + R));
-    return dk * ln2_hi - ((hfsq - (s * (hfsq + R) + dk * ln2_lo)) - f);
-  }
-  if (k == 0) return f - s * (f - R);
-  return dk * ln2_hi - ((s * (f - R) - dk * ln2_lo) - f);
+  const uint64_t ux = double_to_bits(x);
+  const uint64_t mant = ux & 0x000FFFFFFFFFFFFFull;
+  const uint32_t hi = mant >= 0x6A09E667F3BCDull ? 1u : 0u;
+  const int32_t e = (int32_t)(ux >> 52) - 1023 + (int32_t)hi;
+  const double xr = bits_to_double(((uint64_t)(1023u - hi) << 52) | mant);
+  const KeyedLogEntry& E = kKeyedLog[(hi << 7) | (uint32_t)(mant >> 45)];
+  const double r = std::fma(xr, bits_to_double(E.inv_c), -1.0);
+  const double c[7] = {-0.125, 1.0 / 7.0, -1.0 / 6.0, 0.2, -0.25, 1.0 / 3.0, -0.5};
+  double q = c[0];
+  for (int k = 1; k < 7; ++k) q = std::fma(r, q, c[k]);
+  const double p = std::fma(r * r, q, r);
+  const double de = (double)e;
+  const double a = std::fma(de, ln2_hi, bits_to_double(E.t_hi));
+  const double b = std::fma(de, ln2_lo, bits_to_double(E.t_lo));
+  return (a + p) + b;
 }
 
 // cumulative compute thresholds of the keyed miner draw for arbitrary weights:

@@ -658,6 +658,88 @@ static void sink_nodes(const int64_t* a, const double* r, int n, int32_t hm) {
   *g_sink.head_miner = hm;
 }
 
+static TablePolicy table_of(const cpr_config* c);
+
+// Nakamoto / Ethereum Simulator.loop task on the exponential-delay clique
+// (cpr_protocols.ml:200-210,478-485): node 0 runs nakamoto_ssz / ethereum_ssz with the
+// policy (or table), `defenders` honest nodes, equal compute, exponential(propagation_delay)
+// links keyed by share window (kw, off, dest), keyed stream
+static int attack_clique_task(const cpr_config* c, uint64_t ep, cpr_episode_record* rec) {
+  try {
+    const bool eth = c->protocol == CPR_PROTO_ETHEREUM;
+    const int n = c->defenders + 1;
+    const Network net = loop_net(1, n, 0.0, c->activation_delay, c->propagation_delay, 0.0, 0.0);
+    std::unique_ptr<SimRng> rng(new KeyedSimRng(c->seed, ep, net));
+    rng = trace_wrap(std::move(rng), net, false);
+    Sim sim(net, rng.get());
+    if (eth) {
+      sim.proto = 1;
+      sim.eth_scheme = c->reward_scheme;
+    }
+    const EthTable et = eth_table_of(c);
+    const TablePolicy nt = table_of(c);
+    std::vector<std::unique_ptr<NodeImpl>> nodes;
+    NakSszAttackerNode* na = nullptr;
+    EthSszAttackerNode* ea = nullptr;
+    if (eth) {
+      ea = new EthSszAttackerNode();
+      ea->policy = c->policy;
+      ea->table = &et;
+      nodes.emplace_back(ea);
+    } else {
+      na = new NakSszAttackerNode();
+      na->policy = c->policy;
+      na->table = c->policy == POL_TABLE ? &nt : nullptr;
+      nodes.emplace_back(na);
+    }
+    for (int i = 1; i < n; ++i) {
+      if (eth)
+        nodes.emplace_back(new EthHonest());
+      else
+        nodes.emplace_back(new NakHonest());
+    }
+    sim.init(std::move(nodes));
+    Block* root = sim.roots.back();
+    if (eth) {
+      ea->agent.sim = &sim;
+      ea->agent.my_id = 0;
+      ea->agent.init(root);
+      for (int i = 1; i < n; ++i) static_cast<EthHonest*>(sim.nodes[i].get())->state = root;
+    } else {
+      na->agent.sim = &sim;
+      na->agent.my_id = 0;
+      na->agent.init(root);
+      for (int i = 1; i < n; ++i) static_cast<NakHonest*>(sim.nodes[i].get())->state = root;
+    }
+    sim.loop((int)c->activations);
+    Block* h = sim.head();
+    std::vector<int64_t> a(n);
+    std::vector<double> rw(n);
+    for (int i = 0; i < n; ++i) {
+      a[i] = sim.activations[i];
+      rw[i] = h->rewards[i];
+    }
+    sink_nodes(a.data(), rw.data(), n, eth ? -2 : h->value.miner);
+    rec->reward_attacker = rw[0];
+    rec->reward_defender = 0.0;
+    rec->n_activations = 0;
+    for (int i = 1; i < n; ++i) rec->reward_defender += rw[i];
+    for (int i = 0; i < n; ++i) rec->n_activations += a[i];
+    rec->progress = eth ? sim.progress(h) : (double)h->value.height;
+    rec->chain_time = Sim::timestamp(h);
+    rec->sim_time = 0.0;
+    rec->n_steps = 0;
+    rec->head_height = h->value.height;
+    rec->head_miner = -1;
+    rec->status = 0;
+    rec->head_work = eth ? h->value.work : 0;
+    return 0;
+  } catch (std::exception& e) {
+    set_err(e.what());
+    return -1;
+  }
+}
+
 static int run_loop_episode(const cpr_config* c, uint64_t ep, cpr_episode_record* rec) {
   int64_t acts[2];
   double rew[2], ht, hp;
@@ -768,6 +850,9 @@ static int run_loop_episode(const cpr_config* c, uint64_t ep, cpr_episode_record
     rec->head_work = 0;
     return 0;
   }
+  if (c->network == CPR_NET_EXP_CLIQUE &&
+      (c->protocol == CPR_PROTO_NAKAMOTO || c->protocol == CPR_PROTO_ETHEREUM))
+    return attack_clique_task(c, ep, rec);
   if (c->network == CPR_NET_EXP_CLIQUE &&
       (c->protocol == CPR_PROTO_BK || c->protocol == CPR_PROTO_TAILSTORM)) {
     // symmetric clique, exponential(propagation_delay) links, node 0 runs the policy

@@ -49,6 +49,14 @@ CASES = {
                               dict(scheme=L.REWARD_CONSTANT, ad=2.0)),
     "bk-4nodes-get-ahead": (L.PROTO_BK, 3, L.BK_POLICY_GET_AHEAD, 1000,
                             dict(k=4, scheme=L.REWARD_BLOCK, ad=10.0)),
+    # Nakamoto (exact event engine in Nakamoto mode) and Ethereum attackers on the same
+    # network: the reference's policy tests run every protocol there
+    "nak-3nodes-sm1": (L.PROTO_NAKAMOTO, 2, L.POLICY_SAPIRSHTEIN_2016_SM1, 1000, dict(ad=2.0)),
+    "nak-2miners-es14": (L.PROTO_NAKAMOTO, 1, L.POLICY_EYAL_SIRER_2014, 1000, dict(ad=1.0)),
+    "eth-3nodes-fn19": (L.PROTO_ETHEREUM, 2, L.ETH_POLICY_FN19, 1000,
+                        dict(ad=2.0, scheme=L.REWARD_CONSTANT)),
+    "eth-2miners-selfish-release": (L.PROTO_ETHEREUM, 1, L.ETH_POLICY_SELFISH_RELEASE, 1000,
+                                    dict(ad=5.0, scheme=L.REWARD_DISCOUNT)),
 }
 # episodes whose withheld vote tree outgrows the lane's 512-vote scratch are flagged
 # CPR_ST_CAPACITY (ts_lane.h NQS): with equal compute and delays as long as the block
@@ -84,6 +92,8 @@ def test_exp_clique_records_match_oracle(ctx, case):
 
 
 @pytest.mark.parametrize("proto,k,scheme,sel", [
+    (L.PROTO_NAKAMOTO, 8, L.REWARD_CONSTANT, 0),                         # nakamoto/ssz/honest
+    (L.PROTO_ETHEREUM, 8, L.REWARD_CONSTANT, 0),                         # ethereum/ssz/honest
     (L.PROTO_BK, 8, L.REWARD_BLOCK, 0),                                  # bk8/ssz/honest
     (L.PROTO_TAILSTORM, 8, L.REWARD_CONSTANT, L.SELECT_OPTIMAL),         # tailstorm8constant
     (L.PROTO_TAILSTORM, 8, L.REWARD_DISCOUNT, L.SELECT_HEURISTIC),       # tailstorm8discount

@@ -108,10 +108,16 @@ def _ulp_diff(a, b):
 
 
 def test_cpr_log_accuracy():
+    # keyed stream v2 table log (oracle/src/keyed_stream.h) against the exactly rounded
+    # natural log (50-digit decimal): within 2 ulp, correctly rounded for most inputs
+    import decimal
+
+    decimal.getcontext().prec = 50
     rng = np.random.default_rng(7)
     us = np.concatenate([rng.random(20000), [2.0**-53, 0.5, 1 - 2.0**-53, 0.999999, 1e-300]])
-    worst = max(_ulp_diff(O.cpr_log(float(u)), math.log(float(u))) for u in us)
-    assert worst <= 1
+    d = [_ulp_diff(O.cpr_log(float(u)), float(decimal.Decimal(float(u)).ln())) for u in us]
+    assert max(d) <= 2
+    assert sum(x == 0 for x in d) > 0.6 * len(d)
     assert O.cpr_log(0.0) == -math.inf
     assert O.cpr_log(1.0) == 0.0
 
