@@ -123,8 +123,9 @@ def test_exp_clique_rejections(ctx):
         (dict(mode=L.MODE_GYM, max_steps=100), "selfish-mining"),
         (dict(defenders=64), "defenders"),  # make_config maps 0 to 1
         (dict(propagation_delay=0.0), "propagation_delay"),
-        (dict(protocol=L.PROTO_NAKAMOTO, policy=0), "network"),
-        (dict(protocol=L.PROTO_ETHEREUM, policy=0), "network"),
+        (dict(protocol=L.PROTO_NAKAMOTO, policy=0, mode=L.MODE_GYM, max_steps=100),
+         "selfish-mining"),
+        (dict(protocol=L.PROTO_ETHEREUM, policy=0, defenders=64), "defenders"),
     ]
     for kw, msg in cases:
         base = dict(alpha=0.0, gamma=0.0, network=L.NET_EXP_CLIQUE, mode=L.MODE_LOOP, defenders=1,

@@ -8,7 +8,8 @@ the variants' results are meaningless; only their kernel times are read.
   cheap_both: both
   base      : the tree as it is
 
-usage: python tools/nak_probe_variants.py   (writes build/var/<name>.so)
+usage: python tools/nak_probe_variants.py [name | name@gitrev ...]  (build/var/<name>.so;
+       name@rev builds the csrc/ of that git revision, e.g. prev@HEAD)
 """
 import pathlib
 import shutil
@@ -33,11 +34,17 @@ LOG_OLD = "__host__ __device__ inline double cpr_log(double x) {"
 LOG_NEW = LOG_OLD + "\n  return x - 1.0;  // probe: cheap stand-in"
 
 
-def variant(name, rng, log):
+def variant(name, rng, log, rev=None):
     d = ROOT / "cpr_amd" / ("csrc_probe_" + name)  # same depth: ../../include resolves
     if d.exists():
         shutil.rmtree(d)
     shutil.copytree(CSRC, d)
+    if rev:  # the csrc/ tree of a git revision instead of the working tree
+        for f in d.iterdir():
+            blob = subprocess.run(["git", "-C", str(ROOT), "show", f"{rev}:cpr_amd/csrc/{f.name}"],
+                                  capture_output=True)
+            if blob.returncode == 0:
+                f.write_bytes(blob.stdout)
     st = (d / "cpr_stream.h").read_text()
     if rng:
         assert PHILOX_OLD in st
@@ -61,5 +68,7 @@ if __name__ == "__main__":
     OUT.mkdir(parents=True, exist_ok=True)
     names = sys.argv[1:] or ["base", "cheap_rng", "cheap_log", "cheap_both"]
     for n in names:
-        variant(n, "rng" in n or "both" in n, "log" in n or "both" in n)
+        rev = n.split("@", 1)[1] if "@" in n else None  # e.g. prev@HEAD~1
+        n = n.split("@", 1)[0]
+        variant(n, "rng" in n or "both" in n, "log" in n or "both" in n, rev)
         print("built", OUT / f"{n}.so")

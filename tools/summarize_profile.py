@@ -8,16 +8,28 @@ import json
 import shutil
 import sys
 
+import re
+
 tag = sys.argv[1]
 eps = int(sys.argv[2]) if len(sys.argv) > 2 else 393216
 K = "k_run_episodes"
+# the headline sweep's launches: the sapirshtein-2016-sm1 specialisation on the keyed
+# stream (bench.py's abstract-gamma column after the timed sweep runs the generic POL = -1
+# instantiation and is left out)
+HEADLINE = re.compile(r"k_run_episodes<0, (cpr::)?SeedSource, 3>")
+
+
+def is_headline(name):
+    return HEADLINE.search(name) is not None
 
 
 def agg(path):
     a = collections.defaultdict(lambda: collections.defaultdict(float))
     n = collections.Counter()
     for r in csv.DictReader(open(path)):
-        k = "k_run_episodes" if "k_run_episodes" in r["Kernel_Name"] else r["Kernel_Name"].split("(")[0]
+        if K in r["Kernel_Name"] and not is_headline(r["Kernel_Name"]):
+            continue
+        k = K if is_headline(r["Kernel_Name"]) else r["Kernel_Name"].split("(")[0]
         a[k][r["Counter_Name"]] += float(r["Counter_Value"])
         n[(k, r["Counter_Name"])] += 1
     return a, n
@@ -30,7 +42,8 @@ for p in ["prof_pmc_sq", "prof_pmc_fetch", "prof_pmc_write"]:
         for c, x in v.items():
             res.setdefault(k, {})[c] = {"sum": x, "dispatches": n[(k, c)], "per_dispatch": x / n[(k, c)]}
 tr = list(csv.DictReader(open("gpurun_out/prof_trace/run_kernel_trace.csv")))
-durs = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in tr if K in r["Kernel_Name"]]
+durs = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in tr
+        if is_headline(r["Kernel_Name"])]
 acts = eps * 2017
 r = res[K]
 s = {
