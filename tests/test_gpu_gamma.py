@@ -14,6 +14,7 @@ BASELINE configs[1] runs on. Its semantics are pinned here two ways:
 Fixtures: tests/golden/make_gamma_fixtures.py.
 """
 
+import pathlib
 import time
 
 import numpy as np
@@ -56,41 +57,47 @@ def test_gamma_loop_records_match_oracle(ctx, gamma, alpha, policy):
     assert s.episodes == 48 and s.activations == 48 * 10000
 
 
-def test_gamma_loop_rows_within_4_sigma(ctx, say):
-    # each row is one batch of N_TASKS dependent 10,000-activation chains (a few workgroups),
-    # so rows run concurrently: one context (HIP stream) per worker thread, ctypes releases
-    # the GIL; the slow many-defender rows first
-    from concurrent.futures import ThreadPoolExecutor
+def test_gamma_loop_rows_within_4_sigma(ctx, say, tmp_path):
+    # rows are latency-bound (one batch of dependent chains each), so they run side by side:
+    # 4 worker processes x 4 streams (tests/gamma_rows_worker.py), the slow many-defender
+    # rows spread over the workers first
+    import subprocess
+    import sys
 
-    import threading
-
-    rows = sorted(enumerate(G.withholding_rows()), key=lambda x: -x[1]["defenders"])
-    ctxs, batches = [], []
-    local = threading.local()
+    rows = G.withholding_rows()
+    order = sorted(range(len(rows)), key=lambda i: -rows[i]["defenders"])
+    shares = [order[w::4] for w in range(4)]
     t0 = time.perf_counter()
+    procs = []
+    for w, share in enumerate(shares):
+        out = tmp_path / f"w{w}.npz"
+        procs.append((out, subprocess.Popen(
+            [sys.executable, str(pathlib.Path(__file__).parent / "gamma_rows_worker.py"),
+             str(out), str(N_TASKS), *map(str, share)],
+            stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)))
+    done = 0
+    import selectors
 
-    def one(job):
-        i, row = job
-        if not hasattr(local, "ctx"):
-            local.ctx = device.Context(ctx.device)
-            ctxs.append(local.ctx)
-        cfg = G.row_config(device.make_config, L, row, seed=0x6A330000 + i)
-        b = device.Batch(cfg, ctx=local.ctx)
-        _, rec = b.run(N_TASKS, records=True)
-        batches.append(b)  # closed at the end: hipFree would synchronize the device
-        return row, rec
-
+    sel = selectors.DefaultSelector()
+    for _, p in procs:
+        sel.register(p.stdout, selectors.EVENT_READ)
+    open_streams = len(procs)
+    while open_streams:
+        for key, _ in sel.select(timeout=30):
+            line = key.fileobj.readline()
+            if not line:
+                sel.unregister(key.fileobj)
+                open_streams -= 1
+            elif line.startswith("row "):
+                done += 1
+                if done % 8 == 0:
+                    say(f"  gamma rows: {done} of {len(rows)} ({time.perf_counter() - t0:.0f} s)")
     results = []
-    with ThreadPoolExecutor(4) as pool:
-        for row, rec in pool.map(one, rows):
-            results.append((row, rec))
-            if len(results) % 8 == 0:
-                say(f"  gamma rows: {len(results)} of {len(rows)} "
-                    f"({time.perf_counter() - t0:.0f} s)")
-    for b in batches:
-        b.close()
-    for c in ctxs:
-        c.close()
+    for out, p in procs:
+        assert p.wait() == 0, f"worker failed ({out})"
+        z = np.load(out)
+        results += [(rows[int(k[1:])], z[k]) for k in z.files]
+    assert len(results) == len(rows)
     worst = (0.0, None)
     zs = []
     for row, rec in results:
