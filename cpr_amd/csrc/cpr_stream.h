@@ -83,7 +83,7 @@ __host__ __device__ inline uint64_t bitsd(double d) { return __builtin_bit_cast(
 // at most 1-2 ulp from the true log. Replaces v1's fdlibm e_log.c: a quarter of the f64
 // work and no division (tools/nak_probe_ab.sh: the log was 23% of k_run_episodes).
 struct LogEnt {
-  uint64_t inv_c, t_hi, t_lo, pad;
+  uint64_t inv_c, t_hi, t_lo;
 };
 #if defined(__HIP_DEVICE_COMPILE__)
 __constant__ static const LogEnt kLogTab[256] = {
@@ -103,6 +103,7 @@ __host__ __device__ inline double cpr_fma(double a, double b, double c) {
 #endif
 }
 
+// (an LDS copy of the table measured no faster than constant memory: the 6 KB stay in L1)
 __host__ __device__ inline double cpr_log(double x) {
   const double ln2_hi = dbits(0x3fe62e42fee00000ull);  // 32 trailing zeros: e * ln2_hi exact
   const double ln2_lo = dbits(0x3dea39ef35793c76ull);

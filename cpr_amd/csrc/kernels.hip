@@ -46,9 +46,10 @@ __device__ inline CPR_AI BRef run_gym(NakLane& L, const NakParams& P, const St& 
     // only max_steps ends the episode: the trip count is the same in every lane of the
     // wave, so the loop exit is uniform and no lane state is merged at a divergent exit
     do {
+      const NakLane::Draw dr = L.draw(P, S);
       L.apply(L.policy_action<POL>(P));
       L.resolve<St, POL >= 0 ? 0 : -1>(P, S, M);
-      L.activate(P, S, M);
+      L.activate(P, S, M, dr);
       ++steps;
     } while (steps < P.max_steps);
     *steps_out = steps;

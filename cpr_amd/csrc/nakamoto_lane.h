@@ -426,10 +426,30 @@ struct NakLane {
   // StochasticClock + Dag + the attacker's prepare (simulator.ml:465-480, engine.ml:108-121,
   // nakamoto_ssz.ml:191-218). Written as selects: the lanes of a wave take different
   // sides of every decision, so both sides run anyway and the merges cost no copies.
+  struct Draw {
+    double dt;
+    int32_t miner;
+  };
+  // the next activation's miner and clock delay: they depend on the activation count only,
+  // so the gym loop draws them first and the Philox / log chain overlaps the policy and
+  // apply selects of the same iteration
+  template <class St>
+  __host__ __device__ inline CPR_AI Draw draw(const NakParams& P, const St& S) const {
+    Draw d;
+    d.dt = S.act((uint32_t)k, P.t_att, P.d, P.ev, &d.miner);
+    return d;
+  }
+
   template <class St>
   __host__ __device__ inline CPR_AI void activate(const NakParams& P, const St& S, const LaneMem& M) {
-    int32_t miner;
-    const double tn = t + S.act((uint32_t)k, P.t_att, P.d, P.ev, &miner);
+    activate(P, S, M, draw(P, S));
+  }
+
+  template <class St>
+  __host__ __device__ inline CPR_AI void activate(const NakParams& P, const St& S, const LaneMem& M,
+                                                  const Draw dr) {
+    const int32_t miner = dr.miner;
+    const double tn = t + dr.dt;
     if (tn <= w_bound) {
       if (tn <= window_last_arrival(P, S)) status |= ST_OVERLAP;
     }

@@ -81,7 +81,7 @@ static inline uint64_t double_to_bits(double d) {
 // log x = e ln2 + T + log1p(r), r = fma(xr, INV_C, -1), log1p by its Taylor polynomial
 // through r^8, summed as ((e ln2_hi + T_HI) + p) + (e ln2_lo + T_LO).
 struct KeyedLogEntry {
-  uint64_t inv_c, t_hi, t_lo, pad;
+  uint64_t inv_c, t_hi, t_lo;
 };
 static const KeyedLogEntry kKeyedLog[256] = {
 #include "keyed_logtab.inc"

@@ -15,7 +15,9 @@ from concurrent.futures import ThreadPoolExecutor
 
 import numpy as np
 
-sys.path.insert(0, __file__.rsplit("/", 1)[0])
+_HERE = __file__.rsplit("/", 1)[0]
+sys.path.insert(0, _HERE)
+sys.path.insert(0, _HERE + "/..")  # the repository root: cpr_amd
 
 import gamma_stats as G  # noqa: E402
 from cpr_amd import _lib as L  # noqa: E402

@@ -76,6 +76,7 @@ def test_gamma_loop_rows_within_4_sigma(ctx, say, tmp_path):
              str(out), str(N_TASKS), *map(str, share)],
             stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)))
     done = 0
+    log = []
     import selectors
 
     sel = selectors.DefaultSelector()
@@ -88,13 +89,15 @@ def test_gamma_loop_rows_within_4_sigma(ctx, say, tmp_path):
             if not line:
                 sel.unregister(key.fileobj)
                 open_streams -= 1
-            elif line.startswith("row "):
+            elif not line.startswith("row "):
+                log.append(line)
+            else:
                 done += 1
                 if done % 8 == 0:
                     say(f"  gamma rows: {done} of {len(rows)} ({time.perf_counter() - t0:.0f} s)")
     results = []
     for out, p in procs:
-        assert p.wait() == 0, f"worker failed ({out})"
+        assert p.wait() == 0, f"worker failed ({out}): {''.join(log)[-3000:]}"
         z = np.load(out)
         results += [(rows[int(k[1:])], z[k]) for k in z.files]
     assert len(results) == len(rows)
