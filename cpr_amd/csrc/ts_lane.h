@@ -932,8 +932,72 @@ struct TsLane {
     }
     return s;
   }
+  // parent summary of summary x: the tree root of its quorum (tailstorm.ml:124-130)
+  __host__ __device__ inline int32_t psum(const TsParams& P, const TsMem& M, int32_t x) {
+    return X(P, M, Q(P, M, X(P, M, x))[0]).sum;
+  }
+  // Dagtools.common_ancestor of two summaries without the frontier walk. The walk returns
+  // the intersection's maximal (Dag depth, serial) vertex. A vote lies in exactly one
+  // summary tree, and a summary's ancestors are itself, the vote paths from its quorum up
+  // to its parent summary, and that summary's ancestors; so the intersection is s* (the
+  // summaries' last common summary) with everything below it, plus the votes of tree(s*)
+  // on the quorum paths of both chains' children of s*, which all lie deeper than s*.
+  // Cost: the summary-chain distance plus those paths, instead of every vertex above the
+  // answer (tests/native/ts_vs_oracle.cpp compares it with the oracle's frontier walk).
   __host__ __device__ inline int32_t common_ancestor(const TsParams& P, const TsMem& M,
                                                      int32_t a, int32_t b) {
+    int32_t x = a, y = b, cx = -1, cy = -1;
+    while (!dead && X(P, M, x).height > X(P, M, y).height) {
+      cx = x;
+      x = psum(P, M, x);
+    }
+    while (!dead && X(P, M, y).height > X(P, M, x).height) {
+      cy = y;
+      y = psum(P, M, y);
+    }
+    while (!dead && x != y) {
+      cx = x;
+      x = psum(P, M, x);
+      cy = y;
+      y = psum(P, M, y);
+    }
+    if (dead) return 0;
+    const int32_t s = x;
+    if (cx < 0 || cy < 0) return s;  // one head is s* itself
+    const TVtx& bx = X(P, M, cx);
+    const TVtx& by = X(P, M, cy);
+    const int32_t* qx = Q(P, M, bx);
+    const int32_t* qy = Q(P, M, by);
+    // marks are scratch shared with reward() and apply(), which leave theirs set: clear the
+    // two path sets first (at most 2 k walks of at most k votes)
+    for (int32_t i = 0; i < bx.nq && !dead; ++i)
+      for (int32_t v = qx[i]; v != s && !dead; v = X(P, M, v).parent) MK(P, M, v) = 0;
+    for (int32_t i = 0; i < by.nq && !dead; ++i)
+      for (int32_t v = qy[i]; v != s && !dead; v = X(P, M, v).parent) MK(P, M, v) = 0;
+    for (int32_t i = 0; i < bx.nq && !dead; ++i)
+      for (int32_t v = qx[i]; v != s && !dead && !(MK(P, M, v) & 1u); v = X(P, M, v).parent)
+        MK(P, M, v) |= 1u;
+    int32_t best = s;
+    uint64_t bkey = fr_key(X(P, M, s).ddepth, s);
+    for (int32_t i = 0; i < by.nq && !dead; ++i)
+      for (int32_t v = qy[i]; v != s && !dead && !(MK(P, M, v) & 2u); v = X(P, M, v).parent) {
+        uint8_t& mk = MK(P, M, v);
+        if (mk & 1u) {  // shared: its ancestors up to s* are shared and shallower
+          const uint64_t kv = fr_key(X(P, M, v).ddepth, v);
+          if (kv > bkey) {
+            bkey = kv;
+            best = v;
+          }
+          break;
+        }
+        mk |= 2u;
+      }
+    return best;
+  }
+
+  // the frontier walk as the reference performs it (kept for reference and tests)
+  __host__ __device__ inline int32_t common_ancestor_walk(const TsParams& P, const TsMem& M,
+                                                          int32_t a, int32_t b) {
     int32_t* qa = M.fr;
     int32_t* qb = M.fr + 2 * NFR;
     int32_t na = 0, nb = 0;

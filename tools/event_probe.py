@@ -10,6 +10,8 @@ kernel time (HIP events) and activations/s.
   python tools/event_probe.py ts           k_ts_run_episodes: Tailstorm k=8 discount heuristic
                                            get-ahead, two agents, 10^4-activation loop tasks
                                            (BASELINE configs[3])
+  python tools/event_probe.py ts_exp       k_ts_run_episodes: the same on configs[3]'s exp(1)
+                                           clique variant (activation delay 10)
   python tools/event_probe.py bk_rollout   k_bk_rollout: 65,536 B_k k=8 lanes, table policy,
                                            64 lockstep steps (BASELINE configs[4])
   python tools/event_probe.py replay       cpr_replay: Nakamoto two-agents loop tasks from a
@@ -58,6 +60,16 @@ def main():
                                        policy=L.BK_POLICY_MINOR_DELAY, max_steps=2048, seed=1)
         out = fused(cfg, keep, 131072)
         out["kernel"] = "k_bk_run_episodes"
+    elif which == "ts_exp":
+        # configs[3]'s exp(1)-propagation variant: attacker + 1 defender, exponential links
+        cfg, keep = device.make_config(protocol=L.PROTO_TAILSTORM, alpha=0.0, gamma=0.0,
+                                       network=L.NET_EXP_CLIQUE, mode=L.MODE_LOOP, defenders=1,
+                                       activation_delay=10.0, propagation_delay=1.0,
+                                       activations=10000, k=8, reward_scheme=L.REWARD_DISCOUNT,
+                                       subblock_selection=L.SELECT_HEURISTIC,
+                                       policy=L.TS_POLICY_GET_AHEAD, seed=1)
+        out = fused(cfg, keep, 65536)
+        out["kernel"] = "k_ts_run_episodes"
     elif which == "ts":
         cfg, keep = device.make_config(protocol=L.PROTO_TAILSTORM, alpha=0.33,
                                        network=L.NET_TWO_AGENTS, mode=L.MODE_LOOP,

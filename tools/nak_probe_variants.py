@@ -11,6 +11,7 @@ the variants' results are meaningless; only their kernel times are read.
 usage: python tools/nak_probe_variants.py [name | name@gitrev ...]  (build/var/<name>.so;
        name@rev builds the csrc/ of that git revision, e.g. prev@HEAD)
 """
+import os
 import pathlib
 import shutil
 import subprocess
@@ -53,12 +54,13 @@ def variant(name, rng, log, rev=None):
         assert LOG_OLD in st
         st = st.replace(LOG_OLD, LOG_NEW, 1)
     (d / "cpr_stream.h").write_text(st)
-    obj = OUT / f"kernels_{name}.o"
+    tu = os.environ.get("PROBE_TU", "kernels.hip")  # the translation unit rebuilt
+    obj = OUT / f"{tu}_{name}.o"
     subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17",
                     "-ffp-contract=off", "-fPIC", f"-I{ROOT / 'include'}", "-c",
-                    str(d / "kernels.hip"), "-o", str(obj)], check=True)
+                    str(d / tu), "-o", str(obj)], check=True)
     objs = [str(obj)] + [str(p) for p in sorted((ROOT / "build" / "hip").glob("*.o"))
-                         if p.name != "kernels.hip.o"]
+                         if p.name != f"{tu}.o"]
     subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-shared", "-fPIC", *objs,
                     "-o", str(OUT / f"{name}.so")], check=True)
     shutil.rmtree(d)
