@@ -14,7 +14,7 @@ import pytest
 import oracle_py as O
 from cpr_amd import _lib as L
 from cpr_amd import device
-from test_trace import CONFIGS, check_withholding_record, withholding_traces
+from test_trace import CONFIGS, EXP_CONFIGS, check_withholding_record, withholding_traces
 
 pytestmark = pytest.mark.gpu
 
@@ -33,7 +33,8 @@ def _same(a, b, fields=FIELDS):
         assert len(bad) == 0, (f, int(bad[0]), a[f][bad[0]], b[f][bad[0]])
 
 
-@pytest.mark.parametrize("name,kw", CONFIGS, ids=[c[0] for c in CONFIGS])
+@pytest.mark.parametrize("name,kw", CONFIGS + EXP_CONFIGS,
+                         ids=[c[0] for c in CONFIGS + EXP_CONFIGS])
 def test_replay_keyed_trace_matches_oracle_and_keyed_run(ctx, name, kw):
     cfg, keep = device.make_config(**kw)
     n = 96

@@ -46,13 +46,36 @@ CONFIGS = [
 ]
 
 
+# the reference's policy-test network (exponential-delay clique, attacker on node 0),
+# keyed traces only (their oracle tasks draw from the keyed stream)
+EXP_CONFIGS = [
+    ("exp-nak-sm1", dict(protocol=L.PROTO_NAKAMOTO, alpha=0.0, gamma=0.0,
+                         network=L.NET_EXP_CLIQUE, mode=L.MODE_LOOP, defenders=2,
+                         activation_delay=2.0, propagation_delay=1.0, activations=300,
+                         policy=L.POLICY_SAPIRSHTEIN_2016_SM1, seed=21)),
+    ("exp-eth-fn19", dict(protocol=L.PROTO_ETHEREUM, alpha=0.0, gamma=0.0,
+                          network=L.NET_EXP_CLIQUE, mode=L.MODE_LOOP, defenders=2,
+                          activation_delay=2.0, propagation_delay=1.0, activations=300,
+                          policy=L.ETH_POLICY_FN19, seed=22)),
+    ("exp-bk", dict(protocol=L.PROTO_BK, k=4, alpha=0.0, gamma=0.0, network=L.NET_EXP_CLIQUE,
+                    mode=L.MODE_LOOP, defenders=1, activation_delay=5.0,
+                    propagation_delay=1.0, activations=300, policy=L.BK_POLICY_GET_AHEAD,
+                    seed=23)),
+    ("exp-ts", dict(protocol=L.PROTO_TAILSTORM, k=8, alpha=0.0, gamma=0.0,
+                    network=L.NET_EXP_CLIQUE, mode=L.MODE_LOOP, defenders=1,
+                    activation_delay=10.0, propagation_delay=1.0, activations=300,
+                    policy=L.TS_POLICY_GET_AHEAD, reward_scheme=L.REWARD_DISCOUNT, seed=24)),
+]
+
+
 def _assert_same(a, b):
     for f in FIELDS:
         bad = np.nonzero(a[f] != b[f])[0]
         assert len(bad) == 0, (f, int(bad[0]), a[f][bad[0]], b[f][bad[0]])
 
 
-@pytest.mark.parametrize("name,kw", CONFIGS, ids=[c[0] for c in CONFIGS])
+@pytest.mark.parametrize("name,kw", CONFIGS + EXP_CONFIGS,
+                         ids=[c[0] for c in CONFIGS + EXP_CONFIGS])
 def test_keyed_trace_replays_exactly(name, kw):
     cfg, _ = device.make_config(**kw)
     trace, rec = O.export_traces(cfg, 100, 12)
