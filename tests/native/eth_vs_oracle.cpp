@@ -5,7 +5,8 @@
 // after every step; loop-mode tasks on the two-agents network compared at the end; and the
 // lane in Nakamoto mode (P.nak) running Simulator.loop tasks on the selfish-mining network
 // with a nakamoto_ssz attacker (the withholding sweep's gamma-* tasks, incl. gamma = 0)
-// against the oracle's oracle_sm_task.
+// against the oracle's oracle_sm_task; and loop tasks on the exponential-delay clique
+// (Ethereum and Nakamoto mode) against the oracle's public entry.
 // Prints one JSON summary line; exit code 1 on any mismatch.
 #include <cmath>
 #include <cstdio>
@@ -15,6 +16,7 @@
 #include <vector>
 
 #include "../../cpr_amd/csrc/ethereum_lane.h"
+#include "../../include/cpr_hip.h"
 #include "../../oracle/src/ethereum.h"
 
 using namespace cpr;
@@ -34,7 +36,8 @@ struct Cfg {
                // 9 = a random table (CPR_ETH_POLICY_TABLE, loop tasks)
   int scheme;
   int steps;
-  int two_agents;  // 2: Nakamoto-mode loop task on the selfish-mining network
+  int two_agents;  // 2: Nakamoto-mode loop task on the selfish-mining network; 3 / 4: loop
+                   // task on the exponential-delay clique, Ethereum / Nakamoto mode
   double prop = 1e-9;
 };
 
@@ -43,6 +46,8 @@ extern "C" int oracle_sm_task(int rng_mode, void* rng, uint64_t seed, uint64_t e
                               int policy, int activations, int64_t* acts_out,
                               double* rewards_out, double* head_time, double* head_progress,
                               int32_t* head_height, int32_t* head_miner, uint32_t* diag);
+extern "C" int oracle_run_episodes(const cpr_config* c, uint64_t first, int64_t n,
+                                   cpr_episode_record* out, int threads);
 
 struct Counters {
   long episodes = 0, mismatches = 0, capacity = 0, steps = 0;
@@ -89,6 +94,17 @@ static eth::EthParams params_of(const Cfg& cf) {
   P.activations = cf.steps;
   P.max_progress = __builtin_inf();
   P.max_time = __builtin_inf();
+  if (cf.two_agents >= 3) {
+    // capi.hip validate_eth, CPR_NET_EXP_CLIQUE: equal compute, exponential links
+    P.d = cf.defenders;
+    P.n = P.d + 1;
+    P.net = 3;
+    P.nak = cf.two_agents == 4 ? 1 : 0;
+    P.policy = cf.policy;
+    P.t_att = oracle::alpha_threshold(1.0 / (double)P.n);
+    P.cap_e = 64 + 512 * P.n;
+    P.dmax = 0.0;
+  }
   return P;
 }
 
@@ -259,6 +275,56 @@ static bool run_sm_loop(const Cfg& cf, uint64_t seed, uint64_t ep, Counters& C,
   return true;
 }
 
+// a loop task on the exponential-delay clique (cpr_protocols.ml:478-485) through the oracle's
+// public entry (oracle_api.cpp attack_clique_task), compared on the final record
+static bool run_exp(const Cfg& cf, uint64_t seed, uint64_t ep, Counters& C, std::string& why) {
+  cpr_config c{};
+  c.protocol = cf.two_agents == 3 ? CPR_PROTO_ETHEREUM : CPR_PROTO_NAKAMOTO;
+  c.network = CPR_NET_EXP_CLIQUE;
+  c.mode = CPR_MODE_LOOP;
+  c.policy = cf.policy;
+  c.defenders = cf.defenders;
+  c.reward_scheme = cf.scheme;
+  c.activation_delay = 1.0;
+  c.propagation_delay = cf.prop;
+  c.activations = cf.steps;
+  c.seed = seed;
+  cpr_episode_record r{};
+  if (oracle_run_episodes(&c, ep, 1, &r, 1) != 0) {
+    why = "oracle_run_episodes failed";
+    C.mismatches++;
+    return false;
+  }
+  const eth::EthParams P = params_of(cf);
+  std::vector<uint8_t> mem(eth::eth_lane_bytes(P.cap_b, P.cap_e, P.n));
+  const eth::EthMem M = eth::eth_mem_at(mem.data(), P.cap_b, P.cap_e, P.n);
+  const Stream S{(uint32_t)seed, (uint32_t)(seed >> 32), (uint32_t)ep, (uint32_t)(ep >> 32)};
+  eth::EthLane L;
+  const int32_t hd = L.loop(P, S, M);
+  if (L.dead) {
+    C.capacity++;
+    return true;
+  }
+  const eth::EBlock& hb = L.B(P, M, hd);
+  C.episodes++;
+  C.steps += cf.steps;
+  if (hb.rew_att / 32.0 != r.reward_attacker || hb.rew_def / 32.0 != r.reward_defender ||
+      hb.height != r.head_height || hb.time != r.chain_time || L.c_act != r.n_activations ||
+      (cf.two_agents == 3 && hb.work != r.head_work)) {
+    char buf[400];
+    snprintf(buf, sizeof buf,
+             "exp clique lane (ra %.5f rd %.5f h %d w %d tm %.17g k %d) oracle (%.5f %.5f %d %d "
+             "%.17g %ld)",
+             hb.rew_att / 32.0, hb.rew_def / 32.0, hb.height, hb.work, hb.time, L.c_act,
+             r.reward_attacker, r.reward_defender, r.head_height, r.head_work, r.chain_time,
+             (long)r.n_activations);
+    why = buf;
+    C.mismatches++;
+    return false;
+  }
+  return true;
+}
+
 int main(int argc, char** argv) {
   const int eps = argc > 1 ? atoi(argv[1]) : 20;
   const int steps = argc > 2 ? atoi(argv[2]) : 200;
@@ -284,12 +350,21 @@ int main(int argc, char** argv) {
           const int d = std::max(2, (int)std::ceil(1.0 / (1.0 - g)));
           cfgs.push_back(Cfg{a, g, d, pol, 0, steps * 4, 2, prop});
         }
+  // exponential-delay cliques: Ethereum (ethereum_ssz policies, both schemes) and Nakamoto
+  // (nakamoto_ssz policies), fast and slow links
+  for (int d : {1, 3, 7})
+    for (double prop : {0.05, 0.6}) {
+      for (int pol : {0, 1, 2, 3, 4})
+        for (int sch : {0, 1}) cfgs.push_back(Cfg{0, 0, d, pol, sch, steps * 2, 3, prop});
+      for (int pol : {0, 1, 2, 3}) cfgs.push_back(Cfg{0, 0, d, pol, 0, steps * 2, 4, prop});
+    }
   Counters C;
   int shown = 0;
   for (auto& cf : cfgs)
     for (int e = 0; e < eps; e++) {
       std::string why;
-      const bool ok = cf.two_agents == 2   ? run_sm_loop(cf, seed, e, C, why)
+      const bool ok = cf.two_agents >= 3   ? run_exp(cf, seed, e, C, why)
+                      : cf.two_agents == 2 ? run_sm_loop(cf, seed, e, C, why)
                       : cf.two_agents == 1 ? run_loop(cf, seed, e, C, why)
                                            : run_gym(cf, seed, e, C, why);
       if (!ok && shown < 10) {

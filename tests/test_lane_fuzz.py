@@ -33,7 +33,9 @@ def test_ethereum_lane_matches_oracle_fuzz():
     # 5 policies + 2 random-action fuzzers x 2 reward schemes x alpha x gamma, and
     # Simulator.loop tasks on the two-agents network; plus the lane in Nakamoto mode on
     # Simulator.loop tasks of the selfish-mining network (withholding.ml gamma-* tasks,
-    # gamma 0 .. 0.9, defender delays 1e-4 and 0.05) against the oracle's oracle_sm_task
+    # gamma 0 .. 0.9, defender delays 1e-4 and 0.05) against the oracle's oracle_sm_task;
+    # and loop tasks on the exponential-delay clique (Ethereum and Nakamoto mode, 1..7
+    # defenders, mean link delay 0.05 and 0.6) against the oracle's public entry
     subprocess.run(["make", "-s", "-C", str(ROOT / "tests" / "native")], check=True)
     exe = ROOT / "tests" / "native" / "build" / "eth_vs_oracle"
     p = subprocess.run([str(exe), "6", "400"], capture_output=True, text=True, timeout=600)
