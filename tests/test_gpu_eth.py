@@ -182,7 +182,7 @@ def test_eth_table_policy_matches_oracle(ctx, mode):
                          max_steps=400, seed=0x7AB1E)
     else:
         cfg, keep = _cfg(alpha=0.35, network=L.NET_TWO_AGENTS, mode=L.MODE_LOOP,
-                         activations=3000, table=table, reward_scheme=L.REWARD_DISCOUNT,
+                         activations=1200, table=table, reward_scheme=L.REWARD_DISCOUNT,
                          seed=0x7AB1E)
     assert cfg.policy == L.ETH_POLICY_TABLE
     s, rec, ok = _compare(cfg, keep, 256)
