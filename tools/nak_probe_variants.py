@@ -7,12 +7,14 @@ the variants' results are meaningless; only their kernel times are read.
   cheap_log : fdlibm cpr_log -> (x - 1) (a negative number, so delays stay positive)
   cheap_both: both
   base      : the tree as it is
+  wavesN    : k_run_episodes compiled for N waves per SIMD instead of 4 (VGPR budget 512/N)
 
 usage: python tools/nak_probe_variants.py [name | name@gitrev ...]  (build/var/<name>.so;
        name@rev builds the csrc/ of that git revision, e.g. prev@HEAD)
 """
 import os
 import pathlib
+import re
 import shutil
 import subprocess
 import sys
@@ -54,6 +56,12 @@ def variant(name, rng, log, rev=None):
         assert LOG_OLD in st
         st = st.replace(LOG_OLD, LOG_NEW, 1)
     (d / "cpr_stream.h").write_text(st)
+    m = re.match(r"waves(\d+)", name)
+    if m:
+        k = (d / "kernels.hip").read_text()
+        assert "amdgpu_waves_per_eu(4)" in k
+        (d / "kernels.hip").write_text(k.replace("amdgpu_waves_per_eu(4)",
+                                                 f"amdgpu_waves_per_eu({m.group(1)})", 1))
     tu = os.environ.get("PROBE_TU", "kernels.hip")  # the translation unit rebuilt
     obj = OUT / f"{tu}_{name}.o"
     subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17",
