@@ -132,7 +132,7 @@ struct RerunLaunch {
 
 // all queued re-runs (count on the device) in one launch of `lanes` one-wave workgroups,
 // each with a lane region of lane_bytes at mem + i x lane_bytes; lds_bytes (the largest
-// eth_rest_bytes of the launches; used if <= 64 KB) puts all but the block ring in LDS
+// eth_rest_bytes of the launches, capped at 160 KiB) puts all but the block ring in LDS
 hipError_t launch_nak_exact_rerun(const RerunLaunch* launches, const int64_t* queue,
                                   const uint32_t* queue_n, int64_t queue_cap, uint8_t* mem,
                                   int64_t lane_bytes, int64_t lds_bytes, int64_t lanes,

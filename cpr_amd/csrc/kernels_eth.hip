@@ -5,6 +5,9 @@
 // visibility, event heap, scratch) reused for every episode it runs.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+#include <cstdlib>
+
 #include "../../include/cpr_hip.h"
 #include "ethereum_lane.h"
 #include "kernels.h"
@@ -130,12 +133,59 @@ __device__ inline void summary_add_episode(cpr_summary* out, int64_t ra, int64_t
   add(&out->hist[bin], 1);
 }
 
+// one queued episode on the lane region M (params P): the episode's own stream or trace
+__device__ inline int32_t nak_rerun_entry(const RerunLaunch& RL, int64_t e,
+                                          const eth::EthParams& P, const eth::EthMem& M,
+                                          eth::EthLane& L, uint32_t* miss) {
+  if (RL.is_trace) {
+    auto S = RL.tr.at(e);
+    const int32_t hd = nak_rerun_one(P, S, M, L);
+    *miss = TraceSource::missed(S);
+    return hd;
+  }
+  *miss = 0;
+  return nak_rerun_one(P, make_stream(RL.seed, RL.first + (uint64_t)e), M, L);
+}
+
+// the re-run episode's record and summary contribution (replacing the flagged ones)
+__device__ inline void nak_rerun_finish(const RerunLaunch& RL, int64_t e,
+                                        const eth::EthParams& P, const eth::EthMem& M,
+                                        eth::EthLane& L, int32_t hd, uint32_t flags) {
+  const uint32_t status = flags | L.status | CPR_ST_EXACT_RERUN;
+  const eth::EBlock& h = L.B(P, M, hd);
+  const int32_t ra = h.rew_att / 32, rd = h.rew_def / 32;  // 1 per block
+  const int64_t steps = P.mode == CPR_MODE_GYM ? L.steps : 0;
+  // the summary counts the flags the re-run resolved as OVERLAP / TIE only
+  summary_add_episode(
+      RL.sum, ra, rd, h.height, steps, L.c_act,
+      status & ~(uint32_t)(CPR_ST_DEEP_FORK | CPR_ST_TIE_UNRESOLVED | CPR_ST_STALE_TIME));
+  if (RL.recs) {
+    cpr_episode_record rc;
+    rc.reward_attacker = (double)ra;
+    rc.reward_defender = (double)rd;
+    rc.progress = (double)h.height;
+    rc.chain_time = h.time;
+    rc.sim_time = P.mode == CPR_MODE_GYM ? L.now : 0.0;
+    rc.n_steps = steps;
+    rc.n_activations = L.c_act;
+    rc.head_height = h.height;
+    rc.head_miner = P.mode == CPR_MODE_GYM ? h.miner : -1;
+    rc.status = status;
+    rc.head_work = 0;
+    RL.recs[e] = rc;
+  }
+}
+
 __global__ __launch_bounds__(64) void k_nak_exact_rerun(const RerunLaunch* launches,
                                                          const int64_t* queue,
                                                          const uint32_t* queue_n,
                                                          int64_t queue_cap, uint8_t* mem,
-                                                         int64_t lane_bytes, int lds) {
-  // the hot part of the lane region (visibility, event heap, scratch) in LDS when it fits
+                                                         int64_t lane_bytes, int64_t lds_bytes) {
+  // everything but the block ring (visibility, event heap, tips, scratch) in LDS. A lane
+  // whose heap capacity does not fit runs with the capacity that does (the heap's node
+  // order does not depend on it) and, only if its episode outgrows that, again in HBM.
+  // gamma = 0 re-runs are the case: +inf messages stay in the heap (ethereum_lane.h), a
+  // few thousand nodes, whose dependent walks are L2 round trips in HBM
   extern __shared__ __attribute__((aligned(128))) uint8_t lane_lds[];
   if (threadIdx.x != 0) return;
   int64_t nq = (int64_t)*queue_n;
@@ -147,52 +197,59 @@ __global__ __launch_bounds__(64) void k_nak_exact_rerun(const RerunLaunch* launc
     const int64_t e = (q >> 8) & 0xffffffffll;
     const uint32_t flags = (uint32_t)(q & 0xff);
     uint8_t* base = mem + (int64_t)blockIdx.x * lane_bytes;
-    const eth::EthMem M = lds ? eth::eth_mem_split(base, lane_lds, P.cap_b, P.cap_e, P.n)
-                              : eth::eth_mem_at(base, P.cap_b, P.cap_e, P.n);
-    eth::EthLane L;
-    int32_t hd;
-    uint32_t miss = 0;
-    if (RL.is_trace) {
-      const auto S = RL.tr.at(e);
-      hd = nak_rerun_one(P, S, M, L);
-      miss = TraceSource::missed(S);
-    } else {
-      hd = nak_rerun_one(P, make_stream(RL.seed, RL.first + (uint64_t)e), M, L);
+    // attempt 0: LDS (full or reduced heap capacity); attempt 1 (only after the reduced
+    // heap overflowed): the lane's HBM region
+    int32_t lds_cap_e = -1;  // heap capacity in LDS, -1 = HBM
+    if (lds_bytes > 0) {
+      const int64_t heap = eth::align128((int64_t)P.cap_e * 24);
+      const int64_t other = eth::eth_rest_bytes(P.cap_b, P.cap_e, P.n) - heap;
+      const int64_t room = (lds_bytes - other) / 128 * 128;
+      if (room >= heap)
+        lds_cap_e = P.cap_e;
+      else if (room >= 256 * 24)
+        lds_cap_e = (int32_t)(room / 24);
     }
-    const uint32_t status = flags | L.status | miss | CPR_ST_EXACT_RERUN;
-    const eth::EBlock& h = L.B(P, M, hd);
-    const int32_t ra = h.rew_att / 32, rd = h.rew_def / 32;  // 1 per block
-    const int64_t steps = P.mode == CPR_MODE_GYM ? L.steps : 0;
-    // the summary counts the flags the re-run resolved as OVERLAP / TIE only
-    summary_add_episode(
-        RL.sum, ra, rd, h.height, steps, L.c_act,
-        status & ~(uint32_t)(CPR_ST_DEEP_FORK | CPR_ST_TIE_UNRESOLVED | CPR_ST_STALE_TIME));
-    if (RL.recs) {
-      cpr_episode_record rc;
-      rc.reward_attacker = (double)ra;
-      rc.reward_defender = (double)rd;
-      rc.progress = (double)h.height;
-      rc.chain_time = h.time;
-      rc.sim_time = P.mode == CPR_MODE_GYM ? L.now : 0.0;
-      rc.n_steps = steps;
-      rc.n_activations = L.c_act;
-      rc.head_height = h.height;
-      rc.head_miner = P.mode == CPR_MODE_GYM ? h.miner : -1;
-      rc.status = status;
-      rc.head_work = 0;
-      RL.recs[e] = rc;
+    for (int attempt = lds_cap_e < 0 ? 1 : 0; attempt < 2; ++attempt) {
+      eth::EthParams PA = P;
+      if (attempt == 0) PA.cap_e = lds_cap_e;
+      const eth::EthMem M = attempt == 0
+                                ? eth::eth_mem_split(base, lane_lds, PA.cap_b, PA.cap_e, PA.n)
+                                : eth::eth_mem_at(base, P.cap_b, P.cap_e, P.n);
+      eth::EthLane L;
+      uint32_t miss = 0;
+      const int32_t hd = nak_rerun_entry(RL, e, PA, M, L, &miss);
+      if (attempt == 0 && L.dead == 2 && PA.cap_e < P.cap_e) continue;  // outgrew LDS
+      nak_rerun_finish(RL, e, P, M, L, hd, flags | miss);
+      break;
     }
   }
 }
+
+// LDS per one-wave workgroup: up to the whole 160 KiB of a CU when the launch needs it
+constexpr int64_t kRerunLdsMax = 160 * 1024;
 
 hipError_t launch_nak_exact_rerun(const RerunLaunch* launches, const int64_t* queue,
                                   const uint32_t* queue_n, int64_t queue_cap, uint8_t* mem,
                                   int64_t lane_bytes, int64_t lds_bytes, int64_t lanes,
                                   hipStream_t st) {
-  const int lds = lds_bytes > 0 && lds_bytes <= 64 * 1024 ? 1 : 0;
-  hipLaunchKernelGGL(k_nak_exact_rerun, dim3((unsigned)lanes), dim3(64),
-                     lds ? (size_t)lds_bytes : 0, st, launches, queue, queue_n, queue_cap, mem,
-                     lane_bytes, lds);
+  int64_t cap = kRerunLdsMax;
+  if (const char* v = getenv("CPR_RERUN_LDS_MAX"))  // tests: force the reduced-heap paths
+    cap = std::min<int64_t>(cap, std::max<int64_t>(0, atoll(v)));
+  int64_t lds = lds_bytes < cap ? lds_bytes : cap;
+  if (lds > 64 * 1024) {
+    static int64_t granted = -1;  // the attribute once per process
+    if (granted < 0)
+      granted = hipFuncSetAttribute((const void*)k_nak_exact_rerun,
+                                    hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    (int)kRerunLdsMax) == hipSuccess
+                    ? kRerunLdsMax
+                    : 64 * 1024;
+    (void)hipGetLastError();
+    if (lds > granted) lds = granted;
+  }
+  if (lds < 0) lds = 0;
+  hipLaunchKernelGGL(k_nak_exact_rerun, dim3((unsigned)lanes), dim3(64), (size_t)lds, st,
+                     launches, queue, queue_n, queue_cap, mem, lane_bytes, lds);
   return hipGetLastError();
 }
 

@@ -134,6 +134,26 @@ def test_overlapping_windows_rerun_exactly(ctx, alpha, policy, table):
     assert s.status_other == 0
 
 
+@pytest.mark.parametrize("lds_max", [None, 40960])
+def test_gamma0_reruns_exact_with_lds_heap(ctx, lds_max, monkeypatch):
+    # gamma = 0 re-runs keep the +inf messages in the event heap (thousands of nodes in a
+    # 2016-step episode): the re-run kernel holds the heap in LDS with the capacity that
+    # fits and re-runs an episode that outgrows it in HBM (kernels_eth.hip). 40 KiB of LDS
+    # forces both paths; every record must equal the oracle's
+    if lds_max is not None:
+        monkeypatch.setenv("CPR_RERUN_LDS_MAX", str(lds_max))
+    cfg, keep = device.make_config(alpha=0.45, gamma=0.0, policy=L.POLICY_SAPIRSHTEIN_2016_SM1,
+                                   max_steps=2016, seed=0x0E70, propagation_delay=0.05)
+    b = device.Batch(cfg, ctx=ctx, keep=keep)
+    s, rec = b.run(192, first_episode=0, records=True)
+    ref = O.run_episodes(cfg, 0, 192, threads=8)
+    assert _records_equal(rec, ref) == {}
+    flagged = (rec["status"] & L.ST_EXACT_RERUN) != 0
+    assert flagged.sum() > 50, int(flagged.sum())
+    assert not (rec["status"] & L.ST_CAPACITY).any()
+    assert s.episodes == 192
+
+
 def test_gym_overlaps_at_the_reference_delay(ctx):
     # at the gym's own 1e-9 delay overlaps are rare (~1 per 5e8 activations at gamma 0.5);
     # whatever the device flags in 2^16 full episodes was re-run and matches the oracle
