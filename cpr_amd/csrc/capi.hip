@@ -116,6 +116,7 @@ struct cpr_batch {
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   double last_ms = 0.0;
   int64_t last_acts = 0;
+  int64_t last_lanes = 0, last_resident = 0;  // cpr_launch_shape
 };
 
 extern "C" {
@@ -455,13 +456,15 @@ static int validate_eth(const cpr_config* c, eth::EthParams* P) {
   while (cb < span && cb < (1 << 15)) cb <<= 1;
   P->cap_b = cb;
   // gamma = 0: messages at t = +inf stay in the skew heap (they shape its tie order);
-  // Simulator.loop tasks on the selfish-mining network: a release shares every withheld
-  // block at once, d messages each, and loop tasks at alpha near 0.5 withhold thousands
+  // otherwise an attacker release shares every withheld block at once, d messages each
+  // (a 300-block release at alpha .45, gamma .9 overflowed 512 events per node), and each
+  // block is released at most once: d messages per block of the episode bound the heap
   int64_t extra = 0;
+  const int64_t ext = P->mode == CPR_MODE_LOOP ? span : std::min<int64_t>(span, 8192);
   if (P->net == 0 && !std::isfinite(P->dmax))
-    extra = 2 * (int64_t)P->d * (P->mode == CPR_MODE_LOOP ? span : std::min<int64_t>(span, 8192));
-  else if (P->net == 0 && P->mode == CPR_MODE_LOOP)
-    extra = (int64_t)P->d * span;
+    extra = 2 * (int64_t)P->d * ext;
+  else if (P->net == 0 || P->net == 3)
+    extra = (int64_t)P->d * ext;
   P->cap_e = 64 + 512 * P->n + (int32_t)std::min<int64_t>(extra, 1 << 24);
   return CPR_OK;
 }
@@ -749,6 +752,25 @@ int cpr_batch_create(cpr_ctx* ctx, const cpr_config* cfg, cpr_batch** out) {
   return CPR_OK;
 }
 
+int cpr_launch_shape(cpr_batch* b, int64_t* lanes, int64_t* resident) {
+  if (!b) return fail(CPR_E_INVALID_ARG, "NULL argument");
+  if (lanes) *lanes = b->last_lanes;
+  if (resident) *resident = b->last_resident;
+  return CPR_OK;
+}
+
+int cpr_rerun_hbm_retries(cpr_ctx* c, int64_t* retries) {
+  if (!c || !retries) return fail(CPR_E_INVALID_ARG, "NULL argument");
+  *retries = 0;
+  if (!c->rq.p) return CPR_OK;
+  HIP_TRY(hipSetDevice(c->device));
+  uint32_t v = 0;
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  HIP_TRY(hipMemcpy(&v, (char*)c->rq.p + (size_t)kRerunQueue * 8 + 4, 4, hipMemcpyDeviceToHost));
+  *retries = v;
+  return CPR_OK;
+}
+
 int cpr_last_launch(cpr_batch* b, double* kernel_ms, int64_t* activations) {
   if (!b) return fail(CPR_E_INVALID_ARG, "NULL argument");
   if (b->async_launch) {  // cpr_run_episodes_async: the caller has synchronized
@@ -821,14 +843,16 @@ static int flush_reruns(cpr_ctx* c) {
   return CPR_OK;
 }
 
-// Ethereum lanes: resident capacity bounded by a 32 GiB budget for the per-lane regions
+// Ethereum lanes: resident capacity bounded by kLaneBudget for the per-lane regions
 static int run_async_eth(cpr_batch* b, int64_t n, uint64_t first, const TraceSource* tr,
                          cpr_summary* sum_dev, cpr_episode_record* rec_dev) {
   const int64_t full = (int64_t)b->ctx->cus * eth_blocks_per_cu() * 256;
-  const int64_t budget = (int64_t)(32ll << 30) / b->eth_bytes;
+  const int64_t budget = kLaneBudget / b->eth_bytes;
   int64_t lanes = std::min(full, std::max<int64_t>(256, budget));
   lanes = std::min(lanes, ((n + 255) / 256) * 256);
   lanes = std::max<int64_t>(256, (lanes / 256) * 256);
+  b->last_lanes = lanes;
+  b->last_resident = full;
   void* mem = nullptr;
   HIP_TRY(ctx_pool(b->ctx, (size_t)lanes * (size_t)b->eth_bytes, &mem));
   if (!b->ev0) {
@@ -846,7 +870,7 @@ static int run_async_eth(cpr_batch* b, int64_t n, uint64_t first, const TraceSou
   return CPR_OK;
 }
 
-// B_k lanes: resident capacity bounded by a 32 GiB budget for the per-lane regions
+// B_k / Tailstorm lanes: resident capacity bounded by kLaneBudget for the per-lane regions
 static int run_async_bk(cpr_batch* b, int64_t n, uint64_t first, const TraceSource* tr,
                         cpr_summary* sum_dev, cpr_episode_record* rec_dev) {
   const bool tsp = b->cfg.protocol == CPR_PROTO_TAILSTORM;
@@ -855,6 +879,8 @@ static int run_async_bk(cpr_batch* b, int64_t n, uint64_t first, const TraceSour
   int64_t lanes = std::min(full, std::max<int64_t>(256, budget));
   lanes = std::min(lanes, ((n + 255) / 256) * 256);
   lanes = std::max<int64_t>(256, (lanes / 256) * 256);
+  b->last_lanes = lanes;
+  b->last_resident = full;
   void* pool = nullptr;
   HIP_TRY(ctx_pool(b->ctx, (size_t)lanes * (size_t)b->bk_bytes, &pool));
   if (!b->ev0) {
@@ -903,6 +929,8 @@ static int run_async(cpr_batch* b, int64_t n, uint64_t first, const TraceSource*
     return run_async_eth(b, n, first, tr, sum_dev, rec_dev);
   if (b->is_ev) return run_async_bk(b, n, first, tr, sum_dev, rec_dev);
   const int64_t lanes = episode_lanes(b, n);
+  b->last_lanes = lanes;
+  b->last_resident = (int64_t)b->ctx->cus * run_episodes_blocks_per_cu(b->cfg.mode) * 256;
   // spill [lane][cap] f64 mining times | tie-replay scratch [lane]
   const size_t o_replay = align256((size_t)lanes * b->P.cap * sizeof(double));
   void* pool = nullptr;
@@ -924,7 +952,8 @@ static int run_async(cpr_batch* b, int64_t n, uint64_t first, const TraceSource*
     }
     if (!c->rq.p) {
       HIP_TRY(c->rq.ensure((size_t)kRerunQueue * 8 + 64));
-      HIP_TRY(hipMemsetAsync((char*)c->rq.p + (size_t)kRerunQueue * 8, 0, 4, c->stream));
+      // launch counter and the cumulative HBM-retry counter (cpr_rerun_hbm_retries)
+      HIP_TRY(hipMemsetAsync((char*)c->rq.p + (size_t)kRerunQueue * 8, 0, 8, c->stream));
     }
     RerunLaunch rl;
     memset(&rl, 0, sizeof(rl));
@@ -1708,6 +1737,13 @@ int cpr_rollout(cpr_batch* b, int64_t n_steps, double* obs, double* reward, uint
   b->last_ms = ms;
   b->last_acts = s.activations;
   b->reset_done = true;
+  // rollout lanes are the batch's n_lanes (one thread each, 256-thread workgroups); the
+  // resident figure is the fused-episode kernel's occupancy of the same lane
+  b->last_lanes = b->cfg.n_lanes;
+  b->last_resident = (int64_t)b->ctx->cus * 256 *
+                     (b->is_eth ? eth_blocks_per_cu()
+                                : (b->cfg.protocol == CPR_PROTO_TAILSTORM ? ts_blocks_per_cu()
+                                                                          : bk_blocks_per_cu()));
   summary->episodes += s.episodes;
   summary->steps += s.steps;
   summary->activations += s.activations;

@@ -5,6 +5,8 @@
 // visibility, event heap, scratch) reused for every episode it runs.
 #include <hip/hip_runtime.h>
 
+#include <atomic>
+
 #include <algorithm>
 #include <cstdlib>
 
@@ -218,7 +220,10 @@ __global__ __launch_bounds__(64) void k_nak_exact_rerun(const RerunLaunch* launc
       eth::EthLane L;
       uint32_t miss = 0;
       const int32_t hd = nak_rerun_entry(RL, e, PA, M, L, &miss);
-      if (attempt == 0 && L.dead == 2 && PA.cap_e < P.cap_e) continue;  // outgrew LDS
+      if (attempt == 0 && L.dead == 2 && PA.cap_e < P.cap_e) {  // outgrew LDS: count, redo
+        atomicAdd(const_cast<uint32_t*>(queue_n) + 1, 1u);  // cpr_rerun_hbm_retries
+        continue;
+      }
       nak_rerun_finish(RL, e, P, M, L, hd, flags | miss);
       break;
     }
@@ -237,15 +242,23 @@ hipError_t launch_nak_exact_rerun(const RerunLaunch* launches, const int64_t* qu
     cap = std::min<int64_t>(cap, std::max<int64_t>(0, atoll(v)));
   int64_t lds = lds_bytes < cap ? lds_bytes : cap;
   if (lds > 64 * 1024) {
-    static int64_t granted = -1;  // the attribute once per process
-    if (granted < 0)
-      granted = hipFuncSetAttribute((const void*)k_nak_exact_rerun,
-                                    hipFuncAttributeMaxDynamicSharedMemorySize,
-                                    (int)kRerunLdsMax) == hipSuccess
-                    ? kRerunLdsMax
-                    : 64 * 1024;
-    (void)hipGetLastError();
-    if (lds > granted) lds = granted;
+    // the attribute is per device: granted LDS cached per device id (0 = not yet asked),
+    // concurrent first callers may both ask, which is harmless
+    static std::atomic<int64_t> granted[64];
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    std::atomic<int64_t>& g = granted[dev & 63];
+    int64_t have = g.load(std::memory_order_acquire);
+    if (have == 0) {
+      have = hipFuncSetAttribute((const void*)k_nak_exact_rerun,
+                                 hipFuncAttributeMaxDynamicSharedMemorySize,
+                                 (int)kRerunLdsMax) == hipSuccess
+                 ? kRerunLdsMax
+                 : 64 * 1024;
+      (void)hipGetLastError();
+      g.store(have, std::memory_order_release);
+    }
+    if (lds > have) lds = have;
   }
   if (lds < 0) lds = 0;
   hipLaunchKernelGGL(k_nak_exact_rerun, dim3((unsigned)lanes), dim3(64), (size_t)lds, st,

@@ -19,7 +19,14 @@
 //                            and its own reward list summed per node (compare_blocks)
 //   drafts [cap_d][k+2] i32  outstanding summary drafts (tag, #leaves, leaves)
 //   heap   [cap_e] x 24 B    event queue (skew heap, +inf events kept)
-//   tips [n] i32, pend [NPEND] i32 (pending released messages), marks [cap_v] u8, scratch
+//   tips [n] i32, pend [cap_v] i32 (pending released messages), marks [cap_v] u8,
+//   shead [cap_v] i32 (per summary: newest child summary), tree scratch [cap_v] each
+//
+// Tree bookkeeping is incremental: every summary heads a newest-first list of its votes
+// (TVtx.thead / TVtx.next) and of its child summaries (shead / TVtx.next), so the tree
+// scans (count_post, tree, payload_parent, has_children, MadeVisible children, summary
+// dedup) cost the tree's size, not every vertex appended since the summary, and the
+// scratch holds a whole ring window: no tree size is capped below the vertex ring.
 //
 // Reference map: simulator.ml:122-543, tailstorm.ml:86-609, tailstorm_ssz.ml:162-446,
 // combinatorics.ml:5-32, engine.ml:97-249.
@@ -68,7 +75,9 @@ struct TVtx {
   int32_t qslot;   // summary: quorum / reward slot; -1 genesis
   int32_t nq;      // summary: number of leaves
   double time;     // Simulator.timestamp = append time
-  int32_t _pad[2];
+  int32_t next;    // vote: next older vote of the same tree; summary: next older summary
+                   // with the same parent summary (-1 ends either list)
+  int32_t thead;   // summary: newest vote of its tree (-1 none)
 };
 static_assert(sizeof(TVtx) == 64, "TVtx layout");
 
@@ -88,12 +97,7 @@ struct TsParams {
   int32_t table_dim;
 };
 
-constexpr int32_t NQS = 512;     // votes of one summary tree handled at once; a larger
-                                  // withheld tree flags CPR_ST_CAPACITY (its quadratic
-                                  // tree scans would stall the wave for minutes)
-constexpr int32_t NSTACK = 1024; // share stack
-constexpr int32_t NPEND = 1024;  // pending released messages
-constexpr int32_t NFR = 64;      // common-ancestor frontier
+constexpr int32_t NFR = 64;      // common-ancestor frontier (reference walk, tests only)
 
 struct TsMem {
   TVtx* vtx;
@@ -106,13 +110,15 @@ struct TsMem {
   int32_t* tips;
   int32_t* pend;
   uint8_t* marks;   // [cap_v]
-  int32_t* cand;    // [NQS] tree votes, ascending serial
-  int32_t* perm;    // [NQS] indices into cand in BlockSet order (Dag depth, serial)
-  int32_t* aux;     // [NQS] scratch indices
-  uint8_t* flag;    // [NQS]
-  uint8_t* flag2;   // [NQS]
-  uint64_t* key;    // [NQS] sort keys
-  int32_t* stack;   // [NSTACK]
+  int32_t* shead;   // [cap_v] per summary slot: newest child summary
+  int32_t* pos;     // [cap_v] per vertex slot: index in cand while a tree is held
+  int32_t* cand;    // [cap_v] tree votes, ascending serial
+  int32_t* perm;    // [cap_v] indices into cand in BlockSet order (Dag depth, serial)
+  int32_t* aux;     // [cap_v] scratch indices
+  uint8_t* flag;    // [cap_v]
+  uint8_t* flag2;   // [cap_v]
+  uint64_t* key;    // [cap_v] sort keys / merge-sort buffer
+  int32_t* stack;   // [2 cap_v]
   int32_t* fr;      // [4 * NFR] two frontiers of (ddepth, serial)
   int64_t* nact = nullptr;  // per-node activations (cpr_node_outputs), else null
 };
@@ -123,9 +129,10 @@ __host__ __device__ inline int64_t ts_lane_bytes(const TsParams& P) {
   return ts_align((int64_t)P.cap_v * 64) + ts_align((int64_t)P.cap_v * P.n) +
          ts_align((int64_t)P.cap_v * P.n * 8) + ts_align((int64_t)P.cap_q * (P.k + 1) * 4) +
          ts_align((int64_t)P.cap_q * 2 * P.n * 8) + ts_align((int64_t)P.cap_d * (P.k + 2) * 4) +
-         ts_align((int64_t)P.cap_e * 24) + ts_align((int64_t)P.n * 4) + ts_align(NPEND * 4) +
-         ts_align(P.cap_v) + 3 * ts_align(NQS * 4) + 2 * ts_align(NQS) + ts_align(NQS * 8) +
-         ts_align(NSTACK * 4) + ts_align(4 * NFR * 4);
+         ts_align((int64_t)P.cap_e * 24) + ts_align((int64_t)P.n * 4) +
+         ts_align((int64_t)P.cap_v * 4) + ts_align(P.cap_v) + 5 * ts_align((int64_t)P.cap_v * 4) +
+         2 * ts_align(P.cap_v) + ts_align((int64_t)P.cap_v * 8) +
+         ts_align((int64_t)P.cap_v * 8) + ts_align(4 * NFR * 4);
 }
 
 __host__ __device__ inline TsMem ts_mem_at(uint8_t* base, const TsParams& P) {
@@ -144,15 +151,17 @@ __host__ __device__ inline TsMem ts_mem_at(uint8_t* base, const TsParams& P) {
   M.drafts = (int32_t*)take((int64_t)P.cap_d * (P.k + 2) * 4);
   M.heap = (HNode*)take((int64_t)P.cap_e * 24);
   M.tips = (int32_t*)take((int64_t)P.n * 4);
-  M.pend = (int32_t*)take(NPEND * 4);
+  M.pend = (int32_t*)take((int64_t)P.cap_v * 4);
   M.marks = take(P.cap_v);
-  M.cand = (int32_t*)take(NQS * 4);
-  M.perm = (int32_t*)take(NQS * 4);
-  M.aux = (int32_t*)take(NQS * 4);
-  M.flag = take(NQS);
-  M.flag2 = take(NQS);
-  M.key = (uint64_t*)take(NQS * 8);
-  M.stack = (int32_t*)take(NSTACK * 4);
+  M.shead = (int32_t*)take((int64_t)P.cap_v * 4);
+  M.pos = (int32_t*)take((int64_t)P.cap_v * 4);
+  M.cand = (int32_t*)take((int64_t)P.cap_v * 4);
+  M.perm = (int32_t*)take((int64_t)P.cap_v * 4);
+  M.aux = (int32_t*)take((int64_t)P.cap_v * 4);
+  M.flag = take(P.cap_v);
+  M.flag2 = take(P.cap_v);
+  M.key = (uint64_t*)take((int64_t)P.cap_v * 8);
+  M.stack = (int32_t*)take((int64_t)P.cap_v * 8);
   M.fr = (int32_t*)take(4 * NFR * 4);
   return M;
 }
@@ -247,6 +256,7 @@ struct TsLane {
   int32_t zt, dseq;
   int32_t pub, priv, npend;
   int32_t o_pub, o_priv, o_common, o_event;
+  int32_t troot;  // summary whose tree cand[] holds
   int64_t steps;
 
   // ------------------------------------------------------------------ storage
@@ -406,63 +416,80 @@ struct TsLane {
     if (a.depth != b.depth) return a.depth > b.depth;
     return pow_key(a) < pow_key(b);
   }
-  __host__ __device__ inline int32_t index_of(const TsMem& M, int32_t n, int32_t s) {
-    int32_t lo = 0, hi = n - 1;
-    while (lo <= hi) {
-      const int32_t mid = (lo + hi) >> 1;
-      const int32_t v = M.cand[mid];
-      if (v == s) return mid;
-      if (v < s) lo = mid + 1; else hi = mid - 1;
-    }
-    return -1;
+  // slot-indexed tree position: valid for s iff pos names a cand entry holding s
+  __host__ __device__ inline int32_t& PS(const TsParams& P, const TsMem& M, int32_t s) {
+    return M.pos[s & (P.cap_v - 1)];
+  }
+  __host__ __device__ inline int32_t& SH(const TsParams& P, const TsMem& M, int32_t s) {
+    return M.shead[s & (P.cap_v - 1)];
+  }
+  __host__ __device__ inline bool in_tree(const TsParams& P, const TsMem& M, int32_t n,
+                                          int32_t s) {
+    const int32_t i = PS(P, M, s);
+    return i >= 0 && i < n && M.cand[i] == s;
   }
   // votes of summary b's tree visible at `node` into cand[] (ascending serial): the
   // expansion acc_votes children' (children' b) with children' = children |> filter vf when
   // `restrict` (tailstorm.ml:509-535), else all of confirming_votes b; perm[] = BlockSet
-  // order (Dag depth, serial)
+  // order (Dag depth, serial). The candidate set is ancestor-closed down to b (a vote enters
+  // only through its parent), so walks from a candidate end at b. pos[] maps back.
   __host__ __device__ inline int32_t tree(const TsParams& P, const TsMem& M, int32_t b,
                                           int32_t node, int32_t vf) {
     int32_t n = 0;
-    for (int32_t c = b + 1; c <= newest && !dead; ++c) {
+    const int32_t cap = P.cap_v;
+    troot = b;
+    for (int32_t c = X(P, M, b).thead; c >= 0 && !dead; c = X(P, M, c).next) {
       const uint8_t v = V(P, M, c, node);
       if ((v & V_KIND) == V_INV) continue;
-      const TVtx& x = X(P, M, c);
-      if (!x.vote || x.sum != b) continue;
-      if (vf != VF_ALL) {
-        if (!keep_kind(v, vf, false)) continue;
-        if (x.parent != b && index_of(M, n, x.parent) < 0) continue;
-      }
-      if (n >= NQS) {
+      if (vf != VF_ALL && !keep_kind(v, vf, false)) continue;
+      if (n >= cap) {
         fail(3);
         return 0;
       }
       M.cand[n++] = c;
     }
-    // stable insertion by Dag depth (cand is serial-ascending)
-    for (int32_t i = 0; i < n; ++i) {
-      const int32_t dd = X(P, M, M.cand[i]).ddepth;
-      int32_t j = i;
-      while (j > 0 && X(P, M, M.cand[M.perm[j - 1]]).ddepth > dd) {
-        M.perm[j] = M.perm[j - 1];
-        --j;
-      }
-      M.perm[j] = i;
+    if (dead) return 0;
+    for (int32_t i = 0, j = n - 1; i < j; ++i, --j) {  // newest-first list -> ascending
+      const int32_t t = M.cand[i];
+      M.cand[i] = M.cand[j];
+      M.cand[j] = t;
     }
-    return n;
+    int32_t m = 0, maxd = 0;
+    for (int32_t i = 0; i < n; ++i) {
+      const int32_t c = M.cand[i];
+      const TVtx& x = X(P, M, c);
+      if (vf != VF_ALL && x.parent != b && !in_tree(P, M, m, x.parent)) continue;
+      PS(P, M, c) = m;
+      M.cand[m++] = c;
+      maxd = x.depth > maxd ? x.depth : maxd;
+    }
+    // Dag depth of a tree vote = depth(b) + its vote depth: stable counting sort by vote
+    // depth over the serial-ascending cand gives (Dag depth, serial)
+    if (maxd + 2 > cap) {
+      fail(3);
+      return 0;
+    }
+    int32_t* cnt = M.aux;  // [maxd + 2] <= cap_v
+    for (int32_t d = 0; d <= maxd + 1; ++d) cnt[d] = 0;
+    for (int32_t i = 0; i < m; ++i) ++cnt[X(P, M, M.cand[i]).depth + 1];
+    for (int32_t d = 1; d <= maxd + 1; ++d) cnt[d] += cnt[d - 1];
+    for (int32_t i = 0; i < m; ++i) M.perm[cnt[X(P, M, M.cand[i]).depth]++] = i;
+    return m;
   }
   // votes of summary b's tree at `node` passing `vf` after expansion (compare_blocks,
   // observe): count and max depth
   __host__ __device__ inline int32_t count_post(const TsParams& P, const TsMem& M, int32_t b,
                                                 int32_t node, int32_t vf, int32_t* maxd) {
     int32_t n = 0, d = 0;
-    for (int32_t c = b + 1; c <= newest && !dead; ++c) {
-      const uint8_t v = V(P, M, c, node);
-      if ((v & V_KIND) == V_INV) continue;
+    for (int32_t c = X(P, M, b).thead; c >= 0 && !dead;) {
       const TVtx& x = X(P, M, c);
-      if (!x.vote || x.sum != b) continue;
-      if (!keep_kind(v, vf, vf == VF_PUBLIC_OR_MARKED && MK(P, M, c))) continue;
-      ++n;
-      d = x.depth > d ? x.depth : d;
+      const uint8_t v = V(P, M, c, node);
+      if ((v & V_KIND) != V_INV &&
+          keep_kind(v, vf, vf == VF_PUBLIC_OR_MARKED && MK(P, M, c))) {
+        ++n;
+        d = x.depth > d ? x.depth : d;
+      }
+      c = x.next;
     }
     if (maxd) *maxd = d;
     return n;
@@ -472,26 +499,47 @@ struct TsLane {
     const uint8_t kd = V(P, M, s, node) & V_KIND;
     return kd == V_WH || kd == V_REL;
   }
+  // stable bottom-up merge sort of a[0, n) with `before` (strict); tmp holds n entries
+  template <class F>
+  __host__ __device__ static inline void msort(int32_t* a, int32_t* tmp, int32_t n, F before) {
+    int32_t* src = a;
+    int32_t* dst = tmp;
+    for (int32_t w = 1; w < n; w <<= 1) {
+      for (int32_t lo = 0; lo < n; lo += 2 * w) {
+        const int32_t mid = lo + w < n ? lo + w : n, hi = lo + 2 * w < n ? lo + 2 * w : n;
+        int32_t i = lo, j = mid, o = lo;
+        while (i < mid && j < hi) dst[o++] = before(src[j], src[i]) ? src[j++] : src[i++];
+        while (i < mid) dst[o++] = src[i++];
+        while (j < hi) dst[o++] = src[j++];
+      }
+      int32_t* t = src;
+      src = dst;
+      dst = t;
+    }
+    if (src != a)
+      for (int32_t i = 0; i < n; ++i) a[i] = src[i];
+  }
 
-  // writes the draft's leaves (sorted by compare_votes_in_block) to q; returns #leaves or 0
+  // writes the draft's leaves (sorted by compare_votes_in_block) to q; returns #leaves or 0.
+  // The included set is ancestor-closed (a branch enters with all its votes), so a walk up
+  // from a candidate counts its fresh votes until the first included one, and a candidate
+  // whose vote depth exceeds the deepest included vote by more than `need` cannot fit.
   __host__ __device__ inline int32_t heuristic(const TsParams& P, const TsMem& M, int32_t node,
                                                int32_t n, int32_t* q) {
     // flag = included
     for (int32_t i = 0; i < n; ++i) M.flag[i] = 0;
-    int32_t need = P.k, nl = 0;
+    int32_t need = P.k, nl = 0, dinc = 0;
     while (need > 0 && !dead) {
       int32_t best = -1, bo = -1, bt = -1;
       for (int32_t pi = 0; pi < n; ++pi) {
         const int32_t i = M.perm[pi];
         if (M.flag[i]) continue;
+        if (X(P, M, M.cand[i]).depth - dinc > need) continue;
         int32_t own = 0, tot = 0, s = M.cand[i];
-        for (;;) {
-          const int32_t j = index_of(M, n, s);
-          if (j < 0) break;
-          if (!M.flag[j]) {
-            ++tot;
-            own += mine(P, M, s, node) ? 1 : 0;
-          }
+        while (s != troot) {
+          if (M.flag[PS(P, M, s)]) break;
+          if (++tot > need) break;
+          own += mine(P, M, s, node) ? 1 : 0;
           s = X(P, M, s).parent;
         }
         if (tot > need) continue;
@@ -507,13 +555,13 @@ struct TsLane {
       }
       q[nl++] = M.cand[best];
       int32_t s = M.cand[best];
-      for (;;) {
-        const int32_t j = index_of(M, n, s);
-        if (j < 0) break;
-        if (!M.flag[j]) {
-          M.flag[j] = 1;
-          --need;
-        }
+      const int32_t db = X(P, M, s).depth;
+      dinc = db > dinc ? db : dinc;
+      while (s != troot) {
+        uint8_t& f = M.flag[PS(P, M, s)];
+        if (f) break;
+        f = 1;
+        --need;
         s = X(P, M, s).parent;
       }
     }
@@ -531,32 +579,22 @@ struct TsLane {
       if (ox != oy) return ox < oy;
       return VT(P, M, x.serial, node) < VT(P, M, y.serial, node);
     };
-    for (int32_t i = 1; i < n; ++i) {
-      const int32_t v = M.aux[i];
-      int32_t j = i;
-      while (j > 0 && before(v, M.aux[j - 1])) {
-        M.aux[j] = M.aux[j - 1];
-        --j;
-      }
-      M.aux[j] = v;
-    }
-    for (int32_t i = 0; i < n; ++i) M.flag[i] = 0;  // acc
+    msort(M.aux, (int32_t*)M.key, n, before);
+    for (int32_t i = 0; i < n; ++i) M.flag[i] = 0;  // acc (ancestor-closed)
     int32_t cnt = 0, nl = 0;
     for (int32_t t = 0; t < n && cnt < P.k && !dead; ++t) {
       const int32_t hd = M.aux[t];
       int32_t nf = 0, s = M.cand[hd];
-      for (;;) {
-        const int32_t j = index_of(M, n, s);
-        if (j < 0) break;
-        nf += M.flag[j] ? 0 : 1;
+      while (s != troot && cnt + nf <= P.k) {
+        if (M.flag[PS(P, M, s)]) break;
+        ++nf;
         s = X(P, M, s).parent;
       }
       if (cnt + nf > P.k || nf < 1) continue;
-      s = M.cand[hd];
-      for (;;) {
-        const int32_t j = index_of(M, n, s);
-        if (j < 0) break;
-        M.flag[j] = 1;
+      for (s = M.cand[hd]; s != troot;) {
+        uint8_t& f = M.flag[PS(P, M, s)];
+        if (f) break;
+        f = 1;
         s = X(P, M, s).parent;
       }
       cnt += nf;
@@ -572,11 +610,10 @@ struct TsLane {
     const bool discount = P.scheme == SC_DISCOUNT || P.scheme == SC_HYBRID;
     const int32_t upto = punish ? 1 : nl;
     for (int32_t t = 0; t < upto; ++t) {
-      int32_t s = lv[t];
-      for (;;) {
-        const int32_t j = index_of(M, n, s);
-        if (j < 0) break;
-        M.flag2[j] = 1;
+      for (int32_t s = lv[t]; s != troot;) {
+        uint8_t& f = M.flag2[PS(P, M, s)];
+        if (f) break;
+        f = 1;
         s = X(P, M, s).parent;
       }
     }
@@ -622,8 +659,8 @@ struct TsLane {
       bool ok = true;
       for (int32_t t = 0; t < P.k && ok; ++t) {
         const TVtx& x = X(P, M, M.cand[M.perm[c[t]]]);
-        const int32_t ji = index_of(M, n, x.parent);
-        if (ji >= 0) {  // vote parent (summary parents are filtered out)
+        if (x.parent != troot) {  // vote parent (summary parents are filtered out)
+          const int32_t ji = PS(P, M, x.parent);
           const int32_t ip = M.aux[ji];
           M.flag2[ip] = 0;
           ok = M.flag[ip] != 0;
@@ -698,11 +735,10 @@ struct TsLane {
   __host__ __device__ inline int32_t payload_parent(const TsParams& P, const TsMem& M,
                                                     int32_t node, int32_t b) {
     int32_t best = b;
-    for (int32_t c = b + 1; c <= newest && !dead; ++c) {
-      if (!visible(P, M, c, node)) continue;
+    for (int32_t c = X(P, M, b).thead; c >= 0 && !dead;) {
       const TVtx& x = X(P, M, c);
-      if (!x.vote || x.sum != b) continue;
-      if (best == b || vote_before(x, X(P, M, best))) best = c;
+      if (visible(P, M, c, node) && (best == b || vote_before(x, X(P, M, best)))) best = c;
+      c = x.next;
     }
     return best;
   }
@@ -727,11 +763,11 @@ struct TsLane {
   }
   __host__ __device__ inline bool has_children(const TsParams& P, const TsMem& M, int32_t s,
                                                int32_t node) {
-    // children of a summary are votes on it
-    for (int32_t c = newest; c > s && !dead; --c) {
-      if (!visible(P, M, c, node)) continue;
+    // children of a summary are votes on it: the depth-1 votes of its tree
+    for (int32_t c = X(P, M, s).thead; c >= 0 && !dead;) {
       const TVtx& x = X(P, M, c);
-      if (x.vote && x.parent == s) return true;
+      if (x.parent == s && visible(P, M, c, node)) return true;
+      c = x.next;
     }
     return false;
   }
@@ -750,6 +786,8 @@ struct TsLane {
     b.qslot = -1;
     b.nq = 0;
     b.time = now;
+    b.next = -1;
+    b.thead = -1;
     for (int32_t j = 0; j < P.n; ++j) V(P, M, s, j) = V_INV;
   }
   template <class St>
@@ -767,7 +805,10 @@ struct TsLane {
     b.pow = S.pow((uint32_t)s);
     b.ddepth = p.ddepth + 1;
     b.sum = p.vote ? p.sum : parent;
-    X(P, M, b.sum).nconf += 1;
+    TVtx& sb = X(P, M, b.sum);
+    sb.nconf += 1;
+    b.next = sb.thead;  // newest-first vote list of the tree
+    sb.thead = s;
     return s;
   }
   // Dag(node, Append, draft): Simulator.append dedup (simulator.ml:139-159) or a fresh
@@ -785,10 +826,11 @@ struct TsLane {
     const TVtx& l0 = X(P, M, lv[0]);
     const int32_t prev = l0.sum;
     const int32_t height = X(P, M, prev).height + 1;
-    // candidates: children of lv[0], newest first; only summaries can equal the draft
-    for (int32_t c = newest; c > lv[0] && !dead; --c) {
+    // candidates: children of lv[0], newest first; only summaries can equal the draft, and
+    // those are child summaries of prev (newest-first list)
+    for (int32_t c = SH(P, M, prev); c >= 0 && !dead; c = X(P, M, c).next) {
       const TVtx& y = X(P, M, c);
-      if (y.vote || y.height != height || y.parent != lv[0]) continue;
+      if (y.height != height || y.parent != lv[0]) continue;
       const int32_t* yq = Q(P, M, y);
       bool eq = true;
       const int32_t m = y.nq < nl ? y.nq : nl;
@@ -858,6 +900,9 @@ struct TsLane {
     b.sum = s;
     b.qslot = qs;
     b.nq = nl;
+    SH(P, M, s) = -1;
+    b.next = SH(P, M, prev);  // newest-first child-summary list of prev
+    SH(P, M, prev) = s;
     return s;
   }
 
@@ -876,7 +921,7 @@ struct TsLane {
       const TVtx& b = X(P, M, s);
       if (b.parent < 0) continue;
       const int32_t np = b.vote ? 1 : b.nq;
-      if (sp + np > NSTACK) {
+      if (sp + np > 2 * P.cap_v) {
         fail(5);
         return;
       }
@@ -1077,7 +1122,7 @@ struct TsLane {
         if (!d) continue;
         MK(P, M, s) = 1;
         if ((v & V_KIND) == V_WH) {
-          if (nw >= NPEND) {
+          if (nw >= P.cap_v) {
             fail(9);
             break;
           }
@@ -1097,11 +1142,41 @@ struct TsLane {
       }
       // release search: marks now hold the release set
       for (int32_t s = c0; s <= newest; ++s) MK(P, M, s) = 0;
-      int32_t take = nw;
+      // update_head ~vf:public_or_marked o_pub (sum x) for each prefix: the two tree
+      // counts compare_blocks reads change by one per marked (withheld, visible) vote, so
+      // they are kept per summary (o_pub's, and the latest candidate's) instead of rescanned
+      int32_t take = nw, cs = -1, cc = 0, pc = -1;
       for (int32_t i = 0; i < nw && !dead; ++i) {
         const int32_t x = M.pend[i];
         MK(P, M, x) = 1;
-        if (update_head(P, M, 0, VF_PUBLIC_OR_MARKED, o_pub, X(P, M, x).sum) == o_pub) {
+        const TVtx& xv = X(P, M, x);
+        if (xv.vote) {
+          if (xv.sum == cs) ++cc;
+          if (pc >= 0 && xv.sum == o_pub) ++pc;
+        }
+        const int32_t c = xv.sum;
+        bool keep_old = true;  // compare_blocks c o_pub <= 0
+        if (c != o_pub) {
+          const TVtx& xa = X(P, M, c);
+          const TVtx& xb = X(P, M, o_pub);
+          if (xa.height != xb.height) {
+            keep_old = xa.height < xb.height;
+          } else {
+            if (c != cs) {
+              cs = c;
+              cc = count_post(P, M, c, 0, VF_PUBLIC_OR_MARKED, nullptr);
+            }
+            if (pc < 0) pc = count_post(P, M, o_pub, 0, VF_PUBLIC_OR_MARKED, nullptr);
+            if (cc != pc) {
+              keep_old = cc < pc;
+            } else {
+              const double ra = xa.qslot < 0 ? 0.0 : R(P, M, xa.qslot)[P.n + 0];
+              const double rb = xb.qslot < 0 ? 0.0 : R(P, M, xb.qslot)[P.n + 0];
+              keep_old = !(ra > rb);
+            }
+          }
+        }
+        if (keep_old) {
           take = kind == 1 ? i + 1 : i;
           break;
         }
@@ -1157,6 +1232,9 @@ struct TsLane {
     r.qslot = -1;
     r.nq = 0;
     r.time = 0.0;
+    r.next = -1;
+    r.thead = -1;
+    SH(P, M, 0) = -1;
     for (int32_t j = 0; j < P.n; ++j) {
       V(P, M, 0, j) = V_RECV | V_GOT;
       VT(P, M, 0, j) = 0.0;
@@ -1268,17 +1346,37 @@ struct TsLane {
         break;
       }
       case EV_MDV: {
-        // children (newest first) already received here: votes on s, summaries holding s
-        const bool sv = X(P, M, s).vote != 0;
-        for (int32_t c = newest; c > s && !dead; --c) {
-          if (!(V(P, M, c, node) & V_GOT)) continue;
-          const TVtx& cb = X(P, M, c);
-          bool child = cb.vote && cb.parent == s;
-          if (!child && sv && !cb.vote && cb.qslot >= 0) {
+        // children (newest first) already received here: votes on s (in the tree s belongs
+        // to, or heads), summaries holding s (child summaries of s's tree); two newest-first
+        // lists merged by serial
+        const TVtx& sb = X(P, M, s);
+        const bool sv = sb.vote != 0;
+        int32_t cv = sv ? X(P, M, sb.sum).thead : sb.thead;
+        int32_t cq = sv ? SH(P, M, sb.sum) : -1;
+        while (!dead) {
+          while (cv > s && !(X(P, M, cv).parent == s && (V(P, M, cv, node) & V_GOT)))
+            cv = X(P, M, cv).next;
+          while (cq > s && !(V(P, M, cq, node) & V_GOT)) cq = X(P, M, cq).next;
+          if (cq > s) {  // summary holding s?
+            const TVtx& cb = X(P, M, cq);
+            bool child = false;
             const int32_t* q = Q(P, M, cb);
             for (int32_t i = 0; i < cb.nq; ++i) child |= q[i] == s;
+            if (!child) {
+              cq = cb.next;
+              continue;
+            }
           }
-          if (child) push_now(P, M, mkev(EV_MV, node, KD_NET), c);
+          if (cv <= s && cq <= s) break;
+          int32_t c;
+          if (cv > cq) {
+            c = cv;
+            cv = X(P, M, cv).next;
+          } else {
+            c = cq;
+            cq = X(P, M, cq).next;
+          }
+          push_now(P, M, mkev(EV_MV, node, KD_NET), c);
         }
         break;
       }

@@ -36,6 +36,12 @@ class Context:
         except Exception:
             pass
 
+    def rerun_hbm_retries(self):
+        """Cumulative exact re-runs whose event heap outgrew LDS (cpr_rerun_hbm_retries)."""
+        v = ctypes.c_int64()
+        L.check(L.lib().cpr_rerun_hbm_retries(self.handle, ctypes.byref(v)))
+        return v.value
+
     def synchronize(self):
         L.check(L.lib().cpr_synchronize(self.handle))
 
@@ -229,6 +235,13 @@ class Batch:
         acts = ctypes.c_int64()
         L.check(L.lib().cpr_last_launch(self.handle, ctypes.byref(ms), ctypes.byref(acts)))
         return ms.value, acts.value
+
+    def launch_shape(self):
+        """(lanes, resident lanes) of the last episode-kernel launch (cpr_launch_shape)."""
+        lanes = ctypes.c_int64()
+        res = ctypes.c_int64()
+        L.check(L.lib().cpr_launch_shape(self.handle, ctypes.byref(lanes), ctypes.byref(res)))
+        return lanes.value, res.value
 
     def run_async(self, n_episodes, first_episode, summary_dev_ptr, records_dev_ptr=None):
         L.check(

@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define CPR_ABI_VERSION 8
+#define CPR_ABI_VERSION 9
 
 typedef struct cpr_ctx cpr_ctx;
 typedef struct cpr_batch cpr_batch;
@@ -377,6 +377,15 @@ int cpr_node_outputs(cpr_batch* b, int64_t n_episodes, uint64_t first_episode,
  * this batch, and the activations it simulated (valid after cpr_run_episodes returns;
  * after cpr_run_episodes_async + cpr_synchronize the time is valid and activations is -1) */
 int cpr_last_launch(cpr_batch* b, double* kernel_ms, int64_t* activations);
+/* shape of the last episode-kernel launch of this batch (fused episodes, replay, rollout):
+ * lanes = device lanes launched; resident = lanes the device holds at once for that kernel
+ * (occupancy API x CUs x 256, before the HBM budget and the episode count cap the launch).
+ * Diagnostic for bench.py (lanes / resident), no reference counterpart. ABI v9. */
+int cpr_launch_shape(cpr_batch* b, int64_t* lanes, int64_t* resident);
+/* cumulative count of exact Nakamoto re-runs on this context whose episode outgrew the
+ * LDS-resident event heap and ran again with the heap in HBM (k_nak_exact_rerun's second
+ * attempt). Synchronizes the context's stream. Diagnostic, no reference counterpart. ABI v9. */
+int cpr_rerun_hbm_retries(cpr_ctx* ctx, int64_t* retries);
 
 /* Lockstep env API over cfg->n_lanes lanes (host pointers).
  * reset: lanes with mask[i] != 0 (mask NULL = all) start episode episode_ids[i]

@@ -84,8 +84,7 @@ static eth::EthParams params_of(const Cfg& cf) {
   P.scheme = cf.scheme;
   P.cap_b = 1;
   while (P.cap_b < cf.steps + 2) P.cap_b <<= 1;
-  P.cap_e = 64 + 512 * P.n + (cf.gamma == 0.0 ? 2 * P.d * cf.steps : 0);
-  if (cf.two_agents == 2 && cf.gamma != 0.0) P.cap_e += P.d * (cf.steps + 2);  // capi.hip
+  P.cap_e = 64 + 512 * P.n + (cf.gamma == 0.0 ? 2 * P.d * cf.steps : P.d * (cf.steps + 2));
   P.ev = 1.0;
   P.delta = cf.prop;
   const double dd = cf.defenders;
@@ -102,7 +101,7 @@ static eth::EthParams params_of(const Cfg& cf) {
     P.nak = cf.two_agents == 4 ? 1 : 0;
     P.policy = cf.policy;
     P.t_att = oracle::alpha_threshold(1.0 / (double)P.n);
-    P.cap_e = 64 + 512 * P.n;
+    P.cap_e = 64 + 512 * P.n + P.d * (cf.steps + 2);  // capi.hip validate_eth
     P.dmax = 0.0;
   }
   return P;

@@ -145,13 +145,18 @@ def test_gamma0_reruns_exact_with_lds_heap(ctx, lds_max, monkeypatch):
     cfg, keep = device.make_config(alpha=0.45, gamma=0.0, policy=L.POLICY_SAPIRSHTEIN_2016_SM1,
                                    max_steps=2016, seed=0x0E70, propagation_delay=0.05)
     b = device.Batch(cfg, ctx=ctx, keep=keep)
+    r0 = ctx.rerun_hbm_retries()
     s, rec = b.run(192, first_episode=0, records=True)
+    retries = ctx.rerun_hbm_retries() - r0
     ref = O.run_episodes(cfg, 0, 192, threads=8)
     assert _records_equal(rec, ref) == {}
     flagged = (rec["status"] & L.ST_EXACT_RERUN) != 0
     assert flagged.sum() > 50, int(flagged.sum())
     assert not (rec["status"] & L.ST_CAPACITY).any()
     assert s.episodes == 192
+    if lds_max is not None:  # the HBM retry really ran (and its records equal the oracle's)
+        assert retries > 0, retries
+    print(f"lds_max {lds_max}: {int(flagged.sum())} re-runs, {retries} HBM retries")
 
 
 def test_gym_overlaps_at_the_reference_delay(ctx):

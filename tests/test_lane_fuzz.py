@@ -43,7 +43,7 @@ def test_ethereum_lane_matches_oracle_fuzz():
     assert p.returncode == 0, p.stderr[-2000:]
     assert out["mismatches"] == 0, p.stderr[-2000:]
     assert out["episodes"] > 1000 and out["steps"] > 300000
-    assert out["capacity"] <= out["episodes"] // 100
+    assert out["capacity"] == 0  # heap bound: d messages per block (capi.hip validate_eth)
 
 
 def test_bk_lane_matches_oracle_fuzz():
