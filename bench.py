@@ -95,6 +95,175 @@ def cpu_baseline(seconds, points):
     }
 
 
+# ---------------------------------------------------------------- BASELINE configs[0, 2-4]
+# build-defined VALU cost model per activation
+OPS_BY_PROTOCOL = {"nakamoto": 40, "ethereum": 60, "bk": 80, "tailstorm": 120}
+
+
+def other_config_specs():
+    """The other BASELINE.json configs, each as (key, description, protocol, kernel, [points],
+    episodes per point (None = the kernel's resident lanes), rollout steps or None).
+    A point is a device.make_config keyword dict."""
+    from cpr_amd import _lib as L
+
+    specs = [(
+        "configs[0]", "Nakamoto honest, alpha .33, gamma .5 (d = 2), 2016-step cpr-nakamoto-v0 "
+        "episodes (the reference's CPU-runnable case)", "nakamoto", "k_run_episodes",
+        [dict(alpha=0.33, gamma=0.5, policy=L.POLICY_HONEST, max_steps=STEPS_PER_EPISODE)],
+        393216, None)]
+    # configs[2]: Ethereum Byzantium, whitepaper (constant) uncle rewards, ethereum_ssz
+    # selfish_release and fn19 over alpha x gamma, 2016-step gym episodes
+    eth = [dict(protocol=L.PROTO_ETHEREUM, alpha=a, gamma=g, policy=pol,
+                reward_scheme=L.REWARD_CONSTANT, max_steps=STEPS_PER_EPISODE)
+           for pol in (L.ETH_POLICY_SELFISH_RELEASE, L.ETH_POLICY_FN19)
+           for g in (0.0, 0.5, 0.9) for a in (0.25, 0.45)]
+    specs.append(("configs[2]", "Ethereum-PoW uncle-aware selfish mining, Byzantium + whitepaper "
+                  "(constant) uncle rewards, ethereum_ssz selfish_release and fn19, alpha {.25, "
+                  ".45} x gamma {0, .5, .9}, 2016-step gym episodes", "ethereum",
+                  "k_eth_run_episodes", eth, None, None))
+    # configs[3]: Tailstorm k = 8, discount, heuristic sub-block selection, withholding
+    # attack on the two-agents network (Simulator.loop tasks of 10^4 activations,
+    # withholding.ml:68-90), get-ahead and avoid-loss; the exp(1)-propagation variant apart
+    ts = dict(protocol=L.PROTO_TAILSTORM, network=L.NET_TWO_AGENTS, mode=L.MODE_LOOP,
+              activations=10000, k=8, reward_scheme=L.REWARD_DISCOUNT,
+              subblock_selection=L.SELECT_HEURISTIC)
+    specs.append(("configs[3]", "Tailstorm k=8, discount rewards, heuristic quorums, get-ahead "
+                  "and avoid-loss withholding, two-agents network (alpha .33), 10^4-activation "
+                  "Simulator.loop tasks", "tailstorm", "k_ts_run_episodes",
+                  [dict(ts, alpha=0.33, policy=L.TS_POLICY_GET_AHEAD),
+                   dict(ts, alpha=0.33, policy=L.TS_POLICY_AVOID_LOSS)], None, None))
+    specs.append(("configs[3]_exp", "the same on 2 miners of equal compute with exponential(1) "
+                  "link delays (cpr_protocols.ml:478-485), activation delay 10, get-ahead",
+                  "tailstorm", "k_ts_run_episodes",
+                  [dict(ts, alpha=0.0, network=L.NET_EXP_CLIQUE, defenders=1,
+                        activation_delay=10.0, propagation_delay=1.0,
+                        policy=L.TS_POLICY_GET_AHEAD)], None, None))
+    # configs[4]: 65,536 lockstep B_k k = 8 gym envs, constant rewards, table policy, 2048-step
+    # episodes, VecEnv auto-reset; the rollout steps every lane 512 times
+    K, D = 8, 4
+    table = np.random.default_rng(0).integers(0, 8, size=D * D * (K + 1) ** 2 * 3).astype(np.uint8)
+    specs.append(("configs[4]", "65,536 parallel bk_ssz gym envs (B_k k=8, constant rewards, "
+                  "alpha .33, gamma .5, d = 2) stepped in lockstep by an on-device random table "
+                  "policy, 2048-step episodes, VecEnv auto-reset", "bk", "k_bk_rollout",
+                  [dict(protocol=L.PROTO_BK, alpha=0.33, gamma=0.5, k=K, table=table,
+                        reward_scheme=L.REWARD_CONSTANT, max_steps=2048, n_lanes=65536)],
+                  None, 512))
+    return specs
+
+
+def _cpu_sample(cfg, seconds, threads, per_call):
+    """oracle run_episodes on cfg for about `seconds`: activations, steps, episodes, time"""
+    sys.path.insert(0, os.path.join(HERE, "tests"))
+    import oracle_py
+
+    acts = steps = eps = i = 0
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        rec = oracle_py.run_episodes(cfg, 3 * 10**9 + i * per_call, per_call, threads=threads)
+        acts += int(rec["n_activations"].sum())
+        steps += int(rec["n_steps"].sum())
+        eps += per_call
+        i += 1
+    return acts, steps, eps, time.perf_counter() - t0
+
+
+def run_other_configs(ctx, cpu_seconds, with_cpu, pmc):
+    """One launch per point at the kernel's resident lane count (configs[0]: the headline's
+    episode count), timed by the library's HIP events (cpr_last_launch) and by the host
+    clock around each synchronous call; roofline at the §8d cost model; measured HBM bytes
+    from the committed PMC summary of the same launch (tools/profile_configs.sh); a bounded
+    oracle sample of the same config on this host."""
+    from cpr_amd import device
+
+    cores, aff = _host_cores()
+    out = {}
+    for key, desc, proto, kernel, points, eps, roll in other_config_specs():
+        acts = steps = episodes = 0
+        wall = kms = 0.0
+        lanes_l, res_l = [], []
+        for pt in points:
+            cfg, keep = device.make_config(seed=SEED, **pt)
+            b = device.Batch(cfg, ctx=ctx, keep=keep)
+            n = eps
+            if n is None and roll is None:
+                n = b.launch_shape()[1]
+            t0 = time.perf_counter()
+            if roll is not None:
+                b.rollout(8)  # reset + a few steps, untimed
+                t0 = time.perf_counter()
+                s = b.rollout(roll)
+            else:
+                s = b.run(n, first_episode=0)
+            wall += time.perf_counter() - t0
+            ms, _ = b.last_launch()
+            kms += ms
+            ln, res = b.launch_shape()
+            lanes_l.append(ln)
+            res_l.append(res)
+            acts += int(s.activations)
+            steps += int(s.steps)
+            episodes += int(s.episodes)
+            b.close()
+        ops = OPS_BY_PROTOCOL[proto]
+        kact = acts / (kms / 1e3)
+        ach = kact * ops / 1e12
+        entry = {
+            "workload": desc,
+            "points": len(points),
+            "activations": acts,
+            "activations_per_s": acts / wall,
+            "kernel_ms": kms,
+            "kernel_activations_per_s": kact,
+            "lanes_per_launch": lanes_l[0],
+            "resident_lanes": res_l[0],
+            "lanes_over_resident": lanes_l[0] / res_l[0] if res_l[0] else None,
+            "roofline": {"bound": "valu", "kernel": kernel, "achieved": ach,
+                         "peak": VALU_PEAK_TOPS,
+                         "unit": f"Tops/s (VALU lane-ops, {ops} ops/activation cost model)",
+                         "frac": ach / VALU_PEAK_TOPS},
+        }
+        if roll is not None:
+            entry["env_steps_per_s"] = steps / wall
+            entry["env_steps"] = steps
+            entry["rollout_steps_per_lane"] = roll
+        else:
+            entry["episodes_per_s"] = episodes / wall
+        t = pmc.get(key) if pmc else None
+        if t:
+            entry["roofline"]["traffic"] = t["hbm_bytes_per_activation"] * acts
+            entry["roofline"]["traffic_source"] = t["source"]
+            entry["roofline"]["hbm_bytes_per_activation"] = t["hbm_bytes_per_activation"]
+            entry["roofline"]["measured_valu_lane_ops_per_activation"] = t.get("valu_lane_ops_per_activation")
+        else:
+            entry["roofline"]["traffic"] = None
+        if with_cpu:
+            cfg, _ = device.make_config(seed=SEED, **dict(points[0], n_lanes=0))
+            a, st, e, dt = _cpu_sample(cfg, cpu_seconds, cores, 2 * cores)
+            entry["cpu_baseline"] = {
+                "value": a / dt, "unit": "activations/s", "cores": cores, "kind": "port",
+                "sample": f"{e} episodes of the first point ({dt:.1f} s on {cores} threads; "
+                          f"oracle/src event-driven restatement)",
+                "env_steps_per_s": st / dt}
+        out[key] = entry
+    return out
+
+
+def config_pmc():
+    """Newest committed profiles/*_config_pmc.json (tools/summarize_configs.py): per config
+    key, HBM bytes and VALU lane-ops per activation of the same launches."""
+    import glob
+
+    for path in sorted(glob.glob(os.path.join(HERE, "profiles", "*_config_pmc.json")), reverse=True):
+        try:
+            d = json.load(open(path))
+        except (OSError, ValueError):
+            continue
+        for v in d.values():
+            v["source"] = os.path.relpath(path, HERE)
+        return d
+    return {}
+
+
 # algorithmic HBM bytes of k_run_episodes (SURVEY.md §8d): the Monte-Carlo outputs,
 # ~48 B per episode (rewards, progress, status; the summary's share is negligible)
 ALG_BYTES_PER_EPISODE = 48.0
@@ -132,6 +301,9 @@ def main():
     ap.add_argument("--episodes", type=int, default=393216, help="per GPU per sweep point")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-configs", action="store_true",
+                    help="skip BASELINE configs[0], [2]-[4] (other_configs)")
+    ap.add_argument("--config-cpu-seconds", type=float, default=2.0)
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="collective backend (nccl = RCCL; gloo only for the one-GPU "
                          "multi-rank test, tests/test_gpu_distributed.py)")
@@ -187,7 +359,7 @@ def main():
     parallel.barrier(cdev)
     dt = parallel.allreduce_max(time.perf_counter() - t0, cdev)
     sums = read(sums_dev)
-    totals = [parallel.allreduce_summary(s, cdev) for s in sums]
+    totals = parallel.allreduce_summaries(sums, cdev)  # one packed collective
     acts = sum(int(s.activations) for s in totals)
     episodes = sum(int(s.episodes) for s in totals)
 
@@ -213,7 +385,7 @@ def main():
     torch.cuda.synchronize()
     parallel.barrier(cdev)
     dta = parallel.allreduce_max(time.perf_counter() - ta, cdev)
-    atotals = [parallel.allreduce_summary(s, cdev) for s in read(asums[:len(abatches)])]
+    atotals = parallel.allreduce_summaries(read(asums[:len(abatches)]), cdev)
     traffic, traffic_src, valu_meas = pmc_traffic(E)
     kacts = np.full(len(batches), float(E * (STEPS_PER_EPISODE + 1)))
     act_per_s_kernel = float(kacts.sum() / (kms.sum() / 1e3))
@@ -287,6 +459,10 @@ def main():
         }
         if not args.no_cpu and ws == 1:
             out["cpu_baseline"] = cpu_baseline(args.cpu_seconds, points)
+        if not args.no_configs and ws == 1:
+            # the other BASELINE configs on this GPU, after the headline's timed region
+            out["other_configs"] = run_other_configs(ctx, args.config_cpu_seconds,
+                                                     not args.no_cpu, config_pmc())
         print(json.dumps(out), flush=True)
     for b in batches + abatches:
         b.close()

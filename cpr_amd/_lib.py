@@ -255,10 +255,45 @@ class Trace:
     def save(self, path):
         np.savez_compressed(path, **{n: getattr(self, n) for n, _ in self.ARRAYS})
 
+    # binary layout written by the OCaml recorder (integration/ocaml/trace_hooks.ml
+    # `write`): magic, u32 version, u32 n_episodes, then per array of ARRAYS: u64 count and
+    # that many little-endian elements (act_miner / pow_hash as 32-bit ints)
+    MAGIC = b"CPRTRACE"
+    _WIRE = {"act_offset": "<i8", "act_miner": "<i4", "act_delay": "<f8", "pow_offset": "<i8",
+             "pow_hash": "<i4", "link_offset": "<i8", "link_key": "<u8", "link_delay": "<f8"}
+
+    def save_binary(self, path):
+        """The OCaml recorder's format (a Python mirror of trace_hooks.ml `write`)."""
+        with open(path, "wb") as f:
+            f.write(self.MAGIC)
+            f.write(np.array([1, self.n_episodes], dtype="<u4").tobytes())
+            for name, _ in self.ARRAYS:
+                a = np.ascontiguousarray(getattr(self, name), dtype=self._WIRE[name])
+                f.write(np.array([len(a)], dtype="<u8").tobytes())
+                f.write(a.tobytes())
+
     @classmethod
     def load(cls, path):
-        with np.load(path, allow_pickle=False) as z:
-            return cls(**{n: z[n] for n, _ in cls.ARRAYS})
+        """An .npz (Trace.save, the oracle's exporter) or the OCaml recorder's binary file."""
+        with open(path, "rb") as f:
+            head = f.read(len(cls.MAGIC))
+        if head != cls.MAGIC:
+            with np.load(path, allow_pickle=False) as z:
+                return cls(**{n: z[n] for n, _ in cls.ARRAYS})
+        raw = open(path, "rb").read()
+        ver, n_ep = np.frombuffer(raw, dtype="<u4", count=2, offset=8)
+        if ver != 1:
+            raise ValueError(f"{path}: trace format version {ver}, expected 1")
+        o, arrays = 16, {}
+        for name, _ in cls.ARRAYS:
+            (cnt,) = np.frombuffer(raw, dtype="<u8", count=1, offset=o)
+            o += 8
+            dt = np.dtype(cls._WIRE[name])
+            arrays[name] = np.frombuffer(raw, dtype=dt, count=int(cnt), offset=o).copy()
+            o += int(cnt) * dt.itemsize
+        if o != len(raw) or len(arrays["act_offset"]) != n_ep + 1:
+            raise ValueError(f"{path}: malformed trace file")
+        return cls(**arrays)
 
     def ctrace(self):
         t = CTrace()

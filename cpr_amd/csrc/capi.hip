@@ -752,10 +752,22 @@ int cpr_batch_create(cpr_ctx* ctx, const cpr_config* cfg, cpr_batch** out) {
   return CPR_OK;
 }
 
+// lanes the device holds at once for this batch's fused-episode kernel (before any launch)
+static int64_t batch_resident(cpr_batch* b) {
+  const int64_t cus = b->ctx->cus;
+  if (b->cfg.protocol == CPR_PROTO_FC16) return cus * 8 * 256;
+  if (b->cfg.protocol == CPR_PROTO_ETHEREUM || b->nak_ev) return cus * eth_blocks_per_cu() * 256;
+  if (b->is_ev)
+    return cus * (b->cfg.protocol == CPR_PROTO_TAILSTORM ? ts_blocks_per_cu() : bk_blocks_per_cu()) *
+           256;
+  return cus * run_episodes_blocks_per_cu(b->cfg.mode) * 256;
+}
+
 int cpr_launch_shape(cpr_batch* b, int64_t* lanes, int64_t* resident) {
   if (!b) return fail(CPR_E_INVALID_ARG, "NULL argument");
+  HIP_TRY(hipSetDevice(b->ctx->device));
   if (lanes) *lanes = b->last_lanes;
-  if (resident) *resident = b->last_resident;
+  if (resident) *resident = b->last_lanes ? b->last_resident : batch_resident(b);
   return CPR_OK;
 }
 
@@ -931,7 +943,7 @@ static int run_async(cpr_batch* b, int64_t n, uint64_t first, const TraceSource*
   const int64_t lanes = episode_lanes(b, n);
   b->last_lanes = lanes;
   b->last_resident = (int64_t)b->ctx->cus * run_episodes_blocks_per_cu(b->cfg.mode) * 256;
-  // spill [lane][cap] f64 mining times | tie-replay scratch [lane]
+  // spill [cap][lane] f64 mining times (interleaved) | tie-replay scratch [lane]
   const size_t o_replay = align256((size_t)lanes * b->P.cap * sizeof(double));
   void* pool = nullptr;
   HIP_TRY(ctx_pool(b->ctx, o_replay + (size_t)lanes * REPLAY_BYTES, &pool));

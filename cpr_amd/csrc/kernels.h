@@ -12,6 +12,24 @@
 #include "summary.h"
 #include "ts_lane.h"
 
+// occupancy of the per-lane event-engine kernels (B_k, Ethereum, Tailstorm fused episodes
+// and rollouts): they are bound by dependent memory latency, so waves per SIMD matter more
+// than the few VGPRs a tighter budget spills. CPR_EV_WAVES = minimum waves per SIMD the
+// compiler must allow (0: unconstrained). tools/occupancy_ab.sh builds variants.
+#ifndef CPR_EV_WAVES
+#define CPR_EV_WAVES 0
+#endif
+// CPR_EV_SCHED = 1: wave-coherent dispatch of the event engines' work (wave_sched.h);
+// 0: one plain event loop per lane (the round-2 kernels), kept for A/B variants
+#ifndef CPR_EV_SCHED
+#define CPR_EV_SCHED 1
+#endif
+#if CPR_EV_WAVES > 0
+#define CPR_EV_OCC __attribute__((amdgpu_waves_per_eu(CPR_EV_WAVES)))
+#else
+#define CPR_EV_OCC
+#endif
+
 namespace cpr {
 
 // per-step outputs of the lockstep kernel (device pointers)

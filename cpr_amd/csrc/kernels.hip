@@ -105,8 +105,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
   LaneMem M;
   M.ring = ring + threadIdx.x;
   M.ring_stride = kBlock;
-  M.spill = spill + tid * P.cap;
-  M.spill_stride = 1;
+  // spill interleaved [slot][lane] like the LDS ring: the evictions of a wave's lanes at
+  // the same chain depth land in adjacent words instead of 64 lines cap * 8 B apart
+  M.spill = spill + tid;
+  M.spill_stride = nthreads;
   M.cap = P.cap;
   M.replay = ReplayMem::at(replay + tid * REPLAY_BYTES);
   NakLane L;
@@ -166,8 +168,8 @@ __device__ inline LaneMem lock_mem(const NakParams& P, const LockBuffers& B, int
   LaneMem M;
   M.ring = B.ring + i;
   M.ring_stride = n;
-  M.spill = B.spill + i * P.cap;
-  M.spill_stride = 1;
+  M.spill = B.spill + i;  // [slot][lane], as the fused kernel's
+  M.spill_stride = n;
   M.cap = P.cap;
   M.replay = ReplayMem::at(B.replay + i * REPLAY_BYTES);
   return M;

@@ -14,6 +14,7 @@
 #include "bk_lane.h"
 #include "kernels.h"
 #include "summary.h"
+#include "wave_sched.h"
 
 #pragma clang fp contract(off)
 
@@ -37,8 +38,77 @@ __device__ inline void bk_acc(Acc& acc, const bk::BkParams& P, const bk::BkLane&
               (int64_t)h.height * P.k, L.steps, L.c_act, L.status, hist);
 }
 
+// one finished episode: summary, record, per-node row
+template <class Src, class St>
+__device__ inline void bk_finish(const bk::BkParams& P, bk::BkLane& L, const bk::BkMem& M,
+                                 const St& S, int64_t e, int32_t hd, Acc& acc, int32_t* hist,
+                                 cpr_episode_record* recs, const NodeOut& no) {
+  L.status |= Src::missed(S);
+  const bk::BVtx& h = L.X(P, M, hd);
+  bk_acc(acc, P, L, h, hist);
+  if (recs) {
+    cpr_episode_record r;
+    r.reward_attacker = (double)h.rew_att;
+    r.reward_defender = (double)h.rew_def;
+    r.progress = (double)(h.height * P.k);
+    r.chain_time = h.time;
+    r.sim_time = P.mode == CPR_MODE_GYM ? L.now : 0.0;
+    r.n_steps = L.steps;
+    r.n_activations = L.c_act;
+    r.head_height = h.height;
+    r.head_miner = h.who;
+    r.status = L.status;
+    r.head_work = 0;
+    recs[e] = r;
+  }
+  if (no.acts) {  // csv_runner.ml:74-79: sim.activations and (Dag.data head).rewards
+    const int32_t* hr =
+        h.qslot < 0 ? nullptr : M.nrew + (int64_t)(h.qslot & (P.cap_q - 1)) * P.n;
+    for (int32_t j = 0; j < P.n; ++j) {
+      no.acts[e * P.n + j] = M.nact[j];
+      no.rews[e * P.n + j] = hr ? (double)hr[j] : 0.0;
+    }
+    no.head_miner[e] = h.who;
+  }
+}
+
+// wave_sched.h adapter for bk_lane.h
+struct BkAdapter {
+  using Lane = bk::BkLane;
+  using Par = bk::BkParams;
+  using Mem = bk::BkMem;
+  template <class St>
+  __device__ static void begin(Lane& L, const Par& P, const St& S, const Mem& M) {
+    L.init(P, S, M);
+  }
+  __device__ static bool gym(const Par& P) { return P.mode == CPR_MODE_GYM; }
+  __device__ static bool loop_attacker(const Par& P) { return P.net != 2; }
+  __device__ static bool pow0(uint32_t ev) {
+    return (ev & 7u) == bk::EV_DAG && (ev >> 5) == 0u && ((ev >> 3) & 3u) == bk::KD_POW;
+  }
+  template <class St>
+  __device__ static void run_pow0(Lane& L, const Par& P, const St& S, const Mem& M, int32_t) {
+    const int32_t v = L.append_vote(P, S, M, 0, L.priv);
+    L.push_now(P, M, bk::mkev(bk::EV_MV, 0, bk::KD_POW), v);
+  }
+  __device__ static void act(Lane& L, const Par& P, const Mem& M) {
+    L.apply(P, M, bk::bk_policy(P, L.observe(P, M)));
+    ++L.steps;
+  }
+  __device__ static int32_t head_gym(Lane& L, const Par& P, const Mem& M, int32_t att) {
+    return L.head(P, M, att);
+  }
+  __device__ static int32_t head_loop(Lane& L, const Par& P, const Mem& M) {
+    return L.head(P, M, P.net == 2 ? M.tips[0] : L.priv);
+  }
+  __device__ static bool gym_done(Lane& L, const Par& P, const Mem& M, int32_t hd) {
+    const double progress = (double)(L.X(P, M, hd).height * P.k);
+    return L.dead || !(L.steps < P.max_steps && progress < P.max_progress && L.now < P.max_time);
+  }
+};
+
 template <class Src>
-__global__ __launch_bounds__(kBlock) void k_bk_run_episodes(
+__global__ __launch_bounds__(kBlock) CPR_EV_OCC void k_bk_run_episodes(
     bk::BkParams P, Src src, int64_t n_eps, uint8_t* mem,
     int64_t lane_bytes, cpr_episode_record* recs, cpr_summary* sum, NodeOut no) {
   __shared__ int32_t hist[CPR_HIST_BINS];
@@ -50,6 +120,32 @@ __global__ __launch_bounds__(kBlock) void k_bk_run_episodes(
   if (no.mem) bk::bk_node_mem(M, no.mem + tid * no.lane_bytes, P);
   Acc acc = {};
   bk::BkLane L;
+#if CPR_EV_SCHED
+  int64_t e = tid;  // wave-coherent dispatch (wave_sched.h), grid-stride over episodes
+  auto S = src.at(e < n_eps ? e : 0);
+  EvCursor c;
+  c.cls = -1;
+  c.phase = PH_IDLE;
+  if (e < n_eps) ev_begin<BkAdapter>(L, P, S, M, c);
+  for (;;) {
+    while (c.phase != PH_IDLE && c.cls < 0) {
+      if (c.phase != PH_OVER) ev_fetch<BkAdapter>(L, P, S, M, c);
+      if (c.phase == PH_OVER) {
+        bk_finish<Src>(P, L, M, S, e, c.hd, acc, hist, recs, no);
+        e += nthreads;
+        if (e < n_eps) {
+          S = src.at(e);
+          ev_begin<BkAdapter>(L, P, S, M, c);
+        } else {
+          c.phase = PH_IDLE;
+        }
+      }
+    }
+    const int32_t k = ev_choose(c.cls);
+    if (k < 0) break;
+    if (c.cls == k) ev_exec<BkAdapter>(L, P, S, M, c);
+  }
+#else
   for (int64_t e = tid; e < n_eps; e += nthreads) {
     const auto S = src.at(e);
     int32_t hd;
@@ -61,34 +157,9 @@ __global__ __launch_bounds__(kBlock) void k_bk_run_episodes(
     } else {
       hd = L.loop(P, S, M);
     }
-    L.status |= Src::missed(S);
-    const bk::BVtx& h = L.X(P, M, hd);
-    bk_acc(acc, P, L, h, hist);
-    if (recs) {
-      cpr_episode_record r;
-      r.reward_attacker = (double)h.rew_att;
-      r.reward_defender = (double)h.rew_def;
-      r.progress = (double)(h.height * P.k);
-      r.chain_time = h.time;
-      r.sim_time = P.mode == CPR_MODE_GYM ? L.now : 0.0;
-      r.n_steps = L.steps;
-      r.n_activations = L.c_act;
-      r.head_height = h.height;
-      r.head_miner = h.who;
-      r.status = L.status;
-      r.head_work = 0;
-      recs[e] = r;
-    }
-    if (no.acts) {  // csv_runner.ml:74-79: sim.activations and (Dag.data head).rewards
-      const int32_t* hr =
-          h.qslot < 0 ? nullptr : M.nrew + (int64_t)(h.qslot & (P.cap_q - 1)) * P.n;
-      for (int32_t j = 0; j < P.n; ++j) {
-        no.acts[e * P.n + j] = M.nact[j];
-        no.rews[e * P.n + j] = hr ? (double)hr[j] : 0.0;
-      }
-      no.head_miner[e] = h.who;
-    }
+    bk_finish<Src>(P, L, M, S, e, hd, acc, hist, recs, no);
   }
+#endif
   __syncthreads();
   block_flush(acc, hist, sum);
 }
@@ -187,7 +258,7 @@ __global__ __launch_bounds__(kBlock) void k_bk_step(bk::BkParams P, uint64_t see
 // observation written at a done step is the new episode's first observation).
 // summary.steps / .activations count every step / activation of the rollout; the other
 // summary fields cover the episodes that finished in it.
-__global__ __launch_bounds__(kBlock) void k_bk_rollout(bk::BkParams P, uint64_t seed,
+__global__ __launch_bounds__(kBlock) CPR_EV_OCC void k_bk_rollout(bk::BkParams P, uint64_t seed,
                                                         uint8_t* mem, int64_t lane_bytes,
                                                         BkSlot* slots, int64_t n,
                                                         int64_t n_steps, int unit,

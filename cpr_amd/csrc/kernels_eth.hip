@@ -14,14 +14,87 @@
 #include "ethereum_lane.h"
 #include "kernels.h"
 #include "summary.h"
+#include "wave_sched.h"
 
 #pragma clang fp contract(off)
 
 namespace cpr {
 
 
+// one finished episode: summary, record, per-node row
+template <class Src, class St>
+__device__ inline void eth_finish(const eth::EthParams& P, eth::EthLane& L, const eth::EthMem& M,
+                                  const St& S, int64_t e, int32_t hd, Acc& acc, int32_t* hist,
+                                  cpr_episode_record* recs, const NodeOut& no) {
+  L.status |= Src::missed(S);
+  const eth::EBlock& h = L.B(P, M, hd);
+  const int32_t ra = h.rew_att, rd = h.rew_def;
+  const double rel = (ra + rd) != 0 ? (double)ra / (double)(ra + rd) : 0.0;
+  acc_episode(acc, (int64_t)ra << 15, (int64_t)rd << 15, (int64_t)h.work << 20, rel, h.height,
+              L.steps, L.c_act, L.status, hist);
+  if (recs) {
+    cpr_episode_record r;
+    r.reward_attacker = (double)ra / 32.0;
+    r.reward_defender = (double)rd / 32.0;
+    r.progress = (double)h.work;
+    r.chain_time = h.time;
+    r.sim_time = P.mode == CPR_MODE_GYM ? L.now : 0.0;
+    r.n_steps = L.steps;
+    r.n_activations = L.c_act;
+    r.head_height = h.height;
+    r.head_miner = P.mode == CPR_MODE_GYM ? h.miner : -1;
+    r.status = L.status;
+    r.head_work = P.nak ? 0 : h.work;
+    recs[e] = r;
+  }
+  if (no.acts) {  // csv_runner.ml:74-79: sim.activations and (Dag.data head).rewards
+    const int32_t* hr = M.nrew + (int64_t)(hd & (P.cap_b - 1)) * P.n;
+    for (int32_t j = 0; j < P.n; ++j) {
+      no.acts[e * P.n + j] = M.nact[j];
+      no.rews[e * P.n + j] = (double)hr[j] / 32.0;
+    }
+    no.head_miner[e] = h.miner;
+  }
+}
+
+// wave_sched.h adapter for ethereum_lane.h (also the Nakamoto-mode engine)
+struct EthAdapter {
+  using Lane = eth::EthLane;
+  using Par = eth::EthParams;
+  using Mem = eth::EthMem;
+  template <class St>
+  __device__ static void begin(Lane& L, const Par& P, const St& S, const Mem& M) {
+    L.init(P, S, M);
+  }
+  __device__ static bool gym(const Par& P) { return P.mode == CPR_MODE_GYM; }
+  __device__ static bool loop_attacker(const Par& P) { return P.net != 2; }
+  __device__ static bool pow0(uint32_t ev) { return (ev & 7u) == eth::EV_DAG && (ev >> 5) == 0u; }
+  template <class St>
+  __device__ static void run_pow0(Lane& L, const Par& P, const St&, const Mem& M, int32_t) {
+    const eth::Payload d = L.payload(P, M, 0, L.priv, eth::F_MINING, L.own, L.foreign);
+    const int32_t v = L.append(P, M, 0, d);
+    L.push_now(P, M, eth::mkev(eth::EV_MV, 0, eth::KD_POW), v);
+  }
+  __device__ static void act(Lane& L, const Par& P, const Mem& M) {
+    const eth::EthObs o = L.observe(P, M, false);
+    const int32_t sh = L.apply(P, M, eth::lane_action(P, o));
+    if (sh >= 0) L.share(P, M, 0, sh);
+    ++L.steps;
+  }
+  __device__ static int32_t head_gym(Lane& L, const Par& P, const Mem& M, int32_t att) {
+    return L.head(P, M, att);
+  }
+  __device__ static int32_t head_loop(Lane& L, const Par& P, const Mem& M) {
+    return L.head(P, M, P.net == 2 ? M.tips[0] : L.priv);
+  }
+  __device__ static bool gym_done(Lane& L, const Par& P, const Mem& M, int32_t hd) {
+    const double progress = (double)L.B(P, M, hd).work;
+    return L.dead || !(L.steps < P.max_steps && progress < P.max_progress && L.now < P.max_time);
+  }
+};
+
 template <class Src>
-__global__ __launch_bounds__(kBlock) void k_eth_run_episodes(
+__global__ __launch_bounds__(kBlock) CPR_EV_OCC void k_eth_run_episodes(
     eth::EthParams P, Src src, int64_t n_eps, uint8_t* mem,
     int64_t lane_bytes, cpr_episode_record* recs, cpr_summary* sum, NodeOut no) {
   __shared__ int32_t hist[CPR_HIST_BINS];
@@ -33,6 +106,32 @@ __global__ __launch_bounds__(kBlock) void k_eth_run_episodes(
   if (no.mem) eth::eth_node_mem(M, no.mem + tid * no.lane_bytes, P.n);
   Acc acc = {};
   eth::EthLane L;
+#if CPR_EV_SCHED
+  int64_t e = tid;  // wave-coherent dispatch (wave_sched.h), grid-stride over episodes
+  auto S = src.at(e < n_eps ? e : 0);
+  EvCursor c;
+  c.cls = -1;
+  c.phase = PH_IDLE;
+  if (e < n_eps) ev_begin<EthAdapter>(L, P, S, M, c);
+  for (;;) {
+    while (c.phase != PH_IDLE && c.cls < 0) {
+      if (c.phase != PH_OVER) ev_fetch<EthAdapter>(L, P, S, M, c);
+      if (c.phase == PH_OVER) {
+        eth_finish<Src>(P, L, M, S, e, c.hd, acc, hist, recs, no);
+        e += nthreads;
+        if (e < n_eps) {
+          S = src.at(e);
+          ev_begin<EthAdapter>(L, P, S, M, c);
+        } else {
+          c.phase = PH_IDLE;
+        }
+      }
+    }
+    const int32_t k = ev_choose(c.cls);
+    if (k < 0) break;
+    if (c.cls == k) ev_exec<EthAdapter>(L, P, S, M, c);
+  }
+#else
   for (int64_t e = tid; e < n_eps; e += nthreads) {
     const auto S = src.at(e);
     int32_t hd;
@@ -47,36 +146,9 @@ __global__ __launch_bounds__(kBlock) void k_eth_run_episodes(
     } else {
       hd = L.loop(P, S, M);
     }
-    L.status |= Src::missed(S);
-    const eth::EBlock& h = L.B(P, M, hd);
-    const int32_t ra = h.rew_att, rd = h.rew_def;
-    const double rel = (ra + rd) != 0 ? (double)ra / (double)(ra + rd) : 0.0;
-    acc_episode(acc, (int64_t)ra << 15, (int64_t)rd << 15, (int64_t)h.work << 20, rel, h.height,
-                L.steps, L.c_act, L.status, hist);
-    if (recs) {
-      cpr_episode_record r;
-      r.reward_attacker = (double)ra / 32.0;
-      r.reward_defender = (double)rd / 32.0;
-      r.progress = (double)h.work;
-      r.chain_time = h.time;
-      r.sim_time = P.mode == CPR_MODE_GYM ? L.now : 0.0;
-      r.n_steps = L.steps;
-      r.n_activations = L.c_act;
-      r.head_height = h.height;
-      r.head_miner = P.mode == CPR_MODE_GYM ? h.miner : -1;
-      r.status = L.status;
-      r.head_work = P.nak ? 0 : h.work;
-      recs[e] = r;
-    }
-    if (no.acts) {  // csv_runner.ml:74-79: sim.activations and (Dag.data head).rewards
-      const int32_t* hr = M.nrew + (int64_t)(hd & (P.cap_b - 1)) * P.n;
-      for (int32_t j = 0; j < P.n; ++j) {
-        no.acts[e * P.n + j] = M.nact[j];
-        no.rews[e * P.n + j] = (double)hr[j] / 32.0;
-      }
-      no.head_miner[e] = h.miner;
-    }
+    eth_finish<Src>(P, L, M, S, e, hd, acc, hist, recs, no);
   }
+#endif
   __syncthreads();
   block_flush(acc, hist, sum);
 }
@@ -392,7 +464,7 @@ __global__ __launch_bounds__(kBlock) void k_eth_step(eth::EthParams P, uint64_t 
 
 // n_steps lockstep steps per lane with the batch policy on the device, VecEnv auto-reset
 // (episode id + n), as k_bk_rollout
-__global__ __launch_bounds__(kBlock) void k_eth_rollout(eth::EthParams P, uint64_t seed,
+__global__ __launch_bounds__(kBlock) CPR_EV_OCC void k_eth_rollout(eth::EthParams P, uint64_t seed,
                                                          uint8_t* mem, int64_t lane_bytes,
                                                          EthSlot* slots, int64_t n,
                                                          int64_t n_steps, int unit,

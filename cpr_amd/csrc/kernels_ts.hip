@@ -7,6 +7,7 @@
 #include "kernels.h"
 #include "summary.h"
 #include "ts_lane.h"
+#include "wave_sched.h"
 
 #pragma clang fp contract(off)
 
@@ -43,8 +44,77 @@ __device__ inline void ts_acc(Acc& acc, const ts::TsParams& P, ts::TsLane& L,
               (int64_t)h * P.k << 20, rel, (int64_t)h * P.k, L.steps, L.c_act, L.status, hist);
 }
 
+// one finished episode: summary, record, per-node row
+template <class Src, class St>
+__device__ inline void ts_finish(const ts::TsParams& P, ts::TsLane& L, const ts::TsMem& M,
+                                 const St& S, int64_t e, int32_t hd, Acc& acc, int32_t* hist,
+                                 cpr_episode_record* recs, const NodeOut& no) {
+  L.status |= Src::missed(S);
+  ts_acc(acc, P, L, M, hd, hist);
+  if (recs) {
+    cpr_episode_record r;
+    ts_head_rewards(P, L, M, hd, &r.reward_attacker, &r.reward_defender);
+    const ts::TVtx& h = L.X(P, M, hd);
+    r.progress = (double)(h.height * P.k);
+    r.chain_time = h.time;
+    r.sim_time = P.mode == CPR_MODE_GYM ? L.now : 0.0;
+    r.n_steps = L.steps;
+    r.n_activations = L.c_act;
+    r.head_height = h.height;
+    r.head_miner = -1;
+    r.status = L.status;
+    r.head_work = 0;
+    recs[e] = r;
+  }
+  if (no.acts) {  // csv_runner.ml:74-79: sim.activations and (Dag.data head).rewards
+    const ts::TVtx& h = L.X(P, M, hd);
+    const double* hr = h.qslot < 0 ? nullptr : L.R(P, M, h.qslot);
+    for (int32_t j = 0; j < P.n; ++j) {
+      no.acts[e * P.n + j] = M.nact[j];
+      no.rews[e * P.n + j] = hr ? hr[j] : 0.0;
+    }
+    no.head_miner[e] = -1;  // summaries have no miner (tailstorm.ml info: kind, height)
+  }
+}
+
+// wave_sched.h adapter: gym episodes (engine.ml reset / step with the on-device policy) and
+// Simulator.loop tasks of ts_lane.h
+struct TsAdapter {
+  using Lane = ts::TsLane;
+  using Par = ts::TsParams;
+  using Mem = ts::TsMem;
+  template <class St>
+  __device__ static void begin(Lane& L, const Par& P, const St& S, const Mem& M) {
+    L.init(P, S, M);
+  }
+  __device__ static bool gym(const Par& P) { return P.mode == CPR_MODE_GYM; }
+  __device__ static bool loop_attacker(const Par& P) { return P.net != 2; }
+  __device__ static bool pow0(uint32_t ev) {
+    return (ev & 7u) == ts::EV_DAG && (ev >> 5) == 0u && ((ev >> 3) & 3u) == ts::KD_POW;
+  }
+  template <class St>
+  __device__ static void run_pow0(Lane& L, const Par& P, const St& S, const Mem& M, int32_t) {
+    const int32_t v = L.append_vote(P, S, M, 0, L.payload_parent(P, M, 0, L.priv));
+    L.push_now(P, M, bk::mkev(ts::EV_MV, 0, ts::KD_POW), v);
+  }
+  __device__ static void act(Lane& L, const Par& P, const Mem& M) {
+    L.apply(P, M, ts::ts_policy_p(P, L.observe(P, M)));
+    ++L.steps;
+  }
+  __device__ static int32_t head_gym(Lane& L, const Par& P, const Mem& M, int32_t att) {
+    return L.dead ? 0 : L.head(P, M, att);
+  }
+  __device__ static int32_t head_loop(Lane& L, const Par& P, const Mem& M) {
+    return L.dead ? 0 : L.head(P, M, P.net == 2 ? M.tips[0] : L.priv);
+  }
+  __device__ static bool gym_done(Lane& L, const Par& P, const Mem& M, int32_t hd) {
+    const double progress = (double)(L.X(P, M, hd).height * P.k);
+    return L.dead || !(L.steps < P.max_steps && progress < P.max_progress && L.now < P.max_time);
+  }
+};
+
 template <class Src>
-__global__ __launch_bounds__(kBlock) void k_ts_run_episodes(
+__global__ __launch_bounds__(kBlock) CPR_EV_OCC void k_ts_run_episodes(
     ts::TsParams P, Src src, int64_t n_eps, uint8_t* mem,
     int64_t lane_bytes, cpr_episode_record* recs, cpr_summary* sum, NodeOut no) {
   __shared__ int32_t hist[CPR_HIST_BINS];
@@ -56,6 +126,34 @@ __global__ __launch_bounds__(kBlock) void k_ts_run_episodes(
   if (no.mem) M.nact = (int64_t*)(no.mem + tid * no.lane_bytes);
   Acc acc = {};
   ts::TsLane L;
+#if CPR_EV_SCHED
+  // wave-coherent dispatch (wave_sched.h): grid-stride over episodes, every iteration runs
+  // the work class most lanes of the wave hold
+  int64_t e = tid;
+  auto S = src.at(e < n_eps ? e : 0);
+  EvCursor c;
+  c.cls = -1;
+  c.phase = PH_IDLE;
+  if (e < n_eps) ev_begin<TsAdapter>(L, P, S, M, c);
+  for (;;) {
+    while (c.phase != PH_IDLE && c.cls < 0) {
+      if (c.phase != PH_OVER) ev_fetch<TsAdapter>(L, P, S, M, c);
+      if (c.phase == PH_OVER) {
+        ts_finish<Src>(P, L, M, S, e, c.hd, acc, hist, recs, no);
+        e += nthreads;
+        if (e < n_eps) {
+          S = src.at(e);
+          ev_begin<TsAdapter>(L, P, S, M, c);
+        } else {
+          c.phase = PH_IDLE;
+        }
+      }
+    }
+    const int32_t k = ev_choose(c.cls);
+    if (k < 0) break;
+    if (c.cls == k) ev_exec<TsAdapter>(L, P, S, M, c);
+  }
+#else
   for (int64_t e = tid; e < n_eps; e += nthreads) {
     const auto S = src.at(e);
     int32_t hd;
@@ -67,33 +165,9 @@ __global__ __launch_bounds__(kBlock) void k_ts_run_episodes(
     } else {
       hd = L.loop(P, S, M);
     }
-    L.status |= Src::missed(S);
-    ts_acc(acc, P, L, M, hd, hist);
-    if (recs) {
-      cpr_episode_record r;
-      ts_head_rewards(P, L, M, hd, &r.reward_attacker, &r.reward_defender);
-      const ts::TVtx& h = L.X(P, M, hd);
-      r.progress = (double)(h.height * P.k);
-      r.chain_time = h.time;
-      r.sim_time = P.mode == CPR_MODE_GYM ? L.now : 0.0;
-      r.n_steps = L.steps;
-      r.n_activations = L.c_act;
-      r.head_height = h.height;
-      r.head_miner = -1;
-      r.status = L.status;
-      r.head_work = 0;
-      recs[e] = r;
-    }
-    if (no.acts) {  // csv_runner.ml:74-79: sim.activations and (Dag.data head).rewards
-      const ts::TVtx& h = L.X(P, M, hd);
-      const double* hr = h.qslot < 0 ? nullptr : L.R(P, M, h.qslot);
-      for (int32_t j = 0; j < P.n; ++j) {
-        no.acts[e * P.n + j] = M.nact[j];
-        no.rews[e * P.n + j] = hr ? hr[j] : 0.0;
-      }
-      no.head_miner[e] = -1;  // summaries have no miner (tailstorm.ml info: kind, height)
-    }
+    ts_finish<Src>(P, L, M, S, e, hd, acc, hist, recs, no);
   }
+#endif
   __syncthreads();
   block_flush(acc, hist, sum);
 }
@@ -181,7 +255,7 @@ __global__ __launch_bounds__(kBlock) void k_ts_step(ts::TsParams P, uint64_t see
 }
 
 // see k_bk_rollout
-__global__ __launch_bounds__(kBlock) void k_ts_rollout(ts::TsParams P, uint64_t seed,
+__global__ __launch_bounds__(kBlock) CPR_EV_OCC void k_ts_rollout(ts::TsParams P, uint64_t seed,
                                                         uint8_t* mem, int64_t lane_bytes,
                                                         TsSlot* slots, int64_t n,
                                                         int64_t n_steps, int unit,

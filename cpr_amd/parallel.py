@@ -55,6 +55,27 @@ def allreduce_summary(summary, device=None):
     return L.Summary.from_array(t.cpu().numpy())
 
 
+def allreduce_summaries(summaries, device=None):
+    """Sum a list of cpr_summary over all ranks with ONE collective: the int64 vectors are
+    packed into one tensor (one all-reduce of the batch summaries)."""
+    import torch
+    import torch.distributed as dist
+
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return list(summaries)
+    arrs = [s.to_array() for s in summaries]
+    t = torch.from_numpy(np.concatenate(arrs))
+    if device is not None:
+        t = t.to(device)
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    flat = t.cpu().numpy()
+    out, o = [], 0
+    for a in arrs:
+        out.append(L.Summary.from_array(flat[o:o + len(a)].copy()))
+        o += len(a)
+    return out
+
+
 def barrier(device=None):
     import torch.distributed as dist
 

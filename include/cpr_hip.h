@@ -380,6 +380,7 @@ int cpr_last_launch(cpr_batch* b, double* kernel_ms, int64_t* activations);
 /* shape of the last episode-kernel launch of this batch (fused episodes, replay, rollout):
  * lanes = device lanes launched; resident = lanes the device holds at once for that kernel
  * (occupancy API x CUs x 256, before the HBM budget and the episode count cap the launch).
+ * Before any launch lanes = 0 and resident is the fused-episode kernel's figure.
  * Diagnostic for bench.py (lanes / resident), no reference counterpart. ABI v9. */
 int cpr_launch_shape(cpr_batch* b, int64_t* lanes, int64_t* resident);
 /* cumulative count of exact Nakamoto re-runs on this context whose episode outgrew the

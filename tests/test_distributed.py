@@ -89,3 +89,59 @@ def test_gloo_world2_allreduce_equals_single_process():
     whole = summarize(_records()).to_array().tolist()
     for rank, arr, lo, hi in outs:
         assert arr == whole
+
+
+# bench.py's episode bases: step k of rank r runs episodes [(k * ws + r) * E, + E) of every
+# sweep point, and the summaries of all points go through ONE packed all-reduce
+# (parallel.allreduce_summaries). Over K steps the ranks together cover [0, K * ws * E)
+# exactly once, so the all-reduced totals must equal one process's summary of that range,
+# bit for bit, at any world size.
+E_BENCH, K_BENCH = 6, 2
+BENCH_POINTS = [(0.3, 0.5), (0.45, 0.0)]
+
+
+def _bench_records(point, first, n):
+    import oracle_py
+
+    cfg, _ = device.make_config(alpha=point[0], gamma=point[1], max_steps=120, seed=0x5EED0000)
+    return oracle_py.run_episodes(cfg, first, n)
+
+
+def _bench_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    import sys
+
+    sys.path.insert(0, os.path.join(os.path.dirname(__file__)))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    sums = []
+    for pt in BENCH_POINTS:
+        recs = [_bench_records(pt, (k * world + rank) * E_BENCH, E_BENCH) for k in range(K_BENCH)]
+        sums.append(summarize(np.concatenate(recs)))
+    tot = parallel.allreduce_summaries(sums)
+    q.put((rank, [t.to_array().tolist() for t in tot]))
+    dist.destroy_process_group()
+
+
+def _run_world(world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 29700 + world * 7 + os.getpid() % 500
+    procs = [ctx.Process(target=_bench_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    outs = [q.get(timeout=600) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    return outs
+
+
+def test_gloo_bench_bases_world4_and_world8_equal_single_process():
+    for world in (4, 8):
+        outs = _run_world(world)
+        whole = [summarize(_bench_records(pt, 0, K_BENCH * world * E_BENCH)).to_array().tolist()
+                 for pt in BENCH_POINTS]
+        assert len(outs) == world
+        for rank, arrs in outs:
+            assert arrs == whole, (world, rank)

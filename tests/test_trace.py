@@ -166,3 +166,41 @@ def test_withholding_rows_from_ocaml_traces():
     for row, cfg, trace, rec in withholding_traces():
         check_withholding_record(row, rec)
         check_withholding_record(row, O.replay(cfg, trace))
+
+
+def test_ocaml_recorder_format_round_trips(tmp_path):
+    # integration/ocaml/trace_hooks.ml `write` (uncompiled here: no OCaml) emits the binary
+    # layout Trace.load reads. Its array order and element widths are checked against the
+    # reader statically; Trace.save_binary mirrors the writer byte for byte, and traces of
+    # the OCaml Random stream (the reference's own draws) and of the keyed stream survive
+    # the round trip and replay to the same records
+    ml = (pathlib.Path(__file__).parents[1] / "integration" / "ocaml" / "trace_hooks.ml").read_text()
+    writes = __import__("re").findall(r"^  arr (i64|u32|f64) ", ml, flags=__import__("re").M)
+    width = {"i64": 8, "u32": 4, "f64": 8}
+    assert [width[w] for w in writes] == [np.dtype(L.Trace._WIRE[n]).itemsize
+                                         for n, _ in L.Trace.ARRAYS]
+    assert [w == "f64" for w in writes] == [np.dtype(L.Trace._WIRE[n]).kind == "f"
+                                           for n, _ in L.Trace.ARRAYS]
+    assert 'Buffer.add_string buf "CPRTRACE"' in ml
+    cases = [
+        (dict(alpha=0.33, network=L.NET_TWO_AGENTS, mode=L.MODE_LOOP, activations=400,
+              policy=L.POLICY_SAPIRSHTEIN_2016_SM1), O.OcamlRandom()),
+        (dict(alpha=0.35, gamma=0.5, max_steps=200, seed=3), None),
+        (dict(protocol=L.PROTO_BK, k=4, alpha=0.3, gamma=0.5, max_steps=60,
+              policy=L.BK_POLICY_GET_AHEAD, seed=5), None),
+    ]
+    for i, (kw, rng) in enumerate(cases):
+        cfg, _ = device.make_config(**kw)
+        trace, rec = O.export_traces(cfg, 0, 3 if rng is None else 1, rng=rng)
+        path = tmp_path / f"t{i}.cprtrace"
+        trace.save_binary(path)
+        assert open(path, "rb").read(8) == b"CPRTRACE"
+        back = L.Trace.load(path)
+        for name, _ in L.Trace.ARRAYS:
+            assert np.array_equal(getattr(back, name), getattr(trace, name)), name
+        _assert_same(O.replay(cfg, back), rec)
+    # a truncated file is rejected
+    raw = open(tmp_path / "t0.cprtrace", "rb").read()
+    (tmp_path / "bad.cprtrace").write_bytes(raw[:-8])
+    with pytest.raises(ValueError):
+        L.Trace.load(tmp_path / "bad.cprtrace")

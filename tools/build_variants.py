@@ -1,0 +1,41 @@
+"""Occupancy variants of libcpr_hip for A/B runs (tools/occupancy_ab.sh): the three
+event-engine translation units rebuilt with -DCPR_EV_WAVES=<w> (kernels.h), linked with the
+default build's other objects into build/var/ev<w>.so. Run __graft_entry__.build() first.
+
+Usage: python tools/build_variants.py 2 4
+"""
+import pathlib
+import subprocess
+import sys
+
+ROOT = pathlib.Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT))
+import __graft_entry__ as G  # noqa: E402
+
+EV = ["kernels_eth.hip", "kernels_bk.hip", "kernels_ts.hip"]
+
+
+def main():
+    objdir = ROOT / "build" / "hip"
+    out = ROOT / "build" / "var"
+    out.mkdir(parents=True, exist_ok=True)
+    flags = [f for f in G.HIPCC_FLAGS if f != "-shared"]
+    for w in sys.argv[1:]:
+        vdir = out / f"ev{w}"
+        vdir.mkdir(exist_ok=True)
+        procs = []
+        for s in EV:
+            cmd = [G._hipcc(), *flags, f"-DCPR_EV_WAVES={w}", f"-I{ROOT / 'include'}", "-c",
+                   str(G.CSRC / s), "-o", str(vdir / (s + ".o"))]
+            procs.append(subprocess.Popen(cmd))
+        for p in procs:
+            assert p.wait() == 0
+        objs = [str((vdir if s in EV else objdir) / (s + ".o"))
+                for s in ["kernels.hip", *EV, "kernels_fc16.hip", "capi.hip"]]
+        subprocess.run([G._hipcc(), "--offload-arch=gfx950", "-shared", "-fPIC", *objs, "-o",
+                        str(out / f"ev{w}.so")], check=True)
+        print("built", out / f"ev{w}.so")
+
+
+if __name__ == "__main__":
+    main()

@@ -29,36 +29,45 @@ import numpy as np
 from cpr_amd import _lib as L
 from cpr_amd import device
 
+N = None
 
 def fused(cfg, keep, n):
+    """One launch of n episodes; n = 0: the kernel's resident lane count (one episode per
+    resident lane, the grid full), found from a small warm-up launch (cpr_launch_shape)."""
     b = device.Batch(cfg, keep=keep)
-    b.run(min(n, 4096), first_episode=1 << 40)
+    b.run(256, first_episode=1 << 40)
+    _, resident = b.launch_shape()
+    if n == 0:
+        n = resident
     t = time.perf_counter()
     s = b.run(n)
     wall = time.perf_counter() - t
     ms, acts = b.last_launch()
+    lanes, _ = b.launch_shape()
     return dict(episodes=n, activations=int(s.activations), steps=int(s.steps), kernel_ms=ms,
-                wall_s=wall, invalid=int(s.invalid))
+                wall_s=wall, invalid=int(s.invalid), lanes=lanes, resident_lanes=resident)
 
 
 def main():
     which = sys.argv[1]
+    global N
+    N = int(sys.argv[2]) if len(sys.argv) > 2 else None  # episodes; 0 = resident lanes
     if which == "eth":
         cfg, keep = device.make_config(protocol=L.PROTO_ETHEREUM, alpha=0.35, gamma=0.5,
                                        policy=L.ETH_POLICY_FN19, reward_scheme=L.REWARD_CONSTANT,
                                        max_steps=2016, seed=1)
-        out = fused(cfg, keep, 131072)
+        out = fused(cfg, keep, 131072 if N is None else N)
         out["kernel"] = "k_eth_run_episodes"
     elif which == "eth_honest":
         cfg, keep = device.make_config(protocol=L.PROTO_ETHEREUM, alpha=0.25, gamma=0.0,
                                        policy=L.ETH_POLICY_HONEST, reward_scheme=L.REWARD_DISCOUNT,
                                        max_steps=2016, seed=1)
-        out = fused(cfg, keep, 131072)
+        out = fused(cfg, keep, 131072 if N is None else N)
         out["kernel"] = "k_eth_run_episodes"
     elif which == "bk":
         cfg, keep = device.make_config(protocol=L.PROTO_BK, alpha=0.33, gamma=0.5, k=8,
                                        policy=L.BK_POLICY_MINOR_DELAY, max_steps=2048, seed=1)
-        out = fused(cfg, keep, 131072)
+        out = fused(cfg, keep, 131072 if N is None else N)
         out["kernel"] = "k_bk_run_episodes"
     elif which == "ts_exp":
         # configs[3]'s exp(1)-propagation variant: attacker + 1 defender, exponential links
@@ -68,7 +77,7 @@ def main():
                                        activations=10000, k=8, reward_scheme=L.REWARD_DISCOUNT,
                                        subblock_selection=L.SELECT_HEURISTIC,
                                        policy=L.TS_POLICY_GET_AHEAD, seed=1)
-        out = fused(cfg, keep, 65536)
+        out = fused(cfg, keep, 65536 if N is None else N)
         out["kernel"] = "k_ts_run_episodes"
     elif which == "ts":
         cfg, keep = device.make_config(protocol=L.PROTO_TAILSTORM, alpha=0.33,
@@ -76,7 +85,7 @@ def main():
                                        activations=10000, k=8, reward_scheme=L.REWARD_DISCOUNT,
                                        subblock_selection=L.SELECT_HEURISTIC,
                                        policy=L.TS_POLICY_GET_AHEAD, seed=1)
-        out = fused(cfg, keep, 32768)
+        out = fused(cfg, keep, 32768 if N is None else N)
         out["kernel"] = "k_ts_run_episodes"
     elif which == "bk_rollout":
         K, D, lanes = 8, 4, 65536

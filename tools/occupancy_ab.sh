@@ -1,19 +1,15 @@
 #!/bin/bash
-# A/B of k_run_episodes occupancy variants (build/var/w{4,5,6}.so: amdgpu_waves_per_eu 4/5/6
-# for the gym kernel): the default bench workload without the CPU leg, one run per variant.
+# A/B of the event-engine kernels' occupancy (tools/build_variants.py: build/var/ev<w>.so,
+# CPR_EV_WAVES = w) on the event probes at resident capacity (tools/event_probe.py <p> 0).
+# Usage: VARIANTS="0 2 4" PROBES="eth bk ts_exp" bash tools/occupancy_ab.sh
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
-cp cpr_amd/libcpr_hip.so gpurun_out/orig.so
-for v in w4 w5 w6 w5 w4; do
-  cp build/var/$v.so cpr_amd/libcpr_hip.so
-  timeout -k 10 180 python bench.py --steps 5 --warmup 1 --no-cpu > gpurun_out/ab_$v.log 2>&1
-  rc=$?; echo "$v rc=$rc" >> gpurun_out/ab_status.log; [[ $rc -eq 0 ]] || exit $rc
-  python - "$v" >> gpurun_out/ab_status.log <<'PY'
-import json, sys
-v = sys.argv[1]
-line = [l for l in open(f"gpurun_out/ab_{v}.log") if l.startswith("{")][-1]
-d = json.loads(line)
-print(v, "value %.4e" % d["value"], "kernel_ms %.3f" % d["roofline"]["kernel_ms_mean"])
-PY
+for v in ${VARIANTS:-0 2 4}; do
+  lib=cpr_amd/libcpr_hip.so
+  [[ $v != 0 ]] && lib=build/var/ev$v.so
+  for P in ${PROBES:-eth bk ts_exp}; do
+    CPR_HIP_LIB=$PWD/$lib timeout -k 10 ${PROBE_TIMEOUT:-150} python tools/event_probe.py $P 0 > gpurun_out/ab_ev${v}_$P.json 2>gpurun_out/ab_ev${v}_$P.err
+    rc=$?; echo "ev$v $P rc=$rc $(cat gpurun_out/ab_ev${v}_$P.json)" | tee -a gpurun_out/ab_status.log
+    [[ $rc -eq 0 ]] || exit $rc
+  done
 done
-cp gpurun_out/orig.so cpr_amd/libcpr_hip.so
