@@ -113,13 +113,14 @@ def other_config_specs():
         393216, None)]
     # configs[2]: Ethereum Byzantium, whitepaper (constant) uncle rewards, ethereum_ssz
     # selfish_release and fn19 over alpha x gamma, 2016-step gym episodes
-    eth = [dict(protocol=L.PROTO_ETHEREUM, alpha=a, gamma=g, policy=pol,
+    # (a launch at resident capacity lasts one 2016-step episode of the event engine,
+    # ~7 s, whatever the lane count: three points keep the bench within minutes)
+    eth = [dict(protocol=L.PROTO_ETHEREUM, alpha=0.45, gamma=g, policy=L.ETH_POLICY_FN19,
                 reward_scheme=L.REWARD_CONSTANT, max_steps=STEPS_PER_EPISODE)
-           for pol in (L.ETH_POLICY_SELFISH_RELEASE, L.ETH_POLICY_FN19)
-           for g in (0.0, 0.5, 0.9) for a in (0.25, 0.45)]
+           for g in (0.0, 0.5, 0.9)]
     specs.append(("configs[2]", "Ethereum-PoW uncle-aware selfish mining, Byzantium + whitepaper "
-                  "(constant) uncle rewards, ethereum_ssz selfish_release and fn19, alpha {.25, "
-                  ".45} x gamma {0, .5, .9}, 2016-step gym episodes", "ethereum",
+                  "(constant) uncle rewards, ethereum_ssz fn19 (Feng & Niu '19), alpha .45 x "
+                  "gamma {0, .5, .9}, 2016-step gym episodes", "ethereum",
                   "k_eth_run_episodes", eth, None, None))
     # configs[3]: Tailstorm k = 8, discount, heuristic sub-block selection, withholding
     # attack on the two-agents network (Simulator.loop tasks of 10^4 activations,
@@ -167,7 +168,7 @@ def _cpu_sample(cfg, seconds, threads, per_call):
     return acts, steps, eps, time.perf_counter() - t0
 
 
-def run_other_configs(ctx, cpu_seconds, with_cpu, pmc):
+def run_other_configs(ctx, cpu_seconds, with_cpu, pmc, keys=None):
     """One launch per point at the kernel's resident lane count (configs[0]: the headline's
     episode count), timed by the library's HIP events (cpr_last_launch) and by the host
     clock around each synchronous call; roofline at the §8d cost model; measured HBM bytes
@@ -178,6 +179,8 @@ def run_other_configs(ctx, cpu_seconds, with_cpu, pmc):
     cores, aff = _host_cores()
     out = {}
     for key, desc, proto, kernel, points, eps, roll in other_config_specs():
+        if keys is not None and key not in keys:
+            continue
         acts = steps = episodes = 0
         wall = kms = 0.0
         lanes_l, res_l = [], []
@@ -298,8 +301,11 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--episodes", type=int, default=393216, help="per GPU per sweep point")
-    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    # 20 x 262,144 = a whole number of rounds of the resident grid (4 or 5 waves/SIMD on
+    # 256 CUs: 262,144 or 327,680 lanes), and the driver's 20 steps make BASELINE configs[1]'s
+    # 10^8 episodes per (alpha, gamma) point on every GPU
+    ap.add_argument("--episodes", type=int, default=5242880, help="per GPU per sweep point")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-configs", action="store_true",
                     help="skip BASELINE configs[0], [2]-[4] (other_configs)")
@@ -416,6 +422,7 @@ def main():
                             "mining, alpha 0.05..0.50 x gamma {0, 0.5} (gamma=1 is rejected by "
                             "the reference), 2016-step cpr-nakamoto-v0 episodes",
                 "episodes_per_point_per_gpu": E,
+                "episodes_per_point_timed": E * args.steps * ws,
                 "points": len(points),
                 "activations_per_episode": STEPS_PER_EPISODE + 1,
                 "parallelism": f"dp{ws} (episode shards, 1 {'RCCL' if args.backend == 'nccl' else 'gloo'} "

@@ -943,7 +943,7 @@ static int run_async(cpr_batch* b, int64_t n, uint64_t first, const TraceSource*
   const int64_t lanes = episode_lanes(b, n);
   b->last_lanes = lanes;
   b->last_resident = (int64_t)b->ctx->cus * run_episodes_blocks_per_cu(b->cfg.mode) * 256;
-  // spill [cap][lane] f64 mining times (interleaved) | tie-replay scratch [lane]
+  // spill [lane][cap] f64 mining times | tie-replay scratch [lane]
   const size_t o_replay = align256((size_t)lanes * b->P.cap * sizeof(double));
   void* pool = nullptr;
   HIP_TRY(ctx_pool(b->ctx, o_replay + (size_t)lanes * REPLAY_BYTES, &pool));

@@ -57,6 +57,11 @@ struct EBlock {
 };
 static_assert(sizeof(EBlock) == 64, "EBlock layout");
 
+// host studies of the queue's operation sequence (tools/heap_study.cpp) define this
+#ifndef CPR_HEAP_HOOK
+#define CPR_HEAP_HOOK(op, t)
+#endif
+
 struct HNode {
   double t;
   uint32_t ev;
@@ -288,6 +293,7 @@ struct EthLane {
   }
   __host__ __device__ inline void push(const EthParams& P, const EthMem& M, double t,
                                        uint32_t ev, int32_t blk) {
+    CPR_HEAP_HOOK(0, t);
     int32_t parent = -1, node = hroot;
     for (;;) {
       if (node < 0) {
@@ -327,6 +333,7 @@ struct EthLane {
   }
   __host__ __device__ inline bool pop(const EthMem& M, double* t, uint32_t* ev, int32_t* blk) {
     if (hroot < 0) return false;
+    CPR_HEAP_HOOK(1, M.heap[hroot].t);
     *t = M.heap[hroot].t;
     *ev = M.heap[hroot].ev;
     *blk = M.heap[hroot].blk;

@@ -88,7 +88,9 @@ constexpr uint32_t kInexact = ST_OVERLAP | ST_DEEP_FORK | ST_TIE_UNRESOLVED | ST
 
 // POL: nakamoto_ssz policy fixed at compile time (P_HONEST .. P_SM1; these kernels never
 // run the abstract-gamma mode), or -1 for P.policy (and P.abstract_g)
-template <int MODE, class Src, int POL>
+// REC: 1 = per-episode records may be written (block mining times tracked for chain_time);
+// 0 = summary only (recs is null): the lane's time bookkeeping compiles out (LaneMem.times)
+template <int MODE, class Src, int POL, int REC = 1>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) void k_run_episodes(
     NakParams P, Src src, int64_t n_eps, int64_t activations,
     double* spill, uint8_t* replay, cpr_episode_record* recs, cpr_summary* sum,
@@ -105,12 +107,16 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
   LaneMem M;
   M.ring = ring + threadIdx.x;
   M.ring_stride = kBlock;
-  // spill interleaved [slot][lane] like the LDS ring: the evictions of a wave's lanes at
-  // the same chain depth land in adjacent words instead of 64 lines cap * 8 B apart
-  M.spill = spill + tid;
-  M.spill_stride = nthreads;
+  // spill per lane, contiguous: a lane's evictions are consecutive words, which the L2
+  // merges into whole lines over time. (Interleaving it [slot][lane] like the LDS ring was
+  // measured 9 % slower per launch: lanes of a wave evict at different depths, so their
+  // words rarely share a line anyway; profiles/r03e_nak_ab.log)
+  M.spill = spill + tid * P.cap;
+  M.spill_stride = 1;
   M.cap = P.cap;
   M.replay = ReplayMem::at(replay + tid * REPLAY_BYTES);
+  M.times = REC != 0;
+  if (!REC) recs = nullptr;
   NakLane L;
   for (int64_t e = tid; e < n_eps; e += nthreads) {
     const auto S = src.at(e);
@@ -133,7 +139,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
       st_out |= CPR_ST_CAPACITY;  // the exact event engine has no abstract-gamma mode
     }
     acc_add(acc, hd, steps, L.k, st_out, hist);
-    if (recs) {
+    if (REC && recs) {
       cpr_episode_record r;
       r.reward_attacker = (double)hd.ra;
       r.reward_defender = (double)(hd.h - hd.ra);
@@ -168,8 +174,8 @@ __device__ inline LaneMem lock_mem(const NakParams& P, const LockBuffers& B, int
   LaneMem M;
   M.ring = B.ring + i;
   M.ring_stride = n;
-  M.spill = B.spill + i;  // [slot][lane], as the fused kernel's
-  M.spill_stride = n;
+  M.spill = B.spill + i * P.cap;  // per lane, contiguous, as the fused kernel's
+  M.spill_stride = 1;
   M.cap = P.cap;
   M.replay = ReplayMem::at(B.replay + i * REPLAY_BYTES);
   return M;
@@ -301,24 +307,34 @@ hipError_t launch_run_episodes(const NakParams& P, uint64_t seed, uint64_t first
                                uint32_t launch_id, int64_t redo_cap, hipStream_t st) {
   const unsigned blocks = (unsigned)(lanes / kBlock);
   const SeedSource src{seed, first};
-#define CPR_LAUNCH(MODE, POL)                                                                    \
-  hipLaunchKernelGGL((k_run_episodes<MODE, SeedSource, POL>), dim3(blocks), dim3(kBlock), 0, st, \
-                     P, src, n_eps, activations, spill, replay, recs, sum, redo, redo_n,         \
+#define CPR_LAUNCH_R(MODE, POL, REC)                                                            \
+  hipLaunchKernelGGL((k_run_episodes<MODE, SeedSource, POL, REC>), dim3(blocks), dim3(kBlock), 0, \
+                     st, P, src, n_eps, activations, spill, replay, recs, sum, redo, redo_n,     \
                      launch_id, redo_cap)
+#define CPR_LAUNCH(MODE, POL) CPR_LAUNCH_R(MODE, POL, 1)
+  // the built-in policies get their own specialisation, and a summary-only one (no records
+  // asked for: no block-time bookkeeping)
+#define CPR_LAUNCH_POL(POL)                                  \
+  do {                                                       \
+    if (recs) CPR_LAUNCH_R(CPR_MODE_GYM, POL, 1);            \
+    else CPR_LAUNCH_R(CPR_MODE_GYM, POL, 0);                 \
+  } while (0)
   if (mode == CPR_MODE_GYM && P.abstract_g) {
     CPR_LAUNCH(CPR_MODE_GYM, -1);  // flagged abstract-gamma mode: the generic kernel
   } else if (mode == CPR_MODE_GYM) {
-    switch (P.policy) {  // the built-in policies get their own specialisation
-      case P_HONEST: CPR_LAUNCH(CPR_MODE_GYM, P_HONEST); break;
-      case P_SIMPLE: CPR_LAUNCH(CPR_MODE_GYM, P_SIMPLE); break;
-      case P_ES2014: CPR_LAUNCH(CPR_MODE_GYM, P_ES2014); break;
-      case P_SM1: CPR_LAUNCH(CPR_MODE_GYM, P_SM1); break;
+    switch (P.policy) {
+      case P_HONEST: CPR_LAUNCH_POL(P_HONEST); break;
+      case P_SIMPLE: CPR_LAUNCH_POL(P_SIMPLE); break;
+      case P_ES2014: CPR_LAUNCH_POL(P_ES2014); break;
+      case P_SM1: CPR_LAUNCH_POL(P_SM1); break;
       default: CPR_LAUNCH(CPR_MODE_GYM, -1);
     }
   } else {
     CPR_LAUNCH(CPR_MODE_LOOP, -1);
   }
+#undef CPR_LAUNCH_POL
 #undef CPR_LAUNCH
+#undef CPR_LAUNCH_R
   return hipGetLastError();
 }
 

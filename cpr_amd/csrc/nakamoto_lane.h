@@ -73,6 +73,11 @@ struct LaneMem {
   int64_t ring_stride, spill_stride;
   int32_t cap;
   ReplayMem replay;
+  // block mining times are tracked (BRef.tm, the ring and its spill): they feed only the
+  // record's chain_time. A kernel that writes no records sets this to a compile-time false
+  // and every time computation, ring store and spill store drops out of the inlined lane
+  // (the summary does not depend on them).
+  bool times = true;
 };
 
 constexpr int32_t K_GENESIS = -1, K_PRIVATE = -2;
@@ -374,6 +379,7 @@ struct NakLane {
   double w_bound;    // conservative bound on that window's latest arrival
 
   __host__ __device__ inline CPR_AI double chain_t(const LaneMem& M, int32_t m) const {
+    if (!M.times) return 0.0;
     // two loads in their own address spaces (ds_read, then a rare global load) rather than
     // a select of pointers, which would compile to a generic flat load
     double v = M.ring[(m & (RING - 1)) * M.ring_stride];
@@ -468,9 +474,11 @@ struct NakLane {
         status |= ST_DEEP_FORK;
         m = M.cap - 1;
       }
-      double* slot = M.ring + (m & (RING - 1)) * M.ring_stride;
-      if (m > RING) M.spill[(int64_t)(m - RING) * M.spill_stride] = *slot;  // evict
-      *slot = tn;
+      if (M.times) {
+        double* slot = M.ring + (m & (RING - 1)) * M.ring_stride;
+        if (m > RING) M.spill[(int64_t)(m - RING) * M.spill_stride] = *slot;  // evict
+        *slot = tn;
+      }
       n = m;
     }
     // the defender block (its fields are meaningless when the attacker mined)
@@ -479,7 +487,7 @@ struct NakLane {
     b.ra = par_a ? A.ra : D.ra;
     b.fork = par_a ? A.fork : D.fork;
     b.k = ka;
-    b.tm = tn;
+    b.tm = M.times ? tn : 0.0;
     sel(pub, !att && b.h > pub.h, b);
     event = att ? 0 : 1;
   }

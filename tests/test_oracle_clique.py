@@ -68,12 +68,19 @@ CHAINS = json.loads((pathlib.Path(__file__).parent / "golden" / "honest_net_chai
 BY_LINE = {r["line"]: r for r in CHAINS}
 
 
+_CHAIN_END = {}
+
+
 def chained_rng(row):
-    """OCaml's default Random state advanced over the row's recovered worker chain."""
-    rng = O.OcamlRandom()
-    for ln in row["chain"]:
-        CH.run(BY_LINE[ln], rng)
-    return rng
+    """OCaml's default Random state advanced over the row's recovered worker chain (a copy of
+    a per-process memo: several GPU tests start from the same row's state)."""
+    key = tuple(row["chain"])
+    if key not in _CHAIN_END:
+        rng = O.OcamlRandom()
+        for ln in row["chain"]:
+            CH.run(BY_LINE[ln], rng)
+        _CHAIN_END[key] = rng
+    return _CHAIN_END[key].copy()
 
 
 def test_chain_fixture_covers_bk_and_tailstorm():
