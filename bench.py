@@ -183,7 +183,7 @@ def run_other_configs(ctx, cpu_seconds, with_cpu, pmc, keys=None):
             continue
         acts = steps = episodes = 0
         wall = kms = 0.0
-        lanes_l, res_l = [], []
+        lanes_l, res_l, point_ms = [], [], []
         for pt in points:
             cfg, keep = device.make_config(seed=SEED, **pt)
             b = device.Batch(cfg, ctx=ctx, keep=keep)
@@ -200,6 +200,7 @@ def run_other_configs(ctx, cpu_seconds, with_cpu, pmc, keys=None):
             wall += time.perf_counter() - t0
             ms, _ = b.last_launch()
             kms += ms
+            point_ms.append(round(ms, 3))
             ln, res = b.launch_shape()
             lanes_l.append(ln)
             res_l.append(res)
@@ -216,6 +217,7 @@ def run_other_configs(ctx, cpu_seconds, with_cpu, pmc, keys=None):
             "activations": acts,
             "activations_per_s": acts / wall,
             "kernel_ms": kms,
+            "kernel_ms_per_point": point_ms,
             "kernel_activations_per_s": kact,
             "lanes_per_launch": lanes_l[0],
             "resident_lanes": res_l[0],

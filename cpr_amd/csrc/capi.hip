@@ -111,6 +111,10 @@ struct cpr_batch {
   DevBuf tr_off, tr_miner, tr_delay, tr_pow, tr_key, tr_ldelay;  // cpr_replay trace copy
   // lockstep lanes
   DevBuf lanes, lring, lspill, lreplay, l_obs, l_act, l_rew, l_done, l_mask, l_eps, l_info;
+  // exact Nakamoto lockstep lanes (LockBuffers): action log, event-engine slots
+  DevBuf l_alog, l_emem, l_eslots, l_efree;
+  int64_t alog_cap = 0;
+  int32_t n_exact_slots = 0;
   bool reset_done = false;
   int32_t tab_n = 4096;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
@@ -810,7 +814,7 @@ int cpr_batch_destroy(cpr_batch* b) {
   for (DevBuf* d : {&b->table_dev, &b->tabs_dev, &b->summary,
                     &b->records, &b->lanes, &b->lring, &b->lspill, &b->lreplay,
                     &b->l_obs, &b->l_act, &b->l_rew, &b->l_done, &b->l_mask, &b->l_eps,
-                    &b->l_info, &b->tr_off, &b->tr_miner, &b->tr_delay, &b->tr_pow,
+                    &b->l_info, &b->l_alog, &b->l_emem, &b->l_eslots, &b->l_efree, &b->tr_off, &b->tr_miner, &b->tr_delay, &b->tr_pow,
                     &b->tr_key, &b->tr_ldelay})
     d->release();
   delete b;
@@ -1301,7 +1305,29 @@ static int ensure_lockstep(cpr_batch* b) {
   const int64_t n = b->cfg.n_lanes;
   if (n <= 0) return fail(CPR_E_STATE, "batch has no lockstep lanes (cfg.n_lanes = 0)");
   if (b->cfg.mode != CPR_MODE_GYM) return fail(CPR_E_STATE, "lockstep lanes need CPR_MODE_GYM");
-  HIP_TRY(b->lanes.ensure((size_t)n * lock_lane_bytes()));
+  if (!b->lanes.p) {
+    HIP_TRY(b->lanes.ensure((size_t)n * lock_lane_bytes()));
+    HIP_TRY(hipMemsetAsync(b->lanes.p, 0, (size_t)n * lock_lane_bytes(), b->ctx->stream));
+  }
+  if (b->has_rerun && !b->l_alog.p) {
+    // lanes leaving the closed form continue on the exact engine: an action log of the
+    // episode so far (at most 2^14 steps, <= 1 GiB) and kExactSlots event-engine lanes,
+    // handed out on first need and returned at the lane's next reset
+    constexpr int64_t kExactSlots = 256;
+    const int64_t ms = b->P.max_steps > 0 ? b->P.max_steps : (1 << 14);
+    int64_t cap = std::min<int64_t>(ms, 1 << 14);
+    cap = std::max<int64_t>(1, std::min<int64_t>(cap, (1ll << 30) / n));
+    b->alog_cap = cap;
+    b->n_exact_slots = (int32_t)std::min<int64_t>(n, kExactSlots);
+    HIP_TRY(b->l_alog.ensure((size_t)n * (size_t)cap));
+    HIP_TRY(b->l_emem.ensure((size_t)b->n_exact_slots * (size_t)b->nak_bytes));
+    HIP_TRY(b->l_eslots.ensure((size_t)b->n_exact_slots * sizeof(eth::EthLane)));
+    std::vector<int32_t> stack((size_t)b->n_exact_slots + 1);
+    for (int32_t i = 0; i < b->n_exact_slots; i++) stack[i] = i;
+    stack[b->n_exact_slots] = b->n_exact_slots;  // stack height: every slot free
+    HIP_TRY(b->l_efree.ensure(stack.size() * 4));
+    HIP_TRY(hipMemcpy(b->l_efree.p, stack.data(), stack.size() * 4, hipMemcpyHostToDevice));
+  }
   HIP_TRY(b->lring.ensure((size_t)n * RING * sizeof(double)));
   HIP_TRY(b->lspill.ensure((size_t)n * b->P.cap * sizeof(double)));
   HIP_TRY(b->lreplay.ensure((size_t)n * REPLAY_BYTES));
@@ -1321,6 +1347,13 @@ static LockBuffers lock_buffers(cpr_batch* b) {
   B.ring = (double*)b->lring.p;
   B.spill = (double*)b->lspill.p;
   B.replay = (uint8_t*)b->lreplay.p;
+  B.alog = (uint8_t*)b->l_alog.p;
+  B.alog_cap = b->alog_cap;
+  B.emem = (uint8_t*)b->l_emem.p;
+  B.elane_bytes = b->nak_bytes;
+  B.eslots = b->l_eslots.p;
+  B.efree = (int32_t*)b->l_efree.p;
+  B.n_slots = b->n_exact_slots;
   return B;
 }
 
@@ -1413,8 +1446,13 @@ int cpr_step(cpr_batch* b, const int32_t* actions, double* obs, double* reward, 
                            b->bk_slots.p, n, (const int32_t*)b->l_act.p,
                            b->cfg.unit_observation, tabs, b->tab_n, sb, st));
   else
-    HIP_TRY(launch_step(b->P, b->cfg.seed, lock_buffers(b), n, (const int32_t*)b->l_act.p,
+  {
+    const LockBuffers LB = lock_buffers(b);
+    HIP_TRY(launch_step(b->P, b->cfg.seed, LB, n, (const int32_t*)b->l_act.p,
                         b->cfg.unit_observation, tabs, tabs + b->tab_n, b->tab_n, sb, st));
+    HIP_TRY(launch_lock_exact(b->NEP, b->cfg.seed, LB, n, (const int32_t*)b->l_act.p,
+                              b->cfg.unit_observation, tabs, tabs + b->tab_n, b->tab_n, sb, st));
+  }
   HIP_TRY(hipMemcpyAsync(obs, sb.obs, (size_t)n * ol * 8, hipMemcpyDeviceToHost, st));
   HIP_TRY(hipMemcpyAsync(reward, sb.reward, (size_t)n * 8, hipMemcpyDeviceToHost, st));
   HIP_TRY(hipMemcpyAsync(done, sb.done, (size_t)n, hipMemcpyDeviceToHost, st));
@@ -1454,7 +1492,7 @@ int cpr_observe_fields(cpr_batch* b, int32_t* fields) {
     HIP_TRY(launch_ts_observe_fields(b->TP, (uint8_t*)b->bk_lmem.p, b->bk_bytes, b->bk_slots.p,
                                      n, (int32_t*)tmp.p, st));
   else
-    HIP_TRY(launch_observe_fields(b->lanes.p, n, (int32_t*)tmp.p, st));
+    HIP_TRY(launch_observe_fields(b->NEP, lock_buffers(b), n, (int32_t*)tmp.p, st));
   HIP_TRY(hipMemcpyAsync(fields, tmp.p, (size_t)n * per, hipMemcpyDeviceToHost, st));
   HIP_TRY(hipStreamSynchronize(st));
   tmp.release();

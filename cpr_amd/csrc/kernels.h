@@ -55,6 +55,16 @@ struct LockBuffers {
   double* ring;     // [RING][n] mining times of the private chain's last RING blocks
   double* spill;    // [n][cap]
   uint8_t* replay;  // [n][REPLAY_BYTES]
+  // exact lanes: a lockstep lane whose episode leaves the closed form
+  // (CPR_ST_LOCKSTEP_INEXACT) is simulated again on the exact event engine in Nakamoto mode
+  // from its first draw and its logged actions, and continues there. alog = null: none.
+  uint8_t* alog;         // [n][alog_cap] the actions taken in the lane's episode so far
+  int64_t alog_cap;
+  uint8_t* emem;         // [n_slots][elane_bytes] event-engine lane regions
+  int64_t elane_bytes;
+  void* eslots;          // eth::EthLane[n_slots]
+  int32_t* efree;        // [n_slots] stack of free slots, its height at efree[n_slots]
+  int32_t n_slots;
 };
 
 // per-lane bytes the fused kernel needs in HBM besides LDS
@@ -83,7 +93,14 @@ hipError_t launch_step(const NakParams& P, uint64_t seed, const LockBuffers& B, 
                        const int32_t* actions, int unit, const double* tab_nn,
                        const double* tab_sg, int32_t tab_n, const StepBuffers& b,
                        hipStream_t st);
-hipError_t launch_observe_fields(const void* lanes, int64_t n, int32_t* f, hipStream_t st);
+// after launch_step: lanes that left the closed form move to (or step on) the exact engine
+// (EP: the batch's Ethereum lane in Nakamoto mode) and their step outputs are rewritten
+hipError_t launch_lock_exact(const eth::EthParams& EP, uint64_t seed, const LockBuffers& B,
+                             int64_t n, const int32_t* actions, int unit, const double* tab_nn,
+                             const double* tab_sg, int32_t tab_n, const StepBuffers& b,
+                             hipStream_t st);
+hipError_t launch_observe_fields(const eth::EthParams& EP, const LockBuffers& B, int64_t n,
+                                 int32_t* f, hipStream_t st);
 hipError_t launch_policy(int32_t policy, int unit, const double* obs, int64_t n,
                          const uint8_t* table, int32_t dim, int32_t* actions, hipStream_t st);
 hipError_t launch_stream_fill(uint64_t seed, uint64_t ep, uint32_t idx0, uint32_t tag, int64_t n,

@@ -167,8 +167,15 @@ struct LockLane {
   int64_t steps;
   double last_ra;
   int32_t live;
-  int32_t _pad;
+  int32_t exact;  // 1 + the exact-engine slot this lane runs on, 0 = the closed form
 };
+
+// nakamoto_ssz action (0 Adopt .. 3 Wait) -> the Nakamoto-mode Ethereum lane's action index
+// (eth::lane_action's mapping)
+__device__ inline int32_t nak_to_eth_action(int32_t a) {
+  constexpr int32_t map[4] = {eth::A_ADOPT_DISCARD, eth::A_OVERRIDE, eth::A_MATCH, eth::A_WAIT};
+  return map[a & 3] * 4;
+}
 
 __device__ inline LaneMem lock_mem(const NakParams& P, const LockBuffers& B, int64_t i, int64_t n) {
   LaneMem M;
@@ -181,10 +188,9 @@ __device__ inline LaneMem lock_mem(const NakParams& P, const LockBuffers& B, int
   return M;
 }
 
-__device__ inline void write_obs(const NakLane& L, int unit, const double* tab_nn,
-                                 const double* tab_sg, int32_t tab_n, double* o) {
-  int32_t h, a, d, ev;
-  L.observe(&h, &a, &d, &ev);
+__device__ inline void write_obs_fields(int32_t h, int32_t a, int32_t d, int32_t ev, int unit,
+                                        const double* tab_nn, const double* tab_sg,
+                                        int32_t tab_n, double* o) {
   if (unit) {
     // ssz_tools.ml:29-40; host-tabulated (libm) for |x| < tab_n
     o[0] = h < tab_n ? tab_nn[h] : 2.0 / 3.141592653589793 * atan((double)h / 1.0);
@@ -200,6 +206,13 @@ __device__ inline void write_obs(const NakLane& L, int unit, const double* tab_n
   }
 }
 
+__device__ inline void write_obs(const NakLane& L, int unit, const double* tab_nn,
+                                 const double* tab_sg, int32_t tab_n, double* o) {
+  int32_t h, a, d, ev;
+  L.observe(&h, &a, &d, &ev);
+  write_obs_fields(h, a, d, ev, unit, tab_nn, tab_sg, tab_n, o);
+}
+
 __global__ __launch_bounds__(kBlock) void k_reset(NakParams P, uint64_t seed, LockBuffers B,
                                                    int64_t n, const uint8_t* mask,
                                                    const uint64_t* eps, int unit,
@@ -209,6 +222,11 @@ __global__ __launch_bounds__(kBlock) void k_reset(NakParams P, uint64_t seed, Lo
   if (i >= n) return;
   LockLane& LL = ((LockLane*)B.lanes)[i];
   if (mask == nullptr || mask[i]) {
+    if (LL.exact > 0) {  // the lane's exact-engine slot goes back to the free stack
+      const int32_t t = atomicAdd(B.efree + B.n_slots, 1);
+      B.efree[t] = LL.exact - 1;
+    }
+    LL.exact = 0;
     const LaneMem M = lock_mem(P, B, i, n);
     NakLane L;
     L.init();
@@ -230,6 +248,8 @@ __global__ __launch_bounds__(kBlock) void k_step(NakParams P, uint64_t seed, Loc
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   LockLane& LL = ((LockLane*)B.lanes)[i];
+  if (B.alog && LL.steps < B.alog_cap) B.alog[i * B.alog_cap + LL.steps] = (uint8_t)actions[i];
+  if (LL.exact) return;  // stepped on the exact engine by k_lock_exact
   NakLane L = LL.L;
   const LaneMem M = lock_mem(P, B, i, n);
   const Stream S = make_stream(seed, LL.ep);
@@ -260,10 +280,93 @@ __global__ __launch_bounds__(kBlock) void k_step(NakParams P, uint64_t seed, Loc
   write_obs(L, unit, tab_nn, tab_sg, tab_n, out.obs + 4 * i);
 }
 
-__global__ void k_observe_fields(const void* lanes, int64_t n, int32_t* f) {
+// lockstep lanes that left the closed form: engine.ml's step is always
+// exact (engine.ml:176-249), so a lane whose step set CPR_ST_LOCKSTEP_INEXACT bits is
+// simulated again on the exact event engine (Ethereum lane, Nakamoto mode) from its first
+// draw with the actions it was given, and stays there until its next reset; this step's
+// outputs are rewritten from that lane (status: the closed form's bits | EXACT_RERUN)
+__device__ inline eth::EthMem lock_exact_mem(const eth::EthParams& EP, const LockBuffers& B,
+                                             int32_t slot) {
+  return eth::eth_mem_at(B.emem + (int64_t)slot * B.elane_bytes, EP.cap_b, EP.cap_e, EP.n);
+}
+
+__global__ __launch_bounds__(kBlock) void k_lock_exact(eth::EthParams EP, uint64_t seed,
+                                                        LockBuffers B, int64_t n,
+                                                        const int32_t* actions, int unit,
+                                                        const double* tab_nn,
+                                                        const double* tab_sg, int32_t tab_n,
+                                                        StepBuffers out) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  ((const LockLane*)lanes)[i].L.observe(f + 4 * i, f + 4 * i + 1, f + 4 * i + 2, f + 4 * i + 3);
+  LockLane& LL = ((LockLane*)B.lanes)[i];
+  eth::EthLane* slots = (eth::EthLane*)B.eslots;
+  const Stream S = make_stream(seed, LL.ep);
+  int32_t hd;
+  bool done = false;
+  int32_t slot;
+  eth::EthLane E;
+  double prev_ra = LL.last_ra;  // attacker reward after the previous step
+  if (LL.exact) {
+    slot = LL.exact - 1;
+    E = slots[slot];
+    hd = E.gym_step(EP, S, lock_exact_mem(EP, B, slot), nak_to_eth_action(actions[i]), &done);
+    LL.steps += 1;
+  } else {
+    if (!(LL.L.status & kInexact) || LL.steps > B.alog_cap) return;
+    const int32_t t = atomicSub(B.efree + B.n_slots, 1) - 1;
+    if (t < 0) {  // every slot taken: the lane keeps its flags (inexact outputs)
+      atomicAdd(B.efree + B.n_slots, 1);
+      return;
+    }
+    slot = B.efree[t];
+    // k_step already advanced last_ra by this step's closed-form reward (whole blocks:
+    // exact in fp64), so the previous step's value is the difference
+    prev_ra = LL.last_ra - out.reward[i];
+    const eth::EthMem M = lock_exact_mem(EP, B, slot);
+    E.gym_reset(EP, S, M);
+    hd = 0;
+    for (int64_t s = 0; s < LL.steps; ++s)
+      hd = E.gym_step(EP, S, M, nak_to_eth_action(B.alog[i * B.alog_cap + s]), &done);
+    LL.exact = slot + 1;
+  }
+  const eth::EthMem M = lock_exact_mem(EP, B, slot);
+  const eth::EBlock h = E.B(EP, M, hd);
+  const double ra = (double)(h.rew_att / 32);  // 1 per block in Nakamoto mode
+  out.reward[i] = ra - prev_ra;  // engine.ml:223
+  out.done[i] = done ? 1 : 0;
+  out.status[i] = LL.L.status | E.status | CPR_ST_EXACT_RERUN;
+  if (out.era) {
+    out.era[i] = ra;
+    out.erd[i] = (double)(h.rew_def / 32);
+    out.eprog[i] = (double)h.height;
+    out.ect[i] = h.time;
+    out.est[i] = E.now;
+    out.esteps[i] = E.steps;
+    out.eacts[i] = E.c_act;
+    out.hh[i] = h.height;
+    out.hm[i] = h.miner;
+  }
+  LL.last_ra = ra;
+  const eth::EthObs o = E.observe(EP, M, false);
+  slots[slot] = E;
+  write_obs_fields(o.public_height, o.private_height, o.diff_height, o.event, unit, tab_nn,
+                   tab_sg, tab_n, out.obs + 4 * i);
+}
+
+__global__ void k_observe_fields(eth::EthParams EP, LockBuffers B, int64_t n, int32_t* f) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const LockLane& LL = ((const LockLane*)B.lanes)[i];
+  if (LL.exact) {
+    eth::EthLane E = ((eth::EthLane*)B.eslots)[LL.exact - 1];
+    const eth::EthObs o = E.observe(EP, lock_exact_mem(EP, B, LL.exact - 1), false);
+    f[4 * i] = o.public_height;
+    f[4 * i + 1] = o.private_height;
+    f[4 * i + 2] = o.diff_height;
+    f[4 * i + 3] = o.event;
+    return;
+  }
+  LL.L.observe(f + 4 * i, f + 4 * i + 1, f + 4 * i + 2, f + 4 * i + 3);
 }
 
 // engine.ml:258-261: decode the observation (ssz_tools.ml:42-59), apply the policy
@@ -373,9 +476,21 @@ hipError_t launch_step(const NakParams& P, uint64_t seed, const LockBuffers& B, 
   return hipGetLastError();
 }
 
-hipError_t launch_observe_fields(const void* lanes, int64_t n, int32_t* f, hipStream_t st) {
+hipError_t launch_lock_exact(const eth::EthParams& EP, uint64_t seed, const LockBuffers& B,
+                             int64_t n, const int32_t* actions, int unit, const double* tab_nn,
+                             const double* tab_sg, int32_t tab_n, const StepBuffers& b,
+                             hipStream_t st) {
+  if (!B.alog) return hipSuccess;
   const unsigned blocks = (unsigned)((n + kBlock - 1) / kBlock);
-  hipLaunchKernelGGL(k_observe_fields, dim3(blocks), dim3(kBlock), 0, st, lanes, n, f);
+  hipLaunchKernelGGL(k_lock_exact, dim3(blocks), dim3(kBlock), 0, st, EP, seed, B, n, actions,
+                     unit, tab_nn, tab_sg, tab_n, b);
+  return hipGetLastError();
+}
+
+hipError_t launch_observe_fields(const eth::EthParams& EP, const LockBuffers& B, int64_t n,
+                                 int32_t* f, hipStream_t st) {
+  const unsigned blocks = (unsigned)((n + kBlock - 1) / kBlock);
+  hipLaunchKernelGGL(k_observe_fields, dim3(blocks), dim3(kBlock), 0, st, EP, B, n, f);
   return hipGetLastError();
 }
 

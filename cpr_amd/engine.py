@@ -223,9 +223,10 @@ def step(ienv, action):
         info["protocol_family"] = "nakamoto"
         info["head_height"] = int(inf["head_height"][0])
         info["head_miner"] = _miner_str(int(inf["head_miner"][0]))
-    if status & L.ST_LOCKSTEP_INEXACT:
-        # Nakamoto lockstep lane outside its closed form (an activation inside a delivery
-        # window, a fork deeper than the lane's slots): outputs not exact; not a reference key
+    if status & L.ST_LOCKSTEP_INEXACT and not status & L.ST_EXACT_RERUN:
+        # Nakamoto lockstep lane outside its closed form that could not move to the exact
+        # engine (no free exact slot, or a configuration that engine cannot hold): outputs
+        # not exact; not a reference key
         info["device_status"] = status
     ienv._last = (ra, rd, prog, ct, st)
     return obs[0].copy(), float(rew[0]), bool(done[0]), info

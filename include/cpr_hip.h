@@ -200,17 +200,22 @@ enum cpr_episode_status {
   CPR_ST_TRACE_MISS = 128u,     /* cpr_replay: the episode needed a draw its trace does not
                                  hold (too few activations, a missing delay key); outputs
                                  not valid */
-  CPR_ST_EXACT_RERUN = 256u     /* Nakamoto fused episodes (cpr_run_episodes, cpr_replay): the
-                                 closed-form lane flagged the episode (OVERLAP, DEEP_FORK,
-                                 TIE_UNRESOLVED, STALE_TIME) and it was simulated again on the
-                                 exact event engine; its outputs are that
-                                 re-run's, and the lane's flags are kept beside this bit */
+  CPR_ST_EXACT_RERUN = 256u     /* Nakamoto fused episodes (cpr_run_episodes, cpr_replay) and
+                                 lockstep lanes (cpr_step): the closed-form lane flagged the
+                                 episode (OVERLAP, DEEP_FORK, TIE_UNRESOLVED, STALE_TIME) and it
+                                 was simulated again on the exact event engine (DESIGN.md
+                                 §4.3); its outputs are that re-run's, and the lane's flags
+                                 are kept beside this bit */
 };
 
 /* status bits that make an episode's outputs invalid; such episodes never enter a
  * summary's sums (cpr_summary.invalid counts them). A Nakamoto lockstep lane (cpr_step)
- * whose status holds OVERLAP, DEEP_FORK, TIE_UNRESOLVED or STALE_TIME has inexact outputs
- * too: live envs cannot be re-run, so the caller sees the bits in cpr_step_info.status. */
+ * whose step sets OVERLAP, DEEP_FORK, TIE_UNRESOLVED or STALE_TIME is simulated again on the
+ * exact event engine from its first draw and the actions it was given, and stays there
+ * until its next reset: its outputs are exact and its status carries CPR_ST_EXACT_RERUN
+ * beside those bits. Only a lane that cannot move (all exact slots of the batch in use, an
+ * episode longer than its action log, a network the exact engine does not hold) reports
+ * the bits without CPR_ST_EXACT_RERUN, and its outputs are then not exact. */
 #define CPR_ST_INVALID (CPR_ST_CAPACITY | CPR_ST_REFERENCE_RAISES | CPR_ST_TRACE_MISS)
 #define CPR_ST_LOCKSTEP_INEXACT \
   (CPR_ST_OVERLAP | CPR_ST_DEEP_FORK | CPR_ST_TIE_UNRESOLVED | CPR_ST_STALE_TIME)
@@ -291,7 +296,8 @@ typedef struct cpr_step_info {
   int32_t* head_miner;
   uint32_t* status;  /* cpr_episode_status bits of the lane's episode (CPR_ST_INVALID: the
                         reference would have raised / the lane's capacity was exceeded;
-                        CPR_ST_LOCKSTEP_INEXACT: Nakamoto outputs not exact) */
+                        CPR_ST_LOCKSTEP_INEXACT without CPR_ST_EXACT_RERUN: Nakamoto
+                        outputs not exact) */
 } cpr_step_info;
 
 /* An exported activation/delay trace: every random draw of n_episodes

@@ -212,6 +212,48 @@ def test_lockstep_matches_oracle_step_by_step(ctx):
     assert done.all()
 
 
+@pytest.mark.parametrize("policy", ["random", "sm1"])
+def test_lockstep_overlaps_exact_on_event_engine(ctx, policy):
+    # propagation delay 0.05: nearly every episode has an activation inside a delivery
+    # window, where the closed form does not hold; such a lane moves to the exact event
+    # engine (replaying its logged actions) and stays there, so every step of every lane
+    # equals the oracle's engine.ml; a second episode per lane reuses the freed slots
+    n, T = 64, 120
+    cfg, keep = device.make_config(alpha=0.42, gamma=0.5, max_steps=T, seed=901,
+                                   propagation_delay=0.05, unit_observation=False, n_lanes=n)
+    b = device.Batch(cfg, ctx=ctx, keep=keep)
+    rng = np.random.default_rng(5)
+    moved = 0
+    for rnd in range(2):
+        ids = np.arange(n, dtype=np.uint64) + rnd * n
+        obs = b.reset(episode_ids=ids)
+        envs = [O.GymEnv(cfg, episode=int(i)) for i in ids]
+        ref_obs = np.array([e.reset() for e in envs])
+        assert np.array_equal(obs, ref_obs)
+        for t in range(T):
+            if policy == "random":
+                acts = rng.integers(0, 4, size=n).astype(np.int32)
+            else:
+                acts = np.array([O.nak_policy(L.POLICY_SAPIRSHTEIN_2016_SM1, e.fields())
+                                 for e in envs], dtype=np.int32)
+            obs, rew, done, info = b.step(acts)
+            st = info["status"]
+            assert not ((st & L.ST_LOCKSTEP_INEXACT != 0) & (st & L.ST_EXACT_RERUN == 0)).any()
+            for i, e in enumerate(envs):
+                o, r, d, inf = e.step(int(acts[i]))
+                assert np.array_equal(obs[i], o), (rnd, t, i, obs[i], o)
+                assert rew[i] == r and done[i] == d, (rnd, t, i)
+                for k in ["episode_reward_attacker", "episode_reward_defender",
+                          "episode_progress", "episode_chain_time", "episode_sim_time",
+                          "episode_n_steps", "episode_n_activations", "head_height",
+                          "head_miner"]:
+                    assert info[k][i] == inf[k], (rnd, t, i, k)
+            assert np.array_equal(b.observe_fields(), np.array([e.fields() for e in envs]))
+        assert done.all()
+        moved += int(((st & L.ST_EXACT_RERUN) != 0).sum())
+    assert moved >= n  # most lanes of both rounds took the exact path
+
+
 def test_policy_actions_decode(ctx):
     cfg, keep = device.make_config(alpha=0.3, gamma=0.5, n_lanes=1)
     b = device.Batch(cfg, ctx=ctx, keep=keep)

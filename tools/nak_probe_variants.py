@@ -6,6 +6,8 @@ the variants' results are meaningless; only their kernel times are read.
   cheap_rng : Philox4x32-10 -> two multiply-xorshift rounds
   cheap_log : fdlibm cpr_log -> (x - 1) (a negative number, so delays stay positive)
   cheap_both: both
+  cheap_link: the link draws (the race at a match: a second Philox per activation in
+              which any lane of the wave races) -> a multiply-xorshift hash
   base      : the tree as it is
   wavesN    : k_run_episodes compiled for N waves per SIMD instead of 4 (VGPR budget 512/N)
 
@@ -33,6 +35,14 @@ PHILOX_NEW = """#if 1  // probe: cheap stand-in
 #endif
 #pragma unroll
   for (int r = 0; r < 10; ++r) {"""
+LINK_OLD = """  __host__ __device__ inline double link_u(uint32_t kw, uint32_t off, uint32_t dest) const {
+"""
+LINK_NEW = LINK_OLD + """    if (1) {  // probe: cheap stand-in for the race's link draw
+      uint32_t h = (kw * 0x9E3779B9u) ^ (off * 0x85EBCA6Bu) ^ (dest * 0xC2B2AE35u) ^ e0 ^ k0;
+      h ^= h >> 15; h *= 0x2C1B3C6Du; h ^= h >> 12;
+      return (double)h * (1.0 / 4294967296.0);
+    }
+"""
 LOG_OLD = "__host__ __device__ inline double cpr_log(double x) {"
 LOG_NEW = LOG_OLD + "\n  return x - 1.0;  // probe: cheap stand-in"
 
@@ -55,6 +65,9 @@ def variant(name, rng, log, rev=None):
     if log:
         assert LOG_OLD in st
         st = st.replace(LOG_OLD, LOG_NEW, 1)
+    if "link" in name:
+        assert LINK_OLD in st
+        st = st.replace(LINK_OLD, LINK_NEW, 1)
     (d / "cpr_stream.h").write_text(st)
     m = re.match(r"waves(\d+)", name)
     if m:

@@ -4,7 +4,7 @@
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-ARGS="--steps 1 --warmup 0 --no-cpu ${BENCH_ARGS:-}"
+ARGS="--steps 1 --warmup 0 --no-cpu --no-configs ${BENCH_ARGS:-}"
 step() { local rc=$1 name=$2; echo "$name rc=$rc" | tee -a gpurun_out/prof_status.log; [[ $rc -eq 0 ]]; }
 timeout -k 10 120 rocprofv3 -L > gpurun_out/prof_counters.txt 2>&1
 step $? list || true

@@ -11,12 +11,13 @@ import sys
 import re
 
 tag = sys.argv[1]
-eps = int(sys.argv[2]) if len(sys.argv) > 2 else 393216
+eps = int(sys.argv[2]) if len(sys.argv) > 2 else 5242880
 K = "k_run_episodes"
 # the headline sweep's launches: the sapirshtein-2016-sm1 specialisation on the keyed
 # stream (bench.py's abstract-gamma column after the timed sweep runs the generic POL = -1
-# instantiation and is left out)
-HEADLINE = re.compile(r"k_run_episodes<0, (cpr::)?SeedSource, 3>")
+# instantiation and is left out); bench.py asks for no records, so the summary-only
+# specialisation (REC = 0) runs
+HEADLINE = re.compile(r"k_run_episodes<0, (cpr::)?SeedSource, 3(, 0)?>")
 
 
 def is_headline(name):
