@@ -443,6 +443,8 @@ def main():
                 # lane-instructions the kernel really issues per activation, beside the
                 # 40-op cost model `achieved` is priced at
                 "measured_valu_lane_ops_per_activation": valu_meas,
+                # SURVEY §8d's unit figure: 48 B of per-episode outputs; the sweep reduces
+                # them on chip to one summary per launch, so `traffic` is below it
                 "algorithmic_bytes_per_launch": ALG_BYTES_PER_EPISODE * E,
                 "hbm_frac_algorithmic": ALG_BYTES_PER_EPISODE * E / (kms.mean() / 1e3)
                 / (HBM_PEAK_GBS * 1e9),

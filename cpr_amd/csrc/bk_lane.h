@@ -84,6 +84,9 @@ struct BkParams {
   // honest clique (net 2, models.ml:3-28): keyed miner thresholds (n - 1), U(lo, hi) links
   double lo, hi;
   uint32_t thr[64];
+  // fused-episode launches: device counter of episodes handed out beyond the first
+  // lanes-many (zeroed before the launch); null = static grid-stride
+  unsigned long long* next = nullptr;
 };
 
 constexpr int32_t NQS = 128;     // quorum candidates per block and list

@@ -73,12 +73,24 @@ struct cpr_ctx {
   // context: launches on the context's stream run in order, so one grow-only pool serves an
   // alpha x gamma sweep of any number of batches
   DevBuf pool;
+  // work-queue counter of the event-engine fused-episode launches (wave_sched.h
+  // ev_next_episode), zeroed on the stream before each launch
+  DevBuf wq;
 };
 
 // the context's scratch pool with at least `bytes`
 static hipError_t ctx_pool(cpr_ctx* c, size_t bytes, void** out) {
   hipError_t e = c->pool.ensure(bytes);
   *out = c->pool.p;
+  return e;
+}
+
+// a zeroed work-queue counter for the next event-engine launch on the context's stream
+// (launches on the stream run in order, so one counter serves them all)
+static hipError_t ctx_next(cpr_ctx* c, unsigned long long** out) {
+  hipError_t e = c->wq.ensure(8);
+  if (e == hipSuccess) e = hipMemsetAsync(c->wq.p, 0, 8, c->stream);
+  *out = (unsigned long long*)c->wq.p;
   return e;
 }
 
@@ -169,6 +181,7 @@ int cpr_ctx_destroy(cpr_ctx* c) {
   c->rq.release();
   c->rtab.release();
   c->rmem.release();
+  c->wq.release();
   delete c;
   return CPR_OK;
 }
@@ -764,7 +777,7 @@ static int64_t batch_resident(cpr_batch* b) {
   if (b->is_ev)
     return cus * (b->cfg.protocol == CPR_PROTO_TAILSTORM ? ts_blocks_per_cu() : bk_blocks_per_cu()) *
            256;
-  return cus * run_episodes_blocks_per_cu(b->cfg.mode) * 256;
+  return cus * run_episodes_blocks_per_cu(b->P, b->cfg.mode, false) * 256;
 }
 
 int cpr_launch_shape(cpr_batch* b, int64_t* lanes, int64_t* resident) {
@@ -826,13 +839,18 @@ int cpr_batch_destroy(cpr_batch* b) {
 // exact Nakamoto re-runs: one-wave workgroups of the re-run kernel
 constexpr int64_t kRerunLanes = 512;
 
-static int64_t episode_lanes(cpr_batch* b, int64_t n_eps) {
-  const int64_t full = (int64_t)b->ctx->cus * run_episodes_blocks_per_cu(b->cfg.mode) * 256;
+static int64_t episode_lanes(cpr_batch* b, int64_t n_eps, bool recs) {
+  const int64_t full =
+      (int64_t)b->ctx->cus * run_episodes_blocks_per_cu(b->P, b->cfg.mode, recs) * 256;
   const int64_t budget = (int64_t)(16ll << 30) / episode_lane_bytes(b->P);
   int64_t lanes = std::min(full, std::max<int64_t>(256, budget));
-  const int64_t need = ((n_eps + 255) / 256) * 256;
-  lanes = std::min(lanes, need);
-  return std::max<int64_t>(256, (lanes / 256) * 256);
+  lanes = std::max<int64_t>(256, (lanes / 256) * 256);
+  // equal rounds: the episodes of a launch spread evenly over the fewest rounds of the
+  // resident grid, so the last round is not a partly empty one (every lane's episode has
+  // the same trip count in the gym)
+  const int64_t rounds = std::max<int64_t>(1, (n_eps + lanes - 1) / lanes);
+  const int64_t even = ((n_eps + rounds - 1) / rounds + 255) / 256 * 256;
+  return std::max<int64_t>(256, std::min(lanes, even));
 }
 
 // Re-run every queued flagged Nakamoto episode of the launches since the last flush, in
@@ -875,12 +893,14 @@ static int run_async_eth(cpr_batch* b, int64_t n, uint64_t first, const TraceSou
     HIP_TRY(hipEventCreate(&b->ev0));
     HIP_TRY(hipEventCreate(&b->ev1));
   }
+  eth::EthParams EP = b->EP;
+  HIP_TRY(ctx_next(b->ctx, &EP.next));
   HIP_TRY(hipEventRecord(b->ev0, b->ctx->stream));
   if (tr)
-    HIP_TRY(launch_eth_replay_episodes(b->EP, *tr, n, (uint8_t*)mem, b->eth_bytes,
+    HIP_TRY(launch_eth_replay_episodes(EP, *tr, n, (uint8_t*)mem, b->eth_bytes,
                                        lanes, rec_dev, sum_dev, b->ctx->stream));
   else
-    HIP_TRY(launch_eth_run_episodes(b->EP, b->cfg.seed, first, n, (uint8_t*)mem,
+    HIP_TRY(launch_eth_run_episodes(EP, b->cfg.seed, first, n, (uint8_t*)mem,
                                     b->eth_bytes, lanes, rec_dev, sum_dev, b->ctx->stream));
   HIP_TRY(hipEventRecord(b->ev1, b->ctx->stream));
   return CPR_OK;
@@ -903,18 +923,21 @@ static int run_async_bk(cpr_batch* b, int64_t n, uint64_t first, const TraceSour
     HIP_TRY(hipEventCreate(&b->ev0));
     HIP_TRY(hipEventCreate(&b->ev1));
   }
+  ts::TsParams TP = b->TP;
+  bk::BkParams BP = b->BP;
+  HIP_TRY(ctx_next(b->ctx, tsp ? &TP.next : &BP.next));
   HIP_TRY(hipEventRecord(b->ev0, b->ctx->stream));
   uint8_t* mem = (uint8_t*)pool;
   hipStream_t st = b->ctx->stream;
   if (tsp && tr)
-    HIP_TRY(launch_ts_replay_episodes(b->TP, *tr, n, mem, b->bk_bytes, lanes, rec_dev, sum_dev, st));
+    HIP_TRY(launch_ts_replay_episodes(TP, *tr, n, mem, b->bk_bytes, lanes, rec_dev, sum_dev, st));
   else if (tsp)
-    HIP_TRY(launch_ts_run_episodes(b->TP, b->cfg.seed, first, n, mem, b->bk_bytes, lanes, rec_dev,
+    HIP_TRY(launch_ts_run_episodes(TP, b->cfg.seed, first, n, mem, b->bk_bytes, lanes, rec_dev,
                                    sum_dev, st));
   else if (tr)
-    HIP_TRY(launch_bk_replay_episodes(b->BP, *tr, n, mem, b->bk_bytes, lanes, rec_dev, sum_dev, st));
+    HIP_TRY(launch_bk_replay_episodes(BP, *tr, n, mem, b->bk_bytes, lanes, rec_dev, sum_dev, st));
   else
-    HIP_TRY(launch_bk_run_episodes(b->BP, b->cfg.seed, first, n, mem, b->bk_bytes, lanes, rec_dev,
+    HIP_TRY(launch_bk_run_episodes(BP, b->cfg.seed, first, n, mem, b->bk_bytes, lanes, rec_dev,
                                    sum_dev, st));
   HIP_TRY(hipEventRecord(b->ev1, b->ctx->stream));
   return CPR_OK;
@@ -944,9 +967,10 @@ static int run_async(cpr_batch* b, int64_t n, uint64_t first, const TraceSource*
   if (b->cfg.protocol == CPR_PROTO_ETHEREUM || b->nak_ev)
     return run_async_eth(b, n, first, tr, sum_dev, rec_dev);
   if (b->is_ev) return run_async_bk(b, n, first, tr, sum_dev, rec_dev);
-  const int64_t lanes = episode_lanes(b, n);
+  const int64_t lanes = episode_lanes(b, n, rec_dev != nullptr);
   b->last_lanes = lanes;
-  b->last_resident = (int64_t)b->ctx->cus * run_episodes_blocks_per_cu(b->cfg.mode) * 256;
+  b->last_resident =
+      (int64_t)b->ctx->cus * run_episodes_blocks_per_cu(b->P, b->cfg.mode, rec_dev != nullptr) * 256;
   // spill [lane][cap] f64 mining times | tie-replay scratch [lane]
   const size_t o_replay = align256((size_t)lanes * b->P.cap * sizeof(double));
   void* pool = nullptr;
@@ -1202,7 +1226,9 @@ int cpr_node_outputs(cpr_batch* b, int64_t n, uint64_t first, const cpr_trace* t
   hipStream_t st = b->ctx->stream;
   const bool eth = b->cfg.protocol == CPR_PROTO_ETHEREUM || b->cfg.protocol == CPR_PROTO_NAKAMOTO;
   const bool tsp = b->cfg.protocol == CPR_PROTO_TAILSTORM;
-  const eth::EthParams& EP = nak_fused ? b->NEP : b->EP;
+  eth::EthParams EP = nak_fused ? b->NEP : b->EP;
+  ts::TsParams TP = b->TP;
+  bk::BkParams BP = b->BP;
   const int64_t lane_bytes = eth ? eth::eth_lane_bytes(EP.cap_b, EP.cap_e, EP.n) : b->bk_bytes;
   const int64_t node_bytes = eth ? eth::eth_node_bytes(EP.cap_b, EP.n)
                              : tsp ? ts::ts_align((int64_t)b->TP.n * 8)
@@ -1232,20 +1258,21 @@ int cpr_node_outputs(cpr_batch* b, int64_t n, uint64_t first, const cpr_trace* t
   cpr_episode_record* rec = (cpr_episode_record*)((char*)out.p + o_rec);
   cpr_summary* sd = (cpr_summary*)sum.p;
   uint8_t* mem = (uint8_t*)pool;
+  HIP_TRY(ctx_next(b->ctx, eth ? &EP.next : tsp ? &TP.next : &BP.next));
   if (eth && trace)
     HIP_TRY(launch_eth_replay_episodes(EP, src, n, mem, lane_bytes, lanes, rec, sd, st, no));
   else if (eth)
     HIP_TRY(launch_eth_run_episodes(EP, b->cfg.seed, first, n, mem, lane_bytes, lanes, rec, sd,
                                     st, no));
   else if (tsp && trace)
-    HIP_TRY(launch_ts_replay_episodes(b->TP, src, n, mem, lane_bytes, lanes, rec, sd, st, no));
+    HIP_TRY(launch_ts_replay_episodes(TP, src, n, mem, lane_bytes, lanes, rec, sd, st, no));
   else if (tsp)
-    HIP_TRY(launch_ts_run_episodes(b->TP, b->cfg.seed, first, n, mem, lane_bytes, lanes, rec, sd,
+    HIP_TRY(launch_ts_run_episodes(TP, b->cfg.seed, first, n, mem, lane_bytes, lanes, rec, sd,
                                    st, no));
   else if (trace)
-    HIP_TRY(launch_bk_replay_episodes(b->BP, src, n, mem, lane_bytes, lanes, rec, sd, st, no));
+    HIP_TRY(launch_bk_replay_episodes(BP, src, n, mem, lane_bytes, lanes, rec, sd, st, no));
   else
-    HIP_TRY(launch_bk_run_episodes(b->BP, b->cfg.seed, first, n, mem, lane_bytes, lanes, rec, sd,
+    HIP_TRY(launch_bk_run_episodes(BP, b->cfg.seed, first, n, mem, lane_bytes, lanes, rec, sd,
                                    st, no));
   std::vector<int32_t> hm((size_t)n);
   HIP_TRY(hipMemcpyAsync(node_activations, no.acts, rows * 8, hipMemcpyDeviceToHost, st));

@@ -89,6 +89,9 @@ struct EthParams {
   // honest clique (net 2): keyed miner thresholds (n - 1) and uniform link delays
   double lo, hi;
   uint32_t thr[64];
+  // fused-episode launches: device counter of episodes handed out beyond the first
+  // lanes-many (zeroed before the launch); null = static grid-stride
+  unsigned long long* next = nullptr;
 };
 
 constexpr int32_t NCAND = 32, NQ = 32, NSTACK = 64;

@@ -15,7 +15,9 @@
 // occupancy of the per-lane event-engine kernels (B_k, Ethereum, Tailstorm fused episodes
 // and rollouts): they are bound by dependent memory latency, so waves per SIMD matter more
 // than the few VGPRs a tighter budget spills. CPR_EV_WAVES = minimum waves per SIMD the
-// compiler must allow (0: unconstrained). tools/occupancy_ab.sh builds variants.
+// compiler must allow (0: unconstrained; a translation unit may set its own before including
+// this header: kernels_eth.hip 4, kernels_ts.hip 2, B_k unconstrained, as measured in
+// profiles/r03f_event_occupancy_ab.log). tools/occupancy_ab.sh builds variants.
 #ifndef CPR_EV_WAVES
 #define CPR_EV_WAVES 0
 #endif
@@ -225,7 +227,9 @@ hipError_t launch_ts_policy(int32_t policy, int32_t k, int unit, const double* o
                             hipStream_t st);
 size_t ts_slot_bytes();
 int ts_blocks_per_cu();
-int run_episodes_blocks_per_cu(int32_t mode);  // resident 256-lane workgroups per CU
+// resident 256-lane workgroups per CU of the k_run_episodes instantiation a launch of this
+// configuration runs (recs: per-episode records asked for)
+int run_episodes_blocks_per_cu(const NakParams& P, int32_t mode, bool recs);
 
 // FC'16 abstract-model episodes (fc16_lane.h), lanes = multiple of kBlock
 hipError_t launch_fc16_episodes(const fc16::Fc16Params& P, uint64_t seed, uint64_t first,

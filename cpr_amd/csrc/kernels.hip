@@ -45,6 +45,7 @@ __device__ inline CPR_AI BRef run_gym(NakLane& L, const NakParams& P, const St& 
   if (!check_prog && !(P.max_time < __builtin_inf())) {
     // only max_steps ends the episode: the trip count is the same in every lane of the
     // wave, so the loop exit is uniform and no lane state is merged at a divergent exit
+#ifndef CPR_NAK_UNROLL2
     do {
       const NakLane::Draw dr = L.draw(P, S);
       L.apply(L.policy_action<POL>(P));
@@ -52,6 +53,27 @@ __device__ inline CPR_AI BRef run_gym(NakLane& L, const NakParams& P, const St& 
       L.activate(P, S, M, dr);
       ++steps;
     } while (steps < P.max_steps);
+#else
+    // two steps per trip: both activations' draws (two independent Philox / log chains,
+    // which depend on the activation count only) are issued together
+    for (; steps + 2 <= P.max_steps; steps += 2) {
+      const NakLane::Draw d0 = L.draw_at(P, S, L.k);
+      const NakLane::Draw d1 = L.draw_at(P, S, L.k + 1);
+      L.apply(L.policy_action<POL>(P));
+      L.resolve<St, POL >= 0 ? 0 : -1>(P, S, M);
+      L.activate(P, S, M, d0);
+      L.apply(L.policy_action<POL>(P));
+      L.resolve<St, POL >= 0 ? 0 : -1>(P, S, M);
+      L.activate(P, S, M, d1);
+    }
+    if (steps < P.max_steps) {
+      const NakLane::Draw dr = L.draw(P, S);
+      L.apply(L.policy_action<POL>(P));
+      L.resolve<St, POL >= 0 ? 0 : -1>(P, S, M);
+      L.activate(P, S, M, dr);
+      ++steps;
+    }
+#endif
     *steps_out = steps;
     return L.head(P, M);
   }
@@ -90,11 +112,15 @@ constexpr uint32_t kInexact = ST_OVERLAP | ST_DEEP_FORK | ST_TIE_UNRESOLVED | ST
 // run the abstract-gamma mode), or -1 for P.policy (and P.abstract_g)
 // REC: 1 = per-episode records may be written (block mining times tracked for chain_time);
 // 0 = summary only (recs is null): the lane's time bookkeeping compiles out (LaneMem.times)
-template <int MODE, class Src, int POL, int REC = 1>
+// ARR: P.arrive fixed at compile time (0: attacker messages never reach the defenders, the
+// gym's gamma = 0 network, so the second defender tip, the races and the tie replay drop
+// out; 1: they do), or -1 to read it from P
+template <int MODE, class Src, int POL, int REC = 1, int ARR = -1>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) void k_run_episodes(
     NakParams P, Src src, int64_t n_eps, int64_t activations,
     double* spill, uint8_t* replay, cpr_episode_record* recs, cpr_summary* sum,
     int64_t* redo, uint32_t* redo_n, uint32_t launch_id, int64_t redo_cap) {
+  if (ARR >= 0) P.arrive = ARR;
   __shared__ int32_t hist[CPR_HIST_BINS];
   __shared__ double ring[RING * kBlock];
   __shared__ unsigned long long acc_w[13];
@@ -403,6 +429,30 @@ __global__ void k_stream_fill(uint64_t seed, uint64_t ep, uint32_t idx0, uint32_
 
 // ---------------------------------------------------------------- launchers
 
+// the k_run_episodes instantiation a launch runs (keyed stream): the built-in policies get
+// their own specialisation, and summary-only ones (no records asked for: no block-time
+// bookkeeping) for either kind of network; the flagged abstract-gamma mode, tables and loop
+// tasks run the generic kernel. Template arguments do not change the signature.
+using RunFn = void (*)(NakParams, SeedSource, int64_t, int64_t, double*, uint8_t*,
+                       cpr_episode_record*, cpr_summary*, int64_t*, uint32_t*, uint32_t, int64_t);
+template <int POL>
+static RunFn gym_run_fn(const NakParams& P, bool recs) {
+  if (recs) return k_run_episodes<CPR_MODE_GYM, SeedSource, POL, 1, -1>;
+  return P.arrive ? k_run_episodes<CPR_MODE_GYM, SeedSource, POL, 0, 1>
+                  : k_run_episodes<CPR_MODE_GYM, SeedSource, POL, 0, 0>;
+}
+static RunFn run_fn(const NakParams& P, int32_t mode, bool recs) {
+  if (mode != CPR_MODE_GYM) return k_run_episodes<CPR_MODE_LOOP, SeedSource, -1>;
+  if (P.abstract_g) return k_run_episodes<CPR_MODE_GYM, SeedSource, -1>;
+  switch (P.policy) {
+    case P_HONEST: return gym_run_fn<P_HONEST>(P, recs);
+    case P_SIMPLE: return gym_run_fn<P_SIMPLE>(P, recs);
+    case P_ES2014: return gym_run_fn<P_ES2014>(P, recs);
+    case P_SM1: return gym_run_fn<P_SM1>(P, recs);
+    default: return k_run_episodes<CPR_MODE_GYM, SeedSource, -1>;
+  }
+}
+
 hipError_t launch_run_episodes(const NakParams& P, uint64_t seed, uint64_t first, int64_t n_eps,
                                int32_t mode, int64_t activations, double* spill,
                                uint8_t* replay, int64_t lanes, cpr_episode_record* recs,
@@ -410,34 +460,9 @@ hipError_t launch_run_episodes(const NakParams& P, uint64_t seed, uint64_t first
                                uint32_t launch_id, int64_t redo_cap, hipStream_t st) {
   const unsigned blocks = (unsigned)(lanes / kBlock);
   const SeedSource src{seed, first};
-#define CPR_LAUNCH_R(MODE, POL, REC)                                                            \
-  hipLaunchKernelGGL((k_run_episodes<MODE, SeedSource, POL, REC>), dim3(blocks), dim3(kBlock), 0, \
-                     st, P, src, n_eps, activations, spill, replay, recs, sum, redo, redo_n,     \
-                     launch_id, redo_cap)
-#define CPR_LAUNCH(MODE, POL) CPR_LAUNCH_R(MODE, POL, 1)
-  // the built-in policies get their own specialisation, and a summary-only one (no records
-  // asked for: no block-time bookkeeping)
-#define CPR_LAUNCH_POL(POL)                                  \
-  do {                                                       \
-    if (recs) CPR_LAUNCH_R(CPR_MODE_GYM, POL, 1);            \
-    else CPR_LAUNCH_R(CPR_MODE_GYM, POL, 0);                 \
-  } while (0)
-  if (mode == CPR_MODE_GYM && P.abstract_g) {
-    CPR_LAUNCH(CPR_MODE_GYM, -1);  // flagged abstract-gamma mode: the generic kernel
-  } else if (mode == CPR_MODE_GYM) {
-    switch (P.policy) {
-      case P_HONEST: CPR_LAUNCH_POL(P_HONEST); break;
-      case P_SIMPLE: CPR_LAUNCH_POL(P_SIMPLE); break;
-      case P_ES2014: CPR_LAUNCH_POL(P_ES2014); break;
-      case P_SM1: CPR_LAUNCH_POL(P_SM1); break;
-      default: CPR_LAUNCH(CPR_MODE_GYM, -1);
-    }
-  } else {
-    CPR_LAUNCH(CPR_MODE_LOOP, -1);
-  }
-#undef CPR_LAUNCH_POL
-#undef CPR_LAUNCH
-#undef CPR_LAUNCH_R
+  hipLaunchKernelGGL(run_fn(P, mode, recs != nullptr), dim3(blocks), dim3(kBlock), 0, st, P, src,
+                     n_eps, activations, spill, replay, recs, sum, redo, redo_n, launch_id,
+                     redo_cap);
   return hipGetLastError();
 }
 
@@ -512,13 +537,10 @@ hipError_t launch_stream_fill(uint64_t seed, uint64_t ep, uint32_t idx0, uint32_
 
 size_t lock_lane_bytes() { return sizeof(LockLane); }
 
-int run_episodes_blocks_per_cu(int32_t mode) {
+int run_episodes_blocks_per_cu(const NakParams& P, int32_t mode, bool recs) {
   int blocks = 0;
-  hipError_t e = mode == CPR_MODE_GYM
-                     ? hipOccupancyMaxActiveBlocksPerMultiprocessor(
-                           &blocks, k_run_episodes<CPR_MODE_GYM, SeedSource, -1>, kBlock, 0)
-                     : hipOccupancyMaxActiveBlocksPerMultiprocessor(
-                           &blocks, k_run_episodes<CPR_MODE_LOOP, SeedSource, -1>, kBlock, 0);
+  hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
+      &blocks, (const void*)run_fn(P, mode, recs), kBlock, 0);
   if (e != hipSuccess || blocks <= 0) blocks = 2;
   return blocks;
 }

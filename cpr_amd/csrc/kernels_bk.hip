@@ -121,7 +121,7 @@ __global__ __launch_bounds__(kBlock) CPR_EV_OCC void k_bk_run_episodes(
   Acc acc = {};
   bk::BkLane L;
 #if CPR_EV_SCHED
-  int64_t e = tid;  // wave-coherent dispatch (wave_sched.h), grid-stride over episodes
+  int64_t e = tid;  // wave-coherent dispatch (wave_sched.h), episodes from a work queue
   auto S = src.at(e < n_eps ? e : 0);
   EvCursor c;
   c.cls = -1;
@@ -132,7 +132,7 @@ __global__ __launch_bounds__(kBlock) CPR_EV_OCC void k_bk_run_episodes(
       if (c.phase != PH_OVER) ev_fetch<BkAdapter>(L, P, S, M, c);
       if (c.phase == PH_OVER) {
         bk_finish<Src>(P, L, M, S, e, c.hd, acc, hist, recs, no);
-        e += nthreads;
+        e = ev_next_episode(P.next, e, nthreads);
         if (e < n_eps) {
           S = src.at(e);
           ev_begin<BkAdapter>(L, P, S, M, c);

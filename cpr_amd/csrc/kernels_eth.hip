@@ -5,6 +5,13 @@
 // visibility, event heap, scratch) reused for every episode it runs.
 #include <hip/hip_runtime.h>
 
+// occupancy of this TU's event-engine kernels (kernels.h CPR_EV_OCC): 4 waves/SIMD measured
+// +18 % over the unconstrained build on the fn19 probe under wave-coherent dispatch
+// (profiles/r03f_event_occupancy_ab.log); build_variants.py overrides it with -D
+#ifndef CPR_EV_WAVES
+#define CPR_EV_WAVES 4
+#endif
+
 #include <atomic>
 
 #include <algorithm>
@@ -107,7 +114,7 @@ __global__ __launch_bounds__(kBlock) CPR_EV_OCC void k_eth_run_episodes(
   Acc acc = {};
   eth::EthLane L;
 #if CPR_EV_SCHED
-  int64_t e = tid;  // wave-coherent dispatch (wave_sched.h), grid-stride over episodes
+  int64_t e = tid;  // wave-coherent dispatch (wave_sched.h), episodes from a work queue
   auto S = src.at(e < n_eps ? e : 0);
   EvCursor c;
   c.cls = -1;
@@ -118,7 +125,7 @@ __global__ __launch_bounds__(kBlock) CPR_EV_OCC void k_eth_run_episodes(
       if (c.phase != PH_OVER) ev_fetch<EthAdapter>(L, P, S, M, c);
       if (c.phase == PH_OVER) {
         eth_finish<Src>(P, L, M, S, e, c.hd, acc, hist, recs, no);
-        e += nthreads;
+        e = ev_next_episode(P.next, e, nthreads);
         if (e < n_eps) {
           S = src.at(e);
           ev_begin<EthAdapter>(L, P, S, M, c);

@@ -3,6 +3,13 @@
 // structure as kernels_bk.hip: fused episodes, lockstep reset/step, device rollout).
 #include <hip/hip_runtime.h>
 
+// occupancy of this TU's event-engine kernels (kernels.h CPR_EV_OCC): 2 waves/SIMD measured
+// +35 % over the unconstrained build on the configs[3] exp-clique probe under wave-coherent
+// dispatch (profiles/r03f_event_occupancy_ab.log); build_variants.py overrides it with -D
+#ifndef CPR_EV_WAVES
+#define CPR_EV_WAVES 2
+#endif
+
 #include "../../include/cpr_hip.h"
 #include "kernels.h"
 #include "summary.h"
@@ -140,7 +147,7 @@ __global__ __launch_bounds__(kBlock) CPR_EV_OCC void k_ts_run_episodes(
       if (c.phase != PH_OVER) ev_fetch<TsAdapter>(L, P, S, M, c);
       if (c.phase == PH_OVER) {
         ts_finish<Src>(P, L, M, S, e, c.hd, acc, hist, recs, no);
-        e += nthreads;
+        e = ev_next_episode(P.next, e, nthreads);
         if (e < n_eps) {
           S = src.at(e);
           ev_begin<TsAdapter>(L, P, S, M, c);

@@ -441,8 +441,14 @@ struct NakLane {
   // apply selects of the same iteration
   template <class St>
   __host__ __device__ inline CPR_AI Draw draw(const NakParams& P, const St& S) const {
+    return draw_at(P, S, k);
+  }
+  // the draws of activation kk (kk = k: the next one)
+  template <class St>
+  __host__ __device__ inline CPR_AI Draw draw_at(const NakParams& P, const St& S,
+                                                 int32_t kk) const {
     Draw d;
-    d.dt = S.act((uint32_t)k, P.t_att, P.d, P.ev, &d.miner);
+    d.dt = S.act((uint32_t)kk, P.t_att, P.d, P.ev, &d.miner);
     return d;
   }
 

@@ -95,6 +95,9 @@ struct TsParams {
   // table-driven policy (policy == TS_POLICY_TABLE): device table, dimension D
   const uint8_t* table;
   int32_t table_dim;
+  // fused-episode launches: device counter of episodes handed out beyond the first
+  // lanes-many (zeroed before the launch); null = static grid-stride
+  unsigned long long* next = nullptr;
 };
 
 constexpr int32_t NFR = 64;      // common-ancestor frontier (reference walk, tests only)

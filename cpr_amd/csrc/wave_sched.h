@@ -34,6 +34,15 @@ enum : int32_t {
   WK_CLOCK = 0, WK_DAG = 1, WK_TX = 2, WK_RX = 3, WK_ON = 4, WK_MV = 5, WK_MDV = 6,
   WK_ATTACK = 7, WK_POW0 = 8, WK_N = 9
 };
+// the next episode of a lane that finished one: a work queue when the launch has a counter
+// (lanes that drew short episodes take more of them, so a launch of several episodes per lane
+// lasts about its mean work, not its slowest lane's), else the static grid stride. Totals do
+// not depend on which lane ran an episode (integer summaries, records by episode id).
+__device__ inline int64_t ev_next_episode(unsigned long long* next, int64_t e, int64_t nthreads) {
+  if (next == nullptr) return e + nthreads;
+  return nthreads + (int64_t)atomicAdd(next, 1ull);
+}
+
 // cursor phases
 enum : int32_t { PH_FRESH = 0, PH_RUN = 1, PH_OVER = 2, PH_IDLE = 3 };
 

@@ -201,7 +201,7 @@ def test_device_rows_reproduce_reference_text(ctx, line):
 def test_csv_runner_end_to_end(ctx, tmp_path):
     from cpr_amd import csv_runner as C
 
-    tasks = C.honest_net_tasks(2000)[::7] + C.withholding_tasks(2000)[::37]
+    tasks = C.honest_net_tasks(2000)[::13] + C.withholding_tasks(2000)[::61]
     rows = C.run(tasks, ctx=ctx, seed=3)
     out = tmp_path / "rows.tsv"
     C.save_rows_as_tsv(out, rows)

@@ -5,6 +5,8 @@ kernel time (HIP events) and activations/s.
   python tools/event_probe.py eth          k_eth_run_episodes: Ethereum fn19, whitepaper
                                            (constant) uncle rewards, alpha .35, gamma .5,
                                            2016-step gym episodes (BASELINE configs[2])
+  python tools/event_probe.py eth45        k_eth_run_episodes: a bench configs[2] point (fn19,
+                                           alpha .45, gamma .5)
   python tools/event_probe.py eth_honest   k_eth_run_episodes: honest, gamma 0, discount
   python tools/event_probe.py bk           k_bk_run_episodes: B_k k=8 minor-delay, 2048 steps
   python tools/event_probe.py ts           k_ts_run_episodes: Tailstorm k=8 discount heuristic
@@ -37,8 +39,8 @@ def fused(cfg, keep, n):
     b = device.Batch(cfg, keep=keep)
     b.run(256, first_episode=1 << 40)
     _, resident = b.launch_shape()
-    if n == 0:
-        n = resident
+    if n <= 0:  # 0: resident lanes; -k: k episodes per resident lane (work-queue refills)
+        n = resident * max(1, -n)
     t = time.perf_counter()
     s = b.run(n)
     wall = time.perf_counter() - t
@@ -54,6 +56,13 @@ def main():
     N = int(sys.argv[2]) if len(sys.argv) > 2 else None  # episodes; 0 = resident lanes
     if which == "eth":
         cfg, keep = device.make_config(protocol=L.PROTO_ETHEREUM, alpha=0.35, gamma=0.5,
+                                       policy=L.ETH_POLICY_FN19, reward_scheme=L.REWARD_CONSTANT,
+                                       max_steps=2016, seed=1)
+        out = fused(cfg, keep, 131072 if N is None else N)
+        out["kernel"] = "k_eth_run_episodes"
+    elif which == "eth45":
+        # a configs[2] point (bench.py other_configs): fn19, alpha .45, gamma .5
+        cfg, keep = device.make_config(protocol=L.PROTO_ETHEREUM, alpha=0.45, gamma=0.5,
                                        policy=L.ETH_POLICY_FN19, reward_scheme=L.REWARD_CONSTANT,
                                        max_steps=2016, seed=1)
         out = fused(cfg, keep, 131072 if N is None else N)

@@ -9,6 +9,7 @@ the variants' results are meaningless; only their kernel times are read.
   cheap_link: the link draws (the race at a match: a second Philox per activation in
               which any lane of the wave races) -> a multiply-xorshift hash
   base      : the tree as it is
+  unroll2   : the gym loop two activations per trip (CPR_NAK_UNROLL2)
   wavesN    : k_run_episodes compiled for N waves per SIMD instead of 4 (VGPR budget 512/N)
 
 usage: python tools/nak_probe_variants.py [name | name@gitrev ...]  (build/var/<name>.so;
@@ -69,6 +70,9 @@ def variant(name, rng, log, rev=None):
         assert LINK_OLD in st
         st = st.replace(LINK_OLD, LINK_NEW, 1)
     (d / "cpr_stream.h").write_text(st)
+    if "unroll2" in name:  # two activations per trip of the gym loop (kernels.hip)
+        k = (d / "kernels.hip").read_text()
+        (d / "kernels.hip").write_text("#define CPR_NAK_UNROLL2 1\n" + k)
     m = re.match(r"waves(\d+)", name)
     if m:
         k = (d / "kernels.hip").read_text()
