@@ -16,7 +16,7 @@
 // and rollouts): they are bound by dependent memory latency, so waves per SIMD matter more
 // than the few VGPRs a tighter budget spills. CPR_EV_WAVES = minimum waves per SIMD the
 // compiler must allow (0: unconstrained; a translation unit may set its own before including
-// this header: kernels_eth.hip 4, kernels_ts.hip 2, B_k unconstrained, as measured in
+// this header: kernels_ts.hip 2; Ethereum and B_k unconstrained, as measured in
 // profiles/r03f_event_occupancy_ab.log). tools/occupancy_ab.sh builds variants.
 #ifndef CPR_EV_WAVES
 #define CPR_EV_WAVES 0

@@ -5,13 +5,6 @@
 // visibility, event heap, scratch) reused for every episode it runs.
 #include <hip/hip_runtime.h>
 
-// occupancy of this TU's event-engine kernels (kernels.h CPR_EV_OCC): 4 waves/SIMD measured
-// +18 % over the unconstrained build on the fn19 probe under wave-coherent dispatch
-// (profiles/r03f_event_occupancy_ab.log); build_variants.py overrides it with -D
-#ifndef CPR_EV_WAVES
-#define CPR_EV_WAVES 4
-#endif
-
 #include <atomic>
 
 #include <algorithm>
