@@ -35,7 +35,7 @@ __device__ inline void acc_add(LdsAcc& a, const BRef& hd, int64_t steps, int64_t
 
 // One gym episode (engine.ml:164-249): reset = first activation up to the attacker's
 // interaction; step = apply, deliveries, next activation, observe; head at the end.
-template <int POL, class St>
+template <int POL, int TT, class St>
 __device__ inline CPR_AI BRef run_gym(NakLane& L, const NakParams& P, const St& S, const LaneMem& M,
                                int64_t* steps_out) {
   L.init();
@@ -49,7 +49,7 @@ __device__ inline CPR_AI BRef run_gym(NakLane& L, const NakParams& P, const St& 
     do {
       const NakLane::Draw dr = L.draw(P, S);
       L.apply(L.policy_action<POL>(P));
-      L.resolve<St, POL >= 0 ? 0 : -1>(P, S, M);
+      L.resolve<St, POL >= 0 ? 0 : -1, TT>(P, S, M);
       L.activate(P, S, M, dr);
       ++steps;
     } while (steps < P.max_steps);
@@ -80,7 +80,7 @@ __device__ inline CPR_AI BRef run_gym(NakLane& L, const NakParams& P, const St& 
   for (;;) {
     const int32_t a = L.policy_action<POL>(P);
     L.apply(a);
-    L.resolve<St, POL >= 0 ? 0 : -1>(P, S, M);
+    L.resolve<St, POL >= 0 ? 0 : -1, TT>(P, S, M);
     L.activate(P, S, M);
     ++steps;
     bool go = steps < P.max_steps && L.t < P.max_time;
@@ -115,8 +115,10 @@ constexpr uint32_t kInexact = ST_OVERLAP | ST_DEEP_FORK | ST_TIE_UNRESOLVED | ST
 // ARR: P.arrive fixed at compile time (0: attacker messages never reach the defenders, the
 // gym's gamma = 0 network, so the second defender tip, the races and the tie replay drop
 // out; 1: they do), or -1 to read it from P
-template <int MODE, class Src, int POL, int REC = 1, int ARR = -1>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) void k_run_episodes(
+// TT: 1 = launched for d = 2 only: ties take the closed-form rule (tie_table_d2) instead
+// of the inlined heap replay, whose registers otherwise stay live across the whole loop
+template <int MODE, class Src, int POL, int REC = 1, int ARR = -1, int TT = 0>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(TT ? 5 : 4))) void k_run_episodes(
     NakParams P, Src src, int64_t n_eps, int64_t activations,
     double* spill, uint8_t* replay, cpr_episode_record* recs, cpr_summary* sum,
     int64_t* redo, uint32_t* redo_n, uint32_t launch_id, int64_t redo_cap) {
@@ -147,7 +149,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
   for (int64_t e = tid; e < n_eps; e += nthreads) {
     const auto S = src.at(e);
     int64_t steps = 0;
-    const BRef hd = MODE == CPR_MODE_GYM ? run_gym<POL>(L, P, S, M, &steps)
+    const BRef hd = MODE == CPR_MODE_GYM ? run_gym<POL, TT>(L, P, S, M, &steps)
                                          : run_loop<POL>(L, P, S, M, activations);
     const double tm = L.time_of(M, hd);
     const uint32_t status = L.status | Src::missed(S);
@@ -438,8 +440,9 @@ using RunFn = void (*)(NakParams, SeedSource, int64_t, int64_t, double*, uint8_t
 template <int POL>
 static RunFn gym_run_fn(const NakParams& P, bool recs) {
   if (recs) return k_run_episodes<CPR_MODE_GYM, SeedSource, POL, 1, -1>;
-  return P.arrive ? k_run_episodes<CPR_MODE_GYM, SeedSource, POL, 0, 1>
-                  : k_run_episodes<CPR_MODE_GYM, SeedSource, POL, 0, 0>;
+  if (!P.arrive) return k_run_episodes<CPR_MODE_GYM, SeedSource, POL, 0, 0>;
+  return P.d == 2 ? k_run_episodes<CPR_MODE_GYM, SeedSource, POL, 0, 1, 1>
+                  : k_run_episodes<CPR_MODE_GYM, SeedSource, POL, 0, 1>;
 }
 static RunFn run_fn(const NakParams& P, int32_t mode, bool recs) {
   if (mode != CPR_MODE_GYM) return k_run_episodes<CPR_MODE_LOOP, SeedSource, -1>;

@@ -359,6 +359,26 @@ __host__ __device__ inline CPR_AI uint64_t tie_replay(const NakParams& P, const 
   return 0ull;
 }
 
+// tie_replay's outcome in closed form for two defenders and one released block (the
+// attacker matching with one block, the only tie SM1 and ES'14 make at d = 2): the window's
+// events are then fixed, so the heap's order of the two equal-time deliveries at the
+// non-miner defender j = 3 - miner depends only on the miner and on where the miner's own
+// copy of the release lands relative to that instant: j ends on the released block iff
+//   miner 1: that copy arrives at the tie instant too;
+//   miner 2: it arrives no later than the tie instant.
+// Tabulated by running tie_replay over both miners and the four orderings (arrival at t,
+// inside (t, t + delta), at t + delta, after), for several t and delta
+// (tests/native/tie_table.cpp, asserted in the CPU suite); the host fuzzer compares lanes
+// that use it with the oracle (tests/native/lane_vs_oracle.cpp).
+template <class St>
+__host__ __device__ inline CPR_AI uint64_t tie_table_d2(const NakParams& P, const St& S,
+                                                        int32_t miner, double t, int32_t kw) {
+  const double tb = t + P.delta;
+  const double vm = t + S.link((uint32_t)kw, 0u, (uint32_t)miner, P.dmax);
+  const bool on = miner == 1 ? vm == tb : !(vm > tb);
+  return on ? (1ull << (2 - miner)) : 0ull;  // bit j - 1, j = 3 - miner
+}
+
 struct NakLane {
   double t;          // time of the latest activation (clock.now at the interaction)
   int32_t k;         // activations so far (clock.c_activations); the same in every lane of
@@ -543,7 +563,10 @@ struct NakLane {
   // deliveries of the window: the fresh defender block and the attacker's release reach
   // the defenders (simulator.ml:481-508 with update_head, nakamoto.ml:85-89)
   // AG: the abstract-gamma rule fixed at compile time (0 off, 1 on) or read from P (-1)
-  template <class St, int AG = -1>
+  // TT: 1 = ties resolved without the heap replay (tie_table_d2), for kernels that run only
+  // d = 2 configurations; a tie that rule does not cover flags TIE_UNRESOLVED (the fused
+  // kernel hands such an episode to the exact re-run). 0 = tie_replay.
+  template <class St, int AG = -1, int TT = 0>
   __host__ __device__ inline CPR_AI void resolve(const NakParams& P, const St& S, const LaneMem& M) {
     const bool released = rhi >= rlo && P.arrive;
     const uint64_t all = all_mask(P.d);
@@ -579,12 +602,19 @@ struct NakLane {
       if (tie) {
         // same instant at some defender: the queue order decides
         status |= ST_TIE;
-        bool ok = false;
-        const uint64_t exact = tie_replay(P, S, M.replay, wminer, t, rlo, rhi, k, &ok);
-        if (ok)
-          mask = exact;
-        else
-          status |= ST_TIE_UNRESOLVED;
+        if (TT) {
+          if (P.d == 2 && rlo == rhi)
+            mask = tie_table_d2(P, S, wminer, t, k);
+          else
+            status |= ST_TIE_UNRESOLVED;
+        } else {
+          bool ok = false;
+          const uint64_t exact = tie_replay(P, S, M.replay, wminer, t, rlo, rhi, k, &ok);
+          if (ok)
+            mask = exact;
+          else
+            status |= ST_TIE_UNRESOLVED;
+        }
       }
     }
     sel(A, newA, chain_ref(M, rhi));

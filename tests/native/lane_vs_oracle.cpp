@@ -54,6 +54,11 @@ extern "C" int oracle_two_agents_task(int, void*, uint64_t, uint64_t, double, in
 struct Counters {
   long episodes = 0, mismatches = 0, tie_eps = 0, tie_mismatch = 0, overlap_eps = 0,
        lane_tie = 0, unresolved = 0;
+  // odd episodes of the two-defender gym configurations run resolve<..., TT = 1> (the
+  // closed-form tie rule of the d = 2 summary-only kernels) instead of the heap replay; a
+  // tie that rule does not cover (several released blocks) ends the comparison, as the
+  // kernel hands such an episode to the exact re-run
+  long tt_episodes = 0, tt_ties = 0, tt_unresolved = 0;
 };
 
 static bool run_gym(const Cfg& cf, uint64_t seed, uint64_t ep, Counters& C, std::string& why) {
@@ -96,6 +101,8 @@ static bool run_gym(const Cfg& cf, uint64_t seed, uint64_t ep, Counters& C, std:
   L.activate(P, S, M);
   bool ok = true;
   char buf[512];
+  const bool tt = cf.two_agents == 0 && cf.defenders == 2 && (ep & 1);
+  bool tt_stopped = false;
   for (int s = 0;; s++) {
     oracle::NakObs o = g.observe_int();
     int32_t h, a, d, e;
@@ -119,7 +126,15 @@ static bool run_gym(const Cfg& cf, uint64_t seed, uint64_t ep, Counters& C, std:
     oracle::StepInfo info{};
     g.step(act, obs, &done, &info);
     L.apply(act);
-    L.resolve(P, S, M);
+    if (tt) {
+      L.resolve<Stream, -1, 1>(P, S, M);
+      if (L.status & ST_TIE_UNRESOLVED) {
+        tt_stopped = true;
+        break;
+      }
+    } else {
+      L.resolve(P, S, M);
+    }
     L.activate(P, S, M);
     BRef hd = L.head(P, M);
     const double hd_tm = L.time_of(M, hd);
@@ -140,6 +155,14 @@ static bool run_gym(const Cfg& cf, uint64_t seed, uint64_t ep, Counters& C, std:
   }
   uint32_t dg = g.sim->diag;
   C.episodes++;
+  if (tt) {
+    C.tt_episodes++;
+    if (L.status & ST_TIE) C.tt_ties++;
+    if (tt_stopped) {
+      C.tt_unresolved++;
+      return true;
+    }
+  }
   if (L.status & ST_TIE) C.lane_tie++;
   if (L.status & ST_TIE_UNRESOLVED) C.unresolved++;
   if (dg & oracle::DIAG_TIE) C.tie_eps++;
@@ -230,7 +253,9 @@ int main(int argc, char** argv) {
       }
     }
   printf("{\"episodes\": %ld, \"mismatches\": %ld, \"oracle_tie_episodes\": %ld, "
-         "\"lane_tie_episodes\": %ld, \"hazard_mismatches\": %ld, \"overlap_episodes\": %ld, \"unresolved\": %ld}\n",
-         C.episodes, C.mismatches, C.tie_eps, C.lane_tie, C.tie_mismatch, C.overlap_eps, C.unresolved);
+         "\"lane_tie_episodes\": %ld, \"hazard_mismatches\": %ld, \"overlap_episodes\": %ld, \"unresolved\": %ld, "
+         "\"tie_rule_episodes\": %ld, \"tie_rule_ties\": %ld, \"tie_rule_unresolved\": %ld}\n",
+         C.episodes, C.mismatches, C.tie_eps, C.lane_tie, C.tie_mismatch, C.overlap_eps, C.unresolved,
+         C.tt_episodes, C.tt_ties, C.tt_unresolved);
   return C.mismatches ? 1 : 0;
 }

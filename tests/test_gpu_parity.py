@@ -102,6 +102,27 @@ def test_tie_windows_replayed_exactly(ctx):
     assert int(((rec["status"] & L.ST_TIE_UNRESOLVED) != 0).sum()) == 0
 
 
+@pytest.mark.parametrize("policy", [L.POLICY_EYAL_SIRER_2014, L.POLICY_SAPIRSHTEIN_2016_SM1])
+@pytest.mark.parametrize("gamma", [0.0, 0.5])
+def test_summary_only_kernels_equal_record_kernels(ctx, gamma, policy):
+    # cpr_run_episodes without records runs the summary-only specialisations of
+    # k_run_episodes (no block-time bookkeeping; gamma = 0 compiled without arrivals; at
+    # d = 2 ties by the closed-form rule, a tie it does not cover re-run exactly); with
+    # records, the general kernel (heap replay). Match-heavy play at the bench's sizes of
+    # episode: every summary field, ties included, must be identical.
+    cfg, keep = device.make_config(alpha=0.33, gamma=gamma, policy=policy, max_steps=2016,
+                                   seed=0x5A11)
+    b = device.Batch(cfg, ctx=ctx, keep=keep)
+    n = 65536
+    s1, _ = b.run(n, first_episode=0, records=True)
+    s0 = b.run(n, first_episode=0)
+    for f in L.Summary.FIELDS:
+        assert getattr(s0, f) == getattr(s1, f), f
+    assert list(s0.hist) == list(s1.hist)
+    if gamma > 0:
+        assert s1.status_tie > 0  # ties occurred and took the closed-form rule
+
+
 @pytest.mark.parametrize("alpha,policy,table", [(0.35, L.POLICY_SAPIRSHTEIN_2016_SM1, False),
                                                 (0.5, L.POLICY_SAPIRSHTEIN_2016_SM1, False),
                                                 (0.35, L.POLICY_EYAL_SIRER_2014, False),

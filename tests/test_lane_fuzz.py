@@ -24,6 +24,18 @@ def test_lane_matches_oracle_fuzz():
     assert out["mismatches"] == 0 and out["hazard_mismatches"] == 0, p.stderr[-2000:]
     assert out["unresolved"] == 0
     assert out["episodes"] > 1000
+    assert out["tie_rule_episodes"] > 100  # two-defender episodes run with the tie rule
+
+
+def test_tie_rule_equals_heap_replay():
+    # the closed-form tie outcome of the d = 2 summary-only kernels (nakamoto_lane.h
+    # tie_table_d2) against the heap replay over every case it covers
+    subprocess.run(["make", "-s", "-C", str(ROOT / "tests" / "native")], check=True)
+    p = subprocess.run([str(ROOT / "tests" / "native" / "build" / "tie_table")],
+                       capture_output=True, text=True, timeout=120)
+    out = json.loads(p.stdout.strip().splitlines()[-1])
+    assert p.returncode == 0, p.stderr[-2000:]
+    assert out["mismatches"] == 0 and out["cases"] == 320 and 0 < out["on_top"] < 320
 
 
 def test_ethereum_lane_matches_oracle_fuzz():
