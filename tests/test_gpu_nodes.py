@@ -151,6 +151,21 @@ def test_honest_net_rows_per_node(ctx, row):
 
 CHAIN_ROWS = json.loads((GOLDEN / "honest_net_chains.json").read_text())["rows"]
 
+# per-node outputs of a chained row's replayed trace, shared by the two tests below when they
+# build byte-identical configurations (a Tailstorm row is one latency-bound lane, ~7 s)
+_NODE_OUT = {}
+
+
+def _chained_node_outputs(ctx, cfg, keep, row):
+    from test_oracle_clique import chained_rng
+
+    key = (row["line"], bytes(cfg))
+    if key not in _NODE_OUT:
+        trace, _ = O.export_traces(cfg, 0, 1, rng=chained_rng(row))
+        b = device.Batch(cfg, ctx=ctx, keep=keep)
+        _NODE_OUT[key] = b.node_outputs(trace=trace)
+    return _NODE_OUT[key]
+
 
 @pytest.mark.parametrize("row", CHAIN_ROWS, ids=lambda r: f"line{r['line']}-{r['protocol']}")
 def test_chained_honest_net_rows_per_node(ctx, row):
@@ -163,9 +178,7 @@ def test_chained_honest_net_rows_per_node(ctx, row):
     sel = {None: 0, "altruistic": 0, "heuristic": 1, "optimal": 2}[row.get("subblock_selection")]
     cfg, keep = _clique(proto, row["nodes"], row["activation_delay"], row["activations"],
                         k=row.get("k") or 8, scheme=scheme, sel=sel, seed=11)
-    trace, _ = O.export_traces(cfg, 0, 1, rng=chained_rng(row))
-    b = device.Batch(cfg, ctx=ctx, keep=keep)
-    rec, acts, rews = b.node_outputs(trace=trace)
+    rec, acts, rews = _chained_node_outputs(ctx, cfg, keep, row)
     assert not (rec["status"] & L.ST_TRACE_MISS).any()
     assert acts[0].tolist() == row["activations_per_node"]
     assert rews[0].tolist() == row["reward"]
@@ -189,9 +202,7 @@ def test_device_rows_reproduce_reference_text(ctx, line):
     row = CHAINS[line]
     task = _task(row)
     cfg, keep = C.config_of(task, seed=11)
-    trace, _ = O.export_traces(cfg, 0, 1, rng=chained_rng(row))
-    b = device.Batch(cfg, ctx=ctx, keep=keep)
-    rec, acts, rews = b.node_outputs(trace=trace)
+    rec, acts, rews = _chained_node_outputs(ctx, cfg, keep, row)
     got = _fields(C.result_row(task, rec[0], acts[0], rews[0], 0.0), TSV["header"])
     for col, g, r in zip(TSV["header"], got, TSV["rows"][str(line)]):
         if col not in SKIP:
