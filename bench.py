@@ -312,6 +312,8 @@ def main():
     ap.add_argument("--no-configs", action="store_true",
                     help="skip BASELINE configs[0], [2]-[4] (other_configs)")
     ap.add_argument("--config-cpu-seconds", type=float, default=2.0)
+    ap.add_argument("--gammas", default=",".join(str(g) for g in GAMMAS),
+                    help="sweep gammas (A/B runs; the headline is the default)")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="collective backend (nccl = RCCL; gloo only for the one-GPU "
                          "multi-rank test, tests/test_gpu_distributed.py)")
@@ -331,7 +333,8 @@ def main():
     tdev = torch.device("cuda", gpu)
     cdev = tdev if args.backend == "nccl" else None  # where collectives' tensors live
     ctx = device.Context(gpu)
-    points = [(a, g) for g in GAMMAS for a in ALPHAS]
+    gammas = [float(g) for g in args.gammas.split(",")]
+    points = [(a, g) for g in gammas for a in ALPHAS]
     batches = []
     for a, g in points:
         cfg, keep = device.make_config(alpha=a, gamma=g, max_steps=STEPS_PER_EPISODE, seed=SEED)
@@ -450,6 +453,8 @@ def main():
                 / (HBM_PEAK_GBS * 1e9),
                 "kernel": "k_run_episodes",
                 "kernel_ms_mean": float(kms.mean()),
+                "kernel_ms_per_point": {f"{a:.2f},{g:.1f}": round(float(m), 3)
+                                        for (a, g), m in zip(points, kms)},
                 "kernel_activations_per_s": act_per_s_kernel,
             },
             "status": {"tie_episodes": ties, "overlap_episodes": overlaps, "other": other},

@@ -10,6 +10,8 @@ the variants' results are meaningless; only their kernel times are read.
               which any lane of the wave races) -> a multiply-xorshift hash
   base      : the tree as it is
   unroll2   : the gym loop two activations per trip (CPR_NAK_UNROLL2)
+  tt1w4     : the d = 2 tie-rule kernel at 4 waves/SIMD instead of 5
+  tt0       : no tie-rule kernel (d = 2 runs the heap-replay summary-only kernel)
   wavesN    : k_run_episodes compiled for N waves per SIMD instead of 4 (VGPR budget 512/N)
 
 usage: python tools/nak_probe_variants.py [name | name@gitrev ...]  (build/var/<name>.so;
@@ -70,6 +72,16 @@ def variant(name, rng, log, rev=None):
         assert LINK_OLD in st
         st = st.replace(LINK_OLD, LINK_NEW, 1)
     (d / "cpr_stream.h").write_text(st)
+    if name.startswith("tt1w4"):  # the d = 2 tie-rule kernel at the 4-wave budget
+        k = (d / "kernels.hip").read_text()
+        assert "amdgpu_waves_per_eu(TT ? 5 : 4)" in k
+        (d / "kernels.hip").write_text(k.replace("amdgpu_waves_per_eu(TT ? 5 : 4)",
+                                                 "amdgpu_waves_per_eu(4)"))
+    if name.startswith("tt0"):  # no tie-rule kernel: d = 2 runs the heap-replay kernel
+        k = (d / "kernels.hip").read_text()
+        old = "return P.d == 2 ? k_run_episodes<CPR_MODE_GYM, SeedSource, POL, 0, 1, 1>"
+        assert old in k
+        (d / "kernels.hip").write_text(k.replace(old, old.replace("P.d == 2", "P.d == -1")))
     if "unroll2" in name:  # two activations per trip of the gym loop (kernels.hip)
         k = (d / "kernels.hip").read_text()
         (d / "kernels.hip").write_text("#define CPR_NAK_UNROLL2 1\n" + k)

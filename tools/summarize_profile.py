@@ -17,7 +17,7 @@ K = "k_run_episodes"
 # stream (bench.py's abstract-gamma column after the timed sweep runs the generic POL = -1
 # instantiation and is left out); bench.py asks for no records, so the summary-only
 # specialisation (REC = 0) runs
-HEADLINE = re.compile(r"k_run_episodes<0, (cpr::)?SeedSource, 3(, 0)?>")
+HEADLINE = re.compile(r"k_run_episodes<0, (cpr::)?SeedSource, 3(, 0(, -?\d+, \d+)?)?>")
 
 
 def is_headline(name):
