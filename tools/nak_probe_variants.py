@@ -82,6 +82,11 @@ def variant(name, rng, log, rev=None):
         old = "return P.d == 2 ? k_run_episodes<CPR_MODE_GYM, SeedSource, POL, 0, 1, 1>"
         assert old in k
         (d / "kernels.hip").write_text(k.replace(old, old.replace("P.d == 2", "P.d == -1")))
+    if name.startswith("tt1d2"):  # the tie-rule kernel with d = 2 a compile-time constant
+        k = (d / "kernels.hip").read_text()
+        old = "  if (ARR >= 0) P.arrive = ARR;"
+        assert old in k
+        (d / "kernels.hip").write_text(k.replace(old, old + "\n  if (TT) P.d = 2;"))
     if "unroll2" in name:  # two activations per trip of the gym loop (kernels.hip)
         k = (d / "kernels.hip").read_text()
         (d / "kernels.hip").write_text("#define CPR_NAK_UNROLL2 1\n" + k)
