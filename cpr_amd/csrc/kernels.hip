@@ -48,8 +48,18 @@ __device__ inline CPR_AI BRef run_gym(NakLane& L, const NakParams& P, const St& 
 #ifndef CPR_NAK_UNROLL2
     do {
       const NakLane::Draw dr = L.draw(P, S);
+#ifdef CPR_NAK_SPEC_RACE
+      // d = 2: the window's only possible race is at the non-miner defender over one released
+      // block; its link delay depends on the window's coordinates only, so it is drawn here,
+      // a second Philox chain beside the next activation's (SIMT runs it whenever any lane of
+      // the wave races, which is nearly every window)
+      const double ru = TT ? S.link((uint32_t)L.k, 0u, (uint32_t)(3 - (L.wminer & 3)), P.dmax)
+                           : __builtin_nan("");
+#else
+      const double ru = __builtin_nan("");
+#endif
       L.apply(L.policy_action<POL>(P));
-      L.resolve<St, POL >= 0 ? 0 : -1, TT>(P, S, M);
+      L.resolve<St, POL >= 0 ? 0 : -1, TT>(P, S, M, ru);
       L.activate(P, S, M, dr);
       ++steps;
     } while (steps < P.max_steps);
