@@ -48,18 +48,8 @@ __device__ inline CPR_AI BRef run_gym(NakLane& L, const NakParams& P, const St& 
 #ifndef CPR_NAK_UNROLL2
     do {
       const NakLane::Draw dr = L.draw(P, S);
-#ifdef CPR_NAK_SPEC_RACE
-      // d = 2: the window's only possible race is at the non-miner defender over one released
-      // block; its link delay depends on the window's coordinates only, so it is drawn here,
-      // a second Philox chain beside the next activation's (SIMT runs it whenever any lane of
-      // the wave races, which is nearly every window)
-      const double ru = TT ? S.link((uint32_t)L.k, 0u, (uint32_t)(3 - (L.wminer & 3)), P.dmax)
-                           : __builtin_nan("");
-#else
-      const double ru = __builtin_nan("");
-#endif
       L.apply(L.policy_action<POL>(P));
-      L.resolve<St, POL >= 0 ? 0 : -1, TT>(P, S, M, ru);
+      L.resolve<St, POL >= 0 ? 0 : -1, TT>(P, S, M);
       L.activate(P, S, M, dr);
       ++steps;
     } while (steps < P.max_steps);
@@ -133,6 +123,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(TT ? 5 :
     double* spill, uint8_t* replay, cpr_episode_record* recs, cpr_summary* sum,
     int64_t* redo, uint32_t* redo_n, uint32_t launch_id, int64_t redo_cap) {
   if (ARR >= 0) P.arrive = ARR;
+  if (TT) P.d = 2;  // launched for two defenders only (gym_run_fn): masks and loops fold
   __shared__ int32_t hist[CPR_HIST_BINS];
   __shared__ double ring[RING * kBlock];
   __shared__ unsigned long long acc_w[13];

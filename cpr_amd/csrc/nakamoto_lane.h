@@ -566,11 +566,8 @@ struct NakLane {
   // TT: 1 = ties resolved without the heap replay (tie_table_d2), for kernels that run only
   // d = 2 configurations; a tie that rule does not cover flags TIE_UNRESOLVED (the fused
   // kernel hands such an episode to the exact re-run). 0 = tie_replay.
-  // race_u: TT kernels may pass the non-miner defender's link delay for a one-block release,
-  // drawn ahead beside the next activation's draws (NaN: draw it here)
   template <class St, int AG = -1, int TT = 0>
-  __host__ __device__ inline CPR_AI void resolve(const NakParams& P, const St& S, const LaneMem& M,
-                                                 double race_u = __builtin_nan("")) {
+  __host__ __device__ inline CPR_AI void resolve(const NakParams& P, const St& S, const LaneMem& M) {
     const bool released = rhi >= rlo && P.arrive;
     const uint64_t all = all_mask(P.d);
     const bool dm = wminer != 0;
@@ -595,13 +592,9 @@ struct NakLane {
       for (int32_t i = 0; i < P.d - 1; ++i) {
         const int32_t j = i + (i + 1 >= wminer ? 2 : 1);
         double v = -__builtin_inf();
-        if (TT && rlo == rhi && race_u == race_u) {
-          v = t + race_u;
-        } else {
-          for (int32_t m = rlo; m <= rhi; ++m) {
-            const double a = t + S.link((uint32_t)k, (uint32_t)(rhi - m), (uint32_t)j, P.dmax);
-            v = a > v ? a : v;
-          }
+        for (int32_t m = rlo; m <= rhi; ++m) {
+          const double a = t + S.link((uint32_t)k, (uint32_t)(rhi - m), (uint32_t)j, P.dmax);
+          v = a > v ? a : v;
         }
         mask |= v < tb ? 1ull << (j - 1) : 0ull;
         tie |= v == tb;

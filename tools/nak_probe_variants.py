@@ -87,9 +87,6 @@ def variant(name, rng, log, rev=None):
         old = "  if (ARR >= 0) P.arrive = ARR;"
         assert old in k
         (d / "kernels.hip").write_text(k.replace(old, old + "\n  if (TT) P.d = 2;"))
-    if name.startswith("specrace"):  # the d = 2 race's link draw beside the activation draw
-        k = (d / "kernels.hip").read_text()
-        (d / "kernels.hip").write_text("#define CPR_NAK_SPEC_RACE 1\n" + k)
     if "unroll2" in name:  # two activations per trip of the gym loop (kernels.hip)
         k = (d / "kernels.hip").read_text()
         (d / "kernels.hip").write_text("#define CPR_NAK_UNROLL2 1\n" + k)
