@@ -18,8 +18,6 @@ import bench  # noqa: E402
 def test_headline_is_configs1_at_its_stated_size():
     # 20 whole rounds of the 262,144-lane resident grid per point, and the driver's 20 steps
     # make BASELINE's 10^8 episodes per (alpha, gamma) point
-    import argparse
-
     src = (ROOT / "bench.py").read_text()
     assert "default=5242880" in src
     assert 5242880 % 262144 == 0 and 5242880 * 20 >= 10**8
