@@ -12,6 +12,7 @@ the variants' results are meaningless; only their kernel times are read.
   unroll2   : the gym loop two activations per trip (CPR_NAK_UNROLL2)
   tt1w4     : the d = 2 tie-rule kernel at 4 waves/SIMD instead of 5
   tt0       : no tie-rule kernel (d = 2 runs the heap-replay summary-only kernel)
+  norace    : cost probe, the d = 2 kernel's races decided without their link draw
   wavesN    : k_run_episodes compiled for N waves per SIMD instead of 4 (VGPR budget 512/N)
 
 usage: python tools/nak_probe_variants.py [name | name@gitrev ...]  (build/var/<name>.so;
@@ -87,6 +88,12 @@ def variant(name, rng, log, rev=None):
         old = "  if (ARR >= 0) P.arrive = ARR;"
         assert old in k
         (d / "kernels.hip").write_text(k.replace(old, old + "\n  if (TT) P.d = 2;"))
+    if name.startswith("norace"):  # cost probe: d = 2 races always won by the release
+        lane = (d / "nakamoto_lane.h").read_text()
+        old = "      for (int32_t i = 0; i < P.d - 1; ++i) {"
+        assert old in lane
+        lane = lane.replace(old, "      if (TT) { mask = 1ull << (2 - wminer); } else\n" + old, 1)
+        (d / "nakamoto_lane.h").write_text(lane)
     if "unroll2" in name:  # two activations per trip of the gym loop (kernels.hip)
         k = (d / "kernels.hip").read_text()
         (d / "kernels.hip").write_text("#define CPR_NAK_UNROLL2 1\n" + k)
