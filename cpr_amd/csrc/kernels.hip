@@ -42,6 +42,7 @@ __device__ inline CPR_AI BRef run_gym(NakLane& L, const NakParams& P, const St& 
   L.activate(P, S, M);
   const bool check_prog = P.max_progress < __builtin_inf();
   int64_t steps = 0;
+  if constexpr (TT == 2) L.save(M.ck, M.ck_stride);
   if (!check_prog && !(P.max_time < __builtin_inf())) {
     // only max_steps ends the episode: the trip count is the same in every lane of the
     // wave, so the loop exit is uniform and no lane state is merged at a divergent exit
@@ -50,9 +51,15 @@ __device__ inline CPR_AI BRef run_gym(NakLane& L, const NakParams& P, const St& 
       const NakLane::Draw dr = L.draw(P, S);
       L.apply(L.policy_action<POL>(P));
       L.resolve<St, POL >= 0 ? 0 : -1, TT>(P, S, M);
+      if constexpr (TT == 2) enqueue_race(L, M);
       L.activate(P, S, M, dr);
       ++steps;
+      // the lanes of the wave verify together once the wave's list is nearly full
+      if constexpr (TT == 2) {
+        if (races_due(L, M)) verify_races<POL>(L, P, S, M);
+      }
     } while (steps < P.max_steps);
+    if constexpr (TT == 2) verify_races<POL>(L, P, S, M);
 #else
     // two steps per trip: both activations' draws (two independent Philox / log chains,
     // which depend on the activation count only) are issued together
@@ -80,7 +87,7 @@ __device__ inline CPR_AI BRef run_gym(NakLane& L, const NakParams& P, const St& 
   for (;;) {
     const int32_t a = L.policy_action<POL>(P);
     L.apply(a);
-    L.resolve<St, POL >= 0 ? 0 : -1, TT>(P, S, M);
+    L.resolve<St, POL >= 0 ? 0 : -1, TT == 2 ? 1 : TT>(P, S, M);
     L.activate(P, S, M);
     ++steps;
     bool go = steps < P.max_steps && L.t < P.max_time;
@@ -116,7 +123,9 @@ constexpr uint32_t kInexact = ST_OVERLAP | ST_DEEP_FORK | ST_TIE_UNRESOLVED | ST
 // gym's gamma = 0 network, so the second defender tip, the races and the tie replay drop
 // out; 1: they do), or -1 to read it from P
 // TT: 1 = launched for d = 2 only: ties take the closed-form rule (tie_table_d2) instead
-// of the inlined heap replay, whose registers otherwise stay live across the whole loop
+// of the inlined heap replay, whose registers otherwise stay live across the whole loop;
+// 2 = as 1, and the races are deferred and verified in batches (verify_races; REC = 0 only:
+// the queue takes the LDS ring, the checkpoints the spill buffer)
 template <int MODE, class Src, int POL, int REC = 1, int ARR = -1, int TT = 0>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(TT ? 5 : 4))) void k_run_episodes(
     NakParams P, Src src, int64_t n_eps, int64_t activations,
@@ -125,7 +134,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(TT ? 5 :
   if (ARR >= 0) P.arrive = ARR;
   if (TT) P.d = 2;  // launched for two defenders only (gym_run_fn): masks and loops fold
   __shared__ int32_t hist[CPR_HIST_BINS];
-  __shared__ double ring[RING * kBlock];
+  // TT = 2 (summary only): the ring holds the race queue alone, sized so that five
+  // workgroups fit a CU's LDS
+  __shared__ double ring[(REC || TT != 2 ? RING : 2 * RQ_LANE) * kBlock];
+  __shared__ int32_t rflag[TT == 2 ? kBlock : 1];
+  __shared__ uint32_t rep[TT == 2 ? 2 * kBlock : 1];
   __shared__ unsigned long long acc_w[13];
   LdsAcc acc{acc_w};
   acc.init();
@@ -146,6 +159,20 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(TT ? 5 :
   M.replay = ReplayMem::at(replay + tid * REPLAY_BYTES);
   M.times = REC != 0;
   if (!REC) recs = nullptr;
+  if (TT == 2) {
+    // summary-only: the ring and the spill buffer hold no block times. Each wave's race
+    // list in its share of the ring's LDS; checkpoints in the spill buffer, per wave
+    // [quad][lane] (each 16-byte store of a wave writes 1 KB contiguously)
+    M.rq = reinterpret_cast<uint4*>(ring) + (threadIdx.x / WAVE) * (RQ_LANE * WAVE);
+    M.rq_cap = RQ_LANE * WAVE;
+    M.rflag = rflag + (threadIdx.x / WAVE) * WAVE;
+    M.rep = rep + (threadIdx.x / WAVE) * (2 * WAVE);
+    M.lane = (int32_t)(threadIdx.x % WAVE);
+    M.wave = WAVE;
+    M.rflag[M.lane] = 0;
+    M.ck = reinterpret_cast<uint4*>(spill) + (tid / WAVE) * (WAVE * CK_QUADS) + M.lane;
+    M.ck_stride = WAVE;
+  }
   NakLane L;
   for (int64_t e = tid; e < n_eps; e += nthreads) {
     const auto S = src.at(e);
@@ -438,12 +465,24 @@ __global__ void k_stream_fill(uint64_t seed, uint64_t ep, uint32_t idx0, uint32_
 // tasks run the generic kernel. Template arguments do not change the signature.
 using RunFn = void (*)(NakParams, SeedSource, int64_t, int64_t, double*, uint8_t*,
                        cpr_episode_record*, cpr_summary*, int64_t*, uint32_t*, uint32_t, int64_t);
+// deferred races (TT = 2) pay where the release always reaches the non-miner defender no
+// later than the defender block (dmax <= delta: the gym's gamma <= .5 networks), so that a
+// verification almost never rolls back; they need the spill buffer to hold a checkpoint and
+// release indices that fit a queue entry
+#ifndef CPR_DEFER_RACES
+#define CPR_DEFER_RACES 0
+#endif
+static bool deferred_races_ok(const NakParams& P) {
+  return CPR_DEFER_RACES && P.dmax <= P.delta && 8 * (int64_t)P.cap >= 16 * CK_QUADS &&
+         P.cap <= 4096;
+}
 template <int POL>
 static RunFn gym_run_fn(const NakParams& P, bool recs) {
   if (recs) return k_run_episodes<CPR_MODE_GYM, SeedSource, POL, 1, -1>;
   if (!P.arrive) return k_run_episodes<CPR_MODE_GYM, SeedSource, POL, 0, 0>;
-  return P.d == 2 ? k_run_episodes<CPR_MODE_GYM, SeedSource, POL, 0, 1, 1>
-                  : k_run_episodes<CPR_MODE_GYM, SeedSource, POL, 0, 1>;
+  if (P.d != 2) return k_run_episodes<CPR_MODE_GYM, SeedSource, POL, 0, 1>;
+  return deferred_races_ok(P) ? k_run_episodes<CPR_MODE_GYM, SeedSource, POL, 0, 1, 2>
+                              : k_run_episodes<CPR_MODE_GYM, SeedSource, POL, 0, 1, 1>;
 }
 static RunFn run_fn(const NakParams& P, int32_t mode, bool recs) {
   if (mode != CPR_MODE_GYM) return k_run_episodes<CPR_MODE_LOOP, SeedSource, -1>;

@@ -78,7 +78,50 @@ struct LaneMem {
   // and every time computation, ring store and spill store drops out of the inlined lane
   // (the summary does not depend on them).
   bool times = true;
+  // deferred races (NakLane::resolve<.., TT = 2>, enqueue_race, verify_races): the wave's
+  // dense list of unverified races (rq_cap entries, shared by its lanes), the wave's
+  // rollback flags and episode words (the keyed stream's e0, e1: a race is verified on
+  // its owner's stream), one and two per lane, this lane's index in the wave, and the
+  // lane's checkpoint, quad q (16 bytes) at ck[q * ck_stride]
+  uint4* rq = nullptr;
+  int32_t rq_cap = 0;
+  int32_t* rflag = nullptr;
+  uint32_t* rep = nullptr;
+  int32_t lane = 0;
+  int32_t wave = 1;  // lanes that share the list (WAVE in the kernels; the host tests emulate more)
+  uint4* ck = nullptr;
+  int64_t ck_stride = 0;
 };
+
+// deferred races: queue entries per lane of a wave (the list is the wave's: 64 times this)
+constexpr int32_t RQ_LANE = 6;
+// checkpoint words of a NakLane without block times (NakLane::pack / unpack), stored as
+// CK_QUADS 16-byte quads (NakLane::save / load)
+constexpr int32_t CK_WORDS = 38;
+constexpr int32_t CK_QUADS = (CK_WORDS + 3) / 4;
+
+// wave primitives of the deferred races (a wave of one lane on the host)
+#if defined(__HIP_DEVICE_COMPILE__)
+constexpr int32_t WAVE = 64;
+__device__ inline CPR_AI uint64_t wave_ballot(bool p) { return __ballot(p ? 1 : 0); }
+__device__ inline CPR_AI int32_t lanes_below(uint64_t m) {
+  return (int32_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                            __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+// LDS written by some lanes, then read by others of the same wave: keep the order
+__device__ inline CPR_AI void wave_lds_order() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+// several lanes may flag the same owner in one pass
+__device__ inline CPR_AI void flag_or(int32_t* p, int32_t v) { atomicOr(p, v); }
+#else
+constexpr int32_t WAVE = 1;
+inline uint64_t wave_ballot(bool p) { return p ? 1ull : 0ull; }
+inline int32_t lanes_below(uint64_t) { return 0; }
+inline void wave_lds_order() {}
+inline void flag_or(int32_t* p, int32_t v) { *p |= v; }
+#endif
 
 constexpr int32_t K_GENESIS = -1, K_PRIVATE = -2;
 
@@ -397,6 +440,9 @@ struct NakLane {
   int32_t lca_da;    // height of LCA(D, A)
   int32_t w_hasb;    // the window resolved last delivered a defender block
   double w_bound;    // conservative bound on that window's latest arrival
+  int32_t qn;        // deferred races in the wave's list (TT = 2; the same in every lane)
+  uint32_t rw;       // the race resolve<.., 2> took as decided: wminer | rlo << 2 |
+                     // rhi << 14, 0 = none (enqueue_race lists it)
 
   __host__ __device__ inline CPR_AI double chain_t(const LaneMem& M, int32_t m) const {
     if (!M.times) return 0.0;
@@ -429,6 +475,55 @@ struct NakLane {
     k = 0; n = 0; rel = 0; n_ba = 0; pend = -1; wminer = 0; event = 0;
     rlo = 1; rhi = 0; status = 0u; onA = 0ull; lca_da = 0;
     w_hasb = 0; w_bound = -__builtin_inf();
+    qn = 0; rw = 0u;
+  }
+
+  // the lane's state without block times (the summary-only kernels' whole state) as
+  // CK_WORDS words (constant indices: the words stay in registers)
+  __host__ __device__ inline CPR_AI void pack(uint32_t* c) const {
+    int32_t f = 0;
+    auto w = [&](uint32_t x) { c[f++] = x; };
+    auto wd = [&](double x) { const uint64_t b = bitsd(x); w((uint32_t)b); w((uint32_t)(b >> 32)); };
+    auto wb = [&](const BRef& r) { w((uint32_t)r.h); w((uint32_t)r.ra); w((uint32_t)r.k); w((uint32_t)r.fork); };
+    wd(t); w((uint32_t)k); w((uint32_t)n); w((uint32_t)rel); w((uint32_t)n_ba); w((uint32_t)pend);
+    w((uint32_t)wminer); w((uint32_t)event); w((uint32_t)rlo); w((uint32_t)rhi); w(status);
+    wb(p0); wb(pub); wb(D); wb(A); wb(b);
+    w((uint32_t)onA); w((uint32_t)(onA >> 32)); w((uint32_t)lca_da); w((uint32_t)w_hasb);
+    wd(w_bound);
+  }
+  __host__ __device__ inline CPR_AI void unpack(const uint32_t* c) {
+    int32_t f = 0;
+    auto r = [&]() { return c[f++]; };
+    auto rd = [&]() { const uint64_t lo = r(); return dbits(lo | ((uint64_t)r() << 32)); };
+    auto rb = [&](BRef& x) { x.h = (int32_t)r(); x.ra = (int32_t)r(); x.k = (int32_t)r(); x.fork = (int32_t)r(); x.tm = 0.0; };
+    t = rd(); k = (int32_t)r(); n = (int32_t)r(); rel = (int32_t)r(); n_ba = (int32_t)r();
+    pend = (int32_t)r(); wminer = (int32_t)r(); event = (int32_t)r(); rlo = (int32_t)r();
+    rhi = (int32_t)r(); status = r();
+    rb(p0); rb(pub); rb(D); rb(A); rb(b);
+    const uint64_t lo = r();
+    onA = lo | ((uint64_t)r() << 32);
+    lca_da = (int32_t)r(); w_hasb = (int32_t)r();
+    w_bound = rd();
+    rw = 0u;
+  }
+  // the checkpoint: the packed words as quads, quad q at c[q * s] (one 16-byte store each)
+  __host__ __device__ inline CPR_AI void save(uint4* c, int64_t s) const {
+    uint32_t w[CK_QUADS * 4];
+    pack(w);
+    for (int32_t i = CK_WORDS; i < CK_QUADS * 4; ++i) w[i] = 0u;
+    for (int32_t q = 0; q < CK_QUADS; ++q) {
+      uint4 v;
+      v.x = w[4 * q]; v.y = w[4 * q + 1]; v.z = w[4 * q + 2]; v.w = w[4 * q + 3];
+      c[q * s] = v;
+    }
+  }
+  __host__ __device__ inline CPR_AI void load(const uint4* c, int64_t s) {
+    uint32_t w[CK_QUADS * 4];
+    for (int32_t q = 0; q < CK_QUADS; ++q) {
+      const uint4 v = c[q * s];
+      w[4 * q] = v.x; w[4 * q + 1] = v.y; w[4 * q + 2] = v.z; w[4 * q + 3] = v.w;
+    }
+    unpack(w);
   }
 
   // latest finite arrival of the window resolved last (exact; only evaluated when the next
@@ -566,6 +661,11 @@ struct NakLane {
   // TT: 1 = ties resolved without the heap replay (tie_table_d2), for kernels that run only
   // d = 2 configurations; a tie that rule does not cover flags TIE_UNRESOLVED (the fused
   // kernel hands such an episode to the exact re-run). 0 = tie_replay.
+  // 2 = deferred (d = 2 and dmax <= delta, the gym's gamma = .5 network): every release then
+  // reaches the non-miner defender no later than the defender block, so the race's outcome
+  // is decided, the release first, unless the two arrive at the same fp instant. The race is
+  // taken as decided and noted (rw) for enqueue_race; verify_races checks the wave's list in
+  // batches and rolls a lane back to its checkpoint when a tie decided otherwise.
   template <class St, int AG = -1, int TT = 0>
   __host__ __device__ inline CPR_AI void resolve(const NakParams& P, const St& S, const LaneMem& M) {
     const bool released = rhi >= rlo && P.arrive;
@@ -583,6 +683,9 @@ struct NakLane {
       mask = 0ull;
       for (int32_t j = 1; j <= P.d; ++j)
         mask |= S.link((uint32_t)k, 0u, (uint32_t)j, 1.0) < P.gamma ? 1ull << (j - 1) : 0ull;
+    } else if (TT == 2 && released && dm && xh == b.h) {
+      mask = 1ull << (2 - wminer);  // j = 3 - wminer first reached by the release
+      rw = (uint32_t)wminer | ((uint32_t)rlo << 2) | ((uint32_t)rhi << 14);
     } else if (released && dm && xh == b.h) {
       // race at every defender except the miner: first visible wins. One link draw per
       // (non-miner defender, released block); the defender index is per lane.
@@ -668,6 +771,102 @@ struct NakLane {
     return nak_policy(POL >= 0 ? POL : P.policy, h, a, ev, P.table, P.table_dim);
   }
 };
+
+// TT = 2, after resolve: the lanes whose race was taken as decided append it to the wave's
+// dense list (entry: window time, activation count, rw with the owner lane in bits 26..31),
+// so that verify_races spreads the wave's races over all its lanes
+__host__ __device__ inline CPR_AI uint4 race_entry(const NakLane& L, int32_t lane) {
+  const uint64_t tb = bitsd(L.t);
+  uint4 e;
+  e.x = (uint32_t)tb;
+  e.y = (uint32_t)(tb >> 32);
+  e.z = (uint32_t)L.k;
+  e.w = L.rw | ((uint32_t)lane << 26);
+  return e;
+}
+__host__ __device__ inline CPR_AI void enqueue_race(NakLane& L, const LaneMem& M) {
+  const bool race = L.rw != 0u;
+  const uint64_t bal = wave_ballot(race);
+  if (race) M.rq[L.qn + lanes_below(bal)] = race_entry(L, M.lane);
+  L.qn += __builtin_popcountll(bal);
+  L.rw = 0u;
+}
+
+// the wave's list must be verified before the next iteration could overflow it
+__host__ __device__ inline CPR_AI bool races_due(const NakLane& L, const LaneMem& M) {
+  return L.qn > M.rq_cap - M.wave;
+}
+
+// TT = 2: verifies the wave's deferred races, lane i taking entries i, i + 64, ... A race
+// whose release does not strictly precede the defender block at the non-miner defender (a
+// same-instant tie) was decided wrongly or by the queue order: its owner lane then returns
+// to its checkpoint and runs again, eagerly (resolve<TT = 1>), up to where it was
+// (tests/native/defer_vs_eager.cpp compares the two on the host, rollbacks forced by
+// dmax > delta included). Every draw is keyed by the activation count, so the re-run is
+// the same episode. The checkpoint then moves here.
+// in three phases, each over the whole wave (the host tests emulate a wave phase by phase):
+// publish the lane's episode; check entries lane, lane + wave, ...; settle the own flag
+template <class St>
+__host__ __device__ inline CPR_AI void races_publish(const St& S, const LaneMem& M) {
+  M.rep[2 * M.lane] = S.e0;
+  M.rep[2 * M.lane + 1] = S.e1;
+}
+template <class St>
+__host__ __device__ inline CPR_AI void races_check(const NakLane& L, const NakParams& P,
+                                                  const St& S, const LaneMem& M) {
+  for (int32_t i = M.lane; i < L.qn; i += M.wave) {
+    const uint4 e = M.rq[i];
+    const double t = dbits((uint64_t)e.x | ((uint64_t)e.y << 32));
+    const int32_t rlo = (int32_t)((e.w >> 2) & 0xfffu), rhi = (int32_t)((e.w >> 14) & 0xfffu);
+    const uint32_t j = 3u - (e.w & 3u);
+    const int32_t owner = (int32_t)(e.w >> 26);
+    St so = S;  // the owner lane's episode
+    so.e0 = M.rep[2 * owner];
+    so.e1 = M.rep[2 * owner + 1];
+    double v = -__builtin_inf();
+    for (int32_t m = rlo; m <= rhi; ++m) {
+      const double a = t + so.link(e.z, (uint32_t)(rhi - m), j, P.dmax);
+      v = a > v ? a : v;
+    }
+    const double tb = t + P.delta;
+    if (!(v < tb)) {
+      // the release did not arrive first: a same-instant tie whose closed-form rule
+      // (resolve<.., 1>) agrees with the assumed outcome only marks the episode (1);
+      // anything else rolls the owner back (2)
+      const bool kept = v == tb && rlo == rhi &&
+                        tie_table_d2(P, so, (int32_t)(e.w & 3u), t, (int32_t)e.z) != 0ull;
+      flag_or(&M.rflag[owner], kept ? 1 : 2);
+    }
+  }
+}
+template <int POL, class St>
+__host__ __device__ inline CPR_AI void races_settle(NakLane& L, const NakParams& P, const St& S,
+                                                   const LaneMem& M) {
+  const int32_t fl = M.rflag[M.lane];
+  M.rflag[M.lane] = 0;
+  L.qn = 0;
+  if (fl & 1) L.status |= ST_TIE;
+  if (fl & 2) {
+    const int32_t k_now = L.k;
+    L.load(M.ck, M.ck_stride);
+    while (L.k < k_now) {
+      const NakLane::Draw dr = L.draw(P, S);
+      L.apply(L.policy_action<POL>(P));
+      L.resolve<St, POL >= 0 ? 0 : -1, 1>(P, S, M);
+      L.activate(P, S, M, dr);
+    }
+  }
+  L.save(M.ck, M.ck_stride);
+}
+template <int POL, class St>
+__host__ __device__ inline CPR_AI void verify_races(NakLane& L, const NakParams& P, const St& S,
+                                                   const LaneMem& M) {
+  races_publish(S, M);
+  wave_lds_order();
+  races_check(L, P, S, M);
+  wave_lds_order();
+  races_settle<POL>(L, P, S, M);
+}
 
 // miner of activation index ka (for head_miner of the record)
 template <class St>

@@ -38,6 +38,24 @@ def test_tie_rule_equals_heap_replay():
     assert out["mismatches"] == 0 and out["cases"] == 320 and 0 < out["on_top"] < 320
 
 
+def test_deferred_races_equal_eager():
+    # tests/native/defer_vs_eager.cpp: the d = 2 summary-only kernel's deferred races (queued,
+    # verified in batches, rolled back to a checkpoint when a release did not win) end every
+    # episode in the eager closed form's state, word for word (one lane, and emulated
+    # waves whose lanes share the list); the configurations make
+    # rollbacks and same-instant ties common so both paths run
+    subprocess.run(["make", "-s", "-C", str(ROOT / "tests" / "native")], check=True)
+    p = subprocess.run([str(ROOT / "tests" / "native" / "build" / "defer_vs_eager"), "60", "600"],
+                       capture_output=True, text=True, timeout=300)
+    out = json.loads(p.stdout.strip().splitlines()[-1])
+    assert p.returncode == 0, p.stderr[-2000:]
+    assert out["mismatches"] == 0 and out["episodes"] == 4800
+    assert out["rollbacks"] > 1000 and out["tie_episodes"] > 100 and out["drains"] > 10000
+    assert out["ties_kept"] > 100  # ties the closed-form rule decides as assumed: no rollback
+    # waves of 8 lanes sharing one list, verified across lanes on each owner's stream
+    assert out["wave_mismatches"] == 0 and out["wave_episodes"] == 2560
+
+
 def test_ethereum_lane_matches_oracle_fuzz():
     # tests/native/eth_vs_oracle.cpp: cpr_amd/csrc/ethereum_lane.h (host build) vs the
     # oracle's ethereum.cpp, every step: 10 observation fields incl. the three dry-run

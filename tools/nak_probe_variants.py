@@ -13,6 +13,16 @@ the variants' results are meaningless; only their kernel times are read.
   tt1w4     : the d = 2 tie-rule kernel at 4 waves/SIMD instead of 5
   tt0       : no tie-rule kernel (d = 2 runs the heap-replay summary-only kernel)
   norace    : cost probe, the d = 2 kernel's races decided without their link draw
+  nodefer   : the d = 2 kernel with its races verified eagerly (CPR_DEFER_RACES 0, TT = 1)
+  defer*    : the d = 2 kernel with its races deferred (CPR_DEFER_RACES 1, TT = 2)
+  nodrain   : cost probe, deferred races never verified (the queue is only emptied)
+  nosave    : cost probe, deferred races verified without moving the checkpoint
+  rqN       : the deferred races' list with N entries per lane of the wave (RQ_LANE)
+  *_nock    : cost probe, no checkpoint and no rollback after a verification
+  *_nolink  : cost probe, and the verification without its link draws
+  *_norb    : cost probe, the checkpoint kept, no rollback code
+  *_nosv    : cost probe, the rollback code kept (never run), no checkpoint
+  nokeep    : every tie rolls back (no closed-form tie rule in the verification)
   wavesN    : k_run_episodes compiled for N waves per SIMD instead of 4 (VGPR budget 512/N)
 
 usage: python tools/nak_probe_variants.py [name | name@gitrev ...]  (build/var/<name>.so;
@@ -80,9 +90,9 @@ def variant(name, rng, log, rev=None):
                                                  "amdgpu_waves_per_eu(4)"))
     if name.startswith("tt0"):  # no tie-rule kernel: d = 2 runs the heap-replay kernel
         k = (d / "kernels.hip").read_text()
-        old = "return P.d == 2 ? k_run_episodes<CPR_MODE_GYM, SeedSource, POL, 0, 1, 1>"
+        old = "if (P.d != 2) return k_run_episodes<CPR_MODE_GYM, SeedSource, POL, 0, 1>;"
         assert old in k
-        (d / "kernels.hip").write_text(k.replace(old, old.replace("P.d == 2", "P.d == -1")))
+        (d / "kernels.hip").write_text(k.replace(old, old.replace("P.d != 2", "true")))
     if name.startswith("tt1d2"):  # the tie-rule kernel with d = 2 a compile-time constant
         k = (d / "kernels.hip").read_text()
         old = "  if (ARR >= 0) P.arrive = ARR;"
@@ -94,9 +104,61 @@ def variant(name, rng, log, rev=None):
         assert old in lane
         lane = lane.replace(old, "      if (TT) { mask = 1ull << (2 - wminer); } else\n" + old, 1)
         (d / "nakamoto_lane.h").write_text(lane)
+    if "nodefer" in name:  # races verified eagerly (the TT = 1 kernel)
+        k = (d / "kernels.hip").read_text()
+        (d / "kernels.hip").write_text("#define CPR_DEFER_RACES 0\n" + k)
+    elif "defer" in name:  # races deferred (the TT = 2 kernel) whatever the default
+        k = (d / "kernels.hip").read_text()
+        (d / "kernels.hip").write_text("#define CPR_DEFER_RACES 1\n" + k)
+    if name.startswith("nodrain") or name.startswith("nosave"):
+        lane = (d / "nakamoto_lane.h").read_text()
+        old = "  bool wrong = false;\n  for (int32_t i = 0; i < L.qn; ++i) {"
+        assert old in lane
+        if name.startswith("nodrain"):
+            lane = lane.replace(old, "  if (1) { L.qn = 0; return; }\n" + old, 1)
+        else:
+            old2 = "  L.save(M.ck, M.ck_stride);\n}"
+            assert old2 in lane
+            lane = lane.replace(old2, "}", 1)
+        (d / "nakamoto_lane.h").write_text(lane)
     if "unroll2" in name:  # two activations per trip of the gym loop (kernels.hip)
         k = (d / "kernels.hip").read_text()
         (d / "kernels.hip").write_text("#define CPR_NAK_UNROLL2 1\n" + k)
+    if "_nock" in name or "_nolink" in name:
+        lane = (d / "nakamoto_lane.h").read_text()
+        for old, new in [("  if (wrong) {\n    const int32_t k_now", "  if (wrong && false) {\n    const int32_t k_now"),
+                         ("  L.save(M.ck, M.ck_stride);\n}\ntemplate <int POL, class St>",
+                          "}\ntemplate <int POL, class St>")]:
+            assert old in lane, old
+            lane = lane.replace(old, new, 1)
+        if "_nolink" in name:
+            old = "      const double a = t + so.link(e.z, (uint32_t)(rhi - m), j, P.dmax);"
+            assert old in lane
+            lane = lane.replace(old, "      const double a = t + (double)(e.z ^ so.e0) * 1e-20;", 1)
+        (d / "nakamoto_lane.h").write_text(lane)
+    if "_norb" in name or "_nosv" in name:
+        lane = (d / "nakamoto_lane.h").read_text()
+        old = "  if (wrong) {\n    const int32_t k_now"
+        assert old in lane
+        if "_norb" in name:
+            lane = lane.replace(old, "  if (wrong && false) {\n    const int32_t k_now", 1)
+        else:
+            lane = lane.replace(old, "  if (wrong && L.k < 0) {\n    const int32_t k_now", 1)
+            old = "  L.save(M.ck, M.ck_stride);\n}\ntemplate <int POL, class St>"
+            assert old in lane
+            lane = lane.replace(old, "}\ntemplate <int POL, class St>", 1)
+        (d / "nakamoto_lane.h").write_text(lane)
+    if "nokeep" in name:
+        lane = (d / "nakamoto_lane.h").read_text()
+        old = "      const bool kept = v == tb && rlo == rhi &&"
+        assert old in lane
+        lane = lane.replace(old, "      const bool kept = false && v == tb && rlo == rhi &&", 1)
+        (d / "nakamoto_lane.h").write_text(lane)
+    m = re.match(r"rq(\d+)", name)
+    if m:
+        lane = (d / "nakamoto_lane.h").read_text()
+        old = re.search(r"constexpr int32_t RQ_LANE = \d+;", lane).group(0)
+        (d / "nakamoto_lane.h").write_text(lane.replace(old, f"constexpr int32_t RQ_LANE = {m.group(1)};"))
     m = re.match(r"waves(\d+)", name)
     if m:
         k = (d / "kernels.hip").read_text()
