@@ -42,7 +42,6 @@ __device__ inline CPR_AI BRef run_gym(NakLane& L, const NakParams& P, const St& 
   L.activate(P, S, M);
   const bool check_prog = P.max_progress < __builtin_inf();
   int64_t steps = 0;
-  if constexpr (TT == 2) L.save(M.ck, M.ck_stride);
   if (!check_prog && !(P.max_time < __builtin_inf())) {
     // only max_steps ends the episode: the trip count is the same in every lane of the
     // wave, so the loop exit is uniform and no lane state is merged at a divergent exit
@@ -56,10 +55,10 @@ __device__ inline CPR_AI BRef run_gym(NakLane& L, const NakParams& P, const St& 
       ++steps;
       // the lanes of the wave verify together once the wave's list is nearly full
       if constexpr (TT == 2) {
-        if (races_due(L, M)) verify_races<POL>(L, P, S, M);
+        if (races_due(L, M)) verify_races(L, P, S, M);
       }
     } while (steps < P.max_steps);
-    if constexpr (TT == 2) verify_races<POL>(L, P, S, M);
+    if constexpr (TT == 2) verify_races(L, P, S, M);
 #else
     // two steps per trip: both activations' draws (two independent Philox / log chains,
     // which depend on the activation count only) are issued together
@@ -125,7 +124,8 @@ constexpr uint32_t kInexact = ST_OVERLAP | ST_DEEP_FORK | ST_TIE_UNRESOLVED | ST
 // TT: 1 = launched for d = 2 only: ties take the closed-form rule (tie_table_d2) instead
 // of the inlined heap replay, whose registers otherwise stay live across the whole loop;
 // 2 = as 1, and the races are deferred and verified in batches (verify_races; REC = 0 only:
-// the queue takes the LDS ring, the checkpoints the spill buffer)
+// the race lists take the LDS ring); an episode a race went otherwise in is listed in the
+// spill buffer (count, then episode indices) for the eager second pass (ListSource, TT = 1)
 template <int MODE, class Src, int POL, int REC = 1, int ARR = -1, int TT = 0>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(TT ? 5 : 4))) void k_run_episodes(
     NakParams P, Src src, int64_t n_eps, int64_t activations,
@@ -160,9 +160,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(TT ? 5 :
   M.times = REC != 0;
   if (!REC) recs = nullptr;
   if (TT == 2) {
-    // summary-only: the ring and the spill buffer hold no block times. Each wave's race
-    // list in its share of the ring's LDS; checkpoints in the spill buffer, per wave
-    // [quad][lane] (each 16-byte store of a wave writes 1 KB contiguously)
+    // summary-only: the ring holds no block times; each wave's race list takes its share
     M.rq = reinterpret_cast<uint4*>(ring) + (threadIdx.x / WAVE) * (RQ_LANE * WAVE);
     M.rq_cap = RQ_LANE * WAVE;
     M.rflag = rflag + (threadIdx.x / WAVE) * WAVE;
@@ -170,15 +168,22 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(TT ? 5 :
     M.lane = (int32_t)(threadIdx.x % WAVE);
     M.wave = WAVE;
     M.rflag[M.lane] = 0;
-    M.ck = reinterpret_cast<uint4*>(spill) + (tid / WAVE) * (WAVE * CK_QUADS) + M.lane;
-    M.ck_stride = WAVE;
   }
   NakLane L;
-  for (int64_t e = tid; e < n_eps; e += nthreads) {
+  const int64_t n_run = src.size(n_eps);
+  for (int64_t e = tid; e < n_run; e += nthreads) {
     const auto S = src.at(e);
     int64_t steps = 0;
     const BRef hd = MODE == CPR_MODE_GYM ? run_gym<POL, TT>(L, P, S, M, &steps)
                                          : run_loop<POL>(L, P, S, M, activations);
+    if constexpr (TT == 2) {
+      if (L.status & ST_RACE_REDO) {
+        // a deferred race went otherwise: the eager pass runs this episode again
+        const uint32_t r = atomicAdd(reinterpret_cast<uint32_t*>(spill), 1u);
+        reinterpret_cast<int64_t*>(spill)[1 + r] = src.index(e);
+        continue;
+      }
+    }
     const double tm = L.time_of(M, hd);
     const uint32_t status = L.status | Src::missed(S);
     uint32_t st_out = status;
@@ -187,7 +192,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(TT ? 5 :
       // (k_nak_exact_rerun), which writes its record and summary contribution
       const uint32_t r = atomicAdd(redo_n, 1u);
       if ((int64_t)r < redo_cap) {
-        redo[r] = ((int64_t)launch_id << 40) | (e << 8) | (int64_t)(status & 0xffu);
+        redo[r] = ((int64_t)launch_id << 40) | (src.index(e) << 8) | (int64_t)(status & 0xffu);
         continue;
       }
       st_out |= CPR_ST_CAPACITY;  // queue full: the flagged outputs stay, marked invalid
@@ -208,7 +213,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(TT ? 5 :
       r.head_miner = MODE == CPR_MODE_GYM ? miner_of(P, S, hd.k) : -1;
       r.status = st_out;
       r.head_work = 0;
-      recs[e] = r;
+      recs[src.index(e)] = r;
     }
   }
   __syncthreads();
@@ -467,31 +472,36 @@ using RunFn = void (*)(NakParams, SeedSource, int64_t, int64_t, double*, uint8_t
                        cpr_episode_record*, cpr_summary*, int64_t*, uint32_t*, uint32_t, int64_t);
 // deferred races (TT = 2) pay where the release always reaches the non-miner defender no
 // later than the defender block (dmax <= delta: the gym's gamma <= .5 networks), so that a
-// verification almost never rolls back; they need the spill buffer to hold a checkpoint and
-// release indices that fit a queue entry
+// verification almost never sends an episode to the second pass; they need release indices
+// that fit a list entry and the spill buffer to hold the second pass's list
 #ifndef CPR_DEFER_RACES
-#define CPR_DEFER_RACES 0
+#define CPR_DEFER_RACES 1
 #endif
-static bool deferred_races_ok(const NakParams& P) {
-  return CPR_DEFER_RACES && P.dmax <= P.delta && 8 * (int64_t)P.cap >= 16 * CK_QUADS &&
-         P.cap <= 4096;
+static bool deferred_races_ok(const NakParams& P, int64_t n_eps, int64_t lanes) {
+  return CPR_DEFER_RACES && P.dmax <= P.delta && P.cap <= 4096 &&
+         (double)lanes * P.cap > (double)n_eps + 1.0;
 }
+using ListFn = void (*)(NakParams, ListSource, int64_t, int64_t, double*, uint8_t*,
+                        cpr_episode_record*, cpr_summary*, int64_t*, uint32_t*, uint32_t, int64_t);
 template <int POL>
-static RunFn gym_run_fn(const NakParams& P, bool recs) {
+static RunFn gym_run_fn(const NakParams& P, bool recs, bool defer, ListFn* second) {
   if (recs) return k_run_episodes<CPR_MODE_GYM, SeedSource, POL, 1, -1>;
   if (!P.arrive) return k_run_episodes<CPR_MODE_GYM, SeedSource, POL, 0, 0>;
   if (P.d != 2) return k_run_episodes<CPR_MODE_GYM, SeedSource, POL, 0, 1>;
-  return deferred_races_ok(P) ? k_run_episodes<CPR_MODE_GYM, SeedSource, POL, 0, 1, 2>
-                              : k_run_episodes<CPR_MODE_GYM, SeedSource, POL, 0, 1, 1>;
+  if (!defer) return k_run_episodes<CPR_MODE_GYM, SeedSource, POL, 0, 1, 1>;
+  if (second) *second = k_run_episodes<CPR_MODE_GYM, ListSource, POL, 0, 1, 1>;
+  return k_run_episodes<CPR_MODE_GYM, SeedSource, POL, 0, 1, 2>;
 }
-static RunFn run_fn(const NakParams& P, int32_t mode, bool recs) {
+// second: set to the eager second pass when the launch defers its races (else untouched)
+static RunFn run_fn(const NakParams& P, int32_t mode, bool recs, bool defer = false,
+                    ListFn* second = nullptr) {
   if (mode != CPR_MODE_GYM) return k_run_episodes<CPR_MODE_LOOP, SeedSource, -1>;
   if (P.abstract_g) return k_run_episodes<CPR_MODE_GYM, SeedSource, -1>;
   switch (P.policy) {
-    case P_HONEST: return gym_run_fn<P_HONEST>(P, recs);
-    case P_SIMPLE: return gym_run_fn<P_SIMPLE>(P, recs);
-    case P_ES2014: return gym_run_fn<P_ES2014>(P, recs);
-    case P_SM1: return gym_run_fn<P_SM1>(P, recs);
+    case P_HONEST: return gym_run_fn<P_HONEST>(P, recs, defer, second);
+    case P_SIMPLE: return gym_run_fn<P_SIMPLE>(P, recs, defer, second);
+    case P_ES2014: return gym_run_fn<P_ES2014>(P, recs, defer, second);
+    case P_SM1: return gym_run_fn<P_SM1>(P, recs, defer, second);
     default: return k_run_episodes<CPR_MODE_GYM, SeedSource, -1>;
   }
 }
@@ -503,9 +513,24 @@ hipError_t launch_run_episodes(const NakParams& P, uint64_t seed, uint64_t first
                                uint32_t launch_id, int64_t redo_cap, hipStream_t st) {
   const unsigned blocks = (unsigned)(lanes / kBlock);
   const SeedSource src{seed, first};
-  hipLaunchKernelGGL(run_fn(P, mode, recs != nullptr), dim3(blocks), dim3(kBlock), 0, st, P, src,
-                     n_eps, activations, spill, replay, recs, sum, redo, redo_n, launch_id,
-                     redo_cap);
+  ListFn second = nullptr;
+  const RunFn fn = run_fn(P, mode, recs != nullptr, deferred_races_ok(P, n_eps, lanes), &second);
+  // deferred races: the spill buffer (no block times in these kernels) holds the list of
+  // episodes for the eager second pass, its count first
+  if (second) {
+    const hipError_t er = hipMemsetAsync(spill, 0, sizeof(int64_t), st);
+    if (er != hipSuccess) return er;
+  }
+  hipLaunchKernelGGL(fn, dim3(blocks), dim3(kBlock), 0, st, P, src, n_eps, activations, spill,
+                     replay, recs, sum, redo, redo_n, launch_id, redo_cap);
+  if (second) {
+    // a few episodes in a hundred at most: a quarter of the grid runs them in one round
+    const ListSource ls{src, reinterpret_cast<const uint32_t*>(spill),
+                        reinterpret_cast<const int64_t*>(spill) + 1};
+    const unsigned b2 = blocks / 4 > 0 ? blocks / 4 : 1;
+    hipLaunchKernelGGL(second, dim3(b2), dim3(kBlock), 0, st, P, ls, n_eps, activations, spill,
+                       replay, recs, sum, redo, redo_n, launch_id, redo_cap);
+  }
   return hipGetLastError();
 }
 

@@ -42,7 +42,10 @@ enum : uint32_t {
   ST_OVERLAP = 2u,
   ST_DEEP_FORK = 4u,
   ST_TIE_UNRESOLVED = 8u,
-  ST_STALE_TIME = 16u
+  ST_STALE_TIME = 16u,
+  // internal (never output): a deferred race went otherwise than assumed; the episode is
+  // listed and run again with the races decided eagerly (k_run_episodes, TT = 2)
+  ST_RACE_REDO = 1u << 20
 };
 
 constexpr int32_t RING = 16;   // private-chain slots kept in the ring
@@ -80,25 +83,20 @@ struct LaneMem {
   bool times = true;
   // deferred races (NakLane::resolve<.., TT = 2>, enqueue_race, verify_races): the wave's
   // dense list of unverified races (rq_cap entries, shared by its lanes), the wave's
-  // rollback flags and episode words (the keyed stream's e0, e1: a race is verified on
-  // its owner's stream), one and two per lane, this lane's index in the wave, and the
-  // lane's checkpoint, quad q (16 bytes) at ck[q * ck_stride]
+  // outcome flags and episode words (the keyed stream's e0, e1: a race is verified on its
+  // owner's stream), one and two per lane, and this lane's index in the wave
   uint4* rq = nullptr;
   int32_t rq_cap = 0;
   int32_t* rflag = nullptr;
   uint32_t* rep = nullptr;
   int32_t lane = 0;
   int32_t wave = 1;  // lanes that share the list (WAVE in the kernels; the host tests emulate more)
-  uint4* ck = nullptr;
-  int64_t ck_stride = 0;
 };
 
 // deferred races: queue entries per lane of a wave (the list is the wave's: 64 times this)
 constexpr int32_t RQ_LANE = 6;
-// checkpoint words of a NakLane without block times (NakLane::pack / unpack), stored as
-// CK_QUADS 16-byte quads (NakLane::save / load)
+// words of a NakLane without block times (NakLane::pack, the host tests' state comparison)
 constexpr int32_t CK_WORDS = 38;
-constexpr int32_t CK_QUADS = (CK_WORDS + 3) / 4;
 
 // wave primitives of the deferred races (a wave of one lane on the host)
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -479,7 +477,7 @@ struct NakLane {
   }
 
   // the lane's state without block times (the summary-only kernels' whole state) as
-  // CK_WORDS words (constant indices: the words stay in registers)
+  // CK_WORDS words
   __host__ __device__ inline CPR_AI void pack(uint32_t* c) const {
     int32_t f = 0;
     auto w = [&](uint32_t x) { c[f++] = x; };
@@ -490,40 +488,6 @@ struct NakLane {
     wb(p0); wb(pub); wb(D); wb(A); wb(b);
     w((uint32_t)onA); w((uint32_t)(onA >> 32)); w((uint32_t)lca_da); w((uint32_t)w_hasb);
     wd(w_bound);
-  }
-  __host__ __device__ inline CPR_AI void unpack(const uint32_t* c) {
-    int32_t f = 0;
-    auto r = [&]() { return c[f++]; };
-    auto rd = [&]() { const uint64_t lo = r(); return dbits(lo | ((uint64_t)r() << 32)); };
-    auto rb = [&](BRef& x) { x.h = (int32_t)r(); x.ra = (int32_t)r(); x.k = (int32_t)r(); x.fork = (int32_t)r(); x.tm = 0.0; };
-    t = rd(); k = (int32_t)r(); n = (int32_t)r(); rel = (int32_t)r(); n_ba = (int32_t)r();
-    pend = (int32_t)r(); wminer = (int32_t)r(); event = (int32_t)r(); rlo = (int32_t)r();
-    rhi = (int32_t)r(); status = r();
-    rb(p0); rb(pub); rb(D); rb(A); rb(b);
-    const uint64_t lo = r();
-    onA = lo | ((uint64_t)r() << 32);
-    lca_da = (int32_t)r(); w_hasb = (int32_t)r();
-    w_bound = rd();
-    rw = 0u;
-  }
-  // the checkpoint: the packed words as quads, quad q at c[q * s] (one 16-byte store each)
-  __host__ __device__ inline CPR_AI void save(uint4* c, int64_t s) const {
-    uint32_t w[CK_QUADS * 4];
-    pack(w);
-    for (int32_t i = CK_WORDS; i < CK_QUADS * 4; ++i) w[i] = 0u;
-    for (int32_t q = 0; q < CK_QUADS; ++q) {
-      uint4 v;
-      v.x = w[4 * q]; v.y = w[4 * q + 1]; v.z = w[4 * q + 2]; v.w = w[4 * q + 3];
-      c[q * s] = v;
-    }
-  }
-  __host__ __device__ inline CPR_AI void load(const uint4* c, int64_t s) {
-    uint32_t w[CK_QUADS * 4];
-    for (int32_t q = 0; q < CK_QUADS; ++q) {
-      const uint4 v = c[q * s];
-      w[4 * q] = v.x; w[4 * q + 1] = v.y; w[4 * q + 2] = v.z; w[4 * q + 3] = v.w;
-    }
-    unpack(w);
   }
 
   // latest finite arrival of the window resolved last (exact; only evaluated when the next
@@ -665,7 +629,7 @@ struct NakLane {
   // reaches the non-miner defender no later than the defender block, so the race's outcome
   // is decided, the release first, unless the two arrive at the same fp instant. The race is
   // taken as decided and noted (rw) for enqueue_race; verify_races checks the wave's list in
-  // batches and rolls a lane back to its checkpoint when a tie decided otherwise.
+  // batches and flags the episode for an eager re-run when a tie decided otherwise.
   template <class St, int AG = -1, int TT = 0>
   __host__ __device__ inline CPR_AI void resolve(const NakParams& P, const St& S, const LaneMem& M) {
     const bool released = rhi >= rlo && P.arrive;
@@ -799,12 +763,11 @@ __host__ __device__ inline CPR_AI bool races_due(const NakLane& L, const LaneMem
 
 // TT = 2: verifies the wave's deferred races, lane i taking entries i, i + 64, ... A race
 // whose release does not strictly precede the defender block at the non-miner defender (a
-// same-instant tie) was decided wrongly or by the queue order: its owner lane then returns
-// to its checkpoint and runs again, eagerly (resolve<TT = 1>), up to where it was
-// (tests/native/defer_vs_eager.cpp compares the two on the host, rollbacks forced by
-// dmax > delta included). Every draw is keyed by the activation count, so the re-run is
-// the same episode. The checkpoint then moves here.
-// in three phases, each over the whole wave (the host tests emulate a wave phase by phase):
+// same-instant tie) was decided wrongly or by the queue order. A tie the closed-form rule
+// (resolve<.., 1>) decides as assumed only marks the episode (ST_TIE); anything else flags
+// it (ST_RACE_REDO): the kernel lists it, and a second pass runs it again with every race
+// decided eagerly (tests/native/defer_vs_eager.cpp compares the two on the host).
+// In three phases, each over the whole wave (the host tests emulate a wave phase by phase):
 // publish the lane's episode; check entries lane, lane + wave, ...; settle the own flag
 template <class St>
 __host__ __device__ inline CPR_AI void races_publish(const St& S, const LaneMem& M) {
@@ -832,40 +795,28 @@ __host__ __device__ inline CPR_AI void races_check(const NakLane& L, const NakPa
     if (!(v < tb)) {
       // the release did not arrive first: a same-instant tie whose closed-form rule
       // (resolve<.., 1>) agrees with the assumed outcome only marks the episode (1);
-      // anything else rolls the owner back (2)
+      // anything else has it run again (2)
       const bool kept = v == tb && rlo == rhi &&
                         tie_table_d2(P, so, (int32_t)(e.w & 3u), t, (int32_t)e.z) != 0ull;
       flag_or(&M.rflag[owner], kept ? 1 : 2);
     }
   }
 }
-template <int POL, class St>
-__host__ __device__ inline CPR_AI void races_settle(NakLane& L, const NakParams& P, const St& S,
-                                                   const LaneMem& M) {
+__host__ __device__ inline CPR_AI void races_settle(NakLane& L, const LaneMem& M) {
   const int32_t fl = M.rflag[M.lane];
   M.rflag[M.lane] = 0;
   L.qn = 0;
-  if (fl & 1) L.status |= ST_TIE;
-  if (fl & 2) {
-    const int32_t k_now = L.k;
-    L.load(M.ck, M.ck_stride);
-    while (L.k < k_now) {
-      const NakLane::Draw dr = L.draw(P, S);
-      L.apply(L.policy_action<POL>(P));
-      L.resolve<St, POL >= 0 ? 0 : -1, 1>(P, S, M);
-      L.activate(P, S, M, dr);
-    }
-  }
-  L.save(M.ck, M.ck_stride);
+  L.status |= (fl & 1) ? ST_TIE : 0u;
+  L.status |= (fl & 2) ? ST_RACE_REDO : 0u;
 }
-template <int POL, class St>
+template <class St>
 __host__ __device__ inline CPR_AI void verify_races(NakLane& L, const NakParams& P, const St& S,
                                                    const LaneMem& M) {
   races_publish(S, M);
   wave_lds_order();
   races_check(L, P, S, M);
   wave_lds_order();
-  races_settle<POL>(L, P, S, M);
+  races_settle(L, M);
 }
 
 // miner of activation index ka (for head_miner of the record)

@@ -144,9 +144,27 @@ __device__ inline Stream make_stream(uint64_t seed, uint64_t ep) {
 // Where a fused episode kernel gets the draws of its e-th episode: the keyed stream of
 // episode first + e (cpr_run_episodes), or episode e of a device copy of a cpr_trace
 // (cpr_replay). missed() is the status bit a lane adds to its record.
+// size(n): the episodes a launch of n runs; index(e): the launch-relative index of its e-th
 struct SeedSource {
   uint64_t seed, first;
   __device__ inline Stream at(int64_t e) const { return make_stream(seed, first + (uint64_t)e); }
+  __device__ inline int64_t size(int64_t n) const { return n; }
+  __device__ inline int64_t index(int64_t e) const { return e; }
+  __device__ static inline uint32_t missed(const Stream&) { return 0u; }
+};
+
+// the episodes a deferred-race launch (k_run_episodes, TT = 2) handed to its eager second
+// pass: count, then launch-relative indices, in that launch's spill buffer
+struct ListSource {
+  SeedSource base;
+  const uint32_t* count;
+  const int64_t* list;
+  __device__ inline Stream at(int64_t i) const { return base.at(list[i]); }
+  __device__ inline int64_t size(int64_t n) const {
+    const int64_t c = (int64_t)*count;
+    return c < n ? c : n;
+  }
+  __device__ inline int64_t index(int64_t i) const { return list[i]; }
   __device__ static inline uint32_t missed(const Stream&) { return 0u; }
 };
 
@@ -173,6 +191,8 @@ struct TraceSource {
     S.miss = 0u;
     return S;
   }
+  __device__ inline int64_t size(int64_t n) const { return n; }
+  __device__ inline int64_t index(int64_t e) const { return e; }
   __device__ static inline uint32_t missed(const TraceStream& S) {
     return S.miss ? (uint32_t)CPR_ST_TRACE_MISS : 0u;
   }

@@ -3,9 +3,11 @@
 // eager closed form (resolve<.., TT = 1>) on the host: the same episodes, with the gym loop
 // of k_run_episodes (kernels.hip run_gym, as a wave of one lane: the race list is the
 // lane's own, verified when full; list sizes 6 and 64), must end in the same lane state
-// word for word (NakLane::save) and the same head.
-// Configurations with dmax > delta make races go the other way often, so the rollback to the
-// checkpoint and the eager re-run are exercised; a tiny delta makes same-instant ties common.
+// word for word (NakLane::pack) and the same head, unless the verification flagged the
+// episode for the eager second pass (ST_RACE_REDO; the kernel then discards the deferred
+// run), which it must do exactly when a race went otherwise than assumed.
+// Configurations with dmax > delta make races go the other way often, so the flagging is
+// exercised; a tiny delta makes same-instant ties common.
 // Prints one JSON summary line; exit code 1 on any difference.
 #include <cmath>
 #include <cstdio>
@@ -31,12 +33,11 @@ struct Run {
 
 struct Deferred {
   std::vector<uint4> rq;
-  std::vector<uint4> ck;
   int32_t flag = 0;
   uint32_t ep[2] = {0u, 0u};
   Deferred(const Deferred&) = delete;
   LaneMem M;
-  Deferred(const NakParams& P, int32_t cap) : rq(cap), ck(CK_QUADS) {
+  Deferred(const NakParams& P, int32_t cap) : rq(cap) {
     M.times = false;
     M.cap = P.cap;
     M.rq = rq.data();
@@ -44,8 +45,6 @@ struct Deferred {
     M.rflag = &flag;
     M.rep = ep;
     M.lane = 0;
-    M.ck = ck.data();
-    M.ck_stride = 1;
   }
 };
 
@@ -57,7 +56,6 @@ static Run run(const NakParams& P, const Stream& S, int32_t cap) {
   NakLane L;
   L.init();
   L.activate(P, S, M);
-  if (TT == 2) L.save(M.ck, M.ck_stride);
   for (int64_t s = 0; s < P.max_steps; ++s) {
     const NakLane::Draw dr = L.draw(P, S);
     L.apply(L.policy_action<POL>(P));
@@ -67,21 +65,20 @@ static Run run(const NakParams& P, const Stream& S, int32_t cap) {
     r.races += L.qn - q0;
     L.activate(P, S, M, dr);
     if (TT == 2 && races_due(L, M)) {
-      verify_races<POL>(L, P, S, M);
+      verify_races(L, P, S, M);
       ++r.drains;
     }
   }
-  if (TT == 2) verify_races<POL>(L, P, S, M);
-  std::vector<uint32_t> w(CK_QUADS * 4);
+  if (TT == 2) verify_races(L, P, S, M);
+  std::vector<uint32_t> w(CK_WORDS);
   L.pack(w.data());
-  w.resize(CK_WORDS);
   r.words = w;
   r.head = L.head(P, M);
   return r;
 }
 
-// verifications counted by outcome: a rollback (a race the release did not win, or a tie the
-// closed-form rule decides otherwise) or a tie kept as assumed
+// verifications counted by outcome: a redo flag (a race the release did not win, or a tie
+// the closed-form rule decides otherwise) or a tie kept as assumed
 template <int POL>
 static void count_outcomes(const NakParams& P, const Stream& S, int32_t cap, long* rollbacks,
                            long* kept) {
@@ -90,13 +87,12 @@ static void count_outcomes(const NakParams& P, const Stream& S, int32_t cap, lon
   NakLane L;
   L.init();
   L.activate(P, S, M);
-  L.save(M.ck, M.ck_stride);
   auto verify = [&]() {
     races_publish(S, M);
     races_check(L, P, S, M);
     *rollbacks += (D.flag & 2) ? 1 : 0;
     *kept += D.flag == 1 ? 1 : 0;
-    races_settle<POL>(L, P, S, M);
+    races_settle(L, M);
   };
   for (int64_t s = 0; s < P.max_steps; ++s) {
     const NakLane::Draw dr = L.draw(P, S);
@@ -118,7 +114,6 @@ static int run_wave(const NakParams& P, uint64_t ep0, int W, int32_t per_lane, l
   std::vector<uint4> rq(W * per_lane);
   std::vector<int32_t> flag(W, 0);
   std::vector<uint32_t> rep(2 * W);
-  std::vector<std::vector<uint4>> ck(W, std::vector<uint4>(CK_QUADS));
   std::vector<LaneMem> M(W);
   std::vector<Stream> S(W);
   std::vector<NakLane> L(W);
@@ -133,16 +128,13 @@ static int run_wave(const NakParams& P, uint64_t ep0, int W, int32_t per_lane, l
     M[i].rep = rep.data();
     M[i].lane = i;
     M[i].wave = W;
-    M[i].ck = ck[i].data();
-    M[i].ck_stride = 1;
     L[i].init();
     L[i].activate(P, S[i], M[i]);
-    L[i].save(M[i].ck, 1);
   }
   auto drain = [&]() {
     for (int i = 0; i < W; ++i) races_publish(S[i], M[i]);
     for (int i = 0; i < W; ++i) races_check(L[i], P, S[i], M[i]);
-    for (int i = 0; i < W; ++i) races_settle<POL>(L[i], P, S[i], M[i]);
+    for (int i = 0; i < W; ++i) races_settle(L[i], M[i]);
     ++*drains;
   };
   std::vector<NakLane::Draw> dr(W);
@@ -165,10 +157,10 @@ static int run_wave(const NakParams& P, uint64_t ep0, int W, int32_t per_lane, l
   drain();
   int bad = 0;
   for (int i = 0; i < W; ++i) {
+    if (L[i].status & ST_RACE_REDO) continue;  // the eager second pass runs it
     const Run a = run<POL, 1>(P, S[i], per_lane);
-    std::vector<uint32_t> w(CK_QUADS * 4);
+    std::vector<uint32_t> w(CK_WORDS);
     L[i].pack(w.data());
-    w.resize(CK_WORDS);
     bad += w != a.words ? 1 : 0;
   }
   return bad;
@@ -176,7 +168,7 @@ static int run_wave(const NakParams& P, uint64_t ep0, int W, int32_t per_lane, l
 
 template <int POL>
 static bool compare(const Cfg& cf, uint64_t ep, long* races, long* drains, long* rollbacks,
-                    long* kept, long* ties, long* unresolved) {
+                    long* kept, long* ties, long* unresolved, long* redo) {
   NakParams P{};
   P.t_att = oracle::alpha_threshold(cf.alpha);
   P.d = 2;
@@ -200,6 +192,10 @@ static bool compare(const Cfg& cf, uint64_t ep, long* races, long* drains, long*
   const uint32_t st = a.words[11];  // status: after t (2 words) and nine counters
   *ties += (st & ST_TIE) ? 1 : 0;
   *unresolved += (st & ST_TIE_UNRESOLVED) ? 1 : 0;
+  if (b.words[11] & ST_RACE_REDO) {  // the kernel discards this run; the eager pass redoes it
+    ++*redo;
+    return true;
+  }
   if (a.words != b.words || a.head.h != b.head.h || a.head.ra != b.head.ra) {
     for (int i = 0; i < CK_WORDS; ++i)
       if (a.words[i] != b.words[i]) {
@@ -218,23 +214,26 @@ int main(int argc, char** argv) {
   std::vector<Cfg> cfgs;
   for (double a : {0.05, 0.25, 0.33, 0.45, 0.5}) {
     cfgs.push_back(Cfg{a, 1e-9, 1e-9, 0, steps});        // the gym's gamma = .5 network
-    cfgs.push_back(Cfg{a, 1e-9, 0.5e-9 / 0.3, 0, steps});  // gamma = .3: rollbacks
+    cfgs.push_back(Cfg{a, 1e-9, 0.5e-9 / 0.3, 0, steps});  // gamma = .3: many redo flags
     cfgs.push_back(Cfg{a, 1e-13, 1e-13, 0, steps});      // same-instant ties are common
     cfgs.push_back(Cfg{a, 1e-9, 0.3e-9, 0, steps});      // releases always win
   }
   long n = 0, bad = 0, races = 0, drains = 0, rollbacks = 0, kept = 0, ties = 0, unresolved = 0;
-  for (const Cfg& c0 : cfgs)
+  long redo = 0, redo_win = 0;  // episodes flagged; of them in the releases-always-win configs
+  for (size_t c = 0; c < cfgs.size(); ++c)
     for (int pol = 0; pol < 4; ++pol)
       for (int e = 0; e < eps; ++e) {
-        Cfg cf = c0;
+        Cfg cf = cfgs[c];
         cf.policy = pol;
         bool ok = true;
+        const long r0 = redo;
         switch (pol) {
-          case 0: ok = compare<0>(cf, e, &races, &drains, &rollbacks, &kept, &ties, &unresolved); break;
-          case 1: ok = compare<1>(cf, e, &races, &drains, &rollbacks, &kept, &ties, &unresolved); break;
-          case 2: ok = compare<2>(cf, e, &races, &drains, &rollbacks, &kept, &ties, &unresolved); break;
-          default: ok = compare<3>(cf, e, &races, &drains, &rollbacks, &kept, &ties, &unresolved); break;
+          case 0: ok = compare<0>(cf, e, &races, &drains, &rollbacks, &kept, &ties, &unresolved, &redo); break;
+          case 1: ok = compare<1>(cf, e, &races, &drains, &rollbacks, &kept, &ties, &unresolved, &redo); break;
+          case 2: ok = compare<2>(cf, e, &races, &drains, &rollbacks, &kept, &ties, &unresolved, &redo); break;
+          default: ok = compare<3>(cf, e, &races, &drains, &rollbacks, &kept, &ties, &unresolved, &redo); break;
         }
+        if (c % 4 == 3) redo_win += redo - r0;
         ++n;
         bad += ok ? 0 : 1;
       }
@@ -261,8 +260,10 @@ int main(int argc, char** argv) {
     }
   }
   printf("{\"episodes\": %ld, \"mismatches\": %ld, \"races\": %ld, \"drains\": %ld, "
-         "\"rollbacks\": %ld, \"ties_kept\": %ld, \"tie_episodes\": %ld, \"unresolved_episodes\": %ld, "
+         "\"redo_flags\": %ld, \"ties_kept\": %ld, \"tie_episodes\": %ld, \"unresolved_episodes\": %ld, "
+         "\"redo_episodes\": %ld, \"redo_episodes_release_wins\": %ld, "
          "\"wave_episodes\": %ld, \"wave_mismatches\": %ld, \"wave_drains\": %ld}\n",
-         n, bad, races, drains, rollbacks, kept, ties, unresolved, wave_eps, wave_bad, wave_drains);
-  return bad || wave_bad ? 1 : 0;
+         n, bad, races, drains, rollbacks, kept, ties, unresolved, redo, redo_win, wave_eps, wave_bad,
+         wave_drains);
+  return bad || wave_bad || redo_win ? 1 : 0;
 }
