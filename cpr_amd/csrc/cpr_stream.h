@@ -103,6 +103,24 @@ __host__ __device__ inline double cpr_fma(double a, double b, double c) {
 #endif
 }
 
+// fma(a, b, c) for a uniform constant c (the log polynomial's coefficients): on the device
+// always the three-operand v_fma_f64 with c in SGPRs. Left to itself the compiler picks the
+// two-address v_fmac_f64, whose addend is its destination, and copies the loop-invariant
+// coefficient into a fresh VGPR pair before each one (a v_mov per term in the activation
+// loop). Same IEEE fma, so the host and the oracle agree bit for bit.
+#ifndef CPR_FMA_ASM
+#define CPR_FMA_ASM 0
+#endif
+__host__ __device__ inline double cpr_fma_c(double a, double b, double c) {
+#if defined(__HIP_DEVICE_COMPILE__) && CPR_FMA_ASM
+  double r;
+  asm("v_fma_f64 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "s"(c));
+  return r;
+#else
+  return std::fma(a, b, c);
+#endif
+}
+
 // (an LDS copy of the table measured no faster than constant memory: the 6 KB stay in L1)
 __host__ __device__ inline double cpr_log(double x) {
   const double ln2_hi = dbits(0x3fe62e42fee00000ull);  // 32 trailing zeros: e * ln2_hi exact
@@ -115,12 +133,12 @@ __host__ __device__ inline double cpr_log(double x) {
   const LogEnt E = kLogTab[(hi << 7) | (uint32_t)(mant >> 45)];
   const double r = cpr_fma(xr, dbits(E.inv_c), -1.0);
   double q = -0.125;
-  q = cpr_fma(r, q, 1.0 / 7.0);
-  q = cpr_fma(r, q, -1.0 / 6.0);
-  q = cpr_fma(r, q, 0.2);
-  q = cpr_fma(r, q, -0.25);
-  q = cpr_fma(r, q, 1.0 / 3.0);
-  q = cpr_fma(r, q, -0.5);
+  q = cpr_fma_c(r, q, 1.0 / 7.0);
+  q = cpr_fma_c(r, q, -1.0 / 6.0);
+  q = cpr_fma_c(r, q, 0.2);
+  q = cpr_fma_c(r, q, -0.25);
+  q = cpr_fma_c(r, q, 1.0 / 3.0);
+  q = cpr_fma_c(r, q, -0.5);
   const double p = cpr_fma(r * r, q, r);
   const double de = (double)e;
   const double a = cpr_fma(de, ln2_hi, dbits(E.t_hi));

@@ -127,7 +127,10 @@ constexpr uint32_t kInexact = ST_OVERLAP | ST_DEEP_FORK | ST_TIE_UNRESOLVED | ST
 // the race lists take the LDS ring); an episode a race went otherwise in is listed in the
 // spill buffer (count, then episode indices) for the eager second pass (ListSource, TT = 1)
 template <int MODE, class Src, int POL, int REC = 1, int ARR = -1, int TT = 0>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(TT ? 5 : 4))) void k_run_episodes(
+#ifndef CPR_G0_WAVES
+#define CPR_G0_WAVES 4  // the gamma = 0 kernel's minimum waves per SIMD (it reaches 7 unasked)
+#endif
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ARR == 0 ? CPR_G0_WAVES : (TT ? 5 : 4)))) void k_run_episodes(
     NakParams P, Src src, int64_t n_eps, int64_t activations,
     double* spill, uint8_t* replay, cpr_episode_record* recs, cpr_summary* sum,
     int64_t* redo, uint32_t* redo_n, uint32_t launch_id, int64_t redo_cap) {
@@ -524,10 +527,11 @@ hipError_t launch_run_episodes(const NakParams& P, uint64_t seed, uint64_t first
   hipLaunchKernelGGL(fn, dim3(blocks), dim3(kBlock), 0, st, P, src, n_eps, activations, spill,
                      replay, recs, sum, redo, redo_n, launch_id, redo_cap);
   if (second) {
-    // a few episodes in a hundred at most: a quarter of the grid runs them in one round
+    // a few episodes in a hundred: half the grid runs them in one round (more take more
+    // rounds of the same grid-stride loop); blocks without an episode exit at once
     const ListSource ls{src, reinterpret_cast<const uint32_t*>(spill),
                         reinterpret_cast<const int64_t*>(spill) + 1};
-    const unsigned b2 = blocks / 4 > 0 ? blocks / 4 : 1;
+    const unsigned b2 = blocks / 2 > 0 ? blocks / 2 : 1;
     hipLaunchKernelGGL(second, dim3(b2), dim3(kBlock), 0, st, P, ls, n_eps, activations, spill,
                        replay, recs, sum, redo, redo_n, launch_id, redo_cap);
   }

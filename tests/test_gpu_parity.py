@@ -123,6 +123,24 @@ def test_summary_only_kernels_equal_record_kernels(ctx, gamma, policy):
         assert s1.status_tie > 0  # ties occurred and took the closed-form rule
 
 
+@pytest.mark.parametrize("policy", [L.POLICY_EYAL_SIRER_2014, L.POLICY_SAPIRSHTEIN_2016_SM1])
+def test_deferred_races_tie_heavy(ctx, policy):
+    # gamma = .5 defers its races (k_run_episodes TT = 2); a 1e-10 propagation
+    # delay over 2016-step episodes (clock ~1e3, ulp ~1e-13) makes same-instant ties common,
+    # so many episodes are flagged and rerun by the eager second pass, some over several
+    # rounds of its grid: the summary must still equal the record kernel's (heap replay)
+    cfg, keep = device.make_config(alpha=0.4, gamma=0.5, policy=policy, max_steps=2016,
+                                   propagation_delay=1e-10, seed=0x7E5)
+    b = device.Batch(cfg, ctx=ctx, keep=keep)
+    n = 65536
+    s1, _ = b.run(n, first_episode=0, records=True)
+    s0 = b.run(n, first_episode=0)
+    for f in L.Summary.FIELDS:
+        assert getattr(s0, f) == getattr(s1, f), f
+    assert list(s0.hist) == list(s1.hist)
+    assert s1.status_tie > n // 50
+
+
 @pytest.mark.parametrize("alpha,policy,table", [(0.35, L.POLICY_SAPIRSHTEIN_2016_SM1, False),
                                                 (0.5, L.POLICY_SAPIRSHTEIN_2016_SM1, False),
                                                 (0.35, L.POLICY_EYAL_SIRER_2014, False),
