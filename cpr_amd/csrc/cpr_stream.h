@@ -109,7 +109,7 @@ __host__ __device__ inline double cpr_fma(double a, double b, double c) {
 // coefficient into a fresh VGPR pair before each one (a v_mov per term in the activation
 // loop). Same IEEE fma, so the host and the oracle agree bit for bit.
 #ifndef CPR_FMA_ASM
-#define CPR_FMA_ASM 0
+#define CPR_FMA_ASM 1
 #endif
 __host__ __device__ inline double cpr_fma_c(double a, double b, double c) {
 #if defined(__HIP_DEVICE_COMPILE__) && CPR_FMA_ASM

@@ -128,7 +128,7 @@ constexpr uint32_t kInexact = ST_OVERLAP | ST_DEEP_FORK | ST_TIE_UNRESOLVED | ST
 // spill buffer (count, then episode indices) for the eager second pass (ListSource, TT = 1)
 template <int MODE, class Src, int POL, int REC = 1, int ARR = -1, int TT = 0>
 #ifndef CPR_G0_WAVES
-#define CPR_G0_WAVES 4  // the gamma = 0 kernel's minimum waves per SIMD (it reaches 7 unasked)
+#define CPR_G0_WAVES 8  // the gamma = 0 kernel: 61 VGPRs fit 8 waves/SIMD (7 unasked)
 #endif
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ARR == 0 ? CPR_G0_WAVES : (TT ? 5 : 4)))) void k_run_episodes(
     NakParams P, Src src, int64_t n_eps, int64_t activations,

@@ -18,8 +18,10 @@ the variants' results are meaningless; only their kernel times are read.
   nodrain   : cost probe, deferred races never verified (the queue is only emptied)
   nosave    : cost probe, deferred races verified without moving the checkpoint
   rqN       : the deferred races' list with N entries per lane of the wave (RQ_LANE)
-  asmfma    : the log polynomial's fma as v_fma_f64 with SGPR coefficients (CPR_FMA_ASM 1)
-  g0wN      : the gamma = 0 kernel compiled for at least N waves per SIMD (CPR_G0_WAVES)
+  asmfma    : the log polynomial's fma as v_fma_f64 with SGPR coefficients (CPR_FMA_ASM 1,
+              the default since r03n; nofma: CPR_FMA_ASM 0)
+  g0wN      : the gamma = 0 kernel compiled for at least N waves per SIMD (CPR_G0_WAVES,
+              8 by default since r03n)
   *_nock    : cost probe, no checkpoint and no rollback after a verification
   *_nolink  : cost probe, and the verification without its link draws
   *_norb    : cost probe, the checkpoint kept, no rollback code
@@ -123,9 +125,10 @@ def variant(name, rng, log, rev=None):
             assert old2 in lane
             lane = lane.replace(old2, "}", 1)
         (d / "nakamoto_lane.h").write_text(lane)
-    if "asmfma" in name:  # the log polynomial's fma forced to v_fma_f64 (CPR_FMA_ASM)
+    if "asmfma" in name or "nofma" in name:  # the log polynomial's fma (CPR_FMA_ASM)
         st2 = (d / "cpr_stream.h").read_text()
-        (d / "cpr_stream.h").write_text("#define CPR_FMA_ASM 1\n" + st2)
+        flag = 0 if "nofma" in name else 1
+        (d / "cpr_stream.h").write_text(f"#define CPR_FMA_ASM {flag}\n" + st2)
     m8 = re.search(r"g0w(\d+)", name)
     if m8:  # the gamma = 0 kernel's waves-per-SIMD minimum (CPR_G0_WAVES)
         k = (d / "kernels.hip").read_text()
