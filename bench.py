@@ -298,6 +298,68 @@ def pmc_traffic(episodes):
     return None, None, None
 
 
+def _spawn_ranks(n, argv):
+    """`--gpus N` without a launcher (no WORLD_SIZE in the environment): start N fresh rank
+    processes of this script, one per GPU, with the torchrun variables set, as the
+    reference's batch runner forks its own workers (csv_runner.ml:105-131). The parent
+    touches neither torch nor the GPU; the ranks inherit stdout, so rank 0's JSON line is
+    the output. Returns the first non-zero exit status of a rank (the others are ended)."""
+    import signal
+    import socket
+    import subprocess
+
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv,
+                                      env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            c = p.poll()
+            if c is None:
+                continue
+            live.remove(p)
+            if c != 0 and rc == 0:
+                rc = c if c > 0 else 128 - c
+                print(f"bench: rank {procs.index(p)} exited with {c}; stopping the others",
+                      file=sys.stderr)
+                for q in live:  # the exact processes this parent started
+                    q.send_signal(signal.SIGTERM)
+        time.sleep(0.05)
+    return rc
+
+
+def launch_check(args, rank, ws):
+    """--launch-check: the rank/collective skeleton of main() with no GPU work"""
+    from cpr_amd import _lib as L
+    from cpr_amd import parallel
+
+    parallel.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        pass
+    parallel.barrier()
+    dt = parallel.allreduce_max(time.perf_counter() - t0)
+    s = L.Summary()
+    s.episodes = rank + 1
+    tot = parallel.allreduce_summaries([s])[0]
+    if rank == 0:
+        print(json.dumps({"launch_check": True, "value": None, "n_gpus": ws,
+                          "steps": args.steps, "ranks_summed": int(tot.episodes),
+                          "max_dt_s": dt, "backend": args.backend}), flush=True)
+    import torch.distributed as dist
+
+    if dist.is_initialized():
+        dist.destroy_process_group()
+    return 0
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -315,9 +377,17 @@ def main():
     ap.add_argument("--gammas", default=",".join(str(g) for g in GAMMAS),
                     help="sweep gammas (A/B runs; the headline is the default)")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
-                    help="collective backend (nccl = RCCL; gloo only for the one-GPU "
-                         "multi-rank test, tests/test_gpu_distributed.py)")
+                    help="collective backend (nccl = RCCL; gloo for the one-GPU multi-rank "
+                         "test, tests/test_gpu_distributed.py, and the CPU launcher check)")
+    ap.add_argument("--launch-check", action="store_true",
+                    help="CPU check of the rank launch (tests/test_bench_host.py): start the "
+                         "ranks, init the collective, time and all-reduce EMPTY steps without "
+                         "touching a GPU; the line says so and has no value")
     args = ap.parse_args()
+
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # no launcher around us: start the ranks ourselves, before anything touches a GPU
+        sys.exit(_spawn_ranks(args.gpus, sys.argv[1:]))
 
     import torch
 
@@ -325,8 +395,15 @@ def main():
     from cpr_amd import device, parallel
 
     rank, ws, local = parallel.init(args.backend)
-    if ws != args.gpus and rank == 0:
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={ws}", file=sys.stderr)
+    if ws != args.gpus:
+        sys.exit(f"bench: --gpus {args.gpus} but WORLD_SIZE={ws}: every GPU is one rank "
+                 f"(start with --gpus N alone, or under torchrun --nproc-per-node N)")
+    import torch.distributed as dist
+
+    if dist.is_initialized():
+        ws = dist.get_world_size()
+    if args.launch_check:
+        return launch_check(args, rank, ws)
     # one GPU per rank; under gloo several ranks may share one GPU (rank-sharing test)
     gpu = local if args.backend == "nccl" else local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(gpu)

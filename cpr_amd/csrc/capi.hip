@@ -971,12 +971,17 @@ static int run_async(cpr_batch* b, int64_t n, uint64_t first, const TraceSource*
   b->last_lanes = lanes;
   b->last_resident =
       (int64_t)b->ctx->cus * run_episodes_blocks_per_cu(b->P, b->cfg.mode, rec_dev != nullptr) * 256;
-  // spill [lane][cap] f64 mining times | tie-replay scratch [lane]
+  // spill [lane][cap] f64 mining times | tie-replay scratch [lane] | the deferred-race
+  // kernel's second-pass list (1 + n words)
   const size_t o_replay = align256((size_t)lanes * b->P.cap * sizeof(double));
+  const size_t o_list = align256(o_replay + (size_t)lanes * REPLAY_BYTES);
+  const size_t list_bytes = tr ? 0 : (size_t)run_episodes_list_bytes(b->P, b->cfg.mode,
+                                                                      rec_dev != nullptr, n);
   void* pool = nullptr;
-  HIP_TRY(ctx_pool(b->ctx, o_replay + (size_t)lanes * REPLAY_BYTES, &pool));
+  HIP_TRY(ctx_pool(b->ctx, o_list + list_bytes, &pool));
   double* spill = (double*)pool;
   uint8_t* replay = (uint8_t*)pool + o_replay;
+  int64_t* list = list_bytes ? (int64_t*)((uint8_t*)pool + o_list) : nullptr;
   if (!b->ev0) {
     HIP_TRY(hipEventCreate(&b->ev0));
     HIP_TRY(hipEventCreate(&b->ev1));
@@ -1017,9 +1022,8 @@ static int run_async(cpr_batch* b, int64_t n, uint64_t first, const TraceSource*
                                    launch_id, kRerunQueue, b->ctx->stream));
   else
     HIP_TRY(launch_run_episodes(b->P, b->cfg.seed, first, n, b->cfg.mode, b->cfg.activations,
-                                spill, replay,
-                                lanes, rec_dev, sum_dev, redo, redo_n, launch_id, kRerunQueue,
-                                b->ctx->stream));
+                                spill, replay, list, lanes, rec_dev, sum_dev, redo, redo_n,
+                                launch_id, kRerunQueue, b->ctx->stream));
   HIP_TRY(hipEventRecord(b->ev1, b->ctx->stream));
   return CPR_OK;
 }
@@ -1422,7 +1426,7 @@ int cpr_reset(cpr_batch* b, const uint8_t* mask, const uint64_t* eps, double* ob
                             b->bk_slots.p, n, dmask, deps, b->cfg.unit_observation, tabs,
                             b->tab_n, (double*)b->l_obs.p, st));
   else
-    HIP_TRY(launch_reset(b->P, b->cfg.seed, lock_buffers(b), n, dmask, deps,
+    HIP_TRY(launch_reset(b->P, b->NEP, b->cfg.seed, lock_buffers(b), n, dmask, deps,
                          b->cfg.unit_observation, tabs, tabs + b->tab_n, b->tab_n,
                          (double*)b->l_obs.p, st));
   HIP_TRY(hipMemcpyAsync(obs, b->l_obs.p, (size_t)n * ol * sizeof(double), hipMemcpyDeviceToHost, st));

@@ -76,11 +76,15 @@ inline int64_t episode_lane_bytes(const NakParams& P) {
 
 // redo/redo_n (optional, device): flagged episodes are appended to that queue (entries
 // tagged with launch_id, at most redo_cap) instead of accumulated, for launch_nak_exact_rerun
+// list (optional, device, run_episodes_list_bytes): the deferred-race kernel's episodes for
+// its eager second pass; null = races decided eagerly
 hipError_t launch_run_episodes(const NakParams& P, uint64_t seed, uint64_t first, int64_t n_eps,
                                int32_t mode, int64_t activations, double* spill,
-                               uint8_t* replay, int64_t lanes, cpr_episode_record* recs,
-                               cpr_summary* sum, int64_t* redo, uint32_t* redo_n,
-                               uint32_t launch_id, int64_t redo_cap, hipStream_t st);
+                               uint8_t* replay, int64_t* list, int64_t lanes,
+                               cpr_episode_record* recs, cpr_summary* sum, int64_t* redo,
+                               uint32_t* redo_n, uint32_t launch_id, int64_t redo_cap,
+                               hipStream_t st);
+int64_t run_episodes_list_bytes(const NakParams& P, int32_t mode, bool recs, int64_t n_eps);
 // the same fused kernel drawing from a device copy of a cpr_trace (cpr_replay)
 hipError_t launch_replay_episodes(const NakParams& P, const TraceSource& src, int64_t n_eps,
                                   int32_t mode, int64_t activations, double* spill,
@@ -88,9 +92,11 @@ hipError_t launch_replay_episodes(const NakParams& P, const TraceSource& src, in
                                   cpr_episode_record* recs, cpr_summary* sum, int64_t* redo,
                                   uint32_t* redo_n, uint32_t launch_id, int64_t redo_cap,
                                   hipStream_t st);
-hipError_t launch_reset(const NakParams& P, uint64_t seed, const LockBuffers& B, int64_t n,
-                        const uint8_t* mask, const uint64_t* eps, int unit, const double* tab_nn,
-                        const double* tab_sg, int32_t tab_n, double* obs, hipStream_t st);
+// EP: the batch's Ethereum lane in Nakamoto mode (observations of lanes on the exact engine)
+hipError_t launch_reset(const NakParams& P, const eth::EthParams& EP, uint64_t seed,
+                        const LockBuffers& B, int64_t n, const uint8_t* mask, const uint64_t* eps,
+                        int unit, const double* tab_nn, const double* tab_sg, int32_t tab_n,
+                        double* obs, hipStream_t st);
 hipError_t launch_step(const NakParams& P, uint64_t seed, const LockBuffers& B, int64_t n,
                        const int32_t* actions, int unit, const double* tab_nn,
                        const double* tab_sg, int32_t tab_n, const StepBuffers& b,

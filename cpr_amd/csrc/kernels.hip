@@ -124,8 +124,8 @@ constexpr uint32_t kInexact = ST_OVERLAP | ST_DEEP_FORK | ST_TIE_UNRESOLVED | ST
 // TT: 1 = launched for d = 2 only: ties take the closed-form rule (tie_table_d2) instead
 // of the inlined heap replay, whose registers otherwise stay live across the whole loop;
 // 2 = as 1, and the races are deferred and verified in batches (verify_races; REC = 0 only:
-// the race lists take the LDS ring); an episode a race went otherwise in is listed in the
-// spill buffer (count, then episode indices) for the eager second pass (ListSource, TT = 1)
+// the race lists take the LDS ring); an episode a race went otherwise in is listed in
+// `list` (count, then episode indices) for the eager second pass (ListSource, TT = 1)
 template <int MODE, class Src, int POL, int REC = 1, int ARR = -1, int TT = 0>
 #ifndef CPR_G0_WAVES
 #define CPR_G0_WAVES 8  // the gamma = 0 kernel: 61 VGPRs fit 8 waves/SIMD (7 unasked)
@@ -133,7 +133,9 @@ template <int MODE, class Src, int POL, int REC = 1, int ARR = -1, int TT = 0>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ARR == 0 ? CPR_G0_WAVES : (TT ? 5 : 4)))) void k_run_episodes(
     NakParams P, Src src, int64_t n_eps, int64_t activations,
     double* spill, uint8_t* replay, cpr_episode_record* recs, cpr_summary* sum,
-    int64_t* redo, uint32_t* redo_n, uint32_t launch_id, int64_t redo_cap) {
+    int64_t* redo, uint32_t* redo_n, uint32_t launch_id, int64_t redo_cap, int64_t* list) {
+  // the race lists take the LDS ring, which only the summary-only kernels leave free
+  static_assert(TT != 2 || REC == 0, "deferred races need the summary-only kernel");
   if (ARR >= 0) P.arrive = ARR;
   if (TT) P.d = 2;  // launched for two defenders only (gym_run_fn): masks and loops fold
   __shared__ int32_t hist[CPR_HIST_BINS];
@@ -181,9 +183,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ARR == 0
                                          : run_loop<POL>(L, P, S, M, activations);
     if constexpr (TT == 2) {
       if (L.status & ST_RACE_REDO) {
-        // a deferred race went otherwise: the eager pass runs this episode again
-        const uint32_t r = atomicAdd(reinterpret_cast<uint32_t*>(spill), 1u);
-        reinterpret_cast<int64_t*>(spill)[1 + r] = src.index(e);
+        // a deferred race went otherwise: the eager pass runs this episode again (list:
+        // count, then episode indices; room for every episode of the launch)
+        const uint32_t r = atomicAdd(reinterpret_cast<uint32_t*>(list), 1u);
+        list[1 + r] = src.index(e);
         continue;
       }
     }
@@ -277,14 +280,29 @@ __device__ inline void write_obs(const NakLane& L, int unit, const double* tab_n
   write_obs_fields(h, a, d, ev, unit, tab_nn, tab_sg, tab_n, o);
 }
 
-__global__ __launch_bounds__(kBlock) void k_reset(NakParams P, uint64_t seed, LockBuffers B,
-                                                   int64_t n, const uint8_t* mask,
+// a lockstep lane's slot on the exact event engine (k_lock_exact)
+__device__ inline eth::EthMem lock_exact_mem(const eth::EthParams& EP, const LockBuffers& B,
+                                             int32_t slot) {
+  return eth::eth_mem_at(B.emem + (int64_t)slot * B.elane_bytes, EP.cap_b, EP.cap_e, EP.n);
+}
+
+__global__ __launch_bounds__(kBlock) void k_reset(NakParams P, eth::EthParams EP, uint64_t seed,
+                                                   LockBuffers B, int64_t n, const uint8_t* mask,
                                                    const uint64_t* eps, int unit,
                                                    const double* tab_nn, const double* tab_sg,
                                                    int32_t tab_n, double* obs) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   LockLane& LL = ((LockLane*)B.lanes)[i];
+  if (mask != nullptr && !mask[i] && LL.exact > 0) {
+    // a lane left unreset that runs on the exact engine: its observation is the exact
+    // lane's (engine.ml:122-170 returns every env's current observation)
+    eth::EthLane E = ((eth::EthLane*)B.eslots)[LL.exact - 1];
+    const eth::EthObs o = E.observe(EP, lock_exact_mem(EP, B, LL.exact - 1), false);
+    write_obs_fields(o.public_height, o.private_height, o.diff_height, o.event, unit, tab_nn,
+                     tab_sg, tab_n, obs + 4 * i);
+    return;
+  }
   if (mask == nullptr || mask[i]) {
     if (LL.exact > 0) {  // the lane's exact-engine slot goes back to the free stack
       const int32_t t = atomicAdd(B.efree + B.n_slots, 1);
@@ -349,10 +367,6 @@ __global__ __launch_bounds__(kBlock) void k_step(NakParams P, uint64_t seed, Loc
 // simulated again on the exact event engine (Ethereum lane, Nakamoto mode) from its first
 // draw with the actions it was given, and stays there until its next reset; this step's
 // outputs are rewritten from that lane (status: the closed form's bits | EXACT_RERUN)
-__device__ inline eth::EthMem lock_exact_mem(const eth::EthParams& EP, const LockBuffers& B,
-                                             int32_t slot) {
-  return eth::eth_mem_at(B.emem + (int64_t)slot * B.elane_bytes, EP.cap_b, EP.cap_e, EP.n);
-}
 
 __global__ __launch_bounds__(kBlock) void k_lock_exact(eth::EthParams EP, uint64_t seed,
                                                         LockBuffers B, int64_t n,
@@ -472,20 +486,21 @@ __global__ void k_stream_fill(uint64_t seed, uint64_t ep, uint32_t idx0, uint32_
 // bookkeeping) for either kind of network; the flagged abstract-gamma mode, tables and loop
 // tasks run the generic kernel. Template arguments do not change the signature.
 using RunFn = void (*)(NakParams, SeedSource, int64_t, int64_t, double*, uint8_t*,
-                       cpr_episode_record*, cpr_summary*, int64_t*, uint32_t*, uint32_t, int64_t);
+                       cpr_episode_record*, cpr_summary*, int64_t*, uint32_t*, uint32_t, int64_t,
+                       int64_t*);
 // deferred races (TT = 2) pay where the release always reaches the non-miner defender no
 // later than the defender block (dmax <= delta: the gym's gamma <= .5 networks), so that a
 // verification almost never sends an episode to the second pass; they need release indices
-// that fit a list entry and the spill buffer to hold the second pass's list
+// that fit a list entry (the second pass's list has its own buffer, run_episodes_list_bytes)
 #ifndef CPR_DEFER_RACES
 #define CPR_DEFER_RACES 1
 #endif
-static bool deferred_races_ok(const NakParams& P, int64_t n_eps, int64_t lanes) {
-  return CPR_DEFER_RACES && P.dmax <= P.delta && P.cap <= 4096 &&
-         (double)lanes * P.cap > (double)n_eps + 1.0;
+static bool deferred_races_ok(const NakParams& P) {
+  return CPR_DEFER_RACES && P.dmax <= P.delta && P.cap <= 4096;
 }
 using ListFn = void (*)(NakParams, ListSource, int64_t, int64_t, double*, uint8_t*,
-                        cpr_episode_record*, cpr_summary*, int64_t*, uint32_t*, uint32_t, int64_t);
+                        cpr_episode_record*, cpr_summary*, int64_t*, uint32_t*, uint32_t, int64_t,
+                        int64_t*);
 template <int POL>
 static RunFn gym_run_fn(const NakParams& P, bool recs, bool defer, ListFn* second) {
   if (recs) return k_run_episodes<CPR_MODE_GYM, SeedSource, POL, 1, -1>;
@@ -511,31 +526,38 @@ static RunFn run_fn(const NakParams& P, int32_t mode, bool recs, bool defer = fa
 
 hipError_t launch_run_episodes(const NakParams& P, uint64_t seed, uint64_t first, int64_t n_eps,
                                int32_t mode, int64_t activations, double* spill,
-                               uint8_t* replay, int64_t lanes, cpr_episode_record* recs,
-                               cpr_summary* sum, int64_t* redo, uint32_t* redo_n,
-                               uint32_t launch_id, int64_t redo_cap, hipStream_t st) {
+                               uint8_t* replay, int64_t* list, int64_t lanes,
+                               cpr_episode_record* recs, cpr_summary* sum, int64_t* redo,
+                               uint32_t* redo_n, uint32_t launch_id, int64_t redo_cap,
+                               hipStream_t st) {
   const unsigned blocks = (unsigned)(lanes / kBlock);
   const SeedSource src{seed, first};
   ListFn second = nullptr;
-  const RunFn fn = run_fn(P, mode, recs != nullptr, deferred_races_ok(P, n_eps, lanes), &second);
-  // deferred races: the spill buffer (no block times in these kernels) holds the list of
-  // episodes for the eager second pass, its count first
+  const RunFn fn = run_fn(P, mode, recs != nullptr, list != nullptr && deferred_races_ok(P),
+                          &second);
+  // deferred races: `list` (1 + n_eps words) receives the episodes for the eager second
+  // pass, its count first
   if (second) {
-    const hipError_t er = hipMemsetAsync(spill, 0, sizeof(int64_t), st);
+    const hipError_t er = hipMemsetAsync(list, 0, sizeof(int64_t), st);
     if (er != hipSuccess) return er;
   }
   hipLaunchKernelGGL(fn, dim3(blocks), dim3(kBlock), 0, st, P, src, n_eps, activations, spill,
-                     replay, recs, sum, redo, redo_n, launch_id, redo_cap);
+                     replay, recs, sum, redo, redo_n, launch_id, redo_cap, list);
   if (second) {
     // a few episodes in a hundred: half the grid runs them in one round (more take more
     // rounds of the same grid-stride loop); blocks without an episode exit at once
-    const ListSource ls{src, reinterpret_cast<const uint32_t*>(spill),
-                        reinterpret_cast<const int64_t*>(spill) + 1};
+    const ListSource ls{src, reinterpret_cast<const uint32_t*>(list), list + 1};
     const unsigned b2 = blocks / 2 > 0 ? blocks / 2 : 1;
     hipLaunchKernelGGL(second, dim3(b2), dim3(kBlock), 0, st, P, ls, n_eps, activations, spill,
-                       replay, recs, sum, redo, redo_n, launch_id, redo_cap);
+                       replay, recs, sum, redo, redo_n, launch_id, redo_cap, list);
   }
   return hipGetLastError();
+}
+
+// the second pass's list of a launch of n_eps episodes (0: no deferred races for P)
+int64_t run_episodes_list_bytes(const NakParams& P, int32_t mode, bool recs, int64_t n_eps) {
+  if (mode != CPR_MODE_GYM || recs || !deferred_races_ok(P)) return 0;
+  return (n_eps + 1) * (int64_t)sizeof(int64_t);
 }
 
 hipError_t launch_replay_episodes(const NakParams& P, const TraceSource& src, int64_t n_eps,
@@ -547,19 +569,22 @@ hipError_t launch_replay_episodes(const NakParams& P, const TraceSource& src, in
   const unsigned blocks = (unsigned)(lanes / kBlock);
   if (mode == CPR_MODE_GYM)
     hipLaunchKernelGGL((k_run_episodes<CPR_MODE_GYM, TraceSource, -1>), dim3(blocks), dim3(kBlock), 0,
-                       st, P, src, n_eps, activations, spill, replay, recs, sum, redo, redo_n, launch_id, redo_cap);
+                       st, P, src, n_eps, activations, spill, replay, recs, sum, redo, redo_n, launch_id, redo_cap,
+                       nullptr);
   else
     hipLaunchKernelGGL((k_run_episodes<CPR_MODE_LOOP, TraceSource, -1>), dim3(blocks), dim3(kBlock),
-                       0, st, P, src, n_eps, activations, spill, replay, recs, sum, redo, redo_n, launch_id, redo_cap);
+                       0, st, P, src, n_eps, activations, spill, replay, recs, sum, redo, redo_n, launch_id, redo_cap,
+                       nullptr);
   return hipGetLastError();
 }
 
-hipError_t launch_reset(const NakParams& P, uint64_t seed, const LockBuffers& B, int64_t n,
-                        const uint8_t* mask, const uint64_t* eps, int unit, const double* tab_nn,
-                        const double* tab_sg, int32_t tab_n, double* obs, hipStream_t st) {
+hipError_t launch_reset(const NakParams& P, const eth::EthParams& EP, uint64_t seed,
+                        const LockBuffers& B, int64_t n, const uint8_t* mask, const uint64_t* eps,
+                        int unit, const double* tab_nn, const double* tab_sg, int32_t tab_n,
+                        double* obs, hipStream_t st) {
   const unsigned blocks = (unsigned)((n + kBlock - 1) / kBlock);
-  hipLaunchKernelGGL(k_reset, dim3(blocks), dim3(kBlock), 0, st, P, seed, B, n, mask, eps, unit,
-                     tab_nn, tab_sg, tab_n, obs);
+  hipLaunchKernelGGL(k_reset, dim3(blocks), dim3(kBlock), 0, st, P, EP, seed, B, n, mask, eps,
+                     unit, tab_nn, tab_sg, tab_n, obs);
   return hipGetLastError();
 }
 
@@ -609,10 +634,12 @@ hipError_t launch_stream_fill(uint64_t seed, uint64_t ep, uint32_t idx0, uint32_
 
 size_t lock_lane_bytes() { return sizeof(LockLane); }
 
+// occupancy of the instantiation a launch runs (the deferred-race kernel holds more LDS)
 int run_episodes_blocks_per_cu(const NakParams& P, int32_t mode, bool recs) {
   int blocks = 0;
+  ListFn second = nullptr;
   hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
-      &blocks, (const void*)run_fn(P, mode, recs), kBlock, 0);
+      &blocks, (const void*)run_fn(P, mode, recs, deferred_races_ok(P), &second), kBlock, 0);
   if (e != hipSuccess || blocks <= 0) blocks = 2;
   return blocks;
 }

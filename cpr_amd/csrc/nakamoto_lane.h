@@ -777,7 +777,17 @@ __host__ __device__ inline CPR_AI void races_publish(const St& S, const LaneMem&
 template <class St>
 __host__ __device__ inline CPR_AI void races_check(const NakLane& L, const NakParams& P,
                                                   const St& S, const LaneMem& M) {
-  for (int32_t i = M.lane; i < L.qn; i += M.wave) {
+  // the entries are spread over the lanes that are here: in the last grid-stride round of
+  // a launch some lanes of the wave have left the episode loop, and an entry assigned to
+  // one of them would never be checked. (On the host a wave is emulated phase by phase
+  // and every emulated lane takes part: lane / wave as given.)
+  int32_t rank = M.lane, stride = M.wave;
+#if defined(__HIP_DEVICE_COMPILE__)
+  const uint64_t here = wave_ballot(true);
+  rank = lanes_below(here);
+  stride = __builtin_popcountll(here);
+#endif
+  for (int32_t i = rank; i < L.qn; i += stride) {
     const uint4 e = M.rq[i];
     const double t = dbits((uint64_t)e.x | ((uint64_t)e.y << 32));
     const int32_t rlo = (int32_t)((e.w >> 2) & 0xfffu), rhi = (int32_t)((e.w >> 14) & 0xfffu);

@@ -74,3 +74,38 @@ def test_driver_record_shape():
     for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
               "higher_is_better", "scaling", "roofline", "cpu_baseline", "config"):
         assert k in line, k
+
+
+def _bench_cmd(args, env_drop=("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")):
+    import os
+    import subprocess
+
+    env = {k: v for k, v in os.environ.items() if k not in env_drop}
+    env["PYTHONPATH"] = str(ROOT) + os.pathsep + env.get("PYTHONPATH", "")
+    return subprocess.run([sys.executable, str(ROOT / "bench.py")] + args, cwd=str(ROOT),
+                          env=env, capture_output=True, text=True, timeout=300)
+
+
+def test_bench_starts_its_own_ranks():
+    # `bench.py --gpus 4` with no torchrun around it starts 4 rank processes itself (before
+    # anything touches a GPU); the collective sees all of them and rank 0 alone prints
+    p = _bench_cmd(["--gpus", "4", "--backend", "gloo", "--launch-check", "--steps", "3"])
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 4 and d["ranks_summed"] == 1 + 2 + 3 + 4 and d["value"] is None
+
+
+def test_bench_rejects_a_world_size_other_than_gpus():
+    # under a launcher whose WORLD_SIZE disagrees with --gpus the bench stops (it used to
+    # warn and time one rank)
+    import os
+    import subprocess
+
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    env["PYTHONPATH"] = str(ROOT) + os.pathsep + env.get("PYTHONPATH", "")
+    p = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--gpus", "2", "--backend",
+                        "gloo", "--launch-check"], cwd=str(ROOT), env=env, capture_output=True,
+                       text=True, timeout=300)
+    assert p.returncode != 0 and "WORLD_SIZE=1" in p.stderr

@@ -64,3 +64,20 @@ def test_bench_two_ranks_gloo():
     # 20 sweep points x 8192 episodes per rank x 2 ranks x 2 timed steps
     assert round(d["episodes_per_s"] * d["ms_per_step"] * d["steps"] / 1e3) == 20 * 8192 * 2 * 2
     assert d["value"] > 0 and "gloo" in d["config"]["parallelism"]
+
+
+def test_bench_starts_two_ranks_itself():
+    # no torchrun: `bench.py --gpus 2` starts its two ranks itself (both on the box's one
+    # GPU under gloo) and reports the whole job
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    env["PYTHONPATH"] = ROOT + os.pathsep + env.get("PYTHONPATH", "")
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps",
+                        "2", "--warmup", "1", "--episodes", "8192", "--no-cpu", "--backend",
+                        "gloo"], cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stderr[-4000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout[-2000:]
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2
+    assert round(d["episodes_per_s"] * d["ms_per_step"] * d["steps"] / 1e3) == 20 * 8192 * 2 * 2

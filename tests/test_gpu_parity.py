@@ -123,16 +123,19 @@ def test_summary_only_kernels_equal_record_kernels(ctx, gamma, policy):
         assert s1.status_tie > 0  # ties occurred and took the closed-form rule
 
 
+@pytest.mark.parametrize("n", [65536, 65536 + 37])
 @pytest.mark.parametrize("policy", [L.POLICY_EYAL_SIRER_2014, L.POLICY_SAPIRSHTEIN_2016_SM1])
-def test_deferred_races_tie_heavy(ctx, policy):
+def test_deferred_races_tie_heavy(ctx, policy, n):
     # gamma = .5 defers its races (k_run_episodes TT = 2); a 1e-10 propagation
     # delay over 2016-step episodes (clock ~1e3, ulp ~1e-13) makes same-instant ties common,
     # so many episodes are flagged and rerun by the eager second pass, some over several
-    # rounds of its grid: the summary must still equal the record kernel's (heap replay)
+    # rounds of its grid: the summary must still equal the record kernel's (heap replay).
+    # n not a multiple of 64: in the launch's last round part of a wave has left the loop,
+    # and the lanes still there must verify every entry of the wave's list
+    # (nakamoto_lane.h races_check)
     cfg, keep = device.make_config(alpha=0.4, gamma=0.5, policy=policy, max_steps=2016,
                                    propagation_delay=1e-10, seed=0x7E5)
     b = device.Batch(cfg, ctx=ctx, keep=keep)
-    n = 65536
     s1, _ = b.run(n, first_episode=0, records=True)
     s0 = b.run(n, first_episode=0)
     for f in L.Summary.FIELDS:
@@ -291,6 +294,47 @@ def test_lockstep_overlaps_exact_on_event_engine(ctx, policy):
         assert done.all()
         moved += int(((st & L.ST_EXACT_RERUN) != 0).sum())
     assert moved >= n  # most lanes of both rounds took the exact path
+
+
+def test_lockstep_partial_reset_keeps_exact_lanes(ctx):
+    # a masked cpr_reset returns every lane's observation: the reset lanes' fresh ones and
+    # the others' current ones, which for a lane on the exact event engine are that
+    # engine's (kernels.hip k_reset); stepping on afterwards stays equal to the oracle
+    n, T = 64, 120
+    cfg, keep = device.make_config(alpha=0.42, gamma=0.5, max_steps=T, seed=903,
+                                   propagation_delay=0.05, unit_observation=False, n_lanes=n)
+    b = device.Batch(cfg, ctx=ctx, keep=keep)
+    ids = np.arange(n, dtype=np.uint64)
+    b.reset(episode_ids=ids)
+    envs = [O.GymEnv(cfg, episode=int(i)) for i in ids]
+    last = np.array([e.reset() for e in envs])
+
+    def step_all(k):
+        nonlocal last
+        st = None
+        for _ in range(k):
+            acts = np.array([O.nak_policy(L.POLICY_SAPIRSHTEIN_2016_SM1, e.fields())
+                             for e in envs], dtype=np.int32)
+            obs, rew, done, info = b.step(acts)
+            st = info["status"]
+            ref = [e.step(int(acts[i])) for i, e in enumerate(envs)]
+            last = np.array([r[0] for r in ref])
+            assert np.array_equal(obs, last)
+            assert np.array_equal(rew, np.array([r[1] for r in ref]))
+        return st
+
+    st = step_all(T // 2)
+    exact = (st & L.ST_EXACT_RERUN) != 0
+    mask = (np.arange(n) % 2 == 0).astype(np.uint8)
+    assert (exact & (mask == 0)).sum() > 4  # unreset lanes on the exact engine exist
+    new_ids = ids + 1000
+    obs = b.reset(mask=mask, episode_ids=new_ids)
+    for i in np.nonzero(mask)[0]:
+        envs[i] = O.GymEnv(cfg, episode=int(new_ids[i]))
+        last[i] = envs[i].reset()
+    assert np.array_equal(obs, last)
+    assert np.array_equal(b.observe_fields(), np.array([e.fields() for e in envs]))
+    step_all(T // 4)
 
 
 def test_policy_actions_decode(ctx):
