@@ -11,6 +11,7 @@
 #include <vector>
 
 #include "../../include/cpr_hip.h"
+#include "eth_window.h"
 #include "kernels.h"
 
 using namespace cpr;
@@ -877,9 +878,87 @@ static int flush_reruns(cpr_ctx* c) {
   return CPR_OK;
 }
 
+// A launch whose flagged episodes the exact event engine re-runs at the next
+// synchronization point (flush_reruns): its parameters (EP: the Ethereum lane, in Nakamoto
+// mode for the closed-form Nakamoto lane), stream and outputs join the context's table;
+// the kernel appends (launch_id << 40) | (episode << 8) | flags to the queue
+static int register_rerun(cpr_batch* b, const eth::EthParams& EP, int64_t lane_bytes,
+                          uint64_t first, const TraceSource* tr, cpr_episode_record* rec_dev,
+                          cpr_summary* sum_dev, int64_t** redo, uint32_t** redo_n,
+                          uint32_t* launch_id) {
+  cpr_ctx* c = b->ctx;
+  if (c->rlaunch.size() >= kRerunMaxLaunches) {
+    int rc = flush_reruns(c);
+    if (rc) return rc;
+  }
+  if (!c->rq.p) {
+    HIP_TRY(c->rq.ensure((size_t)kRerunQueue * 8 + 64));
+    // launch counter and the cumulative HBM-retry counter (cpr_rerun_hbm_retries)
+    HIP_TRY(hipMemsetAsync((char*)c->rq.p + (size_t)kRerunQueue * 8, 0, 8, c->stream));
+  }
+  RerunLaunch rl;
+  memset(&rl, 0, sizeof(rl));
+  rl.P = EP;
+  rl.P.next = nullptr;
+  rl.seed = b->cfg.seed;
+  rl.first = first;
+  rl.is_trace = tr ? 1 : 0;
+  if (tr) rl.tr = *tr;
+  rl.recs = rec_dev;
+  rl.sum = sum_dev;
+  rl.lane_bytes = lane_bytes;
+  *launch_id = (uint32_t)c->rlaunch.size();
+  c->rlaunch.push_back(rl);
+  *redo = (int64_t*)c->rq.p;
+  *redo_n = (uint32_t*)((char*)c->rq.p + (size_t)kRerunQueue * 8);
+  return CPR_OK;
+}
+
+// The window lane (eth_window.h) takes Ethereum gym episodes on the selfish-mining network
+// whose only limit is max_steps (the lanes of a wave then run equal trip counts);
+// CPR_ETH_WINDOW=0 sends them to the event engine instead (A/B runs)
+static bool eth_window_ok(const cpr_batch* b) {
+  const char* v = getenv("CPR_ETH_WINDOW");
+  return (v == nullptr || atoi(v) != 0) && ethw::win_supported(b->EP) && !(b->EP.max_progress < __builtin_inf()) &&
+         !(b->EP.max_time < __builtin_inf());
+}
+
+static int run_async_ethwin(cpr_batch* b, int64_t n, uint64_t first, cpr_summary* sum_dev,
+                            cpr_episode_record* rec_dev) {
+  const int64_t wbytes = ethw::win_lane_bytes(b->EP.cap_b);
+  const int64_t full = (int64_t)b->ctx->cus * eth_win_blocks_per_cu(rec_dev != nullptr) * 256;
+  const int64_t budget = kLaneBudget / wbytes;
+  int64_t lanes = std::min(full, std::max<int64_t>(256, budget));
+  lanes = std::max<int64_t>(256, (lanes / 256) * 256);
+  // equal rounds of the resident grid (every episode has the same trip count)
+  const int64_t rounds = std::max<int64_t>(1, (n + lanes - 1) / lanes);
+  lanes = std::max<int64_t>(256, std::min(lanes, ((n + rounds - 1) / rounds + 255) / 256 * 256));
+  b->last_lanes = lanes;
+  b->last_resident = full;
+  void* mem = nullptr;
+  HIP_TRY(ctx_pool(b->ctx, (size_t)lanes * (size_t)wbytes, &mem));
+  if (!b->ev0) {
+    HIP_TRY(hipEventCreate(&b->ev0));
+    HIP_TRY(hipEventCreate(&b->ev1));
+  }
+  int64_t* redo = nullptr;
+  uint32_t* redo_n = nullptr;
+  uint32_t launch_id = 0;
+  const int rc = register_rerun(b, b->EP, b->eth_bytes, first, nullptr, rec_dev, sum_dev, &redo,
+                                &redo_n, &launch_id);
+  if (rc) return rc;
+  HIP_TRY(hipEventRecord(b->ev0, b->ctx->stream));
+  HIP_TRY(launch_eth_win_episodes(b->EP, b->cfg.seed, first, n, (uint8_t*)mem, wbytes, lanes,
+                                  rec_dev, sum_dev, redo, redo_n, launch_id, kRerunQueue,
+                                  b->ctx->stream));
+  HIP_TRY(hipEventRecord(b->ev1, b->ctx->stream));
+  return CPR_OK;
+}
+
 // Ethereum lanes: resident capacity bounded by kLaneBudget for the per-lane regions
 static int run_async_eth(cpr_batch* b, int64_t n, uint64_t first, const TraceSource* tr,
                          cpr_summary* sum_dev, cpr_episode_record* rec_dev) {
+  if (!tr && !b->nak_ev && eth_window_ok(b)) return run_async_ethwin(b, n, first, sum_dev, rec_dev);
   const int64_t full = (int64_t)b->ctx->cus * eth_blocks_per_cu() * 256;
   const int64_t budget = kLaneBudget / b->eth_bytes;
   int64_t lanes = std::min(full, std::max<int64_t>(256, budget));
@@ -990,30 +1069,9 @@ static int run_async(cpr_batch* b, int64_t n, uint64_t first, const TraceSource*
   uint32_t* redo_n = nullptr;
   uint32_t launch_id = 0;
   if (b->has_rerun) {
-    cpr_ctx* c = b->ctx;
-    if (c->rlaunch.size() >= kRerunMaxLaunches) {
-      int rc = flush_reruns(c);
-      if (rc) return rc;
-    }
-    if (!c->rq.p) {
-      HIP_TRY(c->rq.ensure((size_t)kRerunQueue * 8 + 64));
-      // launch counter and the cumulative HBM-retry counter (cpr_rerun_hbm_retries)
-      HIP_TRY(hipMemsetAsync((char*)c->rq.p + (size_t)kRerunQueue * 8, 0, 8, c->stream));
-    }
-    RerunLaunch rl;
-    memset(&rl, 0, sizeof(rl));
-    rl.P = b->NEP;
-    rl.seed = b->cfg.seed;
-    rl.first = first;
-    rl.is_trace = tr ? 1 : 0;
-    if (tr) rl.tr = *tr;
-    rl.recs = rec_dev;
-    rl.sum = sum_dev;
-    rl.lane_bytes = b->nak_bytes;
-    launch_id = (uint32_t)c->rlaunch.size();
-    c->rlaunch.push_back(rl);
-    redo = (int64_t*)c->rq.p;
-    redo_n = (uint32_t*)((char*)c->rq.p + (size_t)kRerunQueue * 8);
+    const int rc = register_rerun(b, b->NEP, b->nak_bytes, first, tr, rec_dev, sum_dev, &redo,
+                                  &redo_n, &launch_id);
+    if (rc) return rc;
   }
   HIP_TRY(hipEventRecord(b->ev0, b->ctx->stream));
   if (tr)

@@ -1,0 +1,590 @@
+// Ethereum gym episodes on the gym's selfish-mining network, one activation window at a
+// time: the fast lane of cpr_run_episodes for Ethereum.
+//
+// The exact per-lane event engine (ethereum_lane.h) pushes and pops every event of the
+// reference's queue (simulator.ml:421-508): about 14 per activation with two defenders and
+// 50 with eleven, each a walk of a skew heap in HBM. But on this network (network.ml:61-105:
+// defender -> defender delay delta, defender -> attacker 0, attacker -> defender U(0, dmax))
+// an activation's messages have all arrived before the next activation in all but ~1e-9 of
+// windows, exactly as for Nakamoto (nakamoto_lane.h). At that point every defender holds
+// the same set of blocks (all defender blocks and, when dmax is finite, every block the
+// attacker has released), the attacker holds all of them, and the queue holds the next
+// clock alone. So a window's outcome is a closed-form function of the block DAG:
+//
+//   activation   miner m, clock delay (keyed stream); Honest.puzzle_payload' (uncles from
+//                the visible children of the tip's last six ancestors, ethereum.ml:234-277)
+//                for defender m from its tip, or the agent's payload for the attacker;
+//                append; the attacker's interaction (prepare, ethereum_ssz.ml:325-362)
+//   action       Agent.apply (ethereum_ssz.ml:398-429), the release's closure shared
+//                (simulator.ml:401-419)
+//   deliveries   every defender ends on the first-visible block of maximal height among
+//                its tip, the defender block b (t + delta) and the released top sh (the
+//                latest arrival over sh's closure): update_head keeps strictly higher
+//                blocks (ethereum.ml:279-283). Only a race of equal heights needs link draws.
+//
+// No event queue, no per-node visibility array: visibility at quiescence is a function of
+// the block (miner, released). A same-instant race (fl(t + U_j) == fl(t + delta)) is
+// decided by the queue's order: for a released chain the window is replayed through the
+// skew heap exactly as the Nakamoto lane does (tie_replay, nakamoto_lane.h: the window's
+// events are the same; uncles ride along in payloads only). Everything the closed form
+// cannot vouch for — an activation inside the previous window's deliveries (OVERLAP), a
+// tie on a release that is not a chain or exceeds the replay (TIE_UNRESOLVED), a candidate
+// or frontier overflow (CAPACITY) — flags the episode, and the kernel re-runs it on the
+// exact event engine. Parity: tests/native/ethwin_vs_engine.cpp compares this lane with
+// the event engine step by step on the host; tests/test_gpu_eth.py with the oracle.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "cpr_stream.h"
+#include "ethereum_lane.h"
+#include "nakamoto_lane.h"
+
+#pragma clang fp contract(off)
+
+namespace cpr {
+namespace ethw {
+
+using eth::EthObs;
+using eth::EthParams;
+using eth::Payload;
+
+// window-lane status bits the fused kernel hands to the exact event engine
+constexpr uint32_t W_REDO = ST_OVERLAP | ST_TIE_UNRESOLVED | eth::EST_CAPACITY;
+
+struct WBlock {
+  int32_t serial;
+  int32_t p[3];  // parent, uncles (-1: none)
+  int32_t height, work;
+  int32_t rew_att, rew_def;  // cumulative rewards of the first-parent chain, units of 1/32
+  int32_t child;             // newest block whose first parent this is (-1: none)
+  int32_t sib;               // next older block with the same first parent (-1: none)
+  int16_t miner;             // -1 genesis, 0 attacker, 1..d defenders
+  uint8_t np;                // parents
+  uint8_t rel;               // attacker block shared (V_REL in the attacker's view)
+  int32_t share_k, share_off;  // its release coordinates (keyed link delays)
+  double time;                 // append time (Simulator.timestamp)
+};
+static_assert(sizeof(WBlock) == 64, "WBlock layout");
+
+constexpr int32_t NCAND = eth::NCAND, NQ = eth::NQ, NSTACK = eth::NSTACK;
+// scratch ints: candidates, keys, two frontiers, share stack, closure (share order)
+constexpr int32_t S_CAND = 0, S_KEY = 32, S_QA = 64, S_QB = 96, S_STACK = 128, S_CLOS = 192;
+constexpr int32_t S_INTS = 192 + NSTACK;
+
+struct WinMem {
+  WBlock* blk;     // [cap_b]
+  int32_t* tips;   // [64]: defender j's preferred block at tips[j] (Honest.state)
+  int32_t* scr;    // [S_INTS]
+  ReplayMem replay;  // tie_replay scratch
+};
+
+__host__ __device__ inline int64_t win_lane_bytes(int32_t cap_b) {
+  return eth::align128((int64_t)cap_b * 64) + eth::align128(65 * 4) +
+         eth::align128(S_INTS * 4) + eth::align128(REPLAY_BYTES);
+}
+__host__ __device__ inline WinMem win_mem_at(uint8_t* base, int32_t cap_b) {
+  WinMem M;
+  int64_t o = 0;
+  M.blk = (WBlock*)(base + o);
+  o += eth::align128((int64_t)cap_b * 64);
+  M.tips = (int32_t*)(base + o);
+  o += eth::align128(65 * 4);
+  M.scr = (int32_t*)(base + o);
+  o += eth::align128(S_INTS * 4);
+  M.replay = ReplayMem::at(base + o);
+  return M;
+}
+
+// attacker messages reach the defenders (gamma > 0: dmax finite; gamma = 0: never)
+__host__ __device__ inline bool arrives(const EthParams& P) { return P.dmax < __builtin_inf(); }
+
+// the window lane runs these configurations (else the event engine does): gym episodes on
+// the selfish-mining network, Ethereum proper (not the Nakamoto mode)
+__host__ __device__ inline bool win_supported(const EthParams& P) {
+  return P.net == 0 && P.mode == 0 && !P.nak && P.d >= 2 && P.d <= 63;
+}
+
+struct WinLane {
+  double now;
+  int32_t c_act, newest;
+  uint32_t status;
+  int32_t dead;
+  int64_t steps;
+  // the current window: its defender block (-1: the attacker mined) and miner, the
+  // release shared at its interaction (-1: none) and that release's closure size
+  int32_t wb, wi, sh, nclos;
+  int32_t chain;  // the closure is a first-parent chain (tie_replay applies)
+  // ethereum_ssz agent (BetweenActions + Observable)
+  int32_t pub, priv, pending, own, foreign;
+  int32_t o_pub, o_priv, o_common, o_event;
+
+  __host__ __device__ inline void fail(int32_t why) {
+    status |= eth::EST_CAPACITY;
+    if (!dead) dead = why;
+  }
+  __host__ __device__ inline WBlock& B(const EthParams& P, const WinMem& M, int32_t s) {
+    WBlock& b = M.blk[s & (P.cap_b - 1)];
+    if (b.serial != s) fail(1);
+    return b;
+  }
+  // visibility at quiescence (every message of earlier windows delivered)
+  __host__ __device__ static inline bool def_visible(const EthParams& P, const WBlock& b) {
+    return b.miner != 0 || (b.rel && arrives(P));
+  }
+
+  // Honest.puzzle_payload' (ethereum.ml:234-277) in node `view`'s view: the candidates are
+  // the visible children (via the first parent) of the tip's last six ancestors, not in the
+  // chain, in generation order then newest first — the children lists' order — ordered by
+  // (not own, height) with OCaml's heap sort (Compare.at_most_first, ethereum.ml:269)
+  __host__ __device__ inline Payload payload(const EthParams& P, const WinMem& M, int32_t view,
+                                             int32_t tip, int32_t filter, int32_t f_own,
+                                             int32_t f_foreign) {
+    int32_t* cand = M.scr + S_CAND;
+    int32_t* key = M.scr + S_KEY;
+    int32_t ic[19];  // in-chain set: the tip and the parents of tip .. gen 5
+    int32_t nua[6];
+    int32_t ng = 0, nic = 0;
+    ic[nic++] = tip;
+    {
+      int32_t b = tip;
+      for (int32_t gen = 0; gen < 6; ++gen) {
+        nua[gen] = -2;
+        if (b < 0) continue;
+        const WBlock& x = B(P, M, b);
+        if (x.np == 0) {
+          b = -1;
+          continue;
+        }
+        nua[gen] = x.p[0];
+        ng = gen + 1;
+        for (int32_t i = 0; i < x.np; ++i) ic[nic++] = x.p[i];
+        b = x.p[0];
+      }
+    }
+    int32_t nc = 0;
+    for (int32_t g = 0; g < ng && !dead; ++g) {
+      for (int32_t s = B(P, M, nua[g]).child; s >= 0 && !dead; s = B(P, M, s).sib) {
+        const WBlock& c = B(P, M, s);
+        bool mine, keep;
+        if (view == 0) {  // the attacker sees every block
+          mine = c.miner == 0;
+          keep = filter == eth::F_MINING ? ((f_own && mine) || (f_foreign && !mine))
+                                          : (filter == eth::F_PUBLIC ? (!mine || c.rel) : true);
+        } else {
+          if (!def_visible(P, c)) continue;
+          mine = c.miner == view;
+          keep = true;
+        }
+        if (!keep) continue;
+        bool inchain = false;
+        for (int32_t i = 0; i < nic; ++i) inchain |= ic[i] == s;
+        if (inchain) continue;
+        if (nc >= NCAND) {
+          fail(3);
+          break;
+        }
+        cand[nc] = s;
+        key[nc] = ((mine ? 0 : 1) << 27) | (c.height & 0x7ffffff);
+        ++nc;
+      }
+    }
+    eth::EthLane::ocaml_heap_sort(cand, key, nc);
+    Payload d;
+    const WBlock& t = B(P, M, tip);
+    const int32_t nu = nc < 2 ? nc : 2;
+    d.p[0] = tip;
+    d.p[1] = nu > 0 ? cand[0] : -1;
+    d.p[2] = nu > 1 ? cand[1] : -1;
+    d.np = 1 + nu;
+    d.height = t.height + 1;
+    d.work = t.work + 1 + nu;
+    return d;
+  }
+
+  // simulator.ml:122-136, 377-399 (set_rewards, ethereum.ml:173-197: Constant = whitepaper)
+  __host__ __device__ inline int32_t append(const EthParams& P, const WinMem& M, int32_t node,
+                                            const Payload& d) {
+    WBlock& pb = B(P, M, d.p[0]);
+    int32_t ra = pb.rew_att, rd = pb.rew_def;
+    const int32_t nu = d.np - 1;
+    if (node == 0)
+      ra += 32 + nu;
+    else
+      rd += 32 + nu;
+    for (int32_t i = 1; i < d.np; ++i) {
+      const WBlock& u = B(P, M, d.p[i]);
+      const int32_t amt = P.scheme == 0 ? 30 : 4 * (8 - (d.height - u.height));
+      if (u.miner == 0)
+        ra += amt;
+      else if (u.miner > 0)
+        rd += amt;
+    }
+    const int32_t s = ++newest;
+    WBlock& b = M.blk[s & (P.cap_b - 1)];
+    if (newest >= P.cap_b) fail(1);  // the ring would reuse a live slot
+    b.serial = s;
+    b.p[0] = d.p[0];
+    b.p[1] = d.np > 1 ? d.p[1] : -1;
+    b.p[2] = d.np > 2 ? d.p[2] : -1;
+    b.np = (uint8_t)d.np;
+    b.height = d.height;
+    b.work = d.work;
+    b.miner = (int16_t)node;
+    b.rel = 0;
+    b.rew_att = ra;
+    b.rew_def = rd;
+    b.child = -1;
+    b.sib = pb.child;  // children lists newest first (dag.ml:32)
+    pb.child = s;
+    b.share_k = -1;
+    b.share_off = 0;
+    b.time = now;
+    return s;
+  }
+
+  // Dagtools.common_ancestor (dagtools.ml:102-121) in the attacker's view, which holds
+  // every block: ancestors by descending (height, serial) over all parent edges
+  __host__ __device__ inline void q_insert(int32_t* q, int32_t* nq, int32_t s, int32_t h) {
+    const uint64_t kk = eth::EthLane::ca_key(h, s);
+    for (int32_t j = 0; j < *nq; ++j)
+      if (q[2 * j + 1] == s) return;
+    if (*nq >= NQ / 2) {
+      fail(4);
+      return;
+    }
+    int32_t i = *nq;
+    while (i > 0 && eth::EthLane::ca_key(q[2 * (i - 1)], q[2 * (i - 1) + 1]) < kk) {
+      q[2 * i] = q[2 * (i - 1)];
+      q[2 * i + 1] = q[2 * (i - 1) + 1];
+      --i;
+    }
+    q[2 * i] = h;
+    q[2 * i + 1] = s;
+    ++*nq;
+  }
+  __host__ __device__ inline int32_t q_next(const EthParams& P, const WinMem& M, int32_t* q,
+                                            int32_t* nq) {
+    if (*nq == 0) return -1;
+    const int32_t s = q[1];
+    for (int32_t j = 1; j < *nq; ++j) {
+      q[2 * (j - 1)] = q[2 * j];
+      q[2 * (j - 1) + 1] = q[2 * j + 1];
+    }
+    --*nq;
+    const WBlock& b = B(P, M, s);
+    for (int32_t i = 0; i < b.np; ++i) q_insert(q, nq, b.p[i], B(P, M, b.p[i]).height);
+    return s;
+  }
+  __host__ __device__ inline int32_t common_ancestor(const EthParams& P, const WinMem& M,
+                                                     int32_t a, int32_t b) {
+    if (a == b) return a;
+    int32_t* qa = M.scr + S_QA;
+    int32_t* qb = M.scr + S_QB;
+    int32_t na = 0, nb = 0;
+    q_insert(qa, &na, a, B(P, M, a).height);
+    q_insert(qb, &nb, b, B(P, M, b).height);
+    int32_t x = q_next(P, M, qa, &na);
+    int32_t y = q_next(P, M, qb, &nb);
+    while (x >= 0 && y >= 0 && !dead) {
+      if (x == y) return x;
+      const uint64_t kx = eth::EthLane::ca_key(B(P, M, x).height, x);
+      const uint64_t ky = eth::EthLane::ca_key(B(P, M, y).height, y);
+      if (kx > ky)
+        x = q_next(P, M, qa, &na);
+      else
+        y = q_next(P, M, qb, &nb);
+    }
+    fail(4);
+    return 0;
+  }
+
+  // ---------------------------------------------------------------- agent
+  __host__ __device__ inline int32_t update_head(const EthParams& P, const WinMem& M,
+                                                 int32_t old, int32_t cand) {
+    return B(P, M, cand).height > B(P, M, old).height ? cand : old;
+  }
+  // ethereum_ssz.ml:325-362
+  __host__ __device__ inline void prepare(const EthParams& P, const WinMem& M, uint32_t kind,
+                                          int32_t x) {
+    int32_t p = pub;
+    if (pending >= 0) p = update_head(P, M, p, pending);
+    int32_t q = priv;
+    if (kind == eth::KD_NET) {
+      p = update_head(P, M, p, x);
+      o_event = 1;
+    } else {
+      q = x;
+      o_event = 0;
+    }
+    o_pub = p;
+    o_priv = q;
+    o_common = common_ancestor(P, M, p, q);
+  }
+  // ethereum_ssz.ml:364-396; orphans only when asked
+  __host__ __device__ inline EthObs observe(const EthParams& P, const WinMem& M, bool orphans) {
+    const WBlock& c = B(P, M, o_common);
+    const WBlock& pr = B(P, M, o_priv);
+    const WBlock& pu = B(P, M, o_pub);
+    EthObs o;
+    o.public_height = pu.height - c.height;
+    o.public_work = pu.work - c.work;
+    o.private_height = pr.height - c.height;
+    o.private_work = pr.work - c.work;
+    o.diff_height = o.private_height - o.public_height;
+    o.diff_work = o.private_work - o.public_work;
+    o.event = o_event;
+    o.public_orphans = o.private_orphans_inclusive = o.private_orphans_exclusive = 0;
+    if (orphans) {
+      o.public_orphans = payload(P, M, 0, o_pub, eth::F_PUBLIC, 0, 0).np - 1;
+      o.private_orphans_inclusive = payload(P, M, 0, o_priv, eth::F_MINING, 1, 1).np - 1;
+      o.private_orphans_exclusive = payload(P, M, 0, o_priv, eth::F_MINING, 1, 0).np - 1;
+    }
+    return o;
+  }
+  // ethereum_ssz.ml:398-429; returns the block to share (-1: none)
+  __host__ __device__ inline int32_t apply(const EthParams& P, const WinMem& M, int32_t index) {
+    const int32_t action = index >> 2;
+    auto release_upto = [&](int32_t target) {
+      int32_t b = o_priv;
+      while (!dead) {
+        const WBlock& x = B(P, M, b);
+        if (x.height <= target) break;
+        b = x.p[0];
+      }
+      return b;
+    };
+    int32_t s = -1, np = o_priv;
+    switch (action) {
+      case eth::A_ADOPT_RELEASE:
+        s = o_priv;
+        np = o_pub;
+        break;
+      case eth::A_ADOPT_DISCARD: np = o_pub; break;
+      case eth::A_MATCH: s = release_upto(B(P, M, o_pub).height); break;
+      case eth::A_OVERRIDE: s = release_upto(B(P, M, o_pub).height + 1); break;
+      case eth::A_RELEASE1: s = release_upto(B(P, M, o_common).height + 1); break;
+      default: break;
+    }
+    pub = o_pub;
+    priv = np;
+    pending = s;
+    own = (index >> 1) & 1;
+    foreign = index & 1;
+    return s;
+  }
+
+  // Simulator.handle_action's share (simulator.ml:401-419): the withheld closure of s0 in
+  // the reference's recursive order (parents in order), each with its keyed link
+  // coordinates (activation count, position). The closure is recorded in share order; it
+  // is a chain when each entry's successor is its first parent.
+  __host__ __device__ inline void share(const EthParams& P, const WinMem& M, int32_t s0) {
+    int32_t* st = M.scr + S_STACK;
+    int32_t* clos = M.scr + S_CLOS;
+    int32_t sp = 0, off = 0;
+    st[sp++] = s0;
+    while (sp > 0 && !dead) {
+      const int32_t s = st[--sp];
+      WBlock& b = B(P, M, s);
+      if (b.miner != 0 || b.rel) continue;  // received / released: nothing to share
+      b.rel = 1;
+      b.share_k = c_act;
+      b.share_off = off;
+      clos[off++] = s;
+      if (sp + b.np > NSTACK) {
+        fail(5);
+        return;
+      }
+      for (int32_t i = b.np - 1; i >= 0; --i) st[sp++] = b.p[i];
+    }
+    nclos = off;
+    chain = 1;
+    for (int32_t m = 0; m + 1 < off; ++m) chain &= B(P, M, clos[m]).p[0] == clos[m + 1] ? 1 : 0;
+  }
+
+  // ---------------------------------------------------------------- the window
+  template <class St>
+  __host__ __device__ inline double link_of(const EthParams& P, const St& S, const WBlock& c,
+                                            int32_t j) const {
+    return S.link((uint32_t)c.share_k, (uint32_t)c.share_off, (uint32_t)j, P.dmax);
+  }
+  // the visibility time at defender j of the released top: the latest arrival over its
+  // closure (a block is visible once its parents are, simulator.ml:424-450)
+  template <class St>
+  __host__ __device__ inline double release_visible(const EthParams& P, const St& S,
+                                                    const WinMem& M, int32_t j) {
+    double v = -__builtin_inf();
+    for (int32_t m = 0; m < nclos; ++m) {
+      const double a = now + link_of(P, S, B(P, M, M.scr[S_CLOS + m]), j);
+      v = a > v ? a : v;
+    }
+    return v;
+  }
+
+  // the window's deliveries (simulator.ml:481-508, Honest.handler ethereum.ml:284-297):
+  // every defender ends on the first-visible block of maximal height among its tip, the
+  // defender block b (at now + delta, all but its miner) and the released top sh
+  template <class St>
+  __host__ __device__ inline void deliver(const EthParams& P, const St& S, const WinMem& M) {
+    const bool rel = sh >= 0 && arrives(P);
+    const int32_t hs = rel ? B(P, M, sh).height : -1;
+    const int32_t hb = wb >= 0 ? B(P, M, wb).height : -1;
+    const double tb = now + P.delta;
+    uint64_t tie_mask = 0ull;  // defenders whose race tied
+    bool tied = false;
+    for (int32_t j = 1; j <= P.d; ++j) {
+      const int32_t tj = M.tips[j];
+      const int32_t ht = B(P, M, tj).height;
+      int32_t best = tj, hbest = ht;
+      if (wb >= 0 && j != wi && hb > hbest) {
+        best = wb;
+        hbest = hb;
+      }
+      if (rel && hs > hbest) {
+        best = sh;
+      } else if (rel && hs == hbest && best == wb && j != wi) {
+        // equal heights at a non-miner defender: first visible wins
+        const double v = release_visible(P, S, M, j);
+        if (v < tb) best = sh;
+        if (v == tb) {
+          tied = true;
+          tie_mask |= 1ull << (j - 1);
+        }
+      }
+      M.tips[j] = best;
+    }
+    if (tied) {
+      // same instant at some defender: the skew heap's order decides (tie_replay replays
+      // the window's events, nakamoto_lane.h)
+      status |= ST_TIE;
+      bool ok = false;
+      uint64_t on_top = 0ull;
+      if (chain && nclos <= RMAX) {
+        NakParams NP{};
+        NP.d = P.d;
+        NP.delta = P.delta;
+        NP.dmax = P.dmax;
+        on_top = tie_replay(NP, S, M.replay, wi, now, 1, nclos, B(P, M, sh).share_k, &ok);
+      }
+      if (!ok) {
+        status |= ST_TIE_UNRESOLVED;
+      } else {
+        for (int32_t j = 1; j <= P.d; ++j)
+          if ((tie_mask >> (j - 1)) & 1ull) M.tips[j] = ((on_top >> (j - 1)) & 1ull) ? sh : wb;
+      }
+    }
+  }
+
+  // the next activation (simulator.ml:465-480 + engine.ml:108-121): clock, miner, draft
+  // (Honest.puzzle_payload' or the agent's), append, the attacker's interaction
+  template <class St>
+  __host__ __device__ inline void activate(const EthParams& P, const St& S, const WinMem& M) {
+    int32_t m;
+    const double tn = now + S.act((uint32_t)c_act, P.t_att, P.d, P.ev, &m);
+    // an activation inside the previous window's deliveries: the closed form does not hold
+    double bound = now;  // a zero delay ties the window's own events
+    if (wb >= 0) bound = now + P.delta > bound ? now + P.delta : bound;
+    if (sh >= 0 && arrives(P)) {
+      const double ub = now + (P.dmax - 0.0);
+      bound = ub > bound ? ub : bound;
+    }
+    if (tn <= bound) {
+      double last = now;
+      if (wb >= 0) last = now + P.delta;
+      if (sh >= 0 && arrives(P))
+        for (int32_t j = 1; j <= P.d; ++j) {
+          const double v = release_visible(P, S, M, j);
+          last = v > last ? v : last;
+        }
+      if (tn <= last) status |= ST_OVERLAP;
+    }
+    now = tn;
+    ++c_act;
+    sh = -1;
+    nclos = 0;
+    uint32_t kind;
+    int32_t x;
+    if (m == 0) {
+      const Payload d = payload(P, M, 0, priv, eth::F_MINING, own, foreign);
+      x = append(P, M, 0, d);
+      wb = -1;
+      wi = 0;
+      kind = eth::KD_POW;
+    } else {
+      const Payload d = payload(P, M, m, M.tips[m], eth::F_ALL, 0, 0);
+      x = append(P, M, m, d);
+      M.tips[m] = x;
+      wb = x;
+      wi = m;
+      kind = eth::KD_NET;
+    }
+    prepare(P, M, kind, x);
+  }
+
+  // engine.ml:122-170
+  template <class St>
+  __host__ __device__ inline void gym_reset(const EthParams& P, const St& S, const WinMem& M) {
+    now = 0.0;
+    c_act = 0;
+    newest = 0;
+    status = 0u;
+    dead = 0;
+    steps = 0;
+    wb = sh = -1;
+    wi = 0;
+    nclos = 0;
+    chain = 1;
+    WBlock& r = M.blk[0];
+    r.serial = 0;
+    r.p[0] = r.p[1] = r.p[2] = -1;
+    r.np = 0;
+    r.height = 0;
+    r.work = 0;
+    r.miner = -1;
+    r.rel = 0;
+    r.rew_att = r.rew_def = 0;
+    r.child = r.sib = -1;
+    r.share_k = -1;
+    r.share_off = 0;
+    r.time = 0.0;
+    for (int32_t j = 0; j <= P.d; ++j) M.tips[j] = 0;
+    pub = priv = 0;
+    pending = -1;
+    own = foreign = 1;
+    activate(P, S, M);
+  }
+
+  // winner over [attacker preference; defenders' tips] (ethereum.ml:159-162)
+  __host__ __device__ inline int32_t head(const EthParams& P, const WinMem& M, int32_t att) {
+    int32_t h = att;
+    int32_t hh = B(P, M, att).height;
+    for (int32_t j = 1; j <= P.d; ++j) {
+      const int32_t t = M.tips[j];
+      const int32_t th = B(P, M, t).height;
+      if (th > hh) {
+        h = t;
+        hh = th;
+      }
+    }
+    return h;
+  }
+
+  // engine.ml:176-249: apply, the window's deliveries, the next activation; the head
+  template <class St>
+  __host__ __device__ inline int32_t gym_step(const EthParams& P, const St& S, const WinMem& M,
+                                              int32_t action, bool* done) {
+    sh = apply(P, M, action);
+    if (sh >= 0) share(P, M, sh);
+    ++steps;
+    const int32_t att = priv;
+    deliver(P, S, M);
+    activate(P, S, M);
+    const int32_t hd = head(P, M, att);
+    const double progress = (double)B(P, M, hd).work;
+    *done = dead || !(steps < P.max_steps && progress < P.max_progress && now < P.max_time);
+    return hd;
+  }
+};
+
+}  // namespace ethw
+}  // namespace cpr

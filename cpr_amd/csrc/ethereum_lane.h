@@ -61,6 +61,13 @@ static_assert(sizeof(EBlock) == 64, "EBlock layout");
 #ifndef CPR_HEAP_HOOK
 #define CPR_HEAP_HOOK(op, t)
 #endif
+// host cost studies (tools/eth_cost_study.cpp) count work items by id (CC_* below)
+#ifndef CPR_COST
+#define CPR_COST(id)
+#endif
+enum : int32_t { CC_PUSH = 0, CC_POP = 1, CC_PAYLOAD = 2, CC_SCAN = 3, CC_CA = 4, CC_MDV = 5,
+                 CC_EVENT = 6 /* + event type, 7 types */, CC_SHARE = 13, CC_SORT = 14,
+                 CC_CAND = 15, CC_N = 16 };
 
 struct HNode {
   double t;
@@ -299,6 +306,7 @@ struct EthLane {
     CPR_HEAP_HOOK(0, t);
     int32_t parent = -1, node = hroot;
     for (;;) {
+      CPR_COST(CC_PUSH);
       if (node < 0) {
         const int32_t a = halloc(P, M);
         if (a < 0) return;
@@ -342,6 +350,7 @@ struct EthLane {
     *blk = M.heap[hroot].blk;
     int32_t parent = -1, side = 0, node = hroot;
     for (;;) {
+      CPR_COST(CC_POP);
       const int32_t l = M.heap[node].l, r = M.heap[node].r;
       int32_t repl = -2;
       if (r < 0)
@@ -490,6 +499,7 @@ struct EthLane {
       d.work = t.work + 1;
       return d;
     }
+    CPR_COST(CC_PAYLOAD);
     int32_t* cand = M.scr + SCR_CAND;
     int32_t* key = M.scr + SCR_KEY;
     int32_t* ic = M.scr + SCR_QA;  // in-chain set (tip + parents of tip..gen5), <= 19
@@ -520,6 +530,7 @@ struct EthLane {
     int32_t nc = 0;
     if (ng > 0) {
       for (int32_t s = newest; s > lowest && !dead; --s) {
+        CPR_COST(CC_SCAN);
         const uint8_t vk = V(P, M, s, view) & V_KIND;
         if (vk == V_INV) continue;
         const EBlock& c = B(P, M, s);
@@ -550,6 +561,7 @@ struct EthLane {
           key[pos] = key[pos - 1];
           --pos;
         }
+        CPR_COST(CC_CAND);
         cand[pos] = s;
         // sort key: not own (bit 27), height (27 bits); generation kept in bits 28+
         key[pos] = (g << 28) | ((mine ? 0 : 1) << 27) | (c.height & 0x7ffffff);
@@ -667,6 +679,7 @@ struct EthLane {
   __host__ __device__ inline int32_t q_next(const EthParams& P, const EthMem& M, int32_t* q,
                                             int32_t* nq) {
     if (*nq == 0) return -1;
+    CPR_COST(CC_CA);
     const int32_t s = q[1];
     for (int32_t j = 1; j < *nq; ++j) {
       q[2 * (j - 1)] = q[2 * j];
@@ -736,6 +749,7 @@ struct EthLane {
     st[sp++] = s0;
     while (sp > 0 && !dead) {
       const int32_t s = st[--sp];
+      CPR_COST(CC_SHARE);
       uint8_t& v = V(P, M, s, node);
       if ((v & V_KIND) != V_WH) continue;  // received / released: nothing; invisible: n/a
       v = (uint8_t)((v & ~V_KIND) | V_REL);
@@ -878,6 +892,7 @@ struct EthLane {
                                          uint32_t ev, int32_t s) {
     const uint32_t ty = ev & 7u, kind = (ev >> 3) & 3u;
     const int32_t node = (int32_t)(ev >> 5);
+    CPR_COST(CC_EVENT + (int32_t)ty);
     switch (ty) {
       case EV_MV: {
         uint8_t& v = V(P, M, s, node);
@@ -972,6 +987,7 @@ struct EthLane {
           break;
         }
         for (int32_t c = newest; c > s && !dead; --c) {
+          CPR_COST(CC_MDV);
           if (!(V(P, M, c, node) & V_GOT)) continue;
           const EBlock& cb = B(P, M, c);
           bool child = false;

@@ -137,6 +137,15 @@ hipError_t launch_eth_replay_episodes(const eth::EthParams& P, const TraceSource
                                  cpr_episode_record* recs, cpr_summary* sum, hipStream_t st,
                                    const NodeOut& no = NodeOut());
 int eth_blocks_per_cu();
+// Ethereum gym episodes on the selfish-mining network through the window lane
+// (eth_window.h; ethw::win_supported): mem = lanes x ethw::win_lane_bytes; flagged episodes
+// go to the exact re-run queue (redo / redo_n, entries tagged with launch_id)
+hipError_t launch_eth_win_episodes(const eth::EthParams& P, uint64_t seed, uint64_t first,
+                                   int64_t n_eps, uint8_t* mem, int64_t lane_bytes,
+                                   int64_t lanes, cpr_episode_record* recs, cpr_summary* sum,
+                                   int64_t* redo, uint32_t* redo_n, uint32_t launch_id,
+                                   int64_t redo_cap, hipStream_t st);
+int eth_win_blocks_per_cu(bool recs);
 // Ethereum lockstep lanes: mem = n x lane_bytes; slots = n x eth_slot_bytes()
 hipError_t launch_eth_reset(const eth::EthParams& P, uint64_t seed, uint8_t* mem,
                             int64_t lane_bytes, void* slots, int64_t n, const uint8_t* mask,
@@ -164,7 +173,7 @@ constexpr int64_t kRerunQueue = 1 << 22;       // queue entries per context
 constexpr size_t kRerunMaxLaunches = 1 << 20;  // launches per flush (< 2^23)
 
 struct RerunLaunch {
-  eth::EthParams P;  // the Ethereum lane in Nakamoto mode
+  eth::EthParams P;  // the Ethereum lane in Nakamoto mode, or Ethereum (window-lane episodes)
   uint64_t seed, first;
   int32_t is_trace, _pad;
   TraceSource tr;

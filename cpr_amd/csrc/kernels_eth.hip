@@ -11,6 +11,7 @@
 #include <cstdlib>
 
 #include "../../include/cpr_hip.h"
+#include "eth_window.h"
 #include "ethereum_lane.h"
 #include "kernels.h"
 #include "summary.h"
@@ -153,6 +154,95 @@ __global__ __launch_bounds__(kBlock) CPR_EV_OCC void k_eth_run_episodes(
   block_flush(acc, hist, sum);
 }
 
+// Ethereum gym episodes on the selfish-mining network, a window at a time (eth_window.h):
+// one lane per episode, grid-stride over the launch's episodes, outputs as
+// k_eth_run_episodes. An episode the window lane cannot vouch for (W_REDO) goes to the
+// context's exact re-run queue instead, like the Nakamoto lane's (k_nak_exact_rerun runs it
+// again from its first draw on the event engine at the next synchronization point). Every
+// gym episode has max_steps steps (no progress / time limit: the host routes only those
+// here), so the lanes of a wave run the same number of windows.
+template <int REC>
+__global__ __launch_bounds__(kBlock) void k_eth_win_episodes(
+    eth::EthParams P, SeedSource src, int64_t n_eps, uint8_t* mem, int64_t lane_bytes,
+    cpr_episode_record* recs, cpr_summary* sum, int64_t* redo, uint32_t* redo_n,
+    uint32_t launch_id, int64_t redo_cap) {
+  __shared__ int32_t hist[CPR_HIST_BINS];
+  __shared__ unsigned long long acc_w[13];
+  LdsAcc acc{acc_w};
+  acc.init();
+  if (threadIdx.x < CPR_HIST_BINS) hist[threadIdx.x] = 0;
+  __syncthreads();
+  const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t nthreads = (int64_t)gridDim.x * blockDim.x;
+  const ethw::WinMem M = ethw::win_mem_at(mem + tid * lane_bytes, P.cap_b);
+  if (!REC) recs = nullptr;
+  ethw::WinLane W;
+  for (int64_t e = tid; e < n_eps; e += nthreads) {
+    const Stream S = src.at(e);
+    W.gym_reset(P, S, M);
+    bool done = W.dead != 0;
+    int32_t hd = 0;
+    while (!done) hd = W.gym_step(P, S, M, eth::lane_action(P, W.observe(P, M, false)), &done);
+    uint32_t status = W.status;
+    if (status & ethw::W_REDO) {
+      const uint32_t r = atomicAdd(redo_n, 1u);
+      if ((int64_t)r < redo_cap) {
+        redo[r] = ((int64_t)launch_id << 40) | (e << 8) | (int64_t)(status & 0xffu);
+        continue;
+      }
+      status |= CPR_ST_CAPACITY;  // queue full: the outputs stay, marked invalid
+    }
+    const ethw::WBlock& h = W.B(P, M, hd);
+    const int32_t ra = h.rew_att, rd = h.rew_def;
+    const double rel = (ra + rd) != 0 ? (double)ra / (double)(ra + rd) : 0.0;
+    acc.episode((int64_t)ra << 15, (int64_t)rd << 15, (int64_t)h.work << 20, rel, h.height,
+                W.steps, W.c_act, status, hist);
+    if (REC && recs) {
+      cpr_episode_record r;
+      r.reward_attacker = (double)ra / 32.0;
+      r.reward_defender = (double)rd / 32.0;
+      r.progress = (double)h.work;
+      r.chain_time = h.time;
+      r.sim_time = W.now;
+      r.n_steps = W.steps;
+      r.n_activations = W.c_act;
+      r.head_height = h.height;
+      r.head_miner = h.miner;
+      r.status = status;
+      r.head_work = h.work;
+      recs[e] = r;
+    }
+  }
+  __syncthreads();
+  acc.flush(hist, sum);
+}
+
+using EthWinFn = void (*)(eth::EthParams, SeedSource, int64_t, uint8_t*, int64_t,
+                          cpr_episode_record*, cpr_summary*, int64_t*, uint32_t*, uint32_t,
+                          int64_t);
+static EthWinFn eth_win_fn(bool recs) {
+  return recs ? k_eth_win_episodes<1> : k_eth_win_episodes<0>;
+}
+
+hipError_t launch_eth_win_episodes(const eth::EthParams& P, uint64_t seed, uint64_t first,
+                                   int64_t n_eps, uint8_t* mem, int64_t lane_bytes,
+                                   int64_t lanes, cpr_episode_record* recs, cpr_summary* sum,
+                                   int64_t* redo, uint32_t* redo_n, uint32_t launch_id,
+                                   int64_t redo_cap, hipStream_t st) {
+  hipLaunchKernelGGL(eth_win_fn(recs != nullptr), dim3((unsigned)(lanes / kBlock)), dim3(kBlock),
+                     0, st, P, SeedSource{seed, first}, n_eps, mem, lane_bytes, recs, sum, redo,
+                     redo_n, launch_id, redo_cap);
+  return hipGetLastError();
+}
+
+int eth_win_blocks_per_cu(bool recs) {
+  int blocks = 0;
+  hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
+      &blocks, (const void*)eth_win_fn(recs), kBlock, 0);
+  if (e != hipSuccess || blocks <= 0) blocks = 2;
+  return blocks;
+}
+
 // Exact re-run of the Nakamoto episodes the closed-form lane flagged.
 // Episode kernels queue (launch << 40) | (episode index << 8) | status bits instead of
 // accumulating such an episode; at the next synchronization point this kernel simulates
@@ -176,10 +266,11 @@ __device__ inline int32_t nak_rerun_one(const eth::EthParams& P, const St& S,
   return hd;
 }
 
-__device__ inline void summary_add_episode(cpr_summary* out, int64_t ra, int64_t rd,
-                                           int64_t height, int64_t steps, int64_t acts,
-                                           uint32_t status) {
-  const double rel = (ra + rd) != 0 ? (double)ra / (double)(ra + rd) : 0.0;
+// one episode into a summary with per-episode atomics; rewards and progress in 2^-20
+// fixed point, as acc_episode
+__device__ inline void summary_add_episode(cpr_summary* out, int64_t ra_fx, int64_t rd_fx,
+                                           int64_t prog_fx, double rel, int64_t height,
+                                           int64_t steps, int64_t acts, uint32_t status) {
   auto add = [](int64_t* p, int64_t v) {
     if (v) atomicAdd((unsigned long long*)p, (unsigned long long)v);
   };
@@ -192,9 +283,9 @@ __device__ inline void summary_add_episode(cpr_summary* out, int64_t ra, int64_t
   add(&out->episodes, 1);
   add(&out->steps, steps);
   add(&out->activations, acts);
-  add(&out->reward_attacker_fx, ra << 20);
-  add(&out->reward_defender_fx, rd << 20);
-  add(&out->progress_fx, height << 20);
+  add(&out->reward_attacker_fx, ra_fx);
+  add(&out->reward_defender_fx, rd_fx);
+  add(&out->progress_fx, prog_fx);
   add((int64_t*)&out->rel_revenue_fx, (int64_t)__builtin_rint(rel * 4294967296.0));
   add((int64_t*)&out->rel_revenue_sq_fx, (int64_t)__builtin_rint(rel * rel * 4294967296.0));
   add(&out->orphans, acts - height);
@@ -221,23 +312,28 @@ __device__ inline int32_t nak_rerun_entry(const RerunLaunch& RL, int64_t e,
   return nak_rerun_one(P, make_stream(RL.seed, RL.first + (uint64_t)e), M, L);
 }
 
-// the re-run episode's record and summary contribution (replacing the flagged ones)
+// the re-run episode's record and summary contribution (replacing the flagged ones):
+// Nakamoto episodes of the closed-form lane (P.nak: one reward per block, progress =
+// height) and Ethereum episodes of the window lane (eth_window.h) alike. The flags the
+// re-run resolved (a fast lane's capacity or unresolved tie) leave the status.
 __device__ inline void nak_rerun_finish(const RerunLaunch& RL, int64_t e,
                                         const eth::EthParams& P, const eth::EthMem& M,
                                         eth::EthLane& L, int32_t hd, uint32_t flags) {
-  const uint32_t status = flags | L.status | CPR_ST_EXACT_RERUN;
+  const uint32_t resolved =
+      CPR_ST_DEEP_FORK | CPR_ST_TIE_UNRESOLVED | CPR_ST_STALE_TIME | CPR_ST_CAPACITY;
+  const uint32_t status = (flags & ~(uint32_t)CPR_ST_CAPACITY) | L.status | CPR_ST_EXACT_RERUN;
   const eth::EBlock& h = L.B(P, M, hd);
-  const int32_t ra = h.rew_att / 32, rd = h.rew_def / 32;  // 1 per block
+  const int32_t ra = h.rew_att, rd = h.rew_def;  // units of 1/32
+  const double rel = (ra + rd) != 0 ? (double)ra / (double)(ra + rd) : 0.0;
   const int64_t steps = P.mode == CPR_MODE_GYM ? L.steps : 0;
-  // the summary counts the flags the re-run resolved as OVERLAP / TIE only
-  summary_add_episode(
-      RL.sum, ra, rd, h.height, steps, L.c_act,
-      status & ~(uint32_t)(CPR_ST_DEEP_FORK | CPR_ST_TIE_UNRESOLVED | CPR_ST_STALE_TIME));
+  summary_add_episode(RL.sum, (int64_t)ra << 15, (int64_t)rd << 15, (int64_t)h.work << 20, rel,
+                      h.height, steps, L.c_act,
+                      (flags & ~resolved) | L.status | CPR_ST_EXACT_RERUN);
   if (RL.recs) {
     cpr_episode_record rc;
-    rc.reward_attacker = (double)ra;
-    rc.reward_defender = (double)rd;
-    rc.progress = (double)h.height;
+    rc.reward_attacker = (double)ra / 32.0;
+    rc.reward_defender = (double)rd / 32.0;
+    rc.progress = (double)h.work;
     rc.chain_time = h.time;
     rc.sim_time = P.mode == CPR_MODE_GYM ? L.now : 0.0;
     rc.n_steps = steps;
@@ -245,7 +341,7 @@ __device__ inline void nak_rerun_finish(const RerunLaunch& RL, int64_t e,
     rc.head_height = h.height;
     rc.head_miner = P.mode == CPR_MODE_GYM ? h.miner : -1;
     rc.status = status;
-    rc.head_work = 0;
+    rc.head_work = P.nak ? 0 : h.work;
     RL.recs[e] = rc;
   }
 }

@@ -1,0 +1,193 @@
+// TEST INFRASTRUCTURE ONLY. Differential fuzzer for the Ethereum window lane
+// (cpr_amd/csrc/eth_window.h, compiled here for the host) against the CPU oracle's event-
+// driven restatement (oracle/src/ethereum.cpp GymEthereum), step by step on the same keyed
+// stream: all ten observation fields (the three dry-run uncle selections included) before
+// every action and the step info after it. An episode the lane flags for the exact re-run
+// (W_REDO: overlap, unresolved tie, capacity) stops being compared at that step — the fused
+// kernel re-runs it on the event engine — and is counted; the tie-heavy and overlap-heavy
+// configurations make sure those paths occur.
+// usage: ethwin_vs_oracle [episodes per config] [steps]; one JSON line; exit 1 on mismatch
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../cpr_amd/csrc/eth_window.h"
+#include "../../include/cpr_hip.h"
+#include "../../oracle/src/ethereum.h"
+
+using namespace cpr;
+
+static uint32_t mix(uint64_t a, uint64_t b) {
+  uint64_t x = a * 0x9E3779B97F4A7C15ull ^ (b + 0x632BE59BD9B4E019ull);
+  x ^= x >> 31;
+  x *= 0xD6E8FEB86659FD93ull;
+  x ^= x >> 32;
+  return (uint32_t)x;
+}
+
+struct Cfg {
+  double alpha, gamma;
+  int defenders;
+  int policy;  // 0..4 ethereum_ssz policies, 5 random actions, 6 random biased to release
+  int scheme;
+  int steps;
+  double prop;
+};
+
+struct Counters {
+  long episodes = 0, mismatches = 0, redo = 0, ties = 0, steps = 0, overlaps = 0;
+};
+
+static eth::EthParams params_of(const Cfg& cf) {
+  eth::EthParams P{};
+  P.t_att = oracle::alpha_threshold(cf.alpha);
+  P.d = cf.defenders;
+  P.n = P.d + 1;
+  P.net = 0;
+  P.mode = 0;
+  P.nak = 0;
+  P.policy = cf.policy < 5 ? cf.policy : 0;
+  P.scheme = cf.scheme;
+  P.cap_b = 64;
+  while (P.cap_b < cf.steps + 2) P.cap_b <<= 1;
+  P.ev = 1.0;
+  P.delta = cf.prop;
+  const double dd = cf.defenders;
+  P.dmax = (dd - 1.) / dd * cf.prop / cf.gamma;
+  P.max_steps = cf.steps;
+  P.max_progress = __builtin_inf();
+  P.max_time = __builtin_inf();
+  return P;
+}
+
+static bool run_gym(const Cfg& cf, uint64_t seed, uint64_t ep, Counters& C, std::string& why) {
+  oracle::GymParams gp;
+  gp.alpha = cf.alpha;
+  gp.gamma = cf.gamma;
+  gp.defenders = cf.defenders;
+  gp.max_steps = cf.steps;
+  gp.unit_obs = false;
+  gp.propagation_delay = cf.prop;
+  oracle::GymEthereum g(gp, cf.scheme, 1, nullptr, seed, ep);
+  double obs[10];
+  g.reset(obs);
+  const eth::EthParams P = params_of(cf);
+  std::vector<uint8_t> mem(ethw::win_lane_bytes(P.cap_b));
+  const ethw::WinMem M = ethw::win_mem_at(mem.data(), P.cap_b);
+  const Stream S{(uint32_t)seed, (uint32_t)(seed >> 32), (uint32_t)ep, (uint32_t)(ep >> 32)};
+  ethw::WinLane L;
+  L.gym_reset(P, S, M);
+  char buf[700];
+  bool ok = true;
+  for (int s = 0;; s++) {
+    if (L.status & ethw::W_REDO) {
+      C.redo++;
+      if (L.status & ST_OVERLAP) C.overlaps++;
+      return true;
+    }
+    const oracle::EthObs o = g.observe_int();
+    const eth::EthObs e = L.observe(P, M, true);
+    const int ov[10] = {o.public_height, o.public_work, o.private_height, o.private_work,
+                        o.diff_height, o.diff_work, o.public_orphans,
+                        o.private_orphans_inclusive, o.private_orphans_exclusive, o.event};
+    const int ev[10] = {e.public_height, e.public_work, e.private_height, e.private_work,
+                        e.diff_height, e.diff_work, e.public_orphans,
+                        e.private_orphans_inclusive, e.private_orphans_exclusive, e.event};
+    if (memcmp(ov, ev, sizeof ov) != 0) {
+      snprintf(buf, sizeof buf,
+               "step %d obs oracle (%d %d %d %d %d %d %d %d %d %d) lane (%d %d %d %d %d %d %d %d %d %d)",
+               s, ov[0], ov[1], ov[2], ov[3], ov[4], ov[5], ov[6], ov[7], ov[8], ov[9], ev[0],
+               ev[1], ev[2], ev[3], ev[4], ev[5], ev[6], ev[7], ev[8], ev[9]);
+      why = buf;
+      ok = false;
+      break;
+    }
+    int act;
+    if (cf.policy < 5) {
+      act = oracle::eth_policy(cf.policy, o);
+    } else {
+      const uint32_t r = mix(ep, s);
+      act = (int)(r % 24);
+      if (cf.policy == 6 && (r >> 8) % 2 == 0)
+        act = (int)(((r >> 12) % 4 == 0 ? 1 : 2 + (r >> 14) % 3) * 4 + (r >> 20) % 4);
+    }
+    bool done = false;
+    oracle::StepInfo info{};
+    g.step(act, obs, &done, &info);
+    bool ldone = false;
+    const int32_t hd = L.gym_step(P, S, M, act, &ldone);
+    C.steps++;
+    if (L.status & ethw::W_REDO) {
+      C.redo++;
+      if (L.status & ST_OVERLAP) C.overlaps++;
+      return true;
+    }
+    const ethw::WBlock& hb = L.B(P, M, hd);
+    const double ra = hb.rew_att / 32.0, rd = hb.rew_def / 32.0;
+    if (ra != info.episode_reward_attacker || rd != info.episode_reward_defender ||
+        hb.height != info.head_height || hb.work != info.head_work ||
+        (double)hb.work != info.episode_progress || hb.time != info.episode_chain_time ||
+        L.now != info.episode_sim_time || L.c_act != info.episode_n_activations ||
+        hb.miner != info.head_miner || ldone != done || L.steps != info.episode_n_steps) {
+      snprintf(buf, sizeof buf,
+               "step %d head lane (ra %.5f rd %.5f h %d w %d tm %.17g t %.17g k %d m %d done %d) "
+               "oracle (ra %.5f rd %.5f h %d w %d tm %.17g t %.17g k %ld m %d done %d)",
+               s, ra, rd, hb.height, hb.work, hb.time, L.now, L.c_act, hb.miner, (int)ldone,
+               info.episode_reward_attacker, info.episode_reward_defender, info.head_height,
+               info.head_work, info.episode_chain_time, info.episode_sim_time,
+               info.episode_n_activations, info.head_miner, (int)done);
+      why = buf;
+      ok = false;
+      break;
+    }
+    if (done) break;
+  }
+  C.episodes++;
+  if (L.status & ST_TIE) C.ties++;
+  if (!ok) C.mismatches++;
+  return ok;
+}
+
+int main(int argc, char** argv) {
+  const int per = argc > 1 ? atoi(argv[1]) : 20;
+  const int steps = argc > 2 ? atoi(argv[2]) : 400;
+  std::vector<Cfg> cfgs;
+  const double alphas[] = {0.1, 0.25, 0.33, 0.4, 0.45, 0.5};
+  const double gammas[] = {0.0, 0.3, 0.5, 0.75, 0.9};
+  for (int pol = 0; pol <= 6; ++pol)
+    for (double a : alphas)
+      for (double g : gammas) {
+        int d = (int)std::ceil(1.0 / (1.0 - g));
+        if (d < 2) d = 2;
+        cfgs.push_back({a, g, d, pol, (pol + (int)(a * 100)) % 2, steps, 1e-9});
+      }
+  // more defenders than the gym's rule, and tie-heavy (tiny delay: same-instant races) and
+  // overlap-heavy (long delay: activations inside deliveries) networks
+  for (int pol : {3, 5, 6})
+    for (double a : {0.33, 0.45}) {
+      cfgs.push_back({a, 0.5, 5, pol, 0, steps, 1e-9});
+      cfgs.push_back({a, 0.6, 12, pol, 1, steps, 1e-9});
+      cfgs.push_back({a, 0.5, 2, pol, 0, steps, 1e-13});
+      cfgs.push_back({a, 0.9, 11, pol, 0, steps, 1e-13});
+      cfgs.push_back({a, 0.75, 4, pol, 1, steps, 1e-12});
+      cfgs.push_back({a, 0.5, 2, pol, 0, steps, 0.05});
+      cfgs.push_back({a, 0.9, 11, pol, 1, steps, 0.01});
+    }
+  Counters C;
+  long shown = 0;
+  for (size_t ci = 0; ci < cfgs.size(); ++ci)
+    for (int e = 0; e < per; ++e) {
+      std::string why;
+      if (!run_gym(cfgs[ci], 0x5EED0000ull + ci, (uint64_t)e, C, why) && shown++ < 8)
+        fprintf(stderr, "MISMATCH cfg a=%g g=%g d=%d pol=%d scheme=%d prop=%g ep=%d: %s\n",
+                cfgs[ci].alpha, cfgs[ci].gamma, cfgs[ci].defenders, cfgs[ci].policy,
+                cfgs[ci].scheme, cfgs[ci].prop, e, why.c_str());
+    }
+  printf("{\"configs\": %zu, \"episodes\": %ld, \"steps\": %ld, \"mismatches\": %ld, "
+         "\"redo\": %ld, \"overlaps\": %ld, \"tie_episodes\": %ld}\n",
+         cfgs.size(), C.episodes, C.steps, C.mismatches, C.redo, C.overlaps, C.ties);
+  return C.mismatches ? 1 : 0;
+}

@@ -210,3 +210,57 @@ def test_eth_table_policy_decoding_and_rollout(ctx):
                 ep += n
                 e = O.EthGymEnv(cfg, episode=ep)
                 e.reset()
+
+
+# ---- the window lane (eth_window.h): Ethereum gym episodes on the selfish-mining network
+# run a window at a time; what it cannot vouch for is re-run on the event engine
+
+WINDOW = [
+    # alpha, gamma, policy, scheme, propagation delay, episodes
+    (0.45, 0.0, L.ETH_POLICY_FN19, L.REWARD_CONSTANT, 1e-9, 256),
+    (0.45, 0.9, L.ETH_POLICY_FN19, L.REWARD_CONSTANT, 1e-9, 256),
+    (0.35, 0.5, L.ETH_POLICY_SELFISH_RELEASE, L.REWARD_CONSTANT, 1e-9, 256),
+    # tiny delay: same-instant races are common (tie replay through the skew heap)
+    (0.40, 0.5, L.ETH_POLICY_FN19, L.REWARD_DISCOUNT, 1e-13, 256),
+    (0.45, 0.9, L.ETH_POLICY_FN19PKEL, L.REWARD_CONSTANT, 1e-13, 256),
+    # long delay: activations inside deliveries, re-run on the event engine
+    (0.40, 0.5, L.ETH_POLICY_FN19, L.REWARD_CONSTANT, 0.05, 128),
+    (0.35, 0.9, L.ETH_POLICY_SELFISH_DISCARD, L.REWARD_DISCOUNT, 0.01, 128),
+]
+
+
+@pytest.mark.parametrize("alpha,gamma,policy,scheme,prop,n", WINDOW)
+def test_eth_window_lane_matches_oracle(ctx, alpha, gamma, policy, scheme, prop, n):
+    cfg, keep = _cfg(alpha=alpha, gamma=gamma, policy=policy, reward_scheme=scheme,
+                     max_steps=2016, propagation_delay=prop, seed=0xE7E71000)
+    s, rec, ok = _compare(cfg, keep, n)
+    st = rec["status"]
+    if prop < 1e-12:
+        assert ((st & L.ST_TIE) != 0).sum() > 0  # ties occurred and were replayed
+    if prop > 1e-3:
+        rerun = (st & L.ST_EXACT_RERUN) != 0
+        assert rerun.sum() > n // 4  # most episodes overlapped and were re-run exactly
+        assert ((st[rerun] & L.ST_OVERLAP) != 0).all()
+    # the summary is the sum of the records (re-runs replace the flagged episodes)
+    assert s.episodes == n and s.steps == int(rec["n_steps"].sum())
+    assert s.activations == int(rec["n_activations"].sum())
+    assert s.reward_attacker_fx == int(np.rint(rec["reward_attacker"] * 2**20).sum())
+    assert s.progress_fx == int(np.rint(rec["progress"] * 2**20).sum())
+
+
+@pytest.mark.parametrize("gamma", [0.0, 0.5, 0.9])
+def test_eth_window_lane_equals_event_engine(ctx, gamma, monkeypatch):
+    # the bench's configs[2] point at full episode length: the window lane's summary equals
+    # the event engine's (CPR_ETH_WINDOW=0) field for field
+    cfg, keep = _cfg(alpha=0.45, gamma=gamma, policy=L.ETH_POLICY_FN19,
+                     reward_scheme=L.REWARD_CONSTANT, max_steps=2016, seed=0x5EED0000)
+    b = device.Batch(cfg, keep=keep)
+    n = 2048
+    s_win = b.run(n, first_episode=0)
+    monkeypatch.setenv("CPR_ETH_WINDOW", "0")
+    s_ev = b.run(n, first_episode=0)
+    for f in L.Summary.FIELDS:
+        if f == "status_tie":  # the event engine has no tie bit; the window lane marks replays
+            continue
+        assert getattr(s_win, f) == getattr(s_ev, f), f
+    assert list(s_win.hist) == list(s_ev.hist)
