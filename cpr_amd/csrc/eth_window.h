@@ -53,17 +53,18 @@ using eth::Payload;
 constexpr uint32_t W_REDO = ST_OVERLAP | ST_TIE_UNRESOLVED | eth::EST_CAPACITY;
 
 struct WBlock {
-  int32_t serial;
   int32_t p[3];  // parent, uncles (-1: none)
   int32_t height, work;
   int32_t rew_att, rew_def;  // cumulative rewards of the first-parent chain, units of 1/32
   int32_t child;             // newest block whose first parent this is (-1: none)
   int32_t sib;               // next older block with the same first parent (-1: none)
-  int16_t miner;             // -1 genesis, 0 attacker, 1..d defenders
+  int32_t jump;              // skew-binary jump ancestor (O(log depth) ancestor queries)
+  int8_t miner;              // -1 genesis, 0 attacker, 1..d defenders
   uint8_t np;                // parents
   uint8_t rel;               // attacker block shared (V_REL in the attacker's view)
-  int32_t share_k, share_off;  // its release coordinates (keyed link delays)
-  double time;                 // append time (Simulator.timestamp)
+  uint8_t _pad0;
+  int32_t _pad1[2];
+  double time;               // append time (Simulator.timestamp)
 };
 static_assert(sizeof(WBlock) == 64, "WBlock layout");
 
@@ -118,15 +119,17 @@ struct WinLane {
   // ethereum_ssz agent (BetweenActions + Observable)
   int32_t pub, priv, pending, own, foreign;
   int32_t o_pub, o_priv, o_common, o_event;
+  // the last common ancestor computed: common_ancestor(ca_a, ca_b) = ca_c (-1: none)
+  int32_t ca_a, ca_b, ca_c;
 
   __host__ __device__ inline void fail(int32_t why) {
     status |= eth::EST_CAPACITY;
     if (!dead) dead = why;
   }
+  // serials index the ring directly: append stops the lane before it would wrap
   __host__ __device__ inline WBlock& B(const EthParams& P, const WinMem& M, int32_t s) {
-    WBlock& b = M.blk[s & (P.cap_b - 1)];
-    if (b.serial != s) fail(1);
-    return b;
+    if ((uint32_t)s > (uint32_t)newest) fail(1);
+    return M.blk[s & (P.cap_b - 1)];
   }
   // visibility at quiescence (every message of earlier windows delivered)
   __host__ __device__ static inline bool def_visible(const EthParams& P, const WBlock& b) {
@@ -140,6 +143,7 @@ struct WinLane {
   __host__ __device__ inline Payload payload(const EthParams& P, const WinMem& M, int32_t view,
                                              int32_t tip, int32_t filter, int32_t f_own,
                                              int32_t f_foreign) {
+    CPR_COST(eth::CC_PAYLOAD);
     int32_t* cand = M.scr + S_CAND;
     int32_t* key = M.scr + S_KEY;
     int32_t ic[19];  // in-chain set: the tip and the parents of tip .. gen 5
@@ -165,6 +169,7 @@ struct WinLane {
     int32_t nc = 0;
     for (int32_t g = 0; g < ng && !dead; ++g) {
       for (int32_t s = B(P, M, nua[g]).child; s >= 0 && !dead; s = B(P, M, s).sib) {
+        CPR_COST(eth::CC_SCAN);
         const WBlock& c = B(P, M, s);
         bool mine, keep;
         if (view == 0) {  // the attacker sees every block
@@ -202,6 +207,28 @@ struct WinLane {
     return d;
   }
 
+  // skew-binary jump pointers (Myers 1983) over first parents: a block's jump is its
+  // parent's jump's jump when the parent's two jumps span equal height gaps, else its
+  // parent; jumps depend on the height alone, so ancestor-at-height and first-parent LCA
+  // queries take O(log depth) loads
+  __host__ __device__ inline int32_t jump_for(const EthParams& P, const WinMem& M,
+                                              int32_t parent) {
+    const WBlock& pb = B(P, M, parent);
+    const WBlock& jb = B(P, M, pb.jump);
+    const int32_t jjh = B(P, M, jb.jump).height;
+    return (pb.height - jb.height == jb.height - jjh) ? jb.jump : parent;
+  }
+  // first-parent ancestor of x at height h <= height(x)
+  __host__ __device__ inline int32_t ancestor_at(const EthParams& P, const WinMem& M, int32_t x,
+                                                 int32_t h) {
+    while (!dead) {
+      const WBlock& b = B(P, M, x);
+      if (b.height <= h || b.np == 0) return x;
+      x = B(P, M, b.jump).height >= h ? b.jump : b.p[0];
+    }
+    return x;
+  }
+
   // simulator.ml:122-136, 377-399 (set_rewards, ethereum.ml:173-197: Constant = whitepaper)
   __host__ __device__ inline int32_t append(const EthParams& P, const WinMem& M, int32_t node,
                                             const Payload& d) {
@@ -220,25 +247,27 @@ struct WinLane {
       else if (u.miner > 0)
         rd += amt;
     }
+    if (newest + 1 >= P.cap_b) {  // the ring would wrap onto live blocks
+      fail(1);
+      return 0;
+    }
+    const int32_t jmp = jump_for(P, M, d.p[0]);
     const int32_t s = ++newest;
-    WBlock& b = M.blk[s & (P.cap_b - 1)];
-    if (newest >= P.cap_b) fail(1);  // the ring would reuse a live slot
-    b.serial = s;
+    WBlock& b = M.blk[s];
     b.p[0] = d.p[0];
     b.p[1] = d.np > 1 ? d.p[1] : -1;
     b.p[2] = d.np > 2 ? d.p[2] : -1;
     b.np = (uint8_t)d.np;
     b.height = d.height;
     b.work = d.work;
-    b.miner = (int16_t)node;
+    b.miner = (int8_t)node;
     b.rel = 0;
     b.rew_att = ra;
     b.rew_def = rd;
     b.child = -1;
     b.sib = pb.child;  // children lists newest first (dag.ml:32)
+    b.jump = jmp;
     pb.child = s;
-    b.share_k = -1;
-    b.share_off = 0;
     b.time = now;
     return s;
   }
@@ -247,6 +276,7 @@ struct WinLane {
   // every block: ancestors by descending (height, serial) over all parent edges
   __host__ __device__ inline void q_insert(int32_t* q, int32_t* nq, int32_t s, int32_t h) {
     const uint64_t kk = eth::EthLane::ca_key(h, s);
+    CPR_COST(eth::CC_MDV);  // (window lane: frontier insertions)
     for (int32_t j = 0; j < *nq; ++j)
       if (q[2 * j + 1] == s) return;
     if (*nq >= NQ / 2) {
@@ -266,6 +296,7 @@ struct WinLane {
   __host__ __device__ inline int32_t q_next(const EthParams& P, const WinMem& M, int32_t* q,
                                             int32_t* nq) {
     if (*nq == 0) return -1;
+    CPR_COST(eth::CC_CA);
     const int32_t s = q[1];
     for (int32_t j = 1; j < *nq; ++j) {
       q[2 * (j - 1)] = q[2 * j];
@@ -299,6 +330,51 @@ struct WinLane {
     return 0;
   }
 
+  // Every uncle of a block c is a child (by first parent) of one of the first-parent
+  // ancestors of c's parent (Honest.puzzle_payload'), so all-edge ancestors of a block x
+  // are its first-parent chain plus side blocks whose first parent lies on that chain. Two
+  // blocks' common ancestors above their first-parent fork F can then only be children of
+  // F or siblings of F: the common ancestor has height h(F) or h(F) + 1. So when one side
+  // is a block just appended on the other side's previous argument (first parent), the
+  // answer can change only through blocks of its uncle closure (uncles, their uncles, ...)
+  // at most one level above the previous answer; if all of them are higher, it is the
+  // previous answer. That is the common case in long private forks, where the frontier walk
+  // below costs the whole fork per activation. Anything else walks.
+  __host__ __device__ inline bool uncles_above(const EthParams& P, const WinMem& M, int32_t x,
+                                               int32_t hlim) {
+    int32_t st[8];
+    int32_t sp = 0;
+    st[sp++] = x;
+    while (sp > 0) {
+      const WBlock& b = B(P, M, st[--sp]);
+      for (int32_t i = 1; i < b.np; ++i) {
+        if (B(P, M, b.p[i]).height <= hlim || sp >= 8) return false;
+        st[sp++] = b.p[i];
+      }
+    }
+    return true;
+  }
+  __host__ __device__ inline int32_t common_ancestor_cached(const EthParams& P, const WinMem& M,
+                                                            int32_t a, int32_t b) {
+    if (a == ca_a && b == ca_b) return ca_c;
+    if (ca_c >= 0 && a != b) {
+      const int32_t hl = B(P, M, ca_c).height + 1;
+      if (a == ca_a && b == newest && B(P, M, b).p[0] == ca_b && uncles_above(P, M, b, hl)) {
+        ca_b = b;
+        return ca_c;
+      }
+      if (b == ca_b && a == newest && B(P, M, a).p[0] == ca_a && uncles_above(P, M, a, hl)) {
+        ca_a = a;
+        return ca_c;
+      }
+    }
+    const int32_t c = common_ancestor(P, M, a, b);
+    ca_a = a;
+    ca_b = b;
+    ca_c = c;
+    return c;
+  }
+
   // ---------------------------------------------------------------- agent
   __host__ __device__ inline int32_t update_head(const EthParams& P, const WinMem& M,
                                                  int32_t old, int32_t cand) {
@@ -319,7 +395,7 @@ struct WinLane {
     }
     o_pub = p;
     o_priv = q;
-    o_common = common_ancestor(P, M, p, q);
+    o_common = common_ancestor_cached(P, M, p, q);
   }
   // ethereum_ssz.ml:364-396; orphans only when asked
   __host__ __device__ inline EthObs observe(const EthParams& P, const WinMem& M, bool orphans) {
@@ -345,14 +421,10 @@ struct WinLane {
   // ethereum_ssz.ml:398-429; returns the block to share (-1: none)
   __host__ __device__ inline int32_t apply(const EthParams& P, const WinMem& M, int32_t index) {
     const int32_t action = index >> 2;
+    // the private chain's block at height target (its tip if lower): jump pointers
     auto release_upto = [&](int32_t target) {
-      int32_t b = o_priv;
-      while (!dead) {
-        const WBlock& x = B(P, M, b);
-        if (x.height <= target) break;
-        b = x.p[0];
-      }
-      return b;
+      CPR_COST(eth::CC_SORT);  // (window lane: release walks)
+      return ancestor_at(P, M, o_priv, target);
     };
     int32_t s = -1, np = o_priv;
     switch (action) {
@@ -385,11 +457,10 @@ struct WinLane {
     st[sp++] = s0;
     while (sp > 0 && !dead) {
       const int32_t s = st[--sp];
+      CPR_COST(eth::CC_SHARE);
       WBlock& b = B(P, M, s);
       if (b.miner != 0 || b.rel) continue;  // received / released: nothing to share
-      b.rel = 1;
-      b.share_k = c_act;
-      b.share_off = off;
+      b.rel = 1;  // its link delays are keyed (c_act, off): off = position in clos
       clos[off++] = s;
       if (sp + b.np > NSTACK) {
         fail(5);
@@ -403,19 +474,15 @@ struct WinLane {
   }
 
   // ---------------------------------------------------------------- the window
-  template <class St>
-  __host__ __device__ inline double link_of(const EthParams& P, const St& S, const WBlock& c,
-                                            int32_t j) const {
-    return S.link((uint32_t)c.share_k, (uint32_t)c.share_off, (uint32_t)j, P.dmax);
-  }
   // the visibility time at defender j of the released top: the latest arrival over its
-  // closure (a block is visible once its parents are, simulator.ml:424-450)
+  // closure (a block is visible once its parents are, simulator.ml:424-450); the closure
+  // was shared at activation count c_act, position m in share order (keyed link delays)
   template <class St>
   __host__ __device__ inline double release_visible(const EthParams& P, const St& S,
-                                                    const WinMem& M, int32_t j) {
+                                                    const WinMem& M, int32_t j) const {
     double v = -__builtin_inf();
     for (int32_t m = 0; m < nclos; ++m) {
-      const double a = now + link_of(P, S, B(P, M, M.scr[S_CLOS + m]), j);
+      const double a = now + S.link((uint32_t)c_act, (uint32_t)m, (uint32_t)j, P.dmax);
       v = a > v ? a : v;
     }
     return v;
@@ -464,7 +531,7 @@ struct WinLane {
         NP.d = P.d;
         NP.delta = P.delta;
         NP.dmax = P.dmax;
-        on_top = tie_replay(NP, S, M.replay, wi, now, 1, nclos, B(P, M, sh).share_k, &ok);
+        on_top = tie_replay(NP, S, M.replay, wi, now, 1, nclos, c_act, &ok);
       }
       if (!ok) {
         status |= ST_TIE_UNRESOLVED;
@@ -534,8 +601,8 @@ struct WinLane {
     wi = 0;
     nclos = 0;
     chain = 1;
+    ca_a = ca_b = ca_c = -1;
     WBlock& r = M.blk[0];
-    r.serial = 0;
     r.p[0] = r.p[1] = r.p[2] = -1;
     r.np = 0;
     r.height = 0;
@@ -544,8 +611,7 @@ struct WinLane {
     r.rel = 0;
     r.rew_att = r.rew_def = 0;
     r.child = r.sib = -1;
-    r.share_k = -1;
-    r.share_off = 0;
+    r.jump = 0;
     r.time = 0.0;
     for (int32_t j = 0; j <= P.d; ++j) M.tips[j] = 0;
     pub = priv = 0;

@@ -125,3 +125,21 @@ def test_device_log_and_philox_match_oracle():
     assert p.returncode == 0, p.stderr[-2000:]
     assert out["log_mismatches"] == 0 and out["philox_mismatches"] == 0
     assert out["checked"] > 20_000_000
+
+
+def test_ethereum_window_lane_matches_oracle_fuzz():
+    # tests/native/ethwin_vs_oracle.cpp: the Ethereum window lane (cpr_amd/csrc/eth_window.h,
+    # host build) vs the oracle's event-driven ethereum.cpp, every step (10 observation
+    # fields, rewards, height, work, chain time, clock, activations, head miner, done);
+    # 5 policies + 2 random-action fuzzers x alpha x gamma (defenders per the gym's rule),
+    # more defenders, and tie-heavy (1e-13 / 1e-12 delays: same-instant races replayed
+    # through the skew heap) and overlap-heavy (0.05 / 0.01) networks, whose flagged
+    # episodes stop being compared at the flag (the kernel re-runs them exactly)
+    subprocess.run(["make", "-s", "-C", str(ROOT / "tests" / "native")], check=True)
+    exe = ROOT / "tests" / "native" / "build" / "ethwin_vs_oracle"
+    p = subprocess.run([str(exe), "5", "500"], capture_output=True, text=True, timeout=600)
+    out = json.loads(p.stdout.strip().splitlines()[-1])
+    assert p.returncode == 0, p.stderr[-2000:]
+    assert out["mismatches"] == 0, p.stderr[-2000:]
+    assert out["episodes"] > 1000 and out["steps"] > 400000
+    assert out["tie_episodes"] > 20 and out["overlaps"] > 20  # both hazards exercised

@@ -76,7 +76,8 @@ int main(int argc, char** argv) {
   printf("}");
   // the window lane (eth_window.h) on the same episodes: episodes it hands to the exact
   // re-run and episodes with a replayed tie
-  long redo = 0, ties = 0, unres = 0, ovl = 0;
+  long redo = 0, ties = 0, unres = 0, ovl = 0, wacts = 0;
+  for (int i = 0; i < 16; ++i) g_cost[i] = 0;
   std::vector<uint8_t> wmem(ethw::win_lane_bytes(P.cap_b));
   for (int e = 0; e < episodes; ++e) {
     const ethw::WinMem W = ethw::win_mem_at(wmem.data(), P.cap_b);
@@ -92,8 +93,14 @@ int main(int argc, char** argv) {
     ties += (L.status & ST_TIE) ? 1 : 0;
     unres += (L.status & ST_TIE_UNRESOLVED) ? 1 : 0;
     ovl += (L.status & ST_OVERLAP) ? 1 : 0;
+    wacts += L.c_act;
   }
   printf(", \"window_lane\": {\"redo\": %ld, \"tie\": %ld, \"tie_unresolved\": %ld, "
-         "\"overlap\": %ld}}\n", redo, ties, unres, ovl);
+         "\"overlap\": %ld, \"per_activation\": {\"payloads\": %.2f, \"children_visited\": %.2f, "
+         "\"ca_steps\": %.2f, \"frontier_inserts\": %.2f, \"share_steps\": %.2f, "
+         "\"release_walk\": %.2f}}}\n", redo, ties, unres, ovl, g_cost[eth::CC_PAYLOAD] / (double)wacts,
+         g_cost[eth::CC_SCAN] / (double)wacts, g_cost[eth::CC_CA] / (double)wacts,
+         g_cost[eth::CC_MDV] / (double)wacts, g_cost[eth::CC_SHARE] / (double)wacts,
+         g_cost[eth::CC_SORT] / (double)wacts);
   return 0;
 }
