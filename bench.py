@@ -96,6 +96,8 @@ def cpu_baseline(seconds, points):
 
 
 # ---------------------------------------------------------------- BASELINE configs[0, 2-4]
+CONFIG0_EPISODES = 1 << 20  # >= 10^6 episodes
+CONFIG2_ALPHAS = (0.35, 0.45)
 # build-defined VALU cost model per activation
 OPS_BY_PROTOCOL = {"nakamoto": 40, "ethereum": 60, "bk": 80, "tailstorm": 120}
 
@@ -110,18 +112,18 @@ def other_config_specs():
         "configs[0]", "Nakamoto honest, alpha .33, gamma .5 (d = 2), 2016-step cpr-nakamoto-v0 "
         "episodes (the reference's CPU-runnable case)", "nakamoto", "k_run_episodes",
         [dict(alpha=0.33, gamma=0.5, policy=L.POLICY_HONEST, max_steps=STEPS_PER_EPISODE)],
-        393216, None)]
+        CONFIG0_EPISODES, None)]
     # configs[2]: Ethereum Byzantium, whitepaper (constant) uncle rewards, ethereum_ssz
-    # selfish_release and fn19 over alpha x gamma, 2016-step gym episodes
-    # (a launch at resident capacity lasts one 2016-step episode of the event engine,
-    # ~7 s, whatever the lane count: three points keep the bench within minutes)
-    eth = [dict(protocol=L.PROTO_ETHEREUM, alpha=0.45, gamma=g, policy=L.ETH_POLICY_FN19,
+    # selfish_release and fn19 over alpha x gamma, 2016-step gym episodes (the window lane,
+    # eth_window.h; one launch of the resident lanes per point)
+    eth = [dict(protocol=L.PROTO_ETHEREUM, alpha=a, gamma=g, policy=pol,
                 reward_scheme=L.REWARD_CONSTANT, max_steps=STEPS_PER_EPISODE)
-           for g in (0.0, 0.5, 0.9)]
+           for pol in (L.ETH_POLICY_SELFISH_RELEASE, L.ETH_POLICY_FN19)
+           for a in CONFIG2_ALPHAS for g in (0.0, 0.5, 0.9)]
     specs.append(("configs[2]", "Ethereum-PoW uncle-aware selfish mining, Byzantium + whitepaper "
-                  "(constant) uncle rewards, ethereum_ssz fn19 (Feng & Niu '19), alpha .45 x "
-                  "gamma {0, .5, .9}, 2016-step gym episodes", "ethereum",
-                  "k_eth_run_episodes", eth, None, None))
+                  "(constant) uncle rewards, ethereum_ssz selfish_release and fn19 (Feng & Niu "
+                  "'19), alpha {.35, .45} x gamma {0, .5, .9}, 2016-step gym episodes",
+                  "ethereum", "k_eth_win_episodes", eth, None, None))
     # configs[3]: Tailstorm k = 8, discount, heuristic sub-block selection, withholding
     # attack on the two-agents network (Simulator.loop tasks of 10^4 activations,
     # withholding.ml:68-90), get-ahead and avoid-loss; the exp(1)-propagation variant apart
@@ -145,7 +147,9 @@ def other_config_specs():
     table = np.random.default_rng(0).integers(0, 8, size=D * D * (K + 1) ** 2 * 3).astype(np.uint8)
     specs.append(("configs[4]", "65,536 parallel bk_ssz gym envs (B_k k=8, constant rewards, "
                   "alpha .33, gamma .5, d = 2) stepped in lockstep by an on-device random table "
-                  "policy, 2048-step episodes, VecEnv auto-reset", "bk", "k_bk_rollout",
+                  "policy, 2048-step episodes, VecEnv auto-reset; every step's observation, "
+                  "reward and done written to device buffers [step][lane] (an RL consumer's "
+                  "input)", "bk", "k_bk_rollout",
                   [dict(protocol=L.PROTO_BK, alpha=0.33, gamma=0.5, k=K, table=table,
                         reward_scheme=L.REWARD_CONSTANT, max_steps=2048, n_lanes=65536)],
                   None, 512))
@@ -181,7 +185,7 @@ def run_other_configs(ctx, cpu_seconds, with_cpu, pmc, keys=None):
     for key, desc, proto, kernel, points, eps, roll in other_config_specs():
         if keys is not None and key not in keys:
             continue
-        acts = steps = episodes = 0
+        acts = steps = episodes = invalid = 0
         wall = kms = 0.0
         lanes_l, res_l, point_ms = [], [], []
         for pt in points:
@@ -192,9 +196,21 @@ def run_other_configs(ctx, cpu_seconds, with_cpu, pmc, keys=None):
                 n = b.launch_shape()[1]
             t0 = time.perf_counter()
             if roll is not None:
+                import torch
+
                 b.rollout(8)  # reset + a few steps, untimed
+                # obs / reward / done of every step into device memory, as a VecEnv consumer
+                # reads them (~5 MB per step)
+                nl, ol = b.n_lanes, b.obs_len
+                dev = torch.device("cuda", ctx.device)
+                o_t = torch.empty((roll, nl, ol), dtype=torch.float64, device=dev)
+                r_t = torch.empty((roll, nl), dtype=torch.float64, device=dev)
+                d_t = torch.empty((roll, nl), dtype=torch.uint8, device=dev)
+                torch.cuda.synchronize()
                 t0 = time.perf_counter()
-                s = b.rollout(roll)
+                s = b.rollout(roll, device_outputs=(o_t.data_ptr(), r_t.data_ptr(),
+                                                    d_t.data_ptr()))
+                out_bytes = o_t.numel() * 8 + r_t.numel() * 8 + d_t.numel()
             else:
                 s = b.run(n, first_episode=0)
             wall += time.perf_counter() - t0
@@ -207,6 +223,7 @@ def run_other_configs(ctx, cpu_seconds, with_cpu, pmc, keys=None):
             acts += int(s.activations)
             steps += int(s.steps)
             episodes += int(s.episodes)
+            invalid += int(s.invalid)
             b.close()
         ops = OPS_BY_PROTOCOL[proto]
         kact = acts / (kms / 1e3)
@@ -222,6 +239,9 @@ def run_other_configs(ctx, cpu_seconds, with_cpu, pmc, keys=None):
             "lanes_per_launch": lanes_l[0],
             "resident_lanes": res_l[0],
             "lanes_over_resident": lanes_l[0] / res_l[0] if res_l[0] else None,
+            # episodes whose outputs are not valid (CPR_ST_INVALID: capacity, reference
+            # exception, trace miss): their work is counted, their outputs are not
+            "invalid": invalid,
             "roofline": {"bound": "valu", "kernel": kernel, "achieved": ach,
                          "peak": VALU_PEAK_TOPS,
                          "unit": f"Tops/s (VALU lane-ops, {ops} ops/activation cost model)",
@@ -231,9 +251,13 @@ def run_other_configs(ctx, cpu_seconds, with_cpu, pmc, keys=None):
             entry["env_steps_per_s"] = steps / wall
             entry["env_steps"] = steps
             entry["rollout_steps_per_lane"] = roll
+            entry["device_output_bytes"] = out_bytes
+            entry["device_output_gb_per_s"] = out_bytes / wall / 1e9
         else:
             entry["episodes_per_s"] = episodes / wall
         t = pmc.get(key) if pmc else None
+        if t and t.get("kernel") not in (None, kernel):
+            t = None  # a profile of another kernel (an older build of this config)
         if t:
             entry["roofline"]["traffic"] = t["hbm_bytes_per_activation"] * acts
             entry["roofline"]["traffic_source"] = t["source"]

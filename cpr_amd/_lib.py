@@ -38,6 +38,7 @@ TS_POLICY_AVOID_LOSS = 3
 TS_POLICY_AVOID_LOSS_A = 4
 TS_POLICY_AVOID_LOSS_B = 5
 TS_POLICY_LONG_DELAY = 6
+TS_POLICY_RANDOM = 8  # loop tasks: keyed random Action8 (cpr_protocols.ml:658-782)
 REWARD_CONSTANT = 0
 REWARD_DISCOUNT = 1
 REWARD_BLOCK = 2
@@ -46,12 +47,14 @@ BK_POLICY_GET_AHEAD = 1
 BK_POLICY_MINOR_DELAY = 2
 BK_POLICY_AVOID_LOSS = 3
 BK_POLICY_TABLE = 4
+BK_POLICY_RANDOM = 5
 ETH_POLICY_HONEST = 0
 ETH_POLICY_TABLE = 5  # include/cpr_hip.h: [(pub_h, priv_h) clamped to D][event]
 ETH_POLICY_SELFISH_RELEASE = 1
 ETH_POLICY_SELFISH_DISCARD = 2
 ETH_POLICY_FN19 = 3
 ETH_POLICY_FN19PKEL = 4
+ETH_POLICY_RANDOM = 6
 NET_SELFISH_MINING = 0
 NET_TWO_AGENTS = 1
 NET_HONEST_CLIQUE = 2
@@ -65,6 +68,7 @@ POLICY_SIMPLE = 1
 POLICY_EYAL_SIRER_2014 = 2
 POLICY_SAPIRSHTEIN_2016_SM1 = 3
 POLICY_TABLE = 4
+POLICY_RANDOM = 5  # loop tasks on the event engine (cpr_protocols.ml:658-782)
 
 PROTO_FC16 = 4  # gym/rust/src/fc16.rs abstract model (fused episodes)
 FC16_POLICY_HONEST = 0

@@ -32,8 +32,17 @@
 
 #pragma clang fp contract(off)
 
+// host cost studies (tools/bk_cost_study.cpp) count work items by id (BC_* below)
+#ifndef CPR_BK_COST
+#define CPR_BK_COST(id)
+#endif
+
 namespace cpr {
 namespace bk {
+
+enum : int32_t { BC_PUSH = 0, BC_POP = 1, BC_CONFIRMING = 2, BC_PROPOSE = 3, BC_OBSERVE = 4,
+                 BC_APPLY = 5, BC_MDV = 6, BC_EVENT = 7 /* + event type, 7 types */,
+                 BC_PROPOSE_CALLS = 14, BC_CONFIRMING_CALLS = 15, BC_N = 16 };
 
 constexpr uint32_t BST_CAPACITY = 32u;  // CPR_ST_CAPACITY
 
@@ -267,7 +276,11 @@ __host__ __device__ inline void ocaml_heap_sort64(int32_t* v, uint64_t* k, int32
 // OCaml's Float.compare on them
 __host__ __device__ inline uint64_t time_key(double t) { return bitsd(t); }
 
+// random actions (loop tasks; cpr_protocols.ml:658-782): CPR_BK_POLICY_RANDOM
+constexpr int32_t BK_POLICY_RANDOM = 5;
+
 struct BkLane {
+  int32_t nrand;  // random-policy decisions so far (the keyed draw's index)
   double now;
   int32_t c_act, newest, nblk, act0;
   int32_t hroot, hfree, hused;
@@ -336,6 +349,7 @@ struct BkLane {
                                        int32_t blk) {
     int32_t parent = -1, node = hroot;
     for (;;) {
+      CPR_BK_COST(BC_PUSH);
       if (node < 0) {
         const int32_t a = halloc(P, M);
         if (a < 0) return;
@@ -378,6 +392,7 @@ struct BkLane {
     *blk = M.heap[hroot].blk;
     int32_t parent = -1, side = 0, node = hroot;
     for (;;) {
+      CPR_BK_COST(BC_POP);
       const int32_t l = M.heap[node].l, r = M.heap[node].r;
       int32_t repl = -2;
       if (r < 0)
@@ -524,7 +539,9 @@ struct BkLane {
   __host__ __device__ inline int32_t confirming(const BkParams& P, const BkMem& M, int32_t b,
                                                 int32_t node, int32_t vf) {
     int32_t n = 0;
+    CPR_BK_COST(BC_CONFIRMING_CALLS);
     for (int32_t c = newest; c > b && !dead; --c) {
+      CPR_BK_COST(BC_CONFIRMING);
       const uint8_t v = V(P, M, c, node);
       if ((v & V_KIND) == V_INV || !keep(v, vf)) continue;
       const BVtx& x = X(P, M, c);
@@ -562,7 +579,9 @@ struct BkLane {
     int32_t* tv = M.sval + NQS;
     int32_t nmine = 0, ntheirs = 0;
     uint64_t my_hash = ~0ull;
+    CPR_BK_COST(BC_PROPOSE_CALLS);
     for (int32_t c = newest; c > b && !dead; --c) {
+      CPR_BK_COST(BC_PROPOSE);
       const uint8_t v = V(P, M, c, node);
       if ((v & V_KIND) == V_INV || !keep(v, vf)) continue;
       const BVtx& x = X(P, M, c);
@@ -714,6 +733,7 @@ struct BkLane {
     o.private_votes_inclusive = 0;
     o.private_votes_exclusive = 0;
     for (int32_t c = newest; c > o_priv && !dead; --c) {
+      CPR_BK_COST(BC_OBSERVE);
       const uint8_t v = V(P, M, c, 0);
       if ((v & V_KIND) == V_INV) continue;
       const BVtx& x = X(P, M, c);
@@ -761,6 +781,7 @@ struct BkLane {
       int32_t* vv = M.sval;
       int32_t nv = 0;
       for (int32_t c = newest; c > block && !dead; --c) {
+        CPR_BK_COST(BC_APPLY);
         if (!visible(P, M, c, 0)) continue;
         const BVtx& x = X(P, M, c);
         if (!x.vote || x.parent != block) continue;
@@ -792,6 +813,7 @@ struct BkLane {
   template <class St>
   __host__ __device__ inline void init(const BkParams& P, const St& S, const BkMem& M) {
     now = 0.0;
+    nrand = 0;
     c_act = 0;
     newest = 0;
     nblk = 0;
@@ -841,6 +863,7 @@ struct BkLane {
                                          uint32_t ev, int32_t s) {
     const uint32_t ty = ev & 7u, kind = (ev >> 3) & 3u;
     const int32_t node = (int32_t)(ev >> 5);
+    CPR_BK_COST(BC_EVENT + (int32_t)ty);
     switch (ty) {
       case EV_MV: {
         uint8_t& v = V(P, M, s, node);
@@ -862,7 +885,8 @@ struct BkLane {
         if (node == 0 && P.net != 2) {
           // loop mode: the attacker node's handler (bk_ssz.ml:334-343)
           prepare(P, M, kind, s);
-          apply(P, M, bk_policy(P, observe(P, M)));
+          apply(P, M, P.policy == BK_POLICY_RANDOM ? S.rand_act((uint32_t)nrand++, 8u)
+                                                   : bk_policy(P, observe(P, M)));
           break;
         }
         honest(P, M, node, s);
@@ -925,6 +949,7 @@ struct BkLane {
         // blocks on block s, or blocks whose quorum holds vote s
         const bool is_vote = X(P, M, s).vote != 0;
         for (int32_t c = newest; c > s && !dead; --c) {
+          CPR_BK_COST(BC_MDV);
           if (!(V(P, M, c, node) & V_GOT)) continue;
           const BVtx& cb = X(P, M, c);
           bool child = cb.parent == s;

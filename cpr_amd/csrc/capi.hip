@@ -226,6 +226,11 @@ static int validate_ts(const cpr_config* c, ts::TsParams* P);
 // overlapping windows common (the withholding sweep's 1e-4 defender delay overlaps about
 // once per 10,000 activations, models.ml:54), which the closed-form lane would hand to
 // the same engine episode by episode anyway
+// the random attacker of the reference's policy tests (cpr_protocols.ml:658-782) decides in
+// its handler: Simulator.loop tasks (the gym's agent takes actions from its caller)
+static const char* random_policy_msg =
+    "random attacker actions: Simulator.loop tasks (CPR_MODE_LOOP) on the event engines";
+
 static bool nak_on_event_engine(const cpr_config* c) {
   if (c->protocol != CPR_PROTO_NAKAMOTO) return false;
   if (c->network == CPR_NET_HONEST_CLIQUE || c->network == CPR_NET_EXP_CLIQUE) return true;
@@ -291,8 +296,10 @@ static int validate(const cpr_config* c, NakParams* P, eth::EthParams* EP, bk::B
   if (c->activation_delay <= 0.) return fail(CPR_E_INVALID_ARG, "activation_delay <= 0");
   if (c->mode != CPR_MODE_GYM && c->mode != CPR_MODE_LOOP)
     return fail(CPR_E_INVALID_ARG, "unknown mode");
-  if (c->policy < CPR_POLICY_HONEST || c->policy > CPR_POLICY_TABLE)
+  if (c->policy < CPR_POLICY_HONEST || c->policy > CPR_POLICY_RANDOM)
     return fail(CPR_E_INVALID_ARG, "unknown policy");
+  if (c->policy == CPR_POLICY_RANDOM && !(c->mode == CPR_MODE_LOOP && nak_on_event_engine(c)))
+    return fail(CPR_E_UNSUPPORTED, random_policy_msg);
   if (c->policy == CPR_POLICY_TABLE) {
     if (!c->policy_table || c->policy_table_dim <= 0 || c->policy_table_dim > 256)
       return fail(CPR_E_INVALID_ARG, "policy table missing or dim out of range (1..256)");
@@ -384,8 +391,10 @@ static int validate_eth(const cpr_config* c, eth::EthParams* P) {
   if (c->activation_delay <= 0.) return fail(CPR_E_INVALID_ARG, "activation_delay <= 0");
   if (c->mode != CPR_MODE_GYM && c->mode != CPR_MODE_LOOP)
     return fail(CPR_E_INVALID_ARG, "unknown mode");
-  if (c->policy < CPR_ETH_POLICY_HONEST || c->policy > CPR_ETH_POLICY_TABLE)
+  if (c->policy < CPR_ETH_POLICY_HONEST || c->policy > CPR_ETH_POLICY_RANDOM)
     return fail(CPR_E_INVALID_ARG, "unknown policy");
+  if (c->policy == CPR_ETH_POLICY_RANDOM && c->mode != CPR_MODE_LOOP)
+    return fail(CPR_E_UNSUPPORTED, random_policy_msg);
   if (c->reward_scheme != CPR_REWARD_CONSTANT && c->reward_scheme != CPR_REWARD_DISCOUNT)
     return fail(CPR_E_INVALID_ARG, "unknown incentive scheme");
   if (c->policy == CPR_ETH_POLICY_TABLE) {
@@ -508,8 +517,10 @@ static int validate_bk(const cpr_config* c, bk::BkParams* P) {
   if (c->reward_scheme != CPR_REWARD_CONSTANT && c->reward_scheme != CPR_REWARD_BLOCK)
     return fail(CPR_E_INVALID_ARG, "'" + std::to_string(c->reward_scheme) +
                                        "' is not a valid parameter choice, try 'block' or 'constant'");
-  if (c->policy < CPR_BK_POLICY_HONEST || c->policy > CPR_BK_POLICY_TABLE)
+  if (c->policy < CPR_BK_POLICY_HONEST || c->policy > CPR_BK_POLICY_RANDOM)
     return fail(CPR_E_INVALID_ARG, "unknown policy");
+  if (c->policy == CPR_BK_POLICY_RANDOM && c->mode != CPR_MODE_LOOP)
+    return fail(CPR_E_UNSUPPORTED, random_policy_msg);
   memset(P, 0, sizeof(*P));
   if (c->policy == CPR_BK_POLICY_TABLE) {
     const int64_t D = c->policy_table_dim;
@@ -627,8 +638,10 @@ static int validate_ts(const cpr_config* c, ts::TsParams* P) {
     return fail(CPR_E_INVALID_ARG, "'" + std::to_string(c->subblock_selection) +
                                        "' is not a valid parameter choice, try 'altruistic', "
                                        "'heuristic' or 'optimal'");
-  if (c->policy < CPR_TS_POLICY_HONEST || c->policy > CPR_TS_POLICY_TABLE)
+  if (c->policy < CPR_TS_POLICY_HONEST || c->policy > CPR_TS_POLICY_RANDOM)
     return fail(CPR_E_INVALID_ARG, "unknown policy");
+  if (c->policy == CPR_TS_POLICY_RANDOM && c->mode != CPR_MODE_LOOP)
+    return fail(CPR_E_UNSUPPORTED, random_policy_msg);
   if (c->policy == CPR_TS_POLICY_TABLE) {
     const int64_t D = c->policy_table_dim;
     if (!c->policy_table || D <= 0 || D > 64)

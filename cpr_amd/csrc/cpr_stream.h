@@ -27,6 +27,9 @@ constexpr uint32_t TAG_ACT = 0u;
 constexpr uint32_t TAG_LINK = 0x10000000u;
 constexpr uint32_t TAG_POW = 0x20000000u;
 constexpr uint32_t TAG_MSG = 0x30000000u;
+// random attacker actions (cpr_protocols.ml:658-782, Random.int A.Action.n): decision i of
+// an episode draws word 0 of block (i, TAG_RAND) (oracle/src/keyed_stream.h rand_action)
+constexpr uint32_t TAG_RAND = 0x50000000u;
 
 struct Words4 {
   uint32_t w0, w1, w2, w3;
@@ -186,6 +189,10 @@ struct Stream {
   __host__ __device__ inline int32_t pow(uint32_t serial) const {
     return (int32_t)(block(serial, TAG_POW).w0 & 0x3FFFFFFFu);
   }
+  // the i-th random attacker action among n (integer multiply-high)
+  __host__ __device__ inline int32_t rand_act(uint32_t i, uint32_t n) const {
+    return (int32_t)(((uint64_t)block(i, TAG_RAND).w0 * (uint64_t)n) >> 32);
+  }
   // miner of activation j for arbitrary compute weights (honest cliques): the first node
   // i with w0 < thr[i] (thr: n - 1 cumulative thresholds, see cpr_weight_thresholds)
   __host__ __device__ inline int32_t miner_w(uint32_t j, const uint32_t* thr, int32_t nthr) const {
@@ -310,6 +317,11 @@ struct TraceStream {
   __host__ __device__ inline double link_exp(uint32_t kw, uint32_t off, uint32_t dest,
                                              double) const {
     return lookup(trace_link_key(kw, off, dest));
+  }
+  // traces hold no policy draws (a random attacker cannot be replayed from one)
+  __host__ __device__ inline int32_t rand_act(uint32_t, uint32_t) const {
+    miss = 1u;
+    return 0;
   }
 };
 

@@ -217,6 +217,9 @@ __host__ __device__ inline int32_t eth_policy(int32_t policy, const EthObs& o) {
 // table-driven ethereum_ssz policy (include/cpr_hip.h CPR_ETH_POLICY_TABLE): action =
 // table[(min(public_height, D-1) * D + min(private_height, D-1)) * 2 + event], 0..23
 constexpr int32_t ETH_POLICY_TABLE = 5;
+// random actions (loop tasks; cpr_protocols.ml:658-782): CPR_ETH_POLICY_RANDOM, and
+// CPR_POLICY_RANDOM for the nakamoto_ssz attacker of the Nakamoto mode
+constexpr int32_t ETH_POLICY_RANDOM = 6, NAK_POLICY_RANDOM = 5;
 __host__ __device__ inline int32_t eth_table_index(const EthObs& o, int32_t D) {
   auto cl = [](int32_t x, int32_t hi) { return x < 0 ? 0 : (x > hi ? hi : x); };
   return (cl(o.public_height, D - 1) * D + cl(o.private_height, D - 1)) * 2 + o.event;
@@ -264,6 +267,7 @@ struct EthLane {
   int32_t pub, priv, pending, own, foreign;
   int32_t o_pub, o_priv, o_common, o_event;
   int64_t steps;
+  int32_t nrand;  // random-policy decisions so far (the keyed draw's index)
 
   // ------------------------------------------------------------------ storage
   __host__ __device__ inline void fail(int32_t why) {
@@ -862,6 +866,7 @@ struct EthLane {
     status = 0u;
     dead = 0;
     steps = 0;
+    nrand = 0;
     dr_node = -1;
     EBlock& r = M.blk[0];
     r.serial = 0;
@@ -911,8 +916,15 @@ struct EthLane {
         if (node == 0 && P.net != 2) {
           // loop mode: the attacker node's handler (ethereum_ssz.ml:433-441)
           prepare(P, M, kind, s);
-          const EthObs o = observe(P, M, false);
-          const int32_t sh = apply(P, M, lane_action(P, o));
+          int32_t a;
+          if (P.policy == (P.nak ? NAK_POLICY_RANDOM : ETH_POLICY_RANDOM)) {
+            constexpr int32_t nmap[4] = {A_ADOPT_DISCARD, A_OVERRIDE, A_MATCH, A_WAIT};
+            a = P.nak ? nmap[S.rand_act((uint32_t)nrand++, 4u)] * 4
+                      : S.rand_act((uint32_t)nrand++, 24u);
+          } else {
+            a = lane_action(P, observe(P, M, false));
+          }
+          const int32_t sh = apply(P, M, a);
           if (sh >= 0) share(P, M, 0, sh);
           break;
         }

@@ -161,8 +161,13 @@ __global__ __launch_bounds__(kBlock) CPR_EV_OCC void k_eth_run_episodes(
 // again from its first draw on the event engine at the next synchronization point). Every
 // gym episode has max_steps steps (no progress / time limit: the host routes only those
 // here), so the lanes of a wave run the same number of windows.
+#ifdef CPR_EW_WAVES  // occupancy A/B (tools/build_variants.py --ew)
+#define CPR_EW_OCC __attribute__((amdgpu_waves_per_eu(CPR_EW_WAVES)))
+#else
+#define CPR_EW_OCC
+#endif
 template <int REC>
-__global__ __launch_bounds__(kBlock) void k_eth_win_episodes(
+__global__ __launch_bounds__(kBlock) CPR_EW_OCC void k_eth_win_episodes(
     eth::EthParams P, SeedSource src, int64_t n_eps, uint8_t* mem, int64_t lane_bytes,
     cpr_episode_record* recs, cpr_summary* sum, int64_t* redo, uint32_t* redo_n,
     uint32_t launch_id, int64_t redo_cap) {

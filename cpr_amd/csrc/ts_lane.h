@@ -215,6 +215,8 @@ __host__ __device__ inline int32_t ts_policy(int32_t policy, int32_t k, const Ts
 // layout: table[((((min(pub,D-1)*D + min(priv,D-1))*(k+1) + min(public_votes,k))*(k+1)
 // + min(private_votes_inclusive,k))*3 + event], Action8
 constexpr int32_t TS_POLICY_TABLE = 7;
+// random actions (loop tasks; cpr_protocols.ml:658-782): CPR_TS_POLICY_RANDOM
+constexpr int32_t TS_POLICY_RANDOM = 8;
 __host__ __device__ inline int32_t ts_table_index(const TsObs& o, int32_t D, int32_t k) {
   auto cl = [](int32_t x, int32_t hi) { return x < 0 ? 0 : (x > hi ? hi : x); };
   const int32_t K1 = k + 1;
@@ -249,6 +251,7 @@ __host__ __device__ inline int64_t ocaml_nck(int64_t n, int64_t k, bool* dz) {
 }
 
 struct TsLane {
+  int32_t nrand;  // random-policy decisions so far (the keyed draw's index)
   double now;
   int32_t c_act, newest, nsum, act0;
   int32_t hroot, hfree, hused;
@@ -1208,6 +1211,7 @@ struct TsLane {
   template <class St>
   __host__ __device__ inline void init(const TsParams& P, const St& S, const TsMem& M) {
     now = 0.0;
+    nrand = 0;
     c_act = 0;
     newest = 0;
     nsum = 0;
@@ -1294,7 +1298,9 @@ struct TsLane {
       case EV_ON: {
         if (node == 0 && P.net != 2) {  // loop mode: the attacker's handler (tailstorm_ssz.ml:353-362)
           prepare(P, M, kind, s);
-          if (!dead) apply(P, M, ts_policy_p(P, observe(P, M)));
+          if (!dead)
+            apply(P, M, P.policy == TS_POLICY_RANDOM ? S.rand_act((uint32_t)nrand++, 8u)
+                                                     : ts_policy_p(P, observe(P, M)));
           break;
         }
         honest(P, M, node, s);

@@ -99,9 +99,11 @@ enum cpr_tailstorm_policy {
   CPR_TS_POLICY_AVOID_LOSS_A = 4, /* avoid_loss */
   CPR_TS_POLICY_AVOID_LOSS_B = 5, /* avoid_loss_alt2 */
   CPR_TS_POLICY_LONG_DELAY = 6,
-  CPR_TS_POLICY_TABLE = 7 /* Action8 = table[((((min(pub,D-1)*D + min(priv,D-1))*(k+1)
+  CPR_TS_POLICY_TABLE = 7, /* Action8 = table[((((min(pub,D-1)*D + min(priv,D-1))*(k+1)
                              + min(public_votes,k))*(k+1) + min(private_votes_inclusive,k))*3
                              + event] with D = policy_table_dim (the B_k layout) */
+  CPR_TS_POLICY_RANDOM = 8 /* loop tasks: a keyed random Action8 at every decision (the
+                              reference's random attacker, cpr_protocols.ml:658-782) */
 };
 
 /* policy ids of the bk_ssz attack space (bk_ssz.ml:346-415; "avoid-loss" is avoid_loss_alt) */
@@ -110,9 +112,11 @@ enum cpr_bk_policy {
   CPR_BK_POLICY_GET_AHEAD = 1,
   CPR_BK_POLICY_MINOR_DELAY = 2,
   CPR_BK_POLICY_AVOID_LOSS = 3,
-  CPR_BK_POLICY_TABLE = 4 /* action = table[((((min(pub,D-1)*D + min(priv,D-1))*(k+1)
+  CPR_BK_POLICY_TABLE = 4, /* action = table[((((min(pub,D-1)*D + min(priv,D-1))*(k+1)
                              + min(public_votes,k))*(k+1) + min(private_votes_inclusive,k))*3
                              + event] with D = policy_table_dim */
+  CPR_BK_POLICY_RANDOM = 5 /* loop tasks: a keyed random Action8 at every decision
+                              (cpr_protocols.ml:658-782) */
 };
 
 /* ssz_tools.ml:230-263 Action8, Variants.to_rank */
@@ -128,8 +132,10 @@ enum cpr_ethereum_policy {
   CPR_ETH_POLICY_SELFISH_DISCARD = 2,
   CPR_ETH_POLICY_FN19 = 3,
   CPR_ETH_POLICY_FN19PKEL = 4,
-  CPR_ETH_POLICY_TABLE = 5 /* action (0..23) = table[(min(public_height,D-1)*D
+  CPR_ETH_POLICY_TABLE = 5, /* action (0..23) = table[(min(public_height,D-1)*D
                               + min(private_height,D-1))*2 + event], D = policy_table_dim */
+  CPR_ETH_POLICY_RANDOM = 6 /* loop tasks: a keyed random action of 24 at every decision
+                               (cpr_protocols.ml:658-782) */
 };
 
 /* ethereum_ssz.ml:161-277: action = rank * 4 + own * 2 + foreign, rank in
@@ -174,7 +180,11 @@ enum cpr_policy {
   CPR_POLICY_SIMPLE = 1,
   CPR_POLICY_EYAL_SIRER_2014 = 2,
   CPR_POLICY_SAPIRSHTEIN_2016_SM1 = 3,
-  CPR_POLICY_TABLE = 4 /* action = table[(min(pub,D-1)*D + min(priv,D-1))*2 + event] */
+  CPR_POLICY_TABLE = 4, /* action = table[(min(pub,D-1)*D + min(priv,D-1))*2 + event] */
+  CPR_POLICY_RANDOM = 5 /* loop tasks on the event engine (cpr_protocols.ml:658-782): a keyed
+                           random action of 4 at every decision; the i-th decision of an
+                           episode draws word 0 of Philox block (i, 0x50000000) and takes
+                           (w0 * n) >> 32 (every protocol's *_POLICY_RANDOM likewise) */
 };
 
 /* nakamoto_ssz.ml:116-154, Variants.to_rank */

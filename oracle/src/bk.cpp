@@ -439,7 +439,8 @@ Action BkSszAgent::apply(int action) {
 
 Action BkSszAttackerNode::handler(Kind kd, Block* b) {
   agent.prepare(kd, b);
-  const int act = bk_policy(policy, agent.observe(), agent.k, table);
+  const int act = policy == BKPOL_RANDOM ? agent.sim->rng->rand_action(nrand++, 8)
+                                         : bk_policy(policy, agent.observe(), agent.k, table);
   return agent.apply(act);
 }
 

@@ -29,7 +29,7 @@ constexpr int BK_N_ACTIONS = 8;
 // this build's policy ids (bk_ssz.ml:346-415); BKPOL_AVOID_LOSS is `avoid_loss_alt`, the
 // function registered under "avoid-loss" (bk_ssz.ml:411-414)
 enum BkPolicy { BKPOL_HONEST = 0, BKPOL_GET_AHEAD = 1, BKPOL_MINOR_DELAY = 2,
-                BKPOL_AVOID_LOSS = 3, BKPOL_TABLE = 4 };
+                BKPOL_AVOID_LOSS = 3, BKPOL_TABLE = 4, BKPOL_RANDOM = 5 };
 
 // bk_ssz.ml:22-34, field order = record order; event: 0 Append, 1 ProofOfWork, 2 Network
 struct BkObs {
@@ -115,6 +115,7 @@ struct BkSszAgent {
 struct BkSszAttackerNode : NodeImpl {
   BkSszAgent agent;
   int policy = 0;
+  int nrand = 0;  // BKPOL_RANDOM decisions so far (Action8)
   const BkTable* table = nullptr;
   Draft puzzle_payload() override { return agent.puzzle_payload(); }
   Action handler(Kind k, Block* b) override;

@@ -309,6 +309,7 @@ struct RecordingSimRng : SimRng {
     return x;
   }
   double coin(int kw, int j) override { return inner->coin(kw, j); }
+  int rand_action(int i, int n) override { return inner->rand_action(i, n); }
 };
 
 struct ReplaySimRng : SimRng {
@@ -335,6 +336,10 @@ struct ReplaySimRng : SimRng {
     if (it != buf->link.end()) return it->second;
     buf->miss = 1;
     return 0.0;
+  }
+  int rand_action(int, int) override {  // traces hold no policy draws
+    buf->miss = 1;
+    return 0;
   }
 };
 
@@ -860,7 +865,8 @@ Action NakSszAgent::apply(int action) {
 
 Action NakSszAttackerNode::handler(Kind k, Block* b) {
   agent.prepare(k, b);
-  int act = nak_policy(policy, agent.observe(), table);
+  int act = policy == POL_RANDOM ? agent.sim->rng->rand_action(nrand++, 4)
+                                 : nak_policy(policy, agent.observe(), table);
   return agent.apply(act);
 }
 

@@ -148,6 +148,13 @@ struct SimRng {
     (void)j;
     throw std::runtime_error("abstract-gamma coins need the keyed stream");
   }
+  // the i-th random attacker action among n (the `random` policy of the reference's policy
+  // tests, cpr_protocols.ml:658-782: Random.int A.Action.n at every decision)
+  virtual int rand_action(int i, int n) {
+    (void)i;
+    (void)n;
+    throw std::runtime_error("random attacker actions need the keyed or OCaml stream");
+  }
 };
 
 // OCaml Random: alias sampling exactly as distributions.ml:45-98
@@ -161,6 +168,7 @@ struct OcamlSimRng : SimRng {
   double act_delay(int j) override;
   int32_t pow_bits(int serial) override;
   double link_delay(const Link& l, const Block* msg) override;
+  int rand_action(int, int n) override { return r->int_(n); }  // Random.int, in stream order
 };
 
 // keyed Philox stream (keyed_stream.h); weights must be [alpha, equal rest]
@@ -177,6 +185,7 @@ struct KeyedSimRng : SimRng {
   int32_t pow_bits(int serial) override;
   double link_delay(const Link& l, const Block* msg) override;
   double coin(int kw, int j) override { return ks.link_u((uint32_t)kw, 0u, (uint32_t)j); }
+  int rand_action(int i, int n) override { return ks.rand_action((uint32_t)i, n); }
 };
 
 // keyed miner draw by general weights iff the compute is not [alpha] + equal defenders
@@ -307,7 +316,8 @@ struct NakHonest : NodeImpl {
   Block* preferred() override { return state; }
 };
 
-enum Policy { POL_HONEST = 0, POL_SIMPLE = 1, POL_ES2014 = 2, POL_SM1 = 3, POL_TABLE = 4 };
+enum Policy { POL_HONEST = 0, POL_SIMPLE = 1, POL_ES2014 = 2, POL_SM1 = 3, POL_TABLE = 4,
+              POL_RANDOM = 5 };
 // nakamoto_ssz.ml:116-154 — Variants.to_rank
 enum NakAction { ADOPT = 0, OVERRIDE = 1, MATCH = 2, WAIT = 3 };
 
@@ -347,6 +357,7 @@ struct NakSszAgent {
 struct NakSszAttackerNode : NodeImpl {
   NakSszAgent agent;
   int policy;
+  int nrand = 0;  // POL_RANDOM decisions so far
   const TablePolicy* table = nullptr;
   Draft puzzle_payload() override { return agent.puzzle_payload(); }
   Action handler(Kind k, Block* b) override;

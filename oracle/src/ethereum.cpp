@@ -248,6 +248,7 @@ Action EthSszAgent::apply(int index) {
 
 Action EthSszAttackerNode::handler(Kind k, Block* b) {
   agent.prepare(k, b);
+  if (policy == ETH_POL_RANDOM) return agent.apply(agent.sim->rng->rand_action(nrand++, 24));
   return agent.apply(eth_policy(policy, agent.observe(), table));
 }
 

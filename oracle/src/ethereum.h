@@ -36,6 +36,7 @@ int eth_policy(int policy, const EthObs& o);
 // table-driven policy (include/cpr_hip.h CPR_ETH_POLICY_TABLE): action =
 // table[(min(public_height, D-1) * D + min(private_height, D-1)) * 2 + event]
 constexpr int ETH_POL_TABLE = 5;
+constexpr int ETH_POL_RANDOM = 6;  // a random action of 24 per decision
 struct EthTable {
   int dim = 0;
   std::vector<uint8_t> actions;
@@ -87,6 +88,7 @@ struct EthSszAgent {
 struct EthSszAttackerNode : NodeImpl {
   EthSszAgent agent;
   int policy = 0;
+  int nrand = 0;  // ETH_POL_RANDOM decisions so far
   const EthTable* table = nullptr;
   Draft puzzle_payload() override { return agent.puzzle_payload(); }
   Action handler(Kind k, Block* b) override;

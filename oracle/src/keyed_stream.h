@@ -38,6 +38,9 @@ static const uint32_t TAG_ACT = 0u;
 static const uint32_t TAG_LINK = 0x10000000u;
 static const uint32_t TAG_POW = 0x20000000u;
 static const uint32_t TAG_MSG = 0x30000000u;
+// random attacker actions (cpr_protocols.ml:658-782 `Random.int A.Action.n`): the i-th
+// policy decision of an episode draws word 0 of block (i, TAG_RAND)
+static const uint32_t TAG_RAND = 0x50000000u;
 
 struct Philox4x32 {
   static void block(const uint32_t ctr_in[4], const uint32_t key_in[2], uint32_t out[4]) {
@@ -136,6 +139,12 @@ struct KeyedStream {
   void block(uint32_t idx, uint32_t tag, uint32_t out[4]) const {
     uint32_t ctr[4] = {ep[0], ep[1], idx, tag};
     Philox4x32::block(ctr, key, out);
+  }
+  // the i-th random attacker action among n (an integer multiply-high, no float)
+  int rand_action(uint32_t i, int n) const {
+    uint32_t w[4];
+    block(i, TAG_RAND, w);
+    return (int)(((uint64_t)w[0] * (uint64_t)n) >> 32);
   }
   // miner of activation j among [attacker] + d equal-weight defenders
   int miner(uint32_t j, uint64_t t_att, int d) const {

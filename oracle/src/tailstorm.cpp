@@ -662,6 +662,7 @@ Action TsSszAgent::apply(int action) {
 
 Action TsSszAttackerNode::handler(Kind kd, Block* b) {
   agent.prepare(kd, b);
+  if (policy == TS_POL_RANDOM) return agent.apply(agent.sim->rng->rand_action(nrand++, 8));
   return agent.apply(ts_policy(policy, agent.observe(), agent.k, table));
 }
 

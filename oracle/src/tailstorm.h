@@ -41,6 +41,7 @@ constexpr int TS_OBS_LEN = 10;
 int ts_policy(int policy, const TsObs& o, int k);
 // table-driven policy (include/cpr_hip.h CPR_TS_POLICY_TABLE, the B_k table layout)
 constexpr int TS_POL_TABLE = 7;
+constexpr int TS_POL_RANDOM = 8;  // a random Action8 per decision
 struct TsTable {
   int dim = 0;
   std::vector<uint8_t> actions;
@@ -140,6 +141,7 @@ struct TsSszAgent {
 struct TsSszAttackerNode : NodeImpl {
   TsSszAgent agent;
   int policy = 0;
+  int nrand = 0;  // TS_POL_RANDOM decisions so far
   const TsTable* table = nullptr;
   Draft puzzle_payload() override { return agent.puzzle_payload(); }
   Action handler(Kind k, Block* b) override;

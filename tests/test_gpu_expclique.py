@@ -138,3 +138,35 @@ def test_exp_clique_rejections(ctx):
         cfg, keep = device.make_config(**base)
         with pytest.raises(L.CprError, match=msg):
             device.Batch(cfg, ctx=ctx, keep=keep)
+
+
+# the reference's `random` policy tests (cpr_protocols.ml:658-782): node 0 takes a uniformly
+# random action of its attack space at every decision (the keyed draw of
+# include/cpr_hip.h CPR_*_POLICY_RANDOM), 3-node symmetric clique, activation delay 100,
+# exponential(1) links, 1000 activations, orphan rate <= 0.5
+from test_oracle_expclique import RANDOM_CASES  # noqa: E402
+
+
+@pytest.mark.parametrize("name,proto,pol,k,scheme,sel", RANDOM_CASES)
+def test_random_attacker_matches_oracle(ctx, name, proto, pol, k, scheme, sel):
+    cfg, keep = exp_clique(proto, 2, pol, 1000, k=k, scheme=scheme, sel=sel, ad=100.0, seed=9)
+    b = device.Batch(cfg, ctx=ctx, keep=keep)
+    n = 2048
+    s, rec = b.run(n, records=True)
+    assert not (rec["status"] & L.ST_INVALID).any(), name
+    ref = O.run_episodes(cfg, 0, 64, threads=8)
+    for f in FIELDS:
+        bad = np.nonzero(rec[f][:64] != ref[f])[0]
+        assert len(bad) == 0, (name, f, int(bad[0]), rec[f][bad[0]], ref[f][bad[0]])
+    orphan = (1000.0 - rec["progress"]) / 1000.0
+    assert orphan.max() <= 0.5, (name, orphan.max())
+    print(f"{name}: orphan rate mean {orphan.mean():.3f} max {orphan.max():.3f}")
+
+
+def test_random_attacker_rejected_in_gym(ctx):
+    # the gym's agent takes its actions from the caller (engine.ml), so a random policy
+    # there is the caller's; the device keeps the policy id for loop tasks
+    cfg, keep = device.make_config(alpha=0.3, gamma=0.5, policy=L.ETH_POLICY_RANDOM,
+                                   protocol=L.PROTO_ETHEREUM, max_steps=100)
+    with pytest.raises(L.CprError, match="random attacker"):
+        device.Batch(cfg, ctx=ctx, keep=keep)

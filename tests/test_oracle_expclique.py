@@ -47,3 +47,31 @@ def test_exp_clique_config():
     cfg, _ = exp_clique(L.PROTO_TAILSTORM, 1, L.TS_POLICY_HONEST, 100)
     assert cfg.network == L.NET_EXP_CLIQUE and cfg.defenders == 1
     assert cfg.propagation_delay == 1.0 and cfg.mode == L.MODE_LOOP
+
+
+# the reference's `random` policy tests (cpr_protocols.ml:658-782): node 0 takes a uniformly
+# random action of its attack space at every decision (Random.int A.Action.n; here the
+# keyed draw of include/cpr_hip.h *_POLICY_RANDOM), 3-node symmetric clique, activation
+# delay 100, exponential(1) links, 1000 activations; the orphan rate must stay <= 0.5
+RANDOM_CASES = [
+    ("nakamoto/random", L.PROTO_NAKAMOTO, L.POLICY_RANDOM, 8, L.REWARD_CONSTANT, 0),
+    ("ethereum/random", L.PROTO_ETHEREUM, L.ETH_POLICY_RANDOM, 8, L.REWARD_DISCOUNT, 0),
+    ("bk8/ssz/random", L.PROTO_BK, L.BK_POLICY_RANDOM, 8, L.REWARD_BLOCK, 0),
+    ("tailstorm8constant/ssz/random", L.PROTO_TAILSTORM, L.TS_POLICY_RANDOM, 8,
+     L.REWARD_CONSTANT, L.SELECT_OPTIMAL),
+    ("tailstorm8discount/ssz/random", L.PROTO_TAILSTORM, L.TS_POLICY_RANDOM, 8,
+     L.REWARD_DISCOUNT, L.SELECT_HEURISTIC),
+]
+
+
+@pytest.mark.parametrize("name,proto,pol,k,scheme,sel", RANDOM_CASES)
+def test_random_attacker_orphan_limit(name, proto, pol, k, scheme, sel):
+    cfg, _ = exp_clique(proto, 2, pol, 1000, k=k, scheme=scheme, sel=sel, ad=100.0, seed=9)
+    rec = O.run_episodes(cfg, 0, 32, threads=8)
+    assert not (rec["status"] & L.ST_INVALID).any(), name
+    orphan = (1000.0 - rec["progress"]) / 1000.0
+    assert orphan.max() <= 0.5, (name, orphan.max())
+    # the draws are the keyed stream's: another seed gives other episodes
+    cfg2, _ = exp_clique(proto, 2, pol, 1000, k=k, scheme=scheme, sel=sel, ad=100.0, seed=10)
+    rec2 = O.run_episodes(cfg2, 0, 8, threads=8)
+    assert not np.array_equal(rec2["reward_attacker"], rec["reward_attacker"][:8]), name

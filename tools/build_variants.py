@@ -1,8 +1,9 @@
 """Occupancy variants of libcpr_hip for A/B runs (tools/occupancy_ab.sh): the three
 event-engine translation units rebuilt with -DCPR_EV_WAVES=<w> (kernels.h), linked with the
-default build's other objects into build/var/ev<w>.so. Run __graft_entry__.build() first.
+default build's other objects into build/var/ev<w>.so; with --ew, -DCPR_EW_WAVES=<w> (the
+Ethereum window lane's kernel) into build/var/ew<w>.so. Run __graft_entry__.build() first.
 
-Usage: python tools/build_variants.py 2 4
+Usage: python tools/build_variants.py 2 4;  python tools/build_variants.py --ew 3 4
 """
 import pathlib
 import subprocess
@@ -20,12 +21,16 @@ def main():
     out = ROOT / "build" / "var"
     out.mkdir(parents=True, exist_ok=True)
     flags = [f for f in G.HIPCC_FLAGS if f != "-shared"]
-    for w in sys.argv[1:]:
-        vdir = out / f"ev{w}"
+    args = sys.argv[1:]
+    macro, tag = "CPR_EV_WAVES", "ev"
+    if args and args[0] == "--ew":
+        macro, tag, args = "CPR_EW_WAVES", "ew", args[1:]
+    for w in args:
+        vdir = out / f"{tag}{w}"
         vdir.mkdir(exist_ok=True)
         procs = []
         for s in EV:
-            cmd = [G._hipcc(), *flags, f"-DCPR_EV_WAVES={w}", f"-I{ROOT / 'include'}", "-c",
+            cmd = [G._hipcc(), *flags, f"-D{macro}={w}", f"-I{ROOT / 'include'}", "-c",
                    str(G.CSRC / s), "-o", str(vdir / (s + ".o"))]
             procs.append(subprocess.Popen(cmd))
         for p in procs:
@@ -33,8 +38,8 @@ def main():
         objs = [str((vdir if s in EV else objdir) / (s + ".o"))
                 for s in ["kernels.hip", *EV, "kernels_fc16.hip", "capi.hip"]]
         subprocess.run([G._hipcc(), "--offload-arch=gfx950", "-shared", "-fPIC", *objs, "-o",
-                        str(out / f"ev{w}.so")], check=True)
-        print("built", out / f"ev{w}.so")
+                        str(out / f"{tag}{w}.so")], check=True)
+        print("built", out / f"{tag}{w}.so")
 
 
 if __name__ == "__main__":

@@ -16,3 +16,7 @@ timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/p
 step $? pmc_fetch || exit 1
 timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/prof_pmc_write -o run -- python3 bench.py $ARGS > gpurun_out/prof_pmc_write.log 2>&1
 step $? pmc_write || exit 1
+# LDS evidence for the deferred-race kernel (gamma = .5: race lists in LDS): LDS
+# instructions and bank-conflict cycles, in a pass of their own
+timeout -k 10 400 rocprofv3 --pmc SQ_WAVES SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_VALU --output-format csv -d gpurun_out/prof_pmc_lds -o run -- python3 bench.py $ARGS > gpurun_out/prof_pmc_lds.log 2>&1
+step $? pmc_lds || exit 1
