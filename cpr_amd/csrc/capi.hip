@@ -69,6 +69,12 @@ struct cpr_ctx {
   // episode-kernel launch since then
   DevBuf rq, rtab, rmem;
   std::vector<RerunLaunch> rlaunch, rlaunch_up;
+  // entries a launch may append (kRerunQueue; CPR_RERUN_QUEUE_CAP lowers it for tests);
+  // an episode that finds the queue full waits in its launch's overflow flags: one byte
+  // per episode of every launch since the last flush, carved from `ovf`
+  int64_t rq_cap = kRerunQueue;
+  DevBuf ovf;
+  size_t ovf_used = 0;
   // per-lane scratch regions of fused-episode launches (event-engine rings and heaps, the
   // Nakamoto lane's spill / time log / tie-replay scratch), shared by every batch of the
   // context: launches on the context's stream run in order, so one grow-only pool serves an
@@ -884,10 +890,11 @@ static int flush_reruns(cpr_ctx* c) {
   HIP_TRY(hipMemcpyAsync(c->rtab.p, c->rlaunch_up.data(), tb, hipMemcpyHostToDevice, c->stream));
   HIP_TRY(c->rmem.ensure((size_t)kRerunLanes * (size_t)lb));
   uint32_t* qn = (uint32_t*)((char*)c->rq.p + (size_t)kRerunQueue * 8);
-  HIP_TRY(launch_nak_exact_rerun((const RerunLaunch*)c->rtab.p, (const int64_t*)c->rq.p, qn,
-                                 kRerunQueue, (uint8_t*)c->rmem.p, lb, rest, kRerunLanes,
-                                 c->stream));
+  HIP_TRY(launch_nak_exact_rerun((const RerunLaunch*)c->rtab.p, (int64_t)c->rlaunch_up.size(),
+                                 (const int64_t*)c->rq.p, qn, c->rq_cap, (uint8_t*)c->rmem.p,
+                                 lb, rest, kRerunLanes, c->stream));
   HIP_TRY(hipMemsetAsync(qn, 0, 4, c->stream));
+  c->ovf_used = 0;  // the next launches' flags follow these re-runs on the stream
   return CPR_OK;
 }
 
@@ -897,13 +904,31 @@ static int flush_reruns(cpr_ctx* c) {
 // the kernel appends (launch_id << 40) | (episode << 8) | flags to the queue
 static int register_rerun(cpr_batch* b, const eth::EthParams& EP, int64_t lane_bytes,
                           uint64_t first, const TraceSource* tr, cpr_episode_record* rec_dev,
-                          cpr_summary* sum_dev, int64_t** redo, uint32_t** redo_n,
-                          uint32_t* launch_id) {
+                          cpr_summary* sum_dev, int64_t n_eps, int64_t** redo,
+                          uint32_t** redo_n, uint32_t* launch_id, uint8_t** ovf) {
   cpr_ctx* c = b->ctx;
-  if (c->rlaunch.size() >= kRerunMaxLaunches) {
+  const size_t need = align256((size_t)std::max<int64_t>(1, n_eps));
+  // tests force a small queue (CPR_RERUN_QUEUE_CAP) to exercise the overflow flags; a new
+  // capacity takes effect at a flush (all launches of one flush share it)
+  int64_t cap = kRerunQueue;
+  if (const char* v = getenv("CPR_RERUN_QUEUE_CAP"))
+    cap = std::max<int64_t>(0, std::min<int64_t>(kRerunQueue, atoll(v)));
+  if (cap != c->rq_cap) {
+    int rc = flush_reruns(c);
+    if (rc) return rc;
+    c->rq_cap = cap;
+  }
+  if (c->rlaunch.size() >= kRerunMaxLaunches || c->ovf_used + need > c->ovf.bytes) {
     int rc = flush_reruns(c);
     if (rc) return rc;
   }
+  if (need > c->ovf.bytes) {
+    HIP_TRY(hipStreamSynchronize(c->stream));  // earlier re-runs may still read the flags
+    HIP_TRY(c->ovf.ensure(std::max(need, (size_t)64 << 20)));
+  }
+  *ovf = (uint8_t*)c->ovf.p + c->ovf_used;
+  HIP_TRY(hipMemsetAsync(*ovf, 0, need, c->stream));
+  c->ovf_used += need;
   if (!c->rq.p) {
     HIP_TRY(c->rq.ensure((size_t)kRerunQueue * 8 + 64));
     // launch counter and the cumulative HBM-retry counter (cpr_rerun_hbm_retries)
@@ -920,6 +945,8 @@ static int register_rerun(cpr_batch* b, const eth::EthParams& EP, int64_t lane_b
   rl.recs = rec_dev;
   rl.sum = sum_dev;
   rl.lane_bytes = lane_bytes;
+  rl.ovf = *ovf;
+  rl.n_eps = n_eps;
   *launch_id = (uint32_t)c->rlaunch.size();
   c->rlaunch.push_back(rl);
   *redo = (int64_t*)c->rq.p;
@@ -957,13 +984,14 @@ static int run_async_ethwin(cpr_batch* b, int64_t n, uint64_t first, cpr_summary
   int64_t* redo = nullptr;
   uint32_t* redo_n = nullptr;
   uint32_t launch_id = 0;
-  const int rc = register_rerun(b, b->EP, b->eth_bytes, first, nullptr, rec_dev, sum_dev, &redo,
-                                &redo_n, &launch_id);
+  uint8_t* ovf = nullptr;
+  const int rc = register_rerun(b, b->EP, b->eth_bytes, first, nullptr, rec_dev, sum_dev, n,
+                                &redo, &redo_n, &launch_id, &ovf);
   if (rc) return rc;
   HIP_TRY(hipEventRecord(b->ev0, b->ctx->stream));
   HIP_TRY(launch_eth_win_episodes(b->EP, b->cfg.seed, first, n, (uint8_t*)mem, wbytes, lanes,
-                                  rec_dev, sum_dev, redo, redo_n, launch_id, kRerunQueue,
-                                  b->ctx->stream));
+                                  rec_dev, sum_dev, redo, redo_n, launch_id, b->ctx->rq_cap,
+                                  ovf, b->ctx->stream));
   HIP_TRY(hipEventRecord(b->ev1, b->ctx->stream));
   return CPR_OK;
 }
@@ -1081,20 +1109,21 @@ static int run_async(cpr_batch* b, int64_t n, uint64_t first, const TraceSource*
   int64_t* redo = nullptr;
   uint32_t* redo_n = nullptr;
   uint32_t launch_id = 0;
+  uint8_t* ovf = nullptr;
   if (b->has_rerun) {
-    const int rc = register_rerun(b, b->NEP, b->nak_bytes, first, tr, rec_dev, sum_dev, &redo,
-                                  &redo_n, &launch_id);
+    const int rc = register_rerun(b, b->NEP, b->nak_bytes, first, tr, rec_dev, sum_dev, n,
+                                  &redo, &redo_n, &launch_id, &ovf);
     if (rc) return rc;
   }
   HIP_TRY(hipEventRecord(b->ev0, b->ctx->stream));
   if (tr)
     HIP_TRY(launch_replay_episodes(b->P, *tr, n, b->cfg.mode, b->cfg.activations,
                                    spill, replay, lanes, rec_dev, sum_dev, redo, redo_n,
-                                   launch_id, kRerunQueue, b->ctx->stream));
+                                   launch_id, b->ctx->rq_cap, ovf, b->ctx->stream));
   else
     HIP_TRY(launch_run_episodes(b->P, b->cfg.seed, first, n, b->cfg.mode, b->cfg.activations,
                                 spill, replay, list, lanes, rec_dev, sum_dev, redo, redo_n,
-                                launch_id, kRerunQueue, b->ctx->stream));
+                                launch_id, b->ctx->rq_cap, ovf, b->ctx->stream));
   HIP_TRY(hipEventRecord(b->ev1, b->ctx->stream));
   return CPR_OK;
 }
@@ -1413,14 +1442,20 @@ static int ensure_lockstep(cpr_batch* b) {
   }
   if (b->has_rerun && !b->l_alog.p) {
     // lanes leaving the closed form continue on the exact engine: an action log of the
-    // episode so far (at most 2^14 steps, <= 1 GiB) and kExactSlots event-engine lanes,
-    // handed out on first need and returned at the lane's next reset
-    constexpr int64_t kExactSlots = 256;
-    const int64_t ms = b->P.max_steps > 0 ? b->P.max_steps : (1 << 14);
-    int64_t cap = std::min<int64_t>(ms, 1 << 14);
-    cap = std::max<int64_t>(1, std::min<int64_t>(cap, (1ll << 30) / n));
+    // episode so far and event-engine lanes handed out on first need and returned at the
+    // lane's next reset. Every lane gets a slot and a log of its whole episode when they
+    // fit the budgets (kExactSlotBudget of slots: 65,536 lanes of 2,016-step episodes
+    // take ~27 GB of the 288 GB; kActionLogBudget of logs), so the lockstep API stays
+    // exact for every lane like engine.ml's step (engine.ml:176-249); beyond the budgets
+    // (lanes x episode length), a lane that finds no slot keeps the closed form's flags
+    constexpr int64_t kExactSlotBudget = 48ll << 30, kActionLogBudget = 4ll << 30;
+    const int64_t ms = b->P.max_steps > 0 && b->P.max_steps < (1ll << 30) ? b->P.max_steps
+                                                                          : (1 << 14);
+    int64_t cap = std::min<int64_t>(ms, std::max<int64_t>(1 << 14, kActionLogBudget / n));
+    cap = std::max<int64_t>(1, cap);
     b->alog_cap = cap;
-    b->n_exact_slots = (int32_t)std::min<int64_t>(n, kExactSlots);
+    b->n_exact_slots = (int32_t)std::min<int64_t>(
+        n, std::max<int64_t>(256, kExactSlotBudget / std::max<int64_t>(1, b->nak_bytes)));
     HIP_TRY(b->l_alog.ensure((size_t)n * (size_t)cap));
     HIP_TRY(b->l_emem.ensure((size_t)b->n_exact_slots * (size_t)b->nak_bytes));
     HIP_TRY(b->l_eslots.ensure((size_t)b->n_exact_slots * sizeof(eth::EthLane)));

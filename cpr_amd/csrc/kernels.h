@@ -83,7 +83,7 @@ hipError_t launch_run_episodes(const NakParams& P, uint64_t seed, uint64_t first
                                uint8_t* replay, int64_t* list, int64_t lanes,
                                cpr_episode_record* recs, cpr_summary* sum, int64_t* redo,
                                uint32_t* redo_n, uint32_t launch_id, int64_t redo_cap,
-                               hipStream_t st);
+                               uint8_t* ovf, hipStream_t st);
 int64_t run_episodes_list_bytes(const NakParams& P, int32_t mode, bool recs, int64_t n_eps);
 // the same fused kernel drawing from a device copy of a cpr_trace (cpr_replay)
 hipError_t launch_replay_episodes(const NakParams& P, const TraceSource& src, int64_t n_eps,
@@ -91,7 +91,7 @@ hipError_t launch_replay_episodes(const NakParams& P, const TraceSource& src, in
                                   uint8_t* replay, int64_t lanes,
                                   cpr_episode_record* recs, cpr_summary* sum, int64_t* redo,
                                   uint32_t* redo_n, uint32_t launch_id, int64_t redo_cap,
-                                  hipStream_t st);
+                                  uint8_t* ovf, hipStream_t st);
 // EP: the batch's Ethereum lane in Nakamoto mode (observations of lanes on the exact engine)
 hipError_t launch_reset(const NakParams& P, const eth::EthParams& EP, uint64_t seed,
                         const LockBuffers& B, int64_t n, const uint8_t* mask, const uint64_t* eps,
@@ -144,7 +144,7 @@ hipError_t launch_eth_win_episodes(const eth::EthParams& P, uint64_t seed, uint6
                                    int64_t n_eps, uint8_t* mem, int64_t lane_bytes,
                                    int64_t lanes, cpr_episode_record* recs, cpr_summary* sum,
                                    int64_t* redo, uint32_t* redo_n, uint32_t launch_id,
-                                   int64_t redo_cap, hipStream_t st);
+                                   int64_t redo_cap, uint8_t* ovf, hipStream_t st);
 int eth_win_blocks_per_cu(bool recs);
 // Ethereum lockstep lanes: mem = n x lane_bytes; slots = n x eth_slot_bytes()
 hipError_t launch_eth_reset(const eth::EthParams& P, uint64_t seed, uint8_t* mem,
@@ -180,15 +180,21 @@ struct RerunLaunch {
   cpr_episode_record* recs;
   cpr_summary* sum;
   int64_t lane_bytes;
+  // overflow flags [n_eps] (zeroed at registration): a flagged episode that found the
+  // queue full writes 0x80 | its status bits here instead (k_rerun_overflow re-runs it)
+  uint8_t* ovf;
+  int64_t n_eps;
 };
 
 // all queued re-runs (count on the device) in one launch of `lanes` one-wave workgroups,
 // each with a lane region of lane_bytes at mem + i x lane_bytes; lds_bytes (the largest
-// eth_rest_bytes of the launches, capped at 160 KiB) puts all but the block ring in LDS
-hipError_t launch_nak_exact_rerun(const RerunLaunch* launches, const int64_t* queue,
-                                  const uint32_t* queue_n, int64_t queue_cap, uint8_t* mem,
-                                  int64_t lane_bytes, int64_t lds_bytes, int64_t lanes,
-                                  hipStream_t st);
+// eth_rest_bytes of the launches, capped at 160 KiB) puts all but the block ring in LDS;
+// then, only if the queue overflowed (count > queue_cap), the overflow flags of every
+// launch (k_rerun_overflow on the same lane regions)
+hipError_t launch_nak_exact_rerun(const RerunLaunch* launches, int64_t n_launches,
+                                  const int64_t* queue, const uint32_t* queue_n,
+                                  int64_t queue_cap, uint8_t* mem, int64_t lane_bytes,
+                                  int64_t lds_bytes, int64_t lanes, hipStream_t st);
 
 // B_k (kernels_bk.hip): mem = lanes x lane_bytes; lockstep slots = n x bk_slot_bytes()
 hipError_t launch_bk_run_episodes(const bk::BkParams& P, uint64_t seed, uint64_t first,

@@ -133,7 +133,8 @@ template <int MODE, class Src, int POL, int REC = 1, int ARR = -1, int TT = 0>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ARR == 0 ? CPR_G0_WAVES : (TT ? 5 : 4)))) void k_run_episodes(
     NakParams P, Src src, int64_t n_eps, int64_t activations,
     double* spill, uint8_t* replay, cpr_episode_record* recs, cpr_summary* sum,
-    int64_t* redo, uint32_t* redo_n, uint32_t launch_id, int64_t redo_cap, int64_t* list) {
+    int64_t* redo, uint32_t* redo_n, uint32_t launch_id, int64_t redo_cap, int64_t* list,
+    uint8_t* ovf) {
   // the race lists take the LDS ring, which only the summary-only kernels leave free
   static_assert(TT != 2 || REC == 0, "deferred races need the summary-only kernel");
   if (ARR >= 0) P.arrive = ARR;
@@ -199,9 +200,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ARR == 0
       const uint32_t r = atomicAdd(redo_n, 1u);
       if ((int64_t)r < redo_cap) {
         redo[r] = ((int64_t)launch_id << 40) | (src.index(e) << 8) | (int64_t)(status & 0xffu);
-        continue;
+      } else {
+        // queue full: the episode waits in the launch's overflow flags, which the re-run
+        // pass scans after the queue (k_rerun_overflow)
+        ovf[src.index(e)] = (uint8_t)(0x80u | (status & 0x7fu));
       }
-      st_out |= CPR_ST_CAPACITY;  // queue full: the flagged outputs stay, marked invalid
+      continue;
     } else if (P.abstract_g && (status & kInexact) != 0u) {
       st_out |= CPR_ST_CAPACITY;  // the exact event engine has no abstract-gamma mode
     }
@@ -487,7 +491,7 @@ __global__ void k_stream_fill(uint64_t seed, uint64_t ep, uint32_t idx0, uint32_
 // tasks run the generic kernel. Template arguments do not change the signature.
 using RunFn = void (*)(NakParams, SeedSource, int64_t, int64_t, double*, uint8_t*,
                        cpr_episode_record*, cpr_summary*, int64_t*, uint32_t*, uint32_t, int64_t,
-                       int64_t*);
+                       int64_t*, uint8_t*);
 // deferred races (TT = 2) pay where the release always reaches the non-miner defender no
 // later than the defender block (dmax <= delta: the gym's gamma <= .5 networks), so that a
 // verification almost never sends an episode to the second pass; they need release indices
@@ -500,7 +504,7 @@ static bool deferred_races_ok(const NakParams& P) {
 }
 using ListFn = void (*)(NakParams, ListSource, int64_t, int64_t, double*, uint8_t*,
                         cpr_episode_record*, cpr_summary*, int64_t*, uint32_t*, uint32_t, int64_t,
-                        int64_t*);
+                        int64_t*, uint8_t*);
 template <int POL>
 static RunFn gym_run_fn(const NakParams& P, bool recs, bool defer, ListFn* second) {
   if (recs) return k_run_episodes<CPR_MODE_GYM, SeedSource, POL, 1, -1>;
@@ -529,7 +533,7 @@ hipError_t launch_run_episodes(const NakParams& P, uint64_t seed, uint64_t first
                                uint8_t* replay, int64_t* list, int64_t lanes,
                                cpr_episode_record* recs, cpr_summary* sum, int64_t* redo,
                                uint32_t* redo_n, uint32_t launch_id, int64_t redo_cap,
-                               hipStream_t st) {
+                               uint8_t* ovf, hipStream_t st) {
   const unsigned blocks = (unsigned)(lanes / kBlock);
   const SeedSource src{seed, first};
   ListFn second = nullptr;
@@ -542,14 +546,14 @@ hipError_t launch_run_episodes(const NakParams& P, uint64_t seed, uint64_t first
     if (er != hipSuccess) return er;
   }
   hipLaunchKernelGGL(fn, dim3(blocks), dim3(kBlock), 0, st, P, src, n_eps, activations, spill,
-                     replay, recs, sum, redo, redo_n, launch_id, redo_cap, list);
+                     replay, recs, sum, redo, redo_n, launch_id, redo_cap, list, ovf);
   if (second) {
     // a few episodes in a hundred: half the grid runs them in one round (more take more
     // rounds of the same grid-stride loop); blocks without an episode exit at once
     const ListSource ls{src, reinterpret_cast<const uint32_t*>(list), list + 1};
     const unsigned b2 = blocks / 2 > 0 ? blocks / 2 : 1;
     hipLaunchKernelGGL(second, dim3(b2), dim3(kBlock), 0, st, P, ls, n_eps, activations, spill,
-                       replay, recs, sum, redo, redo_n, launch_id, redo_cap, list);
+                       replay, recs, sum, redo, redo_n, launch_id, redo_cap, list, ovf);
   }
   return hipGetLastError();
 }
@@ -565,16 +569,16 @@ hipError_t launch_replay_episodes(const NakParams& P, const TraceSource& src, in
                                   uint8_t* replay, int64_t lanes,
                                   cpr_episode_record* recs, cpr_summary* sum, int64_t* redo,
                                   uint32_t* redo_n, uint32_t launch_id, int64_t redo_cap,
-                                  hipStream_t st) {
+                                  uint8_t* ovf, hipStream_t st) {
   const unsigned blocks = (unsigned)(lanes / kBlock);
   if (mode == CPR_MODE_GYM)
     hipLaunchKernelGGL((k_run_episodes<CPR_MODE_GYM, TraceSource, -1>), dim3(blocks), dim3(kBlock), 0,
                        st, P, src, n_eps, activations, spill, replay, recs, sum, redo, redo_n, launch_id, redo_cap,
-                       nullptr);
+                       nullptr, ovf);
   else
     hipLaunchKernelGGL((k_run_episodes<CPR_MODE_LOOP, TraceSource, -1>), dim3(blocks), dim3(kBlock),
                        0, st, P, src, n_eps, activations, spill, replay, recs, sum, redo, redo_n, launch_id, redo_cap,
-                       nullptr);
+                       nullptr, ovf);
   return hipGetLastError();
 }
 

@@ -170,7 +170,7 @@ template <int REC>
 __global__ __launch_bounds__(kBlock) CPR_EW_OCC void k_eth_win_episodes(
     eth::EthParams P, SeedSource src, int64_t n_eps, uint8_t* mem, int64_t lane_bytes,
     cpr_episode_record* recs, cpr_summary* sum, int64_t* redo, uint32_t* redo_n,
-    uint32_t launch_id, int64_t redo_cap) {
+    uint32_t launch_id, int64_t redo_cap, uint8_t* ovf) {
   __shared__ int32_t hist[CPR_HIST_BINS];
   __shared__ unsigned long long acc_w[13];
   LdsAcc acc{acc_w};
@@ -191,11 +191,11 @@ __global__ __launch_bounds__(kBlock) CPR_EW_OCC void k_eth_win_episodes(
     uint32_t status = W.status;
     if (status & ethw::W_REDO) {
       const uint32_t r = atomicAdd(redo_n, 1u);
-      if ((int64_t)r < redo_cap) {
+      if ((int64_t)r < redo_cap)
         redo[r] = ((int64_t)launch_id << 40) | (e << 8) | (int64_t)(status & 0xffu);
-        continue;
-      }
-      status |= CPR_ST_CAPACITY;  // queue full: the outputs stay, marked invalid
+      else  // queue full: the launch's overflow flags (k_rerun_overflow)
+        ovf[e] = (uint8_t)(0x80u | (status & 0x7fu));
+      continue;
     }
     const ethw::WBlock& h = W.B(P, M, hd);
     const int32_t ra = h.rew_att, rd = h.rew_def;
@@ -224,7 +224,7 @@ __global__ __launch_bounds__(kBlock) CPR_EW_OCC void k_eth_win_episodes(
 
 using EthWinFn = void (*)(eth::EthParams, SeedSource, int64_t, uint8_t*, int64_t,
                           cpr_episode_record*, cpr_summary*, int64_t*, uint32_t*, uint32_t,
-                          int64_t);
+                          int64_t, uint8_t*);
 static EthWinFn eth_win_fn(bool recs) {
   return recs ? k_eth_win_episodes<1> : k_eth_win_episodes<0>;
 }
@@ -233,10 +233,10 @@ hipError_t launch_eth_win_episodes(const eth::EthParams& P, uint64_t seed, uint6
                                    int64_t n_eps, uint8_t* mem, int64_t lane_bytes,
                                    int64_t lanes, cpr_episode_record* recs, cpr_summary* sum,
                                    int64_t* redo, uint32_t* redo_n, uint32_t launch_id,
-                                   int64_t redo_cap, hipStream_t st) {
+                                   int64_t redo_cap, uint8_t* ovf, hipStream_t st) {
   hipLaunchKernelGGL(eth_win_fn(recs != nullptr), dim3((unsigned)(lanes / kBlock)), dim3(kBlock),
                      0, st, P, SeedSource{seed, first}, n_eps, mem, lane_bytes, recs, sum, redo,
-                     redo_n, launch_id, redo_cap);
+                     redo_n, launch_id, redo_cap, ovf);
   return hipGetLastError();
 }
 
@@ -351,54 +351,89 @@ __device__ inline void nak_rerun_finish(const RerunLaunch& RL, int64_t e,
   }
 }
 
+// one flagged episode again on the event engine, lane region `base` (HBM) and lane_lds:
+// everything but the block ring (visibility, event heap, tips, scratch) in LDS. A lane
+// whose heap capacity does not fit runs with the capacity that does (the heap's node order
+// does not depend on it) and, only if its episode outgrows that, again in HBM. gamma = 0
+// re-runs are the case: +inf messages stay in the heap (ethereum_lane.h), a few thousand
+// nodes, whose dependent walks are L2 round trips in HBM
+__device__ inline void rerun_episode(const RerunLaunch& RL, int64_t e, uint32_t flags,
+                                     uint8_t* base, uint8_t* lane_lds, int64_t lds_bytes,
+                                     const uint32_t* queue_n) {
+  const eth::EthParams P = RL.P;
+  // attempt 0: LDS (full or reduced heap capacity); attempt 1 (only after the reduced
+  // heap overflowed): the lane's HBM region
+  int32_t lds_cap_e = -1;  // heap capacity in LDS, -1 = HBM
+  if (lds_bytes > 0) {
+    const int64_t heap = eth::align128((int64_t)P.cap_e * 24);
+    const int64_t other = eth::eth_rest_bytes(P.cap_b, P.cap_e, P.n) - heap;
+    const int64_t room = (lds_bytes - other) / 128 * 128;
+    if (room >= heap)
+      lds_cap_e = P.cap_e;
+    else if (room >= 256 * 24)
+      lds_cap_e = (int32_t)(room / 24);
+  }
+  for (int attempt = lds_cap_e < 0 ? 1 : 0; attempt < 2; ++attempt) {
+    eth::EthParams PA = P;
+    if (attempt == 0) PA.cap_e = lds_cap_e;
+    const eth::EthMem M = attempt == 0
+                              ? eth::eth_mem_split(base, lane_lds, PA.cap_b, PA.cap_e, PA.n)
+                              : eth::eth_mem_at(base, P.cap_b, P.cap_e, P.n);
+    eth::EthLane L;
+    uint32_t miss = 0;
+    const int32_t hd = nak_rerun_entry(RL, e, PA, M, L, &miss);
+    if (attempt == 0 && L.dead == 2 && PA.cap_e < P.cap_e) {  // outgrew LDS: count, redo
+      atomicAdd(const_cast<uint32_t*>(queue_n) + 1, 1u);  // cpr_rerun_hbm_retries
+      continue;
+    }
+    nak_rerun_finish(RL, e, P, M, L, hd, flags | miss);
+    break;
+  }
+}
+
 __global__ __launch_bounds__(64) void k_nak_exact_rerun(const RerunLaunch* launches,
                                                          const int64_t* queue,
                                                          const uint32_t* queue_n,
                                                          int64_t queue_cap, uint8_t* mem,
                                                          int64_t lane_bytes, int64_t lds_bytes) {
-  // everything but the block ring (visibility, event heap, tips, scratch) in LDS. A lane
-  // whose heap capacity does not fit runs with the capacity that does (the heap's node
-  // order does not depend on it) and, only if its episode outgrows that, again in HBM.
-  // gamma = 0 re-runs are the case: +inf messages stay in the heap (ethereum_lane.h), a
-  // few thousand nodes, whose dependent walks are L2 round trips in HBM
   extern __shared__ __attribute__((aligned(128))) uint8_t lane_lds[];
-  if (threadIdx.x != 0) return;
+  if (threadIdx.x != 0) return;  // one dependent chain per episode: lane 0 runs it
   int64_t nq = (int64_t)*queue_n;
   nq = nq < queue_cap ? nq : queue_cap;
+  uint8_t* base = mem + (int64_t)blockIdx.x * lane_bytes;
   for (int64_t r = blockIdx.x; r < nq; r += gridDim.x) {
     const int64_t q = queue[r];
-    const RerunLaunch& RL = launches[q >> 40];
-    const eth::EthParams P = RL.P;
-    const int64_t e = (q >> 8) & 0xffffffffll;
-    const uint32_t flags = (uint32_t)(q & 0xff);
-    uint8_t* base = mem + (int64_t)blockIdx.x * lane_bytes;
-    // attempt 0: LDS (full or reduced heap capacity); attempt 1 (only after the reduced
-    // heap overflowed): the lane's HBM region
-    int32_t lds_cap_e = -1;  // heap capacity in LDS, -1 = HBM
-    if (lds_bytes > 0) {
-      const int64_t heap = eth::align128((int64_t)P.cap_e * 24);
-      const int64_t other = eth::eth_rest_bytes(P.cap_b, P.cap_e, P.n) - heap;
-      const int64_t room = (lds_bytes - other) / 128 * 128;
-      if (room >= heap)
-        lds_cap_e = P.cap_e;
-      else if (room >= 256 * 24)
-        lds_cap_e = (int32_t)(room / 24);
-    }
-    for (int attempt = lds_cap_e < 0 ? 1 : 0; attempt < 2; ++attempt) {
-      eth::EthParams PA = P;
-      if (attempt == 0) PA.cap_e = lds_cap_e;
-      const eth::EthMem M = attempt == 0
-                                ? eth::eth_mem_split(base, lane_lds, PA.cap_b, PA.cap_e, PA.n)
-                                : eth::eth_mem_at(base, P.cap_b, P.cap_e, P.n);
-      eth::EthLane L;
-      uint32_t miss = 0;
-      const int32_t hd = nak_rerun_entry(RL, e, PA, M, L, &miss);
-      if (attempt == 0 && L.dead == 2 && PA.cap_e < P.cap_e) {  // outgrew LDS: count, redo
-        atomicAdd(const_cast<uint32_t*>(queue_n) + 1, 1u);  // cpr_rerun_hbm_retries
-        continue;
+    rerun_episode(launches[q >> 40], (q >> 8) & 0xffffffffll, (uint32_t)(q & 0xff), base,
+                  lane_lds, lds_bytes, queue_n);
+  }
+}
+
+// The episodes that found the queue full (their launch's overflow flags, nonzero bytes):
+// only when the count passed the capacity. The workgroup's 64 lanes scan 64 flags at a
+// time; lane 0 re-runs the flagged ones.
+__global__ __launch_bounds__(64) void k_rerun_overflow(const RerunLaunch* launches,
+                                                        int64_t n_launches,
+                                                        const uint32_t* queue_n,
+                                                        int64_t queue_cap, uint8_t* mem,
+                                                        int64_t lane_bytes, int64_t lds_bytes) {
+  extern __shared__ __attribute__((aligned(128))) uint8_t lane_lds[];
+  if ((int64_t)*queue_n <= queue_cap) return;
+  uint8_t* base = mem + (int64_t)blockIdx.x * lane_bytes;
+  for (int64_t li = 0; li < n_launches; ++li) {
+    const RerunLaunch& RL = launches[li];
+    if (!RL.ovf) continue;
+    for (int64_t b0 = (int64_t)blockIdx.x * 64; b0 < RL.n_eps; b0 += (int64_t)gridDim.x * 64) {
+      const int64_t e = b0 + threadIdx.x;
+      const uint32_t f = e < RL.n_eps ? RL.ovf[e] : 0u;
+      uint64_t set = __ballot(f != 0u);
+      if (threadIdx.x == 0) {
+        while (set) {
+          const int32_t k = __builtin_ctzll(set);
+          set &= set - 1;
+          const uint32_t fk = RL.ovf[b0 + k];
+          rerun_episode(RL, b0 + k, fk & 0x7fu, base, lane_lds, lds_bytes, queue_n);
+        }
       }
-      nak_rerun_finish(RL, e, P, M, L, hd, flags | miss);
-      break;
     }
   }
 }
@@ -406,10 +441,10 @@ __global__ __launch_bounds__(64) void k_nak_exact_rerun(const RerunLaunch* launc
 // LDS per one-wave workgroup: up to the whole 160 KiB of a CU when the launch needs it
 constexpr int64_t kRerunLdsMax = 160 * 1024;
 
-hipError_t launch_nak_exact_rerun(const RerunLaunch* launches, const int64_t* queue,
-                                  const uint32_t* queue_n, int64_t queue_cap, uint8_t* mem,
-                                  int64_t lane_bytes, int64_t lds_bytes, int64_t lanes,
-                                  hipStream_t st) {
+hipError_t launch_nak_exact_rerun(const RerunLaunch* launches, int64_t n_launches,
+                                  const int64_t* queue, const uint32_t* queue_n,
+                                  int64_t queue_cap, uint8_t* mem, int64_t lane_bytes,
+                                  int64_t lds_bytes, int64_t lanes, hipStream_t st) {
   int64_t cap = kRerunLdsMax;
   if (const char* v = getenv("CPR_RERUN_LDS_MAX"))  // tests: force the reduced-heap paths
     cap = std::min<int64_t>(cap, std::max<int64_t>(0, atoll(v)));
@@ -423,11 +458,13 @@ hipError_t launch_nak_exact_rerun(const RerunLaunch* launches, const int64_t* qu
     std::atomic<int64_t>& g = granted[dev & 63];
     int64_t have = g.load(std::memory_order_acquire);
     if (have == 0) {
-      have = hipFuncSetAttribute((const void*)k_nak_exact_rerun,
-                                 hipFuncAttributeMaxDynamicSharedMemorySize,
-                                 (int)kRerunLdsMax) == hipSuccess
-                 ? kRerunLdsMax
-                 : 64 * 1024;
+      const bool a = hipFuncSetAttribute((const void*)k_nak_exact_rerun,
+                                         hipFuncAttributeMaxDynamicSharedMemorySize,
+                                         (int)kRerunLdsMax) == hipSuccess;
+      const bool b = hipFuncSetAttribute((const void*)k_rerun_overflow,
+                                         hipFuncAttributeMaxDynamicSharedMemorySize,
+                                         (int)kRerunLdsMax) == hipSuccess;
+      have = a && b ? kRerunLdsMax : 64 * 1024;
       (void)hipGetLastError();
       g.store(have, std::memory_order_release);
     }
@@ -436,6 +473,8 @@ hipError_t launch_nak_exact_rerun(const RerunLaunch* launches, const int64_t* qu
   if (lds < 0) lds = 0;
   hipLaunchKernelGGL(k_nak_exact_rerun, dim3((unsigned)lanes), dim3(64), (size_t)lds, st,
                      launches, queue, queue_n, queue_cap, mem, lane_bytes, lds);
+  hipLaunchKernelGGL(k_rerun_overflow, dim3((unsigned)lanes), dim3(64), (size_t)lds, st,
+                     launches, n_launches, queue_n, queue_cap, mem, lane_bytes, lds);
   return hipGetLastError();
 }
 

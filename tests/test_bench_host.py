@@ -33,11 +33,16 @@ def test_other_configs_cover_baseline():
     by = {s[0]: s for s in specs}
     from cpr_amd import _lib as L
 
-    # configs[2]: Ethereum with whitepaper (constant) uncle rewards over gamma
+    # configs[2]: Ethereum with whitepaper (constant) uncle rewards, selfish_release and
+    # fn19 over alpha x gamma
     pts = by["configs[2]"][4]
     assert {p["protocol"] for p in pts} == {L.PROTO_ETHEREUM}
     assert {p["reward_scheme"] for p in pts} == {L.REWARD_CONSTANT}
-    assert sorted(p["gamma"] for p in pts) == [0.0, 0.5, 0.9]
+    assert sorted({p["gamma"] for p in pts}) == [0.0, 0.5, 0.9]
+    assert {p["policy"] for p in pts} == {L.ETH_POLICY_SELFISH_RELEASE, L.ETH_POLICY_FN19}
+    assert len({p["alpha"] for p in pts}) >= 2 and len(pts) == 12
+    # configs[0]: at least 10^6 episodes
+    assert by["configs[0]"][5] >= 10**6
     # configs[3]: Tailstorm k = 8, discount, withholding (two attack policies), 10^4 activations
     for p in by["configs[3]"][4] + by["configs[3]_exp"][4]:
         assert p["protocol"] == L.PROTO_TAILSTORM and p["k"] == 8

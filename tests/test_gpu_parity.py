@@ -414,3 +414,57 @@ def test_configs0_honest_episodes_match_oracle(ctx):
     assert (rec["progress"] >= 2010).all()
     share = rec["reward_attacker"].sum() / rec["progress"].sum()
     assert abs(share - 0.33) < 0.005
+
+
+def test_lockstep_65536_lanes_all_exact_at_long_delay(ctx):
+    # engine.ml's step is exact for every env: with a 0.05 propagation delay nearly every
+    # lane leaves the closed form, and every one of 65,536 lanes gets an exact-engine slot
+    # (capi.hip ensure_lockstep sizes the pool to the lanes), so no step's outputs carry
+    # inexact bits without CPR_ST_EXACT_RERUN; sampled lanes equal the oracle step by step
+    n, T = 65536, 200
+    cfg, keep = device.make_config(alpha=0.42, gamma=0.5, max_steps=T, seed=905,
+                                   propagation_delay=0.05, unit_observation=False, n_lanes=n)
+    b = device.Batch(cfg, ctx=ctx, keep=keep)
+    obs = b.reset()
+    sample = np.arange(0, n, n // 16)
+    envs = {int(i): O.GymEnv(cfg, episode=int(i)) for i in sample}
+    for i, e in envs.items():
+        assert np.array_equal(obs[i], e.reset())
+    moved = 0
+    for t in range(T):
+        acts = b.policy_actions(L.POLICY_SAPIRSHTEIN_2016_SM1, obs)
+        obs, rew, done, info = b.step(acts)
+        st = info["status"]
+        inexact = (st & L.ST_LOCKSTEP_INEXACT) != 0
+        assert not (inexact & ((st & L.ST_EXACT_RERUN) == 0)).any(), t
+        moved = max(moved, int(((st & L.ST_EXACT_RERUN) != 0).sum()))
+        for i, e in envs.items():
+            o, r, d, _ = e.step(int(acts[i]))
+            assert np.array_equal(obs[i], o) and rew[i] == r and done[i] == d, (t, i)
+    assert moved > n // 2, moved  # most lanes ran on the exact engine
+
+
+@pytest.mark.parametrize("cap", [0, 7])
+def test_full_rerun_queue_flushes_not_capacity(ctx, cap, monkeypatch):
+    # a flagged episode that finds the exact re-run queue full waits in its launch's
+    # overflow flags and is re-run after the queue (kernels_eth.hip k_rerun_overflow): no
+    # CPR_ST_CAPACITY, every record equal to the oracle's (a forced capacity of 0 / 7)
+    monkeypatch.setenv("CPR_RERUN_QUEUE_CAP", str(cap))
+    cfg, keep = device.make_config(alpha=0.45, gamma=0.5, policy=L.POLICY_SAPIRSHTEIN_2016_SM1,
+                                   max_steps=400, seed=0x0E7, propagation_delay=0.05)
+    b = device.Batch(cfg, ctx=ctx, keep=keep)
+    s, rec = b.run(512, first_episode=0, records=True)
+    ref = O.run_episodes(cfg, 0, 512, threads=8)
+    assert _records_equal(rec, ref) == {}
+    assert not (rec["status"] & L.ST_CAPACITY).any()
+    assert ((rec["status"] & L.ST_EXACT_RERUN) != 0).sum() > 100
+    assert s.episodes == 512 and s.invalid == 0
+    # the Ethereum window lane's re-runs take the same path
+    cfg, keep = device.make_config(protocol=L.PROTO_ETHEREUM, alpha=0.4, gamma=0.5,
+                                   policy=L.ETH_POLICY_FN19, max_steps=400, seed=0x0E8,
+                                   propagation_delay=0.05)
+    b = device.Batch(cfg, ctx=ctx, keep=keep)
+    s, rec = b.run(256, first_episode=0, records=True)
+    ref = O.run_episodes(cfg, 0, 256, threads=8)
+    assert _records_equal(rec, ref) == {}
+    assert not (rec["status"] & L.ST_CAPACITY).any() and s.invalid == 0
