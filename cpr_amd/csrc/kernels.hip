@@ -45,7 +45,6 @@ __device__ inline CPR_AI BRef run_gym(NakLane& L, const NakParams& P, const St& 
   if (!check_prog && !(P.max_time < __builtin_inf())) {
     // only max_steps ends the episode: the trip count is the same in every lane of the
     // wave, so the loop exit is uniform and no lane state is merged at a divergent exit
-#ifndef CPR_NAK_UNROLL2
     do {
       const NakLane::Draw dr = L.draw(P, S);
       L.apply(L.policy_action<POL>(P));
@@ -59,27 +58,6 @@ __device__ inline CPR_AI BRef run_gym(NakLane& L, const NakParams& P, const St& 
       }
     } while (steps < P.max_steps);
     if constexpr (TT == 2) verify_races(L, P, S, M);
-#else
-    // two steps per trip: both activations' draws (two independent Philox / log chains,
-    // which depend on the activation count only) are issued together
-    for (; steps + 2 <= P.max_steps; steps += 2) {
-      const NakLane::Draw d0 = L.draw_at(P, S, L.k);
-      const NakLane::Draw d1 = L.draw_at(P, S, L.k + 1);
-      L.apply(L.policy_action<POL>(P));
-      L.resolve<St, POL >= 0 ? 0 : -1>(P, S, M);
-      L.activate(P, S, M, d0);
-      L.apply(L.policy_action<POL>(P));
-      L.resolve<St, POL >= 0 ? 0 : -1>(P, S, M);
-      L.activate(P, S, M, d1);
-    }
-    if (steps < P.max_steps) {
-      const NakLane::Draw dr = L.draw(P, S);
-      L.apply(L.policy_action<POL>(P));
-      L.resolve<St, POL >= 0 ? 0 : -1>(P, S, M);
-      L.activate(P, S, M, dr);
-      ++steps;
-    }
-#endif
     *steps_out = steps;
     return L.head(P, M);
   }

@@ -57,7 +57,7 @@ int main(int argc, char** argv) {
   P.max_progress = __builtin_inf();
   P.max_time = __builtin_inf();
   std::vector<uint8_t> mem(bk::bk_lane_bytes(P));
-  long acts = 0, st = 0, cap = 0;
+  long acts = 0, st = 0, cap = 0, hmax = 0, hsum = 0;
   for (int e = 0; e < episodes; ++e) {
     const bk::BkMem M = bk::bk_mem_at(mem.data(), P);
     const Stream S{0x5EED0000u, 0u, (uint32_t)e, 0u};
@@ -68,6 +68,8 @@ int main(int argc, char** argv) {
     acts += L.c_act;
     st += L.steps;
     cap += (L.status & bk::BST_CAPACITY) ? 1 : 0;
+    hsum += L.hused;
+    hmax = L.hused > hmax ? L.hused : hmax;
   }
   const double a = (double)acts;
   const char* names[16] = {"push_visits", "pop_visits", "confirming_scan", "propose_scan",
@@ -75,8 +77,9 @@ int main(int argc, char** argv) {
                            "ev_tx", "ev_rx", "ev_on", "ev_mv", "ev_mdv", "propose_calls",
                            "confirming_calls"};
   printf("{\"episodes\": %d, \"gamma\": %g, \"policy\": %d, \"alpha\": %g, \"k\": %d, "
-         "\"capacity\": %ld, \"steps_per_activation\": %.3f, \"per_activation\": {",
-         episodes, gamma, policy, alpha, k, cap, st / a);
+         "\"capacity\": %ld, \"steps_per_activation\": %.3f, \"heap_high_water_mean\": %.1f, "
+         "\"heap_high_water_max\": %ld, \"per_activation\": {",
+         episodes, gamma, policy, alpha, k, cap, st / a, hsum / (double)episodes, hmax);
   for (int i = 0; i < 16; ++i) printf("%s\"%s\": %.2f", i ? ", " : "", names[i], g_cost[i] / a);
   printf("}}\n");
   return 0;

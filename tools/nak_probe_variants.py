@@ -9,7 +9,6 @@ the variants' results are meaningless; only their kernel times are read.
   cheap_link: the link draws (the race at a match: a second Philox per activation in
               which any lane of the wave races) -> a multiply-xorshift hash
   base      : the tree as it is
-  unroll2   : the gym loop two activations per trip (CPR_NAK_UNROLL2)
   tt1w4     : the d = 2 tie-rule kernel at 4 waves/SIMD instead of 5
   tt0       : no tie-rule kernel (d = 2 runs the heap-replay summary-only kernel)
   norace    : cost probe, the d = 2 kernel's races decided without their link draw
@@ -133,9 +132,6 @@ def variant(name, rng, log, rev=None):
     if m8:  # the gamma = 0 kernel's waves-per-SIMD minimum (CPR_G0_WAVES)
         k = (d / "kernels.hip").read_text()
         (d / "kernels.hip").write_text(f"#define CPR_G0_WAVES {m8.group(1)}\n" + k)
-    if "unroll2" in name:  # two activations per trip of the gym loop (kernels.hip)
-        k = (d / "kernels.hip").read_text()
-        (d / "kernels.hip").write_text("#define CPR_NAK_UNROLL2 1\n" + k)
     if "_nock" in name or "_nolink" in name:
         lane = (d / "nakamoto_lane.h").read_text()
         for old, new in [("  if (wrong) {\n    const int32_t k_now", "  if (wrong && false) {\n    const int32_t k_now"),
