@@ -102,6 +102,12 @@ constexpr int32_t NQS = 128;     // quorum candidates per block and list
 constexpr int32_t NSTACK = 1024; // share stack
 
 struct BkMem {
+  // event-heap nodes 0 .. kl-1 live in the workgroup's LDS slab (hl, this lane's part) for
+  // the duration of a kernel, the rest in HBM (heap): a window's live events (14-22 at the
+  // gym's gamma = .5, tools/bk_cost_study.cpp) stay off the memory hierarchy. Kernels with a
+  // slab load nodes 0 .. kl-1 from heap at entry and store them back at exit (bk_heap_*)
+  HNode* hl = nullptr;
+  int32_t kl = 0, hs = 1;
   BVtx* vtx;
   uint8_t* vis;
   double* vt;
@@ -152,6 +158,24 @@ __host__ __device__ inline BkMem bk_mem_at(uint8_t* base, const BkParams& P) {
   o += bk_align(2 * NQS * 4);
   M.stack = (int32_t*)(base + o);
   return M;
+}
+
+// the LDS heap slab of a kernel (BkMem.hl): this lane's nodes 0 .. kl-1 at
+// slab[i * stride + lane]; persistent lanes (rollouts) load the nodes their heap uses at
+// entry and store them back at exit, so between kernels the whole heap is in HBM
+__host__ __device__ inline void bk_heap_slab(BkMem& M, HNode* slab, int32_t lane,
+                                             int32_t stride, int32_t kl) {
+  M.hl = slab + lane;
+  M.hs = stride;
+  M.kl = kl;
+}
+__host__ __device__ inline void bk_heap_load(const BkMem& M, int32_t hused) {
+  const int32_t n = hused < M.kl ? hused : M.kl;
+  for (int32_t i = 0; i < n; ++i) M.hl[(int64_t)i * M.hs] = M.heap[i];
+}
+__host__ __device__ inline void bk_heap_store(const BkMem& M, int32_t hused) {
+  const int32_t n = hused < M.kl ? hused : M.kl;
+  for (int32_t i = 0; i < n; ++i) M.heap[i] = M.hl[(int64_t)i * M.hs];
 }
 
 // per-node output region of one lane: activations [n] i64 | rewards [cap_q][n] i32
@@ -283,7 +307,7 @@ struct BkLane {
   int32_t nrand;  // random-policy decisions so far (the keyed draw's index)
   double now;
   int32_t c_act, newest, nblk, act0;
-  int32_t hroot, hfree, hused;
+  int32_t hroot, hfree, hused, hfree2;
   uint32_t status;
   int32_t dead;  // capacity exceeded: 1 vertex ring, 2 event heap, 3 quorum list, 4 drafts,
                  // 5 share stack, 6 queue drained, 7 quorum ring, 8 zero-time append loop
@@ -332,18 +356,37 @@ struct BkLane {
   // arrive, gamma = 0) are stored too: every insertion swaps children along its path, so
   // they shape the pop order of equal-time events even though they never pop in a gym
   // episode (B_k is sensitive to that order: which same-instant Append lands first).
+  // node i of the event heap: the LDS slab below M.kl (node-major across the workgroup's
+  // lanes, stride M.hs), else HBM (the heap's order never depends on which node holds an
+  // element)
+  __host__ __device__ static inline HNode& HN(const BkMem& M, int32_t i) {
+    return i < M.kl ? M.hl[(int64_t)i * M.hs] : M.heap[i];
+  }
+  // free nodes: slab nodes first (hfree), then HBM nodes (hfree2)
   __host__ __device__ inline int32_t halloc(const BkParams& P, const BkMem& M) {
     int32_t i;
     if (hfree >= 0) {
       i = hfree;
-      hfree = M.heap[i].l;
-    } else if (hused < P.cap_e) {
+      hfree = HN(M, i).l;
+    } else if (hused < P.cap_e && (hused < M.kl || hfree2 < 0)) {
       i = hused++;
+    } else if (hfree2 >= 0) {
+      i = hfree2;
+      hfree2 = HN(M, i).l;
     } else {
       fail(2);
       return -1;
     }
     return i;
+  }
+  __host__ __device__ inline void hrelease(const BkMem& M, int32_t node) {
+    if (node < M.kl) {
+      HN(M, node).l = hfree;
+      hfree = node;
+    } else {
+      HN(M, node).l = hfree2;
+      hfree2 = node;
+    }
   }
   __host__ __device__ inline void push(const BkParams& P, const BkMem& M, double t, uint32_t ev,
                                        int32_t blk) {
@@ -353,7 +396,7 @@ struct BkLane {
       if (node < 0) {
         const int32_t a = halloc(P, M);
         if (a < 0) return;
-        HNode& h = M.heap[a];
+        HNode& h = HN(M, a);
         h.t = t;
         h.ev = ev;
         h.blk = blk;
@@ -362,10 +405,10 @@ struct BkLane {
         if (parent < 0)
           hroot = a;
         else
-          M.heap[parent].l = a;
+          HN(M, parent).l = a;
         return;
       }
-      HNode& h = M.heap[node];
+      HNode& h = HN(M, node);
       if (t < h.t) {
         const double ot = h.t;
         const uint32_t oe = h.ev;
@@ -387,13 +430,13 @@ struct BkLane {
   }
   __host__ __device__ inline bool pop(const BkMem& M, double* t, uint32_t* ev, int32_t* blk) {
     if (hroot < 0) return false;
-    *t = M.heap[hroot].t;
-    *ev = M.heap[hroot].ev;
-    *blk = M.heap[hroot].blk;
+    *t = HN(M, hroot).t;
+    *ev = HN(M, hroot).ev;
+    *blk = HN(M, hroot).blk;
     int32_t parent = -1, side = 0, node = hroot;
     for (;;) {
       CPR_BK_COST(BC_POP);
-      const int32_t l = M.heap[node].l, r = M.heap[node].r;
+      const int32_t l = HN(M, node).l, r = HN(M, node).r;
       int32_t repl = -2;
       if (r < 0)
         repl = l;
@@ -403,17 +446,16 @@ struct BkLane {
         if (parent < 0)
           hroot = repl;
         else if (side == 0)
-          M.heap[parent].l = repl;
+          HN(M, parent).l = repl;
         else
-          M.heap[parent].r = repl;
-        M.heap[node].l = hfree;
-        hfree = node;
+          HN(M, parent).r = repl;
+        hrelease(M, node);
         return true;
       }
-      const int32_t c = (M.heap[l].t <= M.heap[r].t) ? l : r;
-      M.heap[node].t = M.heap[c].t;
-      M.heap[node].ev = M.heap[c].ev;
-      M.heap[node].blk = M.heap[c].blk;
+      const int32_t c = (HN(M, l).t <= HN(M, r).t) ? l : r;
+      HN(M, node).t = HN(M, c).t;
+      HN(M, node).ev = HN(M, c).ev;
+      HN(M, node).blk = HN(M, c).blk;
       parent = node;
       side = c == l ? 0 : 1;
       node = c;
@@ -820,6 +862,7 @@ struct BkLane {
     act0 = 0;
     hroot = -1;
     hfree = -1;
+    hfree2 = -1;
     hused = 0;
     status = 0u;
     dead = 0;

@@ -137,6 +137,9 @@ hipError_t launch_eth_replay_episodes(const eth::EthParams& P, const TraceSource
                                  cpr_episode_record* recs, cpr_summary* sum, hipStream_t st,
                                    const NodeOut& no = NodeOut());
 int eth_blocks_per_cu();
+// event-heap nodes per lane in the LDS slab of an event-engine kernel launched with
+// `blocks` workgroups (kernels_bk.hip; the B_k and Tailstorm lanes' BkMem / TsMem.hl)
+int32_t ev_slab_nodes(int64_t blocks, const void* kernel);
 // Ethereum gym episodes on the selfish-mining network through the window lane
 // (eth_window.h; ethw::win_supported): mem = lanes x ethw::win_lane_bytes; flagged episodes
 // go to the exact re-run queue (redo / redo_n, entries tagged with launch_id)

@@ -10,6 +10,10 @@
 //                      episodes like a gym VecEnv (BASELINE configs[4])
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+#include <atomic>
+#include <cstdlib>
+
 #include "../../include/cpr_hip.h"
 #include "bk_lane.h"
 #include "kernels.h"
@@ -107,16 +111,21 @@ struct BkAdapter {
   }
 };
 
+// the heap slab of a workgroup (dynamic LDS): kl nodes per lane, node-major
+extern __shared__ __attribute__((aligned(16))) bk::HNode bk_slab[];
+
 template <class Src>
 __global__ __launch_bounds__(kBlock) CPR_EV_OCC void k_bk_run_episodes(
     bk::BkParams P, Src src, int64_t n_eps, uint8_t* mem,
-    int64_t lane_bytes, cpr_episode_record* recs, cpr_summary* sum, NodeOut no) {
+    int64_t lane_bytes, cpr_episode_record* recs, cpr_summary* sum, NodeOut no, int32_t kl) {
   __shared__ int32_t hist[CPR_HIST_BINS];
   if (threadIdx.x < CPR_HIST_BINS) hist[threadIdx.x] = 0;
   __syncthreads();
   const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t nthreads = (int64_t)gridDim.x * blockDim.x;
   bk::BkMem M = bk::bk_mem_at(mem + tid * lane_bytes, P);
+  // every episode starts with an empty heap (init): the slab needs no load or store
+  bk::bk_heap_slab(M, bk_slab, (int32_t)threadIdx.x, (int32_t)blockDim.x, kl);
   if (no.mem) bk::bk_node_mem(M, no.mem + tid * no.lane_bytes, P);
   Acc acc = {};
   bk::BkLane L;
@@ -264,7 +273,8 @@ __global__ __launch_bounds__(kBlock) CPR_EV_OCC void k_bk_rollout(bk::BkParams P
                                                         int64_t n_steps, int unit,
                                                         const double* tabs, int32_t tn,
                                                         double* obs, double* reward,
-                                                        uint8_t* done_out, cpr_summary* sum) {
+                                                        uint8_t* done_out, cpr_summary* sum,
+                                                        int32_t kl) {
   __shared__ int32_t hist[CPR_HIST_BINS];
   if (threadIdx.x < CPR_HIST_BINS) hist[threadIdx.x] = 0;
   __syncthreads();
@@ -272,8 +282,11 @@ __global__ __launch_bounds__(kBlock) CPR_EV_OCC void k_bk_rollout(bk::BkParams P
   Acc acc = {};
   int64_t steps_all = 0, acts_all = 0;
   if (i < n) {
-    const bk::BkMem M = bk::bk_mem_at(mem + i * lane_bytes, P);
+    bk::BkMem M = bk::bk_mem_at(mem + i * lane_bytes, P);
     BkSlot SL = slots[i];
+    // the lane's heap nodes 0 .. kl-1 move to the slab for this launch
+    bk::bk_heap_slab(M, bk_slab, (int32_t)threadIdx.x, (int32_t)blockDim.x, kl);
+    bk::bk_heap_load(M, SL.L.hused);
     if (!SL.live) {
       bk_slot_reset(P, seed, M, SL, (uint64_t)i);
       acts_all += SL.L.c_act;
@@ -300,6 +313,7 @@ __global__ __launch_bounds__(kBlock) CPR_EV_OCC void k_bk_rollout(bk::BkParams P
       }
       if (obs) bk_write_obs(SL.L.observe(P, M), unit, tabs, tn, P.k, obs + 8 * k);
     }
+    bk::bk_heap_store(M, SL.L.hused);
     slots[i] = SL;
   }
   // rollout totals: all steps and activations (acc.steps/activations hold finished
@@ -357,12 +371,43 @@ __global__ void k_bk_policy(bk::BkParams P, int unit, const double* obs, int64_t
 
 static unsigned grid_of(int64_t n) { return (unsigned)((n + kBlock - 1) / kBlock); }
 
+// heap nodes per lane in the LDS slab for a grid of `blocks` workgroups: the LDS a
+// workgroup gets when the grid spreads over the device's CUs (160 KiB per CU), less the
+// kernels' static LDS, at most 32 nodes (the gym's windows hold 14-30 live events);
+// CPR_EV_SLAB overrides it (A/B runs; 0 = every node in HBM)
+int32_t ev_slab_nodes(int64_t blocks, const void* kernel) {
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        cus <= 0)
+      cus = 256;
+  }
+  if (const char* v = getenv("CPR_EV_SLAB")) return std::max(0, std::min(32, atoi(v)));
+  const int64_t per_cu = std::max<int64_t>(1, (blocks + cus - 1) / cus);
+  const int64_t bytes = (160 * 1024) / per_cu - 2048;  // static LDS of the kernels
+  int32_t kl = (int32_t)std::min<int64_t>(32, std::max<int64_t>(0, bytes / (kBlock * 24)));
+  if ((int64_t)kl * kBlock * 24 > 64 * 1024) {
+    // more than the default 64 KiB of dynamic LDS: ask once per kernel
+    if (hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            160 * 1024 - 2048) != hipSuccess) {
+      (void)hipGetLastError();
+      kl = (64 * 1024) / (kBlock * 24);
+    }
+  }
+  return kl;
+}
+
 hipError_t launch_bk_run_episodes(const bk::BkParams& P, uint64_t seed, uint64_t first,
                                   int64_t n_eps, uint8_t* mem, int64_t lane_bytes, int64_t lanes,
                                   cpr_episode_record* recs, cpr_summary* sum, hipStream_t st,
                                   const NodeOut& no) {
-  hipLaunchKernelGGL(k_bk_run_episodes<SeedSource>, dim3((unsigned)(lanes / kBlock)), dim3(kBlock), 0, st, P,
-                     SeedSource{seed, first}, n_eps, mem, lane_bytes, recs, sum, no);
+  const unsigned blocks = (unsigned)(lanes / kBlock);
+  const int32_t kl = ev_slab_nodes(blocks, (const void*)k_bk_run_episodes<SeedSource>);
+  hipLaunchKernelGGL(k_bk_run_episodes<SeedSource>, dim3(blocks), dim3(kBlock),
+                     (size_t)kl * kBlock * 24, st, P, SeedSource{seed, first}, n_eps, mem,
+                     lane_bytes, recs, sum, no, kl);
   return hipGetLastError();
 }
 
@@ -370,8 +415,11 @@ hipError_t launch_bk_replay_episodes(const bk::BkParams& P, const TraceSource& s
                                  uint8_t* mem, int64_t lane_bytes, int64_t lanes,
                                  cpr_episode_record* recs, cpr_summary* sum, hipStream_t st,
                                   const NodeOut& no) {
-  hipLaunchKernelGGL(k_bk_run_episodes<TraceSource>, dim3((unsigned)(lanes / kBlock)),
-                     dim3(kBlock), 0, st, P, src, n_eps, mem, lane_bytes, recs, sum, no);
+  const unsigned blocks = (unsigned)(lanes / kBlock);
+  const int32_t kl = ev_slab_nodes(blocks, (const void*)k_bk_run_episodes<TraceSource>);
+  hipLaunchKernelGGL(k_bk_run_episodes<TraceSource>, dim3(blocks), dim3(kBlock),
+                     (size_t)kl * kBlock * 24, st, P, src, n_eps, mem, lane_bytes, recs, sum, no,
+                     kl);
   return hipGetLastError();
 }
 
@@ -396,9 +444,10 @@ hipError_t launch_bk_rollout(const bk::BkParams& P, uint64_t seed, uint8_t* mem,
                              int64_t lane_bytes, void* slots, int64_t n, int64_t n_steps,
                              int unit, const double* tabs, int32_t tn, double* obs,
                              double* reward, uint8_t* done, cpr_summary* sum, hipStream_t st) {
-  hipLaunchKernelGGL(k_bk_rollout, dim3(grid_of(n)), dim3(kBlock), 0, st, P, seed, mem,
-                     lane_bytes, (BkSlot*)slots, n, n_steps, unit, tabs, tn, obs, reward, done,
-                     sum);
+  const int32_t kl = ev_slab_nodes(grid_of(n), (const void*)k_bk_rollout);
+  hipLaunchKernelGGL(k_bk_rollout, dim3(grid_of(n)), dim3(kBlock), (size_t)kl * kBlock * 24, st,
+                     P, seed, mem, lane_bytes, (BkSlot*)slots, n, n_steps, unit, tabs, tn, obs,
+                     reward, done, sum, kl);
   return hipGetLastError();
 }
 

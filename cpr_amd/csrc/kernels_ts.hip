@@ -120,10 +120,13 @@ struct TsAdapter {
   }
 };
 
+// the heap slab of a workgroup (dynamic LDS): kl nodes per lane, node-major
+extern __shared__ __attribute__((aligned(16))) bk::HNode ts_slab[];
+
 template <class Src>
 __global__ __launch_bounds__(kBlock) CPR_EV_OCC void k_ts_run_episodes(
     ts::TsParams P, Src src, int64_t n_eps, uint8_t* mem,
-    int64_t lane_bytes, cpr_episode_record* recs, cpr_summary* sum, NodeOut no) {
+    int64_t lane_bytes, cpr_episode_record* recs, cpr_summary* sum, NodeOut no, int32_t kl) {
   __shared__ int32_t hist[CPR_HIST_BINS];
   if (threadIdx.x < CPR_HIST_BINS) hist[threadIdx.x] = 0;
   __syncthreads();
@@ -131,6 +134,8 @@ __global__ __launch_bounds__(kBlock) CPR_EV_OCC void k_ts_run_episodes(
   const int64_t nthreads = (int64_t)gridDim.x * blockDim.x;
   ts::TsMem M = ts::ts_mem_at(mem + tid * lane_bytes, P);
   if (no.mem) M.nact = (int64_t*)(no.mem + tid * no.lane_bytes);
+  // every episode starts with an empty heap (init): the slab needs no load or store
+  ts::ts_heap_slab(M, ts_slab, (int32_t)threadIdx.x, (int32_t)blockDim.x, kl);
   Acc acc = {};
   ts::TsLane L;
 #if CPR_EV_SCHED
@@ -268,7 +273,8 @@ __global__ __launch_bounds__(kBlock) CPR_EV_OCC void k_ts_rollout(ts::TsParams P
                                                         int64_t n_steps, int unit,
                                                         const double* tabs, int32_t tn,
                                                         double* obs, double* reward,
-                                                        uint8_t* done_out, cpr_summary* sum) {
+                                                        uint8_t* done_out, cpr_summary* sum,
+                                                        int32_t kl) {
   __shared__ int32_t hist[CPR_HIST_BINS];
   if (threadIdx.x < CPR_HIST_BINS) hist[threadIdx.x] = 0;
   __syncthreads();
@@ -276,8 +282,11 @@ __global__ __launch_bounds__(kBlock) CPR_EV_OCC void k_ts_rollout(ts::TsParams P
   Acc acc = {};
   int64_t steps_all = 0, acts_all = 0;
   if (i < n) {
-    const ts::TsMem M = ts::ts_mem_at(mem + i * lane_bytes, P);
+    ts::TsMem M = ts::ts_mem_at(mem + i * lane_bytes, P);
     TsSlot SL = slots[i];
+    // the lane's heap nodes 0 .. kl-1 move to the slab for this launch
+    ts::ts_heap_slab(M, ts_slab, (int32_t)threadIdx.x, (int32_t)blockDim.x, kl);
+    ts::ts_heap_load(M, SL.L.hused);
     if (!SL.live) {
       ts_slot_reset(P, seed, M, SL, (uint64_t)i);
       acts_all += SL.L.c_act;
@@ -304,6 +313,7 @@ __global__ __launch_bounds__(kBlock) CPR_EV_OCC void k_ts_rollout(ts::TsParams P
       }
       if (obs) ts_write_obs(SL.L.observe(P, M), unit, tabs, tn, P.k, obs + 10 * kk);
     }
+    ts::ts_heap_store(M, SL.L.hused);
     slots[i] = SL;
   }
   acc.steps = steps_all;
@@ -358,8 +368,11 @@ hipError_t launch_ts_run_episodes(const ts::TsParams& P, uint64_t seed, uint64_t
                                   int64_t n_eps, uint8_t* mem, int64_t lane_bytes, int64_t lanes,
                                   cpr_episode_record* recs, cpr_summary* sum, hipStream_t st,
                                   const NodeOut& no) {
-  hipLaunchKernelGGL(k_ts_run_episodes<SeedSource>, dim3((unsigned)(lanes / kBlock)), dim3(kBlock), 0, st, P,
-                     SeedSource{seed, first}, n_eps, mem, lane_bytes, recs, sum, no);
+  const unsigned blocks = (unsigned)(lanes / kBlock);
+  const int32_t kl = ev_slab_nodes(blocks, (const void*)k_ts_run_episodes<SeedSource>);
+  hipLaunchKernelGGL(k_ts_run_episodes<SeedSource>, dim3(blocks), dim3(kBlock),
+                     (size_t)kl * kBlock * 24, st, P, SeedSource{seed, first}, n_eps, mem,
+                     lane_bytes, recs, sum, no, kl);
   return hipGetLastError();
 }
 
@@ -367,8 +380,11 @@ hipError_t launch_ts_replay_episodes(const ts::TsParams& P, const TraceSource& s
                                  uint8_t* mem, int64_t lane_bytes, int64_t lanes,
                                  cpr_episode_record* recs, cpr_summary* sum, hipStream_t st,
                                   const NodeOut& no) {
-  hipLaunchKernelGGL(k_ts_run_episodes<TraceSource>, dim3((unsigned)(lanes / kBlock)),
-                     dim3(kBlock), 0, st, P, src, n_eps, mem, lane_bytes, recs, sum, no);
+  const unsigned blocks = (unsigned)(lanes / kBlock);
+  const int32_t kl = ev_slab_nodes(blocks, (const void*)k_ts_run_episodes<TraceSource>);
+  hipLaunchKernelGGL(k_ts_run_episodes<TraceSource>, dim3(blocks), dim3(kBlock),
+                     (size_t)kl * kBlock * 24, st, P, src, n_eps, mem, lane_bytes, recs, sum, no,
+                     kl);
   return hipGetLastError();
 }
 
@@ -393,9 +409,10 @@ hipError_t launch_ts_rollout(const ts::TsParams& P, uint64_t seed, uint8_t* mem,
                              int64_t lane_bytes, void* slots, int64_t n, int64_t n_steps,
                              int unit, const double* tabs, int32_t tn, double* obs,
                              double* reward, uint8_t* done, cpr_summary* sum, hipStream_t st) {
-  hipLaunchKernelGGL(k_ts_rollout, dim3(ts_grid(n)), dim3(kBlock), 0, st, P, seed, mem,
-                     lane_bytes, (TsSlot*)slots, n, n_steps, unit, tabs, tn, obs, reward, done,
-                     sum);
+  const int32_t kl = ev_slab_nodes(ts_grid(n), (const void*)k_ts_rollout);
+  hipLaunchKernelGGL(k_ts_rollout, dim3(ts_grid(n)), dim3(kBlock), (size_t)kl * kBlock * 24, st,
+                     P, seed, mem, lane_bytes, (TsSlot*)slots, n, n_steps, unit, tabs, tn, obs,
+                     reward, done, sum, kl);
   return hipGetLastError();
 }
 

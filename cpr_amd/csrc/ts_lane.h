@@ -103,6 +103,10 @@ struct TsParams {
 constexpr int32_t NFR = 64;      // common-ancestor frontier (reference walk, tests only)
 
 struct TsMem {
+  // event-heap nodes 0 .. kl-1 in the workgroup's LDS slab (node-major, stride hs), the
+  // rest in HBM (heap); see bk_lane.h BkMem
+  HNode* hl = nullptr;
+  int32_t kl = 0, hs = 1;
   TVtx* vtx;
   uint8_t* vis;
   double* vt;
@@ -167,6 +171,22 @@ __host__ __device__ inline TsMem ts_mem_at(uint8_t* base, const TsParams& P) {
   M.stack = (int32_t*)take((int64_t)P.cap_v * 8);
   M.fr = (int32_t*)take(4 * NFR * 4);
   return M;
+}
+
+// the LDS heap slab of a kernel (as bk_lane.h bk_heap_*)
+__host__ __device__ inline void ts_heap_slab(TsMem& M, HNode* slab, int32_t lane, int32_t stride,
+                                             int32_t kl) {
+  M.hl = slab + lane;
+  M.hs = stride;
+  M.kl = kl;
+}
+__host__ __device__ inline void ts_heap_load(const TsMem& M, int32_t hused) {
+  const int32_t n = hused < M.kl ? hused : M.kl;
+  for (int32_t i = 0; i < n; ++i) M.hl[(int64_t)i * M.hs] = M.heap[i];
+}
+__host__ __device__ inline void ts_heap_store(const TsMem& M, int32_t hused) {
+  const int32_t n = hused < M.kl ? hused : M.kl;
+  for (int32_t i = 0; i < n; ++i) M.heap[i] = M.hl[(int64_t)i * M.hs];
 }
 
 // ---- observation and policies (tailstorm_ssz.ml:22-38, 365-446); Action8 ranks
@@ -254,7 +274,7 @@ struct TsLane {
   int32_t nrand;  // random-policy decisions so far (the keyed draw's index)
   double now;
   int32_t c_act, newest, nsum, act0;
-  int32_t hroot, hfree, hused;
+  int32_t hroot, hfree, hused, hfree2;
   uint32_t status;
   int32_t dead;  // 1 vertex ring, 2 heap, 3 tree list, 4 drafts, 5 stack, 6 drained, 7 quorum
                  // ring, 8 zero-time loop, 9 pending list, 10 frontier, 11 reference raises,
@@ -311,18 +331,36 @@ struct TsLane {
 
   // ------------------------------------------------------------------ event queue
   // orderedQueue.ml:17-47, in place; +inf events are stored (they shape the tie order)
+  // node i of the event heap: the LDS slab below M.kl, else HBM (the heap's order never
+  // depends on which node holds an element)
+  __host__ __device__ static inline HNode& HN(const TsMem& M, int32_t i) {
+    return i < M.kl ? M.hl[(int64_t)i * M.hs] : M.heap[i];
+  }
+  // free nodes: slab nodes first (hfree), then HBM nodes (hfree2)
   __host__ __device__ inline int32_t halloc(const TsParams& P, const TsMem& M) {
     int32_t i;
     if (hfree >= 0) {
       i = hfree;
-      hfree = M.heap[i].l;
-    } else if (hused < P.cap_e) {
+      hfree = HN(M, i).l;
+    } else if (hused < P.cap_e && (hused < M.kl || hfree2 < 0)) {
       i = hused++;
+    } else if (hfree2 >= 0) {
+      i = hfree2;
+      hfree2 = HN(M, i).l;
     } else {
       fail(2);
       return -1;
     }
     return i;
+  }
+  __host__ __device__ inline void hrelease(const TsMem& M, int32_t node) {
+    if (node < M.kl) {
+      HN(M, node).l = hfree;
+      hfree = node;
+    } else {
+      HN(M, node).l = hfree2;
+      hfree2 = node;
+    }
   }
   __host__ __device__ inline void push(const TsParams& P, const TsMem& M, double t, uint32_t ev,
                                        int32_t blk) {
@@ -331,7 +369,7 @@ struct TsLane {
       if (node < 0) {
         const int32_t a = halloc(P, M);
         if (a < 0) return;
-        HNode& h = M.heap[a];
+        HNode& h = HN(M, a);
         h.t = t;
         h.ev = ev;
         h.blk = blk;
@@ -340,10 +378,10 @@ struct TsLane {
         if (parent < 0)
           hroot = a;
         else
-          M.heap[parent].l = a;
+          HN(M, parent).l = a;
         return;
       }
-      HNode& h = M.heap[node];
+      HNode& h = HN(M, node);
       if (t < h.t) {
         const double ot = h.t;
         const uint32_t oe = h.ev;
@@ -365,12 +403,12 @@ struct TsLane {
   }
   __host__ __device__ inline bool pop(const TsMem& M, double* t, uint32_t* ev, int32_t* blk) {
     if (hroot < 0) return false;
-    *t = M.heap[hroot].t;
-    *ev = M.heap[hroot].ev;
-    *blk = M.heap[hroot].blk;
+    *t = HN(M, hroot).t;
+    *ev = HN(M, hroot).ev;
+    *blk = HN(M, hroot).blk;
     int32_t parent = -1, side = 0, node = hroot;
     for (;;) {
-      const int32_t l = M.heap[node].l, r = M.heap[node].r;
+      const int32_t l = HN(M, node).l, r = HN(M, node).r;
       int32_t repl = -2;
       if (r < 0)
         repl = l;
@@ -380,17 +418,16 @@ struct TsLane {
         if (parent < 0)
           hroot = repl;
         else if (side == 0)
-          M.heap[parent].l = repl;
+          HN(M, parent).l = repl;
         else
-          M.heap[parent].r = repl;
-        M.heap[node].l = hfree;
-        hfree = node;
+          HN(M, parent).r = repl;
+        hrelease(M, node);
         return true;
       }
-      const int32_t c = (M.heap[l].t <= M.heap[r].t) ? l : r;
-      M.heap[node].t = M.heap[c].t;
-      M.heap[node].ev = M.heap[c].ev;
-      M.heap[node].blk = M.heap[c].blk;
+      const int32_t c = (HN(M, l).t <= HN(M, r).t) ? l : r;
+      HN(M, node).t = HN(M, c).t;
+      HN(M, node).ev = HN(M, c).ev;
+      HN(M, node).blk = HN(M, c).blk;
       parent = node;
       side = c == l ? 0 : 1;
       node = c;
@@ -1218,6 +1255,7 @@ struct TsLane {
     act0 = 0;
     hroot = -1;
     hfree = -1;
+    hfree2 = -1;
     hused = 0;
     status = 0u;
     dead = 0;
