@@ -108,7 +108,10 @@ template <int MODE, class Src, int POL, int REC = 1, int ARR = -1, int TT = 0>
 #ifndef CPR_G0_WAVES
 #define CPR_G0_WAVES 8  // the gamma = 0 kernel: 61 VGPRs fit 8 waves/SIMD (7 unasked)
 #endif
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ARR == 0 ? CPR_G0_WAVES : (TT ? 5 : 4)))) void k_run_episodes(
+#ifndef CPR_TT_WAVES
+#define CPR_TT_WAVES 5  // the d = 2 tie-rule kernels (96 VGPRs)
+#endif
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ARR == 0 ? CPR_G0_WAVES : (TT ? CPR_TT_WAVES : 4)))) void k_run_episodes(
     NakParams P, Src src, int64_t n_eps, int64_t activations,
     double* spill, uint8_t* replay, cpr_episode_record* recs, cpr_summary* sum,
     int64_t* redo, uint32_t* redo_n, uint32_t launch_id, int64_t redo_cap, int64_t* list,
