@@ -31,7 +31,8 @@ struct Cfg {
   double alpha, gamma;
   int defenders;
   int policy;  // 0..6 tailstorm_ssz policies, 7 = random actions, 8 = random release-heavy,
-               // 9 = a random table (CPR_TS_POLICY_TABLE, loop tasks)
+               // 9 = a random table (CPR_TS_POLICY_TABLE, loop tasks), 10 = the keyed random
+               // attacker (CPR_TS_POLICY_RANDOM, loop tasks)
   int scheme;  // 0 Constant, 1 Discount, 3 Punish, 4 Hybrid
   int steps;
   int two_agents;  // 0 gym, 1 two-agents loop, 2 honest-clique loop (defenders = nodes),
@@ -81,7 +82,9 @@ static ts::TsParams params_of(const Cfg& cf) {
     P.lo = 0.5;
     P.hi = 1.5;
   }
-  P.policy = cf.policy < 7 ? cf.policy : (cf.policy == 9 ? ts::TS_POLICY_TABLE : 0);
+  P.policy = cf.policy < 7 ? cf.policy
+                          : (cf.policy == 9 ? ts::TS_POLICY_TABLE
+                                            : (cf.policy == 10 ? ts::TS_POLICY_RANDOM : 0));
   if (cf.policy == 9) {
     P.table = g_table(cf.k).actions.data();
     P.table_dim = g_table(cf.k).dim;
@@ -303,7 +306,8 @@ static bool run_loop(const Cfg& cf, uint64_t seed, uint64_t ep, Counters& C, std
       }
     }
     oracle::ts_loop_task(net, 1, nullptr, seed, ep, cf.k, cf.scheme, g_sel,
-                         cf.two_agents == 2 ? -1 : (cf.policy == 9 ? oracle::TS_POL_TABLE : cf.policy),
+                         cf.two_agents == 2 ? -1 : (cf.policy == 9 ? oracle::TS_POL_TABLE
+                                                           : (cf.policy == 10 ? oracle::TS_POL_RANDOM : cf.policy)),
                          cf.steps, &r, &g_table(cf.k));
   } catch (oracle::BudgetExceeded&) {
     budget = true;

@@ -144,7 +144,15 @@ def test_exp_clique_rejections(ctx):
 # random action of its attack space at every decision (the keyed draw of
 # include/cpr_hip.h CPR_*_POLICY_RANDOM), 3-node symmetric clique, activation delay 100,
 # exponential(1) links, 1000 activations, orphan rate <= 0.5
-from test_oracle_expclique import RANDOM_CASES  # noqa: E402
+RANDOM_CASES = [
+    ("nakamoto/random", L.PROTO_NAKAMOTO, L.POLICY_RANDOM, 8, L.REWARD_CONSTANT, 0),
+    ("ethereum/random", L.PROTO_ETHEREUM, L.ETH_POLICY_RANDOM, 8, L.REWARD_DISCOUNT, 0),
+    ("bk8/ssz/random", L.PROTO_BK, L.BK_POLICY_RANDOM, 8, L.REWARD_BLOCK, 0),
+    ("tailstorm8constant/ssz/random", L.PROTO_TAILSTORM, L.TS_POLICY_RANDOM, 8,
+     L.REWARD_CONSTANT, L.SELECT_OPTIMAL),
+    ("tailstorm8discount/ssz/random", L.PROTO_TAILSTORM, L.TS_POLICY_RANDOM, 8,
+     L.REWARD_DISCOUNT, L.SELECT_HEURISTIC),
+]
 
 
 @pytest.mark.parametrize("name,proto,pol,k,scheme,sel", RANDOM_CASES)
@@ -153,14 +161,27 @@ def test_random_attacker_matches_oracle(ctx, name, proto, pol, k, scheme, sel):
     b = device.Batch(cfg, ctx=ctx, keep=keep)
     n = 2048
     s, rec = b.run(n, records=True)
-    assert not (rec["status"] & L.ST_INVALID).any(), name
+    # the one invalid outcome allowed is the reference's own exception: optimal quorum
+    # selection raises when its brute-force search exceeds the n-choose-k budget
+    # (tailstorm.ml:271-507), which a random attacker's withheld votes reach in ~1 % of
+    # episodes (the reference's test runs one simulation); the oracle flags the same ones
+    inv = (rec["status"] & L.ST_INVALID) != 0
+    if sel == L.SELECT_OPTIMAL:
+        assert not (rec["status"][inv] & (L.ST_INVALID & ~L.ST_REFERENCE_RAISES)).any(), name
+        assert inv.mean() < 0.05, (name, inv.mean())
+    else:
+        assert not inv.any(), name
     ref = O.run_episodes(cfg, 0, 64, threads=8)
+    ref_inv = (ref["status"] & L.ST_INVALID) != 0
+    assert np.array_equal(inv[:64], ref_inv), name
+    ok = ~ref_inv
     for f in FIELDS:
-        bad = np.nonzero(rec[f][:64] != ref[f])[0]
+        bad = np.nonzero((rec[f][:64] != ref[f]) & ok)[0]
         assert len(bad) == 0, (name, f, int(bad[0]), rec[f][bad[0]], ref[f][bad[0]])
-    orphan = (1000.0 - rec["progress"]) / 1000.0
+    orphan = (1000.0 - rec["progress"][~inv]) / 1000.0
     assert orphan.max() <= 0.5, (name, orphan.max())
-    print(f"{name}: orphan rate mean {orphan.mean():.3f} max {orphan.max():.3f}")
+    print(f"{name}: orphan rate mean {orphan.mean():.3f} max {orphan.max():.3f}, "
+          f"reference-raises {int(inv.sum())} of {n}")
 
 
 def test_random_attacker_rejected_in_gym(ctx):

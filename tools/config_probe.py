@@ -14,6 +14,12 @@ import bench  # noqa: E402
 from cpr_amd import device  # noqa: E402
 
 if __name__ == "__main__":
+    import torch
+
+    # torch's HIP runtime first, then the library's context on the same device (bench.py's
+    # order: a context opened before torch leaves torch without a device)
+    torch.cuda.set_device(0)
+    torch.zeros(1, device="cuda")
     ctx = device.Context(0)
     out = bench.run_other_configs(ctx, 0.0, False, {}, keys=set(sys.argv[1:]))
     print(json.dumps(out), flush=True)
