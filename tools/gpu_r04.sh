@@ -21,3 +21,16 @@ for s in ${SLABS:-}; do
   env $E timeout -k 10 400 python tools/config_probe.py ${CONFIGS:-'configs[3]' 'configs[4]'} >> gpurun_out/${TAG}_configs.log 2>&1
   rc=$?; echo "configs $s rc=$rc" | tee -a gpurun_out/${TAG}_status.log; [[ $rc -eq 0 ]] || exit $rc
 done
+# k_run_episodes variants (tools/nak_probe_variants.py) on the default sweep, per gamma
+for v in ${NAK_VARIANTS:-}; do
+  for g in ${NAK_GAMMAS:-0.5 0}; do
+    CPR_HIP_LIB=build/var/$v.so timeout -k 10 300 python bench.py --steps 3 --warmup 1 --no-cpu --no-configs --gammas $g > gpurun_out/${TAG}_nak_${v}_$g.log 2>&1
+    rc=$?; echo "nak $v $g rc=$rc" | tee -a gpurun_out/${TAG}_status.log; [[ $rc -eq 0 ]] || exit $rc
+  done
+done
+# per-gamma PMC instruction mix of k_run_episodes (SQ counters, one pass per gamma)
+export TMPDIR=/tmp
+for g in ${PMC_GAMMAS:-}; do
+  timeout -k 10 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_LDS SQ_WAIT_INST_ANY SQ_INSTS_VMEM_RD --output-format csv -d gpurun_out/${TAG}_pmc_g$g -o run -- python3 bench.py --steps 1 --warmup 0 --no-cpu --no-configs --gammas $g > gpurun_out/${TAG}_pmc_g$g.log 2>&1
+  rc=$?; echo "pmc $g rc=$rc" | tee -a gpurun_out/${TAG}_status.log; [[ $rc -eq 0 ]] || exit $rc
+done

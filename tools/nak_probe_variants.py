@@ -27,6 +27,8 @@ the variants' results are meaningless; only their kernel times are read.
   *_nosv    : cost probe, the rollback code kept (never run), no checkpoint
   nokeep    : every tie rolls back (no closed-form tie rule in the verification)
   wavesN    : k_run_episodes compiled for N waves per SIMD instead of 4 (VGPR budget 512/N)
+  ilp       : the scheduler's max-ILP strategy (-mllvm -amdgpu-sched-strategy=max-ilp)
+  biasN     : the scheduler's occupancy-vs-latency bias N (-amdgpu-schedule-metric-bias)
 
 usage: python tools/nak_probe_variants.py [name | name@gitrev ...]  (build/var/<name>.so;
        name@rev builds the csrc/ of that git revision, e.g. prev@HEAD)
@@ -173,10 +175,16 @@ def variant(name, rng, log, rev=None):
         assert "amdgpu_waves_per_eu(4)" in k
         (d / "kernels.hip").write_text(k.replace("amdgpu_waves_per_eu(4)",
                                                  f"amdgpu_waves_per_eu({m.group(1)})", 1))
+    extra = []
+    if name.startswith("ilp"):
+        extra = ["-mllvm", "-amdgpu-sched-strategy=max-ilp"]
+    m = re.match(r"bias(\d+)", name)
+    if m:
+        extra = ["-mllvm", f"-amdgpu-schedule-metric-bias={m.group(1)}"]
     tu = os.environ.get("PROBE_TU", "kernels.hip")  # the translation unit rebuilt
     obj = OUT / f"{tu}_{name}.o"
     subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17",
-                    "-ffp-contract=off", "-fPIC", f"-I{ROOT / 'include'}", "-c",
+                    "-ffp-contract=off", "-fPIC", f"-I{ROOT / 'include'}", *extra, "-c",
                     str(d / tu), "-o", str(obj)], check=True)
     objs = [str(obj)] + [str(p) for p in sorted((ROOT / "build" / "hip").glob("*.o"))
                          if p.name != f"{tu}.o"]
