@@ -281,6 +281,90 @@ __global__ __launch_bounds__(kBlock) CPR_EV_OCC void k_bk_rollout(bk::BkParams P
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   Acc acc = {};
   int64_t steps_all = 0, acts_all = 0;
+#if CPR_EV_SCHED
+  // wave-coherent dispatch (wave_sched.h roll_fetch): the plain loop below split into items;
+  // every lane's own sequence of events, actions and outputs is the plain loop's
+  bk::BkMem M = bk::bk_mem_at(mem + (i < n ? i : 0) * lane_bytes, P);
+  bk::bk_heap_slab(M, bk_slab, (int32_t)threadIdx.x, (int32_t)blockDim.x, kl);
+  BkSlot SL;
+  EvCursor c;
+  c.cls = -1;
+  c.phase = PH_IDLE;
+  int64_t ts = 0;  // steps of this launch taken
+  int32_t a0 = 0;  // activations of the current episode before this launch
+  Stream S = make_stream(seed, 0);
+  if (i < n) {
+    SL = slots[i];
+    bk::bk_heap_load(M, SL.L.hused);
+    if (!SL.live)
+      bk_slot_reset(P, seed, M, SL, (uint64_t)i);
+    else
+      a0 = SL.L.c_act;
+    S = make_stream(seed, SL.ep);
+    if (n_steps > 0) {
+      BkAdapter::act(SL.L, P, M);
+      c.att = SL.L.priv;
+      c.phase = PH_RUN;
+    }
+  }
+  for (;;) {
+    if (c.phase != PH_IDLE && c.cls < 0) roll_fetch<BkAdapter>(SL.L, M, c);
+    const int32_t kc = ev_choose(c.cls);
+    if (kc < 0) break;
+    if (c.cls != kc) continue;
+    c.cls = -1;
+    if (kc == WK_POW0) {
+      BkAdapter::run_pow0(SL.L, P, S, M, c.s);
+      continue;
+    }
+    if (kc != WK_ATTACK) {
+      SL.L.handle(P, S, M, c.ev, c.s);
+      continue;
+    }
+    if (c.ev != kRollFail) SL.L.prepare(P, M, (c.ev >> 3) & 3u, c.s);
+    if (c.phase == PH_FRESH) {
+      // the reset after a done step reached its first interaction: that step's observation
+      c.phase = PH_RUN;
+      if (obs) bk_write_obs(SL.L.observe(P, M), unit, tabs, tn, P.k, obs + 8 * ((ts - 1) * n + i));
+    } else {
+      const int32_t hd = BkAdapter::head_gym(SL.L, P, M, c.att);
+      const bool done = BkAdapter::gym_done(SL.L, P, M, hd);
+      const bk::BVtx& h = SL.L.X(P, M, hd);
+      const double ra = (double)h.rew_att;
+      const int64_t k = ts * n + i;
+      if (reward) reward[k] = ra - SL.last_ra;
+      if (done_out) done_out[k] = done ? 1 : 0;
+      SL.last_ra = ra;
+      ++ts;
+      if (done) {
+        bk_acc(acc, P, SL.L, h, hist);
+        acts_all += SL.L.c_act - a0;
+        a0 = 0;
+        SL.ep += (uint64_t)n;  // bk_slot_reset, its events run as items
+        SL.last_ra = 0.0;
+        SL.head = 0;
+        SL.live = 1;
+        S = make_stream(seed, SL.ep);
+        SL.L.init(P, S, M);
+        c.phase = PH_FRESH;
+        continue;
+      }
+      if (obs) bk_write_obs(SL.L.observe(P, M), unit, tabs, tn, P.k, obs + 8 * k);
+    }
+    if (ts >= n_steps) {
+      c.phase = PH_IDLE;  // at the decision point of the next launch's first step
+      continue;
+    }
+    BkAdapter::act(SL.L, P, M);
+    c.att = SL.L.priv;
+  }
+  if (i < n) {
+    acts_all += SL.L.c_act - a0;
+    steps_all = n_steps;
+    bk::bk_heap_store(M, SL.L.hused);
+    slots[i] = SL;
+  }
+#else
   if (i < n) {
     bk::BkMem M = bk::bk_mem_at(mem + i * lane_bytes, P);
     BkSlot SL = slots[i];
@@ -316,6 +400,7 @@ __global__ __launch_bounds__(kBlock) CPR_EV_OCC void k_bk_rollout(bk::BkParams P
     bk::bk_heap_store(M, SL.L.hused);
     slots[i] = SL;
   }
+#endif
   // rollout totals: all steps and activations (acc.steps/activations hold finished
   // episodes only, so replace them before the block reduction)
   acc.steps = steps_all;

@@ -281,6 +281,88 @@ __global__ __launch_bounds__(kBlock) CPR_EV_OCC void k_ts_rollout(ts::TsParams P
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   Acc acc = {};
   int64_t steps_all = 0, acts_all = 0;
+#if CPR_EV_SCHED
+  // wave-coherent dispatch, as k_bk_rollout
+  ts::TsMem M = ts::ts_mem_at(mem + (i < n ? i : 0) * lane_bytes, P);
+  ts::ts_heap_slab(M, ts_slab, (int32_t)threadIdx.x, (int32_t)blockDim.x, kl);
+  TsSlot SL;
+  EvCursor c;
+  c.cls = -1;
+  c.phase = PH_IDLE;
+  int64_t tsn = 0;  // steps of this launch taken
+  int32_t a0 = 0;   // activations of the current episode before this launch
+  Stream S = make_stream(seed, 0);
+  if (i < n) {
+    SL = slots[i];
+    ts::ts_heap_load(M, SL.L.hused);
+    if (!SL.live)
+      ts_slot_reset(P, seed, M, SL, (uint64_t)i);
+    else
+      a0 = SL.L.c_act;
+    S = make_stream(seed, SL.ep);
+    if (n_steps > 0) {
+      TsAdapter::act(SL.L, P, M);
+      c.att = SL.L.priv;
+      c.phase = PH_RUN;
+    }
+  }
+  for (;;) {
+    if (c.phase != PH_IDLE && c.cls < 0) roll_fetch<TsAdapter>(SL.L, M, c);
+    const int32_t kc = ev_choose(c.cls);
+    if (kc < 0) break;
+    if (c.cls != kc) continue;
+    c.cls = -1;
+    if (kc == WK_POW0) {
+      TsAdapter::run_pow0(SL.L, P, S, M, c.s);
+      continue;
+    }
+    if (kc != WK_ATTACK) {
+      SL.L.handle(P, S, M, c.ev, c.s);
+      continue;
+    }
+    if (c.ev != kRollFail) SL.L.prepare(P, M, (c.ev >> 3) & 3u, c.s);
+    if (c.phase == PH_FRESH) {
+      c.phase = PH_RUN;
+      if (obs)
+        ts_write_obs(SL.L.observe(P, M), unit, tabs, tn, P.k, obs + 10 * ((tsn - 1) * n + i));
+    } else {
+      const int32_t hd = TsAdapter::head_gym(SL.L, P, M, c.att);
+      const bool done = TsAdapter::gym_done(SL.L, P, M, hd);
+      double ra, rd;
+      ts_head_rewards(P, SL.L, M, hd, &ra, &rd);
+      const int64_t kk = tsn * n + i;
+      if (reward) reward[kk] = ra - SL.last_ra;
+      if (done_out) done_out[kk] = done ? 1 : 0;
+      SL.last_ra = ra;
+      ++tsn;
+      if (done) {
+        ts_acc(acc, P, SL.L, M, hd, hist);
+        acts_all += SL.L.c_act - a0;
+        a0 = 0;
+        SL.ep += (uint64_t)n;  // ts_slot_reset, its events run as items
+        SL.last_ra = 0.0;
+        SL.live = 1;
+        S = make_stream(seed, SL.ep);
+        SL.L.init(P, S, M);
+        c.phase = PH_FRESH;
+        continue;
+      }
+      if (obs) ts_write_obs(SL.L.observe(P, M), unit, tabs, tn, P.k, obs + 10 * kk);
+    }
+    if (tsn >= n_steps) {
+      c.phase = PH_IDLE;
+      continue;
+    }
+    TsAdapter::act(SL.L, P, M);
+    c.att = SL.L.priv;
+  }
+  if (i < n) {
+    acts_all += SL.L.c_act - a0;
+    steps_all = n_steps;
+    ts::ts_heap_store(M, SL.L.hused);
+    slots[i] = SL;
+  }
+#else
   if (i < n) {
     ts::TsMem M = ts::ts_mem_at(mem + i * lane_bytes, P);
     TsSlot SL = slots[i];
@@ -316,6 +398,7 @@ __global__ __launch_bounds__(kBlock) CPR_EV_OCC void k_ts_rollout(ts::TsParams P
     ts::ts_heap_store(M, SL.L.hused);
     slots[i] = SL;
   }
+#endif
   acc.steps = steps_all;
   acc.activations = acts_all;
   __syncthreads();

@@ -142,6 +142,42 @@ __device__ inline void ev_exec(typename A::Lane& L, const typename A::Par& P, co
   L.handle(P, S, M, c.ev, c.s);
 }
 
+// ---- rollouts (k_bk_rollout / k_ts_rollout: lockstep steps with the on-device policy,
+// VecEnv auto-reset) under the same dispatch. A lane starts a launch at the attacker's
+// decision point (prepared); its items are the events up to the next interaction
+// (engine.ml:108-121 skip_to_interaction, with the PoW substitution), and the interaction
+// itself ends the step: head / done / reward, then the observation and the next action, or
+// on done the reset (init, whose events up to the first interaction run as items as well).
+// An empty heap or a dead lane ends the step as gym_step does (no prepare, done).
+constexpr uint32_t kRollFail = 0xffffffffu;  // the step's interaction is an episode failure
+
+template <class A>
+__device__ inline void roll_fetch(typename A::Lane& L, const typename A::Mem& M, EvCursor& c) {
+  double t;
+  uint32_t ev;
+  int32_t s;
+  if (L.dead) {
+    c.ev = kRollFail;
+    c.cls = WK_ATTACK;
+    return;
+  }
+  if (!L.pop(M, &t, &ev, &s)) {
+    L.fail(6);  // engine.ml:120 "simulation should continue forever"
+    c.ev = kRollFail;
+    c.cls = WK_ATTACK;
+    return;
+  }
+  L.now = t;
+  c.ev = ev;
+  c.s = s;
+  if ((ev & 7u) == 4u && (ev >> 5) == 0u)  // EV_ON at node 0: the attacker's interaction
+    c.cls = WK_ATTACK;
+  else if (A::pow0(ev))
+    c.cls = WK_POW0;
+  else
+    c.cls = (int32_t)(ev & 7u);
+}
+
 // the class the most lanes of this wave hold (-1: none), wave-uniform
 __device__ inline int32_t ev_choose(int32_t cls) {
   int32_t best = -1, bn = 0;

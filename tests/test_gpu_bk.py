@@ -161,8 +161,21 @@ def test_bk_rollout_matches_sequential_oracle_episodes(ctx):
                 e = O.BkGymEnv(cfg, episode=ep)
                 o = e.reset()
             assert np.array_equal(obs[t, i], o), (i, t)
+        assert not d  # T is no multiple of max_steps: every lane ends mid-episode
+        acts_total += int(info["episode_n_activations"])
     assert s.episodes == finished
-    # a second call continues from the lanes' state
+    # every activation of the rollout: finished episodes + the lanes' current ones
+    assert s.activations == acts_total, (s.activations, acts_total)
+    # the same rollout in two launches (lanes resume at their decision point)
+    b2 = device.Batch(cfg, keep=keep)
+    sa, obs_a, rew_a, done_a = b2.rollout(123, outputs=True)
+    sb, obs_b, rew_b, done_b = b2.rollout(T - 123, outputs=True)
+    assert np.array_equal(np.concatenate([obs_a, obs_b]), obs)
+    assert np.array_equal(np.concatenate([rew_a, rew_b]), rew)
+    assert np.array_equal(np.concatenate([done_a, done_b]), done)
+    assert sa.activations + sb.activations == s.activations
+    assert sa.episodes + sb.episodes == s.episodes
+    # a further call continues from the lanes' state
     s2 = b.rollout(10)
     assert s2.steps == n * 10
 

@@ -134,20 +134,34 @@ def test_ts_rollout_matches_sequential_oracle_episodes(ctx):
     s, obs, rew, done = b.rollout(T, outputs=True)
     assert s.steps == n * T
     finished = 0
+    acts_total = 0
     for i in range(n):
         ep = i
         e = O.TsGymEnv(cfg, episode=ep)
         e.reset()
         for t in range(T):
-            o, r, d, _ = e.step(O.ts_policy("get-ahead", e.fields(), 8))
+            o, r, d, info = e.step(O.ts_policy("get-ahead", e.fields(), 8))
             assert rew[t, i] == r and done[t, i] == d, (i, t)
             if d:
                 finished += 1
+                acts_total += int(info["episode_n_activations"])
                 ep += n
                 e = O.TsGymEnv(cfg, episode=ep)
                 o = e.reset()
             assert np.array_equal(obs[t, i], o), (i, t)
+        assert not d  # T is no multiple of max_steps: every lane ends mid-episode
+        acts_total += int(info["episode_n_activations"])
     assert s.episodes == finished
+    assert s.activations == acts_total, (s.activations, acts_total)
+    # the same rollout in two launches (lanes resume at their decision point)
+    b2 = device.Batch(cfg, keep=keep)
+    sa, obs_a, rew_a, done_a = b2.rollout(77, outputs=True)
+    sb, obs_b, rew_b, done_b = b2.rollout(T - 77, outputs=True)
+    assert np.array_equal(np.concatenate([obs_a, obs_b]), obs)
+    assert np.array_equal(np.concatenate([rew_a, rew_b]), rew)
+    assert np.array_equal(np.concatenate([done_a, done_b]), done)
+    assert sa.activations + sb.activations == s.activations
+    assert sa.episodes + sb.episodes == s.episodes
 
 
 def test_ts_spec_registry_and_validation(ctx):
