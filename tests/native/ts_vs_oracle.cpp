@@ -376,6 +376,25 @@ int main(int argc, char** argv) {
   g_sel = argc > 4 ? atoi(argv[4]) : 1;
   const uint64_t seed = 0x7A110000ull + (uint64_t)k * 16 + (uint64_t)g_sel;
   std::vector<Cfg> cfgs;
+  if (const char* prof = getenv("TSPROF")) {
+    // lane only (host profiling, tools: gprof): "policy,episodes" of bench.py configs[3]
+    // (two agents, alpha .33, 10^4 activations, discount rewards, selection argv[4])
+    int pol = 5, neps = 20;
+    if (sscanf(prof, "%d,%d", &pol, &neps) != 2) return 2;
+    Cfg cf{0.33, 0.0, 1, pol, 1, 10000, 1, k};
+    const ts::TsParams P = params_of(cf);
+    std::vector<uint8_t> mem(ts::ts_lane_bytes(P));
+    const ts::TsMem M = ts::ts_mem_at(mem.data(), P);
+    long acts = 0;
+    for (int e = 0; e < neps; e++) {
+      const Stream S{(uint32_t)seed, (uint32_t)(seed >> 32), (uint32_t)e, 0u};
+      ts::TsLane L;
+      L.loop(P, S, M);
+      acts += L.c_act;
+    }
+    printf("{\"episodes\": %d, \"activations\": %ld}\n", neps, acts);
+    return 0;
+  }
   if (const char* one = getenv("TSCASE")) {
     // one exponential-clique case: "defenders,policy,scheme,ev,prop,activations,seed,first,n"
     int d, pol, sch, acts, first, n;
