@@ -6,7 +6,11 @@ is the activation loop (the depth-2 loop: depth 1 is the grid-stride episode loo
 plus those of loops nested in it, separately. Used to compare layouts of the Nakamoto
 lane without a GPU; the PMC-measured SQ_INSTS_VALU per activation is the real figure.
 
-usage: python tools/isa_loop_stats.py [kernels.hip] [kernel-substring] [-D...]
+usage: python tools/isa_loop_stats.py [kernels.hip] [kernel-substring] [-D...] [--by-source]
+
+--by-source compiles with -g as well and splits the activation loop's VALU instructions by
+the source function their .loc line falls in (inlined callees keep their own lines): the
+static cost-centre breakdown of one iteration (Philox, log, policy, apply, resolve, ...).
 """
 import collections
 import pathlib
@@ -17,11 +21,11 @@ import sys
 ROOT = pathlib.Path(__file__).resolve().parent.parent
 
 
-def compile_asm(src, defines):
-    out = pathlib.Path("/tmp") / (pathlib.Path(src).stem + ".s")
+def compile_asm(src, defines, debug=False):
+    out = pathlib.Path("/tmp") / (pathlib.Path(src).stem + ("_g" if debug else "") + ".s")
     cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17",
            "-ffp-contract=off", f"-I{ROOT / 'include'}", "--cuda-device-only", "-S",
-           *defines, str(src), "-o", str(out)]
+           *(["-g"] if debug else []), *defines, str(src), "-o", str(out)]
     subprocess.run(cmd, check=True, stderr=subprocess.DEVNULL)
     return out.read_text().split("\n")
 
@@ -47,12 +51,71 @@ def kernel_lines(lines, sub):
     raise SystemExit(f"kernel {sub!r} not found")
 
 
+FUNC_RE = re.compile(r"(?:inline|__device__|__global__)[^;{()]*?\b([A-Za-z_]\w*)\s*\(")
+
+
+def func_table(path):
+    """(line, function) of every function head in a source file, ascending"""
+    out = []
+    try:
+        text = pathlib.Path(path).read_text().split("\n")
+    except OSError:
+        return out
+    for i, l in enumerate(text, 1):
+        m = FUNC_RE.search(l)
+        if m and m.group(1) not in ("if", "for", "while", "return", "sizeof"):
+            out.append((i, m.group(1)))
+    return out
+
+
+def by_source(all_lines, lines, loop_labels):
+    files = {}
+    for l in all_lines:
+        m = re.match(r'\s*\.file\s+(\d+)\s+"([^"]*)"(?:\s+"([^"]*)")?', l)
+        if m:
+            files[m.group(1)] = (m.group(2) + "/" + m.group(3)) if m.group(3) else m.group(2)
+    tables = {}
+    cur = None
+    inloop = False
+    cnt = collections.Counter()
+    for l in lines:
+        m = re.match(r"^(\.L(BB\d+_\d+):|; %bb\.\d+:)(.*)$", l)
+        if m:
+            lab = m.group(2)
+            ann = m.group(3)
+            mm = re.search(r"in Loop: Header=(BB\d+_\d+)", ann)
+            inloop = (lab in loop_labels) or (mm is not None and mm.group(1) in loop_labels)
+            continue
+        t = l.strip()
+        m = re.match(r"\.loc\s+(\d+)\s+(\d+)", t)
+        if m:
+            cur = (m.group(1), int(m.group(2)))
+            continue
+        if not inloop or not t.startswith("v_") or cur is None or cur[1] == 0:
+            continue
+        path = files.get(cur[0], "?")
+        if path not in tables:
+            tables[path] = func_table(path)
+        fn = "?"
+        for ln, name in tables[path]:
+            if ln <= cur[1]:
+                fn = name
+            else:
+                break
+        cnt[(pathlib.Path(path).name, fn)] += 1
+    total = sum(cnt.values())
+    print(f" VALU by source function (loop body, {total} instructions):")
+    for (f, fn), c in cnt.most_common(40):
+        print(f"   {c:4d} {100.0 * c / max(1, total):5.1f}%  {f}:{fn}")
+
+
 def main():
-    args = [a for a in sys.argv[1:] if not a.startswith("-D")]
+    dbg = "--by-source" in sys.argv
+    args = [a for a in sys.argv[1:] if not a.startswith("-")]
     defines = [a for a in sys.argv[1:] if a.startswith("-D")]
     src = args[0] if args else str(ROOT / "cpr_amd" / "csrc" / "kernels.hip")
     sub = args[1] if len(args) > 1 else "k_run_episodesILi0ENS_10SeedSourceELi3E"
-    all_lines = compile_asm(src, defines)
+    all_lines = compile_asm(src, defines, dbg)
     lines, name = kernel_lines(all_lines, sub)
     meta = kernel_meta(all_lines, name)
     # basic blocks: (label, annotation comments, instructions)
@@ -110,6 +173,9 @@ def main():
     print(f" nested loops inside it: VALU {nv}")
     for o, c in body.most_common(25):
         print(f"   {c:4d} {o}")
+    if dbg and hdr2:
+        # the loop body: its header block and every block annotated as in that loop
+        by_source(all_lines, lines, {hdr2[0]})
 
 
 if __name__ == "__main__":
