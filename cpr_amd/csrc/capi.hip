@@ -7,6 +7,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <memory>
 #include <string>
 #include <vector>
 
@@ -71,10 +72,13 @@ struct cpr_ctx {
   std::vector<RerunLaunch> rlaunch, rlaunch_up;
   // entries a launch may append (kRerunQueue; CPR_RERUN_QUEUE_CAP lowers it for tests);
   // an episode that finds the queue full waits in its launch's overflow flags: one byte
-  // per episode of every launch since the last flush, carved from `ovf`
+  // per episode of every launch since the last flush, carved from the chunks of `ovf` in
+  // order (chunk ovf_chunk, ovf_used bytes taken). Chunks are only added, never
+  // reallocated, so filling one never forces a flush: a flush costs the latency of one
+  // exact episode (~80 ms at the gym's 2016 steps), paid once per synchronization
   int64_t rq_cap = kRerunQueue;
-  DevBuf ovf;
-  size_t ovf_used = 0;
+  std::vector<std::unique_ptr<DevBuf>> ovf;
+  size_t ovf_chunk = 0, ovf_used = 0;
   // per-lane scratch regions of fused-episode launches (event-engine rings and heaps, the
   // Nakamoto lane's spill / time log / tie-replay scratch), shared by every batch of the
   // context: launches on the context's stream run in order, so one grow-only pool serves an
@@ -894,7 +898,8 @@ static int flush_reruns(cpr_ctx* c) {
                                  (const int64_t*)c->rq.p, qn, c->rq_cap, (uint8_t*)c->rmem.p,
                                  lb, rest, kRerunLanes, c->stream));
   HIP_TRY(hipMemsetAsync(qn, 0, 4, c->stream));
-  c->ovf_used = 0;  // the next launches' flags follow these re-runs on the stream
+  c->ovf_chunk = 0;  // the next launches' flags follow these re-runs on the stream
+  c->ovf_used = 0;
   return CPR_OK;
 }
 
@@ -918,15 +923,21 @@ static int register_rerun(cpr_batch* b, const eth::EthParams& EP, int64_t lane_b
     if (rc) return rc;
     c->rq_cap = cap;
   }
-  if (c->rlaunch.size() >= kRerunMaxLaunches || c->ovf_used + need > c->ovf.bytes) {
+  if (c->rlaunch.size() >= kRerunMaxLaunches) {
     int rc = flush_reruns(c);
     if (rc) return rc;
   }
-  if (need > c->ovf.bytes) {
-    HIP_TRY(hipStreamSynchronize(c->stream));  // earlier re-runs may still read the flags
-    HIP_TRY(c->ovf.ensure(std::max(need, (size_t)64 << 20)));
+  // the launch's flags: the rest of the current chunk, else the next chunk that holds them
+  // (a new one if none does; earlier chunks stay, queued kernels may still read them)
+  while (c->ovf_chunk < c->ovf.size() && c->ovf_used + need > c->ovf[c->ovf_chunk]->bytes) {
+    ++c->ovf_chunk;
+    c->ovf_used = 0;
   }
-  *ovf = (uint8_t*)c->ovf.p + c->ovf_used;
+  if (c->ovf_chunk == c->ovf.size()) {
+    c->ovf.emplace_back(new DevBuf());
+    HIP_TRY(c->ovf.back()->ensure(std::max(need, (size_t)256 << 20)));
+  }
+  *ovf = (uint8_t*)c->ovf[c->ovf_chunk]->p + c->ovf_used;
   HIP_TRY(hipMemsetAsync(*ovf, 0, need, c->stream));
   c->ovf_used += need;
   if (!c->rq.p) {
