@@ -73,10 +73,23 @@ s = {
     "hbm_write_bytes_per_dispatch (WRITE_SIZE x1024)": r["WRITE_SIZE"]["per_dispatch"] * 1024,
     "counters": r,
 }
+# the LDS pass (tools/profile.sh pmc_lds): LDS instructions and bank-conflict cycles of the
+# same launches, in a pass of its own
+try:
+    la, ln = agg("gpurun_out/prof_pmc_lds/run_counter_collection.csv")
+    lk = la.get(K, {})
+    if "SQ_INSTS_LDS" in lk:
+        lds = lk["SQ_INSTS_LDS"] / ln[(K, "SQ_INSTS_LDS")]
+        conf = lk.get("SQ_LDS_BANK_CONFLICT", 0.0) / max(1, ln.get((K, "SQ_LDS_BANK_CONFLICT"), 1))
+        s["lds_wave_instr_per_activation"] = lds * 64 / acts
+        s["lds_bank_conflict_cycles_per_lds_instr"] = conf / lds if lds else 0.0
+        s["lds_counters"] = {c: {"sum": x, "dispatches": ln[(K, c)]} for c, x in lk.items()}
+except FileNotFoundError:
+    pass
 s["valu_issue_frac_of_78.6T"] = s["valu_lane_ops_per_s"] / 7.86432e13
 s["hbm_bytes_per_activation"] = (s["hbm_read_bytes_per_dispatch (FETCH_SIZE x1024 x2, gfx950 correction)"]
                                  + s["hbm_write_bytes_per_dispatch (WRITE_SIZE x1024)"]) / acts
 json.dump(s, open(f"profiles/{tag}_pmc_summary.json", "w"), indent=1)
 shutil.copy("gpurun_out/prof_trace/run_kernel_stats.csv", f"profiles/{tag}_kernel_stats.csv")
 shutil.copy("gpurun_out/bench.log", f"profiles/{tag}_bench.jsonl") if False else None
-print(json.dumps({k: v for k, v in s.items() if k != "counters"}, indent=1))
+print(json.dumps({k: v for k, v in s.items() if k not in ("counters", "lds_counters")}, indent=1))
