@@ -283,6 +283,7 @@ struct TsLane {
   int32_t pub, priv, npend;
   int32_t o_pub, o_priv, o_common, o_event;
   int32_t troot;  // summary whose tree cand[] holds
+  int32_t tclosed;  // every tree vote's parent is troot or a tree vote (M.key parent links)
   int64_t steps;
 
   // ------------------------------------------------------------------ storage
@@ -498,10 +499,18 @@ struct TsLane {
       M.cand[j] = t;
     }
     int32_t m = 0, maxd = 0;
+    tclosed = 1;
     for (int32_t i = 0; i < n; ++i) {
       const int32_t c = M.cand[i];
       const TVtx& x = X(P, M, c);
-      if (vf != VF_ALL && x.parent != b && !in_tree(P, M, m, x.parent)) continue;
+      const bool pin = x.parent != b && in_tree(P, M, m, x.parent);
+      if (vf != VF_ALL && x.parent != b && !pin) continue;
+      // the selections' view of the tree vote (M.key[m]): vote depth, position of its
+      // parent + 1 (0 = the summary b), and whether `node` withholds or released it
+      const int32_t pp = x.parent == b ? 0 : (pin ? PS(P, M, x.parent) + 1 : 0);
+      if (x.parent != b && !pin) tclosed = 0;  // parent outside the tree: walk the DAG
+      M.key[m] = (uint64_t)(uint32_t)x.depth | ((uint64_t)(uint32_t)pp << 32) |
+                 (mine(P, M, c, node) ? (1ull << 63) : 0ull);
       PS(P, M, c) = m;
       M.cand[m++] = c;
       maxd = x.depth > maxd ? x.depth : maxd;
@@ -514,9 +523,9 @@ struct TsLane {
     }
     int32_t* cnt = M.aux;  // [maxd + 2] <= cap_v
     for (int32_t d = 0; d <= maxd + 1; ++d) cnt[d] = 0;
-    for (int32_t i = 0; i < m; ++i) ++cnt[X(P, M, M.cand[i]).depth + 1];
+    for (int32_t i = 0; i < m; ++i) ++cnt[(int32_t)(uint32_t)M.key[i] + 1];
     for (int32_t d = 1; d <= maxd + 1; ++d) cnt[d] += cnt[d - 1];
-    for (int32_t i = 0; i < m; ++i) M.perm[cnt[X(P, M, M.cand[i]).depth]++] = i;
+    for (int32_t i = 0; i < m; ++i) M.perm[cnt[(int32_t)(uint32_t)M.key[i]]++] = i;
     return m;
   }
   // votes of summary b's tree at `node` passing `vf` after expansion (compare_blocks,
@@ -572,6 +581,47 @@ struct TsLane {
     // flag = included
     for (int32_t i = 0; i < n; ++i) M.flag[i] = 0;
     int32_t need = P.k, nl = 0, dinc = 0;
+    if (tclosed) {
+      // on tree()'s view (M.key: depth, parent position, own): the same walks by position
+      // instead of by vertex (PS(s) is s's position; the parent chain ends at troot = 0)
+      while (need > 0 && !dead) {
+        int32_t best = -1, bo = -1, bt = -1;
+        for (int32_t pi = 0; pi < n; ++pi) {
+          const int32_t i = M.perm[pi];
+          if (M.flag[i]) continue;
+          if ((int32_t)(uint32_t)M.key[i] - dinc > need) continue;
+          int32_t own = 0, tot = 0, p = i + 1;
+          while (p != 0) {
+            if (M.flag[p - 1]) break;
+            if (++tot > need) break;
+            const uint64_t kp = M.key[p - 1];
+            own += (int32_t)(kp >> 63);
+            p = (int32_t)((kp >> 32) & 0x7fffffffu);
+          }
+          if (tot > need) continue;
+          if (own > bo || (own == bo && tot > bt)) {
+            best = i;
+            bo = own;
+            bt = tot;
+          }
+        }
+        if (best < 0) {  // `assert false` in the reference
+          fail(11);
+          return 0;
+        }
+        q[nl++] = M.cand[best];
+        const int32_t db = (int32_t)(uint32_t)M.key[best];
+        dinc = db > dinc ? db : dinc;
+        for (int32_t p = best + 1; p != 0;) {
+          uint8_t& f = M.flag[p - 1];
+          if (f) break;
+          f = 1;
+          --need;
+          p = (int32_t)((M.key[p - 1] >> 32) & 0x7fffffffu);
+        }
+      }
+      return nl;
+    }
     while (need > 0 && !dead) {
       int32_t best = -1, bo = -1, bt = -1;
       for (int32_t pi = 0; pi < n; ++pi) {
@@ -743,6 +793,10 @@ struct TsLane {
   // Honest.next_summary' (tailstorm.ml:530-535): draft seq or -1
   __host__ __device__ inline int32_t next_summary(const TsParams& P, const TsMem& M,
                                                   int32_t node, int32_t b, int32_t vf) {
+    // the tree's votes are a subset of b's vote list, whose length is b.nconf (append_vote):
+    // fewer than k there and the tree walk cannot find k (every vote of the list is newer
+    // than b, so the walk could not meet an overwritten ring slot either)
+    if (X(P, M, b).nconf < P.k) return -1;
     const int32_t n = tree(P, M, b, node, vf);
     if (dead || n < P.k) return -1;  // all three selections need k votes
     const int32_t seq = dseq;
