@@ -482,38 +482,54 @@ struct TsLane {
     int32_t n = 0;
     const int32_t cap = P.cap_v;
     troot = b;
-    for (int32_t c = X(P, M, b).thead; c >= 0 && !dead; c = X(P, M, c).next) {
+    // one read of each vote: its parent, depth and kind at `node` go to M.key with it
+    for (int32_t c = X(P, M, b).thead; c >= 0 && !dead;) {
+      const TVtx& x = X(P, M, c);
+      const int32_t nx = x.next;
       const uint8_t v = V(P, M, c, node);
-      if ((v & V_KIND) == V_INV) continue;
-      if (vf != VF_ALL && !keep_kind(v, vf, false)) continue;
-      if (n >= cap) {
-        fail(3);
-        return 0;
+      if ((v & V_KIND) != V_INV && (vf == VF_ALL || keep_kind(v, vf, false))) {
+        if (n >= cap) {
+          fail(3);
+          return 0;
+        }
+        const uint8_t kd = v & V_KIND;
+        M.key[n] = (uint64_t)(uint32_t)x.depth | ((uint64_t)(uint32_t)x.parent << 32);
+        M.flag[n] = (kd == V_WH || kd == V_REL) ? 1 : 0;  // mine()
+        M.cand[n++] = c;
       }
-      M.cand[n++] = c;
+      c = nx;
     }
     if (dead) return 0;
     for (int32_t i = 0, j = n - 1; i < j; ++i, --j) {  // newest-first list -> ascending
       const int32_t t = M.cand[i];
       M.cand[i] = M.cand[j];
       M.cand[j] = t;
+      const uint64_t tk = M.key[i];
+      M.key[i] = M.key[j];
+      M.key[j] = tk;
+      const uint8_t tf = M.flag[i];
+      M.flag[i] = M.flag[j];
+      M.flag[j] = tf;
     }
     int32_t m = 0, maxd = 0;
     tclosed = 1;
     for (int32_t i = 0; i < n; ++i) {
       const int32_t c = M.cand[i];
-      const TVtx& x = X(P, M, c);
-      const bool pin = x.parent != b && in_tree(P, M, m, x.parent);
-      if (vf != VF_ALL && x.parent != b && !pin) continue;
+      const uint64_t ki = M.key[i];
+      const int32_t depth = (int32_t)(uint32_t)ki, parent = (int32_t)(ki >> 32);
+      const bool own = M.flag[i] != 0;
+      const bool pin = parent != b && in_tree(P, M, m, parent);
+      if (vf != VF_ALL && parent != b && !pin) continue;
       // the selections' view of the tree vote (M.key[m]): vote depth, position of its
       // parent + 1 (0 = the summary b), and whether `node` withholds or released it
-      const int32_t pp = x.parent == b ? 0 : (pin ? PS(P, M, x.parent) + 1 : 0);
-      if (x.parent != b && !pin) tclosed = 0;  // parent outside the tree: walk the DAG
-      M.key[m] = (uint64_t)(uint32_t)x.depth | ((uint64_t)(uint32_t)pp << 32) |
-                 (mine(P, M, c, node) ? (1ull << 63) : 0ull);
+      // (m <= i: entry i is read before entry m is written)
+      const int32_t pp = parent == b ? 0 : (pin ? PS(P, M, parent) + 1 : 0);
+      if (parent != b && !pin) tclosed = 0;  // parent outside the tree: walk the DAG
+      M.key[m] = (uint64_t)(uint32_t)depth | ((uint64_t)(uint32_t)pp << 32) |
+                 (own ? (1ull << 63) : 0ull);
       PS(P, M, c) = m;
       M.cand[m++] = c;
-      maxd = x.depth > maxd ? x.depth : maxd;
+      maxd = depth > maxd ? depth : maxd;
     }
     // Dag depth of a tree vote = depth(b) + its vote depth: stable counting sort by vote
     // depth over the serial-ascending cand gives (Dag depth, serial)
@@ -1184,8 +1200,27 @@ struct TsLane {
   __host__ __device__ inline TsObs observe(const TsParams& P, const TsMem& M) {
     TsObs o;
     o.public_votes = count_post(P, M, o_pub, 0, VF_PUBLIC, &o.public_depth);
-    o.private_votes_inclusive = count_post(P, M, o_priv, 0, VF_ALL, &o.private_depth_inclusive);
-    o.private_votes_exclusive = count_post(P, M, o_priv, 0, VF_MINE, &o.private_depth_exclusive);
+    // VF_ALL and VF_MINE over the same list in one walk (count_post twice, fused)
+    {
+      int32_t na = 0, da = 0, nm = 0, dm = 0;
+      for (int32_t c = X(P, M, o_priv).thead; c >= 0 && !dead;) {
+        const TVtx& x = X(P, M, c);
+        const uint8_t kd = V(P, M, c, 0) & V_KIND;
+        if (kd != V_INV) {
+          ++na;
+          da = x.depth > da ? x.depth : da;
+          if (kd == V_WH || kd == V_REL) {
+            ++nm;
+            dm = x.depth > dm ? x.depth : dm;
+          }
+        }
+        c = x.next;
+      }
+      o.private_votes_inclusive = na;
+      o.private_depth_inclusive = da;
+      o.private_votes_exclusive = nm;
+      o.private_depth_exclusive = dm;
+    }
     const int32_t ca = X(P, M, o_common).height;
     const int32_t ph = X(P, M, o_priv).height, qh = X(P, M, o_pub).height;
     o.private_blocks = ph - ca;
