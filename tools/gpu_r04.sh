@@ -34,3 +34,10 @@ for g in ${PMC_GAMMAS:-}; do
   timeout -k 10 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_LDS SQ_WAIT_INST_ANY SQ_INSTS_VMEM_RD --output-format csv -d gpurun_out/${TAG}_pmc_g$g -o run -- python3 bench.py --steps 1 --warmup 0 --no-cpu --no-configs --gammas $g > gpurun_out/${TAG}_pmc_g$g.log 2>&1
   rc=$?; echo "pmc $g rc=$rc" | tee -a gpurun_out/${TAG}_status.log; [[ $rc -eq 0 ]] || exit $rc
 done
+# BASELINE's other configs under library variants (build/var/<name>.so; default = the tree's)
+for v in ${LIBS:-}; do
+  if [[ $v == default ]]; then L=cpr_amd/libcpr_hip.so; else L=build/var/$v.so; fi
+  echo "== lib $v" >> gpurun_out/${TAG}_libs.log
+  CPR_HIP_LIB=$L timeout -k 10 400 python tools/config_probe.py ${CONFIGS:-'configs[3]'} >> gpurun_out/${TAG}_libs.log 2>&1
+  rc=$?; echo "lib $v rc=$rc" | tee -a gpurun_out/${TAG}_status.log; [[ $rc -eq 0 ]] || exit $rc
+done
