@@ -66,8 +66,12 @@ struct BVtx {
   int32_t nconf;   // blocks: confirming votes in the global view (Referee.winner)
   int32_t qslot;   // blocks: quorum ring slot
   double time;     // Simulator.timestamp = append time
+  // the votes of a block, newest first (the order of the reference's children scans):
+  // block: its newest vote (-1 none); vote: the next older vote of the same block
+  int32_t vhead, vnext;
+  int32_t pad_[2];  // 64 B: one vertex per cache line
 };
-static_assert(sizeof(BVtx) == 48, "BVtx layout");
+static_assert(sizeof(BVtx) == 64, "BVtx layout");
 
 struct HNode {
   double t;
@@ -128,7 +132,7 @@ struct BkMem {
 __host__ __device__ inline int64_t bk_align(int64_t x) { return (x + 127) / 128 * 128; }
 
 __host__ __device__ inline int64_t bk_lane_bytes(const BkParams& P) {
-  return bk_align((int64_t)P.cap_v * 48) + bk_align((int64_t)P.cap_v * P.n) +
+  return bk_align((int64_t)P.cap_v * (int64_t)sizeof(BVtx)) + bk_align((int64_t)P.cap_v * P.n) +
          bk_align((int64_t)P.cap_v * P.n * 8) + bk_align((int64_t)P.cap_q * (P.k + 1) * 4) +
          bk_align((int64_t)P.cap_d * (P.k + 2) * 4) + bk_align((int64_t)P.cap_e * 24) +
          bk_align((int64_t)P.n * 4) + bk_align(2 * NQS * 8) + bk_align(2 * NQS * 4) +
@@ -139,7 +143,7 @@ __host__ __device__ inline BkMem bk_mem_at(uint8_t* base, const BkParams& P) {
   BkMem M;
   int64_t o = 0;
   M.vtx = (BVtx*)(base + o);
-  o += bk_align((int64_t)P.cap_v * 48);
+  o += bk_align((int64_t)P.cap_v * (int64_t)sizeof(BVtx));
   M.vis = base + o;
   o += bk_align((int64_t)P.cap_v * P.n);
   M.vt = (double*)(base + o);
@@ -485,6 +489,8 @@ struct BkLane {
     b.nconf = 0;
     b.qslot = -1;
     b.time = now;
+    b.vhead = -1;
+    b.vnext = -1;
     for (int32_t j = 0; j < P.n; ++j) V(P, M, s, j) = V_INV;
   }
   // vote: simulator.ml:122-136 (pow = (bits, serial)), bk.ml:281-286 payload
@@ -503,6 +509,8 @@ struct BkLane {
     b.rew_att = p.rew_att;  // precursor = the block; votes carry no reward (bk.ml:151-176)
     b.rew_def = p.rew_def;
     p.nconf += 1;
+    b.vnext = p.vhead;
+    p.vhead = s;
     return s;
   }
   // block from an Append draft (bk.ml:288-295), set_rewards (simulator.ml:377-388)
@@ -582,12 +590,11 @@ struct BkLane {
                                                 int32_t node, int32_t vf) {
     int32_t n = 0;
     CPR_BK_COST(BC_CONFIRMING_CALLS);
-    for (int32_t c = newest; c > b && !dead; --c) {
+    // b's votes (the vertices after b that are votes on b, newest first)
+    for (int32_t c = X(P, M, b).vhead; c >= 0 && !dead; c = X(P, M, c).vnext) {
       CPR_BK_COST(BC_CONFIRMING);
       const uint8_t v = V(P, M, c, node);
-      if ((v & V_KIND) == V_INV || !keep(v, vf)) continue;
-      const BVtx& x = X(P, M, c);
-      n += (x.vote && x.parent == b) ? 1 : 0;
+      n += ((v & V_KIND) != V_INV && keep(v, vf)) ? 1 : 0;
     }
     return n;
   }
@@ -622,12 +629,15 @@ struct BkLane {
     int32_t nmine = 0, ntheirs = 0;
     uint64_t my_hash = ~0ull;
     CPR_BK_COST(BC_PROPOSE_CALLS);
-    for (int32_t c = newest; c > b && !dead; --c) {
+    for (int32_t c = X(P, M, b).vhead; c >= 0 && !dead;) {  // b's votes, newest first
       CPR_BK_COST(BC_PROPOSE);
-      const uint8_t v = V(P, M, c, node);
-      if ((v & V_KIND) == V_INV || !keep(v, vf)) continue;
       const BVtx& x = X(P, M, c);
-      if (!x.vote || x.parent != b) continue;
+      const int32_t cn = x.vnext;
+      const uint8_t v = V(P, M, c, node);
+      if ((v & V_KIND) == V_INV || !keep(v, vf)) {
+        c = cn;
+        continue;
+      }
       const uint64_t key = pow_key(x);
       if (x.who == node) {
         if (nmine >= NQS) {
@@ -645,6 +655,7 @@ struct BkLane {
         tk[ntheirs] = key;
         tv[ntheirs++] = c;
       }
+      c = cn;
     }
     if (dead || nmine == 0 || nmine + ntheirs < P.k) return -1;  // fast path (bk.ml:254)
     const int32_t seq = dseq++;
@@ -774,12 +785,10 @@ struct BkLane {
     o.public_votes = confirming(P, M, o_pub, 0, VF_PUBLIC);
     o.private_votes_inclusive = 0;
     o.private_votes_exclusive = 0;
-    for (int32_t c = newest; c > o_priv && !dead; --c) {
+    for (int32_t c = X(P, M, o_priv).vhead; c >= 0 && !dead; c = X(P, M, c).vnext) {
       CPR_BK_COST(BC_OBSERVE);
       const uint8_t v = V(P, M, c, 0);
       if ((v & V_KIND) == V_INV) continue;
-      const BVtx& x = X(P, M, c);
-      if (!x.vote || x.parent != o_priv) continue;
       ++o.private_votes_inclusive;
       o.private_votes_exclusive += keep(v, VF_MINE) ? 1 : 0;
     }
@@ -822,17 +831,20 @@ struct BkLane {
       uint64_t* vk = M.skey;
       int32_t* vv = M.sval;
       int32_t nv = 0;
-      for (int32_t c = newest; c > block && !dead; --c) {
+      for (int32_t c = X(P, M, block).vhead; c >= 0 && !dead;) {  // block's votes
         CPR_BK_COST(BC_APPLY);
-        if (!visible(P, M, c, 0)) continue;
-        const BVtx& x = X(P, M, c);
-        if (!x.vote || x.parent != block) continue;
+        const int32_t cn = X(P, M, c).vnext;
+        if (!visible(P, M, c, 0)) {
+          c = cn;
+          continue;
+        }
         if (nv >= 2 * NQS) {
           fail(3);
           break;
         }
         vk[nv] = time_key(VT(P, M, c, 0));
         vv[nv++] = c;
+        c = cn;
       }
       int32_t take = nv;
       if (nv >= nvotes) {
@@ -880,6 +892,8 @@ struct BkLane {
     r.nconf = 0;
     r.qslot = -1;
     r.time = 0.0;
+    r.vhead = -1;
+    r.vnext = -1;
     for (int32_t j = 0; j < P.n; ++j) {
       V(P, M, 0, j) = V_RECV | V_GOT;
       VT(P, M, 0, j) = 0.0;
