@@ -66,12 +66,8 @@ struct BVtx {
   int32_t nconf;   // blocks: confirming votes in the global view (Referee.winner)
   int32_t qslot;   // blocks: quorum ring slot
   double time;     // Simulator.timestamp = append time
-  // the votes of a block, newest first (the order of the reference's children scans):
-  // block: its newest vote (-1 none); vote: the next older vote of the same block
-  int32_t vhead, vnext;
-  int32_t pad_[2];  // 64 B: one vertex per cache line
 };
-static_assert(sizeof(BVtx) == 64, "BVtx layout");
+static_assert(sizeof(BVtx) == 48, "BVtx layout");
 
 struct HNode {
   double t;
@@ -113,6 +109,12 @@ struct BkMem {
   HNode* hl = nullptr;
   int32_t kl = 0, hs = 1;
   BVtx* vtx;
+  // the votes of each block, newest first (the order of the reference's children scans),
+  // as two compact per-slot arrays beside the vertices so that a walk reads 4-byte links
+  // and visibility bytes, and a vote's 48-byte vertex only when it passes the filter:
+  // vh[block] = its newest vote (-1 none), vn[vote] = the next older vote of its block
+  int32_t* vh;
+  int32_t* vn;
   uint8_t* vis;
   double* vt;
   int32_t* quo;
@@ -132,7 +134,8 @@ struct BkMem {
 __host__ __device__ inline int64_t bk_align(int64_t x) { return (x + 127) / 128 * 128; }
 
 __host__ __device__ inline int64_t bk_lane_bytes(const BkParams& P) {
-  return bk_align((int64_t)P.cap_v * (int64_t)sizeof(BVtx)) + bk_align((int64_t)P.cap_v * P.n) +
+  return bk_align((int64_t)P.cap_v * (int64_t)sizeof(BVtx)) + 2 * bk_align((int64_t)P.cap_v * 4) +
+         bk_align((int64_t)P.cap_v * P.n) +
          bk_align((int64_t)P.cap_v * P.n * 8) + bk_align((int64_t)P.cap_q * (P.k + 1) * 4) +
          bk_align((int64_t)P.cap_d * (P.k + 2) * 4) + bk_align((int64_t)P.cap_e * 24) +
          bk_align((int64_t)P.n * 4) + bk_align(2 * NQS * 8) + bk_align(2 * NQS * 4) +
@@ -144,6 +147,10 @@ __host__ __device__ inline BkMem bk_mem_at(uint8_t* base, const BkParams& P) {
   int64_t o = 0;
   M.vtx = (BVtx*)(base + o);
   o += bk_align((int64_t)P.cap_v * (int64_t)sizeof(BVtx));
+  M.vh = (int32_t*)(base + o);
+  o += bk_align((int64_t)P.cap_v * 4);
+  M.vn = (int32_t*)(base + o);
+  o += bk_align((int64_t)P.cap_v * 4);
   M.vis = base + o;
   o += bk_align((int64_t)P.cap_v * P.n);
   M.vt = (double*)(base + o);
@@ -332,6 +339,12 @@ struct BkLane {
     if (b.serial != s) fail(1);
     return b;
   }
+  __host__ __device__ inline int32_t& VH(const BkParams& P, const BkMem& M, int32_t s) {
+    return M.vh[s & (P.cap_v - 1)];
+  }
+  __host__ __device__ inline int32_t& VN(const BkParams& P, const BkMem& M, int32_t s) {
+    return M.vn[s & (P.cap_v - 1)];
+  }
   __host__ __device__ inline uint8_t& V(const BkParams& P, const BkMem& M, int32_t s,
                                         int32_t node) {
     return M.vis[(int64_t)(s & (P.cap_v - 1)) * P.n + node];
@@ -489,8 +502,8 @@ struct BkLane {
     b.nconf = 0;
     b.qslot = -1;
     b.time = now;
-    b.vhead = -1;
-    b.vnext = -1;
+    VH(P, M, s) = -1;
+    VN(P, M, s) = -1;
     for (int32_t j = 0; j < P.n; ++j) V(P, M, s, j) = V_INV;
   }
   // vote: simulator.ml:122-136 (pow = (bits, serial)), bk.ml:281-286 payload
@@ -509,8 +522,8 @@ struct BkLane {
     b.rew_att = p.rew_att;  // precursor = the block; votes carry no reward (bk.ml:151-176)
     b.rew_def = p.rew_def;
     p.nconf += 1;
-    b.vnext = p.vhead;
-    p.vhead = s;
+    VN(P, M, s) = VH(P, M, parent);
+    VH(P, M, parent) = s;
     return s;
   }
   // block from an Append draft (bk.ml:288-295), set_rewards (simulator.ml:377-388)
@@ -591,7 +604,7 @@ struct BkLane {
     int32_t n = 0;
     CPR_BK_COST(BC_CONFIRMING_CALLS);
     // b's votes (the vertices after b that are votes on b, newest first)
-    for (int32_t c = X(P, M, b).vhead; c >= 0 && !dead; c = X(P, M, c).vnext) {
+    for (int32_t c = VH(P, M, b); c >= 0 && !dead; c = VN(P, M, c)) {
       CPR_BK_COST(BC_CONFIRMING);
       const uint8_t v = V(P, M, c, node);
       n += ((v & V_KIND) != V_INV && keep(v, vf)) ? 1 : 0;
@@ -629,15 +642,15 @@ struct BkLane {
     int32_t nmine = 0, ntheirs = 0;
     uint64_t my_hash = ~0ull;
     CPR_BK_COST(BC_PROPOSE_CALLS);
-    for (int32_t c = X(P, M, b).vhead; c >= 0 && !dead;) {  // b's votes, newest first
+    for (int32_t c = VH(P, M, b); c >= 0 && !dead;) {  // b's votes, newest first
       CPR_BK_COST(BC_PROPOSE);
-      const BVtx& x = X(P, M, c);
-      const int32_t cn = x.vnext;
+      const int32_t cn = VN(P, M, c);
       const uint8_t v = V(P, M, c, node);
       if ((v & V_KIND) == V_INV || !keep(v, vf)) {
         c = cn;
         continue;
       }
+      const BVtx& x = X(P, M, c);
       const uint64_t key = pow_key(x);
       if (x.who == node) {
         if (nmine >= NQS) {
@@ -785,7 +798,7 @@ struct BkLane {
     o.public_votes = confirming(P, M, o_pub, 0, VF_PUBLIC);
     o.private_votes_inclusive = 0;
     o.private_votes_exclusive = 0;
-    for (int32_t c = X(P, M, o_priv).vhead; c >= 0 && !dead; c = X(P, M, c).vnext) {
+    for (int32_t c = VH(P, M, o_priv); c >= 0 && !dead; c = VN(P, M, c)) {
       CPR_BK_COST(BC_OBSERVE);
       const uint8_t v = V(P, M, c, 0);
       if ((v & V_KIND) == V_INV) continue;
@@ -831,9 +844,9 @@ struct BkLane {
       uint64_t* vk = M.skey;
       int32_t* vv = M.sval;
       int32_t nv = 0;
-      for (int32_t c = X(P, M, block).vhead; c >= 0 && !dead;) {  // block's votes
+      for (int32_t c = VH(P, M, block); c >= 0 && !dead;) {  // block's votes
         CPR_BK_COST(BC_APPLY);
-        const int32_t cn = X(P, M, c).vnext;
+        const int32_t cn = VN(P, M, c);
         if (!visible(P, M, c, 0)) {
           c = cn;
           continue;
@@ -892,8 +905,8 @@ struct BkLane {
     r.nconf = 0;
     r.qslot = -1;
     r.time = 0.0;
-    r.vhead = -1;
-    r.vnext = -1;
+    VH(P, M, 0) = -1;
+    VN(P, M, 0) = -1;
     for (int32_t j = 0; j < P.n; ++j) {
       V(P, M, 0, j) = V_RECV | V_GOT;
       VT(P, M, 0, j) = 0.0;
