@@ -102,12 +102,25 @@ struct TsParams {
 
 constexpr int32_t NFR = 64;      // common-ancestor frontier (reference walk, tests only)
 
+// the list view of a vertex slot, beside the 64-byte vertices (TsMem.trec): the walks over a
+// summary's vote list and child-summary list (tree, count_post, observe, payload_parent,
+// has_children, MadeDescendantsVisible) read these 16 bytes and the visibility byte instead
+// of a whole vertex. Written once when the vertex is appended (the fields never change).
+struct TRec {
+  int32_t next;    // TVtx.next
+  int32_t depth;   // TVtx.depth
+  int32_t pow;     // TVtx.pow
+  int32_t parent;  // TVtx.parent
+};
+static_assert(sizeof(TRec) == 16, "TRec layout");
+
 struct TsMem {
   // event-heap nodes 0 .. kl-1 in the workgroup's LDS slab (node-major, stride hs), the
   // rest in HBM (heap); see bk_lane.h BkMem
   HNode* hl = nullptr;
   int32_t kl = 0, hs = 1;
   TVtx* vtx;
+  TRec* trec;
   uint8_t* vis;
   double* vt;
   int32_t* quo;
@@ -133,7 +146,8 @@ struct TsMem {
 __host__ __device__ inline int64_t ts_align(int64_t x) { return (x + 127) / 128 * 128; }
 
 __host__ __device__ inline int64_t ts_lane_bytes(const TsParams& P) {
-  return ts_align((int64_t)P.cap_v * 64) + ts_align((int64_t)P.cap_v * P.n) +
+  return ts_align((int64_t)P.cap_v * 64) + ts_align((int64_t)P.cap_v * 16) +
+         ts_align((int64_t)P.cap_v * P.n) +
          ts_align((int64_t)P.cap_v * P.n * 8) + ts_align((int64_t)P.cap_q * (P.k + 1) * 4) +
          ts_align((int64_t)P.cap_q * 2 * P.n * 8) + ts_align((int64_t)P.cap_d * (P.k + 2) * 4) +
          ts_align((int64_t)P.cap_e * 24) + ts_align((int64_t)P.n * 4) +
@@ -151,6 +165,7 @@ __host__ __device__ inline TsMem ts_mem_at(uint8_t* base, const TsParams& P) {
     return p;
   };
   M.vtx = (TVtx*)take((int64_t)P.cap_v * 64);
+  M.trec = (TRec*)take((int64_t)P.cap_v * 16);
   M.vis = take((int64_t)P.cap_v * P.n);
   M.vt = (double*)take((int64_t)P.cap_v * P.n * 8);
   M.quo = (int32_t*)take((int64_t)P.cap_q * (P.k + 1) * 4);
@@ -296,6 +311,18 @@ struct TsLane {
     TVtx& b = M.vtx[s & (P.cap_v - 1)];
     if (b.serial != s) fail(1);
     return b;
+  }
+  // the list view of vertex s (TRec). Unchecked: the walks start from a vertex read with X,
+  // and every vertex of its lists is newer, so it is in the ring whenever the start is
+  __host__ __device__ inline TRec& TR(const TsParams& P, const TsMem& M, int32_t s) {
+    return M.trec[s & (P.cap_v - 1)];
+  }
+  __host__ __device__ inline void set_trec(const TsParams& P, const TsMem& M, const TVtx& b) {
+    TRec& r = TR(P, M, b.serial);
+    r.next = b.next;
+    r.depth = b.depth;
+    r.pow = b.pow;
+    r.parent = b.parent;
   }
   __host__ __device__ inline uint8_t& V(const TsParams& P, const TsMem& M, int32_t s,
                                         int32_t node) {
@@ -485,7 +512,7 @@ struct TsLane {
     troot = b;
     // one read of each vote: its parent, depth and kind at `node` go to M.key with it
     for (int32_t c = X(P, M, b).thead; c >= 0 && !dead;) {
-      const TVtx& x = X(P, M, c);
+      const TRec& x = TR(P, M, c);
       const int32_t nx = x.next;
       const uint8_t v = V(P, M, c, node);
       if ((v & V_KIND) != V_INV && (vf == VF_ALL || keep_kind(v, vf, false))) {
@@ -551,7 +578,7 @@ struct TsLane {
                                                 int32_t node, int32_t vf, int32_t* maxd) {
     int32_t n = 0, d = 0;
     for (int32_t c = X(P, M, b).thead; c >= 0 && !dead;) {
-      const TVtx& x = X(P, M, c);
+      const TRec& x = TR(P, M, c);
       const uint8_t v = V(P, M, c, node);
       if ((v & V_KIND) != V_INV &&
           keep_kind(v, vf, vf == VF_PUBLIC_OR_MARKED && MK(P, M, c))) {
@@ -848,10 +875,18 @@ struct TsLane {
   // Honest.puzzle_payload (tailstorm.ml:509-528): parent of the next vote on summary b
   __host__ __device__ inline int32_t payload_parent(const TsParams& P, const TsMem& M,
                                                     int32_t node, int32_t b) {
-    int32_t best = b;
+    int32_t best = b, bd = 0, bp = 0;
     for (int32_t c = X(P, M, b).thead; c >= 0 && !dead;) {
-      const TVtx& x = X(P, M, c);
-      if (visible(P, M, c, node) && (best == b || vote_before(x, X(P, M, best)))) best = c;
+      const TRec& x = TR(P, M, c);
+      // vote_before (deeper first, then the smaller (pow, serial))
+      if (visible(P, M, c, node) &&
+          (best == b || x.depth > bd ||
+           (x.depth == bd && (((uint64_t)(uint32_t)x.pow << 32) | (uint32_t)c) <
+                                 (((uint64_t)(uint32_t)bp << 32) | (uint32_t)best)))) {
+        best = c;
+        bd = x.depth;
+        bp = x.pow;
+      }
       c = x.next;
     }
     return best;
@@ -879,7 +914,7 @@ struct TsLane {
                                                int32_t node) {
     // children of a summary are votes on it: the depth-1 votes of its tree
     for (int32_t c = X(P, M, s).thead; c >= 0 && !dead;) {
-      const TVtx& x = X(P, M, c);
+      const TRec& x = TR(P, M, c);
       if (x.parent == s && visible(P, M, c, node)) return true;
       c = x.next;
     }
@@ -923,6 +958,7 @@ struct TsLane {
     sb.nconf += 1;
     b.next = sb.thead;  // newest-first vote list of the tree
     sb.thead = s;
+    set_trec(P, M, b);
     return s;
   }
   // Dag(node, Append, draft): Simulator.append dedup (simulator.ml:139-159) or a fresh
@@ -1017,6 +1053,7 @@ struct TsLane {
     SH(P, M, s) = -1;
     b.next = SH(P, M, prev);  // newest-first child-summary list of prev
     SH(P, M, prev) = s;
+    set_trec(P, M, b);
     return s;
   }
 
@@ -1221,7 +1258,7 @@ struct TsLane {
     {
       int32_t na = 0, da = 0, nm = 0, dm = 0;
       for (int32_t c = X(P, M, o_priv).thead; c >= 0 && !dead;) {
-        const TVtx& x = X(P, M, c);
+        const TRec& x = TR(P, M, c);
         const uint8_t kd = V(P, M, c, 0) & V_KIND;
         if (kd != V_INV) {
           ++na;
@@ -1385,6 +1422,7 @@ struct TsLane {
     r.time = 0.0;
     r.next = -1;
     r.thead = -1;
+    set_trec(P, M, r);
     SH(P, M, 0) = -1;
     for (int32_t j = 0; j < P.n; ++j) {
       V(P, M, 0, j) = V_RECV | V_GOT;
@@ -1508,9 +1546,9 @@ struct TsLane {
         int32_t cv = sv ? X(P, M, sb.sum).thead : sb.thead;
         int32_t cq = sv ? SH(P, M, sb.sum) : -1;
         while (!dead) {
-          while (cv > s && !(X(P, M, cv).parent == s && (V(P, M, cv, node) & V_GOT)))
-            cv = X(P, M, cv).next;
-          while (cq > s && !(V(P, M, cq, node) & V_GOT)) cq = X(P, M, cq).next;
+          while (cv > s && !(TR(P, M, cv).parent == s && (V(P, M, cv, node) & V_GOT)))
+            cv = TR(P, M, cv).next;
+          while (cq > s && !(V(P, M, cq, node) & V_GOT)) cq = TR(P, M, cq).next;
           if (cq > s) {  // summary holding s?
             const TVtx& cb = X(P, M, cq);
             bool child = false;
@@ -1525,10 +1563,10 @@ struct TsLane {
           int32_t c;
           if (cv > cq) {
             c = cv;
-            cv = X(P, M, cv).next;
+            cv = TR(P, M, cv).next;
           } else {
             c = cq;
-            cq = X(P, M, cq).next;
+            cq = TR(P, M, cq).next;
           }
           push_now(P, M, mkev(EV_MV, node, KD_NET), c);
         }
