@@ -114,7 +114,7 @@ struct BkMem {
   // and visibility bytes, and a vote's 48-byte vertex only when it passes the filter:
   // vh[block] = its newest vote (-1 none), vn[vote] = the next older vote of its block
   int32_t* vh;
-  int32_t* vn;
+  int4* vn;  // x = next older vote of the block, y = pow, z = who (the propose scan's fields)
   uint8_t* vis;
   double* vt;
   int32_t* quo;
@@ -134,7 +134,8 @@ struct BkMem {
 __host__ __device__ inline int64_t bk_align(int64_t x) { return (x + 127) / 128 * 128; }
 
 __host__ __device__ inline int64_t bk_lane_bytes(const BkParams& P) {
-  return bk_align((int64_t)P.cap_v * (int64_t)sizeof(BVtx)) + 2 * bk_align((int64_t)P.cap_v * 4) +
+  return bk_align((int64_t)P.cap_v * (int64_t)sizeof(BVtx)) + bk_align((int64_t)P.cap_v * 4) +
+         bk_align((int64_t)P.cap_v * 16) +
          bk_align((int64_t)P.cap_v * P.n) +
          bk_align((int64_t)P.cap_v * P.n * 8) + bk_align((int64_t)P.cap_q * (P.k + 1) * 4) +
          bk_align((int64_t)P.cap_d * (P.k + 2) * 4) + bk_align((int64_t)P.cap_e * 24) +
@@ -149,8 +150,8 @@ __host__ __device__ inline BkMem bk_mem_at(uint8_t* base, const BkParams& P) {
   o += bk_align((int64_t)P.cap_v * (int64_t)sizeof(BVtx));
   M.vh = (int32_t*)(base + o);
   o += bk_align((int64_t)P.cap_v * 4);
-  M.vn = (int32_t*)(base + o);
-  o += bk_align((int64_t)P.cap_v * 4);
+  M.vn = (int4*)(base + o);
+  o += bk_align((int64_t)P.cap_v * 16);
   M.vis = base + o;
   o += bk_align((int64_t)P.cap_v * P.n);
   M.vt = (double*)(base + o);
@@ -343,6 +344,9 @@ struct BkLane {
     return M.vh[s & (P.cap_v - 1)];
   }
   __host__ __device__ inline int32_t& VN(const BkParams& P, const BkMem& M, int32_t s) {
+    return M.vn[s & (P.cap_v - 1)].x;
+  }
+  __host__ __device__ inline int4& VR(const BkParams& P, const BkMem& M, int32_t s) {
     return M.vn[s & (P.cap_v - 1)];
   }
   __host__ __device__ inline uint8_t& V(const BkParams& P, const BkMem& M, int32_t s,
@@ -522,7 +526,10 @@ struct BkLane {
     b.rew_att = p.rew_att;  // precursor = the block; votes carry no reward (bk.ml:151-176)
     b.rew_def = p.rew_def;
     p.nconf += 1;
-    VN(P, M, s) = VH(P, M, parent);
+    int4& r = VR(P, M, s);
+    r.x = VH(P, M, parent);
+    r.y = b.pow;
+    r.z = node;
     VH(P, M, parent) = s;
     return s;
   }
@@ -644,15 +651,15 @@ struct BkLane {
     CPR_BK_COST(BC_PROPOSE_CALLS);
     for (int32_t c = VH(P, M, b); c >= 0 && !dead;) {  // b's votes, newest first
       CPR_BK_COST(BC_PROPOSE);
-      const int32_t cn = VN(P, M, c);
+      const int4 r = VR(P, M, c);  // (next, pow, who): pow_key without the vertex
+      const int32_t cn = r.x;
       const uint8_t v = V(P, M, c, node);
       if ((v & V_KIND) == V_INV || !keep(v, vf)) {
         c = cn;
         continue;
       }
-      const BVtx& x = X(P, M, c);
-      const uint64_t key = pow_key(x);
-      if (x.who == node) {
+      const uint64_t key = ((uint64_t)(uint32_t)r.y << 32) | (uint32_t)c;
+      if (r.z == node) {
         if (nmine >= NQS) {
           fail(3);
           return -1;
