@@ -117,7 +117,7 @@ static_assert(sizeof(TRec) == 16, "TRec layout");
 struct TsMem {
   // event-heap nodes 0 .. kl-1 in the workgroup's LDS slab (node-major, stride hs), the
   // rest in HBM (heap); see bk_lane.h BkMem
-  HNode* hl = nullptr;
+  CPR_LDS HNode* hl = nullptr;
   int32_t kl = 0, hs = 1;
   TVtx* vtx;
   TRec* trec;
@@ -191,7 +191,7 @@ __host__ __device__ inline TsMem ts_mem_at(uint8_t* base, const TsParams& P) {
 // the LDS heap slab of a kernel (as bk_lane.h bk_heap_*)
 __host__ __device__ inline void ts_heap_slab(TsMem& M, HNode* slab, int32_t lane, int32_t stride,
                                              int32_t kl) {
-  M.hl = slab + lane;
+  M.hl = (CPR_LDS HNode*)(slab + lane);
   M.hs = stride;
   M.kl = kl;
 }
@@ -360,22 +360,77 @@ struct TsLane {
 
   // ------------------------------------------------------------------ event queue
   // orderedQueue.ml:17-47, in place; +inf events are stored (they shape the tie order)
-  // node i of the event heap: the LDS slab below M.kl, else HBM (the heap's order never
-  // depends on which node holds an element)
-  __host__ __device__ static inline HNode& HN(const TsMem& M, int32_t i) {
-    return i < M.kl ? M.hl[(int64_t)i * M.hs] : M.heap[i];
+  // Nodes are read and written by value through hn_*, each picking the slab (LDS, an
+  // address-space-3 pointer: ds_read / ds_write) or the HBM part (global loads) by index,
+  // so the compiler never merges the two into one generic (flat) access.
+  __host__ __device__ static inline HNode hn_get(const TsMem& M, int32_t i) {
+    if (i < M.kl) {
+      // volatile: keeps this a load of its own (the compiler would otherwise merge the two
+      // branches into one load through a generic pointer)
+      const volatile CPR_LDS HNode& v = M.hl[(int64_t)i * M.hs];
+      HNode h;
+      h.t = v.t;
+      h.ev = v.ev;
+      h.blk = v.blk;
+      h.l = v.l;
+      h.r = v.r;
+      return h;
+    }
+    return M.heap[i];
+  }
+  __host__ __device__ static inline void hn_put(const TsMem& M, int32_t i, const HNode& h) {
+    if (i < M.kl)
+      M.hl[(int64_t)i * M.hs] = h;
+    else
+      M.heap[i] = h;
+  }
+  __host__ __device__ static inline void hn_set_l(const TsMem& M, int32_t i, int32_t v) {
+    if (i < M.kl)
+      M.hl[(int64_t)i * M.hs].l = v;
+    else
+      M.heap[i].l = v;
+  }
+  __host__ __device__ static inline void hn_set_r(const TsMem& M, int32_t i, int32_t v) {
+    if (i < M.kl)
+      M.hl[(int64_t)i * M.hs].r = v;
+    else
+      M.heap[i].r = v;
+  }
+  __host__ __device__ static inline void hn_set_lr(const TsMem& M, int32_t i, int32_t l,
+                                                   int32_t r) {
+    if (i < M.kl) {
+      M.hl[(int64_t)i * M.hs].l = l;
+      M.hl[(int64_t)i * M.hs].r = r;
+    } else {
+      M.heap[i].l = l;
+      M.heap[i].r = r;
+    }
+  }
+  __host__ __device__ static inline void hn_set_key(const TsMem& M, int32_t i, double t,
+                                                    uint32_t ev, int32_t blk) {
+    if (i < M.kl) {
+      CPR_LDS HNode& h = M.hl[(int64_t)i * M.hs];
+      h.t = t;
+      h.ev = ev;
+      h.blk = blk;
+    } else {
+      HNode& h = M.heap[i];
+      h.t = t;
+      h.ev = ev;
+      h.blk = blk;
+    }
   }
   // free nodes: slab nodes first (hfree), then HBM nodes (hfree2)
   __host__ __device__ inline int32_t halloc(const TsParams& P, const TsMem& M) {
     int32_t i;
     if (hfree >= 0) {
       i = hfree;
-      hfree = HN(M, i).l;
+      hfree = hn_get(M, i).l;
     } else if (hused < P.cap_e && (hused < M.kl || hfree2 < 0)) {
       i = hused++;
     } else if (hfree2 >= 0) {
       i = hfree2;
-      hfree2 = HN(M, i).l;
+      hfree2 = hn_get(M, i).l;
     } else {
       fail(2);
       return -1;
@@ -384,10 +439,10 @@ struct TsLane {
   }
   __host__ __device__ inline void hrelease(const TsMem& M, int32_t node) {
     if (node < M.kl) {
-      HN(M, node).l = hfree;
+      hn_set_l(M, node, hfree);
       hfree = node;
     } else {
-      HN(M, node).l = hfree2;
+      hn_set_l(M, node, hfree2);
       hfree2 = node;
     }
   }
@@ -398,46 +453,44 @@ struct TsLane {
       if (node < 0) {
         const int32_t a = halloc(P, M);
         if (a < 0) return;
-        HNode& h = HN(M, a);
+        HNode h;
         h.t = t;
         h.ev = ev;
         h.blk = blk;
         h.l = -1;
         h.r = -1;
+        hn_put(M, a, h);
         if (parent < 0)
           hroot = a;
         else
-          HN(M, parent).l = a;
+          hn_set_l(M, parent, a);
         return;
       }
-      HNode& h = HN(M, node);
-      if (t < h.t) {
-        const double ot = h.t;
-        const uint32_t oe = h.ev;
-        const int32_t ob = h.blk;
-        h.t = t;
-        h.ev = ev;
-        h.blk = blk;
-        t = ot;
-        ev = oe;
-        blk = ob;
-      } else {
-        const int32_t tmp = h.l;
-        h.l = h.r;
-        h.r = tmp;
+      const HNode h = hn_get(M, node);
+      int32_t next;
+      if (t < h.t) {  // the new element takes the node, the old one moves down
+        hn_set_key(M, node, t, ev, blk);
+        t = h.t;
+        ev = h.ev;
+        blk = h.blk;
+        next = h.l;
+      } else {  // children swapped, then down the (new) left
+        hn_set_lr(M, node, h.r, h.l);
+        next = h.r;
       }
       parent = node;
-      node = h.l;
+      node = next;
     }
   }
   __host__ __device__ inline bool pop(const TsMem& M, double* t, uint32_t* ev, int32_t* blk) {
     if (hroot < 0) return false;
-    *t = HN(M, hroot).t;
-    *ev = HN(M, hroot).ev;
-    *blk = HN(M, hroot).blk;
+    HNode cur = hn_get(M, hroot);
+    *t = cur.t;
+    *ev = cur.ev;
+    *blk = cur.blk;
     int32_t parent = -1, side = 0, node = hroot;
     for (;;) {
-      const int32_t l = HN(M, node).l, r = HN(M, node).r;
+      const int32_t l = cur.l, r = cur.r;
       int32_t repl = -2;
       if (r < 0)
         repl = l;
@@ -447,19 +500,19 @@ struct TsLane {
         if (parent < 0)
           hroot = repl;
         else if (side == 0)
-          HN(M, parent).l = repl;
+          hn_set_l(M, parent, repl);
         else
-          HN(M, parent).r = repl;
+          hn_set_r(M, parent, repl);
         hrelease(M, node);
         return true;
       }
-      const int32_t c = (HN(M, l).t <= HN(M, r).t) ? l : r;
-      HN(M, node).t = HN(M, c).t;
-      HN(M, node).ev = HN(M, c).ev;
-      HN(M, node).blk = HN(M, c).blk;
+      const HNode hl_ = hn_get(M, l), hr_ = hn_get(M, r);
+      const bool left = hl_.t <= hr_.t;
+      cur = left ? hl_ : hr_;
+      hn_set_key(M, node, cur.t, cur.ev, cur.blk);
       parent = node;
-      side = c == l ? 0 : 1;
-      node = c;
+      side = left ? 0 : 1;
+      node = left ? l : r;
     }
   }
   __host__ __device__ inline void push_now(const TsParams& P, const TsMem& M, uint32_t ev,
