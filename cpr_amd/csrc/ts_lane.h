@@ -108,9 +108,11 @@ constexpr int32_t NFR = 64;      // common-ancestor frontier (reference walk, te
 // of a whole vertex. Written once when the vertex is appended (the fields never change).
 struct TRec {
   int32_t next;    // TVtx.next
-  int32_t depth;   // TVtx.depth
+  int32_t depth;   // TVtx.depth (< cap_v <= 4096) | TVtx.who << 16
   int32_t pow;     // TVtx.pow
   int32_t parent;  // TVtx.parent
+  __host__ __device__ inline int32_t dep() const { return depth & 0xffff; }
+  __host__ __device__ inline int32_t who() const { return depth >> 16; }
 };
 static_assert(sizeof(TRec) == 16, "TRec layout");
 
@@ -320,7 +322,7 @@ struct TsLane {
   __host__ __device__ inline void set_trec(const TsParams& P, const TsMem& M, const TVtx& b) {
     TRec& r = TR(P, M, b.serial);
     r.next = b.next;
-    r.depth = b.depth;
+    r.depth = (b.depth & 0xffff) | (int32_t)((uint32_t)b.who << 16);
     r.pow = b.pow;
     r.parent = b.parent;
   }
@@ -574,7 +576,7 @@ struct TsLane {
           return 0;
         }
         const uint8_t kd = v & V_KIND;
-        M.key[n] = (uint64_t)(uint32_t)x.depth | ((uint64_t)(uint32_t)x.parent << 32);
+        M.key[n] = (uint64_t)(uint32_t)x.dep() | ((uint64_t)(uint32_t)x.parent << 32);
         M.flag[n] = (kd == V_WH || kd == V_REL) ? 1 : 0;  // mine()
         M.cand[n++] = c;
       }
@@ -636,7 +638,7 @@ struct TsLane {
       if ((v & V_KIND) != V_INV &&
           keep_kind(v, vf, vf == VF_PUBLIC_OR_MARKED && MK(P, M, c))) {
         ++n;
-        d = x.depth > d ? x.depth : d;
+        d = x.dep() > d ? x.dep() : d;
       }
       c = x.next;
     }
@@ -933,11 +935,11 @@ struct TsLane {
       const TRec& x = TR(P, M, c);
       // vote_before (deeper first, then the smaller (pow, serial))
       if (visible(P, M, c, node) &&
-          (best == b || x.depth > bd ||
-           (x.depth == bd && (((uint64_t)(uint32_t)x.pow << 32) | (uint32_t)c) <
+          (best == b || x.dep() > bd ||
+           (x.dep() == bd && (((uint64_t)(uint32_t)x.pow << 32) | (uint32_t)c) <
                                  (((uint64_t)(uint32_t)bp << 32) | (uint32_t)best)))) {
         best = c;
-        bd = x.depth;
+        bd = x.dep();
         bp = x.pow;
       }
       c = x.next;
@@ -1071,24 +1073,26 @@ struct TsLane {
     const double r = discount ? (double)l0.depth / (double)P.k * 1.0 : 1.0;
     // the confirmed set = union of the leaves' branches; mark to count each vote once
     const int32_t upto = punish ? 1 : nl;
+    // (the branches' votes are newer than prev: their list records are in the ring)
     for (int32_t t = 0; t < upto; ++t) {
       int32_t v = lv[t];
       while (v != prev && !dead) {
         MK(P, M, v) = 0;
-        v = X(P, M, v).parent;
+        v = TR(P, M, v).parent;
       }
     }
     for (int32_t t = 0; t < upto; ++t) {
       int32_t v = lv[t];
       while (v != prev && !dead) {
         uint8_t& mk = MK(P, M, v);
+        const TRec& x = TR(P, M, v);
         if (!mk) {
           mk = 1;
-          const int32_t w = X(P, M, v).who;
+          const int32_t w = x.who();
           rw[w] += r;
           rw[P.n + w] += r;
         }
-        v = X(P, M, v).parent;
+        v = x.parent;
       }
     }
     TVtx& b = M.vtx[s & (P.cap_v - 1)];
@@ -1315,10 +1319,10 @@ struct TsLane {
         const uint8_t kd = V(P, M, c, 0) & V_KIND;
         if (kd != V_INV) {
           ++na;
-          da = x.depth > da ? x.depth : da;
+          da = x.dep() > da ? x.dep() : da;
           if (kd == V_WH || kd == V_REL) {
             ++nm;
-            dm = x.depth > dm ? x.depth : dm;
+            dm = x.dep() > dm ? x.dep() : dm;
           }
         }
         c = x.next;
