@@ -94,7 +94,10 @@ struct LaneMem {
 };
 
 // deferred races: queue entries per lane of a wave (the list is the wave's: 64 times this)
-constexpr int32_t RQ_LANE = 6;
+#ifndef CPR_RQ_LANE
+#define CPR_RQ_LANE 6
+#endif
+constexpr int32_t RQ_LANE = CPR_RQ_LANE;
 // words of a NakLane without block times (NakLane::pack, the host tests' state comparison)
 constexpr int32_t CK_WORDS = 38;
 

@@ -175,12 +175,12 @@ def variant(name, rng, log, rev=None):
         assert "amdgpu_waves_per_eu(4)" in k
         (d / "kernels.hip").write_text(k.replace("amdgpu_waves_per_eu(4)",
                                                  f"amdgpu_waves_per_eu({m.group(1)})", 1))
-    extra = []
+    extra = os.environ.get("PROBE_DEFS", "").split()  # e.g. "-DCPR_TT_WAVES=6 -DCPR_RQ_LANE=5"
     if name.startswith("ilp"):
-        extra = ["-mllvm", "-amdgpu-sched-strategy=max-ilp"]
+        extra += ["-mllvm", "-amdgpu-sched-strategy=max-ilp"]
     m = re.match(r"bias(\d+)", name)
     if m:
-        extra = ["-mllvm", f"-amdgpu-schedule-metric-bias={m.group(1)}"]
+        extra += ["-mllvm", f"-amdgpu-schedule-metric-bias={m.group(1)}"]
     tu = os.environ.get("PROBE_TU", "kernels.hip")  # the translation unit rebuilt
     obj = OUT / f"{tu}_{name}.o"
     subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17",
