@@ -116,6 +116,12 @@ struct BkMem {
   // slab load nodes 0 .. kl-1 from heap at entry and store them back at exit (bk_heap_*)
   CPR_LDS HNode* hl = nullptr;
   int32_t kl = 0, hs = 1;
+  // visibility rows of the newest vw vertices (vw a power of 2, 0 = none) in the same
+  // workgroup slab, row-major per lane: byte (slot * n + node) * hs of vl, slot = s & (vw - 1).
+  // Writes go to both places (HBM stays complete), reads of a vertex in the window to LDS:
+  // the walks (vote lists, MadeDescendantsVisible, the release closure) read recent rows
+  CPR_LDS uint8_t* vl = nullptr;
+  int32_t vw = 0;
   BVtx* vtx;
   // the votes of each block, newest first (the order of the reference's children scans),
   // as two compact per-slot arrays beside the vertices so that a walk reads 4-byte links
@@ -188,6 +194,18 @@ __host__ __device__ inline void bk_heap_slab(BkMem& M, HNode* slab, int32_t lane
   M.hl = (CPR_LDS HNode*)(slab + lane);
   M.hs = stride;
   M.kl = kl;
+}
+// the visibility window (BkMem.vl) of a kernel: after the heap slab's kl nodes; persistent
+// lanes (rollouts) load the window's rows at entry (bk_vis_load)
+__host__ __device__ inline void bk_vis_window(BkMem& M, uint8_t* base, int32_t lane, int32_t vw) {
+  M.vl = (CPR_LDS uint8_t*)(base + lane);
+  M.vw = vw;
+}
+__host__ __device__ inline void bk_vis_load(const BkMem& M, const BkParams& P, int32_t newest) {
+  for (int32_t s = newest - M.vw + 1 < 0 ? 0 : newest - M.vw + 1; s <= newest; ++s)
+    for (int32_t j = 0; j < P.n; ++j)
+      M.vl[(int64_t)((s & (M.vw - 1)) * P.n + j) * M.hs] =
+          M.vis[(int64_t)(s & (P.cap_v - 1)) * P.n + j];
 }
 __host__ __device__ inline void bk_heap_load(const BkMem& M, int32_t hused) {
   const int32_t n = hused < M.kl ? hused : M.kl;
@@ -367,7 +385,23 @@ struct BkLane {
   }
   __host__ __device__ inline bool visible(const BkParams& P, const BkMem& M, int32_t s,
                                           int32_t node) {
-    return (V(P, M, s, node) & V_KIND) != V_INV;
+    return (Vg(P, M, s, node) & V_KIND) != V_INV;
+  }
+  // visibility of vertex s at node: from the LDS window when s is one of the newest vw
+  // vertices (every append writes its row into the window slot it takes), else HBM
+  __host__ __device__ inline uint8_t Vg(const BkParams& P, const BkMem& M, int32_t s,
+                                        int32_t node) const {
+    if (s > newest - M.vw) {
+      // volatile: a load of its own (not merged with the HBM branch into a flat access)
+      return *(const volatile CPR_LDS uint8_t*)&M.vl[(int64_t)((s & (M.vw - 1)) * P.n + node) *
+                                                      M.hs];
+    }
+    return M.vis[(int64_t)(s & (P.cap_v - 1)) * P.n + node];
+  }
+  __host__ __device__ inline void Vs(const BkParams& P, const BkMem& M, int32_t s, int32_t node,
+                                     uint8_t v) const {
+    M.vis[(int64_t)(s & (P.cap_v - 1)) * P.n + node] = v;
+    if (s > newest - M.vw) M.vl[(int64_t)((s & (M.vw - 1)) * P.n + node) * M.hs] = v;
   }
   __host__ __device__ inline int32_t* Q(const BkParams& P, const BkMem& M, const BVtx& b) {
     int32_t* q = M.quo + (int64_t)(b.qslot & (P.cap_q - 1)) * (P.k + 1);
@@ -568,7 +602,7 @@ struct BkLane {
     b.time = now;
     VH(P, M, s) = -1;
     VN(P, M, s) = -1;
-    for (int32_t j = 0; j < P.n; ++j) V(P, M, s, j) = V_INV;
+    for (int32_t j = 0; j < P.n; ++j) Vs(P, M, s, j, V_INV);
   }
   // vote: simulator.ml:122-136 (pow = (bits, serial)), bk.ml:281-286 payload
   template <class St>
@@ -673,7 +707,7 @@ struct BkLane {
     // b's votes (the vertices after b that are votes on b, newest first)
     for (int32_t c = VH(P, M, b); c >= 0 && !dead; c = VN(P, M, c)) {
       CPR_BK_COST(BC_CONFIRMING);
-      const uint8_t v = V(P, M, c, node);
+      const uint8_t v = Vg(P, M, c, node);
       n += ((v & V_KIND) != V_INV && keep(v, vf)) ? 1 : 0;
     }
     return n;
@@ -713,7 +747,7 @@ struct BkLane {
       CPR_BK_COST(BC_PROPOSE);
       const int4 r = VR(P, M, c);  // (next, pow, who): pow_key without the vertex
       const int32_t cn = r.x;
-      const uint8_t v = V(P, M, c, node);
+      const uint8_t v = Vg(P, M, c, node);
       if ((v & V_KIND) == V_INV || !keep(v, vf)) {
         c = cn;
         continue;
@@ -794,9 +828,9 @@ struct BkLane {
     st[sp++] = s0;
     while (sp > 0 && !dead) {
       const int32_t s = st[--sp];
-      uint8_t& v = V(P, M, s, node);
+      const uint8_t v = Vg(P, M, s, node);
       if ((v & V_KIND) != V_WH) continue;  // received / released: nothing
-      v = (uint8_t)((v & ~V_KIND) | V_REL);
+      Vs(P, M, s, node, (uint8_t)((v & ~V_KIND) | V_REL));
       push_now(P, M, mkev(EV_TX, node, KD_NET), s);
       const BVtx& b = X(P, M, s);
       if (b.parent < 0) continue;
@@ -867,7 +901,7 @@ struct BkLane {
     o.private_votes_exclusive = 0;
     for (int32_t c = VH(P, M, o_priv); c >= 0 && !dead; c = VN(P, M, c)) {
       CPR_BK_COST(BC_OBSERVE);
-      const uint8_t v = V(P, M, c, 0);
+      const uint8_t v = Vg(P, M, c, 0);
       if ((v & V_KIND) == V_INV) continue;
       ++o.private_votes_inclusive;
       o.private_votes_exclusive += keep(v, VF_MINE) ? 1 : 0;
@@ -975,7 +1009,7 @@ struct BkLane {
     VH(P, M, 0) = -1;
     VN(P, M, 0) = -1;
     for (int32_t j = 0; j < P.n; ++j) {
-      V(P, M, 0, j) = V_RECV | V_GOT;
+      Vs(P, M, 0, j, V_RECV | V_GOT);
       VT(P, M, 0, j) = 0.0;
       M.tips[j] = 0;
       if (M.nact) M.nact[j] = 0;
@@ -989,7 +1023,7 @@ struct BkLane {
                                          int32_t x) {
     const int32_t b = last_block(P, M, x);
     const int32_t d = propose(P, M, node, VF_ALL, b);
-    if ((V(P, M, x, node) & V_KIND) == V_WH) share(P, M, node, x);
+    if ((Vg(P, M, x, node) & V_KIND) == V_WH) share(P, M, node, x);
     M.tips[node] = update_head(P, M, node, VF_ALL, M.tips[node], b);
     if (d >= 0) push_now(P, M, mkev(EV_DAG, node, KD_APP), d);
   }
@@ -1003,7 +1037,7 @@ struct BkLane {
     CPR_BK_COST(BC_EVENT + (int32_t)ty);
     switch (ty) {
       case EV_MV: {
-        uint8_t& v = V(P, M, s, node);
+        const uint8_t v = Vg(P, M, s, node);
         if ((v & V_KIND) != V_INV) break;
         const BVtx& b = X(P, M, s);
         bool ok = b.parent < 0 || visible(P, M, b.parent, node);
@@ -1012,7 +1046,7 @@ struct BkLane {
           for (int32_t i = 0; i < P.k && ok; ++i) ok = visible(P, M, q[i], node);
         }
         if (!ok) break;
-        v = (uint8_t)((v & ~V_KIND) | (kind == KD_NET ? V_RECV : V_WH));
+        Vs(P, M, s, node, (uint8_t)((v & ~V_KIND) | (kind == KD_NET ? V_RECV : V_WH)));
         VT(P, M, s, node) = now;
         push_now(P, M, mkev(EV_ON, node, kind), s);
         push_now(P, M, mkev(EV_MDV, node, kind), s);
@@ -1074,9 +1108,9 @@ struct BkLane {
         // first receipt, so a delivery at t = +inf (Simulator.loop draining gamma = 0
         // messages) changes nothing
         if (!(now < __builtin_inf())) break;
-        uint8_t& v = V(P, M, s, node);
+        const uint8_t v = Vg(P, M, s, node);
         if (!(v & V_GOT)) {
-          v |= V_GOT;
+          Vs(P, M, s, node, (uint8_t)(v | V_GOT));
           push_now(P, M, mkev(EV_MV, node, KD_NET), s);
         }
         break;
@@ -1087,7 +1121,7 @@ struct BkLane {
         const bool is_vote = X(P, M, s).vote != 0;
         for (int32_t c = newest; c > s && !dead; --c) {
           CPR_BK_COST(BC_MDV);
-          if (!(V(P, M, c, node) & V_GOT)) continue;
+          if (!(Vg(P, M, c, node) & V_GOT)) continue;
           const BVtx& cb = X(P, M, c);
           bool child = cb.parent == s;
           if (!child && is_vote && !cb.vote) {

@@ -117,15 +117,18 @@ extern __shared__ __attribute__((aligned(16))) bk::HNode bk_slab[];
 template <class Src>
 __global__ __launch_bounds__(kBlock) CPR_EV_OCC void k_bk_run_episodes(
     bk::BkParams P, Src src, int64_t n_eps, uint8_t* mem,
-    int64_t lane_bytes, cpr_episode_record* recs, cpr_summary* sum, NodeOut no, int32_t kl) {
+    int64_t lane_bytes, cpr_episode_record* recs, cpr_summary* sum, NodeOut no, int32_t kl,
+    int32_t vw) {
   __shared__ int32_t hist[CPR_HIST_BINS];
   if (threadIdx.x < CPR_HIST_BINS) hist[threadIdx.x] = 0;
   __syncthreads();
   const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t nthreads = (int64_t)gridDim.x * blockDim.x;
   bk::BkMem M = bk::bk_mem_at(mem + tid * lane_bytes, P);
-  // every episode starts with an empty heap (init): the slab needs no load or store
+  // every episode starts with an empty heap and a fresh window (init): the slab needs no
+  // load or store
   bk::bk_heap_slab(M, bk_slab, (int32_t)threadIdx.x, (int32_t)blockDim.x, kl);
+  bk::bk_vis_window(M, (uint8_t*)(bk_slab + (size_t)kl * blockDim.x), (int32_t)threadIdx.x, vw);
   if (no.mem) bk::bk_node_mem(M, no.mem + tid * no.lane_bytes, P);
   Acc acc = {};
   bk::BkLane L;
@@ -274,7 +277,7 @@ __global__ __launch_bounds__(kBlock) CPR_EV_OCC void k_bk_rollout(bk::BkParams P
                                                         const double* tabs, int32_t tn,
                                                         double* obs, double* reward,
                                                         uint8_t* done_out, cpr_summary* sum,
-                                                        int32_t kl) {
+                                                        int32_t kl, int32_t vw) {
   __shared__ int32_t hist[CPR_HIST_BINS];
   if (threadIdx.x < CPR_HIST_BINS) hist[threadIdx.x] = 0;
   __syncthreads();
@@ -286,6 +289,7 @@ __global__ __launch_bounds__(kBlock) CPR_EV_OCC void k_bk_rollout(bk::BkParams P
   // every lane's own sequence of events, actions and outputs is the plain loop's
   bk::BkMem M = bk::bk_mem_at(mem + (i < n ? i : 0) * lane_bytes, P);
   bk::bk_heap_slab(M, bk_slab, (int32_t)threadIdx.x, (int32_t)blockDim.x, kl);
+  bk::bk_vis_window(M, (uint8_t*)(bk_slab + (size_t)kl * blockDim.x), (int32_t)threadIdx.x, vw);
   BkSlot SL;
   EvCursor c;
   c.cls = -1;
@@ -296,6 +300,7 @@ __global__ __launch_bounds__(kBlock) CPR_EV_OCC void k_bk_rollout(bk::BkParams P
   if (i < n) {
     SL = slots[i];
     bk::bk_heap_load(M, SL.L.hused);
+    bk::bk_vis_load(M, P, SL.L.newest);
     if (!SL.live)
       bk_slot_reset(P, seed, M, SL, (uint64_t)i);
     else
@@ -370,7 +375,10 @@ __global__ __launch_bounds__(kBlock) CPR_EV_OCC void k_bk_rollout(bk::BkParams P
     BkSlot SL = slots[i];
     // the lane's heap nodes 0 .. kl-1 move to the slab for this launch
     bk::bk_heap_slab(M, bk_slab, (int32_t)threadIdx.x, (int32_t)blockDim.x, kl);
+    bk::bk_vis_window(M, (uint8_t*)(bk_slab + (size_t)kl * blockDim.x), (int32_t)threadIdx.x,
+                      vw);
     bk::bk_heap_load(M, SL.L.hused);
+    bk::bk_vis_load(M, P, SL.L.newest);
     if (!SL.live) {
       bk_slot_reset(P, seed, M, SL, (uint64_t)i);
       acts_all += SL.L.c_act;
@@ -484,15 +492,59 @@ int32_t ev_slab_nodes(int64_t blocks, const void* kernel) {
   return kl;
 }
 
+// the B_k kernels' slab: the heap's first kl nodes and the visibility rows of the newest vw
+// vertices (BkMem.vl; 64, else 32, when they take at most a third of the workgroup's share
+// of LDS; CPR_BK_VWIN overrides it, 0 = none); kl from what is left (ev_slab_nodes' rules)
+struct BkSlab {
+  int32_t kl, vw;
+  size_t bytes;
+};
+static BkSlab bk_slab_plan(int64_t blocks, const void* kernel, int32_t n) {
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        cus <= 0)
+      cus = 256;
+  }
+  const int64_t per_cu = std::max<int64_t>(1, (blocks + cus - 1) / cus);
+  const int64_t avail = (160 * 1024) / per_cu - 2048;  // static LDS of the kernels
+  int32_t vw = 0;
+  for (int32_t w : {64, 32})
+    if (vw == 0 && (int64_t)w * n * kBlock * 3 <= avail) vw = w;
+  if (const char* v = getenv("CPR_BK_VWIN")) {
+    const int32_t w = atoi(v);
+    vw = (w >= 1 && (w & (w - 1)) == 0 && w <= 256) ? w : 0;
+  }
+  int64_t rest = avail - (int64_t)vw * n * kBlock;
+  if (rest < 0) {
+    vw = 0;
+    rest = avail;
+  }
+  int32_t kl = (int32_t)std::min<int64_t>(32, std::max<int64_t>(0, rest / (kBlock * 24)));
+  if (const char* v = getenv("CPR_EV_SLAB")) kl = std::max(0, std::min(32, atoi(v)));
+  size_t bytes = (size_t)kl * kBlock * 24 + (size_t)vw * n * kBlock;
+  if (bytes > 64 * 1024 &&
+      hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                          160 * 1024 - 2048) != hipSuccess) {
+    (void)hipGetLastError();  // the default 64 KiB: the heap slab alone
+    vw = 0;
+    kl = (64 * 1024) / (kBlock * 24);
+    bytes = (size_t)kl * kBlock * 24;
+  }
+  return BkSlab{kl, vw, bytes};
+}
+
 hipError_t launch_bk_run_episodes(const bk::BkParams& P, uint64_t seed, uint64_t first,
                                   int64_t n_eps, uint8_t* mem, int64_t lane_bytes, int64_t lanes,
                                   cpr_episode_record* recs, cpr_summary* sum, hipStream_t st,
                                   const NodeOut& no) {
   const unsigned blocks = (unsigned)(lanes / kBlock);
-  const int32_t kl = ev_slab_nodes(blocks, (const void*)k_bk_run_episodes<SeedSource>);
-  hipLaunchKernelGGL(k_bk_run_episodes<SeedSource>, dim3(blocks), dim3(kBlock),
-                     (size_t)kl * kBlock * 24, st, P, SeedSource{seed, first}, n_eps, mem,
-                     lane_bytes, recs, sum, no, kl);
+  const BkSlab sl = bk_slab_plan(blocks, (const void*)k_bk_run_episodes<SeedSource>, P.n);
+  hipLaunchKernelGGL(k_bk_run_episodes<SeedSource>, dim3(blocks), dim3(kBlock), sl.bytes, st, P,
+                     SeedSource{seed, first}, n_eps, mem, lane_bytes, recs, sum, no, sl.kl,
+                     sl.vw);
   return hipGetLastError();
 }
 
@@ -501,10 +553,9 @@ hipError_t launch_bk_replay_episodes(const bk::BkParams& P, const TraceSource& s
                                  cpr_episode_record* recs, cpr_summary* sum, hipStream_t st,
                                   const NodeOut& no) {
   const unsigned blocks = (unsigned)(lanes / kBlock);
-  const int32_t kl = ev_slab_nodes(blocks, (const void*)k_bk_run_episodes<TraceSource>);
-  hipLaunchKernelGGL(k_bk_run_episodes<TraceSource>, dim3(blocks), dim3(kBlock),
-                     (size_t)kl * kBlock * 24, st, P, src, n_eps, mem, lane_bytes, recs, sum, no,
-                     kl);
+  const BkSlab sl = bk_slab_plan(blocks, (const void*)k_bk_run_episodes<TraceSource>, P.n);
+  hipLaunchKernelGGL(k_bk_run_episodes<TraceSource>, dim3(blocks), dim3(kBlock), sl.bytes, st, P,
+                     src, n_eps, mem, lane_bytes, recs, sum, no, sl.kl, sl.vw);
   return hipGetLastError();
 }
 
@@ -529,10 +580,10 @@ hipError_t launch_bk_rollout(const bk::BkParams& P, uint64_t seed, uint8_t* mem,
                              int64_t lane_bytes, void* slots, int64_t n, int64_t n_steps,
                              int unit, const double* tabs, int32_t tn, double* obs,
                              double* reward, uint8_t* done, cpr_summary* sum, hipStream_t st) {
-  const int32_t kl = ev_slab_nodes(grid_of(n), (const void*)k_bk_rollout);
-  hipLaunchKernelGGL(k_bk_rollout, dim3(grid_of(n)), dim3(kBlock), (size_t)kl * kBlock * 24, st,
-                     P, seed, mem, lane_bytes, (BkSlot*)slots, n, n_steps, unit, tabs, tn, obs,
-                     reward, done, sum, kl);
+  const BkSlab sl = bk_slab_plan(grid_of(n), (const void*)k_bk_rollout, P.n);
+  hipLaunchKernelGGL(k_bk_rollout, dim3(grid_of(n)), dim3(kBlock), sl.bytes, st, P, seed, mem,
+                     lane_bytes, (BkSlot*)slots, n, n_steps, unit, tabs, tn, obs, reward, done,
+                     sum, sl.kl, sl.vw);
   return hipGetLastError();
 }
 

@@ -81,6 +81,18 @@ static bk::BkParams params_of(const Cfg& cf) {
   return P;
 }
 
+// SLABTEST=1: the lane's event-heap slab (nodes 0..5) and visibility window (8 vertices)
+// in host buffers, stride 1, so the host fuzz runs the device kernels' LDS paths too
+static bk::BkMem with_slab(bk::BkMem M, const bk::BkParams& P) {
+  static std::vector<bk::HNode> slab(6);
+  static std::vector<uint8_t> win;
+  if (!getenv("SLABTEST")) return M;
+  win.assign((size_t)8 * P.n, 0);
+  bk::bk_heap_slab(M, slab.data(), 0, 1, 6);
+  bk::bk_vis_window(M, win.data(), 0, 8);
+  return M;
+}
+
 static bool run_gym(const Cfg& cf, uint64_t seed, uint64_t ep, Counters& C, std::string& why) {
   oracle::GymParams gp;
   gp.alpha = cf.alpha;
@@ -98,7 +110,7 @@ static bool run_gym(const Cfg& cf, uint64_t seed, uint64_t ep, Counters& C, std:
 
   const bk::BkParams P = params_of(cf);
   std::vector<uint8_t> mem(bk::bk_lane_bytes(P));
-  const bk::BkMem M = bk::bk_mem_at(mem.data(), P);
+  const bk::BkMem M = with_slab(bk::bk_mem_at(mem.data(), P), P);
   const Stream S{(uint32_t)seed, (uint32_t)(seed >> 32), (uint32_t)ep, (uint32_t)(ep >> 32)};
   bk::BkLane L;
   L.gym_reset(P, S, M);
@@ -212,7 +224,7 @@ static bool run_loop(const Cfg& cf, uint64_t seed, uint64_t ep, Counters& C, std
   const int64_t a0 = cf.two_agents == 2 ? L0_ANY : r.activations[0];
   const bk::BkParams P = params_of(cf);
   std::vector<uint8_t> mem(bk::bk_lane_bytes(P));
-  const bk::BkMem M = bk::bk_mem_at(mem.data(), P);
+  const bk::BkMem M = with_slab(bk::bk_mem_at(mem.data(), P), P);
   const Stream S{(uint32_t)seed, (uint32_t)(seed >> 32), (uint32_t)ep, (uint32_t)(ep >> 32)};
   bk::BkLane L;
   const int32_t hd = L.loop(P, S, M);

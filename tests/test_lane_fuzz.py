@@ -9,6 +9,7 @@ alpha x gamma (defenders 2..42) and for Simulator.loop on the two-agents network
 """
 
 import json
+import os
 import pathlib
 import subprocess
 
@@ -93,6 +94,11 @@ def test_bk_lane_matches_oracle_fuzz():
         assert p.returncode == 0, p.stderr[-2000:]
         assert out["mismatches"] == 0, p.stderr[-2000:]
         assert out["episodes"] > 700 and out["capacity"] == 0
+    # the device kernels' LDS paths (event-heap slab, visibility window) in host buffers
+    p = subprocess.run([str(exe), "2", "400", "8"], capture_output=True, text=True,
+                       timeout=600, env=dict(os.environ, SLABTEST="1"))
+    out = json.loads(p.stdout.strip().splitlines()[-1])
+    assert p.returncode == 0 and out["mismatches"] == 0, p.stderr[-2000:]
 
 
 def test_tailstorm_lane_matches_oracle_fuzz():
@@ -111,6 +117,11 @@ def test_tailstorm_lane_matches_oracle_fuzz():
         assert p.returncode == 0, p.stderr[-2000:]
         assert out["mismatches"] == 0, p.stderr[-2000:]
         assert out["episodes"] > 250 and out["capacity"] == 0
+    # the device kernels' LDS path (event-heap slab) in a host buffer
+    p = subprocess.run([str(exe), "2", "300", "8", "1"], capture_output=True, text=True,
+                       timeout=600, env=dict(os.environ, SLABTEST="1"))
+    out = json.loads(p.stdout.strip().splitlines()[-1])
+    assert p.returncode == 0 and out["mismatches"] == 0, p.stderr[-2000:]
 
 
 def test_device_log_and_philox_match_oracle():
