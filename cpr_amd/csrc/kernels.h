@@ -140,6 +140,13 @@ int eth_blocks_per_cu();
 // event-heap nodes per lane in the LDS slab of an event-engine kernel launched with
 // `blocks` workgroups (kernels_bk.hip; the B_k and Tailstorm lanes' BkMem / TsMem.hl)
 int32_t ev_slab_nodes(int64_t blocks, const void* kernel);
+// heap slab nodes, visibility-window vertices and dynamic LDS bytes of a B_k / Tailstorm
+// kernel launched with `blocks` workgroups on n nodes (kernels_bk.hip)
+struct EvSlab {
+  int32_t kl, vw;
+  size_t bytes;
+};
+EvSlab ev_slab_plan(int64_t blocks, const void* kernel, int32_t n);
 // Ethereum gym episodes on the selfish-mining network through the window lane
 // (eth_window.h; ethw::win_supported): mem = lanes x ethw::win_lane_bytes; flagged episodes
 // go to the exact re-run queue (redo / redo_n, entries tagged with launch_id)

@@ -492,14 +492,11 @@ int32_t ev_slab_nodes(int64_t blocks, const void* kernel) {
   return kl;
 }
 
-// the B_k kernels' slab: the heap's first kl nodes and the visibility rows of the newest vw
-// vertices (BkMem.vl; 64, else 32, when they take at most a third of the workgroup's share
-// of LDS; CPR_BK_VWIN overrides it, 0 = none); kl from what is left (ev_slab_nodes' rules)
-struct BkSlab {
-  int32_t kl, vw;
-  size_t bytes;
-};
-static BkSlab bk_slab_plan(int64_t blocks, const void* kernel, int32_t n) {
+// an event-engine kernel's slab: the heap's first kl nodes and the visibility rows of the
+// newest vw vertices (BkMem.vl / TsMem.vl; 64, else 32, when they take at most a third of
+// the workgroup's share of LDS; CPR_EV_VWIN overrides it, 0 = none); kl from what is left
+// (ev_slab_nodes' rules)
+EvSlab ev_slab_plan(int64_t blocks, const void* kernel, int32_t n) {
   static int cus = 0;
   if (!cus) {
     int dev = 0;
@@ -513,7 +510,7 @@ static BkSlab bk_slab_plan(int64_t blocks, const void* kernel, int32_t n) {
   int32_t vw = 0;
   for (int32_t w : {64, 32})
     if (vw == 0 && (int64_t)w * n * kBlock * 3 <= avail) vw = w;
-  if (const char* v = getenv("CPR_BK_VWIN")) {
+  if (const char* v = getenv("CPR_EV_VWIN")) {
     const int32_t w = atoi(v);
     vw = (w >= 1 && (w & (w - 1)) == 0 && w <= 256) ? w : 0;
   }
@@ -533,7 +530,7 @@ static BkSlab bk_slab_plan(int64_t blocks, const void* kernel, int32_t n) {
     kl = (64 * 1024) / (kBlock * 24);
     bytes = (size_t)kl * kBlock * 24;
   }
-  return BkSlab{kl, vw, bytes};
+  return EvSlab{kl, vw, bytes};
 }
 
 hipError_t launch_bk_run_episodes(const bk::BkParams& P, uint64_t seed, uint64_t first,
@@ -541,7 +538,7 @@ hipError_t launch_bk_run_episodes(const bk::BkParams& P, uint64_t seed, uint64_t
                                   cpr_episode_record* recs, cpr_summary* sum, hipStream_t st,
                                   const NodeOut& no) {
   const unsigned blocks = (unsigned)(lanes / kBlock);
-  const BkSlab sl = bk_slab_plan(blocks, (const void*)k_bk_run_episodes<SeedSource>, P.n);
+  const EvSlab sl = ev_slab_plan(blocks, (const void*)k_bk_run_episodes<SeedSource>, P.n);
   hipLaunchKernelGGL(k_bk_run_episodes<SeedSource>, dim3(blocks), dim3(kBlock), sl.bytes, st, P,
                      SeedSource{seed, first}, n_eps, mem, lane_bytes, recs, sum, no, sl.kl,
                      sl.vw);
@@ -553,7 +550,7 @@ hipError_t launch_bk_replay_episodes(const bk::BkParams& P, const TraceSource& s
                                  cpr_episode_record* recs, cpr_summary* sum, hipStream_t st,
                                   const NodeOut& no) {
   const unsigned blocks = (unsigned)(lanes / kBlock);
-  const BkSlab sl = bk_slab_plan(blocks, (const void*)k_bk_run_episodes<TraceSource>, P.n);
+  const EvSlab sl = ev_slab_plan(blocks, (const void*)k_bk_run_episodes<TraceSource>, P.n);
   hipLaunchKernelGGL(k_bk_run_episodes<TraceSource>, dim3(blocks), dim3(kBlock), sl.bytes, st, P,
                      src, n_eps, mem, lane_bytes, recs, sum, no, sl.kl, sl.vw);
   return hipGetLastError();
@@ -580,7 +577,7 @@ hipError_t launch_bk_rollout(const bk::BkParams& P, uint64_t seed, uint8_t* mem,
                              int64_t lane_bytes, void* slots, int64_t n, int64_t n_steps,
                              int unit, const double* tabs, int32_t tn, double* obs,
                              double* reward, uint8_t* done, cpr_summary* sum, hipStream_t st) {
-  const BkSlab sl = bk_slab_plan(grid_of(n), (const void*)k_bk_rollout, P.n);
+  const EvSlab sl = ev_slab_plan(grid_of(n), (const void*)k_bk_rollout, P.n);
   hipLaunchKernelGGL(k_bk_rollout, dim3(grid_of(n)), dim3(kBlock), sl.bytes, st, P, seed, mem,
                      lane_bytes, (BkSlot*)slots, n, n_steps, unit, tabs, tn, obs, reward, done,
                      sum, sl.kl, sl.vw);

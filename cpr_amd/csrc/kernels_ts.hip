@@ -126,7 +126,8 @@ extern __shared__ __attribute__((aligned(16))) bk::HNode ts_slab[];
 template <class Src>
 __global__ __launch_bounds__(kBlock) CPR_EV_OCC void k_ts_run_episodes(
     ts::TsParams P, Src src, int64_t n_eps, uint8_t* mem,
-    int64_t lane_bytes, cpr_episode_record* recs, cpr_summary* sum, NodeOut no, int32_t kl) {
+    int64_t lane_bytes, cpr_episode_record* recs, cpr_summary* sum, NodeOut no, int32_t kl,
+    int32_t vw) {
   __shared__ int32_t hist[CPR_HIST_BINS];
   if (threadIdx.x < CPR_HIST_BINS) hist[threadIdx.x] = 0;
   __syncthreads();
@@ -134,8 +135,10 @@ __global__ __launch_bounds__(kBlock) CPR_EV_OCC void k_ts_run_episodes(
   const int64_t nthreads = (int64_t)gridDim.x * blockDim.x;
   ts::TsMem M = ts::ts_mem_at(mem + tid * lane_bytes, P);
   if (no.mem) M.nact = (int64_t*)(no.mem + tid * no.lane_bytes);
-  // every episode starts with an empty heap (init): the slab needs no load or store
+  // every episode starts with an empty heap and a fresh window (init): the slab needs no
+  // load or store
   ts::ts_heap_slab(M, ts_slab, (int32_t)threadIdx.x, (int32_t)blockDim.x, kl);
+  ts::ts_vis_window(M, (uint8_t*)(ts_slab + (size_t)kl * blockDim.x), (int32_t)threadIdx.x, vw);
   Acc acc = {};
   ts::TsLane L;
 #if CPR_EV_SCHED
@@ -274,7 +277,7 @@ __global__ __launch_bounds__(kBlock) CPR_EV_OCC void k_ts_rollout(ts::TsParams P
                                                         const double* tabs, int32_t tn,
                                                         double* obs, double* reward,
                                                         uint8_t* done_out, cpr_summary* sum,
-                                                        int32_t kl) {
+                                                        int32_t kl, int32_t vw) {
   __shared__ int32_t hist[CPR_HIST_BINS];
   if (threadIdx.x < CPR_HIST_BINS) hist[threadIdx.x] = 0;
   __syncthreads();
@@ -285,6 +288,7 @@ __global__ __launch_bounds__(kBlock) CPR_EV_OCC void k_ts_rollout(ts::TsParams P
   // wave-coherent dispatch, as k_bk_rollout
   ts::TsMem M = ts::ts_mem_at(mem + (i < n ? i : 0) * lane_bytes, P);
   ts::ts_heap_slab(M, ts_slab, (int32_t)threadIdx.x, (int32_t)blockDim.x, kl);
+  ts::ts_vis_window(M, (uint8_t*)(ts_slab + (size_t)kl * blockDim.x), (int32_t)threadIdx.x, vw);
   TsSlot SL;
   EvCursor c;
   c.cls = -1;
@@ -295,6 +299,7 @@ __global__ __launch_bounds__(kBlock) CPR_EV_OCC void k_ts_rollout(ts::TsParams P
   if (i < n) {
     SL = slots[i];
     ts::ts_heap_load(M, SL.L.hused);
+    ts::ts_vis_load(M, P, SL.L.newest);
     if (!SL.live)
       ts_slot_reset(P, seed, M, SL, (uint64_t)i);
     else
@@ -368,7 +373,10 @@ __global__ __launch_bounds__(kBlock) CPR_EV_OCC void k_ts_rollout(ts::TsParams P
     TsSlot SL = slots[i];
     // the lane's heap nodes 0 .. kl-1 move to the slab for this launch
     ts::ts_heap_slab(M, ts_slab, (int32_t)threadIdx.x, (int32_t)blockDim.x, kl);
+    ts::ts_vis_window(M, (uint8_t*)(ts_slab + (size_t)kl * blockDim.x), (int32_t)threadIdx.x,
+                      vw);
     ts::ts_heap_load(M, SL.L.hused);
+    ts::ts_vis_load(M, P, SL.L.newest);
     if (!SL.live) {
       ts_slot_reset(P, seed, M, SL, (uint64_t)i);
       acts_all += SL.L.c_act;
@@ -452,10 +460,10 @@ hipError_t launch_ts_run_episodes(const ts::TsParams& P, uint64_t seed, uint64_t
                                   cpr_episode_record* recs, cpr_summary* sum, hipStream_t st,
                                   const NodeOut& no) {
   const unsigned blocks = (unsigned)(lanes / kBlock);
-  const int32_t kl = ev_slab_nodes(blocks, (const void*)k_ts_run_episodes<SeedSource>);
-  hipLaunchKernelGGL(k_ts_run_episodes<SeedSource>, dim3(blocks), dim3(kBlock),
-                     (size_t)kl * kBlock * 24, st, P, SeedSource{seed, first}, n_eps, mem,
-                     lane_bytes, recs, sum, no, kl);
+  const EvSlab sl = ev_slab_plan(blocks, (const void*)k_ts_run_episodes<SeedSource>, P.n);
+  hipLaunchKernelGGL(k_ts_run_episodes<SeedSource>, dim3(blocks), dim3(kBlock), sl.bytes, st, P,
+                     SeedSource{seed, first}, n_eps, mem, lane_bytes, recs, sum, no, sl.kl,
+                     sl.vw);
   return hipGetLastError();
 }
 
@@ -464,10 +472,9 @@ hipError_t launch_ts_replay_episodes(const ts::TsParams& P, const TraceSource& s
                                  cpr_episode_record* recs, cpr_summary* sum, hipStream_t st,
                                   const NodeOut& no) {
   const unsigned blocks = (unsigned)(lanes / kBlock);
-  const int32_t kl = ev_slab_nodes(blocks, (const void*)k_ts_run_episodes<TraceSource>);
-  hipLaunchKernelGGL(k_ts_run_episodes<TraceSource>, dim3(blocks), dim3(kBlock),
-                     (size_t)kl * kBlock * 24, st, P, src, n_eps, mem, lane_bytes, recs, sum, no,
-                     kl);
+  const EvSlab sl = ev_slab_plan(blocks, (const void*)k_ts_run_episodes<TraceSource>, P.n);
+  hipLaunchKernelGGL(k_ts_run_episodes<TraceSource>, dim3(blocks), dim3(kBlock), sl.bytes, st, P,
+                     src, n_eps, mem, lane_bytes, recs, sum, no, sl.kl, sl.vw);
   return hipGetLastError();
 }
 
@@ -492,10 +499,10 @@ hipError_t launch_ts_rollout(const ts::TsParams& P, uint64_t seed, uint8_t* mem,
                              int64_t lane_bytes, void* slots, int64_t n, int64_t n_steps,
                              int unit, const double* tabs, int32_t tn, double* obs,
                              double* reward, uint8_t* done, cpr_summary* sum, hipStream_t st) {
-  const int32_t kl = ev_slab_nodes(ts_grid(n), (const void*)k_ts_rollout);
-  hipLaunchKernelGGL(k_ts_rollout, dim3(ts_grid(n)), dim3(kBlock), (size_t)kl * kBlock * 24, st,
-                     P, seed, mem, lane_bytes, (TsSlot*)slots, n, n_steps, unit, tabs, tn, obs,
-                     reward, done, sum, kl);
+  const EvSlab sl = ev_slab_plan(ts_grid(n), (const void*)k_ts_rollout, P.n);
+  hipLaunchKernelGGL(k_ts_rollout, dim3(ts_grid(n)), dim3(kBlock), sl.bytes, st, P, seed, mem,
+                     lane_bytes, (TsSlot*)slots, n, n_steps, unit, tabs, tn, obs, reward, done,
+                     sum, sl.kl, sl.vw);
   return hipGetLastError();
 }
 

@@ -121,6 +121,9 @@ struct TsMem {
   // rest in HBM (heap); see bk_lane.h BkMem
   CPR_LDS HNode* hl = nullptr;
   int32_t kl = 0, hs = 1;
+  // visibility rows of the newest vw vertices in the same slab (see bk_lane.h BkMem.vl)
+  CPR_LDS uint8_t* vl = nullptr;
+  int32_t vw = 0;
   TVtx* vtx;
   TRec* trec;
   uint8_t* vis;
@@ -196,6 +199,16 @@ __host__ __device__ inline void ts_heap_slab(TsMem& M, HNode* slab, int32_t lane
   M.hl = (CPR_LDS HNode*)(slab + lane);
   M.hs = stride;
   M.kl = kl;
+}
+__host__ __device__ inline void ts_vis_window(TsMem& M, uint8_t* base, int32_t lane, int32_t vw) {
+  M.vl = (CPR_LDS uint8_t*)(base + lane);
+  M.vw = vw;
+}
+__host__ __device__ inline void ts_vis_load(const TsMem& M, const TsParams& P, int32_t newest) {
+  for (int32_t s = newest - M.vw + 1 < 0 ? 0 : newest - M.vw + 1; s <= newest; ++s)
+    for (int32_t j = 0; j < P.n; ++j)
+      M.vl[(int64_t)((s & (M.vw - 1)) * P.n + j) * M.hs] =
+          M.vis[(int64_t)(s & (P.cap_v - 1)) * P.n + j];
 }
 __host__ __device__ inline void ts_heap_load(const TsMem& M, int32_t hused) {
   const int32_t n = hused < M.kl ? hused : M.kl;
@@ -329,14 +342,27 @@ struct TsLane {
   __host__ __device__ inline uint8_t& V(const TsParams& P, const TsMem& M, int32_t s,
                                         int32_t node) {
     return M.vis[(int64_t)(s & (P.cap_v - 1)) * P.n + node];
+  }  // visibility through the LDS window of the newest vw vertices (see bk_lane.h Vg / Vs)
+  __host__ __device__ inline uint8_t Vg(const TsParams& P, const TsMem& M, int32_t s,
+                                        int32_t node) const {
+    if (s > newest - M.vw)
+      return *(const volatile CPR_LDS uint8_t*)&M.vl[(int64_t)((s & (M.vw - 1)) * P.n + node) *
+                                                      M.hs];
+    return M.vis[(int64_t)(s & (P.cap_v - 1)) * P.n + node];
   }
+  __host__ __device__ inline void Vs(const TsParams& P, const TsMem& M, int32_t s, int32_t node,
+                                     uint8_t v) const {
+    M.vis[(int64_t)(s & (P.cap_v - 1)) * P.n + node] = v;
+    if (s > newest - M.vw) M.vl[(int64_t)((s & (M.vw - 1)) * P.n + node) * M.hs] = v;
+  }
+
   __host__ __device__ inline double& VT(const TsParams& P, const TsMem& M, int32_t s,
                                         int32_t node) {
     return M.vt[(int64_t)(s & (P.cap_v - 1)) * P.n + node];
   }
   __host__ __device__ inline bool visible(const TsParams& P, const TsMem& M, int32_t s,
                                           int32_t node) {
-    return (V(P, M, s, node) & V_KIND) != V_INV;
+    return (Vg(P, M, s, node) & V_KIND) != V_INV;
   }
   __host__ __device__ inline uint8_t& MK(const TsParams& P, const TsMem& M, int32_t s) {
     return M.marks[s & (P.cap_v - 1)];
@@ -569,7 +595,7 @@ struct TsLane {
     for (int32_t c = X(P, M, b).thead; c >= 0 && !dead;) {
       const TRec& x = TR(P, M, c);
       const int32_t nx = x.next;
-      const uint8_t v = V(P, M, c, node);
+      const uint8_t v = Vg(P, M, c, node);
       if ((v & V_KIND) != V_INV && (vf == VF_ALL || keep_kind(v, vf, false))) {
         if (n >= cap) {
           fail(3);
@@ -634,7 +660,7 @@ struct TsLane {
     int32_t n = 0, d = 0;
     for (int32_t c = X(P, M, b).thead; c >= 0 && !dead;) {
       const TRec& x = TR(P, M, c);
-      const uint8_t v = V(P, M, c, node);
+      const uint8_t v = Vg(P, M, c, node);
       if ((v & V_KIND) != V_INV &&
           keep_kind(v, vf, vf == VF_PUBLIC_OR_MARKED && MK(P, M, c))) {
         ++n;
@@ -647,7 +673,7 @@ struct TsLane {
   }
   __host__ __device__ inline bool mine(const TsParams& P, const TsMem& M, int32_t s,
                                        int32_t node) {
-    const uint8_t kd = V(P, M, s, node) & V_KIND;
+    const uint8_t kd = Vg(P, M, s, node) & V_KIND;
     return kd == V_WH || kd == V_REL;
   }
   // stable bottom-up merge sort of a[0, n) with `before` (strict); tmp holds n entries
@@ -992,7 +1018,7 @@ struct TsLane {
     b.time = now;
     b.next = -1;
     b.thead = -1;
-    for (int32_t j = 0; j < P.n; ++j) V(P, M, s, j) = V_INV;
+    for (int32_t j = 0; j < P.n; ++j) Vs(P, M, s, j, V_INV);
   }
   template <class St>
   __host__ __device__ inline int32_t append_vote(const TsParams& P, const St& S,
@@ -1122,9 +1148,9 @@ struct TsLane {
     st[sp++] = s0;
     while (sp > 0 && !dead) {
       const int32_t s = st[--sp];
-      uint8_t& v = V(P, M, s, node);
+      const uint8_t v = Vg(P, M, s, node);
       if ((v & V_KIND) != V_WH) continue;
-      v = (uint8_t)((v & ~V_KIND) | V_REL);
+      Vs(P, M, s, node, (uint8_t)((v & ~V_KIND) | V_REL));
       push_now(P, M, mkev(EV_TX, node, KD_NET), s);
       const TVtx& b = X(P, M, s);
       if (b.parent < 0) continue;
@@ -1316,7 +1342,7 @@ struct TsLane {
       int32_t na = 0, da = 0, nm = 0, dm = 0;
       for (int32_t c = X(P, M, o_priv).thead; c >= 0 && !dead;) {
         const TRec& x = TR(P, M, c);
-        const uint8_t kd = V(P, M, c, 0) & V_KIND;
+        const uint8_t kd = Vg(P, M, c, 0) & V_KIND;
         if (kd != V_INV) {
           ++na;
           da = x.dep() > da ? x.dep() : da;
@@ -1350,7 +1376,7 @@ struct TsLane {
       for (int32_t s = c0; s <= newest; ++s) MK(P, M, s) = 0;
       int32_t nw = 0;
       for (int32_t s = c0; s <= newest && !dead; ++s) {
-        const uint8_t v = V(P, M, s, 0);
+        const uint8_t v = Vg(P, M, s, 0);
         if ((v & V_KIND) == V_INV) continue;
         const TVtx& x = X(P, M, s);
         bool d = s == c0;
@@ -1482,7 +1508,7 @@ struct TsLane {
     set_trec(P, M, r);
     SH(P, M, 0) = -1;
     for (int32_t j = 0; j < P.n; ++j) {
-      V(P, M, 0, j) = V_RECV | V_GOT;
+      Vs(P, M, 0, j, V_RECV | V_GOT);
       VT(P, M, 0, j) = 0.0;
       M.tips[j] = 0;
       if (M.nact) M.nact[j] = 0;
@@ -1495,7 +1521,7 @@ struct TsLane {
   // Honest.handler (tailstorm.ml:565-608) at defender `node` for vertex x
   __host__ __device__ inline void honest(const TsParams& P, const TsMem& M, int32_t node,
                                          int32_t x) {
-    if ((V(P, M, x, node) & V_KIND) == V_WH) share(P, M, node, x);
+    if ((Vg(P, M, x, node) & V_KIND) == V_WH) share(P, M, node, x);
     const TVtx& b = X(P, M, x);
     int32_t& tip = M.tips[node];
     if (!b.vote) {
@@ -1516,7 +1542,7 @@ struct TsLane {
     const int32_t node = (int32_t)(ev >> 5);
     switch (ty) {
       case EV_MV: {
-        uint8_t& v = V(P, M, s, node);
+        const uint8_t v = Vg(P, M, s, node);
         if ((v & V_KIND) != V_INV) break;
         const TVtx& b = X(P, M, s);
         bool ok = true;
@@ -1529,7 +1555,7 @@ struct TsLane {
           }
         }
         if (!ok) break;
-        v = (uint8_t)((v & ~V_KIND) | (kind == KD_NET ? V_RECV : V_WH));
+        Vs(P, M, s, node, (uint8_t)((v & ~V_KIND) | (kind == KD_NET ? V_RECV : V_WH)));
         VT(P, M, s, node) = now;
         push_now(P, M, mkev(EV_ON, node, kind), s);
         push_now(P, M, mkev(EV_MDV, node, kind), s);
@@ -1587,9 +1613,9 @@ struct TsLane {
       }
       case EV_RX: {
         if (!(now < __builtin_inf())) break;  // see bk_lane.h
-        uint8_t& v = V(P, M, s, node);
+        const uint8_t v = Vg(P, M, s, node);
         if (!(v & V_GOT)) {
-          v |= V_GOT;
+          Vs(P, M, s, node, (uint8_t)(v | V_GOT));
           push_now(P, M, mkev(EV_MV, node, KD_NET), s);
         }
         break;
@@ -1603,9 +1629,9 @@ struct TsLane {
         int32_t cv = sv ? X(P, M, sb.sum).thead : sb.thead;
         int32_t cq = sv ? SH(P, M, sb.sum) : -1;
         while (!dead) {
-          while (cv > s && !(TR(P, M, cv).parent == s && (V(P, M, cv, node) & V_GOT)))
+          while (cv > s && !(TR(P, M, cv).parent == s && (Vg(P, M, cv, node) & V_GOT)))
             cv = TR(P, M, cv).next;
-          while (cq > s && !(V(P, M, cq, node) & V_GOT)) cq = TR(P, M, cq).next;
+          while (cq > s && !(Vg(P, M, cq, node) & V_GOT)) cq = TR(P, M, cq).next;
           if (cq > s) {  // summary holding s?
             const TVtx& cb = X(P, M, cq);
             bool child = false;

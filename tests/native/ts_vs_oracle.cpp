@@ -116,12 +116,15 @@ static ts::TsParams params_of(const Cfg& cf) {
   return P;
 }
 
-// SLABTEST=1: the lane's event-heap slab (nodes 0..5) in a host buffer, stride 1, so the
-// host fuzz runs the device kernels' LDS path too
-static ts::TsMem with_slab(ts::TsMem M) {
+// SLABTEST=1: the lane's event-heap slab (nodes 0..5) and visibility window in host
+// buffers, stride 1, so the host fuzz runs the device kernels' LDS paths too
+static ts::TsMem with_slab(ts::TsMem M, const ts::TsParams& P) {
   static std::vector<bk::HNode> slab(6);
+  static std::vector<uint8_t> win;
   if (!getenv("SLABTEST")) return M;
+  win.assign((size_t)8 * P.n, 0);
   ts::ts_heap_slab(M, slab.data(), 0, 1, 6);
+  ts::ts_vis_window(M, win.data(), 0, 8);  // and the visibility rows of the newest 8 vertices
   return M;
 }
 
@@ -136,7 +139,7 @@ static bool run_gym(const Cfg& cf, uint64_t seed, uint64_t ep, Counters& C, std:
   double obs[10];
   const ts::TsParams P = params_of(cf);
   std::vector<uint8_t> mem(ts::ts_lane_bytes(P));
-  const ts::TsMem M = with_slab(ts::ts_mem_at(mem.data(), P));
+  const ts::TsMem M = with_slab(ts::ts_mem_at(mem.data(), P), P);
   const Stream S{(uint32_t)seed, (uint32_t)(seed >> 32), (uint32_t)ep, (uint32_t)(ep >> 32)};
   ts::TsLane L;
   bool oracle_raised = false;
@@ -325,7 +328,7 @@ static bool run_loop(const Cfg& cf, uint64_t seed, uint64_t ep, Counters& C, std
   }
   const ts::TsParams P = params_of(cf);
   std::vector<uint8_t> mem(ts::ts_lane_bytes(P));
-  const ts::TsMem M = with_slab(ts::ts_mem_at(mem.data(), P));
+  const ts::TsMem M = with_slab(ts::ts_mem_at(mem.data(), P), P);
   const Stream S{(uint32_t)seed, (uint32_t)(seed >> 32), (uint32_t)ep, (uint32_t)(ep >> 32)};
   ts::TsLane L;
   const int32_t hd = L.loop(P, S, M);
@@ -393,7 +396,7 @@ int main(int argc, char** argv) {
     Cfg cf{0.33, 0.0, 1, pol, 1, 10000, 1, k};
     const ts::TsParams P = params_of(cf);
     std::vector<uint8_t> mem(ts::ts_lane_bytes(P));
-    const ts::TsMem M = with_slab(ts::ts_mem_at(mem.data(), P));
+    const ts::TsMem M = with_slab(ts::ts_mem_at(mem.data(), P), P);
     long acts = 0;
     for (int e = 0; e < neps; e++) {
       const Stream S{(uint32_t)seed, (uint32_t)(seed >> 32), (uint32_t)e, 0u};
