@@ -312,9 +312,40 @@ __global__ __launch_bounds__(kBlock) CPR_EV_OCC void k_bk_rollout(bk::BkParams P
       c.phase = PH_RUN;
     }
   }
+#ifdef CPR_EV_CLOCKS
+  // diagnostic build: shader-clock cycles of the wave per item class (the exec that follows
+  // the choice), of fetching and of choosing; printed by lane 0 of a few workgroups
+  uint64_t clk[WK_N + 2] = {};
+  uint32_t cnt[WK_N] = {};
+  uint64_t tprev = clock64();
+  int32_t last = -1;
+#endif
   for (;;) {
+#ifdef CPR_EV_CLOCKS
+    {
+      const uint64_t tn = clock64();
+      if (last >= 0) clk[last] += tn - tprev;
+      tprev = tn;
+    }
+#endif
     if (c.phase != PH_IDLE && c.cls < 0) roll_fetch<BkAdapter>(SL.L, M, c);
+#ifdef CPR_EV_CLOCKS
+    {
+      const uint64_t tn = clock64();
+      clk[WK_N] += tn - tprev;
+      tprev = tn;
+    }
+#endif
     const int32_t kc = ev_choose(c.cls);
+#ifdef CPR_EV_CLOCKS
+    {
+      const uint64_t tn = clock64();
+      clk[WK_N + 1] += tn - tprev;
+      tprev = tn;
+      last = kc;
+      if (kc >= 0) cnt[kc] += 1;
+    }
+#endif
     if (kc < 0) break;
     if (c.cls != kc) continue;
     c.cls = -1;
@@ -369,6 +400,21 @@ __global__ __launch_bounds__(kBlock) CPR_EV_OCC void k_bk_rollout(bk::BkParams P
     bk::bk_heap_store(M, SL.L.hused);
     slots[i] = SL;
   }
+#ifdef CPR_EV_CLOCKS
+  if (threadIdx.x == 0 && (blockIdx.x == 0 || blockIdx.x == 77 || blockIdx.x == 200)) {
+    uint64_t tot = 0;
+    for (int32_t q = 0; q < WK_N + 2; ++q) tot += clk[q];
+    printf("EVCLK block %d total %llu fetch %llu choose %llu | clock %llu/%u dag %llu/%u "
+           "tx %llu/%u rx %llu/%u on %llu/%u mv %llu/%u mdv %llu/%u attack %llu/%u "
+           "pow0 %llu/%u\n",
+           (int)blockIdx.x, (unsigned long long)tot, (unsigned long long)clk[WK_N],
+           (unsigned long long)clk[WK_N + 1], (unsigned long long)clk[0], cnt[0],
+           (unsigned long long)clk[1], cnt[1], (unsigned long long)clk[2], cnt[2],
+           (unsigned long long)clk[3], cnt[3], (unsigned long long)clk[4], cnt[4],
+           (unsigned long long)clk[5], cnt[5], (unsigned long long)clk[6], cnt[6],
+           (unsigned long long)clk[7], cnt[7], (unsigned long long)clk[8], cnt[8]);
+  }
+#endif
 #else
   if (i < n) {
     bk::BkMem M = bk::bk_mem_at(mem + i * lane_bytes, P);
