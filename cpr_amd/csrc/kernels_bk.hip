@@ -316,6 +316,7 @@ __global__ __launch_bounds__(kBlock) CPR_EV_OCC void k_bk_rollout(bk::BkParams P
   // diagnostic build: shader-clock cycles of the wave per item class (the exec that follows
   // the choice), of fetching and of choosing; printed by lane 0 of a few workgroups
   uint64_t clk[WK_N + 2] = {};
+  uint64_t sub[5] = {};  // the attack item: prepare, head/done, obs write, observe, apply
   uint32_t cnt[WK_N] = {};
   uint64_t tprev = clock64();
   int32_t last = -1;
@@ -358,6 +359,10 @@ __global__ __launch_bounds__(kBlock) CPR_EV_OCC void k_bk_rollout(bk::BkParams P
       continue;
     }
     if (c.ev != kRollFail) SL.L.prepare(P, M, (c.ev >> 3) & 3u, c.s);
+#ifdef CPR_EV_CLOCKS
+    uint64_t ta = clock64();
+    sub[0] += ta - tprev;  // prepare
+#endif
     if (c.phase == PH_FRESH) {
       // the reset after a done step reached its first interaction: that step's observation
       c.phase = PH_RUN;
@@ -365,6 +370,13 @@ __global__ __launch_bounds__(kBlock) CPR_EV_OCC void k_bk_rollout(bk::BkParams P
     } else {
       const int32_t hd = BkAdapter::head_gym(SL.L, P, M, c.att);
       const bool done = BkAdapter::gym_done(SL.L, P, M, hd);
+#ifdef CPR_EV_CLOCKS
+      {
+        const uint64_t tb = clock64();
+        sub[1] += tb - ta;  // head, done
+        ta = tb;
+      }
+#endif
       const bk::BVtx& h = SL.L.X(P, M, hd);
       const double ra = (double)h.rew_att;
       const int64_t k = ts * n + i;
@@ -387,11 +399,30 @@ __global__ __launch_bounds__(kBlock) CPR_EV_OCC void k_bk_rollout(bk::BkParams P
       }
       if (obs) bk_write_obs(SL.L.observe(P, M), unit, tabs, tn, P.k, obs + 8 * k);
     }
+#ifdef CPR_EV_CLOCKS
+    {
+      const uint64_t tb = clock64();
+      sub[2] += tb - ta;  // observation written
+      ta = tb;
+    }
+#endif
     if (ts >= n_steps) {
       c.phase = PH_IDLE;  // at the decision point of the next launch's first step
       continue;
     }
+#ifdef CPR_EV_CLOCKS
+    {
+      const bk::BkObs o = SL.L.observe(P, M);
+      const uint64_t tb = clock64();
+      sub[3] += tb - ta;  // observe (the policy's)
+      ta = tb;
+      SL.L.apply(P, M, bk::bk_policy(P, o));
+      ++SL.L.steps;
+      sub[4] += clock64() - ta;  // policy + apply
+    }
+#else
     BkAdapter::act(SL.L, P, M);
+#endif
     c.att = SL.L.priv;
   }
   if (i < n) {
@@ -413,6 +444,9 @@ __global__ __launch_bounds__(kBlock) CPR_EV_OCC void k_bk_rollout(bk::BkParams P
            (unsigned long long)clk[3], cnt[3], (unsigned long long)clk[4], cnt[4],
            (unsigned long long)clk[5], cnt[5], (unsigned long long)clk[6], cnt[6],
            (unsigned long long)clk[7], cnt[7], (unsigned long long)clk[8], cnt[8]);
+    printf("EVCLK block %d attack: prepare %llu head %llu obs %llu observe %llu apply %llu\n",
+           (int)blockIdx.x, (unsigned long long)sub[0], (unsigned long long)sub[1],
+           (unsigned long long)sub[2], (unsigned long long)sub[3], (unsigned long long)sub[4]);
   }
 #endif
 #else
