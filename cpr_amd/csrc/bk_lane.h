@@ -128,7 +128,9 @@ struct BkMem {
   // and visibility bytes, and a vote's 48-byte vertex only when it passes the filter:
   // vh[block] = its newest vote (-1 none), vn[vote] = the next older vote of its block
   int32_t* vh;
-  int4* vn;  // x = next older vote of the block, y = pow, z = who (the propose scan's fields)
+  // vote: x = next older vote of its block, y = pow, z = who (the propose scan's fields);
+  // block: x = next older child block of its parent, w = its newest child block (-1 none)
+  int4* vn;
   uint8_t* vis;
   double* vt;
   int32_t* quo;
@@ -601,7 +603,8 @@ struct BkLane {
     b.qslot = -1;
     b.time = now;
     VH(P, M, s) = -1;
-    VN(P, M, s) = -1;
+    VR(P, M, s).x = -1;
+    VR(P, M, s).w = -1;
     for (int32_t j = 0; j < P.n; ++j) Vs(P, M, s, j, V_INV);
   }
   // vote: simulator.ml:122-136 (pow = (bits, serial)), bk.ml:281-286 payload
@@ -677,6 +680,11 @@ struct BkLane {
     BVtx& b = M.vtx[s & (P.cap_v - 1)];
     init_vertex(P, M, b, s);
     b.parent = dr[1];
+    {  // newest-first child-block list of the parent
+      int4& pr = VR(P, M, dr[1]);
+      VR(P, M, s).x = pr.w;
+      pr.w = s;
+    }
     b.height = ph + 1;
     b.vote = 0;
     b.who = node;
@@ -931,14 +939,13 @@ struct BkLane {
       int32_t block = o_priv;
       while (!dead && X(P, M, block).height > height) block = X(P, M, block).parent;
       if (nvotes >= P.k) {
-        for (int32_t c = newest; c > block && !dead; --c) {
+        // newest visible child block (the attacker's proposal, if any): the block's
+        // newest-first child-block list instead of every vertex appended since
+        for (int32_t c = VR(P, M, block).w; c >= 0 && !dead; c = VR(P, M, c).x) {
           if (!visible(P, M, c, 0)) continue;
-          const BVtx& x = X(P, M, c);
-          if (!x.vote && x.parent == block) {
-            block = c;  // newest visible child block (the attacker's proposal, if any)
-            nvotes = 0;
-            break;
-          }
+          block = c;
+          nvotes = 0;
+          break;
         }
       }
       // votes confirming `block` in children order; Compare.first by visible_since
@@ -1007,7 +1014,8 @@ struct BkLane {
     r.qslot = -1;
     r.time = 0.0;
     VH(P, M, 0) = -1;
-    VN(P, M, 0) = -1;
+    VR(P, M, 0).x = -1;
+    VR(P, M, 0).w = -1;
     for (int32_t j = 0; j < P.n; ++j) {
       Vs(P, M, 0, j, V_RECV | V_GOT);
       VT(P, M, 0, j) = 0.0;
