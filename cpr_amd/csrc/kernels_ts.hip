@@ -150,7 +150,22 @@ __global__ __launch_bounds__(kBlock) CPR_EV_OCC void k_ts_run_episodes(
   c.cls = -1;
   c.phase = PH_IDLE;
   if (e < n_eps) ev_begin<TsAdapter>(L, P, S, M, c);
+#ifdef CPR_EV_CLOCKS
+  // diagnostic build: shader-clock cycles of the wave per item class (the exec after the
+  // choice), of fetching / finishing episodes and of choosing; lane 0 of a few workgroups
+  uint64_t clk[WK_N + 2] = {};
+  uint32_t cnt[WK_N] = {};
+  uint64_t tprev = clock64();
+  int32_t last = -1;
+#endif
   for (;;) {
+#ifdef CPR_EV_CLOCKS
+    {
+      const uint64_t tn = clock64();
+      if (last >= 0) clk[last] += tn - tprev;
+      tprev = tn;
+    }
+#endif
     while (c.phase != PH_IDLE && c.cls < 0) {
       if (c.phase != PH_OVER) ev_fetch<TsAdapter>(L, P, S, M, c);
       if (c.phase == PH_OVER) {
@@ -164,10 +179,41 @@ __global__ __launch_bounds__(kBlock) CPR_EV_OCC void k_ts_run_episodes(
         }
       }
     }
+#ifdef CPR_EV_CLOCKS
+    {
+      const uint64_t tn = clock64();
+      clk[WK_N] += tn - tprev;
+      tprev = tn;
+    }
+#endif
     const int32_t k = ev_choose(c.cls);
+#ifdef CPR_EV_CLOCKS
+    {
+      const uint64_t tn = clock64();
+      clk[WK_N + 1] += tn - tprev;
+      tprev = tn;
+      last = k;
+      if (k >= 0) cnt[k] += 1;
+    }
+#endif
     if (k < 0) break;
     if (c.cls == k) ev_exec<TsAdapter>(L, P, S, M, c);
   }
+#ifdef CPR_EV_CLOCKS
+  if (threadIdx.x == 0 && (blockIdx.x == 0 || blockIdx.x == 77 || blockIdx.x == 200)) {
+    uint64_t tot = 0;
+    for (int32_t q = 0; q < WK_N + 2; ++q) tot += clk[q];
+    printf("TSCLK block %d total %llu fetch %llu choose %llu | clock %llu/%u dag %llu/%u "
+           "tx %llu/%u rx %llu/%u on %llu/%u mv %llu/%u mdv %llu/%u attack %llu/%u "
+           "pow0 %llu/%u\n",
+           (int)blockIdx.x, (unsigned long long)tot, (unsigned long long)clk[WK_N],
+           (unsigned long long)clk[WK_N + 1], (unsigned long long)clk[0], cnt[0],
+           (unsigned long long)clk[1], cnt[1], (unsigned long long)clk[2], cnt[2],
+           (unsigned long long)clk[3], cnt[3], (unsigned long long)clk[4], cnt[4],
+           (unsigned long long)clk[5], cnt[5], (unsigned long long)clk[6], cnt[6],
+           (unsigned long long)clk[7], cnt[7], (unsigned long long)clk[8], cnt[8]);
+  }
+#endif
 #else
   for (int64_t e = tid; e < n_eps; e += nthreads) {
     const auto S = src.at(e);
