@@ -1378,12 +1378,16 @@ struct TsLane {
       for (int32_t s = c0; s <= newest && !dead; ++s) {
         const uint8_t v = Vg(P, M, s, 0);
         if ((v & V_KIND) == V_INV) continue;
-        const TVtx& x = X(P, M, s);
+        // the 16-byte list record (a vote has depth >= 1, a summary 0) instead of the
+        // 64-byte vertex: this scan covers every vertex since the common ancestor, and only
+        // a summary's quorum needs the vertex
+        const TRec& r = TR(P, M, s);
         bool d = s == c0;
-        if (!d && x.parent >= 0) {
-          if (x.vote) {
-            d = x.parent >= c0 && MK(P, M, x.parent);
+        if (!d && r.parent >= 0) {
+          if (r.dep() > 0) {
+            d = r.parent >= c0 && MK(P, M, r.parent);
           } else {
+            const TVtx& x = X(P, M, s);
             const int32_t* lq = Q(P, M, x);
             for (int32_t i = 0; i < x.nq && !d; ++i) d = lq[i] >= c0 && MK(P, M, lq[i]);
           }
