@@ -1375,13 +1375,27 @@ struct TsLane {
       const int32_t c0 = o_common;
       for (int32_t s = c0; s <= newest; ++s) MK(P, M, s) = 0;
       int32_t nw = 0;
+      // this scan covers every vertex since the common ancestor: the visibility bytes and
+      // 16-byte list records (a vote has depth >= 1, a summary 0) of 8 vertices are loaded
+      // together, so their latencies overlap, then the vertices are processed in order
+      // (a vertex's parent precedes it, so its mark is final when it is read); only a
+      // summary's quorum reads the vertex itself
+      constexpr int32_t B8 = 8;
+      uint8_t vb[B8];
+      TRec rb[B8];
       for (int32_t s = c0; s <= newest && !dead; ++s) {
-        const uint8_t v = Vg(P, M, s, 0);
+        const int32_t j8 = (s - c0) & (B8 - 1);
+        if (j8 == 0) {
+#pragma unroll
+          for (int32_t q = 0; q < B8; ++q) {
+            const int32_t sq = s + q <= newest ? s + q : s;
+            vb[q] = Vg(P, M, sq, 0);
+            rb[q] = TR(P, M, sq);
+          }
+        }
+        const uint8_t v = vb[j8];
         if ((v & V_KIND) == V_INV) continue;
-        // the 16-byte list record (a vote has depth >= 1, a summary 0) instead of the
-        // 64-byte vertex: this scan covers every vertex since the common ancestor, and only
-        // a summary's quorum needs the vertex
-        const TRec& r = TR(P, M, s);
+        const TRec& r = rb[j8];
         bool d = s == c0;
         if (!d && r.parent >= 0) {
           if (r.dep() > 0) {
