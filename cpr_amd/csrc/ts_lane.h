@@ -1376,45 +1376,55 @@ struct TsLane {
       for (int32_t s = c0; s <= newest; ++s) MK(P, M, s) = 0;
       int32_t nw = 0;
       // this scan covers every vertex since the common ancestor: the visibility bytes and
-      // 16-byte list records (a vote has depth >= 1, a summary 0) of 8 vertices are loaded
+      // list records (a vote has depth >= 1, a summary 0) of several vertices are loaded
       // together, so their latencies overlap, then the vertices are processed in order
       // (a vertex's parent precedes it, so its mark is final when it is read); only a
       // summary's quorum reads the vertex itself
-      constexpr int32_t B8 = 8;
-      uint8_t vb[B8];
-      TRec rb[B8];
-      for (int32_t s = c0; s <= newest && !dead; ++s) {
-        const int32_t j8 = (s - c0) & (B8 - 1);
-        if (j8 == 0) {
+      // four vertices' visibility and list-record fields are loaded together (static
+      // indices: they stay in registers), then processed in order
+      for (int32_t base = c0; base <= newest && !dead; base += 4) {
+        uint8_t vb[4];
+        int32_t pb[4], db[4];
 #pragma unroll
-          for (int32_t q = 0; q < B8; ++q) {
-            const int32_t sq = s + q <= newest ? s + q : s;
-            vb[q] = Vg(P, M, sq, 0);
-            rb[q] = TR(P, M, sq);
+        for (int32_t q = 0; q < 4; ++q) {
+          const int32_t sq = base + q <= newest ? base + q : base;
+          vb[q] = Vg(P, M, sq, 0);
+          const TRec& r = TR(P, M, sq);
+          pb[q] = r.parent;
+          db[q] = r.dep();
+        }
+        bool stop = false;
+#pragma unroll
+        for (int32_t q = 0; q < 4; ++q) {
+          const int32_t s = base + q;
+          if (stop || s > newest || dead) {
+            stop = true;
+            continue;
+          }
+          const uint8_t v = vb[q];
+          if ((v & V_KIND) == V_INV) continue;
+          bool d = s == c0;
+          if (!d && pb[q] >= 0) {
+            if (db[q] > 0) {
+              d = pb[q] >= c0 && MK(P, M, pb[q]);
+            } else {
+              const TVtx& x = X(P, M, s);
+              const int32_t* lq = Q(P, M, x);
+              for (int32_t i = 0; i < x.nq && !d; ++i) d = lq[i] >= c0 && MK(P, M, lq[i]);
+            }
+          }
+          if (!d) continue;
+          MK(P, M, s) = 1;
+          if ((v & V_KIND) == V_WH) {
+            if (nw >= P.cap_v) {
+              fail(9);
+              stop = true;
+              continue;
+            }
+            M.pend[nw++] = s;
           }
         }
-        const uint8_t v = vb[j8];
-        if ((v & V_KIND) == V_INV) continue;
-        const TRec& r = rb[j8];
-        bool d = s == c0;
-        if (!d && r.parent >= 0) {
-          if (r.dep() > 0) {
-            d = r.parent >= c0 && MK(P, M, r.parent);
-          } else {
-            const TVtx& x = X(P, M, s);
-            const int32_t* lq = Q(P, M, x);
-            for (int32_t i = 0; i < x.nq && !d; ++i) d = lq[i] >= c0 && MK(P, M, lq[i]);
-          }
-        }
-        if (!d) continue;
-        MK(P, M, s) = 1;
-        if ((v & V_KIND) == V_WH) {
-          if (nw >= P.cap_v) {
-            fail(9);
-            break;
-          }
-          M.pend[nw++] = s;
-        }
+        if (stop) break;
       }
       // sort by (Dag depth, serial): insertion sort on the (mostly sorted) list
       for (int32_t i = 1; i < nw; ++i) {
