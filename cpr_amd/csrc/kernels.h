@@ -146,7 +146,9 @@ struct EvSlab {
   int32_t kl, vw;
   size_t bytes;
 };
-EvSlab ev_slab_plan(int64_t blocks, const void* kernel, int32_t n);
+// lanes: used lanes per workgroup (0: all of kBlock)
+EvSlab ev_slab_plan(int64_t blocks, const void* kernel, int32_t n, int32_t lanes = 0);
+int32_t rollout_lanes_per_wave(int64_t n);
 // Ethereum gym episodes on the selfish-mining network through the window lane
 // (eth_window.h; ethw::win_supported): mem = lanes x ethw::win_lane_bytes; flagged episodes
 // go to the exact re-run queue (redo / redo_n, entries tagged with launch_id)

@@ -277,19 +277,24 @@ __global__ __launch_bounds__(kBlock) CPR_EV_OCC void k_bk_rollout(bk::BkParams P
                                                         const double* tabs, int32_t tn,
                                                         double* obs, double* reward,
                                                         uint8_t* done_out, cpr_summary* sum,
-                                                        int32_t kl, int32_t vw) {
+                                                        int32_t kl, int32_t vw, int32_t lpw) {
   __shared__ int32_t hist[CPR_HIST_BINS];
   if (threadIdx.x < CPR_HIST_BINS) hist[threadIdx.x] = 0;
   __syncthreads();
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  // lpw envs per wave (lanes lpw..63 idle): fewer envs per wave, more waves per SIMD to hide
+  // the dependent loads (rollout_lanes_per_wave); the slab holds the used lanes' columns
+  const int32_t wl = (int32_t)(threadIdx.x & 63u);
+  const int32_t wpb = (int32_t)(blockDim.x >> 6);
+  const int32_t col = (int32_t)(threadIdx.x >> 6) * lpw + (wl < lpw ? wl : 0);
+  const int64_t i = wl < lpw ? (int64_t)blockIdx.x * wpb * lpw + col : n;
   Acc acc = {};
   int64_t steps_all = 0, acts_all = 0;
 #if CPR_EV_SCHED
   // wave-coherent dispatch (wave_sched.h roll_fetch): the plain loop below split into items;
   // every lane's own sequence of events, actions and outputs is the plain loop's
   bk::BkMem M = bk::bk_mem_at(mem + (i < n ? i : 0) * lane_bytes, P);
-  bk::bk_heap_slab(M, bk_slab, (int32_t)threadIdx.x, (int32_t)blockDim.x, kl);
-  bk::bk_vis_window(M, (uint8_t*)(bk_slab + (size_t)kl * blockDim.x), (int32_t)threadIdx.x, vw);
+  bk::bk_heap_slab(M, bk_slab, col, wpb * lpw, kl);
+  bk::bk_vis_window(M, (uint8_t*)(bk_slab + (size_t)kl * wpb * lpw), col, vw);
   BkSlot SL;
   EvCursor c;
   c.cls = -1;
@@ -454,9 +459,8 @@ __global__ __launch_bounds__(kBlock) CPR_EV_OCC void k_bk_rollout(bk::BkParams P
     bk::BkMem M = bk::bk_mem_at(mem + i * lane_bytes, P);
     BkSlot SL = slots[i];
     // the lane's heap nodes 0 .. kl-1 move to the slab for this launch
-    bk::bk_heap_slab(M, bk_slab, (int32_t)threadIdx.x, (int32_t)blockDim.x, kl);
-    bk::bk_vis_window(M, (uint8_t*)(bk_slab + (size_t)kl * blockDim.x), (int32_t)threadIdx.x,
-                      vw);
+    bk::bk_heap_slab(M, bk_slab, col, wpb * lpw, kl);
+    bk::bk_vis_window(M, (uint8_t*)(bk_slab + (size_t)kl * wpb * lpw), col, vw);
     bk::bk_heap_load(M, SL.L.hused);
     bk::bk_vis_load(M, P, SL.L.newest);
     if (!SL.live) {
@@ -572,11 +576,33 @@ int32_t ev_slab_nodes(int64_t blocks, const void* kernel) {
   return kl;
 }
 
+// envs per wave of a lockstep rollout of n envs: 32 when 64 would leave a SIMD with one
+// wave (n <= 64 per SIMD; BASELINE configs[4]'s 65,536 envs), so that two waves per SIMD hide
+// each other's dependent loads (+5.6 % env-steps/s on configs[4], 16 per wave -28 %: the
+// kernels' registers allow two waves per SIMD; profiles/r05f_lpw.log), else 64
+// (CPR_ROLL_LPW overrides it)
+int32_t rollout_lanes_per_wave(int64_t n) {
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        cus <= 0)
+      cus = 256;
+  }
+  if (const char* v = getenv("CPR_ROLL_LPW")) {
+    const int32_t w = atoi(v);
+    if (w == 64 || w == 32 || w == 16) return w;
+  }
+  return n <= (int64_t)cus * 4 * 64 ? 32 : 64;
+}
+
 // an event-engine kernel's slab: the heap's first kl nodes and the visibility rows of the
 // newest vw vertices (BkMem.vl / TsMem.vl; 64, else 32, when they take at most a third of
 // the workgroup's share of LDS; CPR_EV_VWIN overrides it, 0 = none); kl from what is left
 // (ev_slab_nodes' rules)
-EvSlab ev_slab_plan(int64_t blocks, const void* kernel, int32_t n) {
+EvSlab ev_slab_plan(int64_t blocks, const void* kernel, int32_t n, int32_t lanes) {
+  if (lanes <= 0) lanes = kBlock;
   static int cus = 0;
   if (!cus) {
     int dev = 0;
@@ -589,26 +615,26 @@ EvSlab ev_slab_plan(int64_t blocks, const void* kernel, int32_t n) {
   const int64_t avail = (160 * 1024) / per_cu - 2048;  // static LDS of the kernels
   int32_t vw = 0;
   for (int32_t w : {64, 32})
-    if (vw == 0 && (int64_t)w * n * kBlock * 3 <= avail) vw = w;
+    if (vw == 0 && (int64_t)w * n * lanes * 3 <= avail) vw = w;
   if (const char* v = getenv("CPR_EV_VWIN")) {
     const int32_t w = atoi(v);
     vw = (w >= 1 && (w & (w - 1)) == 0 && w <= 256) ? w : 0;
   }
-  int64_t rest = avail - (int64_t)vw * n * kBlock;
+  int64_t rest = avail - (int64_t)vw * n * lanes;
   if (rest < 0) {
     vw = 0;
     rest = avail;
   }
-  int32_t kl = (int32_t)std::min<int64_t>(32, std::max<int64_t>(0, rest / (kBlock * 24)));
+  int32_t kl = (int32_t)std::min<int64_t>(32, std::max<int64_t>(0, rest / (lanes * 24)));
   if (const char* v = getenv("CPR_EV_SLAB")) kl = std::max(0, std::min(32, atoi(v)));
-  size_t bytes = (size_t)kl * kBlock * 24 + (size_t)vw * n * kBlock;
+  size_t bytes = (size_t)kl * lanes * 24 + (size_t)vw * n * lanes;
   if (bytes > 64 * 1024 &&
       hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                           160 * 1024 - 2048) != hipSuccess) {
     (void)hipGetLastError();  // the default 64 KiB: the heap slab alone
     vw = 0;
-    kl = (64 * 1024) / (kBlock * 24);
-    bytes = (size_t)kl * kBlock * 24;
+    kl = std::min(32, (64 * 1024) / (lanes * 24));
+    bytes = (size_t)kl * lanes * 24;
   }
   return EvSlab{kl, vw, bytes};
 }
@@ -657,10 +683,13 @@ hipError_t launch_bk_rollout(const bk::BkParams& P, uint64_t seed, uint8_t* mem,
                              int64_t lane_bytes, void* slots, int64_t n, int64_t n_steps,
                              int unit, const double* tabs, int32_t tn, double* obs,
                              double* reward, uint8_t* done, cpr_summary* sum, hipStream_t st) {
-  const EvSlab sl = ev_slab_plan(grid_of(n), (const void*)k_bk_rollout, P.n);
-  hipLaunchKernelGGL(k_bk_rollout, dim3(grid_of(n)), dim3(kBlock), sl.bytes, st, P, seed, mem,
+  const int32_t lpw = rollout_lanes_per_wave(n);
+  const int64_t per_block = (int64_t)(kBlock / 64) * lpw;
+  const unsigned blocks = (unsigned)((n + per_block - 1) / per_block);
+  const EvSlab sl = ev_slab_plan(blocks, (const void*)k_bk_rollout, P.n, (int32_t)per_block);
+  hipLaunchKernelGGL(k_bk_rollout, dim3(blocks), dim3(kBlock), sl.bytes, st, P, seed, mem,
                      lane_bytes, (BkSlot*)slots, n, n_steps, unit, tabs, tn, obs, reward, done,
-                     sum, sl.kl, sl.vw);
+                     sum, sl.kl, sl.vw, lpw);
   return hipGetLastError();
 }
 

@@ -323,18 +323,22 @@ __global__ __launch_bounds__(kBlock) CPR_EV_OCC void k_ts_rollout(ts::TsParams P
                                                         const double* tabs, int32_t tn,
                                                         double* obs, double* reward,
                                                         uint8_t* done_out, cpr_summary* sum,
-                                                        int32_t kl, int32_t vw) {
+                                                        int32_t kl, int32_t vw, int32_t lpw) {
   __shared__ int32_t hist[CPR_HIST_BINS];
   if (threadIdx.x < CPR_HIST_BINS) hist[threadIdx.x] = 0;
   __syncthreads();
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  // lpw envs per wave, as k_bk_rollout
+  const int32_t wl = (int32_t)(threadIdx.x & 63u);
+  const int32_t wpb = (int32_t)(blockDim.x >> 6);
+  const int32_t col = (int32_t)(threadIdx.x >> 6) * lpw + (wl < lpw ? wl : 0);
+  const int64_t i = wl < lpw ? (int64_t)blockIdx.x * wpb * lpw + col : n;
   Acc acc = {};
   int64_t steps_all = 0, acts_all = 0;
 #if CPR_EV_SCHED
   // wave-coherent dispatch, as k_bk_rollout
   ts::TsMem M = ts::ts_mem_at(mem + (i < n ? i : 0) * lane_bytes, P);
-  ts::ts_heap_slab(M, ts_slab, (int32_t)threadIdx.x, (int32_t)blockDim.x, kl);
-  ts::ts_vis_window(M, (uint8_t*)(ts_slab + (size_t)kl * blockDim.x), (int32_t)threadIdx.x, vw);
+  ts::ts_heap_slab(M, ts_slab, col, wpb * lpw, kl);
+  ts::ts_vis_window(M, (uint8_t*)(ts_slab + (size_t)kl * wpb * lpw), col, vw);
   TsSlot SL;
   EvCursor c;
   c.cls = -1;
@@ -418,9 +422,8 @@ __global__ __launch_bounds__(kBlock) CPR_EV_OCC void k_ts_rollout(ts::TsParams P
     ts::TsMem M = ts::ts_mem_at(mem + i * lane_bytes, P);
     TsSlot SL = slots[i];
     // the lane's heap nodes 0 .. kl-1 move to the slab for this launch
-    ts::ts_heap_slab(M, ts_slab, (int32_t)threadIdx.x, (int32_t)blockDim.x, kl);
-    ts::ts_vis_window(M, (uint8_t*)(ts_slab + (size_t)kl * blockDim.x), (int32_t)threadIdx.x,
-                      vw);
+    ts::ts_heap_slab(M, ts_slab, col, wpb * lpw, kl);
+    ts::ts_vis_window(M, (uint8_t*)(ts_slab + (size_t)kl * wpb * lpw), col, vw);
     ts::ts_heap_load(M, SL.L.hused);
     ts::ts_vis_load(M, P, SL.L.newest);
     if (!SL.live) {
@@ -545,10 +548,13 @@ hipError_t launch_ts_rollout(const ts::TsParams& P, uint64_t seed, uint8_t* mem,
                              int64_t lane_bytes, void* slots, int64_t n, int64_t n_steps,
                              int unit, const double* tabs, int32_t tn, double* obs,
                              double* reward, uint8_t* done, cpr_summary* sum, hipStream_t st) {
-  const EvSlab sl = ev_slab_plan(ts_grid(n), (const void*)k_ts_rollout, P.n);
-  hipLaunchKernelGGL(k_ts_rollout, dim3(ts_grid(n)), dim3(kBlock), sl.bytes, st, P, seed, mem,
+  const int32_t lpw = rollout_lanes_per_wave(n);
+  const int64_t per_block = (int64_t)(kBlock / 64) * lpw;
+  const unsigned blocks = (unsigned)((n + per_block - 1) / per_block);
+  const EvSlab sl = ev_slab_plan(blocks, (const void*)k_ts_rollout, P.n, (int32_t)per_block);
+  hipLaunchKernelGGL(k_ts_rollout, dim3(blocks), dim3(kBlock), sl.bytes, st, P, seed, mem,
                      lane_bytes, (TsSlot*)slots, n, n_steps, unit, tabs, tn, obs, reward, done,
-                     sum, sl.kl, sl.vw);
+                     sum, sl.kl, sl.vw, lpw);
   return hipGetLastError();
 }
 
