@@ -597,6 +597,17 @@ int32_t rollout_lanes_per_wave(int64_t n) {
   return n <= (int64_t)cus * 4 * 64 ? 32 : 64;
 }
 
+// lanes per wave that run episodes in the fused event-engine kernels (the others idle):
+// 64 (CPR_EV_LPW overrides it for A/B runs: 32 with an occupancy variant runs the same
+// lanes as twice the waves)
+int32_t event_lanes_per_wave() {
+  if (const char* v = getenv("CPR_EV_LPW")) {
+    const int32_t w = atoi(v);
+    if (w == 64 || w == 32 || w == 16) return w;
+  }
+  return 64;
+}
+
 // an event-engine kernel's slab: the heap's first kl nodes and the visibility rows of the
 // newest vw vertices (BkMem.vl / TsMem.vl; 64, else 32, when they take at most a third of
 // the workgroup's share of LDS; CPR_EV_VWIN overrides it, 0 = none); kl from what is left

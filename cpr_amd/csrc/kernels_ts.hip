@@ -127,24 +127,29 @@ template <class Src>
 __global__ __launch_bounds__(kBlock) CPR_EV_OCC void k_ts_run_episodes(
     ts::TsParams P, Src src, int64_t n_eps, uint8_t* mem,
     int64_t lane_bytes, cpr_episode_record* recs, cpr_summary* sum, NodeOut no, int32_t kl,
-    int32_t vw) {
+    int32_t vw, int32_t lpw) {
   __shared__ int32_t hist[CPR_HIST_BINS];
   if (threadIdx.x < CPR_HIST_BINS) hist[threadIdx.x] = 0;
   __syncthreads();
-  const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const int64_t nthreads = (int64_t)gridDim.x * blockDim.x;
+  // lpw lanes per wave run episodes (the others idle; event_lanes_per_wave)
+  const int32_t wl = (int32_t)(threadIdx.x & 63u);
+  const int32_t wpb = (int32_t)(blockDim.x >> 6);
+  const bool used = wl < lpw;
+  const int32_t col = (int32_t)(threadIdx.x >> 6) * lpw + (used ? wl : 0);
+  const int64_t tid = (int64_t)blockIdx.x * wpb * lpw + col;
+  const int64_t nthreads = (int64_t)gridDim.x * wpb * lpw;
   ts::TsMem M = ts::ts_mem_at(mem + tid * lane_bytes, P);
   if (no.mem) M.nact = (int64_t*)(no.mem + tid * no.lane_bytes);
   // every episode starts with an empty heap and a fresh window (init): the slab needs no
   // load or store
-  ts::ts_heap_slab(M, ts_slab, (int32_t)threadIdx.x, (int32_t)blockDim.x, kl);
-  ts::ts_vis_window(M, (uint8_t*)(ts_slab + (size_t)kl * blockDim.x), (int32_t)threadIdx.x, vw);
+  ts::ts_heap_slab(M, ts_slab, col, wpb * lpw, kl);
+  ts::ts_vis_window(M, (uint8_t*)(ts_slab + (size_t)kl * wpb * lpw), col, vw);
   Acc acc = {};
   ts::TsLane L;
 #if CPR_EV_SCHED
   // wave-coherent dispatch (wave_sched.h): grid-stride over episodes, every iteration runs
   // the work class most lanes of the wave hold
-  int64_t e = tid;
+  int64_t e = used ? tid : n_eps;
   auto S = src.at(e < n_eps ? e : 0);
   EvCursor c;
   c.cls = -1;
@@ -215,7 +220,7 @@ __global__ __launch_bounds__(kBlock) CPR_EV_OCC void k_ts_run_episodes(
   }
 #endif
 #else
-  for (int64_t e = tid; e < n_eps; e += nthreads) {
+  for (int64_t e = used ? tid : n_eps; e < n_eps; e += nthreads) {
     const auto S = src.at(e);
     int32_t hd;
     if (P.mode == CPR_MODE_GYM) {
@@ -508,11 +513,14 @@ hipError_t launch_ts_run_episodes(const ts::TsParams& P, uint64_t seed, uint64_t
                                   int64_t n_eps, uint8_t* mem, int64_t lane_bytes, int64_t lanes,
                                   cpr_episode_record* recs, cpr_summary* sum, hipStream_t st,
                                   const NodeOut& no) {
+  // the resident grid; lpw < 64 runs lanes * lpw / 64 episodes at a time in it
+  const int32_t lpw = event_lanes_per_wave();
   const unsigned blocks = (unsigned)(lanes / kBlock);
-  const EvSlab sl = ev_slab_plan(blocks, (const void*)k_ts_run_episodes<SeedSource>, P.n);
+  const EvSlab sl = ev_slab_plan(blocks, (const void*)k_ts_run_episodes<SeedSource>, P.n,
+                                 (kBlock / 64) * lpw);
   hipLaunchKernelGGL(k_ts_run_episodes<SeedSource>, dim3(blocks), dim3(kBlock), sl.bytes, st, P,
                      SeedSource{seed, first}, n_eps, mem, lane_bytes, recs, sum, no, sl.kl,
-                     sl.vw);
+                     sl.vw, lpw);
   return hipGetLastError();
 }
 
@@ -520,10 +528,13 @@ hipError_t launch_ts_replay_episodes(const ts::TsParams& P, const TraceSource& s
                                  uint8_t* mem, int64_t lane_bytes, int64_t lanes,
                                  cpr_episode_record* recs, cpr_summary* sum, hipStream_t st,
                                   const NodeOut& no) {
+  // the resident grid; lpw < 64 runs lanes * lpw / 64 episodes at a time in it
+  const int32_t lpw = event_lanes_per_wave();
   const unsigned blocks = (unsigned)(lanes / kBlock);
-  const EvSlab sl = ev_slab_plan(blocks, (const void*)k_ts_run_episodes<TraceSource>, P.n);
+  const EvSlab sl = ev_slab_plan(blocks, (const void*)k_ts_run_episodes<TraceSource>, P.n,
+                                 (kBlock / 64) * lpw);
   hipLaunchKernelGGL(k_ts_run_episodes<TraceSource>, dim3(blocks), dim3(kBlock), sl.bytes, st, P,
-                     src, n_eps, mem, lane_bytes, recs, sum, no, sl.kl, sl.vw);
+                     src, n_eps, mem, lane_bytes, recs, sum, no, sl.kl, sl.vw, lpw);
   return hipGetLastError();
 }
 
