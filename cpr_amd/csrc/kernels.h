@@ -148,7 +148,7 @@ struct EvSlab {
 };
 // lanes: used lanes per workgroup (0: all of kBlock)
 EvSlab ev_slab_plan(int64_t blocks, const void* kernel, int32_t n, int32_t lanes = 0);
-int32_t rollout_lanes_per_wave(int64_t n);
+int32_t rollout_lanes_per_wave(int64_t n, const void* kernel);
 int32_t event_lanes_per_wave();
 // Ethereum gym episodes on the selfish-mining network through the window lane
 // (eth_window.h; ethw::win_supported): mem = lanes x ethw::win_lane_bytes; flagged episodes

@@ -270,7 +270,13 @@ __global__ __launch_bounds__(kBlock) void k_bk_step(bk::BkParams P, uint64_t see
 // observation written at a done step is the new episode's first observation).
 // summary.steps / .activations count every step / activation of the rollout; the other
 // summary fields cover the episodes that finished in it.
-__global__ __launch_bounds__(kBlock) CPR_EV_OCC void k_bk_rollout(bk::BkParams P, uint64_t seed,
+// four waves per SIMD (128 VGPRs): rollout_lanes_per_wave spreads a small batch over them
+#if CPR_EV_WAVES > 0
+#define CPR_ROLL_OCC CPR_EV_OCC
+#else
+#define CPR_ROLL_OCC __attribute__((amdgpu_waves_per_eu(4)))
+#endif
+__global__ __launch_bounds__(kBlock) CPR_ROLL_OCC void k_bk_rollout(bk::BkParams P, uint64_t seed,
                                                         uint8_t* mem, int64_t lane_bytes,
                                                         BkSlot* slots, int64_t n,
                                                         int64_t n_steps, int unit,
@@ -576,12 +582,13 @@ int32_t ev_slab_nodes(int64_t blocks, const void* kernel) {
   return kl;
 }
 
-// envs per wave of a lockstep rollout of n envs: 32 when 64 would leave a SIMD with one
-// wave (n <= 64 per SIMD; BASELINE configs[4]'s 65,536 envs), so that two waves per SIMD hide
-// each other's dependent loads (+5.6 % env-steps/s on configs[4], 16 per wave -28 %: the
-// kernels' registers allow two waves per SIMD; profiles/r05f_lpw.log), else 64
-// (CPR_ROLL_LPW overrides it)
-int32_t rollout_lanes_per_wave(int64_t n) {
+// envs per wave of a lockstep rollout of n envs on `kernel`: the widest of 64 / 32 / 16 whose
+// waves fit the kernel's resident waves per SIMD (occupancy query), so that a small batch
+// still runs several waves per SIMD, which hide each other's dependent loads (BASELINE
+// configs[4], 65,536 B_k envs: one wave per SIMD at 64; 32 per wave +5.6 % env-steps/s,
+// 16 per wave at the 4-wave budget of k_bk_rollout +3.7 % more;
+// profiles/r05f_lpw.log, profiles/r05g_lpw.log). CPR_ROLL_LPW overrides it.
+int32_t rollout_lanes_per_wave(int64_t n, const void* kernel) {
   static int cus = 0;
   if (!cus) {
     int dev = 0;
@@ -594,7 +601,16 @@ int32_t rollout_lanes_per_wave(int64_t n) {
     const int32_t w = atoi(v);
     if (w == 64 || w == 32 || w == 16) return w;
   }
-  return n <= (int64_t)cus * 4 * 64 ? 32 : 64;
+  int per_cu = 0;  // workgroups of kBlock / 64 waves, i.e. waves per SIMD
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, kBlock, 0) != hipSuccess ||
+      per_cu <= 0) {
+    (void)hipGetLastError();
+    per_cu = 1;
+  }
+  const int64_t simds = (int64_t)cus * 4;
+  for (int32_t w : {16, 32})
+    if ((n + w * simds - 1) / (w * simds) <= per_cu) return w;
+  return 64;
 }
 
 // lanes per wave that run episodes in the fused event-engine kernels (the others idle):
@@ -694,7 +710,7 @@ hipError_t launch_bk_rollout(const bk::BkParams& P, uint64_t seed, uint8_t* mem,
                              int64_t lane_bytes, void* slots, int64_t n, int64_t n_steps,
                              int unit, const double* tabs, int32_t tn, double* obs,
                              double* reward, uint8_t* done, cpr_summary* sum, hipStream_t st) {
-  const int32_t lpw = rollout_lanes_per_wave(n);
+  const int32_t lpw = rollout_lanes_per_wave(n, (const void*)k_bk_rollout);
   const int64_t per_block = (int64_t)(kBlock / 64) * lpw;
   const unsigned blocks = (unsigned)((n + per_block - 1) / per_block);
   const EvSlab sl = ev_slab_plan(blocks, (const void*)k_bk_rollout, P.n, (int32_t)per_block);

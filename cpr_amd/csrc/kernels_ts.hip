@@ -559,7 +559,7 @@ hipError_t launch_ts_rollout(const ts::TsParams& P, uint64_t seed, uint8_t* mem,
                              int64_t lane_bytes, void* slots, int64_t n, int64_t n_steps,
                              int unit, const double* tabs, int32_t tn, double* obs,
                              double* reward, uint8_t* done, cpr_summary* sum, hipStream_t st) {
-  const int32_t lpw = rollout_lanes_per_wave(n);
+  const int32_t lpw = rollout_lanes_per_wave(n, (const void*)k_ts_rollout);
   const int64_t per_block = (int64_t)(kBlock / 64) * lpw;
   const unsigned blocks = (unsigned)((n + per_block - 1) / per_block);
   const EvSlab sl = ev_slab_plan(blocks, (const void*)k_ts_rollout, P.n, (int32_t)per_block);
