@@ -275,3 +275,39 @@ def test_configs4_full_size_table_rollout(ctx):
     finally:
         rew.free()
         done.free()
+
+
+def test_bk_rollout_envs_per_wave_ragged(ctx, monkeypatch):
+    """A ragged batch (100 envs: the last wave partly used) gives the same outputs at 64, 32
+    and 16 envs per wave (CPR_ROLL_LPW; the default picks 16 here), and sampled lanes equal
+    sequential oracle episodes."""
+    n, T, ms = 100, 40, 25
+    cfg, keep = _cfg(alpha=0.33, gamma=0.5, policy=L.BK_POLICY_AVOID_LOSS, max_steps=ms,
+                     seed=321, n_lanes=n)
+    outs = {}
+    for w in ("64", "32", "16", None):
+        if w is None:
+            monkeypatch.delenv("CPR_ROLL_LPW", raising=False)
+        else:
+            monkeypatch.setenv("CPR_ROLL_LPW", w)
+        b = device.Batch(cfg, keep=keep)
+        s, obs, rew, done = b.rollout(T, outputs=True)
+        outs[w] = (s.steps, s.episodes, s.activations, obs, rew, done)
+    ref = outs["64"]
+    for w, o in outs.items():
+        assert o[:3] == ref[:3], w
+        for a, r in zip(o[3:], ref[3:]):
+            assert np.array_equal(a, r), w
+    _, _, _, obs, rew, done = ref
+    for i in (0, 15, 16, 63, 64, 95, 96, 99):
+        ep = i
+        e = O.BkGymEnv(cfg, episode=ep)
+        e.reset()
+        for t in range(T):
+            o, r, d, info = e.step(O.bk_policy("avoid-loss", e.fields(), 8))
+            assert rew[t, i] == r and bool(done[t, i]) == d, (i, t)
+            if d:
+                ep += n
+                e = O.BkGymEnv(cfg, episode=ep)
+                o = e.reset()
+            assert np.array_equal(obs[t, i], o), (i, t)

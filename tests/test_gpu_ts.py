@@ -219,3 +219,37 @@ def test_ts_table_policy_decoding_and_rollout(ctx):
                 ep += n
                 e = O.TsGymEnv(cfg, episode=ep)
                 e.reset()
+
+
+def test_ts_rollout_envs_per_wave_ragged(ctx, monkeypatch):
+    """As test_bk_rollout_envs_per_wave_ragged, for the Tailstorm rollout."""
+    n, T, ms = 100, 40, 25
+    cfg, keep = _cfg(alpha=0.33, gamma=0.5, policy=L.TS_POLICY_GET_AHEAD, max_steps=ms,
+                     seed=654, n_lanes=n)
+    outs = {}
+    for w in ("64", "32", "16", None):
+        if w is None:
+            monkeypatch.delenv("CPR_ROLL_LPW", raising=False)
+        else:
+            monkeypatch.setenv("CPR_ROLL_LPW", w)
+        b = device.Batch(cfg, keep=keep)
+        s, obs, rew, done = b.rollout(T, outputs=True)
+        outs[w] = (s.steps, s.episodes, s.activations, obs, rew, done)
+    ref = outs["64"]
+    for w, o in outs.items():
+        assert o[:3] == ref[:3], w
+        for a, r in zip(o[3:], ref[3:]):
+            assert np.array_equal(a, r), w
+    _, _, _, obs, rew, done = ref
+    for i in (0, 15, 16, 63, 64, 95, 96, 99):
+        ep = i
+        e = O.TsGymEnv(cfg, episode=ep)
+        e.reset()
+        for t in range(T):
+            o, r, d, info = e.step(O.ts_policy("get-ahead", e.fields(), 8))
+            assert rew[t, i] == r and done[t, i] == d, (i, t)
+            if d:
+                ep += n
+                e = O.TsGymEnv(cfg, episode=ep)
+                o = e.reset()
+            assert np.array_equal(obs[t, i], o), (i, t)
