@@ -271,10 +271,13 @@ __global__ __launch_bounds__(kBlock) void k_bk_step(bk::BkParams P, uint64_t see
 // summary.steps / .activations count every step / activation of the rollout; the other
 // summary fields cover the episodes that finished in it.
 // four waves per SIMD (128 VGPRs): rollout_lanes_per_wave spreads a small batch over them
+#ifndef CPR_ROLL_WAVES
+#define CPR_ROLL_WAVES 4
+#endif
 #if CPR_EV_WAVES > 0
 #define CPR_ROLL_OCC CPR_EV_OCC
 #else
-#define CPR_ROLL_OCC __attribute__((amdgpu_waves_per_eu(4)))
+#define CPR_ROLL_OCC __attribute__((amdgpu_waves_per_eu(CPR_ROLL_WAVES)))
 #endif
 __global__ __launch_bounds__(kBlock) CPR_ROLL_OCC void k_bk_rollout(bk::BkParams P, uint64_t seed,
                                                         uint8_t* mem, int64_t lane_bytes,
@@ -599,7 +602,7 @@ int32_t rollout_lanes_per_wave(int64_t n, const void* kernel) {
   }
   if (const char* v = getenv("CPR_ROLL_LPW")) {
     const int32_t w = atoi(v);
-    if (w == 64 || w == 32 || w == 16) return w;
+    if (w >= 1 && w <= 64) return w;
   }
   int per_cu = 0;  // workgroups of kBlock / 64 waves, i.e. waves per SIMD
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, kBlock, 0) != hipSuccess ||

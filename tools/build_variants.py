@@ -1,7 +1,8 @@
 """Occupancy variants of libcpr_hip for A/B runs (tools/occupancy_ab.sh): the three
 event-engine translation units rebuilt with -DCPR_EV_WAVES=<w> (kernels.h), linked with the
 default build's other objects into build/var/ev<w>.so; with --ew, -DCPR_EW_WAVES=<w> (the
-Ethereum window lane's kernel) into build/var/ew<w>.so. Run __graft_entry__.build() first.
+Ethereum window lane's kernel) into build/var/ew<w>.so; with --roll, -DCPR_ROLL_WAVES=<w>
+(k_bk_rollout's wave budget) into build/var/rw<w>.so. Run __graft_entry__.build() first.
 
 Usage: python tools/build_variants.py 2 4;  python tools/build_variants.py --ew 3 4
 """
@@ -25,6 +26,8 @@ def main():
     macro, tag = "CPR_EV_WAVES", "ev"
     if args and args[0] == "--ew":
         macro, tag, args = "CPR_EW_WAVES", "ew", args[1:]
+    if args and args[0] == "--roll":
+        macro, tag, args = "CPR_ROLL_WAVES", "rw", args[1:]
     for w in args:
         vdir = out / f"{tag}{w}"
         vdir.mkdir(exist_ok=True)
