@@ -622,7 +622,7 @@ int32_t rollout_lanes_per_wave(int64_t n, const void* kernel) {
 int32_t event_lanes_per_wave() {
   if (const char* v = getenv("CPR_EV_LPW")) {
     const int32_t w = atoi(v);
-    if (w == 64 || w == 32 || w == 16) return w;
+    if (w >= 1 && w <= 64) return w;
   }
   return 64;
 }
