@@ -574,7 +574,10 @@ def main():
                 "invalid_episodes": sum(int(s.invalid) for s in atotals),
             },
         }
-        if not args.no_cpu and ws == 1:
+        if not args.no_cpu:
+            # host only, after every collective of the timed region: at N > 1 rank 0
+            # measures the same bounded oracle sample, so every line of a 1/2/4/8-GPU series
+            # carries the CPU baseline of its own job (north_star)
             out["cpu_baseline"] = cpu_baseline(args.cpu_seconds, points)
         if not args.no_configs and ws == 1:
             # the other BASELINE configs on this GPU, after the headline's timed region

@@ -73,9 +73,10 @@ struct cpr_ctx {
   // entries a launch may append (kRerunQueue; CPR_RERUN_QUEUE_CAP lowers it for tests);
   // an episode that finds the queue full waits in its launch's overflow flags: one byte
   // per episode of every launch since the last flush, carved from the chunks of `ovf` in
-  // order (chunk ovf_chunk, ovf_used bytes taken). Chunks are only added, never
-  // reallocated, so filling one never forces a flush: a flush costs the latency of one
-  // exact episode (~80 ms at the gym's 2016 steps), paid once per synchronization
+  // order (chunk ovf_chunk, ovf_used bytes taken). Chunks are never reallocated, so
+  // filling one forces no flush until kOvfMaxChunks are in use (1 GiB of flags, ~200
+  // launches of the bench's 5.2M episodes): a flush costs the latency of one exact episode
+  // (~80 ms at the gym's 2016 steps), paid once per synchronization
   int64_t rq_cap = kRerunQueue;
   std::vector<std::unique_ptr<DevBuf>> ovf;
   size_t ovf_chunk = 0, ovf_used = 0;
@@ -880,6 +881,8 @@ static int64_t episode_lanes(cpr_batch* b, int64_t n_eps, bool recs) {
 // Re-run every queued flagged Nakamoto episode of the launches since the last flush, in
 // one k_nak_exact_rerun launch on the context's stream (after those launches, before the
 // caller reads summaries or records), then empty the queue.
+constexpr size_t kOvfMaxChunks = 4;  // overflow-flag chunks (256 MiB each) before a flush
+
 static int flush_reruns(cpr_ctx* c) {
   if (c->rlaunch.empty()) return CPR_OK;
   int64_t lb = 0, rest = 0;
@@ -928,10 +931,18 @@ static int register_rerun(cpr_batch* b, const eth::EthParams& EP, int64_t lane_b
     if (rc) return rc;
   }
   // the launch's flags: the rest of the current chunk, else the next chunk that holds them
-  // (a new one if none does; earlier chunks stay, queued kernels may still read them)
-  while (c->ovf_chunk < c->ovf.size() && c->ovf_used + need > c->ovf[c->ovf_chunk]->bytes) {
-    ++c->ovf_chunk;
-    c->ovf_used = 0;
+  // (a new one if none does; earlier chunks stay, queued kernels may still read them).
+  // Chunks are reused from the first after every flush; once kOvfMaxChunks are taken the
+  // launches so far are flushed first, so many large asynchronous launches between two
+  // synchronizations do not keep adding chunks for the life of the context
+  for (int pass = 0;; ++pass) {
+    while (c->ovf_chunk < c->ovf.size() && c->ovf_used + need > c->ovf[c->ovf_chunk]->bytes) {
+      ++c->ovf_chunk;
+      c->ovf_used = 0;
+    }
+    if (c->ovf_chunk < c->ovf.size() || c->ovf.size() < kOvfMaxChunks || pass > 0) break;
+    const int rc = flush_reruns(c);  // resets ovf_chunk / ovf_used to chunk 0
+    if (rc) return rc;
   }
   if (c->ovf_chunk == c->ovf.size()) {
     c->ovf.emplace_back(new DevBuf());
@@ -966,12 +977,15 @@ static int register_rerun(cpr_batch* b, const eth::EthParams& EP, int64_t lane_b
 }
 
 // The window lane (eth_window.h) takes Ethereum gym episodes on the selfish-mining network
-// whose only limit is max_steps (the lanes of a wave then run equal trip counts);
-// CPR_ETH_WINDOW=0 sends them to the event engine instead (A/B runs)
+// whose whole episode fits its block ring: the ring does not wrap (WinLane::append fails
+// instead), so an episode of max_steps + 1 activations (+ genesis) must fit cap_b, or every
+// episode would end in W_REDO and a one-lane exact re-run. max_progress / max_time only end
+// episodes earlier (each lane leaves its loop on its own done). CPR_ETH_WINDOW=0 sends them
+// to the event engine instead (A/B runs)
 static bool eth_window_ok(const cpr_batch* b) {
   const char* v = getenv("CPR_ETH_WINDOW");
-  return (v == nullptr || atoi(v) != 0) && ethw::win_supported(b->EP) && !(b->EP.max_progress < __builtin_inf()) &&
-         !(b->EP.max_time < __builtin_inf());
+  return (v == nullptr || atoi(v) != 0) && ethw::win_supported(b->EP) &&
+         b->EP.max_steps <= (int64_t)b->EP.cap_b - 2;
 }
 
 static int run_async_ethwin(cpr_batch* b, int64_t n, uint64_t first, cpr_summary* sum_dev,
@@ -1458,17 +1472,31 @@ static int ensure_lockstep(cpr_batch* b) {
     // fit the budgets (kExactSlotBudget of slots: 65,536 lanes of 2,016-step episodes
     // take ~27 GB of the 288 GB; kActionLogBudget of logs), so the lockstep API stays
     // exact for every lane like engine.ml's step (engine.ml:176-249); beyond the budgets
-    // (lanes x episode length), a lane that finds no slot keeps the closed form's flags
+    // (lanes x episode length), a lane that finds no slot keeps the closed form's flags.
+    // The slot pool is also capped at a quarter of the device's free memory, and an
+    // allocation that fails is retried with half the slots (down to 256) instead of failing
+    // the reset: at the gym's delays almost no lane ever leaves the closed form
     constexpr int64_t kExactSlotBudget = 48ll << 30, kActionLogBudget = 4ll << 30;
     const int64_t ms = b->P.max_steps > 0 && b->P.max_steps < (1ll << 30) ? b->P.max_steps
                                                                           : (1 << 14);
-    int64_t cap = std::min<int64_t>(ms, std::max<int64_t>(1 << 14, kActionLogBudget / n));
+    int64_t cap = std::min<int64_t>(ms, kActionLogBudget / n);
     cap = std::max<int64_t>(1, cap);
     b->alog_cap = cap;
-    b->n_exact_slots = (int32_t)std::min<int64_t>(
-        n, std::max<int64_t>(256, kExactSlotBudget / std::max<int64_t>(1, b->nak_bytes)));
+    const int64_t eb = std::max<int64_t>(1, b->nak_bytes);
+    int64_t slots = std::min<int64_t>(n, std::max<int64_t>(256, kExactSlotBudget / eb));
+    size_t free_b = 0, total_b = 0;
+    if (hipMemGetInfo(&free_b, &total_b) == hipSuccess)
+      slots = std::min<int64_t>(slots, std::max<int64_t>(256, (int64_t)(free_b / 4) / eb));
+    slots = std::min<int64_t>(slots, n);
     HIP_TRY(b->l_alog.ensure((size_t)n * (size_t)cap));
-    HIP_TRY(b->l_emem.ensure((size_t)b->n_exact_slots * (size_t)b->nak_bytes));
+    for (;;) {
+      const hipError_t e = b->l_emem.ensure((size_t)slots * (size_t)eb);
+      if (e == hipSuccess) break;
+      (void)hipGetLastError();
+      if (slots <= 256) HIP_TRY(e);
+      slots = std::max<int64_t>(256, slots / 2);
+    }
+    b->n_exact_slots = (int32_t)slots;
     HIP_TRY(b->l_eslots.ensure((size_t)b->n_exact_slots * sizeof(eth::EthLane)));
     std::vector<int32_t> stack((size_t)b->n_exact_slots + 1);
     for (int32_t i = 0; i < b->n_exact_slots; i++) stack[i] = i;

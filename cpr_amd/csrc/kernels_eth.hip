@@ -158,9 +158,9 @@ __global__ __launch_bounds__(kBlock) CPR_EV_OCC void k_eth_run_episodes(
 // one lane per episode, grid-stride over the launch's episodes, outputs as
 // k_eth_run_episodes. An episode the window lane cannot vouch for (W_REDO) goes to the
 // context's exact re-run queue instead, like the Nakamoto lane's (k_nak_exact_rerun runs it
-// again from its first draw on the event engine at the next synchronization point). Every
-// gym episode has max_steps steps (no progress / time limit: the host routes only those
-// here), so the lanes of a wave run the same number of windows.
+// again from its first draw on the event engine at the next synchronization point). Each
+// lane leaves its loop at its own done (max_steps, max_progress or max_time, engine.ml:
+// 209-214); with max_steps alone the lanes of a wave run the same number of windows.
 #ifdef CPR_EW_WAVES  // occupancy A/B (tools/build_variants.py --ew)
 #define CPR_EW_OCC __attribute__((amdgpu_waves_per_eu(CPR_EW_WAVES)))
 #else

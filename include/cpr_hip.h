@@ -285,6 +285,11 @@ typedef struct cpr_summary {
   uint64_t rel_revenue_fx;      /* sum of round(attacker/(attacker+defender) * 2^32) */
   uint64_t rel_revenue_sq_fx;   /* sum of round((attacker/(attacker+defender))^2 * 2^32) */
   int64_t orphans;              /* activations - head height */
+  /* status_tie / status_overlap are diagnostics of the route that ran: the closed-form
+     Nakamoto lane and the Ethereum window lane set CPR_ST_TIE when they replay a
+     same-instant race and CPR_ST_OVERLAP when they hand an episode to the exact re-run;
+     the per-lane event engines follow the reference's queue and set neither. Every other
+     field is route-independent. */
   int64_t status_tie;           /* episodes with CPR_ST_TIE */
   int64_t status_overlap;       /* episodes with CPR_ST_OVERLAP */
   int64_t status_other;         /* valid episodes with other status bits */

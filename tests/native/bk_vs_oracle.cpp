@@ -34,6 +34,9 @@ struct Cfg {
   int two_agents;  // 0 gym, 1 two-agents loop, 2 honest-clique loop (defenders = nodes)
   int k;
   double ev = 1.0;
+  // engine.ml:209-214's other two done clauses (+inf = off; gym configurations only)
+  double max_time = __builtin_inf();
+  double max_progress = __builtin_inf();
 };
 
 struct Counters {
@@ -76,8 +79,8 @@ static bk::BkParams params_of(const Cfg& cf) {
   P.dmax = (dd - 1.) / dd * 1e-9 / cf.gamma;
   P.max_steps = cf.steps;
   P.activations = cf.steps;
-  P.max_progress = __builtin_inf();
-  P.max_time = __builtin_inf();
+  P.max_progress = cf.max_progress;
+  P.max_time = cf.max_time;
   return P;
 }
 
@@ -99,6 +102,8 @@ static bool run_gym(const Cfg& cf, uint64_t seed, uint64_t ep, Counters& C, std:
   gp.gamma = cf.gamma;
   gp.defenders = cf.defenders;
   gp.max_steps = cf.steps;
+  gp.max_progress = cf.max_progress;
+  gp.max_time = cf.max_time;
   gp.unit_obs = false;
   oracle::GymBk g(gp, cf.k, cf.scheme, 1, nullptr, seed, ep);
   double obs[8];
@@ -277,6 +282,16 @@ int main(int argc, char** argv) {
   for (int n : {2, 3, 10})
     for (double ev : {0.5, 2.0, 30.0, 600.0})
       for (int sch : {0, 2}) cfgs.push_back(Cfg{0, 0, n, 0, sch, steps * 2, 2, k, ev});
+  // gym episodes ended by max_time / max_progress before max_steps (engine.ml:209-214)
+  for (int pol : {1, 3, 5})
+    for (double g : {0.0, 0.5}) {
+      Cfg c{0.33, g, 2, pol, pol == 3 ? 2 : 0, steps, 0, k};
+      c.max_time = 0.3 * steps;
+      cfgs.push_back(c);
+      c.max_time = __builtin_inf();
+      c.max_progress = steps / 6;
+      cfgs.push_back(c);
+    }
   Counters C;
   int shown = 0;
   for (auto& cf : cfgs)

@@ -35,6 +35,9 @@ struct Cfg {
   int scheme;
   int steps;
   double prop;
+  // engine.ml:209-214's other two done clauses (+inf = off)
+  double max_time = __builtin_inf();
+  double max_progress = __builtin_inf();
 };
 
 struct Counters {
@@ -58,8 +61,8 @@ static eth::EthParams params_of(const Cfg& cf) {
   const double dd = cf.defenders;
   P.dmax = (dd - 1.) / dd * cf.prop / cf.gamma;
   P.max_steps = cf.steps;
-  P.max_progress = __builtin_inf();
-  P.max_time = __builtin_inf();
+  P.max_progress = cf.max_progress;
+  P.max_time = cf.max_time;
   return P;
 }
 
@@ -71,6 +74,8 @@ static bool run_gym(const Cfg& cf, uint64_t seed, uint64_t ep, Counters& C, std:
   gp.max_steps = cf.steps;
   gp.unit_obs = false;
   gp.propagation_delay = cf.prop;
+  gp.max_progress = cf.max_progress;
+  gp.max_time = cf.max_time;
   oracle::GymEthereum g(gp, cf.scheme, 1, nullptr, seed, ep);
   double obs[10];
   g.reset(obs);
@@ -176,6 +181,21 @@ int main(int argc, char** argv) {
       cfgs.push_back({a, 0.5, 2, pol, 0, steps, 0.05});
       cfgs.push_back({a, 0.9, 11, pol, 1, steps, 0.01});
     }
+  // episodes ended by max_time / max_progress before max_steps (engine.ml:209-214)
+  for (int pol : {1, 3, 5})
+    for (double a : {0.25, 0.45})
+      for (double g : {0.0, 0.5, 0.9}) {
+        const int d = g == 0.9 ? 10 : 2;
+        Cfg c{a, g, d, pol, pol % 2, steps, 1e-9};
+        c.max_time = 0.3 * steps;
+        cfgs.push_back(c);
+        c.max_time = __builtin_inf();
+        c.max_progress = steps / 5;
+        cfgs.push_back(c);
+        c.max_time = 0.5 * steps;
+        c.prop = 0.05;  // overlaps: the re-run path's episodes stop being compared at W_REDO
+        cfgs.push_back(c);
+      }
   Counters C;
   long shown = 0;
   for (size_t ci = 0; ci < cfgs.size(); ++ci)

@@ -40,6 +40,9 @@ struct Cfg {
   int k;
   double ev = 1.0;
   double prop = 1.0;
+  // engine.ml:209-214's other two done clauses (+inf = off; gym configurations only)
+  double max_time = __builtin_inf();
+  double max_progress = __builtin_inf();
 };
 
 struct Counters {
@@ -111,8 +114,8 @@ static ts::TsParams params_of(const Cfg& cf) {
   }
   P.max_steps = cf.steps;
   P.activations = cf.steps;
-  P.max_progress = __builtin_inf();
-  P.max_time = __builtin_inf();
+  P.max_progress = cf.max_progress;
+  P.max_time = cf.max_time;
   return P;
 }
 
@@ -134,6 +137,8 @@ static bool run_gym(const Cfg& cf, uint64_t seed, uint64_t ep, Counters& C, std:
   gp.gamma = cf.gamma;
   gp.defenders = cf.defenders;
   gp.max_steps = cf.steps;
+  gp.max_progress = cf.max_progress;
+  gp.max_time = cf.max_time;
   gp.unit_obs = false;
   oracle::GymTailstorm g(gp, cf.k, cf.scheme, g_sel, 1, nullptr, seed, ep);
   double obs[10];
@@ -445,6 +450,16 @@ int main(int argc, char** argv) {
   for (int d : {1, 2})
     for (double ev : {1.0, 10.0})
       for (int pol : {0, 1, 2, 3, 9}) cfgs.push_back(Cfg{0, 0, d, pol, 1, steps * 2, 3, k, ev, 1.0});
+  // gym episodes ended by max_time / max_progress before max_steps (engine.ml:209-214)
+  for (int pol : {1, 3, 7})
+    for (double g : {0.0, 0.5}) {
+      Cfg c{0.33, g, 2, pol, 1, steps, 0, k};
+      c.max_time = 0.3 * steps;
+      cfgs.push_back(c);
+      c.max_time = __builtin_inf();
+      c.max_progress = steps / 6;
+      cfgs.push_back(c);
+    }
   Counters C;
   int shown = 0;
   for (auto& cf : cfgs)

@@ -72,12 +72,18 @@ def test_bench_starts_two_ranks_itself():
     env = {k: v for k, v in os.environ.items()
            if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
     env["PYTHONPATH"] = ROOT + os.pathsep + env.get("PYTHONPATH", "")
+    # reports the whole job, with rank 0's bounded CPU baseline (measured after the timed
+    # region) in the N-GPU line too
     p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps",
-                        "2", "--warmup", "1", "--episodes", "8192", "--no-cpu", "--backend",
-                        "gloo"], cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+                        "2", "--warmup", "1", "--episodes", "8192", "--cpu-seconds", "2",
+                        "--backend", "gloo"], cwd=ROOT, env=env, capture_output=True, text=True,
+                       timeout=300)
     assert p.returncode == 0, p.stderr[-4000:]
     lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, p.stdout[-2000:]
     d = json.loads(lines[0])
     assert d["n_gpus"] == 2
     assert round(d["episodes_per_s"] * d["ms_per_step"] * d["steps"] / 1e3) == 20 * 8192 * 2 * 2
+    cb = d["cpu_baseline"]
+    assert cb["value"] > 0 and cb["cores"] >= 1 and cb["kind"] == "port"
+    assert "other_configs" not in d  # GPU work beyond the headline stays at N = 1

@@ -248,19 +248,44 @@ def test_eth_window_lane_matches_oracle(ctx, alpha, gamma, policy, scheme, prop,
     assert s.progress_fx == int(np.rint(rec["progress"] * 2**20).sum())
 
 
-@pytest.mark.parametrize("gamma", [0.0, 0.5, 0.9])
-def test_eth_window_lane_equals_event_engine(ctx, gamma, monkeypatch):
+# status_tie / status_overlap are route diagnostics (include/cpr_hip.h cpr_summary): the
+# window lane counts its tie replays and hand-backs, the event engine sets neither bit
+ROUTE_FIELDS = ("status_tie", "status_overlap")
+
+
+@pytest.mark.parametrize("gamma,prop", [(0.0, 1e-9), (0.5, 1e-9), (0.9, 1e-9), (0.5, 0.05)])
+def test_eth_window_lane_equals_event_engine(ctx, gamma, prop, monkeypatch):
     # the bench's configs[2] point at full episode length: the window lane's summary equals
-    # the event engine's (CPR_ETH_WINDOW=0) field for field
+    # the event engine's (CPR_ETH_WINDOW=0) field for field; at a 0.05 delay most episodes
+    # overlap, so the window route's hand-backs (status_overlap) are many and every one was
+    # re-run exactly (its records carry CPR_ST_EXACT_RERUN)
     cfg, keep = _cfg(alpha=0.45, gamma=gamma, policy=L.ETH_POLICY_FN19,
-                     reward_scheme=L.REWARD_CONSTANT, max_steps=2016, seed=0x5EED0000)
+                     reward_scheme=L.REWARD_CONSTANT, max_steps=2016, seed=0x5EED0000,
+                     propagation_delay=prop)
     b = device.Batch(cfg, keep=keep)
-    n = 2048
-    s_win = b.run(n, first_episode=0)
+    n = 2048 if prop < 1e-3 else 256
+    s_win, rec = b.run(n, first_episode=0, records=True)
     monkeypatch.setenv("CPR_ETH_WINDOW", "0")
     s_ev = b.run(n, first_episode=0)
     for f in L.Summary.FIELDS:
-        if f == "status_tie":  # the event engine has no tie bit; the window lane marks replays
+        if f in ROUTE_FIELDS:
             continue
         assert getattr(s_win, f) == getattr(s_ev, f), f
     assert list(s_win.hist) == list(s_ev.hist)
+    assert s_ev.status_tie == 0 and s_ev.status_overlap == 0
+    handed = int(((rec["status"] & L.ST_OVERLAP) != 0).sum())
+    assert s_win.status_overlap == handed
+    assert ((rec["status"][(rec["status"] & L.ST_OVERLAP) != 0] & L.ST_EXACT_RERUN) != 0).all()
+    if prop > 1e-3:
+        assert handed > n // 4
+
+
+def test_eth_long_episodes_stay_on_the_event_engine(ctx):
+    # episodes longer than the window lane's block ring (2^15) go to the event engine, whose
+    # ring wraps, instead of ending in a hand-back and a one-lane exact re-run each
+    # (capi.hip eth_window_ok); every record equals the oracle's
+    cfg, keep = _cfg(alpha=0.35, gamma=0.5, policy=L.ETH_POLICY_FN19,
+                     reward_scheme=L.REWARD_CONSTANT, max_steps=33000, seed=0xE7E72000)
+    s, rec, ok = _compare(cfg, keep, 32)
+    assert not (rec["status"] & (L.ST_EXACT_RERUN | L.ST_OVERLAP)).any()
+    assert (rec["n_steps"] == 33000).all() and s.status_overlap == 0
