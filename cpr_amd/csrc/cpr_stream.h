@@ -186,6 +186,14 @@ struct Stream {
     *miner_out = (uint64_t)w.w0 < t_att ? 0 : 1 + (int32_t)(((uint64_t)w.w1 * (uint64_t)d) >> 32);
     return (-1.0 * ev) * cpr_log(u53(w.w2, w.w3));
   }
+  // activation j's miner and its clock uniform as the 53-bit integer U (u53 = U * 2^-53),
+  // without the log: for lanes that read the clock only in rare windows (NakLane LZ)
+  __host__ __device__ inline uint64_t act_u(uint32_t j, uint64_t t_att, int32_t d,
+                                            int32_t* miner_out) const {
+    const Words4 w = block(j, TAG_ACT);
+    *miner_out = (uint64_t)w.w0 < t_att ? 0 : 1 + (int32_t)(((uint64_t)w.w1 * (uint64_t)d) >> 32);
+    return ((uint64_t)(w.w2 >> 5) << 26) | (uint64_t)(w.w3 >> 6);
+  }
   __host__ __device__ inline int32_t pow(uint32_t serial) const {
     return (int32_t)(block(serial, TAG_POW).w0 & 0x3FFFFFFFu);
   }

@@ -182,6 +182,17 @@ size_t eth_slot_bytes();
 // queue entries (launch << 40) | (episode index << 8) | lane status bits; one RerunLaunch
 // per episode-kernel launch tells the re-run kernel where that launch's draws come from and
 // where its records and summary go.
+// A launcher whose translation unit lays a lane's region out larger than the region the
+// library allocated refuses the launch (hipErrorInvalidValue) instead of running lanes past
+// their regions. The two can only disagree in a partial rebuild: round 4's illegal memory
+// access (gpurun_out/r04o_libs.log, k_bk_rollout) came from an A/B library that rebuilt
+// kernels_bk.hip with a larger vote-record array (vn: 4 -> 16 bytes per slot) but linked
+// the default capi.hip, which sized every lane's region by the old bk_lane_bytes
+#define CPR_LAYOUT_GUARD(have, need)                  \
+  do {                                                \
+    if ((int64_t)(have) < (int64_t)(need)) return hipErrorInvalidValue; \
+  } while (0)
+
 constexpr int64_t kRerunQueue = 1 << 22;       // queue entries per context
 constexpr size_t kRerunMaxLaunches = 1 << 20;  // launches per flush (< 2^23)
 

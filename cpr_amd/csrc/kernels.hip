@@ -35,22 +35,24 @@ __device__ inline void acc_add(LdsAcc& a, const BRef& hd, int64_t steps, int64_t
 
 // One gym episode (engine.ml:164-249): reset = first activation up to the attacker's
 // interaction; step = apply, deliveries, next activation, observe; head at the end.
-template <int POL, int TT, class St>
+// LZ: the lazy clock (NakLane::lazy_overlap_check), launched only when the host's
+// lazy_clock_ok holds and only max_steps ends the episode
+template <int POL, int TT, class St, bool LZ = false>
 __device__ inline CPR_AI BRef run_gym(NakLane& L, const NakParams& P, const St& S, const LaneMem& M,
                                int64_t* steps_out) {
   L.init();
-  L.activate(P, S, M);
+  L.activate<St, LZ>(P, S, M);
   const bool check_prog = P.max_progress < __builtin_inf();
   int64_t steps = 0;
-  if (!check_prog && !(P.max_time < __builtin_inf())) {
+  if (LZ || (!check_prog && !(P.max_time < __builtin_inf()))) {
     // only max_steps ends the episode: the trip count is the same in every lane of the
     // wave, so the loop exit is uniform and no lane state is merged at a divergent exit
     do {
-      const NakLane::Draw dr = L.draw(P, S);
+      const NakLane::Draw dr = L.draw<St, LZ>(P, S);
       L.apply(L.policy_action<POL>(P));
       L.resolve<St, POL >= 0 ? 0 : -1, TT>(P, S, M);
       if constexpr (TT == 2) enqueue_race(L, M);
-      L.activate(P, S, M, dr);
+      L.activate<St, LZ>(P, S, M, dr);
       ++steps;
       // the lanes of the wave verify together once the wave's list is nearly full
       if constexpr (TT == 2) {
@@ -104,7 +106,8 @@ constexpr uint32_t kInexact = ST_OVERLAP | ST_DEEP_FORK | ST_TIE_UNRESOLVED | ST
 // 2 = as 1, and the races are deferred and verified in batches (verify_races; REC = 0 only:
 // the race lists take the LDS ring); an episode a race went otherwise in is listed in
 // `list` (count, then episode indices) for the eager second pass (ListSource, TT = 1)
-template <int MODE, class Src, int POL, int REC = 1, int ARR = -1, int TT = 0>
+// LZ: lazy clock (REC = 0, ARR = 0 only; NakLane::lazy_overlap_check)
+template <int MODE, class Src, int POL, int REC = 1, int ARR = -1, int TT = 0, int LZ = 0>
 #ifndef CPR_G0_WAVES
 #define CPR_G0_WAVES 8  // the gamma = 0 kernel: 61 VGPRs fit 8 waves/SIMD (7 unasked)
 #endif
@@ -118,6 +121,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ARR == 0
     uint8_t* ovf) {
   // the race lists take the LDS ring, which only the summary-only kernels leave free
   static_assert(TT != 2 || REC == 0, "deferred races need the summary-only kernel");
+  static_assert(!LZ || (REC == 0 && ARR == 0 && MODE == CPR_MODE_GYM),
+                "the lazy clock is for the summary-only gamma = 0 gym kernel");
   if (ARR >= 0) P.arrive = ARR;
   if (TT) P.d = 2;  // launched for two defenders only (gym_run_fn): masks and loops fold
   __shared__ int32_t hist[CPR_HIST_BINS];
@@ -161,7 +166,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ARR == 0
   for (int64_t e = tid; e < n_run; e += nthreads) {
     const auto S = src.at(e);
     int64_t steps = 0;
-    const BRef hd = MODE == CPR_MODE_GYM ? run_gym<POL, TT>(L, P, S, M, &steps)
+    const BRef hd = MODE == CPR_MODE_GYM ? run_gym<POL, TT, decltype(S), LZ != 0>(L, P, S, M, &steps)
                                          : run_loop<POL>(L, P, S, M, activations);
     if constexpr (TT == 2) {
       if (L.status & ST_RACE_REDO) {
@@ -480,6 +485,9 @@ using RunFn = void (*)(NakParams, SeedSource, int64_t, int64_t, double*, uint8_t
 #ifndef CPR_DEFER_RACES
 #define CPR_DEFER_RACES 1
 #endif
+#ifndef CPR_LAZY_CLOCK  // 0: the gamma = 0 summary kernel draws every clock (A/B runs)
+#define CPR_LAZY_CLOCK 1
+#endif
 static bool deferred_races_ok(const NakParams& P) {
   return CPR_DEFER_RACES && P.dmax <= P.delta && P.cap <= 4096;
 }
@@ -489,6 +497,8 @@ using ListFn = void (*)(NakParams, ListSource, int64_t, int64_t, double*, uint8_
 template <int POL>
 static RunFn gym_run_fn(const NakParams& P, bool recs, bool defer, ListFn* second) {
   if (recs) return k_run_episodes<CPR_MODE_GYM, SeedSource, POL, 1, -1>;
+  if (!P.arrive && lazy_clock_ok(P) && CPR_LAZY_CLOCK)
+    return k_run_episodes<CPR_MODE_GYM, SeedSource, POL, 0, 0, 0, 1>;
   if (!P.arrive) return k_run_episodes<CPR_MODE_GYM, SeedSource, POL, 0, 0>;
   if (P.d != 2) return k_run_episodes<CPR_MODE_GYM, SeedSource, POL, 0, 1>;
   if (!defer) return k_run_episodes<CPR_MODE_GYM, SeedSource, POL, 0, 1, 1>;
@@ -509,7 +519,7 @@ static RunFn run_fn(const NakParams& P, int32_t mode, bool recs, bool defer = fa
   }
 }
 
-hipError_t launch_run_episodes(const NakParams& P, uint64_t seed, uint64_t first, int64_t n_eps,
+hipError_t launch_run_episodes(const NakParams& P0, uint64_t seed, uint64_t first, int64_t n_eps,
                                int32_t mode, int64_t activations, double* spill,
                                uint8_t* replay, int64_t* list, int64_t lanes,
                                cpr_episode_record* recs, cpr_summary* sum, int64_t* redo,
@@ -518,8 +528,10 @@ hipError_t launch_run_episodes(const NakParams& P, uint64_t seed, uint64_t first
   const unsigned blocks = (unsigned)(lanes / kBlock);
   const SeedSource src{seed, first};
   ListFn second = nullptr;
-  const RunFn fn = run_fn(P, mode, recs != nullptr, list != nullptr && deferred_races_ok(P),
+  const RunFn fn = run_fn(P0, mode, recs != nullptr, list != nullptr && deferred_races_ok(P0),
                           &second);
+  NakParams P = P0;
+  P.u_lazy = lazy_clock_ok(P0) ? lazy_threshold(P0) : 0ull;
   // deferred races: `list` (1 + n_eps words) receives the episodes for the eager second
   // pass, its count first
   if (second) {

@@ -673,6 +673,7 @@ hipError_t launch_bk_run_episodes(const bk::BkParams& P, uint64_t seed, uint64_t
                                   int64_t n_eps, uint8_t* mem, int64_t lane_bytes, int64_t lanes,
                                   cpr_episode_record* recs, cpr_summary* sum, hipStream_t st,
                                   const NodeOut& no) {
+  CPR_LAYOUT_GUARD(lane_bytes, bk::bk_lane_bytes(P));
   const unsigned blocks = (unsigned)(lanes / kBlock);
   const EvSlab sl = ev_slab_plan(blocks, (const void*)k_bk_run_episodes<SeedSource>, P.n);
   hipLaunchKernelGGL(k_bk_run_episodes<SeedSource>, dim3(blocks), dim3(kBlock), sl.bytes, st, P,
@@ -685,6 +686,7 @@ hipError_t launch_bk_replay_episodes(const bk::BkParams& P, const TraceSource& s
                                  uint8_t* mem, int64_t lane_bytes, int64_t lanes,
                                  cpr_episode_record* recs, cpr_summary* sum, hipStream_t st,
                                   const NodeOut& no) {
+  CPR_LAYOUT_GUARD(lane_bytes, bk::bk_lane_bytes(P));
   const unsigned blocks = (unsigned)(lanes / kBlock);
   const EvSlab sl = ev_slab_plan(blocks, (const void*)k_bk_run_episodes<TraceSource>, P.n);
   hipLaunchKernelGGL(k_bk_run_episodes<TraceSource>, dim3(blocks), dim3(kBlock), sl.bytes, st, P,
@@ -696,6 +698,7 @@ hipError_t launch_bk_reset(const bk::BkParams& P, uint64_t seed, uint8_t* mem, i
                            void* slots, int64_t n, const uint8_t* mask, const uint64_t* eps,
                            int unit, const double* tabs, int32_t tn, double* obs,
                            hipStream_t st) {
+  CPR_LAYOUT_GUARD(lane_bytes, bk::bk_lane_bytes(P));
   hipLaunchKernelGGL(k_bk_reset, dim3(grid_of(n)), dim3(kBlock), 0, st, P, seed, mem, lane_bytes,
                      (BkSlot*)slots, n, mask, eps, unit, tabs, tn, obs);
   return hipGetLastError();
@@ -704,6 +707,7 @@ hipError_t launch_bk_reset(const bk::BkParams& P, uint64_t seed, uint8_t* mem, i
 hipError_t launch_bk_step(const bk::BkParams& P, uint64_t seed, uint8_t* mem, int64_t lane_bytes,
                           void* slots, int64_t n, const int32_t* actions, int unit,
                           const double* tabs, int32_t tn, const StepBuffers& b, hipStream_t st) {
+  CPR_LAYOUT_GUARD(lane_bytes, bk::bk_lane_bytes(P));
   hipLaunchKernelGGL(k_bk_step, dim3(grid_of(n)), dim3(kBlock), 0, st, P, seed, mem, lane_bytes,
                      (BkSlot*)slots, n, actions, unit, tabs, tn, b);
   return hipGetLastError();
@@ -713,6 +717,7 @@ hipError_t launch_bk_rollout(const bk::BkParams& P, uint64_t seed, uint8_t* mem,
                              int64_t lane_bytes, void* slots, int64_t n, int64_t n_steps,
                              int unit, const double* tabs, int32_t tn, double* obs,
                              double* reward, uint8_t* done, cpr_summary* sum, hipStream_t st) {
+  CPR_LAYOUT_GUARD(lane_bytes, bk::bk_lane_bytes(P));
   const int32_t lpw = rollout_lanes_per_wave(n, (const void*)k_bk_rollout);
   const int64_t per_block = (int64_t)(kBlock / 64) * lpw;
   const unsigned blocks = (unsigned)((n + per_block - 1) / per_block);
@@ -725,6 +730,7 @@ hipError_t launch_bk_rollout(const bk::BkParams& P, uint64_t seed, uint8_t* mem,
 
 hipError_t launch_bk_observe_fields(const bk::BkParams& P, uint8_t* mem, int64_t lane_bytes,
                                     const void* slots, int64_t n, int32_t* f, hipStream_t st) {
+  CPR_LAYOUT_GUARD(lane_bytes, bk::bk_lane_bytes(P));
   hipLaunchKernelGGL(k_bk_observe_fields, dim3(grid_of(n)), dim3(kBlock), 0, st, P, mem,
                      lane_bytes, (const BkSlot*)slots, n, f);
   return hipGetLastError();

@@ -234,6 +234,7 @@ hipError_t launch_eth_win_episodes(const eth::EthParams& P, uint64_t seed, uint6
                                    int64_t lanes, cpr_episode_record* recs, cpr_summary* sum,
                                    int64_t* redo, uint32_t* redo_n, uint32_t launch_id,
                                    int64_t redo_cap, uint8_t* ovf, hipStream_t st) {
+  CPR_LAYOUT_GUARD(lane_bytes, ethw::win_lane_bytes(P.cap_b));
   hipLaunchKernelGGL(eth_win_fn(recs != nullptr), dim3((unsigned)(lanes / kBlock)), dim3(kBlock),
                      0, st, P, SeedSource{seed, first}, n_eps, mem, lane_bytes, recs, sum, redo,
                      redo_n, launch_id, redo_cap, ovf);
@@ -482,6 +483,7 @@ hipError_t launch_eth_run_episodes(const eth::EthParams& P, uint64_t seed, uint6
                                    int64_t n_eps, uint8_t* mem, int64_t lane_bytes,
                                    int64_t lanes, cpr_episode_record* recs, cpr_summary* sum,
                                    hipStream_t st, const NodeOut& no) {
+  CPR_LAYOUT_GUARD(lane_bytes, eth::eth_lane_bytes(P.cap_b, P.cap_e, P.n));
   const unsigned blocks = (unsigned)(lanes / kBlock);
   hipLaunchKernelGGL(k_eth_run_episodes<SeedSource>, dim3(blocks), dim3(kBlock), 0, st, P,
                      SeedSource{seed, first}, n_eps, mem, lane_bytes, recs, sum, no);
@@ -492,6 +494,7 @@ hipError_t launch_eth_replay_episodes(const eth::EthParams& P, const TraceSource
                                  uint8_t* mem, int64_t lane_bytes, int64_t lanes,
                                  cpr_episode_record* recs, cpr_summary* sum, hipStream_t st,
                                  const NodeOut& no) {
+  CPR_LAYOUT_GUARD(lane_bytes, eth::eth_lane_bytes(P.cap_b, P.cap_e, P.n));
   hipLaunchKernelGGL(k_eth_run_episodes<TraceSource>, dim3((unsigned)(lanes / kBlock)),
                      dim3(kBlock), 0, st, P, src, n_eps, mem, lane_bytes, recs, sum, no);
   return hipGetLastError();
@@ -714,6 +717,7 @@ hipError_t launch_eth_reset(const eth::EthParams& P, uint64_t seed, uint8_t* mem
                             int64_t lane_bytes, void* slots, int64_t n, const uint8_t* mask,
                             const uint64_t* eps, int unit, const double* tabs, int32_t tn,
                             double* obs, hipStream_t st) {
+  CPR_LAYOUT_GUARD(lane_bytes, eth::eth_lane_bytes(P.cap_b, P.cap_e, P.n));
   hipLaunchKernelGGL(k_eth_reset, dim3(eth_grid_of(n)), dim3(kBlock), 0, st, P, seed, mem,
                      lane_bytes, (EthSlot*)slots, n, mask, eps, unit, tabs, tn, obs);
   return hipGetLastError();
@@ -723,6 +727,7 @@ hipError_t launch_eth_step(const eth::EthParams& P, uint64_t seed, uint8_t* mem,
                            int64_t lane_bytes, void* slots, int64_t n, const int32_t* actions,
                            int unit, const double* tabs, int32_t tn, const StepBuffers& b,
                            hipStream_t st) {
+  CPR_LAYOUT_GUARD(lane_bytes, eth::eth_lane_bytes(P.cap_b, P.cap_e, P.n));
   hipLaunchKernelGGL(k_eth_step, dim3(eth_grid_of(n)), dim3(kBlock), 0, st, P, seed, mem,
                      lane_bytes, (EthSlot*)slots, n, actions, unit, tabs, tn, b);
   return hipGetLastError();
@@ -732,6 +737,7 @@ hipError_t launch_eth_rollout(const eth::EthParams& P, uint64_t seed, uint8_t* m
                               int64_t lane_bytes, void* slots, int64_t n, int64_t n_steps,
                               int unit, const double* tabs, int32_t tn, double* obs,
                               double* reward, uint8_t* done, cpr_summary* sum, hipStream_t st) {
+  CPR_LAYOUT_GUARD(lane_bytes, eth::eth_lane_bytes(P.cap_b, P.cap_e, P.n));
   hipLaunchKernelGGL(k_eth_rollout, dim3(eth_grid_of(n)), dim3(kBlock), 0, st, P, seed, mem,
                      lane_bytes, (EthSlot*)slots, n, n_steps, unit, tabs, tn, obs, reward, done,
                      sum);
@@ -740,6 +746,7 @@ hipError_t launch_eth_rollout(const eth::EthParams& P, uint64_t seed, uint8_t* m
 
 hipError_t launch_eth_observe_fields(const eth::EthParams& P, uint8_t* mem, int64_t lane_bytes,
                                      const void* slots, int64_t n, int32_t* f, hipStream_t st) {
+  CPR_LAYOUT_GUARD(lane_bytes, eth::eth_lane_bytes(P.cap_b, P.cap_e, P.n));
   hipLaunchKernelGGL(k_eth_observe_fields, dim3(eth_grid_of(n)), dim3(kBlock), 0, st, P, mem,
                      lane_bytes, (const EthSlot*)slots, n, f);
   return hipGetLastError();

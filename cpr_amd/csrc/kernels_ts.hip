@@ -513,6 +513,7 @@ hipError_t launch_ts_run_episodes(const ts::TsParams& P, uint64_t seed, uint64_t
                                   int64_t n_eps, uint8_t* mem, int64_t lane_bytes, int64_t lanes,
                                   cpr_episode_record* recs, cpr_summary* sum, hipStream_t st,
                                   const NodeOut& no) {
+  CPR_LAYOUT_GUARD(lane_bytes, ts::ts_lane_bytes(P));
   // the resident grid; lpw < 64 runs lanes * lpw / 64 episodes at a time in it
   const int32_t lpw = event_lanes_per_wave();
   const unsigned blocks = (unsigned)(lanes / kBlock);
@@ -528,6 +529,7 @@ hipError_t launch_ts_replay_episodes(const ts::TsParams& P, const TraceSource& s
                                  uint8_t* mem, int64_t lane_bytes, int64_t lanes,
                                  cpr_episode_record* recs, cpr_summary* sum, hipStream_t st,
                                   const NodeOut& no) {
+  CPR_LAYOUT_GUARD(lane_bytes, ts::ts_lane_bytes(P));
   // the resident grid; lpw < 64 runs lanes * lpw / 64 episodes at a time in it
   const int32_t lpw = event_lanes_per_wave();
   const unsigned blocks = (unsigned)(lanes / kBlock);
@@ -542,6 +544,7 @@ hipError_t launch_ts_reset(const ts::TsParams& P, uint64_t seed, uint8_t* mem, i
                            void* slots, int64_t n, const uint8_t* mask, const uint64_t* eps,
                            int unit, const double* tabs, int32_t tn, double* obs,
                            hipStream_t st) {
+  CPR_LAYOUT_GUARD(lane_bytes, ts::ts_lane_bytes(P));
   hipLaunchKernelGGL(k_ts_reset, dim3(ts_grid(n)), dim3(kBlock), 0, st, P, seed, mem, lane_bytes,
                      (TsSlot*)slots, n, mask, eps, unit, tabs, tn, obs);
   return hipGetLastError();
@@ -550,6 +553,7 @@ hipError_t launch_ts_reset(const ts::TsParams& P, uint64_t seed, uint8_t* mem, i
 hipError_t launch_ts_step(const ts::TsParams& P, uint64_t seed, uint8_t* mem, int64_t lane_bytes,
                           void* slots, int64_t n, const int32_t* actions, int unit,
                           const double* tabs, int32_t tn, const StepBuffers& b, hipStream_t st) {
+  CPR_LAYOUT_GUARD(lane_bytes, ts::ts_lane_bytes(P));
   hipLaunchKernelGGL(k_ts_step, dim3(ts_grid(n)), dim3(kBlock), 0, st, P, seed, mem, lane_bytes,
                      (TsSlot*)slots, n, actions, unit, tabs, tn, b);
   return hipGetLastError();
@@ -559,6 +563,7 @@ hipError_t launch_ts_rollout(const ts::TsParams& P, uint64_t seed, uint8_t* mem,
                              int64_t lane_bytes, void* slots, int64_t n, int64_t n_steps,
                              int unit, const double* tabs, int32_t tn, double* obs,
                              double* reward, uint8_t* done, cpr_summary* sum, hipStream_t st) {
+  CPR_LAYOUT_GUARD(lane_bytes, ts::ts_lane_bytes(P));
   const int32_t lpw = rollout_lanes_per_wave(n, (const void*)k_ts_rollout);
   const int64_t per_block = (int64_t)(kBlock / 64) * lpw;
   const unsigned blocks = (unsigned)((n + per_block - 1) / per_block);
@@ -571,6 +576,7 @@ hipError_t launch_ts_rollout(const ts::TsParams& P, uint64_t seed, uint8_t* mem,
 
 hipError_t launch_ts_observe_fields(const ts::TsParams& P, uint8_t* mem, int64_t lane_bytes,
                                     const void* slots, int64_t n, int32_t* f, hipStream_t st) {
+  CPR_LAYOUT_GUARD(lane_bytes, ts::ts_lane_bytes(P));
   hipLaunchKernelGGL(k_ts_observe_fields, dim3(ts_grid(n)), dim3(kBlock), 0, st, P, mem,
                      lane_bytes, (const TsSlot*)slots, n, f);
   return hipGetLastError();

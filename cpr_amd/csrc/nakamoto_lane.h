@@ -161,7 +161,27 @@ struct NakParams {
   int32_t cap;          // spill slots per lane
   int32_t abstract_g;   // CPR_NET_ABSTRACT_GAMMA: match races decided by per-defender coins
   double gamma;         //   U(k, 0, j) < gamma (zero delays otherwise)
+  // lazy clock (NakLane LZ): a clock uniform U (53-bit integer) below u_lazy draws a delay
+  // > 2 delta, which no later window can overlap (set by the launcher, lazy_clock_ok)
+  uint64_t u_lazy;
 };
+
+// the lazy clock (NakLane LZ) is exact when a delay above 2 delta cannot overlap anywhere in
+// the episode: ulp(t) <= delta / 4 for every reachable clock t (each delay is at most
+// 53 ln 2 ev < 40 ev, or +inf, which the lane handles apart), and max_steps alone ends it
+inline bool lazy_clock_ok(const NakParams& P) {
+  if (!(P.delta > 0.0) || !std::isfinite(P.delta) || !(P.ev > 0.0) || !std::isfinite(P.ev))
+    return false;
+  if (P.max_progress < __builtin_inf() || P.max_time < __builtin_inf()) return false;
+  if (P.max_steps <= 0 || P.max_steps > (1ll << 30)) return false;
+  const double tmax = ((double)P.max_steps + 2.0) * P.ev * 40.0;
+  return std::ldexp(1.0, std::ilogb(tmax) - 52) <= P.delta / 4.0;
+}
+// u_lazy = floor(exp(-2.5 delta / ev) 2^53): U < u_lazy gives dt > 2 delta with margin to
+// spare for the log's rounding
+inline uint64_t lazy_threshold(const NakParams& P) {
+  return (uint64_t)std::floor(std::exp(-2.5 * P.delta / P.ev) * 9007199254740992.0);
+}
 
 __host__ __device__ inline CPR_AI uint64_t all_mask(int32_t d) {
   return d >= 64 ? ~0ull : ((1ull << d) - 1ull);
@@ -444,6 +464,7 @@ struct NakLane {
   int32_t qn;        // deferred races in the wave's list (TT = 2; the same in every lane)
   uint32_t rw;       // the race resolve<.., 2> took as decided: wminer | rlo << 2 |
                      // rhi << 14, 0 = none (enqueue_race lists it)
+  int32_t tinf;      // LZ: a clock delay of +inf was drawn (the clock is +inf from then on)
 
   __host__ __device__ inline CPR_AI double chain_t(const LaneMem& M, int32_t m) const {
     if (!M.times) return 0.0;
@@ -476,7 +497,7 @@ struct NakLane {
     k = 0; n = 0; rel = 0; n_ba = 0; pend = -1; wminer = 0; event = 0;
     rlo = 1; rhi = 0; status = 0u; onA = 0ull; lca_da = 0;
     w_hasb = 0; w_bound = -__builtin_inf();
-    qn = 0; rw = 0u;
+    qn = 0; rw = 0u; tinf = 0;
   }
 
   // the lane's state without block times (the summary-only kernels' whole state) as
@@ -517,37 +538,79 @@ struct NakLane {
   struct Draw {
     double dt;
     int32_t miner;
+    uint64_t u;  // LZ: the clock uniform as a 53-bit integer (dt not computed)
   };
   // the next activation's miner and clock delay: they depend on the activation count only,
   // so the gym loop draws them first and the Philox / log chain overlaps the policy and
   // apply selects of the same iteration
-  template <class St>
+  template <class St, bool LZ = false>
   __host__ __device__ inline CPR_AI Draw draw(const NakParams& P, const St& S) const {
-    return draw_at(P, S, k);
+    return draw_at<St, LZ>(P, S, k);
   }
   // the draws of activation kk (kk = k: the next one)
-  template <class St>
+  template <class St, bool LZ = false>
   __host__ __device__ inline CPR_AI Draw draw_at(const NakParams& P, const St& S,
                                                  int32_t kk) const {
     Draw d;
-    d.dt = S.act((uint32_t)kk, P.t_att, P.d, P.ev, &d.miner);
+    if constexpr (LZ) {
+      d.u = S.act_u((uint32_t)kk, P.t_att, P.d, &d.miner);
+      d.dt = 0.0;
+    } else {
+      d.u = 0;
+      d.dt = S.act((uint32_t)kk, P.t_att, P.d, P.ev, &d.miner);
+    }
     return d;
   }
 
+  // LZ = lazy clock, for the summary-only gamma = 0 kernel (no arrivals, no records): there
+  // the clock feeds nothing but the overlap check, which can fire only when the previous
+  // window delivered a defender block at t + delta and the new activation comes no later,
+  // fl(t + dt) <= fl(t + delta). A uniform below P.u_lazy draws dt > 2 delta, which (with
+  // the launcher's bound ulp(t) <= delta / 4 over the whole episode) rules that out without
+  // the log, so the clock is neither drawn nor summed. Only the rest, ~2.5 delta / ev of
+  // activations, takes this branch: it sums the clock from the episode's first draw in the
+  // same order as the eager lane and makes the same comparison, so the status bits (and the
+  // exact re-run an overlap sends the episode to) are the eager lane's. tinf: a zero uniform
+  // (delay +inf) leaves the eager lane's clock at +inf, where every later defender window
+  // overlaps.
   template <class St>
-  __host__ __device__ inline CPR_AI void activate(const NakParams& P, const St& S, const LaneMem& M) {
-    activate(P, S, M, draw(P, S));
+  __host__ __device__ inline void lazy_overlap_check(const NakParams& P, const St& S,
+                                                     uint64_t u) {
+    const bool wb = w_hasb != 0 && P.d >= 2;
+    if (tinf) {
+      if (wb) status |= ST_OVERLAP;
+      return;
+    }
+    if (u == 0ull) {  // this activation's delay is +inf: t + inf > t + delta
+      tinf = 1;
+      return;
+    }
+    if (!wb) return;
+    double tp = 0.0;
+    for (int32_t j = 0; j < k; ++j) tp = tp + S.clock((uint32_t)j, P.ev);
+    const double tn = tp + S.clock((uint32_t)k, P.ev);
+    if (tn <= tp + P.delta) status |= ST_OVERLAP;
   }
 
-  template <class St>
+  template <class St, bool LZ = false>
+  __host__ __device__ inline CPR_AI void activate(const NakParams& P, const St& S, const LaneMem& M) {
+    activate<St, LZ>(P, S, M, draw<St, LZ>(P, S));
+  }
+
+  template <class St, bool LZ = false>
   __host__ __device__ inline CPR_AI void activate(const NakParams& P, const St& S, const LaneMem& M,
                                                   const Draw dr) {
     const int32_t miner = dr.miner;
     const double tn = t + dr.dt;
-    if (tn <= w_bound) {
-      if (tn <= window_last_arrival(P, S)) status |= ST_OVERLAP;
+    if constexpr (LZ) {
+      // u >= u_lazy, or u == 0 (unsigned wrap), or a +inf clock: the exact check
+      if ((dr.u - 1ull) >= (P.u_lazy - 1ull) || tinf) lazy_overlap_check(P, S, dr.u);
+    } else {
+      if (tn <= w_bound) {
+        if (tn <= window_last_arrival(P, S)) status |= ST_OVERLAP;
+      }
+      t = tn;
     }
-    t = tn;
     const int32_t ka = k;
     ++k;
     wminer = miner;

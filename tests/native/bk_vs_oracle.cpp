@@ -282,6 +282,12 @@ int main(int argc, char** argv) {
   for (int n : {2, 3, 10})
     for (double ev : {0.5, 2.0, 30.0, 600.0})
       for (int sch : {0, 2}) cfgs.push_back(Cfg{0, 0, n, 0, sch, steps * 2, 2, k, ev});
+  // episodes longer than the 4096-vertex window: the vertex ring, the vote-list links
+  // (vh / vn, indexed serial & (cap_v - 1)) and the visibility rows wrap around (the
+  // path of round 4's r04o fault investigation)
+  cfgs.push_back(Cfg{0.33, 0.5, 2, 1, 0, 6000, 0, k});
+  cfgs.push_back(Cfg{0.45, 0.0, 2, 5, 2, 6000, 0, k});
+  cfgs.push_back(Cfg{0.40, 0.9, 10, 6, 0, 6000, 0, k});
   // gym episodes ended by max_time / max_progress before max_steps (engine.ml:209-214)
   for (int pol : {1, 3, 5})
     for (double g : {0.0, 0.5}) {

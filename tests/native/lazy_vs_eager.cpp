@@ -1,0 +1,139 @@
+// TEST INFRASTRUCTURE ONLY. The lazy clock of the gamma = 0 summary-only kernel
+// (NakLane LZ, cpr_amd/csrc/nakamoto_lane.h lazy_overlap_check) against the eager lane,
+// host build: the same episodes with the same actions, and after every step the lanes'
+// state words (NakLane::pack without the clock and the window bound, which the lazy lane
+// does not keep) and status bits must be identical. Long propagation delays make the
+// lazy branch (U >= u_lazy) and real overlaps common; a stream with a zero clock uniform
+// at a chosen activation (delay +inf) checks the +inf clock.
+// usage: lazy_vs_eager [episodes per config] [steps]; one JSON line; exit 1 on mismatch
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#include "../../cpr_amd/csrc/nakamoto_lane.h"
+#include "../../oracle/src/keyed_stream.h"
+
+using namespace cpr;
+
+// the keyed stream with activation `zero_at`'s clock uniform forced to 0 (delay +inf)
+struct ZStream : Stream {
+  uint32_t zero_at = 0xffffffffu;
+  double act(uint32_t j, uint64_t t_att, int32_t d, double ev, int32_t* m) const {
+    const double dt = Stream::act(j, t_att, d, ev, m);
+    return j == zero_at ? (-1.0 * ev) * cpr_log(0.0) : dt;
+  }
+  double clock(uint32_t j, double ev) const {
+    return j == zero_at ? (-1.0 * ev) * cpr_log(0.0) : Stream::clock(j, ev);
+  }
+  uint64_t act_u(uint32_t j, uint64_t t_att, int32_t d, int32_t* m) const {
+    const uint64_t u = Stream::act_u(j, t_att, d, m);
+    return j == zero_at ? 0ull : u;
+  }
+};
+
+static uint32_t mix(uint64_t a, uint64_t b) {
+  uint64_t x = a * 0x9E3779B97F4A7C15ull ^ (b + 0x632BE59BD9B4E019ull);
+  x ^= x >> 31;
+  x *= 0xD6E8FEB86659FD93ull;
+  x ^= x >> 32;
+  return (uint32_t)x;
+}
+
+struct Counters {
+  long episodes = 0, mismatches = 0, slow = 0, overlaps = 0, inf_eps = 0;
+};
+
+// pack() without t (words 0, 1) and w_bound (the last two)
+static std::vector<uint32_t> words(const NakLane& L) {
+  std::vector<uint32_t> w(CK_WORDS);
+  L.pack(w.data());
+  return std::vector<uint32_t>(w.begin() + 2, w.end() - 2);
+}
+
+static bool episode(double alpha, int d, double delta, int policy, int steps, uint64_t ep,
+                    uint32_t zero_at, Counters& C) {
+  NakParams P{};
+  P.t_att = oracle::alpha_threshold(alpha);
+  P.d = d;
+  P.ev = 1.0;
+  P.delta = delta;
+  P.dmax = __builtin_inf();  // gamma = 0: attacker messages never arrive
+  P.arrive = 0;
+  P.max_steps = steps;
+  P.max_progress = __builtin_inf();
+  P.max_time = __builtin_inf();
+  P.policy = policy < 4 ? policy : 0;
+  P.cap = steps + 64;
+  if (!lazy_clock_ok(P)) {
+    fprintf(stderr, "lazy clock not applicable: delta %g\n", delta);
+    exit(2);
+  }
+  P.u_lazy = lazy_threshold(P);
+  std::vector<uint8_t> replay(REPLAY_BYTES);
+  LaneMem M{};
+  std::vector<double> ring(RING), spill(P.cap);
+  M.ring = ring.data();
+  M.spill = spill.data();
+  M.ring_stride = M.spill_stride = 1;
+  M.cap = P.cap;
+  M.replay = ReplayMem::at(replay.data());
+  M.times = false;  // the summary-only kernel
+  ZStream S;
+  S.k0 = 0x5eed0000u;
+  S.k1 = 0;
+  S.e0 = (uint32_t)ep;
+  S.e1 = (uint32_t)(ep >> 32);
+  S.zero_at = zero_at;
+  NakLane E, Z;
+  E.init();
+  Z.init();
+  E.activate(P, S, M);
+  Z.activate<ZStream, true>(P, S, M);
+  bool ok = words(E) == words(Z);
+  for (int s = 0; ok && s < steps; ++s) {
+    int32_t act;
+    if (policy < 4) {
+      act = E.policy_action(P);
+    } else {
+      act = (int32_t)(mix(ep, s) & 3u);
+    }
+    const NakLane::Draw de = E.draw(P, S);
+    const NakLane::Draw dz = Z.draw<ZStream, true>(P, S);
+    C.slow += ((dz.u - 1ull) >= (P.u_lazy - 1ull)) ? 1 : 0;
+    E.apply(act);
+    Z.apply(act);
+    E.resolve<ZStream, 0, 0>(P, S, M);
+    Z.resolve<ZStream, 0, 0>(P, S, M);
+    E.activate(P, S, M, de);
+    Z.activate<ZStream, true>(P, S, M, dz);
+    ok = words(E) == words(Z);
+    if (!ok)
+      fprintf(stderr, "MISMATCH alpha=%g d=%d delta=%g pol=%d ep=%llu zero_at=%u step %d: status eager %u lazy %u\n",
+              alpha, d, delta, policy, (unsigned long long)ep, zero_at, s, E.status, Z.status);
+  }
+  C.episodes++;
+  C.mismatches += ok ? 0 : 1;
+  C.overlaps += (E.status & ST_OVERLAP) ? 1 : 0;
+  C.inf_eps += zero_at < (uint32_t)steps ? 1 : 0;
+  return ok;
+}
+
+int main(int argc, char** argv) {
+  const int eps = argc > 1 ? atoi(argv[1]) : 40;
+  const int steps = argc > 2 ? atoi(argv[2]) : 400;
+  Counters C;
+  for (double delta : {1e-9, 1e-3, 0.05, 0.4})
+    for (int d : {2, 3, 10})
+      for (double a : {0.1, 0.33, 0.45})
+        for (int pol = 0; pol <= 4; ++pol)
+          for (int e = 0; e < eps; ++e) {
+            // every fifth episode draws a zero clock uniform (delay +inf) somewhere
+            const uint32_t z = (e % 5 == 4) ? mix(e, 7) % (uint32_t)steps : 0xffffffffu;
+            episode(a, d, delta, pol, steps, (uint64_t)e, z, C);
+          }
+  printf("{\"episodes\": %ld, \"mismatches\": %ld, \"lazy_branch_activations\": %ld, "
+         "\"overlap_episodes\": %ld, \"inf_clock_episodes\": %ld}\n",
+         C.episodes, C.mismatches, C.slow, C.overlaps, C.inf_eps);
+  return C.mismatches ? 1 : 0;
+}

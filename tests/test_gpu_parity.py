@@ -103,15 +103,18 @@ def test_tie_windows_replayed_exactly(ctx):
 
 
 @pytest.mark.parametrize("policy", [L.POLICY_EYAL_SIRER_2014, L.POLICY_SAPIRSHTEIN_2016_SM1])
-@pytest.mark.parametrize("gamma", [0.0, 0.5])
-def test_summary_only_kernels_equal_record_kernels(ctx, gamma, policy):
+@pytest.mark.parametrize("gamma,prop", [(0.0, 1e-9), (0.5, 1e-9), (0.0, 1e-5)])
+def test_summary_only_kernels_equal_record_kernels(ctx, gamma, prop, policy):
     # cpr_run_episodes without records runs the summary-only specialisations of
-    # k_run_episodes (no block-time bookkeeping; gamma = 0 compiled without arrivals; at
+    # k_run_episodes (no block-time bookkeeping; gamma = 0 compiled without arrivals and
+    # with the lazy clock, which draws no delay while the uniform rules out an overlap; at
     # d = 2 ties by the closed-form rule, a tie it does not cover re-run exactly); with
     # records, the general kernel (heap replay). Match-heavy play at the bench's sizes of
-    # episode: every summary field, ties included, must be identical.
+    # episode: every summary field, ties and overlaps included, must be identical. A 1e-5
+    # delay sends ~2.5e-5 of activations down the lazy clock's exact branch and makes
+    # overlaps (and their exact re-runs) ~1 % of episodes.
     cfg, keep = device.make_config(alpha=0.33, gamma=gamma, policy=policy, max_steps=2016,
-                                   seed=0x5A11)
+                                   seed=0x5A11, propagation_delay=prop)
     b = device.Batch(cfg, ctx=ctx, keep=keep)
     n = 65536
     s1, _ = b.run(n, first_episode=0, records=True)
@@ -121,6 +124,8 @@ def test_summary_only_kernels_equal_record_kernels(ctx, gamma, policy):
     assert list(s0.hist) == list(s1.hist)
     if gamma > 0:
         assert s1.status_tie > 0  # ties occurred and took the closed-form rule
+    if prop > 1e-6:
+        assert s1.status_overlap > n // 100  # the exact branch found real overlaps
 
 
 @pytest.mark.parametrize("n", [65536, 65536 + 37])

@@ -59,6 +59,21 @@ def test_deferred_races_equal_eager():
     assert out["wave_mismatches"] == 0 and out["wave_episodes"] == 2560
 
 
+def test_lazy_clock_equals_eager():
+    # tests/native/lazy_vs_eager.cpp: the gamma = 0 summary-only kernel's lazy clock
+    # (NakLane LZ: no log while the uniform rules out an overlap) against the eager lane,
+    # word for word after every step, status bits included; long delays make the exact
+    # branch and real overlaps common, and some episodes draw a +inf clock delay
+    subprocess.run(["make", "-s", "-C", str(ROOT / "tests" / "native")], check=True)
+    p = subprocess.run([str(ROOT / "tests" / "native" / "build" / "lazy_vs_eager"), "20", "400"],
+                       capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stderr[-2000:]
+    out = json.loads(p.stdout.strip().splitlines()[-1])
+    assert out["mismatches"] == 0 and out["episodes"] == 3600
+    assert out["lazy_branch_activations"] > 100000 and out["overlap_episodes"] > 1000
+    assert out["inf_clock_episodes"] == 720
+
+
 def test_ethereum_lane_matches_oracle_fuzz():
     # tests/native/eth_vs_oracle.cpp: cpr_amd/csrc/ethereum_lane.h (host build) vs the
     # oracle's ethereum.cpp, every step: 10 observation fields incl. the three dry-run
