@@ -188,7 +188,11 @@ def run_other_configs(ctx, cpu_seconds, with_cpu, pmc, keys=None):
         acts = steps = episodes = invalid = 0
         wall = kms = 0.0
         lanes_l, res_l, point_ms = [], [], []
+        # per point: episodes handed to the exact re-run (Ethereum window-lane hand-backs,
+        # Nakamoto overlaps) and the re-run kernels' ms, beside the point's status counts
+        pt_reruns, pt_rerun_ms, pt_overlap, pt_tie = [], [], [], []
         for pt in points:
+            r0 = ctx.rerun_stats()
             cfg, keep = device.make_config(seed=SEED, **pt)
             b = device.Batch(cfg, ctx=ctx, keep=keep)
             n = eps
@@ -220,6 +224,11 @@ def run_other_configs(ctx, cpu_seconds, with_cpu, pmc, keys=None):
             ln, res = b.launch_shape()
             lanes_l.append(ln)
             res_l.append(res)
+            r1 = ctx.rerun_stats()
+            pt_reruns.append(r1[0] - r0[0])
+            pt_rerun_ms.append(round(r1[2] - r0[2], 3))
+            pt_overlap.append(int(s.status_overlap))
+            pt_tie.append(int(s.status_tie))
             acts += int(s.activations)
             steps += int(s.steps)
             episodes += int(s.episodes)
@@ -235,6 +244,10 @@ def run_other_configs(ctx, cpu_seconds, with_cpu, pmc, keys=None):
             "activations_per_s": acts / wall,
             "kernel_ms": kms,
             "kernel_ms_per_point": point_ms,
+            "exact_reruns_per_point": pt_reruns,
+            "exact_rerun_ms_per_point": pt_rerun_ms,
+            "status_overlap_per_point": pt_overlap,
+            "status_tie_per_point": pt_tie,
             "kernel_activations_per_s": kact,
             "lanes_per_launch": lanes_l[0],
             "resident_lanes": res_l[0],
@@ -460,6 +473,7 @@ def main():
     for w in range(args.warmup):
         one_step(10**6 + w, new_sums())
     ctx.synchronize()
+    rr0 = ctx.rerun_stats()
     sums_dev = new_sums()
     parallel.barrier(cdev)
     torch.cuda.synchronize()
@@ -470,6 +484,7 @@ def main():
     torch.cuda.synchronize()
     parallel.barrier(cdev)
     dt = parallel.allreduce_max(time.perf_counter() - t0, cdev)
+    rr1 = ctx.rerun_stats()  # this rank's exact re-runs of the timed region
     sums = read(sums_dev)
     totals = parallel.allreduce_summaries(sums, cdev)  # one packed collective
     acts = sum(int(s.activations) for s in totals)
@@ -558,7 +573,12 @@ def main():
                                         for (a, g), m in zip(points, kms)},
                 "kernel_activations_per_s": act_per_s_kernel,
             },
-            "status": {"tie_episodes": ties, "overlap_episodes": overlaps, "other": other},
+            "status": {"tie_episodes": ties, "overlap_episodes": overlaps, "other": other,
+                       # rank 0's timed region: episodes re-run exactly, and those kernels'
+                       # ms on the context's stream (they overlap the sweep's launches)
+                       "exact_reruns_rank0": rr1[0] - rr0[0],
+                       "exact_rerun_flushes_rank0": rr1[1] - rr0[1],
+                       "exact_rerun_ms_rank0": round(rr1[2] - rr0[2], 3)},
             "sweep_mean_rel_revenue": sweep,
             "abstract_gamma_1": {
                 "mode": "FLAGGED abstract-gamma (CPR_NET_ABSTRACT_GAMMA): not the reference's "

@@ -69,6 +69,16 @@ struct cpr_ctx {
   // launch: rq = [kRerunQueue] int64 entries + a uint32 counter; one RerunLaunch per
   // episode-kernel launch since then
   DevBuf rq, rtab, rmem;
+  // cpr_rerun_stats: per flush, HIP events around the re-run kernels and the count of
+  // episodes the launches since the previous flush queued (copied to pinned host memory
+  // before the counter is cleared); summed when the caller asks
+  struct FlushRec {
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    uint32_t* cnt = nullptr;  // pinned host word
+  };
+  std::vector<FlushRec> fl_pending, fl_free;
+  int64_t rr_episodes = 0, rr_flushes = 0;
+  double rr_ms = 0.0;
   std::vector<RerunLaunch> rlaunch, rlaunch_up;
   // entries a launch may append (kRerunQueue; CPR_RERUN_QUEUE_CAP lowers it for tests);
   // an episode that finds the queue full waits in its launch's overflow flags: one byte
@@ -189,6 +199,12 @@ int cpr_ctx_destroy(cpr_ctx* c) {
   // pending work first: queued exact re-runs complete their callers' summaries and records
   (void)flush_reruns(c);
   (void)hipStreamSynchronize(c->stream);
+  for (auto* v : {&c->fl_pending, &c->fl_free})
+    for (cpr_ctx::FlushRec& r : *v) {
+      (void)hipEventDestroy(r.e0);
+      (void)hipEventDestroy(r.e1);
+      (void)hipHostFree(r.cnt);
+    }
   (void)hipStreamDestroy(c->stream);
   c->rq.release();
   c->rtab.release();
@@ -825,6 +841,27 @@ int cpr_rerun_hbm_retries(cpr_ctx* c, int64_t* retries) {
   return CPR_OK;
 }
 
+int cpr_rerun_stats(cpr_ctx* c, int64_t* episodes, int64_t* flushes, double* ms) {
+  if (!c) return fail(CPR_E_INVALID_ARG, "NULL argument");
+  HIP_TRY(hipSetDevice(c->device));
+  if (!c->fl_pending.empty()) {
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    for (const cpr_ctx::FlushRec& r : c->fl_pending) {
+      float t = 0.f;
+      HIP_TRY(hipEventElapsedTime(&t, r.e0, r.e1));
+      c->rr_ms += t;
+      c->rr_episodes += *r.cnt;
+      c->rr_flushes += 1;
+      c->fl_free.push_back(r);
+    }
+    c->fl_pending.clear();
+  }
+  if (episodes) *episodes = c->rr_episodes;
+  if (flushes) *flushes = c->rr_flushes;
+  if (ms) *ms = c->rr_ms;
+  return CPR_OK;
+}
+
 int cpr_last_launch(cpr_batch* b, double* kernel_ms, int64_t* activations) {
   if (!b) return fail(CPR_E_INVALID_ARG, "NULL argument");
   if (b->async_launch) {  // cpr_run_episodes_async: the caller has synchronized
@@ -897,9 +934,22 @@ static int flush_reruns(cpr_ctx* c) {
   HIP_TRY(hipMemcpyAsync(c->rtab.p, c->rlaunch_up.data(), tb, hipMemcpyHostToDevice, c->stream));
   HIP_TRY(c->rmem.ensure((size_t)kRerunLanes * (size_t)lb));
   uint32_t* qn = (uint32_t*)((char*)c->rq.p + (size_t)kRerunQueue * 8);
+  cpr_ctx::FlushRec fr;
+  if (!c->fl_free.empty()) {
+    fr = c->fl_free.back();
+    c->fl_free.pop_back();
+  } else {
+    HIP_TRY(hipEventCreate(&fr.e0));
+    HIP_TRY(hipEventCreate(&fr.e1));
+    HIP_TRY(hipHostMalloc((void**)&fr.cnt, sizeof(uint32_t)));
+  }
+  HIP_TRY(hipEventRecord(fr.e0, c->stream));
   HIP_TRY(launch_nak_exact_rerun((const RerunLaunch*)c->rtab.p, (int64_t)c->rlaunch_up.size(),
                                  (const int64_t*)c->rq.p, qn, c->rq_cap, (uint8_t*)c->rmem.p,
                                  lb, rest, kRerunLanes, c->stream));
+  HIP_TRY(hipEventRecord(fr.e1, c->stream));
+  HIP_TRY(hipMemcpyAsync(fr.cnt, qn, sizeof(uint32_t), hipMemcpyDeviceToHost, c->stream));
+  c->fl_pending.push_back(fr);
   HIP_TRY(hipMemsetAsync(qn, 0, 4, c->stream));
   c->ovf_chunk = 0;  // the next launches' flags follow these re-runs on the stream
   c->ovf_used = 0;

@@ -30,8 +30,8 @@
 // cannot vouch for — an activation inside the previous window's deliveries (OVERLAP), a
 // tie on a release that is not a chain or exceeds the replay (TIE_UNRESOLVED), a candidate
 // or frontier overflow (CAPACITY) — flags the episode, and the kernel re-runs it on the
-// exact event engine. Parity: tests/native/ethwin_vs_engine.cpp compares this lane with
-// the event engine step by step on the host; tests/test_gpu_eth.py with the oracle.
+// exact event engine. Parity: tests/native/ethwin_vs_oracle.cpp compares this lane with
+// the oracle's event-driven ethereum.cpp step by step on the host; tests/test_gpu_eth.py with the oracle.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -63,7 +63,10 @@ struct WBlock {
   uint8_t np;                // parents
   uint8_t rel;               // attacker block shared (V_REL in the attacker's view)
   uint8_t _pad0;
-  int32_t _pad1[2];
+  int32_t plain;             // this block and its first-parent ancestors below it that have
+                             // one parent each, counted from here (0: this one has uncles or
+                             // is genesis): the frontier walk skips such runs (q_advance)
+  int32_t _pad1;
   double time;               // append time (Simulator.timestamp)
 };
 static_assert(sizeof(WBlock) == 64, "WBlock layout");
@@ -229,6 +232,28 @@ struct WinLane {
     return x;
   }
 
+  // first-parent LCA of x and y: level the heights, then descend by jump pointers while
+  // the two jumps differ (jumps depend on the height alone, so they stay level)
+  __host__ __device__ inline int32_t fp_lca(const EthParams& P, const WinMem& M, int32_t x,
+                                            int32_t y) {
+    const int32_t hx = B(P, M, x).height, hy = B(P, M, y).height;
+    if (hx > hy) x = ancestor_at(P, M, x, hy);
+    if (hy > hx) y = ancestor_at(P, M, y, hx);
+    while (x != y && !dead) {
+      const WBlock& a = B(P, M, x);
+      const WBlock& b = B(P, M, y);
+      if (a.np == 0 || b.np == 0) break;
+      if (a.jump != b.jump) {
+        x = a.jump;
+        y = b.jump;
+      } else {
+        x = a.p[0];
+        y = b.p[0];
+      }
+    }
+    return x;
+  }
+
   // simulator.ml:122-136, 377-399 (set_rewards, ethereum.ml:173-197: Constant = whitepaper)
   __host__ __device__ inline int32_t append(const EthParams& P, const WinMem& M, int32_t node,
                                             const Payload& d) {
@@ -267,6 +292,7 @@ struct WinLane {
     b.child = -1;
     b.sib = pb.child;  // children lists newest first (dag.ml:32)
     b.jump = jmp;
+    b.plain = d.np == 1 ? pb.plain + 1 : 0;
     pb.child = s;
     b.time = now;
     return s;
@@ -307,6 +333,57 @@ struct WinLane {
     for (int32_t i = 0; i < b.np; ++i) q_insert(q, nq, b.p[i], B(P, M, b.p[i]).height);
     return s;
   }
+  // q_next for the side whose popped block is above the other side's `y` (the walk keeps
+  // advancing this side while its popped keys stay above key(y)). When the frontier's top e
+  // heads a run of one-parent blocks (WBlock.plain), popping a run block pushes just its
+  // first parent, so the walk pops e, its parent, ... for as long as (A) the block popped
+  // before stays above key(y) and (B) the next one stays above the frontier's second key
+  // k2 (else that one is the top). One jump-pointer descent to the lowest such block
+  // replaces those pops and leaves the frontier exactly as they would: that block popped,
+  // its parent queued, the rest unchanged. Long private forks otherwise walked the whole
+  // fork a block at a time every activation (selfish_release at gamma = 0: ~13 pops per
+  // activation, bench configs[2]'s slowest point by 3x)
+  __host__ __device__ inline int32_t q_advance(const EthParams& P, const WinMem& M, int32_t* q,
+                                               int32_t* nq, int32_t y) {
+    if (*nq >= 1) {
+      const int32_t e = q[1];
+      const WBlock& be = B(P, M, e);
+      if (be.plain >= 2) {
+        const int32_t he = be.height;
+        int32_t lo = he - be.plain + 1;  // the run's last block
+        // (A) the block above the landing one is above y: height >= hy, or hy - 1 when the
+        // run's block at hy is above y by serial
+        const int32_t hy = B(P, M, y).height;
+        if (hy > lo) {
+          int32_t ha = hy;
+          if (hy <= he && ancestor_at(P, M, e, hy) > y) ha = hy - 1;
+          lo = ha > lo ? ha : lo;
+        }
+        // (B) the landing block is above the frontier's second element
+        if (*nq >= 2) {
+          const int32_t h2 = q[2], s2 = q[3];
+          if (h2 >= lo) {
+            int32_t hb = h2 + 1;
+            if (h2 <= he && ancestor_at(P, M, e, h2) > s2) hb = h2;
+            lo = hb > lo ? hb : lo;
+          }
+        }
+        if (lo < he && !dead) {
+          CPR_COST(eth::CC_CA);
+          const int32_t z = ancestor_at(P, M, e, lo);
+          for (int32_t j = 1; j < *nq; ++j) {  // e leaves the frontier
+            q[2 * (j - 1)] = q[2 * j];
+            q[2 * (j - 1) + 1] = q[2 * j + 1];
+          }
+          --*nq;
+          const int32_t pz = B(P, M, z).p[0];
+          q_insert(q, nq, pz, B(P, M, pz).height);
+          return z;
+        }
+      }
+    }
+    return q_next(P, M, q, nq);
+  }
   __host__ __device__ inline int32_t common_ancestor(const EthParams& P, const WinMem& M,
                                                      int32_t a, int32_t b) {
     if (a == b) return a;
@@ -319,12 +396,39 @@ struct WinLane {
     int32_t y = q_next(P, M, qb, &nb);
     while (x >= 0 && y >= 0 && !dead) {
       if (x == y) return x;
+      // both sides on runs of one-parent blocks (each frontier is just the popped block's
+      // parent): the walk pops the two first-parent chains alternately, highest key first,
+      // and its first common block is their first-parent LCA F. If F lies within both runs
+      // that is the answer; otherwise the walk passes both sides at the height L where the
+      // first run ends, which one jump-pointer descent per side reaches (q_advance handles a
+      // side whose run lies above the other side's block)
+      if (na == 1 && nb == 1) {
+        const WBlock& bx = B(P, M, x);
+        const WBlock& by = B(P, M, y);
+        if (bx.plain >= 2 && by.plain >= 2 && qa[1] == bx.p[0] && qb[1] == by.p[0]) {
+          const int32_t lx = bx.height - bx.plain + 1, ly = by.height - by.plain + 1;
+          const int32_t L = lx > ly ? lx : ly;
+          const int32_t f = fp_lca(P, M, x, y);
+          if (B(P, M, f).height >= L) return f;
+          const int32_t hmin = bx.height < by.height ? bx.height : by.height;
+          if (L < hmin && !dead) {
+            CPR_COST(eth::CC_CA);
+            x = ancestor_at(P, M, x, L);
+            y = ancestor_at(P, M, y, L);
+            na = nb = 0;
+            const int32_t px = B(P, M, x).p[0], py = B(P, M, y).p[0];
+            q_insert(qa, &na, px, B(P, M, px).height);
+            q_insert(qb, &nb, py, B(P, M, py).height);
+            continue;
+          }
+        }
+      }
       const uint64_t kx = eth::EthLane::ca_key(B(P, M, x).height, x);
       const uint64_t ky = eth::EthLane::ca_key(B(P, M, y).height, y);
       if (kx > ky)
-        x = q_next(P, M, qa, &na);
+        x = q_advance(P, M, qa, &na, y);
       else
-        y = q_next(P, M, qb, &nb);
+        y = q_advance(P, M, qb, &nb, x);
     }
     fail(4);
     return 0;
@@ -367,6 +471,17 @@ struct WinLane {
         ca_a = a;
         return ca_c;
       }
+    }
+    // one argument a first-parent ancestor of the other (the attacker's public model on
+    // its own released chain, ethereum_ssz.ml:325-362): every ancestor of the lower one is
+    // an ancestor of both and it is the highest of them, so it is the answer of the walk.
+    // Not cached: the cached pair is the walk's, which the next activation's incremental
+    // rule above extends (selfish_release at gamma = 0 alternates the two cases; caching
+    // this one cost it the walk over the whole fork at every other activation)
+    if (a != b) {
+      const bool al = B(P, M, a).height <= B(P, M, b).height;
+      const int32_t lo = al ? a : b, hi = al ? b : a;
+      if (ancestor_at(P, M, hi, B(P, M, lo).height) == lo) return lo;
     }
     const int32_t c = common_ancestor(P, M, a, b);
     ca_a = a;
@@ -612,6 +727,7 @@ struct WinLane {
     r.rew_att = r.rew_def = 0;
     r.child = r.sib = -1;
     r.jump = 0;
+    r.plain = 0;
     r.time = 0.0;
     for (int32_t j = 0; j <= P.d; ++j) M.tips[j] = 0;
     pub = priv = 0;

@@ -42,6 +42,14 @@ class Context:
         L.check(L.lib().cpr_rerun_hbm_retries(self.handle, ctypes.byref(v)))
         return v.value
 
+    def rerun_stats(self):
+        """Cumulative (episodes, flushes, kernel ms) of exact re-runs on this context
+        (cpr_rerun_stats): episodes the fused kernels handed to the exact event engine."""
+        e, f, ms = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_double()
+        L.check(L.lib().cpr_rerun_stats(self.handle, ctypes.byref(e), ctypes.byref(f),
+                                        ctypes.byref(ms)))
+        return e.value, f.value, ms.value
+
     def synchronize(self):
         L.check(L.lib().cpr_synchronize(self.handle))
 

@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define CPR_ABI_VERSION 9
+#define CPR_ABI_VERSION 10
 
 typedef struct cpr_ctx cpr_ctx;
 typedef struct cpr_batch cpr_batch;
@@ -408,6 +408,12 @@ int cpr_launch_shape(cpr_batch* b, int64_t* lanes, int64_t* resident);
  * LDS-resident event heap and ran again with the heap in HBM (k_nak_exact_rerun's second
  * attempt). Synchronizes the context's stream. Diagnostic, no reference counterpart. ABI v9. */
 int cpr_rerun_hbm_retries(cpr_ctx* ctx, int64_t* retries);
+/* cumulative exact re-runs on this context: episodes the fused kernels flagged (closed-form
+ * Nakamoto overlaps, deep forks and unresolved ties; Ethereum window-lane hand-backs) and
+ * re-ran on the exact event engine, the flushes that ran them and those flushes' kernel
+ * milliseconds (HIP events on the context's stream). Synchronizes the stream if a flush is
+ * pending. Diagnostic for bench.py, no reference counterpart. ABI v10. */
+int cpr_rerun_stats(cpr_ctx* ctx, int64_t* episodes, int64_t* flushes, double* ms);
 
 /* Lockstep env API over cfg->n_lanes lanes (host pointers).
  * reset: lanes with mask[i] != 0 (mask NULL = all) start episode episode_ids[i]

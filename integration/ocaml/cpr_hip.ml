@@ -1,4 +1,4 @@
-(* OCaml ctypes bindings of libcpr_hip (include/cpr_hip.h, CPR_ABI_VERSION 9).
+(* OCaml ctypes bindings of libcpr_hip (include/cpr_hip.h, CPR_ABI_VERSION 10).
 
    For a host that has OCaml: dropped next to the reference's gym engine
    (simulator/gym/), it lets Hip_engine.of_module (hip_engine.ml) stand in for
@@ -12,7 +12,7 @@
 open Ctypes
 open Foreign
 
-let abi_version = 9
+let abi_version = 10
 
 (* ---- status codes and enums (cpr_status, cpr_protocol, cpr_network, cpr_mode) *)
 let ok = 0
@@ -209,6 +209,9 @@ let launch_shape =
 
 let rerun_hbm_retries =
   foreign "cpr_rerun_hbm_retries" (ptr ctx @-> ptr int64_t @-> returning int)
+let rerun_stats =
+  foreign "cpr_rerun_stats"
+    (ptr ctx @-> ptr int64_t @-> ptr int64_t @-> ptr double @-> returning int)
 ;;
 
 let reset =

@@ -41,7 +41,7 @@ struct Cfg {
 };
 
 struct Counters {
-  long episodes = 0, mismatches = 0, redo = 0, ties = 0, steps = 0, overlaps = 0;
+  long episodes = 0, mismatches = 0, redo = 0, ties = 0, steps = 0, overlaps = 0, ca_pairs = 0;
 };
 
 static eth::EthParams params_of(const Cfg& cf) {
@@ -150,6 +150,44 @@ static bool run_gym(const Cfg& cf, uint64_t seed, uint64_t ep, Counters& C, std:
     }
     if (done) break;
   }
+  // the lane's common-ancestor walk (run jumps included) against a brute-force restatement
+  // of Dagtools.common_ancestor (max (height, serial) over the intersection of the two
+  // all-edge ancestor sets) for random pairs of this episode's blocks
+  if (ok && !(L.status & ethw::W_REDO) && L.newest > 2) {
+    std::vector<uint8_t> in_a(L.newest + 1), in_b(L.newest + 1);
+    auto anc = [&](int32_t x, std::vector<uint8_t>& in) {
+      std::fill(in.begin(), in.end(), 0);
+      std::vector<int32_t> st{x};
+      while (!st.empty()) {
+        const int32_t s = st.back();
+        st.pop_back();
+        if (s < 0 || in[s]) continue;
+        in[s] = 1;
+        const ethw::WBlock& b = L.B(P, M, s);
+        for (int i = 0; i < b.np; ++i) st.push_back(b.p[i]);
+      }
+    };
+    for (int t = 0; t < 64; ++t) {
+      const int32_t a = (int32_t)(mix(ep * 977 + t, 1) % (uint32_t)(L.newest + 1));
+      const int32_t b = (int32_t)(mix(ep * 977 + t, 2) % (uint32_t)(L.newest + 1));
+      anc(a, in_a);
+      anc(b, in_b);
+      int32_t best = -1;
+      for (int32_t s = 0; s <= L.newest; ++s)
+        if (in_a[s] && in_b[s] &&
+            (best < 0 || L.B(P, M, s).height > L.B(P, M, best).height ||
+             (L.B(P, M, s).height == L.B(P, M, best).height && s > best)))
+          best = s;
+      const int32_t got = L.common_ancestor(P, M, a, b);
+      C.ca_pairs++;
+      if (got != best && !L.dead) {
+        snprintf(buf, sizeof buf, "common_ancestor(%d, %d) lane %d brute force %d", a, b, got, best);
+        why = buf;
+        ok = false;
+        break;
+      }
+    }
+  }
   C.episodes++;
   if (L.status & ST_TIE) C.ties++;
   if (!ok) C.mismatches++;
@@ -181,6 +219,12 @@ int main(int argc, char** argv) {
       cfgs.push_back({a, 0.5, 2, pol, 0, steps, 0.05});
       cfgs.push_back({a, 0.9, 11, pol, 1, steps, 0.01});
     }
+  // full-length episodes with long private forks (the common-ancestor walk's run jumps,
+  // eth_window.h q_advance / common_ancestor: selfish_release at gamma = 0 forks for
+  // hundreds of blocks), every policy and both random fuzzers
+  for (int pol = 0; pol <= 6; ++pol)
+    for (double g : {0.0, 0.5})
+      cfgs.push_back({0.45, g, 2, pol, pol % 2, 2016, 1e-9});
   // episodes ended by max_time / max_progress before max_steps (engine.ml:209-214)
   for (int pol : {1, 3, 5})
     for (double a : {0.25, 0.45})
@@ -207,7 +251,7 @@ int main(int argc, char** argv) {
                 cfgs[ci].scheme, cfgs[ci].prop, e, why.c_str());
     }
   printf("{\"configs\": %zu, \"episodes\": %ld, \"steps\": %ld, \"mismatches\": %ld, "
-         "\"redo\": %ld, \"overlaps\": %ld, \"tie_episodes\": %ld}\n",
-         cfgs.size(), C.episodes, C.steps, C.mismatches, C.redo, C.overlaps, C.ties);
+         "\"redo\": %ld, \"overlaps\": %ld, \"tie_episodes\": %ld, \"ca_pairs\": %ld}\n",
+         cfgs.size(), C.episodes, C.steps, C.mismatches, C.redo, C.overlaps, C.ties, C.ca_pairs);
   return C.mismatches ? 1 : 0;
 }
