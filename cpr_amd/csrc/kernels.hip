@@ -11,6 +11,8 @@
 #define CPR_UNIFORM_SEED 1
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "../../include/cpr_hip.h"
 #include "kernels.h"
 #include "nakamoto_lane.h"
@@ -35,9 +37,9 @@ __device__ inline void acc_add(LdsAcc& a, const BRef& hd, int64_t steps, int64_t
 
 // One gym episode (engine.ml:164-249): reset = first activation up to the attacker's
 // interaction; step = apply, deliveries, next activation, observe; head at the end.
-// LZ: the lazy clock (NakLane::lazy_overlap_check), launched only when the host's
-// lazy_clock_ok holds and only max_steps ends the episode
-template <int POL, int TT, class St, bool LZ = false>
+// LZ: the lazy clock (NakLane::lazy_overlap_check; 2 = with deferred races, races_check),
+// launched only when the host's lazy_clock_ok holds and only max_steps ends the episode
+template <int POL, int TT, class St, int LZ = 0>
 __device__ inline CPR_AI BRef run_gym(NakLane& L, const NakParams& P, const St& S, const LaneMem& M,
                                int64_t* steps_out) {
   L.init();
@@ -51,15 +53,15 @@ __device__ inline CPR_AI BRef run_gym(NakLane& L, const NakParams& P, const St& 
       const NakLane::Draw dr = L.draw<St, LZ>(P, S);
       L.apply(L.policy_action<POL>(P));
       L.resolve<St, POL >= 0 ? 0 : -1, TT>(P, S, M);
-      if constexpr (TT == 2) enqueue_race(L, M);
+      if constexpr (TT == 2) enqueue_race<LZ>(L, M);
       L.activate<St, LZ>(P, S, M, dr);
       ++steps;
       // the lanes of the wave verify together once the wave's list is nearly full
       if constexpr (TT == 2) {
-        if (races_due(L, M)) verify_races(L, P, S, M);
+        if (races_due(L, M)) verify_races<St, LZ>(L, P, S, M);
       }
     } while (steps < P.max_steps);
-    if constexpr (TT == 2) verify_races(L, P, S, M);
+    if constexpr (TT == 2) verify_races<St, LZ>(L, P, S, M);
     *steps_out = steps;
     return L.head(P, M);
   }
@@ -106,7 +108,7 @@ constexpr uint32_t kInexact = ST_OVERLAP | ST_DEEP_FORK | ST_TIE_UNRESOLVED | ST
 // 2 = as 1, and the races are deferred and verified in batches (verify_races; REC = 0 only:
 // the race lists take the LDS ring); an episode a race went otherwise in is listed in
 // `list` (count, then episode indices) for the eager second pass (ListSource, TT = 1)
-// LZ: lazy clock (REC = 0, ARR = 0 only; NakLane::lazy_overlap_check)
+// LZ: lazy clock (REC = 0 only; 1 at ARR = 0, 2 with the deferred races TT = 2)
 template <int MODE, class Src, int POL, int REC = 1, int ARR = -1, int TT = 0, int LZ = 0>
 #ifndef CPR_G0_WAVES
 #define CPR_G0_WAVES 8  // the gamma = 0 kernel: 61 VGPRs fit 8 waves/SIMD (7 unasked)
@@ -121,8 +123,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ARR == 0
     uint8_t* ovf) {
   // the race lists take the LDS ring, which only the summary-only kernels leave free
   static_assert(TT != 2 || REC == 0, "deferred races need the summary-only kernel");
-  static_assert(!LZ || (REC == 0 && ARR == 0 && MODE == CPR_MODE_GYM),
-                "the lazy clock is for the summary-only gamma = 0 gym kernel");
+  static_assert(!LZ || (REC == 0 && MODE == CPR_MODE_GYM && (LZ == 1 ? ARR == 0 : TT == 2)),
+                "the lazy clock is for the summary-only gym kernels (gamma = 0, deferred races)");
   if (ARR >= 0) P.arrive = ARR;
   if (TT) P.d = 2;  // launched for two defenders only (gym_run_fn): masks and loops fold
   __shared__ int32_t hist[CPR_HIST_BINS];
@@ -166,7 +168,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ARR == 0
   for (int64_t e = tid; e < n_run; e += nthreads) {
     const auto S = src.at(e);
     int64_t steps = 0;
-    const BRef hd = MODE == CPR_MODE_GYM ? run_gym<POL, TT, decltype(S), LZ != 0>(L, P, S, M, &steps)
+    const BRef hd = MODE == CPR_MODE_GYM ? run_gym<POL, TT, std::remove_const_t<decltype(S)>, LZ>(L, P, S, M, &steps)
                                          : run_loop<POL>(L, P, S, M, activations);
     if constexpr (TT == 2) {
       if (L.status & ST_RACE_REDO) {
@@ -503,6 +505,8 @@ static RunFn gym_run_fn(const NakParams& P, bool recs, bool defer, ListFn* secon
   if (P.d != 2) return k_run_episodes<CPR_MODE_GYM, SeedSource, POL, 0, 1>;
   if (!defer) return k_run_episodes<CPR_MODE_GYM, SeedSource, POL, 0, 1, 1>;
   if (second) *second = k_run_episodes<CPR_MODE_GYM, ListSource, POL, 0, 1, 1>;
+  if (lazy_clock_ok(P) && CPR_LAZY_CLOCK)
+    return k_run_episodes<CPR_MODE_GYM, SeedSource, POL, 0, 1, 2, 2>;
   return k_run_episodes<CPR_MODE_GYM, SeedSource, POL, 0, 1, 2>;
 }
 // second: set to the eager second pass when the launch defers its races (else untouched)

@@ -465,6 +465,8 @@ struct NakLane {
   uint32_t rw;       // the race resolve<.., 2> took as decided: wminer | rlo << 2 |
                      // rhi << 14, 0 = none (enqueue_race lists it)
   int32_t tinf;      // LZ: a clock delay of +inf was drawn (the clock is +inf from then on)
+  uint32_t esum;     // LZ = 2: sum over the activations so far of 54 - bitlength(U), so
+                     // that t <= esum ln2 ev (each delay -ev log(U 2^-53) <= (54 - L) ln2 ev)
 
   __host__ __device__ inline CPR_AI double chain_t(const LaneMem& M, int32_t m) const {
     if (!M.times) return 0.0;
@@ -497,7 +499,7 @@ struct NakLane {
     k = 0; n = 0; rel = 0; n_ba = 0; pend = -1; wminer = 0; event = 0;
     rlo = 1; rhi = 0; status = 0u; onA = 0ull; lca_da = 0;
     w_hasb = 0; w_bound = -__builtin_inf();
-    qn = 0; rw = 0u; tinf = 0;
+    qn = 0; rw = 0u; tinf = 0; esum = 0u;
   }
 
   // the lane's state without block times (the summary-only kernels' whole state) as
@@ -520,12 +522,18 @@ struct NakLane {
   template <class St>
   __host__ __device__ inline CPR_AI double window_last_arrival(const NakParams& P,
                                                         const St& S) const {
+    return window_last_arrival_at(P, S, t);
+  }
+  // the same with the window's time given (the lazy clock recomputes it)
+  template <class St>
+  __host__ __device__ inline CPR_AI double window_last_arrival_at(const NakParams& P,
+                                                                  const St& S, double tw) const {
     double last = -__builtin_inf();
-    if (w_hasb && P.d >= 2) last = t + P.delta;
+    if (w_hasb && P.d >= 2) last = tw + P.delta;
     if (rhi >= rlo && P.arrive) {
       for (int32_t j = 1; j <= P.d; ++j)
         for (int32_t m = rlo; m <= rhi; ++m) {
-          const double a = t + S.link((uint32_t)k, (uint32_t)(rhi - m), (uint32_t)j, P.dmax);
+          const double a = tw + S.link((uint32_t)k, (uint32_t)(rhi - m), (uint32_t)j, P.dmax);
           last = a > last ? a : last;
         }
     }
@@ -543,12 +551,12 @@ struct NakLane {
   // the next activation's miner and clock delay: they depend on the activation count only,
   // so the gym loop draws them first and the Philox / log chain overlaps the policy and
   // apply selects of the same iteration
-  template <class St, bool LZ = false>
+  template <class St, int LZ = 0>
   __host__ __device__ inline CPR_AI Draw draw(const NakParams& P, const St& S) const {
     return draw_at<St, LZ>(P, S, k);
   }
   // the draws of activation kk (kk = k: the next one)
-  template <class St, bool LZ = false>
+  template <class St, int LZ = 0>
   __host__ __device__ inline CPR_AI Draw draw_at(const NakParams& P, const St& S,
                                                  int32_t kk) const {
     Draw d;
@@ -562,42 +570,55 @@ struct NakLane {
     return d;
   }
 
-  // LZ = lazy clock, for the summary-only gamma = 0 kernel (no arrivals, no records): there
-  // the clock feeds nothing but the overlap check, which can fire only when the previous
-  // window delivered a defender block at t + delta and the new activation comes no later,
-  // fl(t + dt) <= fl(t + delta). A uniform below P.u_lazy draws dt > 2 delta, which (with
-  // the launcher's bound ulp(t) <= delta / 4 over the whole episode) rules that out without
-  // the log, so the clock is neither drawn nor summed. Only the rest, ~2.5 delta / ev of
-  // activations, takes this branch: it sums the clock from the episode's first draw in the
-  // same order as the eager lane and makes the same comparison, so the status bits (and the
-  // exact re-run an overlap sends the episode to) are the eager lane's. tinf: a zero uniform
-  // (delay +inf) leaves the eager lane's clock at +inf, where every later defender window
-  // overlaps.
+  // LZ = lazy clock, for the summary-only kernels (no records), where the clock feeds only
+  // the overlap check and, at gamma = .5 (LZ = 2, deferred races), the races' same-instant
+  // test. The overlap check can fire only when the previous window sent a message (its
+  // defender block at t + delta, a release at t + U dmax <= t + delta) and the new activation
+  // comes no later. A uniform below P.u_lazy draws dt > 2 delta, which (with the launcher's
+  // bound ulp(t) <= delta / 4 over the whole episode) rules that out without the log, so the
+  // clock is neither drawn nor summed. Only the rest, ~2.5 delta / ev of activations, takes
+  // this branch: it sums the clock from the episode's first draw in the same order as the
+  // eager lane and makes the same comparisons, so the status bits (and the exact re-run an
+  // overlap sends the episode to) are the eager lane's. tinf: a zero uniform (delay +inf)
+  // leaves the eager lane's clock at +inf, where every later window with a message
+  // overlaps. LZ = 2 races: see races_check.
   template <class St>
   __host__ __device__ inline void lazy_overlap_check(const NakParams& P, const St& S,
                                                      uint64_t u) {
     const bool wb = w_hasb != 0 && P.d >= 2;
+    const bool wr = rhi >= rlo && P.arrive;  // the previous window's release
     if (tinf) {
-      if (wb) status |= ST_OVERLAP;
+      if (wb || wr) status |= ST_OVERLAP;
       return;
     }
-    if (u == 0ull) {  // this activation's delay is +inf: t + inf > t + delta
+    if (u == 0ull) {  // this activation's delay is +inf: t + inf > every arrival
       tinf = 1;
       return;
     }
-    if (!wb) return;
+    if (!wb && !wr) return;
     double tp = 0.0;
     for (int32_t j = 0; j < k; ++j) tp = tp + S.clock((uint32_t)j, P.ev);
     const double tn = tp + S.clock((uint32_t)k, P.ev);
-    if (tn <= tp + P.delta) status |= ST_OVERLAP;
+    double bound = wb ? tp + P.delta : -__builtin_inf();
+    if (wr) {
+      const double ub = tp + (P.dmax - 0.0);
+      bound = ub > bound ? ub : bound;
+    }
+    if (tn <= bound) {
+      if (tn <= window_last_arrival_at(P, S, tp)) status |= ST_OVERLAP;
+    }
+  }
+  // 54 - bitlength(U): -log(U 2^-53) <= that times ln 2 (U = 0: +inf, tinf)
+  __host__ __device__ static inline CPR_AI uint32_t lz_bits(uint64_t u) {
+    return u == 0ull ? 0u : (uint32_t)(__builtin_clzll(u) - 10);
   }
 
-  template <class St, bool LZ = false>
+  template <class St, int LZ = 0>
   __host__ __device__ inline CPR_AI void activate(const NakParams& P, const St& S, const LaneMem& M) {
     activate<St, LZ>(P, S, M, draw<St, LZ>(P, S));
   }
 
-  template <class St, bool LZ = false>
+  template <class St, int LZ = 0>
   __host__ __device__ inline CPR_AI void activate(const NakParams& P, const St& S, const LaneMem& M,
                                                   const Draw dr) {
     const int32_t miner = dr.miner;
@@ -605,6 +626,7 @@ struct NakLane {
     if constexpr (LZ) {
       // u >= u_lazy, or u == 0 (unsigned wrap), or a +inf clock: the exact check
       if ((dr.u - 1ull) >= (P.u_lazy - 1ull) || tinf) lazy_overlap_check(P, S, dr.u);
+      if constexpr (LZ == 2) esum += lz_bits(dr.u);
     } else {
       if (tn <= w_bound) {
         if (tn <= window_last_arrival(P, S)) status |= ST_OVERLAP;
@@ -805,19 +827,28 @@ struct NakLane {
 // TT = 2, after resolve: the lanes whose race was taken as decided append it to the wave's
 // dense list (entry: window time, activation count, rw with the owner lane in bits 26..31),
 // so that verify_races spreads the wave's races over all its lanes
+// LZ = 2 (lazy clock): instead of the window time, its bound esum (t <= esum ln2 ev) and
+// whether the clock is +inf
+template <int LZ = 0>
 __host__ __device__ inline CPR_AI uint4 race_entry(const NakLane& L, int32_t lane) {
-  const uint64_t tb = bitsd(L.t);
   uint4 e;
-  e.x = (uint32_t)tb;
-  e.y = (uint32_t)(tb >> 32);
+  if constexpr (LZ == 2) {
+    e.x = L.esum;
+    e.y = (uint32_t)L.tinf;
+  } else {
+    const uint64_t tb = bitsd(L.t);
+    e.x = (uint32_t)tb;
+    e.y = (uint32_t)(tb >> 32);
+  }
   e.z = (uint32_t)L.k;
   e.w = L.rw | ((uint32_t)lane << 26);
   return e;
 }
+template <int LZ = 0>
 __host__ __device__ inline CPR_AI void enqueue_race(NakLane& L, const LaneMem& M) {
   const bool race = L.rw != 0u;
   const uint64_t bal = wave_ballot(race);
-  if (race) M.rq[L.qn + lanes_below(bal)] = race_entry(L, M.lane);
+  if (race) M.rq[L.qn + lanes_below(bal)] = race_entry<LZ>(L, M.lane);
   L.qn += __builtin_popcountll(bal);
   L.rw = 0u;
 }
@@ -840,7 +871,13 @@ __host__ __device__ inline CPR_AI void races_publish(const St& S, const LaneMem&
   M.rep[2 * M.lane] = S.e0;
   M.rep[2 * M.lane + 1] = S.e1;
 }
-template <class St>
+// LZ = 2: the window time is not known, only a bound T >= t + delta (esum ln2 ev, widened
+// by 1e-9 for the log's and the sum's rounding, plus delta). t + a and t + delta both round
+// to the grid of spacing <= ulp(T), each within half of it, so a < delta - ulp(T) puts the
+// release strictly first, as the eager check would find. Anything closer (~ulp(t) / delta,
+// 1e-4 of races at the gym's delay; or a +inf clock) cannot be decided without t and flags
+// the episode for the eager second pass, which decides it with t as the eager kernel does.
+template <class St, int LZ = 0>
 __host__ __device__ inline CPR_AI void races_check(const NakLane& L, const NakParams& P,
                                                   const St& S, const LaneMem& M) {
   // the entries are spread over the lanes that are here: in the last grid-stride round of
@@ -855,13 +892,25 @@ __host__ __device__ inline CPR_AI void races_check(const NakLane& L, const NakPa
 #endif
   for (int32_t i = rank; i < L.qn; i += stride) {
     const uint4 e = M.rq[i];
-    const double t = dbits((uint64_t)e.x | ((uint64_t)e.y << 32));
     const int32_t rlo = (int32_t)((e.w >> 2) & 0xfffu), rhi = (int32_t)((e.w >> 14) & 0xfffu);
     const uint32_t j = 3u - (e.w & 3u);
     const int32_t owner = (int32_t)(e.w >> 26);
     St so = S;  // the owner lane's episode
     so.e0 = M.rep[2 * owner];
     so.e1 = M.rep[2 * owner + 1];
+    if constexpr (LZ == 2) {
+      double a = -__builtin_inf();
+      for (int32_t m = rlo; m <= rhi; ++m) {
+        const double x = so.link(e.z, (uint32_t)(rhi - m), j, P.dmax);
+        a = x > a ? x : a;
+      }
+      const double T = (double)e.x * (0.6931471805599453 * P.ev) * (1.0 + 1e-9) + P.delta;
+      const int32_t ex = (int32_t)((bitsd(T) >> 52) & 0x7ffu);  // T > 0, normal
+      const double ulp = dbits((uint64_t)(ex > 52 ? ex - 52 : 1) << 52);
+      if (e.y != 0u || !(a < P.delta - ulp)) flag_or(&M.rflag[owner], 2);
+      continue;
+    }
+    const double t = dbits((uint64_t)e.x | ((uint64_t)e.y << 32));
     double v = -__builtin_inf();
     for (int32_t m = rlo; m <= rhi; ++m) {
       const double a = t + so.link(e.z, (uint32_t)(rhi - m), j, P.dmax);
@@ -885,12 +934,12 @@ __host__ __device__ inline CPR_AI void races_settle(NakLane& L, const LaneMem& M
   L.status |= (fl & 1) ? ST_TIE : 0u;
   L.status |= (fl & 2) ? ST_RACE_REDO : 0u;
 }
-template <class St>
+template <class St, int LZ = 0>
 __host__ __device__ inline CPR_AI void verify_races(NakLane& L, const NakParams& P, const St& S,
                                                    const LaneMem& M) {
   races_publish(S, M);
   wave_lds_order();
-  races_check(L, P, S, M);
+  races_check<St, LZ>(L, P, S, M);
   wave_lds_order();
   races_settle(L, M);
 }

@@ -119,6 +119,92 @@ static bool episode(double alpha, int d, double delta, int policy, int steps, ui
   return ok;
 }
 
+// ---- gamma = .5 (d = 2, dmax <= delta): the deferred-race kernel (TT = 2) eager vs lazy
+// (LZ = 2: no clock; races decided by a bound on t, the undecidable ones flagged for the
+// eager second pass). A lazy run must flag every episode the eager run flags; where neither
+// flags, the lanes end in the same state word for word.
+struct Deferred {
+  std::vector<uint4> rq;
+  int32_t flag = 0;
+  uint32_t ep[2] = {0u, 0u};
+  LaneMem M{};
+  Deferred(const NakParams& P, int32_t cap) : rq(cap) {
+    M.times = false;
+    M.cap = P.cap;
+    M.rq = rq.data();
+    M.rq_cap = cap;
+    M.rflag = &flag;
+    M.rep = ep;
+    M.lane = 0;
+  }
+};
+
+template <int LZ>
+static NakLane run_tt2(const NakParams& P, const ZStream& S, int policy, uint64_t ep,
+                       int32_t cap) {
+  Deferred D(P, cap);
+  const LaneMem& M = D.M;
+  NakLane L;
+  L.init();
+  L.activate<ZStream, LZ>(P, S, M);
+  for (int64_t s = 0; s < P.max_steps; ++s) {
+    const NakLane::Draw dr = L.draw<ZStream, LZ>(P, S);
+    const int32_t act = policy < 4 ? L.policy_action(P) : (int32_t)(mix(ep, s) & 3u);
+    L.apply(act);
+    L.resolve<ZStream, 0, 2>(P, S, M);
+    enqueue_race<LZ>(L, M);
+    L.activate<ZStream, LZ>(P, S, M, dr);
+    if (races_due(L, M)) verify_races<ZStream, LZ>(L, P, S, M);
+  }
+  verify_races<ZStream, LZ>(L, P, S, M);
+  return L;
+}
+
+struct Counters2 {
+  long episodes = 0, mismatches = 0, eager_redo = 0, lazy_redo = 0, overlaps = 0, ties = 0;
+};
+
+static void episode_tt2(double alpha, double delta, double dmax, int policy, int steps,
+                        uint64_t ep, uint32_t zero_at, Counters2& C) {
+  NakParams P{};
+  P.t_att = oracle::alpha_threshold(alpha);
+  P.d = 2;
+  P.ev = 1.0;
+  P.delta = delta;
+  P.dmax = dmax;
+  P.arrive = 1;
+  P.max_steps = steps;
+  P.max_progress = __builtin_inf();
+  P.max_time = __builtin_inf();
+  P.policy = policy < 4 ? policy : 0;
+  P.cap = steps + 64;
+  if (!lazy_clock_ok(P)) exit(2);
+  P.u_lazy = lazy_threshold(P);
+  ZStream S;
+  S.k0 = 0x5eed0000u;
+  S.k1 = 0;
+  S.e0 = (uint32_t)ep;
+  S.e1 = (uint32_t)(ep >> 32);
+  S.zero_at = zero_at;
+  const int32_t cap = (ep & 1) ? 64 : 6;
+  const NakLane E = run_tt2<0>(P, S, policy, ep, cap);
+  const NakLane Z = run_tt2<2>(P, S, policy, ep, cap);
+  const bool er = (E.status & ST_RACE_REDO) != 0, zr = (Z.status & ST_RACE_REDO) != 0;
+  C.episodes++;
+  C.eager_redo += er ? 1 : 0;
+  C.lazy_redo += zr ? 1 : 0;
+  C.overlaps += (E.status & ST_OVERLAP) ? 1 : 0;
+  C.ties += (E.status & ST_TIE) ? 1 : 0;
+  bool ok = true;
+  if (er && !zr) ok = false;  // the lazy run must flag whatever the eager run flags
+  if (!er && !zr && words(E) != words(Z)) ok = false;
+  if (!ok) {
+    C.mismatches++;
+    fprintf(stderr, "MISMATCH tt2 alpha=%g delta=%g dmax=%g pol=%d ep=%llu zero_at=%u: status eager %u lazy %u\n",
+            alpha, delta, dmax, policy, (unsigned long long)ep, zero_at, E.status, Z.status);
+  }
+}
+
 int main(int argc, char** argv) {
   const int eps = argc > 1 ? atoi(argv[1]) : 40;
   const int steps = argc > 2 ? atoi(argv[2]) : 400;
@@ -132,8 +218,20 @@ int main(int argc, char** argv) {
             const uint32_t z = (e % 5 == 4) ? mix(e, 7) % (uint32_t)steps : 0xffffffffu;
             episode(a, d, delta, pol, steps, (uint64_t)e, z, C);
           }
+  Counters2 C2;
+  for (double delta : {1e-9, 1e-10, 1e-3, 0.05})
+    for (double ratio : {1.0, 0.3})
+      for (double a : {0.25, 0.33, 0.45})
+        for (int pol = 0; pol <= 4; ++pol)
+          for (int e = 0; e < eps; ++e) {
+            const uint32_t z = (e % 7 == 6) ? mix(e, 9) % (uint32_t)steps : 0xffffffffu;
+            episode_tt2(a, delta, delta * ratio, pol, steps, (uint64_t)e, z, C2);
+          }
   printf("{\"episodes\": %ld, \"mismatches\": %ld, \"lazy_branch_activations\": %ld, "
-         "\"overlap_episodes\": %ld, \"inf_clock_episodes\": %ld}\n",
-         C.episodes, C.mismatches, C.slow, C.overlaps, C.inf_eps);
-  return C.mismatches ? 1 : 0;
+         "\"overlap_episodes\": %ld, \"inf_clock_episodes\": %ld, \"tt2_episodes\": %ld, "
+         "\"tt2_mismatches\": %ld, \"tt2_eager_redo\": %ld, \"tt2_lazy_redo\": %ld, "
+         "\"tt2_overlap_episodes\": %ld, \"tt2_tie_episodes\": %ld}\n",
+         C.episodes, C.mismatches, C.slow, C.overlaps, C.inf_eps, C2.episodes, C2.mismatches,
+         C2.eager_redo, C2.lazy_redo, C2.overlaps, C2.ties);
+  return C.mismatches || C2.mismatches ? 1 : 0;
 }
