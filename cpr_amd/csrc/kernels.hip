@@ -545,10 +545,12 @@ hipError_t launch_run_episodes(const NakParams& P0, uint64_t seed, uint64_t firs
   hipLaunchKernelGGL(fn, dim3(blocks), dim3(kBlock), 0, st, P, src, n_eps, activations, spill,
                      replay, recs, sum, redo, redo_n, launch_id, redo_cap, list, ovf);
   if (second) {
-    // a few episodes in a hundred: half the grid runs them in one round (more take more
-    // rounds of the same grid-stride loop); blocks without an episode exit at once
+    // a few episodes in a hundred (~1 % eager, ~3.5 % with the lazy clock, whose races
+    // near a tie cannot be decided without the clock): the whole grid runs them in one round
+    // (more take more rounds of the same grid-stride loop); blocks without an episode exit
+    // at once
     const ListSource ls{src, reinterpret_cast<const uint32_t*>(list), list + 1};
-    const unsigned b2 = blocks / 2 > 0 ? blocks / 2 : 1;
+    const unsigned b2 = blocks;
     hipLaunchKernelGGL(second, dim3(b2), dim3(kBlock), 0, st, P, ls, n_eps, activations, spill,
                        replay, recs, sum, redo, redo_n, launch_id, redo_cap, list, ovf);
   }

@@ -173,7 +173,8 @@ inline bool lazy_clock_ok(const NakParams& P) {
   if (!(P.delta > 0.0) || !std::isfinite(P.delta) || !(P.ev > 0.0) || !std::isfinite(P.ev))
     return false;
   if (P.max_progress < __builtin_inf() || P.max_time < __builtin_inf()) return false;
-  if (P.max_steps <= 0 || P.max_steps > (1ll << 30)) return false;
+  // (<= 2^14 steps: the race kernel's clock bound esum, <= 150500 a step, stays in 32 bits)
+  if (P.max_steps <= 0 || P.max_steps > (1ll << 14)) return false;
   const double tmax = ((double)P.max_steps + 2.0) * P.ev * 40.0;
   return std::ldexp(1.0, std::ilogb(tmax) - 52) <= P.delta / 4.0;
 }
@@ -465,8 +466,8 @@ struct NakLane {
   uint32_t rw;       // the race resolve<.., 2> took as decided: wminer | rlo << 2 |
                      // rhi << 14, 0 = none (enqueue_race lists it)
   int32_t tinf;      // LZ: a clock delay of +inf was drawn (the clock is +inf from then on)
-  uint32_t esum;     // LZ = 2: sum over the activations so far of 54 - bitlength(U), so
-                     // that t <= esum ln2 ev (each delay -ev log(U 2^-53) <= (54 - L) ln2 ev)
+  uint32_t esum;     // LZ = 2: sum over the activations so far of lz_term(U), so that
+                     // t <= esum ev / 4096 (lz_term bounds -log(U 2^-53) in units of 2^-12)
 
   __host__ __device__ inline CPR_AI double chain_t(const LaneMem& M, int32_t m) const {
     if (!M.times) return 0.0;
@@ -608,9 +609,21 @@ struct NakLane {
       if (tn <= window_last_arrival_at(P, S, tp)) status |= ST_OVERLAP;
     }
   }
-  // 54 - bitlength(U): -log(U 2^-53) <= that times ln 2 (U = 0: +inf, tinf)
-  __host__ __device__ static inline CPR_AI uint32_t lz_bits(uint64_t u) {
-    return u == 0ull ? 0u : (uint32_t)(__builtin_clzll(u) - 10);
+  // an upper bound of -log(U 2^-53) in units of 2^-12: with uh = the top 24 bits of U
+  // (U >> 29, so U >= uh 2^29), -log(U 2^-53) <= (24 - log2 uh) ln 2. log2 in f32 (the
+  // hardware's v_log_f32 on the device, within a few 1e-6 of the true value; std::log2f on
+  // the host: the bound need not be the same bits on both sides, only a bound) with ln 2
+  // rounded up and a margin of 8 units for log2's and the f32 fma's rounding, plus 1 for
+  // the truncation. uh = 0 (U < 2^29): 53 ln 2 and some. U = 0 (+inf) is tinf's case
+  __host__ __device__ static inline CPR_AI uint32_t lz_term(uint64_t u) {
+    const uint32_t uh = (uint32_t)(u >> 29);
+#if defined(__HIP_DEVICE_COMPILE__)
+    const float y = __builtin_amdgcn_logf((float)uh);
+#else
+    const float y = std::log2((float)uh);
+#endif
+    const float b = __builtin_fmaf(y, -2839.1309f, 68148.2f);  // 4096 ((24 - y) ln2) + 9
+    return uh == 0u ? 150500u : (uint32_t)b;
   }
 
   template <class St, int LZ = 0>
@@ -626,7 +639,7 @@ struct NakLane {
     if constexpr (LZ) {
       // u >= u_lazy, or u == 0 (unsigned wrap), or a +inf clock: the exact check
       if ((dr.u - 1ull) >= (P.u_lazy - 1ull) || tinf) lazy_overlap_check(P, S, dr.u);
-      if constexpr (LZ == 2) esum += lz_bits(dr.u);
+      if constexpr (LZ == 2) esum += lz_term(dr.u);
     } else {
       if (tn <= w_bound) {
         if (tn <= window_last_arrival(P, S)) status |= ST_OVERLAP;
@@ -871,8 +884,8 @@ __host__ __device__ inline CPR_AI void races_publish(const St& S, const LaneMem&
   M.rep[2 * M.lane] = S.e0;
   M.rep[2 * M.lane + 1] = S.e1;
 }
-// LZ = 2: the window time is not known, only a bound T >= t + delta (esum ln2 ev, widened
-// by 1e-9 for the log's and the sum's rounding, plus delta). t + a and t + delta both round
+// LZ = 2: the window time is not known, only a bound T >= t + delta (esum ev / 4096,
+// widened by 1e-9 for the log's and the sum's rounding, plus delta). t + a and t + delta both round
 // to the grid of spacing <= ulp(T), each within half of it, so a < delta - ulp(T) puts the
 // release strictly first, as the eager check would find. Anything closer (~ulp(t) / delta,
 // 1e-4 of races at the gym's delay; or a +inf clock) cannot be decided without t and flags
@@ -904,7 +917,7 @@ __host__ __device__ inline CPR_AI void races_check(const NakLane& L, const NakPa
         const double x = so.link(e.z, (uint32_t)(rhi - m), j, P.dmax);
         a = x > a ? x : a;
       }
-      const double T = (double)e.x * (0.6931471805599453 * P.ev) * (1.0 + 1e-9) + P.delta;
+      const double T = (double)e.x * (P.ev * (1.0 / 4096.0)) * (1.0 + 1e-9) + P.delta;
       const int32_t ex = (int32_t)((bitsd(T) >> 52) & 0x7ffu);  // T > 0, normal
       const double ulp = dbits((uint64_t)(ex > 52 ? ex - 52 : 1) << 52);
       if (e.y != 0u || !(a < P.delta - ulp)) flag_or(&M.rflag[owner], 2);

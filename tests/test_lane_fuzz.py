@@ -72,6 +72,11 @@ def test_lazy_clock_equals_eager():
     assert out["mismatches"] == 0 and out["episodes"] == 3600
     assert out["lazy_branch_activations"] > 100000 and out["overlap_episodes"] > 1000
     assert out["inf_clock_episodes"] == 720
+    # the gamma = .5 kernel (deferred races): the lazy run flags a superset of the eager
+    # run's episodes for the second pass and otherwise ends in the same state
+    assert out["tt2_mismatches"] == 0 and out["tt2_episodes"] == 2400
+    assert out["tt2_lazy_redo"] >= out["tt2_eager_redo"] > 0
+    assert out["tt2_overlap_episodes"] > 100 and out["tt2_tie_episodes"] > 50
 
 
 def test_ethereum_lane_matches_oracle_fuzz():
