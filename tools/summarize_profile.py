@@ -19,7 +19,8 @@ K = "k_run_episodes"
 # specialisation (REC = 0) runs. At gamma = .5 (d = 2, dmax = delta) it defers its races and
 # an eager second pass (ListSource) reruns the few episodes a race went otherwise in: a
 # point's launch is both kernels, so their times and counters are summed per main dispatch
-HEADLINE = re.compile(r"k_run_episodes<0, (cpr::)?(Seed|List)Source, 3(, 0(, -?\d+, \d+)?)?>")
+# (the template's trailing arguments: REC, ARR, TT, LZ; any of them may be printed)
+HEADLINE = re.compile(r"k_run_episodes<0, (cpr::)?(Seed|List)Source, 3(, 0(, -?\d+)*)?>")
 SECOND = re.compile(r"k_run_episodes<0, (cpr::)?ListSource")
 
 
