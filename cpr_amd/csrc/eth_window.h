@@ -52,24 +52,27 @@ using eth::Payload;
 // window-lane status bits the fused kernel hands to the exact event engine
 constexpr uint32_t W_REDO = ST_OVERLAP | ST_TIE_UNRESOLVED | eth::EST_CAPACITY;
 
+// 32 bytes: serials are < cap_b <= 2^15 (append stops the lane before the ring would wrap),
+// so block references and heights fit 16 bits, and a 128-byte line holds four blocks (the
+// lane's walks read neighbouring serials: chains, children lists). The append time, read
+// only for the head's chain time at the end, lives in a separate array (WinMem.tm)
 struct WBlock {
-  int32_t p[3];  // parent, uncles (-1: none)
-  int32_t height, work;
+  int16_t p[3];    // parent, uncles (-1: none)
+  int16_t child;   // newest block whose first parent this is (-1: none)
+  int16_t sib;     // next older block with the same first parent (-1: none)
+  int16_t jump;    // skew-binary jump ancestor (O(log depth) ancestor queries)
+  int16_t plain;   // this block and its first-parent ancestors below it that have one
+                   // parent each, counted from here (0: this one has uncles or is genesis):
+                   // the frontier walk skips such runs (q_advance)
+  int16_t height;
+  int8_t miner;    // -1 genesis, 0 attacker, 1..d defenders
+  uint8_t np;      // parents
+  uint8_t rel;     // attacker block shared (V_REL in the attacker's view)
+  uint8_t _pad;
+  int32_t work;
   int32_t rew_att, rew_def;  // cumulative rewards of the first-parent chain, units of 1/32
-  int32_t child;             // newest block whose first parent this is (-1: none)
-  int32_t sib;               // next older block with the same first parent (-1: none)
-  int32_t jump;              // skew-binary jump ancestor (O(log depth) ancestor queries)
-  int8_t miner;              // -1 genesis, 0 attacker, 1..d defenders
-  uint8_t np;                // parents
-  uint8_t rel;               // attacker block shared (V_REL in the attacker's view)
-  uint8_t _pad0;
-  int32_t plain;             // this block and its first-parent ancestors below it that have
-                             // one parent each, counted from here (0: this one has uncles or
-                             // is genesis): the frontier walk skips such runs (q_advance)
-  int32_t _pad1;
-  double time;               // append time (Simulator.timestamp)
 };
-static_assert(sizeof(WBlock) == 64, "WBlock layout");
+static_assert(sizeof(WBlock) == 32, "WBlock layout");
 
 constexpr int32_t NCAND = eth::NCAND, NQ = eth::NQ, NSTACK = eth::NSTACK;
 // scratch ints: candidates, keys, two frontiers, share stack, closure (share order)
@@ -78,20 +81,24 @@ constexpr int32_t S_INTS = 192 + NSTACK;
 
 struct WinMem {
   WBlock* blk;     // [cap_b]
+  double* tm;      // [cap_b] append times (Simulator.timestamp)
   int32_t* tips;   // [64]: defender j's preferred block at tips[j] (Honest.state)
   int32_t* scr;    // [S_INTS]
   ReplayMem replay;  // tie_replay scratch
 };
 
 __host__ __device__ inline int64_t win_lane_bytes(int32_t cap_b) {
-  return eth::align128((int64_t)cap_b * 64) + eth::align128(65 * 4) +
+  return eth::align128((int64_t)cap_b * (int64_t)sizeof(WBlock)) +
+         eth::align128((int64_t)cap_b * 8) + eth::align128(65 * 4) +
          eth::align128(S_INTS * 4) + eth::align128(REPLAY_BYTES);
 }
 __host__ __device__ inline WinMem win_mem_at(uint8_t* base, int32_t cap_b) {
   WinMem M;
   int64_t o = 0;
   M.blk = (WBlock*)(base + o);
-  o += eth::align128((int64_t)cap_b * 64);
+  o += eth::align128((int64_t)cap_b * (int64_t)sizeof(WBlock));
+  M.tm = (double*)(base + o);
+  o += eth::align128((int64_t)cap_b * 8);
   M.tips = (int32_t*)(base + o);
   o += eth::align128(65 * 4);
   M.scr = (int32_t*)(base + o);
@@ -133,6 +140,11 @@ struct WinLane {
   __host__ __device__ inline WBlock& B(const EthParams& P, const WinMem& M, int32_t s) {
     if ((uint32_t)s > (uint32_t)newest) fail(1);
     return M.blk[s & (P.cap_b - 1)];
+  }
+  // Simulator.timestamp of block s (its append time)
+  __host__ __device__ inline double time_of(const EthParams& P, const WinMem& M, int32_t s) {
+    B(P, M, s);  // range check
+    return M.tm[s & (P.cap_b - 1)];
   }
   // visibility at quiescence (every message of earlier windows delivered)
   __host__ __device__ static inline bool def_visible(const EthParams& P, const WBlock& b) {
@@ -279,11 +291,11 @@ struct WinLane {
     const int32_t jmp = jump_for(P, M, d.p[0]);
     const int32_t s = ++newest;
     WBlock& b = M.blk[s];
-    b.p[0] = d.p[0];
-    b.p[1] = d.np > 1 ? d.p[1] : -1;
-    b.p[2] = d.np > 2 ? d.p[2] : -1;
+    b.p[0] = (int16_t)d.p[0];
+    b.p[1] = (int16_t)(d.np > 1 ? d.p[1] : -1);
+    b.p[2] = (int16_t)(d.np > 2 ? d.p[2] : -1);
     b.np = (uint8_t)d.np;
-    b.height = d.height;
+    b.height = (int16_t)d.height;
     b.work = d.work;
     b.miner = (int8_t)node;
     b.rel = 0;
@@ -291,10 +303,10 @@ struct WinLane {
     b.rew_def = rd;
     b.child = -1;
     b.sib = pb.child;  // children lists newest first (dag.ml:32)
-    b.jump = jmp;
-    b.plain = d.np == 1 ? pb.plain + 1 : 0;
-    pb.child = s;
-    b.time = now;
+    b.jump = (int16_t)jmp;
+    b.plain = (int16_t)(d.np == 1 ? pb.plain + 1 : 0);
+    pb.child = (int16_t)s;
+    M.tm[s] = now;
     return s;
   }
 
@@ -728,7 +740,7 @@ struct WinLane {
     r.child = r.sib = -1;
     r.jump = 0;
     r.plain = 0;
-    r.time = 0.0;
+    M.tm[0] = 0.0;
     for (int32_t j = 0; j <= P.d; ++j) M.tips[j] = 0;
     pub = priv = 0;
     pending = -1;

@@ -207,7 +207,7 @@ __global__ __launch_bounds__(kBlock) CPR_EW_OCC void k_eth_win_episodes(
       r.reward_attacker = (double)ra / 32.0;
       r.reward_defender = (double)rd / 32.0;
       r.progress = (double)h.work;
-      r.chain_time = h.time;
+      r.chain_time = W.time_of(P, M, hd);
       r.sim_time = W.now;
       r.n_steps = W.steps;
       r.n_activations = W.c_act;

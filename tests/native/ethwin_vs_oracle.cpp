@@ -134,13 +134,13 @@ static bool run_gym(const Cfg& cf, uint64_t seed, uint64_t ep, Counters& C, std:
     const double ra = hb.rew_att / 32.0, rd = hb.rew_def / 32.0;
     if (ra != info.episode_reward_attacker || rd != info.episode_reward_defender ||
         hb.height != info.head_height || hb.work != info.head_work ||
-        (double)hb.work != info.episode_progress || hb.time != info.episode_chain_time ||
+        (double)hb.work != info.episode_progress || L.time_of(P, M, hd) != info.episode_chain_time ||
         L.now != info.episode_sim_time || L.c_act != info.episode_n_activations ||
         hb.miner != info.head_miner || ldone != done || L.steps != info.episode_n_steps) {
       snprintf(buf, sizeof buf,
                "step %d head lane (ra %.5f rd %.5f h %d w %d tm %.17g t %.17g k %d m %d done %d) "
                "oracle (ra %.5f rd %.5f h %d w %d tm %.17g t %.17g k %ld m %d done %d)",
-               s, ra, rd, hb.height, hb.work, hb.time, L.now, L.c_act, hb.miner, (int)ldone,
+               s, ra, rd, (int)hb.height, hb.work, L.time_of(P, M, hd), L.now, L.c_act, hb.miner, (int)ldone,
                info.episode_reward_attacker, info.episode_reward_defender, info.head_height,
                info.head_work, info.episode_chain_time, info.episode_sim_time,
                info.episode_n_activations, info.head_miner, (int)done);
