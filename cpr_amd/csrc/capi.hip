@@ -900,6 +900,7 @@ int cpr_batch_destroy(cpr_batch* b) {
 // this kernel's register/LDS use x CUs x 256), bounded by a 16 GiB budget for per-lane HBM
 // exact Nakamoto re-runs: one-wave workgroups of the re-run kernel
 constexpr int64_t kRerunLanes = 512;
+constexpr int64_t kRerunLanesMax = 8192;  // one workgroup per queued episode, up to this
 
 static int64_t episode_lanes(cpr_batch* b, int64_t n_eps, bool recs) {
   const int64_t full =
@@ -932,8 +933,31 @@ static int flush_reruns(cpr_ctx* c) {
   const size_t tb = c->rlaunch_up.size() * sizeof(RerunLaunch);
   HIP_TRY(c->rtab.ensure(tb));
   HIP_TRY(hipMemcpyAsync(c->rtab.p, c->rlaunch_up.data(), tb, hipMemcpyHostToDevice, c->stream));
-  HIP_TRY(c->rmem.ensure((size_t)kRerunLanes * (size_t)lb));
   uint32_t* qn = (uint32_t*)((char*)c->rq.p + (size_t)kRerunQueue * 8);
+  // how many episodes the launches queued (a flush is a synchronization point anyway). Up to
+  // one per CU: one-wave workgroups of 512 with the lane's heap, visibility and scratch in up
+  // to a whole CU's LDS, the fastest per episode (a re-run is one dependent chain). More
+  // (the headline's sweep queues ~140 per step, ~2,850 in a 20-step timed region, half of
+  // them gamma = 0 re-runs whose +inf messages keep the heap large): LDS of that size would
+  // run them one CU at a time, round after round, so each episode gets a workgroup of its own
+  // with its region in HBM instead and they all run at once
+  int64_t lanes = kRerunLanes, lds_rest = rest;
+#ifndef CPR_FLUSH_ADAPTIVE
+#define CPR_FLUSH_ADAPTIVE 1
+#endif
+  if (CPR_FLUSH_ADAPTIVE) {
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    uint32_t nq = 0;
+    HIP_TRY(hipMemcpy(&nq, qn, sizeof(nq), hipMemcpyDeviceToHost));
+    if ((int64_t)nq > (int64_t)c->cus) {
+      lanes = std::min<int64_t>((int64_t)nq, kRerunLanesMax);
+      lds_rest = 0;
+      // A/B: LDS per workgroup in this mode (the heap at the capacity that fits, an episode
+      // that outgrows it again in HBM); 0 = the whole region in HBM
+      if (const char* v = getenv("CPR_RERUN_WIDE_LDS")) lds_rest = std::min<int64_t>(rest, atoll(v));
+    }
+  }
+  HIP_TRY(c->rmem.ensure((size_t)lanes * (size_t)lb));
   cpr_ctx::FlushRec fr;
   if (!c->fl_free.empty()) {
     fr = c->fl_free.back();
@@ -946,7 +970,7 @@ static int flush_reruns(cpr_ctx* c) {
   HIP_TRY(hipEventRecord(fr.e0, c->stream));
   HIP_TRY(launch_nak_exact_rerun((const RerunLaunch*)c->rtab.p, (int64_t)c->rlaunch_up.size(),
                                  (const int64_t*)c->rq.p, qn, c->rq_cap, (uint8_t*)c->rmem.p,
-                                 lb, rest, kRerunLanes, c->stream));
+                                 lb, lds_rest, lanes, c->stream));
   HIP_TRY(hipEventRecord(fr.e1, c->stream));
   HIP_TRY(hipMemcpyAsync(fr.cnt, qn, sizeof(uint32_t), hipMemcpyDeviceToHost, c->stream));
   c->fl_pending.push_back(fr);
