@@ -15,6 +15,9 @@
 //                           a stale slot (serial mismatch) marks the lane CPR_ST_CAPACITY
 //   vis    [cap_v][n] u8    per node: kind (invisible/received/released/withheld) + got bit
 //   vt     [cap_v][n] f64   per node: visible_since (simulator.ml:291-294)
+//   vc     [cap_v][n] u64   blocks, per node: visible votes on the block by kind (16-bit
+//                           received / released / withheld counts), maintained where a
+//                           vote's kind changes, so vote counts need no list walk
 //   quo    [cap_q][k+1] i32 block quorums (tag = block serial, then k vote serials by hash)
 //   drafts [cap_d][k+2] i32 outstanding Append drafts (tag, parent, k votes)
 //   heap   [cap_e] x 24 B   skew-heap nodes of the event queue
@@ -133,6 +136,7 @@ struct BkMem {
   int4* vn;
   uint8_t* vis;
   double* vt;
+  uint64_t* vc;
   int32_t* quo;
   int32_t* drafts;
   HNode* heap;
@@ -153,7 +157,8 @@ __host__ __device__ inline int64_t bk_lane_bytes(const BkParams& P) {
   return bk_align((int64_t)P.cap_v * (int64_t)sizeof(BVtx)) + bk_align((int64_t)P.cap_v * 4) +
          bk_align((int64_t)P.cap_v * 16) +
          bk_align((int64_t)P.cap_v * P.n) +
-         bk_align((int64_t)P.cap_v * P.n * 8) + bk_align((int64_t)P.cap_q * (P.k + 1) * 4) +
+         bk_align((int64_t)P.cap_v * P.n * 8) + bk_align((int64_t)P.cap_v * P.n * 8) +
+         bk_align((int64_t)P.cap_q * (P.k + 1) * 4) +
          bk_align((int64_t)P.cap_d * (P.k + 2) * 4) + bk_align((int64_t)P.cap_e * 24) +
          bk_align((int64_t)P.n * 4) + bk_align(2 * NQS * 8) + bk_align(2 * NQS * 4) +
          bk_align(NSTACK * 4);
@@ -171,6 +176,8 @@ __host__ __device__ inline BkMem bk_mem_at(uint8_t* base, const BkParams& P) {
   M.vis = base + o;
   o += bk_align((int64_t)P.cap_v * P.n);
   M.vt = (double*)(base + o);
+  o += bk_align((int64_t)P.cap_v * P.n * 8);
+  M.vc = (uint64_t*)(base + o);
   o += bk_align((int64_t)P.cap_v * P.n * 8);
   M.quo = (int32_t*)(base + o);
   o += bk_align((int64_t)P.cap_q * (P.k + 1) * 4);
@@ -384,6 +391,20 @@ struct BkLane {
   __host__ __device__ inline double& VT(const BkParams& P, const BkMem& M, int32_t s,
                                         int32_t node) {
     return M.vt[(int64_t)(s & (P.cap_v - 1)) * P.n + node];
+  }
+  // visible-vote counts of block b at node (vc): 16-bit fields by kind, V_RECV at bit 0,
+  // V_REL at 16, V_WH at 32
+  __host__ __device__ inline uint64_t& VC(const BkParams& P, const BkMem& M, int32_t b,
+                                          int32_t node) {
+    return M.vc[(int64_t)(b & (P.cap_v - 1)) * P.n + node];
+  }
+  __host__ __device__ static inline int32_t vc_field(uint64_t c, uint8_t kind) {
+    return (int32_t)((c >> (16 * (kind - 1))) & 0xffffu);
+  }
+  // counts passing vf: kinds kept by keep(., vf)
+  __host__ __device__ static inline int32_t vc_count(uint64_t c, int32_t vf) {
+    const int32_t rc = vc_field(c, V_RECV), rl = vc_field(c, V_REL), wh = vc_field(c, V_WH);
+    return vf == VF_ALL ? rc + rl + wh : (vf == VF_MINE ? wh + rl : rl + rc);
   }
   __host__ __device__ inline bool visible(const BkParams& P, const BkMem& M, int32_t s,
                                           int32_t node) {
@@ -679,6 +700,7 @@ struct BkLane {
     }
     BVtx& b = M.vtx[s & (P.cap_v - 1)];
     init_vertex(P, M, b, s);
+    for (int32_t j = 0; j < P.n; ++j) VC(P, M, s, j) = 0;
     b.parent = dr[1];
     {  // newest-first child-block list of the parent
       int4& pr = VR(P, M, dr[1]);
@@ -708,17 +730,11 @@ struct BkLane {
   }
   // confirming votes of block b visible at `node` that pass `vf` (children scan, newest
   // first: only vertices appended after b can be its children)
+  // (the count of b's visible votes the children scan would find, from b's counters)
   __host__ __device__ inline int32_t confirming(const BkParams& P, const BkMem& M, int32_t b,
                                                 int32_t node, int32_t vf) {
-    int32_t n = 0;
     CPR_BK_COST(BC_CONFIRMING_CALLS);
-    // b's votes (the vertices after b that are votes on b, newest first)
-    for (int32_t c = VH(P, M, b); c >= 0 && !dead; c = VN(P, M, c)) {
-      CPR_BK_COST(BC_CONFIRMING);
-      const uint8_t v = Vg(P, M, c, node);
-      n += ((v & V_KIND) != V_INV && keep(v, vf)) ? 1 : 0;
-    }
-    return n;
+    return vc_count(VC(P, M, b, node), vf);
   }
   // bk.ml:217-226 (skip_eq; by height; by #votes; by neg leader hash; by neg visible_since)
   __host__ __device__ inline int32_t compare_blocks(const BkParams& P, const BkMem& M,
@@ -751,6 +767,18 @@ struct BkLane {
     int32_t nmine = 0, ntheirs = 0;
     uint64_t my_hash = ~0ull;
     CPR_BK_COST(BC_PROPOSE_CALLS);
+    {
+      // the scan's outcome when it would not draft, from b's counters: a node's own votes
+      // are exactly those it holds withheld or released (V_WH / V_REL), the others received
+      const uint64_t cv = VC(P, M, b, node);
+      const int32_t rl = vc_field(cv, V_REL), wh = vc_field(cv, V_WH), rc = vc_field(cv, V_RECV);
+      const int32_t nm = rl + (vf != VF_PUBLIC ? wh : 0), nt = vf != VF_MINE ? rc : 0;
+      if (nm > NQS || nt > NQS) {  // the scan overflows a candidate list
+        fail(3);
+        return -1;
+      }
+      if (dead || nm == 0 || nm + nt < P.k) return -1;  // fast path (bk.ml:254)
+    }
     for (int32_t c = VH(P, M, b); c >= 0 && !dead;) {  // b's votes, newest first
       CPR_BK_COST(BC_PROPOSE);
       const int4 r = VR(P, M, c);  // (next, pow, who): pow_key without the vertex
@@ -841,6 +869,10 @@ struct BkLane {
       Vs(P, M, s, node, (uint8_t)((v & ~V_KIND) | V_REL));
       push_now(P, M, mkev(EV_TX, node, KD_NET), s);
       const BVtx& b = X(P, M, s);
+      if (b.vote) {  // WH -> REL in the block's counts (X: the block is still in the ring)
+        X(P, M, b.parent);
+        VC(P, M, b.parent, node) += (1ull << 16) - (1ull << 32);
+      }
       if (b.parent < 0) continue;
       const int32_t np = b.vote ? 1 : P.k + 1;
       if (sp + np > NSTACK) {
@@ -905,15 +937,9 @@ struct BkLane {
     o.private_blocks = ph - ca;
     o.diff_blocks = ph - qh;
     o.public_votes = confirming(P, M, o_pub, 0, VF_PUBLIC);
-    o.private_votes_inclusive = 0;
-    o.private_votes_exclusive = 0;
-    for (int32_t c = VH(P, M, o_priv); c >= 0 && !dead; c = VN(P, M, c)) {
-      CPR_BK_COST(BC_OBSERVE);
-      const uint8_t v = Vg(P, M, c, 0);
-      if ((v & V_KIND) == V_INV) continue;
-      ++o.private_votes_inclusive;
-      o.private_votes_exclusive += keep(v, VF_MINE) ? 1 : 0;
-    }
+    const uint64_t cv = VC(P, M, o_priv, 0);
+    o.private_votes_inclusive = vc_count(cv, VF_ALL);
+    o.private_votes_exclusive = vc_count(cv, VF_MINE);
     // `lead` compares the signature of the lowest-hash vote with my_id; votes are never
     // signed (bk.ml:281-286), so it is always false in the reference
     o.lead = 0;
@@ -1017,6 +1043,7 @@ struct BkLane {
     VR(P, M, 0).x = -1;
     VR(P, M, 0).w = -1;
     for (int32_t j = 0; j < P.n; ++j) {
+      VC(P, M, 0, j) = 0;
       Vs(P, M, 0, j, V_RECV | V_GOT);
       VT(P, M, 0, j) = 0.0;
       M.tips[j] = 0;
@@ -1054,7 +1081,12 @@ struct BkLane {
           for (int32_t i = 0; i < P.k && ok; ++i) ok = visible(P, M, q[i], node);
         }
         if (!ok) break;
-        Vs(P, M, s, node, (uint8_t)((v & ~V_KIND) | (kind == KD_NET ? V_RECV : V_WH)));
+        const uint8_t nk = kind == KD_NET ? V_RECV : V_WH;
+        Vs(P, M, s, node, (uint8_t)((v & ~V_KIND) | nk));
+        if (b.vote) {  // X: the counts' block is still in the ring
+          X(P, M, b.parent);
+          VC(P, M, b.parent, node) += 1ull << (16 * (nk - 1));
+        }
         VT(P, M, s, node) = now;
         push_now(P, M, mkev(EV_ON, node, kind), s);
         push_now(P, M, mkev(EV_MDV, node, kind), s);
