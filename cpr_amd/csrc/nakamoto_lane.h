@@ -453,7 +453,8 @@ struct NakLane {
   int32_t n_ba;      // private length of the BetweenActions state (attacker's preferred)
   int32_t pend;      // pending private->public message: chain index, -1 = none
   int32_t wminer;    // miner of the current window's activation (0 = attacker)
-  int32_t event;     // observation event: 0 ProofOfWork, 1 Network
+  int32_t event;     // observation event: 0 ProofOfWork, 1 Network; bit 1: the window's
+                     // defender block became pub (apply's `fresh`)
   int32_t rlo, rhi;  // chain indices released in the current window (shared at count k);
                      // kept until the next activation, whose overlap check reads them
   uint32_t status;
@@ -674,8 +675,9 @@ struct NakLane {
     b.fork = par_a ? A.fork : D.fork;
     b.k = ka;
     b.tm = M.times ? tn : 0.0;
-    sel(pub, !att && b.h > pub.h, b);
-    event = att ? 0 : 1;
+    const bool fresh = !att && b.h > pub.h;
+    sel(pub, fresh, b);
+    event = att ? 0 : (fresh ? 3 : 1);
   }
 
   __host__ __device__ inline CPR_AI void observe(int32_t* pub_blocks, int32_t* priv_blocks,
@@ -685,7 +687,7 @@ struct NakLane {
     *pub_blocks = pub.h - ca;
     *priv_blocks = ph - ca;
     *diff_blocks = ph - pub.h;
-    *ev = event;
+    *ev = event & 1;
   }
 
   // Agent.apply (nakamoto_ssz.ml:232-260) + Simulator.handle_action share (:401-419).
@@ -696,7 +698,7 @@ struct NakLane {
     const bool adopt = action == A_ADOPT;
     const bool relx = action == A_MATCH || action == A_OVERRIDE;
     const int32_t hp = pub.h;
-    const bool fresh = wminer != 0 && pub.k == b.k;  // pub is this window's defender block
+    const bool fresh = (event & 2) != 0;  // pub is this window's defender block
     const bool onch = pub.fork == hp;                // pub lies on the private chain
     const int32_t bf = fresh ? b.h : (onch ? (b.fork < hp ? b.fork : hp) : b.fork);
     const int32_t df = fresh ? D.fork : (onch ? (D.fork < hp ? D.fork : hp) : D.h);
