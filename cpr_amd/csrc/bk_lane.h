@@ -18,6 +18,9 @@
 //   vc     [cap_v][n] u64   blocks, per node: visible votes on the block by kind (16-bit
 //                           received / released / withheld counts), maintained where a
 //                           vote's kind changes, so vote counts need no list walk
+//   (CPR_BK_AOS = 1, the default: vtx, vn, vh, vis, vt and vc of one slot share one record
+//   of 2^rsh bytes — 128 for n <= 3 — so the handlers' accesses to a vertex touch one
+//   cache line instead of six; 0: the six arrays above, for A/B runs)
 //   quo    [cap_q][k+1] i32 block quorums (tag = block serial, then k vote serials by hash)
 //   drafts [cap_d][k+2] i32 outstanding Append drafts (tag, parent, k votes)
 //   heap   [cap_e] x 24 B   skew-heap nodes of the event queue
@@ -112,6 +115,19 @@ struct BkParams {
 constexpr int32_t NQS = 128;     // quorum candidates per block and list
 constexpr int32_t NSTACK = 1024; // share stack
 
+#ifndef CPR_BK_AOS
+#define CPR_BK_AOS 1
+#endif
+// the per-slot record (CPR_BK_AOS): BVtx | vn (int4) | vh (int32) | vis [n] | vt [n] | vc [n]
+constexpr int32_t BK_OFF_VN = 48, BK_OFF_VH = 64, BK_OFF_VIS = 68;
+__host__ __device__ inline int32_t bk_off_vt(int32_t n) { return (BK_OFF_VIS + n + 7) & ~7; }
+__host__ __device__ inline int32_t bk_off_vc(int32_t n) { return bk_off_vt(n) + 8 * n; }
+__host__ __device__ inline int32_t bk_rec_shift(int32_t n) {
+  int32_t sh = 6;
+  while ((1 << sh) < bk_off_vc(n) + 8 * n) ++sh;
+  return sh;
+}
+
 struct BkMem {
   // event-heap nodes 0 .. kl-1 live in the workgroup's LDS slab (hl, this lane's part) for
   // the duration of a kernel, the rest in HBM (heap): a window's live events (14-22 at the
@@ -125,6 +141,10 @@ struct BkMem {
   // the walks (vote lists, MadeDescendantsVisible, the release closure) read recent rows
   CPR_LDS uint8_t* vl = nullptr;
   int32_t vw = 0;
+#if CPR_BK_AOS
+  uint8_t* rec;     // [cap_v] records of 2^rsh bytes
+  int32_t rsh;
+#else
   BVtx* vtx;
   // the votes of each block, newest first (the order of the reference's children scans),
   // as two compact per-slot arrays beside the vertices so that a walk reads 4-byte links
@@ -137,6 +157,7 @@ struct BkMem {
   uint8_t* vis;
   double* vt;
   uint64_t* vc;
+#endif
   int32_t* quo;
   int32_t* drafts;
   HNode* heap;
@@ -154,10 +175,15 @@ struct BkMem {
 __host__ __device__ inline int64_t bk_align(int64_t x) { return (x + 127) / 128 * 128; }
 
 __host__ __device__ inline int64_t bk_lane_bytes(const BkParams& P) {
-  return bk_align((int64_t)P.cap_v * (int64_t)sizeof(BVtx)) + bk_align((int64_t)P.cap_v * 4) +
+  return
+#if CPR_BK_AOS
+         bk_align((int64_t)P.cap_v << bk_rec_shift(P.n)) +
+#else
+         bk_align((int64_t)P.cap_v * (int64_t)sizeof(BVtx)) + bk_align((int64_t)P.cap_v * 4) +
          bk_align((int64_t)P.cap_v * 16) +
          bk_align((int64_t)P.cap_v * P.n) +
          bk_align((int64_t)P.cap_v * P.n * 8) + bk_align((int64_t)P.cap_v * P.n * 8) +
+#endif
          bk_align((int64_t)P.cap_q * (P.k + 1) * 4) +
          bk_align((int64_t)P.cap_d * (P.k + 2) * 4) + bk_align((int64_t)P.cap_e * 24) +
          bk_align((int64_t)P.n * 4) + bk_align(2 * NQS * 8) + bk_align(2 * NQS * 4) +
@@ -167,6 +193,11 @@ __host__ __device__ inline int64_t bk_lane_bytes(const BkParams& P) {
 __host__ __device__ inline BkMem bk_mem_at(uint8_t* base, const BkParams& P) {
   BkMem M;
   int64_t o = 0;
+#if CPR_BK_AOS
+  M.rec = base + o;
+  M.rsh = bk_rec_shift(P.n);
+  o += bk_align((int64_t)P.cap_v << M.rsh);
+#else
   M.vtx = (BVtx*)(base + o);
   o += bk_align((int64_t)P.cap_v * (int64_t)sizeof(BVtx));
   M.vh = (int32_t*)(base + o);
@@ -179,6 +210,7 @@ __host__ __device__ inline BkMem bk_mem_at(uint8_t* base, const BkParams& P) {
   o += bk_align((int64_t)P.cap_v * P.n * 8);
   M.vc = (uint64_t*)(base + o);
   o += bk_align((int64_t)P.cap_v * P.n * 8);
+#endif
   M.quo = (int32_t*)(base + o);
   o += bk_align((int64_t)P.cap_q * (P.k + 1) * 4);
   M.drafts = (int32_t*)(base + o);
@@ -194,6 +226,56 @@ __host__ __device__ inline BkMem bk_mem_at(uint8_t* base, const BkParams& P) {
   M.stack = (int32_t*)(base + o);
   return M;
 }
+
+// raw per-slot fields of vertex serial s (no serial check)
+#if CPR_BK_AOS
+__host__ __device__ inline uint8_t* bk_rec(const BkParams& P, const BkMem& M, int32_t s) {
+  return M.rec + ((int64_t)(s & (P.cap_v - 1)) << M.rsh);
+}
+__host__ __device__ inline BVtx& bk_vtx(const BkParams& P, const BkMem& M, int32_t s) {
+  return *reinterpret_cast<BVtx*>(bk_rec(P, M, s));
+}
+__host__ __device__ inline int32_t& bk_vh(const BkParams& P, const BkMem& M, int32_t s) {
+  return *reinterpret_cast<int32_t*>(bk_rec(P, M, s) + BK_OFF_VH);
+}
+__host__ __device__ inline int4& bk_vn(const BkParams& P, const BkMem& M, int32_t s) {
+  return *reinterpret_cast<int4*>(bk_rec(P, M, s) + BK_OFF_VN);
+}
+__host__ __device__ inline uint8_t& bk_vis(const BkParams& P, const BkMem& M, int32_t s,
+                                           int32_t node) {
+  return bk_rec(P, M, s)[BK_OFF_VIS + node];
+}
+__host__ __device__ inline double& bk_vt(const BkParams& P, const BkMem& M, int32_t s,
+                                         int32_t node) {
+  return reinterpret_cast<double*>(bk_rec(P, M, s) + bk_off_vt(P.n))[node];
+}
+__host__ __device__ inline uint64_t& bk_vc(const BkParams& P, const BkMem& M, int32_t s,
+                                           int32_t node) {
+  return reinterpret_cast<uint64_t*>(bk_rec(P, M, s) + bk_off_vc(P.n))[node];
+}
+#else
+__host__ __device__ inline BVtx& bk_vtx(const BkParams& P, const BkMem& M, int32_t s) {
+  return M.vtx[s & (P.cap_v - 1)];
+}
+__host__ __device__ inline int32_t& bk_vh(const BkParams& P, const BkMem& M, int32_t s) {
+  return M.vh[s & (P.cap_v - 1)];
+}
+__host__ __device__ inline int4& bk_vn(const BkParams& P, const BkMem& M, int32_t s) {
+  return M.vn[s & (P.cap_v - 1)];
+}
+__host__ __device__ inline uint8_t& bk_vis(const BkParams& P, const BkMem& M, int32_t s,
+                                           int32_t node) {
+  return M.vis[(int64_t)(s & (P.cap_v - 1)) * P.n + node];
+}
+__host__ __device__ inline double& bk_vt(const BkParams& P, const BkMem& M, int32_t s,
+                                         int32_t node) {
+  return M.vt[(int64_t)(s & (P.cap_v - 1)) * P.n + node];
+}
+__host__ __device__ inline uint64_t& bk_vc(const BkParams& P, const BkMem& M, int32_t s,
+                                           int32_t node) {
+  return M.vc[(int64_t)(s & (P.cap_v - 1)) * P.n + node];
+}
+#endif
 
 // the LDS heap slab of a kernel (BkMem.hl): this lane's nodes 0 .. kl-1 at
 // slab[i * stride + lane]; persistent lanes (rollouts) load the nodes their heap uses at
@@ -213,8 +295,7 @@ __host__ __device__ inline void bk_vis_window(BkMem& M, uint8_t* base, int32_t l
 __host__ __device__ inline void bk_vis_load(const BkMem& M, const BkParams& P, int32_t newest) {
   for (int32_t s = newest - M.vw + 1 < 0 ? 0 : newest - M.vw + 1; s <= newest; ++s)
     for (int32_t j = 0; j < P.n; ++j)
-      M.vl[(int64_t)((s & (M.vw - 1)) * P.n + j) * M.hs] =
-          M.vis[(int64_t)(s & (P.cap_v - 1)) * P.n + j];
+      M.vl[(int64_t)((s & (M.vw - 1)) * P.n + j) * M.hs] = bk_vis(P, M, s, j);
 }
 __host__ __device__ inline void bk_heap_load(const BkMem& M, int32_t hused) {
   const int32_t n = hused < M.kl ? hused : M.kl;
@@ -371,32 +452,32 @@ struct BkLane {
     if (!dead) dead = why;
   }
   __host__ __device__ inline BVtx& X(const BkParams& P, const BkMem& M, int32_t s) {
-    BVtx& b = M.vtx[s & (P.cap_v - 1)];
+    BVtx& b = bk_vtx(P, M, s);
     if (b.serial != s) fail(1);
     return b;
   }
   __host__ __device__ inline int32_t& VH(const BkParams& P, const BkMem& M, int32_t s) {
-    return M.vh[s & (P.cap_v - 1)];
+    return bk_vh(P, M, s);
   }
   __host__ __device__ inline int32_t& VN(const BkParams& P, const BkMem& M, int32_t s) {
-    return M.vn[s & (P.cap_v - 1)].x;
+    return bk_vn(P, M, s).x;
   }
   __host__ __device__ inline int4& VR(const BkParams& P, const BkMem& M, int32_t s) {
-    return M.vn[s & (P.cap_v - 1)];
+    return bk_vn(P, M, s);
   }
   __host__ __device__ inline uint8_t& V(const BkParams& P, const BkMem& M, int32_t s,
                                         int32_t node) {
-    return M.vis[(int64_t)(s & (P.cap_v - 1)) * P.n + node];
+    return bk_vis(P, M, s, node);
   }
   __host__ __device__ inline double& VT(const BkParams& P, const BkMem& M, int32_t s,
                                         int32_t node) {
-    return M.vt[(int64_t)(s & (P.cap_v - 1)) * P.n + node];
+    return bk_vt(P, M, s, node);
   }
   // visible-vote counts of block b at node (vc): 16-bit fields by kind, V_RECV at bit 0,
   // V_REL at 16, V_WH at 32
   __host__ __device__ inline uint64_t& VC(const BkParams& P, const BkMem& M, int32_t b,
                                           int32_t node) {
-    return M.vc[(int64_t)(b & (P.cap_v - 1)) * P.n + node];
+    return bk_vc(P, M, b, node);
   }
   __host__ __device__ static inline int32_t vc_field(uint64_t c, uint8_t kind) {
     return (int32_t)((c >> (16 * (kind - 1))) & 0xffffu);
@@ -419,11 +500,11 @@ struct BkLane {
       return *(const volatile CPR_LDS uint8_t*)&M.vl[(int64_t)((s & (M.vw - 1)) * P.n + node) *
                                                       M.hs];
     }
-    return M.vis[(int64_t)(s & (P.cap_v - 1)) * P.n + node];
+    return bk_vis(P, M, s, node);
   }
   __host__ __device__ inline void Vs(const BkParams& P, const BkMem& M, int32_t s, int32_t node,
                                      uint8_t v) const {
-    M.vis[(int64_t)(s & (P.cap_v - 1)) * P.n + node] = v;
+    bk_vis(P, M, s, node) = v;
     if (s > newest - M.vw) M.vl[(int64_t)((s & (M.vw - 1)) * P.n + node) * M.hs] = v;
   }
   __host__ __device__ inline int32_t* Q(const BkParams& P, const BkMem& M, const BVtx& b) {
@@ -634,7 +715,7 @@ struct BkLane {
                                                  const BkMem& M, int32_t node, int32_t parent) {
     BVtx& p = X(P, M, parent);
     const int32_t s = ++newest;
-    BVtx& b = M.vtx[s & (P.cap_v - 1)];
+    BVtx& b = bk_vtx(P, M, s);
     init_vertex(P, M, b, s);
     b.parent = parent;
     b.height = p.height;
@@ -698,7 +779,7 @@ struct BkLane {
       else
         br[node] += P.k;
     }
-    BVtx& b = M.vtx[s & (P.cap_v - 1)];
+    BVtx& b = bk_vtx(P, M, s);
     init_vertex(P, M, b, s);
     for (int32_t j = 0; j < P.n; ++j) VC(P, M, s, j) = 0;
     b.parent = dr[1];
@@ -1028,7 +1109,7 @@ struct BkLane {
     dseq = 0;
     zt = 0;
     steps = 0;
-    BVtx& r = M.vtx[0];
+    BVtx& r = bk_vtx(P, M, 0);
     r.serial = 0;
     r.parent = -1;
     r.height = 0;
