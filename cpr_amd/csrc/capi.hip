@@ -14,6 +14,7 @@
 #include "../../include/cpr_hip.h"
 #include "eth_window.h"
 #include "kernels.h"
+#include "nak_hybrid.h"
 
 using namespace cpr;
 
@@ -987,7 +988,8 @@ static int flush_reruns(cpr_ctx* c) {
 static int register_rerun(cpr_batch* b, const eth::EthParams& EP, int64_t lane_bytes,
                           uint64_t first, const TraceSource* tr, cpr_episode_record* rec_dev,
                           cpr_summary* sum_dev, int64_t n_eps, int64_t** redo,
-                          uint32_t** redo_n, uint32_t* launch_id, uint8_t** ovf) {
+                          uint32_t** redo_n, uint32_t* launch_id, uint8_t** ovf,
+                          const NakParams* hybrid = nullptr) {
   cpr_ctx* c = b->ctx;
   const size_t need = align256((size_t)std::max<int64_t>(1, n_eps));
   // tests force a small queue (CPR_RERUN_QUEUE_CAP) to exercise the overflow flags; a new
@@ -1043,6 +1045,11 @@ static int register_rerun(cpr_batch* b, const eth::EthParams& EP, int64_t lane_b
   rl.lane_bytes = lane_bytes;
   rl.ovf = *ovf;
   rl.n_eps = n_eps;
+  if (hybrid) {  // nak_hybrid.h: the closed form's state after the engine's region
+    rl.NP = *hybrid;
+    rl.hybrid = 1;
+    rl.lane_bytes = lane_bytes + hybrid_bytes(hybrid->cap);
+  }
   *launch_id = (uint32_t)c->rlaunch.size();
   c->rlaunch.push_back(rl);
   *redo = (int64_t*)c->rq.p;
@@ -1210,8 +1217,22 @@ static int run_async(cpr_batch* b, int64_t n, uint64_t first, const TraceSource*
   uint32_t launch_id = 0;
   uint8_t* ovf = nullptr;
   if (b->has_rerun) {
+    // hybrid re-runs (nak_hybrid.h) where a quiescent point has the reference's queue state:
+    // gym episodes on the selfish-mining network whose attacker messages arrive (gamma > 0),
+    // ended by max_steps alone, the whole episode in the engine's block ring, a seeded
+    // stream and a deterministic policy; CPR_RERUN_HYBRID=0 re-runs whole episodes (A/B)
+    const char* hv = getenv("CPR_RERUN_HYBRID");
+    const bool hyb = !(hv && hv[0] == '0') && !tr && b->cfg.mode == CPR_MODE_GYM &&
+                     b->cfg.network == CPR_NET_SELFISH_MINING && b->P.arrive == 1 &&
+                     !b->P.abstract_g && b->cfg.policy != CPR_POLICY_RANDOM &&
+                     !(b->P.max_progress < __builtin_inf()) &&
+                     !(b->P.max_time < __builtin_inf()) &&
+                     b->NEP.max_steps < (1 << 20) &&
+                     b->NEP.max_steps + 2 <= (int64_t)b->NEP.cap_b;
+    NakParams NP = b->P;
+    NP.cap = (int32_t)((b->NEP.max_steps + 2 + 63) / 64 * 64);
     const int rc = register_rerun(b, b->NEP, b->nak_bytes, first, tr, rec_dev, sum_dev, n,
-                                  &redo, &redo_n, &launch_id, &ovf);
+                                  &redo, &redo_n, &launch_id, &ovf, hyb ? &NP : nullptr);
     if (rc) return rc;
   }
   HIP_TRY(hipEventRecord(b->ev0, b->ctx->stream));

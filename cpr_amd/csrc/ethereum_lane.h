@@ -256,6 +256,7 @@ struct EthLane {
   double now;
   int32_t c_act, newest;
   int32_t act0;  // attacker activations
+  double tclk;   // time of the latest activation (the last clock event popped)
   int32_t hroot, hfree, hused;
   uint32_t status;
   int32_t dead;  // capacity exceeded: 1 block ring, 2 event heap, 3 candidates, 4 frontier, 5 stack
@@ -860,6 +861,7 @@ struct EthLane {
     c_act = 0;
     newest = 0;
     act0 = 0;
+    tclk = 0.0;
     hroot = -1;
     hfree = -1;
     hused = 0;
@@ -935,6 +937,7 @@ struct EthLane {
         break;
       }
       case EV_CLOCK: {
+        tclk = now;
         const int32_t m = miner_of(P, S, c_act);
         if (m == 0 && P.net != 2) {
           ++act0;
@@ -1041,6 +1044,109 @@ struct EthLane {
       handle(P, S, M, ev, s);
     }
     return false;
+  }
+
+  // ---- Nakamoto mode, hybrid re-runs (nak_hybrid.h): the engine is entered and left at
+  // quiescent points whose state the closed-form lane (nakamoto_lane.h) holds exactly
+  //
+  // Quiescent and trivial: the queue holds the next clock event alone (every message of
+  // the earlier windows delivered), every defender prefers the same block x, which a
+  // defender mined (or genesis), the attacker's private and public blocks are x with no
+  // share pending, and no received block waits for a parent. Then the closed-form lane's
+  // state is a function of x, the latest activation's time and the counts.
+  __host__ __device__ inline bool quiescent_trivial(const EthParams& P, const EthMem& M,
+                                                    int32_t* x_out) {
+    if (hroot < 0 || dead) return false;
+    const HNode& h = M.heap[hroot];
+    if (h.l >= 0 || h.r >= 0 || (h.ev & 7u) != EV_CLOCK) return false;
+    if (pending >= 0 || priv != pub) return false;
+    const int32_t x = priv;
+    for (int32_t j = 0; j < P.n; ++j) {
+      if (j > 0 && M.tips[j] != x) return false;
+      if (M.scr[SCR_PEND + j] != 0) return false;
+    }
+    if (B(P, M, x).miner == 0) return false;
+    *x_out = x;
+    return true;
+  }
+  // the engine at such a point, from the closed-form lane's: block x (serial xs, its
+  // height, rewards in 1/32, mining time and miner) is the only block (a root: no parent is
+  // ever asked for below it, every later block descends from it), k activations done, the
+  // latest at time t, `steps` gym steps counted as gym_step counts them (apply of the
+  // current step done); the clock of activation k is scheduled from t as the engine did
+  template <class St>
+  __host__ __device__ inline void enter_trivial(const EthParams& P, const St& S,
+                                                const EthMem& M, int32_t xs, int32_t height,
+                                                int32_t ra32, int32_t rd32, double tm,
+                                                int32_t miner, int32_t k, double t,
+                                                int64_t steps_) {
+    now = t;
+    tclk = t;
+    c_act = k;
+    newest = k;
+    act0 = 0;
+    hroot = -1;
+    hfree = -1;
+    hused = 0;
+    dead = 0;
+    steps = steps_;
+    nrand = 0;
+    dr_node = -1;
+    EBlock& r = M.blk[xs & (P.cap_b - 1)];
+    r.serial = xs;
+    r.p[0] = r.p[1] = r.p[2] = -1;
+    r.np = 0;
+    r.height = height;
+    r.work = height;  // Nakamoto mode: work = height
+    r.miner = miner;
+    r.rew_att = ra32;
+    r.rew_def = rd32;
+    r.share_k = -1;
+    r.share_off = 0;
+    r.time = tm;
+    r.jump = xs;
+    for (int32_t j = 0; j < P.n; ++j) {
+      V(P, M, xs, j) = V_RECV | V_GOT;
+      M.tips[j] = xs;
+      M.scr[SCR_PEND + j] = 0;
+    }
+    agent_init(xs);
+    schedule_pow(P, S, M);
+  }
+  // skip_to_interaction that stops (returns 1, *x_out = the block) before popping the clock
+  // of an activation >= stop_k at a quiescent trivial point; 0 = the attacker's interaction
+  // (*kind, *blk), -1 = none (dead)
+  template <class St>
+  __host__ __device__ inline int32_t skip_or_stop(const EthParams& P, const St& S,
+                                                  const EthMem& M, uint32_t* kind,
+                                                  int32_t* blk, int32_t stop_k,
+                                                  int32_t* x_out) {
+    double t;
+    uint32_t ev;
+    int32_t s;
+    while (!dead) {
+      if (c_act >= stop_k && quiescent_trivial(P, M, x_out)) return 1;
+      if (!pop(M, &t, &ev, &s)) {
+        fail(6);
+        return -1;
+      }
+      now = t;
+      const uint32_t ty = ev & 7u;
+      const int32_t node = (int32_t)(ev >> 5);
+      if (ty == EV_ON && node == 0) {
+        *kind = (ev >> 3) & 3u;
+        *blk = s;
+        return 0;
+      }
+      if (ty == EV_DAG && node == 0) {
+        const Payload d = payload(P, M, 0, priv, F_MINING, own, foreign);
+        const int32_t v = append(P, M, 0, d);
+        push_now(P, M, mkev(EV_MV, 0, KD_POW), v);
+        continue;
+      }
+      handle(P, S, M, ev, s);
+    }
+    return -1;
   }
 
   // winner over [attacker preference; defenders' tips] (ethereum.ml:159-162)

@@ -208,6 +208,11 @@ struct RerunLaunch {
   // queue full writes 0x80 | its status bits here instead (k_rerun_overflow re-runs it)
   uint8_t* ovf;
   int64_t n_eps;
+  // Nakamoto episodes of the closed-form lane re-run as hybrids (nak_hybrid.h): its
+  // parameters (cap: spill slots for a whole episode) and 1 when the launcher's condition
+  // holds; the lane region then ends with hybrid_bytes(NP.cap) for the closed form
+  NakParams NP;
+  int32_t hybrid, _pad2;
 };
 
 // all queued re-runs (count on the device) in one launch of `lanes` one-wave workgroups,

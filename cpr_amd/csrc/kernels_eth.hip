@@ -14,6 +14,7 @@
 #include "eth_window.h"
 #include "ethereum_lane.h"
 #include "kernels.h"
+#include "nak_hybrid.h"
 #include "summary.h"
 #include "wave_sched.h"
 
@@ -352,6 +353,35 @@ __device__ inline void nak_rerun_finish(const RerunLaunch& RL, int64_t e,
   }
 }
 
+// a hybrid re-run that ended on the closed form: the record and summary the engine would
+// have written for the same head (nak_rerun_finish's fields; rewards in units of 1/32)
+__device__ inline void nak_hybrid_finish(const RerunLaunch& RL, int64_t e, const Stream& S,
+                                         const HybridResult& R, uint32_t flags,
+                                         uint32_t est) {
+  const uint32_t resolved =
+      CPR_ST_DEEP_FORK | CPR_ST_TIE_UNRESOLVED | CPR_ST_STALE_TIME | CPR_ST_CAPACITY;
+  const uint32_t status = (flags & ~(uint32_t)CPR_ST_CAPACITY) | est | CPR_ST_EXACT_RERUN;
+  const int32_t ra = R.hd.ra * 32, rd = (R.hd.h - R.hd.ra) * 32;
+  const double rel = (ra + rd) != 0 ? (double)ra / (double)(ra + rd) : 0.0;
+  summary_add_episode(RL.sum, (int64_t)ra << 15, (int64_t)rd << 15, (int64_t)R.hd.h << 20, rel,
+                      R.hd.h, R.steps, R.acts, (flags & ~resolved) | est | CPR_ST_EXACT_RERUN);
+  if (RL.recs) {
+    cpr_episode_record rc;
+    rc.reward_attacker = (double)ra / 32.0;
+    rc.reward_defender = (double)rd / 32.0;
+    rc.progress = (double)R.hd.h;
+    rc.chain_time = R.hd.tm;
+    rc.sim_time = R.now;
+    rc.n_steps = R.steps;
+    rc.n_activations = R.acts;
+    rc.head_height = R.hd.h;
+    rc.head_miner = miner_of(RL.NP, S, R.hd.k);
+    rc.status = status;
+    rc.head_work = 0;
+    RL.recs[e] = rc;
+  }
+}
+
 // one flagged episode again on the event engine, lane region `base` (HBM) and lane_lds:
 // everything but the block ring (visibility, event heap, tips, scratch) in LDS. A lane
 // whose heap capacity does not fit runs with the capacity that does (the heap's node order
@@ -360,7 +390,7 @@ __device__ inline void nak_rerun_finish(const RerunLaunch& RL, int64_t e,
 // nodes, whose dependent walks are L2 round trips in HBM
 __device__ inline void rerun_episode(const RerunLaunch& RL, int64_t e, uint32_t flags,
                                      uint8_t* base, uint8_t* lane_lds, int64_t lds_bytes,
-                                     const uint32_t* queue_n) {
+                                     const uint32_t* queue_n, double* hring = nullptr) {
   const eth::EthParams P = RL.P;
   // attempt 0: LDS (full or reduced heap capacity); attempt 1 (only after the reduced
   // heap overflowed): the lane's HBM region
@@ -381,6 +411,28 @@ __device__ inline void rerun_episode(const RerunLaunch& RL, int64_t e, uint32_t 
                               ? eth::eth_mem_split(base, lane_lds, PA.cap_b, PA.cap_e, PA.n)
                               : eth::eth_mem_at(base, P.cap_b, P.cap_e, P.n);
     eth::EthLane L;
+    if (RL.hybrid && !RL.is_trace) {
+      // the closed form with the engine around the flagged windows (nak_hybrid.h); its
+      // lane state after the engine's region
+      const Stream S = make_stream(RL.seed, RL.first + (uint64_t)e);
+      LaneMem LM = hybrid_mem(base + eth::eth_lane_bytes(P.cap_b, P.cap_e, P.n), RL.NP.cap);
+      // block times feed only the record's chain_time: a summary-only launch skips them;
+      // the private-chain ring in the workgroup's LDS (hring) rather than HBM
+      LM.times = RL.recs != nullptr;
+      if (hring) LM.ring = hring;
+      NakLane NL;
+      const HybridResult R = nak_hybrid_episode(RL.NP, PA, S, LM, M, L, NL);
+      if (attempt == 0 && R.entries && L.dead == 2 && PA.cap_e < P.cap_e) {
+        atomicAdd(const_cast<uint32_t*>(queue_n) + 1, 1u);
+        continue;
+      }
+      const uint32_t est = R.entries ? L.status : 0u;
+      if (R.closed)
+        nak_hybrid_finish(RL, e, S, R, flags, est);
+      else
+        nak_rerun_finish(RL, e, P, M, L, R.ehd, flags);
+      break;
+    }
     uint32_t miss = 0;
     const int32_t hd = nak_rerun_entry(RL, e, PA, M, L, &miss);
     if (attempt == 0 && L.dead == 2 && PA.cap_e < P.cap_e) {  // outgrew LDS: count, redo
@@ -398,14 +450,15 @@ __global__ __launch_bounds__(64) void k_nak_exact_rerun(const RerunLaunch* launc
                                                          int64_t queue_cap, uint8_t* mem,
                                                          int64_t lane_bytes, int64_t lds_bytes) {
   extern __shared__ __attribute__((aligned(128))) uint8_t lane_lds[];
-  if (threadIdx.x != 0) return;  // one dependent chain per episode: lane 0 runs it
+  __shared__ double hring[RING];  // a hybrid's private-chain ring (nak_hybrid.h)
   int64_t nq = (int64_t)*queue_n;
   nq = nq < queue_cap ? nq : queue_cap;
   uint8_t* base = mem + (int64_t)blockIdx.x * lane_bytes;
+  if (threadIdx.x != 0) return;  // one dependent chain per episode: lane 0 runs it
   for (int64_t r = blockIdx.x; r < nq; r += gridDim.x) {
     const int64_t q = queue[r];
     rerun_episode(launches[q >> 40], (q >> 8) & 0xffffffffll, (uint32_t)(q & 0xff), base,
-                  lane_lds, lds_bytes, queue_n);
+                  lane_lds, lds_bytes, queue_n, hring);
   }
 }
 
@@ -439,8 +492,9 @@ __global__ __launch_bounds__(64) void k_rerun_overflow(const RerunLaunch* launch
   }
 }
 
-// LDS per one-wave workgroup: up to the whole 160 KiB of a CU when the launch needs it
-constexpr int64_t kRerunLdsMax = 160 * 1024;
+// LDS per one-wave workgroup: up to a whole CU's 160 KiB when the launch needs it, less the
+// kernel's static hybrid ring (256 bytes kept)
+constexpr int64_t kRerunLdsMax = 160 * 1024 - 256;
 
 hipError_t launch_nak_exact_rerun(const RerunLaunch* launches, int64_t n_launches,
                                   const int64_t* queue, const uint32_t* queue_n,

@@ -174,3 +174,22 @@ def test_ethereum_window_lane_matches_oracle_fuzz():
     assert out["mismatches"] == 0, p.stderr[-2000:]
     assert out["episodes"] > 1000 and out["steps"] > 400000
     assert out["tie_episodes"] > 20 and out["overlaps"] > 20  # both hazards exercised
+
+
+def test_hybrid_rerun_equals_whole_episode_engine():
+    # tests/native/hybrid_vs_exact.cpp: the hybrid exact re-run (cpr_amd/csrc/nak_hybrid.h:
+    # the closed-form lane, the event engine from the last quiescent trivial point before a
+    # flagged window to the first one after it) against the whole episode on the event
+    # engine in Nakamoto mode (the re-run it replaces), host builds on the same keyed
+    # stream: rewards, height, chain time, head miner, steps, activations, sim time and the
+    # engine's status for 5 alphas x 3 gammas x 4 propagation delays (up to 0.3, where most
+    # windows overlap) x 5 policies (a random table among them)
+    subprocess.run(["make", "-s", "-C", str(ROOT / "tests" / "native")], check=True)
+    exe = ROOT / "tests" / "native" / "build" / "hybrid_vs_exact"
+    p = subprocess.run([str(exe), "8", "2016"], capture_output=True, text=True, timeout=600)
+    out = json.loads(p.stdout.strip().splitlines()[-1])
+    assert p.returncode == 0, p.stderr[-2000:]
+    assert out["mismatches"] == 0, p.stderr[-2000:]
+    assert out["episodes"] == 2400 and out["activations"] > 4_000_000
+    # both directions exercised many times: the engine entered and left again
+    assert out["entered"] > 1000 and out["entries"] > 50_000 and out["ended_closed"] > 1000
