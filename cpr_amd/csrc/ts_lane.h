@@ -101,6 +101,9 @@ struct TsParams {
 };
 
 constexpr int32_t NFR = 64;      // common-ancestor frontier (reference walk, tests only)
+// optimal quorum: prefixes the search visits before it flags the episode (the oracle's
+// TS_BRUTE_FORCE_BUDGET)
+constexpr int64_t TS_OPT_BUDGET = 100000;
 
 // the list view of a vertex slot, beside the 64-byte vertices (TsMem.trec): the walks over a
 // summary's vote list and child-summary list (tree, count_post, observe, payload_parent,
@@ -851,52 +854,61 @@ struct TsLane {
     }
     if (nck > 100) return heuristic(P, M, node, n, q);
     if (n < P.k) return 0;
-    {  // brute-force budget (oracle/src/tailstorm.h TS_BRUTE_FORCE_BUDGET): the reference's
-       // overflowed n_choose_k can send it through millions of choices
-      int64_t kk = P.k < n - P.k ? P.k : n - P.k;
-      double r = 1.0;
-      for (int64_t i = 1; i <= kk; ++i) r = r * (double)(n - kk + i) / (double)i;
-      if (r > 100000.5) {
-        fail(12);
-        return 0;
-      }
-    }
     // a = BlockSet order; pos[cand index] = position in a (M.aux)
     for (int32_t pi = 0; pi < n; ++pi) M.aux[M.perm[pi]] = pi;
+    // The reference's subsets in its lexicographic order (iter_n_choose_k), minus the
+    // prefixes no completion of which can count (oracle/src/tailstorm.cpp TsView::optimal):
+    // the newest vote's vote parent not chosen (Not_connected), or own votes chosen plus
+    // min(slots left, own votes after it) worth at most maxdepth / k (discount) or 1 each,
+    // summed as the reward sums them, not above the best so far (strict >). Per position:
+    // par = its vote parent's position (-1 a summary), own, and own votes after it
+    // (M.key as int32 pairs: positions are < cap_v). The search stops after
+    // TS_OPT_BUDGET prefixes (= oracle/src/tailstorm.h TS_BRUTE_FORCE_BUDGET) and flags
+    // the episode.
+    int32_t* par = reinterpret_cast<int32_t*>(M.key);
+    int32_t* oaft = par + n;  // own votes at positions > i, [n + 1]
+    int32_t maxdepth = 0;
+    for (int32_t i = 0; i < n; ++i) {
+      const TVtx& x = X(P, M, M.cand[M.perm[i]]);
+      par[i] = x.parent != troot ? M.aux[PS(P, M, x.parent)] : -1;
+      maxdepth = x.depth > maxdepth ? x.depth : maxdepth;
+    }
+    oaft[n] = 0;
+    for (int32_t i = n - 1; i >= 0; --i)
+      oaft[i] = oaft[i + 1] + (X(P, M, M.cand[M.perm[i]]).who == node ? 1 : 0);
+    const bool disc = P.scheme == SC_DISCOUNT || P.scheme == SC_HYBRID;
+    const double rmax = disc ? (double)maxdepth / (double)P.k * 1.0 : 1.0;
     int32_t* c = M.stack;        // current choice (k <= 64); stack is free here
     int32_t* lv = M.stack + 64;  // leaves of the choice
-    for (int32_t t = 0; t < P.k; ++t) c[t] = t;
+    // [n]: position chosen in the current prefix (stack holds 2 cap_v ints, n <= cap_v)
+    uint8_t* chosen = reinterpret_cast<uint8_t*>(M.stack + 128);
+    for (int32_t i = 0; i < n; ++i) chosen[i] = 0;
     double best = -1.0;
     int32_t nbest = 0;
+    int64_t visits = 0;
+    int32_t j = 0, nxt = 0, ownp = 0;
     for (;;) {
-      // leaves c (tailstorm.ml:442-481): reach (flag) and leave (flag2) over positions
-      for (int32_t i = 0; i < n; ++i) {
-        M.flag[i] = 0;
-        M.flag2[i] = 1;
-      }
-      bool ok = true;
-      for (int32_t t = 0; t < P.k && ok; ++t) {
-        const TVtx& x = X(P, M, M.cand[M.perm[c[t]]]);
-        if (x.parent != troot) {  // vote parent (summary parents are filtered out)
-          const int32_t ji = PS(P, M, x.parent);
-          const int32_t ip = M.aux[ji];
-          M.flag2[ip] = 0;
-          ok = M.flag[ip] != 0;
+      if (j == P.k) {
+        // leaves c (tailstorm.ml:442-481): reach (flag) and leave (flag2) over positions
+        for (int32_t i = 0; i < n; ++i) {
+          M.flag[i] = 0;
+          M.flag2[i] = 1;
         }
-        if (ok) M.flag[c[t]] = 1;
-      }
-      if (ok) {
+        for (int32_t t = 0; t < P.k; ++t) {
+          if (par[c[t]] >= 0) M.flag2[par[c[t]]] = 0;
+          M.flag[c[t]] = 1;
+        }
         int32_t nl = 0;
         for (int32_t i = 0; i < n; ++i)
           if (M.flag[i] && M.flag2[i]) lv[nl++] = M.cand[M.perm[i]];
         for (int32_t i = 1; i < nl; ++i) {  // sort by compare_votes_in_block (unique keys)
           const int32_t v = lv[i];
-          int32_t j = i;
-          while (j > 0 && vote_before(X(P, M, v), X(P, M, lv[j - 1]))) {
-            lv[j] = lv[j - 1];
-            --j;
+          int32_t u = i;
+          while (u > 0 && vote_before(X(P, M, v), X(P, M, lv[u - 1]))) {
+            lv[u] = lv[u - 1];
+            --u;
           }
-          lv[j] = v;
+          lv[u] = v;
         }
         const double r = draft_reward(P, M, node, n, lv, nl);
         if (r > best) {
@@ -904,13 +916,45 @@ struct TsLane {
           nbest = nl;
           for (int32_t i = 0; i < nl; ++i) q[i] = lv[i];
         }
+        // back to the last choice; the next index there
+        --j;
+        chosen[c[j]] = 0;
+        ownp -= X(P, M, M.cand[M.perm[c[j]]]).who == node ? 1 : 0;
+        nxt = c[j] + 1;
+        continue;
       }
-      // next combination in lexicographic order (iter_n_choose_k)
-      int32_t t = P.k - 1;
-      while (t >= 0 && c[t] == n - P.k + t) --t;
-      if (t < 0) break;
-      ++c[t];
-      for (int32_t u = t + 1; u < P.k; ++u) c[u] = c[u - 1] + 1;
+      int32_t placed = -1;
+      for (int32_t i = nxt; i <= n - (P.k - j) && !dead; ++i) {
+        if (par[i] >= 0 && !chosen[par[i]]) continue;  // every completion Not_connected
+        const int32_t oi = X(P, M, M.cand[M.perm[i]]).who == node ? 1 : 0;
+        const int32_t rest = P.k - j - 1 < oaft[i + 1] ? P.k - j - 1 : oaft[i + 1];
+        const int32_t cap = ownp + oi + rest;
+        if (nbest > 0) {  // cannot beat the best: rmax added cap times
+          double bnd = 0.0;
+          for (int32_t m = 0; m < cap; ++m) bnd += rmax;
+          if (bnd <= best) continue;
+        }
+        if (++visits > TS_OPT_BUDGET) {
+          fail(12);
+          return 0;
+        }
+        placed = i;
+        ownp += oi;
+        break;
+      }
+      if (dead) return 0;
+      if (placed >= 0) {
+        c[j] = placed;
+        chosen[placed] = 1;
+        ++j;
+        nxt = placed + 1;
+        continue;
+      }
+      if (j == 0) break;
+      --j;
+      chosen[c[j]] = 0;
+      ownp -= X(P, M, M.cand[M.perm[c[j]]]).who == node ? 1 : 0;
+      nxt = c[j] + 1;
     }
     if (nbest == 0) fail(11);  // "reward_optim_quorum: no choice"
     return nbest;

@@ -326,26 +326,96 @@ bool TsView::heuristic(Block* b, const VFilter& vf, std::vector<Block*>* q) cons
   return true;
 }
 
-// tailstorm.ml:418-500 (max_options = 100)
-bool TsView::optimal(Block* b, const VFilter& vf, std::vector<Block*>* q) const {
+// tailstorm.ml:418-500 (max_options = 100). The reference visits the k-subsets of the
+// candidate votes (BlockSet order) in lexicographic order (iter_n_choose_k), skips the
+// ones that are not connected (a vote whose vote parent is not chosen), and keeps the
+// first of maximal reward. `brute` = 1 restates that literally. The default enumerates the
+// same subsets in the same order but (a) drops a prefix as soon as its newest vote's vote
+// parent is not in it — every completion is `Not_connected` — and (b) drops a prefix whose
+// best completion cannot reward more than the best so far: own votes chosen plus
+// min(slots left, own votes after the prefix's last index), each worth at most the
+// largest depth / k (discount) or 1, summed as the reward sums them. A dropped subset is
+// either skipped by the reference too or cannot replace its maximum (strict >), so the
+// result is the reference's (tests/native/optimal_quorum_bnb.cpp checks it against the
+// literal one). The search stops at TS_BRUTE_FORCE_BUDGET prefixes (BudgetExceeded).
+// tests (tests/native/optimal_quorum_bnb.cpp): re-derive every pruned search's result by
+// the literal enumeration, whose budget they raise
+int64_t g_ts_brute_budget = TS_BRUTE_FORCE_BUDGET;
+OptimalCheck g_ts_optimal_check;
+
+bool TsView::optimal(Block* b, const VFilter& vf, std::vector<Block*>* q, bool brute) const {
+  if (!brute && g_ts_optimal_check.on) {
+    std::vector<Block*> q1, q2;
+    bool r1 = false, r2 = false, x1 = false, x2 = false;
+    g_ts_optimal_check.on = false;
+    try {
+      r1 = optimal(b, vf, &q1, false);
+    } catch (BudgetExceeded&) {
+      x1 = true;
+    } catch (std::exception& ex) {
+      fprintf(stderr, "OPTCHECK: pruned search raised %s (n = %d, k = %d)\n", ex.what(),
+              (int)votes_below(b, vf).size(), k);
+      g_ts_optimal_check.on = true;
+      throw;
+    }
+    bool e2 = false;
+    try {
+      r2 = optimal(b, vf, &q2, true);
+    } catch (BudgetExceeded&) {
+      x2 = true;
+    } catch (std::exception& ex) {
+      e2 = true;
+      fprintf(stderr, "OPTCHECK: literal search raised %s (n = %d, k = %d)\n", ex.what(),
+              (int)votes_below(b, vf).size(), k);
+    }
+    if (e2) ++g_ts_optimal_check.mismatches;
+    if (x2) ++g_ts_optimal_check.unverified;
+    g_ts_optimal_check.on = true;
+    if (!x2) {
+      ++g_ts_optimal_check.compared;
+      const int64_t nv = (int64_t)votes_below(b, vf).size();
+      // (the literal search completed, so n_choose_k did not raise)
+      if (nv >= k && ocaml_n_choose_k(nv, k) <= 100 &&
+          true_n_choose_k_saturated(nv, k) > TS_BRUTE_FORCE_BUDGET)
+        ++g_ts_optimal_check.large;
+      if (x1 || r1 != r2 || q1 != q2) ++g_ts_optimal_check.mismatches;
+    }
+    if (x1) throw BudgetExceeded();
+    *q = q1;
+    return r1;
+  }
   const BlockSet votes = votes_below(b, vf);
   std::vector<Block*> a(votes.begin(), votes.end());
   const int n = (int)a.size();
   if (ocaml_n_choose_k(n, k) > 100) return heuristic(b, vf, q);
   if (n < k) return false;
-  if (true_n_choose_k_saturated(n, k) > TS_BRUTE_FORCE_BUDGET) throw BudgetExceeded();
+  if (brute && true_n_choose_k_saturated(n, k) > g_ts_brute_budget) throw BudgetExceeded();
   auto index_of = [&](Block* x) {
     for (int i = 0; i < n; ++i)
       if (a[i] == x) return i;
     throw std::runtime_error("Not_found in BlockMap");
   };
-  std::vector<char> reach(n), leave(n);
+  // vote parent's index (-1: a summary), own flags, own votes after each index
+  std::vector<int> par(n, -1), own(n), own_after(n + 1, 0);
+  int maxdepth = 0;
+  for (int i = 0; i < n; ++i) {
+    for (auto* p : parents(a[i]))
+      if (is_vote(p)) par[i] = index_of(p);
+    own[i] = a[i]->value.miner == view ? 1 : 0;
+    maxdepth = std::max(maxdepth, ts_depth(a[i]));
+  }
+  for (int i = n - 1; i >= 0; --i) own_after[i] = own_after[i + 1] + own[i];
+  const bool discount = scheme == TS_DISCOUNT || scheme == TS_HYBRID;
+  const double rmax = discount ? (double)maxdepth / (double)k * 1. : 1.;
+  std::vector<double> bound(k + 1, 0.);  // bound[m] = rmax added m times
+  for (int m = 1; m <= k; ++m) bound[m] = bound[m - 1] + rmax;
+  std::vector<char> reach(n), leave(n), chosen(n, 0);
   double opt_reward = -1.;
   bool have = false;
   std::vector<Block*> best;
   std::vector<int> c(k);
-  // iter_n_choose_k: increasing choices in lexicographic order
-  std::function<void(int, int)> iter = [&](int s, int j) {
+  int64_t visits = 0;
+  std::function<void(int, int, int)> iter = [&](int s, int j, int ownp) {
     if (j == k) {
       std::fill(reach.begin(), reach.end(), 0);
       std::fill(leave.begin(), leave.end(), 1);
@@ -379,11 +449,19 @@ bool TsView::optimal(Block* b, const VFilter& vf, std::vector<Block*>* q) const 
       return;
     }
     for (int i = s; i <= n - 1; ++i) {
+      if (!brute) {
+        if (par[i] >= 0 && !chosen[par[i]]) continue;  // every completion Not_connected
+        const int cap = ownp + own[i] + std::min(k - j - 1, own_after[i + 1]);
+        if (have && bound[cap] <= opt_reward) continue;  // cannot beat the best
+        if (++visits > TS_BRUTE_FORCE_BUDGET) throw BudgetExceeded();
+      }
       c[j] = i;
-      iter(i + 1, j + 1);
+      chosen[i] = 1;
+      iter(i + 1, j + 1, ownp + own[i]);
+      chosen[i] = 0;
     }
   };
-  iter(0, 0);
+  iter(0, 0, 0);
   if (!have) throw std::runtime_error("reward_optim_quorum: no choice");
   *q = best;
   return true;

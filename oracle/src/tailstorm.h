@@ -54,13 +54,23 @@ TsObs ts_obs_of_floats(const double in[TS_OBS_LEN], bool unit, int k);
 int64_t ocaml_n_choose_k(int64_t n, int64_t k);
 // For n >= 21 the reference's n_choose_k overflows and often returns <= 100, so the
 // optimal quorum brute-forces the true C(n, k) choices (e.g. 48 million for n = 38, k = 8).
-// Both engines stop such a search at this budget and flag the episode (not a semantic
-// difference: an episode either completes identically or is flagged on both sides).
+// Both engines enumerate the same choices in the same order but skip prefixes that cannot
+// be connected or cannot beat the best reward so far (TsView::optimal), and stop after this
+// many prefixes, flagging the episode (on both sides identically)
 constexpr int64_t TS_BRUTE_FORCE_BUDGET = 100000;
 struct BudgetExceeded : std::runtime_error {
   BudgetExceeded() : std::runtime_error("optimal quorum: brute-force budget exceeded") {}
 };
 int64_t true_n_choose_k_saturated(int64_t n, int64_t k);  // saturates at INT64_MAX
+// tests: the literal enumeration's budget, and a mode in which every optimal quorum is
+// computed both ways and compared (compared: literal searches that completed; large: of
+// those, with more than TS_BRUTE_FORCE_BUDGET choices)
+extern int64_t g_ts_brute_budget;
+struct OptimalCheck {
+  bool on = false;
+  int64_t compared = 0, large = 0, mismatches = 0, unverified = 0;  // unverified: over budget
+};
+extern OptimalCheck g_ts_optimal_check;
 
 struct DagCmp {
   bool operator()(const Block* a, const Block* b) const {
@@ -97,7 +107,8 @@ struct TsView {
   bool quorum(Block* b, const VFilter& vf, std::vector<Block*>* q) const;
   bool altruistic(Block* b, const VFilter& vf, std::vector<Block*>* q) const;
   bool heuristic(Block* b, const VFilter& vf, std::vector<Block*>* q) const;
-  bool optimal(Block* b, const VFilter& vf, std::vector<Block*>* q) const;
+  // brute = true: the reference's literal enumeration (tests only)
+  bool optimal(Block* b, const VFilter& vf, std::vector<Block*>* q, bool brute = false) const;
   Draft puzzle_payload(Block* b, const VFilter& vf) const;
   bool next_summary(Block* b, const VFilter& vf, Draft* d) const;
   int compare_blocks(const VFilter& vf, Block* a, Block* b) const;

@@ -393,6 +393,13 @@ int main(int argc, char** argv) {
   g_sel = argc > 4 ? atoi(argv[4]) : 1;
   const uint64_t seed = 0x7A110000ull + (uint64_t)k * 16 + (uint64_t)g_sel;
   std::vector<Cfg> cfgs;
+  // OPTCHECK=<budget>: every optimal quorum of the oracle is also computed by the
+  // reference's literal enumeration (up to <budget> choices) and compared with the pruned
+  // search both engines run (oracle/src/tailstorm.cpp TsView::optimal)
+  if (const char* oc = getenv("OPTCHECK")) {
+    oracle::g_ts_optimal_check.on = true;
+    oracle::g_ts_brute_budget = atoll(oc);
+  }
   if (const char* prof = getenv("TSPROF")) {
     // lane only (host profiling, tools: gprof): "policy,episodes" of bench.py configs[3]
     // (two agents, alpha .33, 10^4 activations, discount rewards, selection argv[4])
@@ -426,9 +433,11 @@ int main(int argc, char** argv) {
       std::string why;
       if (!run_loop(cf, sd, e, C, why)) fprintf(stderr, "MISMATCH ep=%d: %s\n", e, why.c_str());
     }
-    printf("{\"episodes\": %ld, \"mismatches\": %ld, \"capacity\": %ld, \"raises\": %ld}\n",
-           C.episodes, C.mismatches, C.capacity, C.raises);
-    return C.mismatches ? 1 : 0;
+    const auto& oc = oracle::g_ts_optimal_check;
+    printf("{\"episodes\": %ld, \"mismatches\": %ld, \"capacity\": %ld, \"raises\": %ld, \"opt_compared\": %ld, \"opt_large\": %ld, \"opt_mismatches\": %ld, \"opt_unverified\": %ld}\n",
+           C.episodes, C.mismatches, C.capacity, C.raises, (long)oc.compared, (long)oc.large,
+           (long)oc.mismatches, (long)oc.unverified);
+    return (C.mismatches || oc.mismatches) ? 1 : 0;
   }
   const double alphas[] = {0.1, 0.25, 0.33, 0.45};
   const double gammas[] = {0.0, 0.5, 0.9};
@@ -476,7 +485,9 @@ int main(int argc, char** argv) {
                 why.c_str());
       }
     }
-  printf("{\"episodes\": %ld, \"steps\": %ld, \"mismatches\": %ld, \"capacity\": %ld, \"raises\": %ld, \"budget\": %ld}\n",
-         C.episodes, C.steps, C.mismatches, C.capacity, C.raises, C.budget);
-  return C.mismatches ? 1 : 0;
+  const auto& oc = oracle::g_ts_optimal_check;
+  printf("{\"episodes\": %ld, \"steps\": %ld, \"mismatches\": %ld, \"capacity\": %ld, \"raises\": %ld, \"budget\": %ld, \"opt_compared\": %ld, \"opt_large\": %ld, \"opt_mismatches\": %ld, \"opt_unverified\": %ld}\n",
+         C.episodes, C.steps, C.mismatches, C.capacity, C.raises, C.budget, (long)oc.compared,
+         (long)oc.large, (long)oc.mismatches, (long)oc.unverified);
+  return (C.mismatches || oc.mismatches) ? 1 : 0;
 }

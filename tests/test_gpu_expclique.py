@@ -161,18 +161,14 @@ def test_random_attacker_matches_oracle(ctx, name, proto, pol, k, scheme, sel):
     b = device.Batch(cfg, ctx=ctx, keep=keep)
     n = 2048
     s, rec = b.run(n, records=True)
-    # the one invalid outcome allowed: optimal quorum selection whose brute-force search
-    # (tailstorm.ml:271-507, entered when OCaml's overflowed n_choose_k says <= 100) would
-    # visit more than the 10^5 choices of the lane's and the oracle's budget
-    # (oracle/src/tailstorm.h TS_BRUTE_FORCE_BUDGET; CPR_ST_CAPACITY): a random attacker's
-    # withheld votes reach it in ~1 % of episodes (the reference's test runs one
-    # simulation); the oracle flags the same episodes
+    # optimal quorum selection (tailstorm.ml:418-507) brute-forces up to tens of millions
+    # of choices when OCaml's overflowed n_choose_k says <= 100 (~1 % of these episodes);
+    # both engines search the same choices in the same order with provably inert prefixes
+    # skipped (oracle/src/tailstorm.cpp TsView::optimal), so every episode completes
+    # (tests/test_lane_fuzz.py::test_optimal_quorum_pruned_search_equals_literal checks
+    # the pruned search against the literal one on these 2048 episodes' shape)
     inv = (rec["status"] & L.ST_INVALID) != 0
-    if sel == L.SELECT_OPTIMAL:
-        assert not (rec["status"][inv] & (L.ST_INVALID & ~L.ST_CAPACITY)).any(), name
-        assert inv.mean() < 0.05, (name, inv.mean())
-    else:
-        assert not inv.any(), name
+    assert not inv.any(), (name, int(inv.sum()))
     ref = O.run_episodes(cfg, 0, 64, threads=8)
     ref_inv = (ref["status"] & L.ST_INVALID) != 0
     assert np.array_equal(inv[:64], ref_inv), name

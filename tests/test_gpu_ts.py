@@ -4,9 +4,9 @@ Every record field is bit-identical: per-node rewards are accumulated in the ref
 fp64 order (set_rewards adds r per confirmed vote; the head's defender reward is the left
 fold over nodes), heights are integers and event times follow the same IEEE operation
 sequence on both sides. Episodes in which the reference raises (the oracle catches the
-exception and records CPR_ST_REFERENCE_RAISES) or whose optimal quorum exceeds the
-brute-force budget (CPR_ST_CAPACITY on both sides) must be flagged identically on the
-device; the lane's own capacities must never be hit at these configurations, and flagged
+exception and records CPR_ST_REFERENCE_RAISES) or whose optimal quorum search would pass
+its budget (pruned, so not reached at these configurations; CPR_ST_CAPACITY on both
+sides) must be flagged identically on the device; the lane's own capacities must never be hit at these configurations, and flagged
 episodes stay out of the summary (cpr_summary.invalid).
 """
 

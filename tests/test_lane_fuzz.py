@@ -193,3 +193,31 @@ def test_hybrid_rerun_equals_whole_episode_engine():
     assert out["episodes"] == 2400 and out["activations"] > 4_000_000
     # both directions exercised many times: the engine entered and left again
     assert out["entered"] > 1000 and out["entries"] > 50_000 and out["ended_closed"] > 1000
+
+
+def test_optimal_quorum_pruned_search_equals_literal():
+    # Tailstorm's optimal sub-block selection (tailstorm.ml:418-507): both engines enumerate
+    # the reference's k-subsets in its lexicographic order but skip prefixes that cannot be
+    # connected or cannot beat the best reward so far. OPTCHECK makes the oracle recompute
+    # every selection with the reference's literal enumeration (here up to 3e7 choices) and
+    # compare, while tests/native/ts_vs_oracle.cpp compares the lane with the oracle step by
+    # step: (1) the random-attacker exp-clique case of tests/test_gpu_expclique.py (seed 9,
+    # constant rewards, 1000 activations; its large searches used to exceed the old 1e5
+    # budget in ~1 % of episodes), (2) gym episodes with optimal selection
+    subprocess.run(["make", "-s", "-C", str(ROOT / "tests" / "native")], check=True)
+    exe = ROOT / "tests" / "native" / "build" / "ts_vs_oracle"
+    env = dict(os.environ, OPTCHECK="30000000", TSCASE="2,10,0,100,1.0,1000,9,0,256")
+    p = subprocess.run([str(exe), "1", "1", "8", "2"], capture_output=True, text=True,
+                       timeout=600, env=env)
+    out = json.loads(p.stdout.strip().splitlines()[-1])
+    assert p.returncode == 0, p.stderr[-2000:]
+    assert out["mismatches"] == 0 and out["capacity"] == 0 and out["episodes"] == 256
+    assert out["opt_mismatches"] == 0 and out["opt_unverified"] == 0
+    assert out["opt_compared"] > 100_000 and out["opt_large"] > 0
+    env = dict(os.environ, OPTCHECK="30000000")
+    p = subprocess.run([str(exe), "2", "300", "8", "2"], capture_output=True, text=True,
+                       timeout=600, env=env)
+    out = json.loads(p.stdout.strip().splitlines()[-1])
+    assert p.returncode == 0, p.stderr[-2000:]
+    assert out["mismatches"] == 0 and out["budget"] == 0
+    assert out["opt_mismatches"] == 0 and out["opt_compared"] > 100_000

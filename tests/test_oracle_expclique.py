@@ -53,9 +53,8 @@ def test_exp_clique_config():
 # random action of its attack space at every decision (Random.int A.Action.n; here the
 # keyed draw of include/cpr_hip.h *_POLICY_RANDOM), 3-node symmetric clique, activation
 # delay 100, exponential(1) links, 1000 activations; the orphan rate must stay <= 0.5
-# (RANDOM_CASES: test_gpu_expclique.py). The 32 episodes of seed 9 include none that hit
-# the optimal selection's brute-force budget (flagged CAPACITY; the GPU test allows those
-# at ~1 %)
+# (RANDOM_CASES: test_gpu_expclique.py). Every episode completes: the optimal selection's
+# large searches (OCaml's overflowed n_choose_k) run pruned (oracle/src/tailstorm.cpp)
 @pytest.mark.parametrize("name,proto,pol,k,scheme,sel", RANDOM_CASES)
 def test_random_attacker_orphan_limit(name, proto, pol, k, scheme, sel):
     cfg, _ = exp_clique(proto, 2, pol, 1000, k=k, scheme=scheme, sel=sel, ad=100.0, seed=9)
