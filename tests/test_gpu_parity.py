@@ -181,6 +181,34 @@ def test_overlapping_windows_rerun_exactly(ctx, alpha, policy, table):
     assert s.status_other == 0
 
 
+@pytest.mark.parametrize("gamma,prop,policy", [(0.5, 0.05, L.POLICY_SAPIRSHTEIN_2016_SM1),
+                                               (0.5, 0.3, L.POLICY_HONEST),
+                                               (0.75, 0.05, L.POLICY_EYAL_SIRER_2014)])
+def test_hybrid_reruns_equal_whole_episode_reruns(ctx, gamma, prop, policy, monkeypatch):
+    # hybrid re-runs (cpr_amd/csrc/nak_hybrid.h: the closed form, the event engine only
+    # between quiescent trivial points around each flagged window) against whole-episode
+    # re-runs on the event engine (CPR_RERUN_HYBRID=0), on the device: every record field,
+    # status included, for 2016-step episodes at delays where nearly every episode
+    # overlaps, many times over
+    cfg, keep = device.make_config(alpha=0.4, gamma=gamma, policy=policy, max_steps=2016,
+                                   seed=0x4B1D, propagation_delay=prop)
+    b = device.Batch(cfg, ctx=ctx, keep=keep)
+    r0 = ctx.rerun_stats()
+    _, hyb = b.run(256, first_episode=0, records=True)
+    r1 = ctx.rerun_stats()
+    monkeypatch.setenv("CPR_RERUN_HYBRID", "0")
+    _, whole = b.run(256, first_episode=0, records=True)
+    r2 = ctx.rerun_stats()
+    assert _records_equal(hyb, whole) == {}
+    assert np.array_equal(hyb["status"], whole["status"])
+    assert ((hyb["status"] & L.ST_EXACT_RERUN) != 0).sum() > 200
+    # both re-ran the same episodes; the hybrid's flush is the shorter by far (the engine
+    # simulates only the stretches around the flagged windows)
+    assert r1[0] - r0[0] == r2[0] - r1[0]
+    print(f"re-run flush ms: hybrid {r1[2] - r0[2]:.1f}, whole episodes {r2[2] - r1[2]:.1f}")
+    assert r1[2] - r0[2] < r2[2] - r1[2]
+
+
 @pytest.mark.parametrize("lds_max", [None, 40960])
 def test_gamma0_reruns_exact_with_lds_heap(ctx, lds_max, monkeypatch):
     # gamma = 0 re-runs keep the +inf messages in the event heap (thousands of nodes in a
