@@ -86,7 +86,7 @@ ST_TRACE_MISS = 128
 ST_EXACT_RERUN = 256
 ST_INVALID = ST_CAPACITY | ST_REFERENCE_RAISES | ST_TRACE_MISS  # include/cpr_hip.h
 ST_LOCKSTEP_INEXACT = ST_OVERLAP | ST_DEEP_FORK | ST_TIE_UNRESOLVED | ST_STALE_TIME
-ABI_VERSION = 10  # include/cpr_hip.h CPR_ABI_VERSION this module's structures follow
+ABI_VERSION = 11  # include/cpr_hip.h CPR_ABI_VERSION this module's structures follow
 
 HIST_BINS = 64
 
@@ -326,6 +326,7 @@ EXPORTS = [
     "cpr_launch_shape",
     "cpr_rerun_hbm_retries",
     "cpr_rerun_stats",
+    "cpr_lockstep_coverage",
     "cpr_reset",
     "cpr_step",
     "cpr_observe_fields",
@@ -368,6 +369,7 @@ def _declare(L):
     L.cpr_launch_shape.argtypes = [vp, P(ctypes.c_int64), P(ctypes.c_int64)]
     L.cpr_rerun_hbm_retries.argtypes = [vp, P(ctypes.c_int64)]
     L.cpr_rerun_stats.argtypes = [vp, P(ctypes.c_int64), P(ctypes.c_int64), P(ctypes.c_double)]
+    L.cpr_lockstep_coverage.argtypes = [vp, P(ctypes.c_int64), P(ctypes.c_int64)]
     L.cpr_reset.argtypes = [vp, vp, vp, vp]
     L.cpr_step.argtypes = [vp, vp, vp, vp, vp, P(StepInfo)]
     L.cpr_observe_fields.argtypes = [vp, vp]

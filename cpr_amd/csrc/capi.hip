@@ -9,6 +9,7 @@
 #include <cstring>
 #include <memory>
 #include <string>
+#include <deque>
 #include <vector>
 
 #include "../../include/cpr_hip.h"
@@ -72,12 +73,16 @@ struct cpr_ctx {
   DevBuf rq, rtab, rmem;
   // cpr_rerun_stats: per flush, HIP events around the re-run kernels and the count of
   // episodes the launches since the previous flush queued (copied to pinned host memory
-  // before the counter is cleared); summed when the caller asks
+  // before the counter is cleared; e2 follows that copy). Every flush folds the records
+  // whose e2 has completed into rr_* and recycles them (drain_flush_recs), and waits for the
+  // oldest when kFlushRecMax are outstanding, so a context that never asks for the stats
+  // holds a bounded set of events and pinned words
   struct FlushRec {
-    hipEvent_t e0 = nullptr, e1 = nullptr;
+    hipEvent_t e0 = nullptr, e1 = nullptr, e2 = nullptr;
     uint32_t* cnt = nullptr;  // pinned host word
   };
-  std::vector<FlushRec> fl_pending, fl_free;
+  std::deque<FlushRec> fl_pending;
+  std::vector<FlushRec> fl_free;
   int64_t rr_episodes = 0, rr_flushes = 0;
   double rr_ms = 0.0;
   std::vector<RerunLaunch> rlaunch, rlaunch_up;
@@ -200,12 +205,14 @@ int cpr_ctx_destroy(cpr_ctx* c) {
   // pending work first: queued exact re-runs complete their callers' summaries and records
   (void)flush_reruns(c);
   (void)hipStreamSynchronize(c->stream);
-  for (auto* v : {&c->fl_pending, &c->fl_free})
-    for (cpr_ctx::FlushRec& r : *v) {
-      (void)hipEventDestroy(r.e0);
-      (void)hipEventDestroy(r.e1);
-      (void)hipHostFree(r.cnt);
-    }
+  c->fl_free.insert(c->fl_free.end(), c->fl_pending.begin(), c->fl_pending.end());
+  c->fl_pending.clear();
+  for (cpr_ctx::FlushRec& r : c->fl_free) {
+    (void)hipEventDestroy(r.e0);
+    (void)hipEventDestroy(r.e1);
+    (void)hipEventDestroy(r.e2);
+    (void)hipHostFree(r.cnt);
+  }
   (void)hipStreamDestroy(c->stream);
   c->rq.release();
   c->rtab.release();
@@ -842,24 +849,46 @@ int cpr_rerun_hbm_retries(cpr_ctx* c, int64_t* retries) {
   return CPR_OK;
 }
 
+// fold finished flush records (oldest first: one stream, so they finish in order) into the
+// totals and recycle them; wait: every one (cpr_rerun_stats), else only those done, plus the
+// oldest while more than kFlushRecMax are outstanding
+constexpr size_t kFlushRecMax = 32;
+
+static int drain_flush_recs(cpr_ctx* c, bool wait) {
+  while (!c->fl_pending.empty()) {
+    const cpr_ctx::FlushRec r = c->fl_pending.front();
+    if (wait || c->fl_pending.size() > kFlushRecMax) {
+      HIP_TRY(hipEventSynchronize(r.e2));
+    } else {
+      const hipError_t q = hipEventQuery(r.e2);
+      if (q == hipErrorNotReady) break;
+      HIP_TRY(q);
+    }
+    float t = 0.f;
+    HIP_TRY(hipEventElapsedTime(&t, r.e0, r.e1));
+    c->rr_ms += t;
+    c->rr_episodes += *r.cnt;
+    c->rr_flushes += 1;
+    c->fl_free.push_back(r);
+    c->fl_pending.pop_front();
+  }
+  return CPR_OK;
+}
+
 int cpr_rerun_stats(cpr_ctx* c, int64_t* episodes, int64_t* flushes, double* ms) {
   if (!c) return fail(CPR_E_INVALID_ARG, "NULL argument");
   HIP_TRY(hipSetDevice(c->device));
-  if (!c->fl_pending.empty()) {
-    HIP_TRY(hipStreamSynchronize(c->stream));
-    for (const cpr_ctx::FlushRec& r : c->fl_pending) {
-      float t = 0.f;
-      HIP_TRY(hipEventElapsedTime(&t, r.e0, r.e1));
-      c->rr_ms += t;
-      c->rr_episodes += *r.cnt;
-      c->rr_flushes += 1;
-      c->fl_free.push_back(r);
-    }
-    c->fl_pending.clear();
-  }
+  if (const int rc = drain_flush_recs(c, true)) return rc;
   if (episodes) *episodes = c->rr_episodes;
   if (flushes) *flushes = c->rr_flushes;
   if (ms) *ms = c->rr_ms;
+  return CPR_OK;
+}
+
+int cpr_lockstep_coverage(cpr_batch* b, int64_t* log_steps, int64_t* exact_slots) {
+  if (!b) return fail(CPR_E_INVALID_ARG, "NULL argument");
+  if (log_steps) *log_steps = b->l_alog.p ? b->alog_cap : 0;
+  if (exact_slots) *exact_slots = b->l_alog.p ? b->n_exact_slots : 0;
   return CPR_OK;
 }
 
@@ -958,7 +987,15 @@ static int flush_reruns(cpr_ctx* c) {
       if (const char* v = getenv("CPR_RERUN_WIDE_LDS")) lds_rest = std::min<int64_t>(rest, atoll(v));
     }
   }
-  HIP_TRY(c->rmem.ensure((size_t)lanes * (size_t)lb));
+  if (c->rmem.ensure((size_t)lanes * (size_t)lb) != hipSuccess) {
+    // the wide grid's regions do not fit: the default grid (its LDS mode), episodes looping
+    // over its workgroups, rather than failing the caller's synchronization
+    (void)hipGetLastError();
+    lanes = kRerunLanes;
+    lds_rest = rest;
+    HIP_TRY(c->rmem.ensure((size_t)lanes * (size_t)lb));
+  }
+  if (const int rc = drain_flush_recs(c, false)) return rc;
   cpr_ctx::FlushRec fr;
   if (!c->fl_free.empty()) {
     fr = c->fl_free.back();
@@ -966,6 +1003,7 @@ static int flush_reruns(cpr_ctx* c) {
   } else {
     HIP_TRY(hipEventCreate(&fr.e0));
     HIP_TRY(hipEventCreate(&fr.e1));
+    HIP_TRY(hipEventCreate(&fr.e2));
     HIP_TRY(hipHostMalloc((void**)&fr.cnt, sizeof(uint32_t)));
   }
   HIP_TRY(hipEventRecord(fr.e0, c->stream));
@@ -974,6 +1012,7 @@ static int flush_reruns(cpr_ctx* c) {
                                  lb, lds_rest, lanes, c->stream));
   HIP_TRY(hipEventRecord(fr.e1, c->stream));
   HIP_TRY(hipMemcpyAsync(fr.cnt, qn, sizeof(uint32_t), hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipEventRecord(fr.e2, c->stream));
   c->fl_pending.push_back(fr);
   HIP_TRY(hipMemsetAsync(qn, 0, 4, c->stream));
   c->ovf_chunk = 0;  // the next launches' flags follow these re-runs on the stream

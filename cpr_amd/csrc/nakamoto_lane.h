@@ -166,6 +166,12 @@ struct NakParams {
   uint64_t u_lazy;
 };
 
+// u_lazy = floor(exp(-2.5 delta / ev) 2^53): U < u_lazy gives dt > 2 delta with margin to
+// spare for the log's rounding
+inline uint64_t lazy_threshold(const NakParams& P) {
+  return (uint64_t)std::floor(std::exp(-2.5 * P.delta / P.ev) * 9007199254740992.0);
+}
+
 // the lazy clock (NakLane LZ) is exact when a delay above 2 delta cannot overlap anywhere in
 // the episode: ulp(t) <= delta / 4 for every reachable clock t (each delay is at most
 // 53 ln 2 ev < 40 ev, or +inf, which the lane handles apart), and max_steps alone ends it
@@ -176,12 +182,10 @@ inline bool lazy_clock_ok(const NakParams& P) {
   // (<= 2^14 steps: the race kernel's clock bound esum, <= 150500 a step, stays in 32 bits)
   if (P.max_steps <= 0 || P.max_steps > (1ll << 14)) return false;
   const double tmax = ((double)P.max_steps + 2.0) * P.ev * 40.0;
-  return std::ldexp(1.0, std::ilogb(tmax) - 52) <= P.delta / 4.0;
-}
-// u_lazy = floor(exp(-2.5 delta / ev) 2^53): U < u_lazy gives dt > 2 delta with margin to
-// spare for the log's rounding
-inline uint64_t lazy_threshold(const NakParams& P) {
-  return (uint64_t)std::floor(std::exp(-2.5 * P.delta / P.ev) * 9007199254740992.0);
+  if (!(std::ldexp(1.0, std::ilogb(tmax) - 52) <= P.delta / 4.0)) return false;
+  // delta > ~14.7 ev puts the threshold at 0: no uniform can skip the check, and the lane's
+  // skip test (u - 1 >= u_lazy - 1) would wrap and skip every one of them instead
+  return lazy_threshold(P) >= 2ull;
 }
 
 __host__ __device__ inline CPR_AI uint64_t all_mask(int32_t d) {

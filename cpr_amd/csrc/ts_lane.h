@@ -81,6 +81,10 @@ struct TVtx {
 };
 static_assert(sizeof(TVtx) == 64, "TVtx layout");
 
+// optimal quorum: prefixes the search visits before it flags the episode (the oracle's
+// TS_BRUTE_FORCE_BUDGET); TsParams.opt_budget, lowered only by the host fuzzer
+constexpr int64_t TS_OPT_BUDGET = 100000;
+
 struct TsParams {
   uint64_t t_att;
   int32_t d, n, net, mode;
@@ -98,12 +102,10 @@ struct TsParams {
   // fused-episode launches: device counter of episodes handed out beyond the first
   // lanes-many (zeroed before the launch); null = static grid-stride
   unsigned long long* next = nullptr;
+  int64_t opt_budget = TS_OPT_BUDGET;
 };
 
 constexpr int32_t NFR = 64;      // common-ancestor frontier (reference walk, tests only)
-// optimal quorum: prefixes the search visits before it flags the episode (the oracle's
-// TS_BRUTE_FORCE_BUDGET)
-constexpr int64_t TS_OPT_BUDGET = 100000;
 
 // the list view of a vertex slot, beside the 64-byte vertices (TsMem.trec): the walks over a
 // summary's vote list and child-summary list (tree, count_post, observe, payload_parent,
@@ -863,8 +865,9 @@ struct TsLane {
     // summed as the reward sums them, not above the best so far (strict >). Per position:
     // par = its vote parent's position (-1 a summary), own, and own votes after it
     // (M.key as int32 pairs: positions are < cap_v). The search stops after
-    // TS_OPT_BUDGET prefixes (= oracle/src/tailstorm.h TS_BRUTE_FORCE_BUDGET) and flags
-    // the episode.
+    // P.opt_budget prefixes (TS_OPT_BUDGET = oracle/src/tailstorm.h TS_BRUTE_FORCE_BUDGET)
+    // and flags the episode; both engines count the same prefixes (only those that can
+    // still reach k positions), so they flag the same searches at any budget.
     int32_t* par = reinterpret_cast<int32_t*>(M.key);
     int32_t* oaft = par + n;  // own votes at positions > i, [n + 1]
     int32_t maxdepth = 0;
@@ -934,7 +937,7 @@ struct TsLane {
           for (int32_t m = 0; m < cap; ++m) bnd += rmax;
           if (bnd <= best) continue;
         }
-        if (++visits > TS_OPT_BUDGET) {
+        if (++visits > P.opt_budget) {
           fail(12);
           return 0;
         }

@@ -10,6 +10,7 @@ launch; ``Batch.reset``/``Batch.step`` expose the per-step gym API over many lan
 import ctypes
 import math
 import os
+import warnings
 
 import numpy as np
 
@@ -181,6 +182,7 @@ class Batch:
         self.handle = h
         self.n_lanes = int(config.n_lanes)
         self.obs_len = self.observation_spec()[0]
+        self._coverage_warned = False
 
     def close(self):
         if self.handle:
@@ -264,7 +266,22 @@ class Batch:
         m = None if mask is None else np.ascontiguousarray(mask, dtype=np.uint8)
         e = None if episode_ids is None else np.ascontiguousarray(episode_ids, dtype=np.uint64)
         L.check(L.lib().cpr_reset(self.handle, L.ptr(m), L.ptr(e), L.ptr(obs)))
+        log_steps, _ = self.lockstep_coverage()
+        ms = int(self.config.max_steps)
+        if log_steps and 0 < ms < 2**30 and log_steps < ms and not self._coverage_warned:
+            self._coverage_warned = True
+            warnings.warn(f"{self.n_lanes} lockstep lanes x {ms}-step episodes exceed the "
+                          f"action-log budget: lanes leaving the closed form after step "
+                          f"{log_steps} keep its flags instead of an exact re-run",
+                          RuntimeWarning, stacklevel=2)
         return obs
+
+    def lockstep_coverage(self):
+        """(action-log steps, exact-engine slots) of the lockstep lanes
+        (cpr_lockstep_coverage); (0, 0) before the first reset or without exact lanes."""
+        s, k = ctypes.c_int64(), ctypes.c_int64()
+        L.check(L.lib().cpr_lockstep_coverage(self.handle, ctypes.byref(s), ctypes.byref(k)))
+        return s.value, k.value
 
     def step(self, actions, with_info=True):
         n = self.n_lanes

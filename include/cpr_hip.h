@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define CPR_ABI_VERSION 10
+#define CPR_ABI_VERSION 11
 
 typedef struct cpr_ctx cpr_ctx;
 typedef struct cpr_batch cpr_batch;
@@ -368,7 +368,11 @@ int cpr_run_episodes(cpr_batch* b, int64_t n_episodes, uint64_t first_episode,
 /* Same, asynchronous on the context's streams; summary must be a device pointer to a
  * zeroed cpr_summary and records (optional) a device pointer. Both are complete after
  * cpr_synchronize (Nakamoto: exact re-runs of flagged episodes, CPR_ST_EXACT_RERUN, run on
- * the context's second stream). */
+ * the context's stream at the next flush). Blocking point: a flush (cpr_synchronize, or one
+ * forced inside this call when the context's re-run table or overflow-flag chunks are full)
+ * waits for the stream to read how many episodes were queued, so that it can size the
+ * re-run grid; an _async call that forces one therefore returns only after the launches
+ * before it have finished. */
 int cpr_run_episodes_async(cpr_batch* b, int64_t n_episodes, uint64_t first_episode,
                            cpr_summary* summary_dev, cpr_episode_record* records_dev);
 int cpr_synchronize(cpr_ctx* ctx);
@@ -414,6 +418,15 @@ int cpr_rerun_hbm_retries(cpr_ctx* ctx, int64_t* retries);
  * milliseconds (HIP events on the context's stream). Synchronizes the stream if a flush is
  * pending. Diagnostic for bench.py, no reference counterpart. ABI v10. */
 int cpr_rerun_stats(cpr_ctx* ctx, int64_t* episodes, int64_t* flushes, double* ms);
+/* exact-replay coverage of this batch's lockstep lanes (Nakamoto closed-form lanes that
+ * leave the closed form continue on the exact engine from an action log): log_steps = the
+ * steps of each lane's action log, exact_slots = the engine slots shared by the lanes (both
+ * 0 before the first cpr_reset, or where no lane can leave the closed form). A lane whose
+ * episode is past log_steps, or that finds every slot taken, when it leaves the closed form
+ * keeps the closed form's status flags (not exact); log_steps < max_steps happens only
+ * beyond 4 GiB of logs (lanes x episode length). Diagnostic, no reference counterpart.
+ * ABI v11. */
+int cpr_lockstep_coverage(cpr_batch* b, int64_t* log_steps, int64_t* exact_slots);
 
 /* Lockstep env API over cfg->n_lanes lanes (host pointers).
  * reset: lanes with mask[i] != 0 (mask NULL = all) start episode episode_ids[i]

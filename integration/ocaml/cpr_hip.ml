@@ -12,7 +12,7 @@
 open Ctypes
 open Foreign
 
-let abi_version = 10
+let abi_version = 11
 
 (* ---- status codes and enums (cpr_status, cpr_protocol, cpr_network, cpr_mode) *)
 let ok = 0
@@ -212,6 +212,11 @@ let rerun_hbm_retries =
 let rerun_stats =
   foreign "cpr_rerun_stats"
     (ptr ctx @-> ptr int64_t @-> ptr int64_t @-> ptr double @-> returning int)
+;;
+
+let lockstep_coverage =
+  foreign "cpr_lockstep_coverage"
+    (ptr batch @-> ptr int64_t @-> ptr int64_t @-> returning int)
 ;;
 
 let reset =

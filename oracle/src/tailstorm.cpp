@@ -341,6 +341,7 @@ bool TsView::heuristic(Block* b, const VFilter& vf, std::vector<Block*>* q) cons
 // tests (tests/native/optimal_quorum_bnb.cpp): re-derive every pruned search's result by
 // the literal enumeration, whose budget they raise
 int64_t g_ts_brute_budget = TS_BRUTE_FORCE_BUDGET;
+int64_t g_ts_opt_budget = TS_BRUTE_FORCE_BUDGET;
 OptimalCheck g_ts_optimal_check;
 
 bool TsView::optimal(Block* b, const VFilter& vf, std::vector<Block*>* q, bool brute) const {
@@ -448,12 +449,16 @@ bool TsView::optimal(Block* b, const VFilter& vf, std::vector<Block*>* q, bool b
       }
       return;
     }
-    for (int i = s; i <= n - 1; ++i) {
+    // the literal enumeration tries every index (a prefix that cannot reach k positions
+    // enumerates nothing); the pruned search, like ts_lane.h TsLane::optimal, only indices
+    // from which k - j positions remain, so both count the same visits
+    const int last = brute ? n - 1 : n - (k - j);
+    for (int i = s; i <= last; ++i) {
       if (!brute) {
         if (par[i] >= 0 && !chosen[par[i]]) continue;  // every completion Not_connected
         const int cap = ownp + own[i] + std::min(k - j - 1, own_after[i + 1]);
         if (have && bound[cap] <= opt_reward) continue;  // cannot beat the best
-        if (++visits > TS_BRUTE_FORCE_BUDGET) throw BudgetExceeded();
+        if (++visits > g_ts_opt_budget) throw BudgetExceeded();
       }
       c[j] = i;
       chosen[i] = 1;

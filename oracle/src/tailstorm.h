@@ -66,6 +66,8 @@ int64_t true_n_choose_k_saturated(int64_t n, int64_t k);  // saturates at INT64_
 // computed both ways and compared (compared: literal searches that completed; large: of
 // those, with more than TS_BRUTE_FORCE_BUDGET choices)
 extern int64_t g_ts_brute_budget;
+// the pruned search's visit budget (TS_BRUTE_FORCE_BUDGET; the host fuzzer lowers it)
+extern int64_t g_ts_opt_budget;
 struct OptimalCheck {
   bool on = false;
   int64_t compared = 0, large = 0, mismatches = 0, unverified = 0;  // unverified: over budget

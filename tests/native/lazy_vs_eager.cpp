@@ -51,8 +51,11 @@ static std::vector<uint32_t> words(const NakLane& L) {
   return std::vector<uint32_t>(w.begin() + 2, w.end() - 2);
 }
 
+// force: run the lazy lane even where lazy_clock_ok refuses it, with u_lazy as
+// lazy_threshold gives it (0 for delta > ~14.7 ev) -- the configuration the launcher must
+// never build, used below to show the guard is needed
 static bool episode(double alpha, int d, double delta, int policy, int steps, uint64_t ep,
-                    uint32_t zero_at, Counters& C) {
+                    uint32_t zero_at, Counters& C, bool force = false) {
   NakParams P{};
   P.t_att = oracle::alpha_threshold(alpha);
   P.d = d;
@@ -65,7 +68,7 @@ static bool episode(double alpha, int d, double delta, int policy, int steps, ui
   P.max_time = __builtin_inf();
   P.policy = policy < 4 ? policy : 0;
   P.cap = steps + 64;
-  if (!lazy_clock_ok(P)) {
+  if (!force && !lazy_clock_ok(P)) {
     fprintf(stderr, "lazy clock not applicable: delta %g\n", delta);
     exit(2);
   }
@@ -108,7 +111,7 @@ static bool episode(double alpha, int d, double delta, int policy, int steps, ui
     E.activate(P, S, M, de);
     Z.activate<ZStream, true>(P, S, M, dz);
     ok = words(E) == words(Z);
-    if (!ok)
+    if (!ok && !force)
       fprintf(stderr, "MISMATCH alpha=%g d=%d delta=%g pol=%d ep=%llu zero_at=%u step %d: status eager %u lazy %u\n",
               alpha, d, delta, policy, (unsigned long long)ep, zero_at, s, E.status, Z.status);
   }
@@ -227,11 +230,28 @@ int main(int argc, char** argv) {
             const uint32_t z = (e % 7 == 6) ? mix(e, 9) % (uint32_t)steps : 0xffffffffu;
             episode_tt2(a, delta, delta * ratio, pol, steps, (uint64_t)e, z, C2);
           }
+  // delta / ev >= 14.8: lazy_threshold is 0, so the lazy clock must be refused (the launcher
+  // then runs the eager lane); forced anyway, the wrapped skip test misses overlaps
+  long guard_fail = 0;
+  Counters F;
+  for (double delta : {14.8, 15.0, 20.0, 100.0}) {
+    NakParams P{};
+    P.d = 2;
+    P.ev = 1.0;
+    P.delta = delta;
+    P.max_steps = steps;
+    P.max_progress = __builtin_inf();
+    P.max_time = __builtin_inf();
+    if (lazy_clock_ok(P) || lazy_threshold(P) != 0ull) guard_fail++;
+    for (int e = 0; e < 8; ++e) episode(0.33, 2, delta, 1, steps, (uint64_t)e, 0xffffffffu, F, true);
+  }
+  if (F.mismatches == 0) guard_fail++;  // the forced lazy lane must go wrong somewhere
   printf("{\"episodes\": %ld, \"mismatches\": %ld, \"lazy_branch_activations\": %ld, "
          "\"overlap_episodes\": %ld, \"inf_clock_episodes\": %ld, \"tt2_episodes\": %ld, "
          "\"tt2_mismatches\": %ld, \"tt2_eager_redo\": %ld, \"tt2_lazy_redo\": %ld, "
-         "\"tt2_overlap_episodes\": %ld, \"tt2_tie_episodes\": %ld}\n",
+         "\"tt2_overlap_episodes\": %ld, \"tt2_tie_episodes\": %ld, \"guard_failures\": %ld, "
+         "\"forced_zero_threshold_mismatches\": %ld}\n",
          C.episodes, C.mismatches, C.slow, C.overlaps, C.inf_eps, C2.episodes, C2.mismatches,
-         C2.eager_redo, C2.lazy_redo, C2.overlaps, C2.ties);
-  return C.mismatches || C2.mismatches ? 1 : 0;
+         C2.eager_redo, C2.lazy_redo, C2.overlaps, C2.ties, guard_fail, F.mismatches);
+  return C.mismatches || C2.mismatches || guard_fail ? 1 : 0;
 }

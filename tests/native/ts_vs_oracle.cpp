@@ -116,6 +116,7 @@ static ts::TsParams params_of(const Cfg& cf) {
   P.activations = cf.steps;
   P.max_progress = cf.max_progress;
   P.max_time = cf.max_time;
+  P.opt_budget = oracle::g_ts_opt_budget;
   return P;
 }
 
@@ -400,6 +401,9 @@ int main(int argc, char** argv) {
     oracle::g_ts_optimal_check.on = true;
     oracle::g_ts_brute_budget = atoll(oc);
   }
+  // OPTBUDGET=<visits>: both engines' pruned-search budget lowered to <visits>, so that
+  // many searches run out of it: the episodes each engine flags must be the same
+  if (const char* ob = getenv("OPTBUDGET")) oracle::g_ts_opt_budget = atoll(ob);
   if (const char* prof = getenv("TSPROF")) {
     // lane only (host profiling, tools: gprof): "policy,episodes" of bench.py configs[3]
     // (two agents, alpha .33, 10^4 activations, discount rewards, selection argv[4])
@@ -434,8 +438,8 @@ int main(int argc, char** argv) {
       if (!run_loop(cf, sd, e, C, why)) fprintf(stderr, "MISMATCH ep=%d: %s\n", e, why.c_str());
     }
     const auto& oc = oracle::g_ts_optimal_check;
-    printf("{\"episodes\": %ld, \"mismatches\": %ld, \"capacity\": %ld, \"raises\": %ld, \"opt_compared\": %ld, \"opt_large\": %ld, \"opt_mismatches\": %ld, \"opt_unverified\": %ld}\n",
-           C.episodes, C.mismatches, C.capacity, C.raises, (long)oc.compared, (long)oc.large,
+    printf("{\"episodes\": %ld, \"mismatches\": %ld, \"capacity\": %ld, \"raises\": %ld, \"budget\": %ld, \"opt_compared\": %ld, \"opt_large\": %ld, \"opt_mismatches\": %ld, \"opt_unverified\": %ld}\n",
+           C.episodes, C.mismatches, C.capacity, C.raises, C.budget, (long)oc.compared, (long)oc.large,
            (long)oc.mismatches, (long)oc.unverified);
     return (C.mismatches || oc.mismatches) ? 1 : 0;
   }

@@ -128,6 +128,25 @@ def test_summary_only_kernels_equal_record_kernels(ctx, gamma, prop, policy):
         assert s1.status_overlap > n // 100  # the exact branch found real overlaps
 
 
+def test_summary_only_kernel_long_delay_matches_oracle(ctx):
+    # propagation delay 20 x the activation delay at gamma = 0: lazy_threshold is 0 there,
+    # so lazy_clock_ok must keep the summary-only kernel on the eager clock (with the lazy
+    # one its skip test wrapped and missed every overlap, reporting closed-form results);
+    # nearly every episode overlaps and is re-run exactly, and the summary must equal the
+    # oracle's episodes summed
+    cfg, keep = device.make_config(alpha=0.33, gamma=0.0, policy=L.POLICY_SAPIRSHTEIN_2016_SM1,
+                                   max_steps=256, seed=0x1A2E, propagation_delay=20.0)
+    b = device.Batch(cfg, ctx=ctx, keep=keep)
+    n = 512
+    s0 = b.run(n, first_episode=0)
+    s1, rec = b.run(n, first_episode=0, records=True)
+    ref = O.run_episodes(cfg, 0, n, threads=8)
+    assert _records_equal(rec, ref) == {}
+    for f in L.Summary.FIELDS:
+        assert getattr(s0, f) == getattr(s1, f), f
+    assert s0.status_overlap > n // 2
+
+
 @pytest.mark.parametrize("n", [65536, 65536 + 37])
 @pytest.mark.parametrize("policy", [L.POLICY_EYAL_SIRER_2014, L.POLICY_SAPIRSHTEIN_2016_SM1])
 def test_deferred_races_tie_heavy(ctx, policy, n):

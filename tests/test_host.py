@@ -30,7 +30,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_version_and_registry():
     lib = L.lib()
-    assert lib.cpr_abi_version() == L.ABI_VERSION == 10
+    assert lib.cpr_abi_version() == L.ABI_VERSION == 11
     assert lib.cpr_version().decode().startswith("cpr-hip")
     from cpr_amd import device
 

@@ -77,6 +77,10 @@ def test_lazy_clock_equals_eager():
     assert out["tt2_mismatches"] == 0 and out["tt2_episodes"] == 2400
     assert out["tt2_lazy_redo"] >= out["tt2_eager_redo"] > 0
     assert out["tt2_overlap_episodes"] > 100 and out["tt2_tie_episodes"] > 50
+    # delta / ev >= 14.8 zeroes lazy_threshold: lazy_clock_ok must refuse the lazy clock
+    # (round-5 advisor finding: u_lazy - 1 wrapped and skipped every overlap check); run
+    # anyway, the lazy lane misses overlaps, so the guard is what keeps it exact
+    assert out["guard_failures"] == 0 and out["forced_zero_threshold_mismatches"] > 0
 
 
 def test_ethereum_lane_matches_oracle_fuzz():
@@ -221,3 +225,20 @@ def test_optimal_quorum_pruned_search_equals_literal():
     assert p.returncode == 0, p.stderr[-2000:]
     assert out["mismatches"] == 0 and out["budget"] == 0
     assert out["opt_mismatches"] == 0 and out["opt_compared"] > 100_000
+
+
+def test_tailstorm_optimal_budget_flags_same_searches():
+    # round-5 advisor finding: the oracle's pruned search counted prefixes that cannot reach
+    # k positions (i <= n - 1) while ts_lane.h counts only i <= n - (k - j), so a search near
+    # the budget could flag in one engine only. Both now count the same prefixes; with the
+    # budget lowered to 10 / 20 / 40 visits in both (OPTBUDGET) many searches run out of it,
+    # and every episode must be flagged by both engines or by neither (the old count
+    # disagreed on 34 / 25 / 5 episodes of this run)
+    subprocess.run(["make", "-s", "-C", str(ROOT / "tests" / "native")], check=True)
+    exe = ROOT / "tests" / "native" / "build" / "ts_vs_oracle"
+    for budget, least in [("10", 100), ("20", 40), ("40", 1)]:
+        p = subprocess.run([str(exe), "1", "200", "8", "2"], capture_output=True, text=True,
+                           timeout=600, env=dict(os.environ, OPTBUDGET=budget))
+        out = json.loads(p.stdout.strip().splitlines()[-1])
+        assert p.returncode == 0, p.stderr[-2000:]
+        assert out["mismatches"] == 0 and out["budget"] >= least, out
