@@ -955,6 +955,15 @@ static int flush_reruns(cpr_ctx* c) {
   if (c->rlaunch.empty()) return CPR_OK;
   int64_t lb = 0, rest = 0;
   for (const RerunLaunch& r : c->rlaunch) {
+    // the re-run region's layout (rerun_episode): the engine lane, then a hybrid's
+    // closed-form ring, spill and tie-replay scratch (hybrid_mem); a launch registered with
+    // a smaller region is refused here rather than run past it
+    const int64_t need = eth::eth_lane_bytes(r.P.cap_b, r.P.cap_e, r.P.n) +
+                         (r.hybrid ? hybrid_bytes(r.NP.cap) : 0);
+    if (r.lane_bytes < need || (r.hybrid && r.NP.cap < r.P.max_steps + 2))
+      return fail(CPR_E_HIP, "re-run region smaller than its layout (" +
+                                 std::to_string(r.lane_bytes) + " < " + std::to_string(need) +
+                                 " bytes)");
     lb = std::max(lb, r.lane_bytes);
     rest = std::max(rest, eth::eth_rest_bytes(r.P.cap_b, r.P.cap_e, r.P.n));
   }

@@ -193,6 +193,21 @@ size_t eth_slot_bytes();
     if ((int64_t)(have) < (int64_t)(need)) return hipErrorInvalidValue; \
   } while (0)
 
+// The LDS guard. hipLaunchKernelGGL does not refuse a dispatch whose static plus dynamic
+// LDS exceeds the CU's 160 KiB, even after hipFuncSetAttribute refused that size: the
+// queue aborts it (HSA_STATUS_ERROR_INVALID_ALLOCATION), and HIP reports the abort as "an
+// illegal memory access was encountered" although no memory was accessed
+// (tools/probes/lds_limit_probe.hip, profiles/r6a_lds_probe.log; the round-5 fault of the
+// rejected wave-wide re-run variant). lds_dynamic_max(kernel) = the
+// device's LDS per workgroup less the kernel's static LDS (hipFuncGetAttributes), cached per
+// kernel and device; every launcher that asks for dynamic LDS checks its request with
+// CPR_LDS_GUARD and refuses (hipErrorInvalidValue) rather than dispatch
+int64_t lds_dynamic_max(const void* kernel);
+#define CPR_LDS_GUARD(kernel, dyn)                                          \
+  do {                                                                      \
+    if ((int64_t)(dyn) > lds_dynamic_max((const void*)(kernel))) return hipErrorInvalidValue; \
+  } while (0)
+
 constexpr int64_t kRerunQueue = 1 << 22;       // queue entries per context
 constexpr size_t kRerunMaxLaunches = 1 << 20;  // launches per flush (< 2^23)
 

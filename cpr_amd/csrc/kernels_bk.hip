@@ -13,6 +13,8 @@
 #include <algorithm>
 #include <atomic>
 #include <cstdlib>
+#include <mutex>
+#include <vector>
 
 #include "../../include/cpr_hip.h"
 #include "bk_lane.h"
@@ -557,6 +559,33 @@ __global__ void k_bk_policy(bk::BkParams P, int unit, const double* obs, int64_t
 
 static unsigned grid_of(int64_t n) { return (unsigned)((n + kBlock - 1) / kBlock); }
 
+int64_t lds_dynamic_max(const void* kernel) {
+  struct Entry {
+    const void* k;
+    int dev;
+    int64_t room;
+  };
+  static std::mutex mu;
+  static std::vector<Entry> cache;
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  std::lock_guard<std::mutex> lock(mu);
+  for (const Entry& e : cache)
+    if (e.k == kernel && e.dev == dev) return e.room;
+  int lds = 0;
+  if (hipDeviceGetAttribute(&lds, hipDeviceAttributeMaxSharedMemoryPerBlock, dev) != hipSuccess ||
+      lds <= 0)
+    lds = 64 * 1024;
+  hipFuncAttributes fa{};
+  if (hipFuncGetAttributes(&fa, kernel) != hipSuccess) {
+    (void)hipGetLastError();
+    return 0;  // unknown: no dynamic LDS (not cached, asked again next time)
+  }
+  const int64_t room = std::max<int64_t>(0, (int64_t)lds - (int64_t)fa.sharedSizeBytes);
+  cache.push_back(Entry{kernel, dev, room});
+  return room;
+}
+
 // heap nodes per lane in the LDS slab for a grid of `blocks` workgroups: the LDS a
 // workgroup gets when the grid spreads over the device's CUs (160 KiB per CU), less the
 // kernels' static LDS, at most 32 nodes (the gym's windows hold 14-30 live events);
@@ -572,12 +601,14 @@ int32_t ev_slab_nodes(int64_t blocks, const void* kernel) {
   }
   if (const char* v = getenv("CPR_EV_SLAB")) return std::max(0, std::min(32, atoi(v)));
   const int64_t per_cu = std::max<int64_t>(1, (blocks + cus - 1) / cus);
-  const int64_t bytes = (160 * 1024) / per_cu - 2048;  // static LDS of the kernels
+  // 160 KiB less the kernel's static LDS (reserved as at least 2 KiB, the plans' rule)
+  const int64_t room = std::min<int64_t>(lds_dynamic_max(kernel), 160 * 1024 - 2048);
+  const int64_t bytes = std::min<int64_t>(room, (160 * 1024) / per_cu - (160 * 1024 - room));
   int32_t kl = (int32_t)std::min<int64_t>(32, std::max<int64_t>(0, bytes / (kBlock * 24)));
   if ((int64_t)kl * kBlock * 24 > 64 * 1024) {
     // more than the default 64 KiB of dynamic LDS: ask once per kernel
     if (hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            160 * 1024 - 2048) != hipSuccess) {
+                            (int)room) != hipSuccess) {
       (void)hipGetLastError();
       kl = (64 * 1024) / (kBlock * 24);
     }
@@ -642,7 +673,9 @@ EvSlab ev_slab_plan(int64_t blocks, const void* kernel, int32_t n, int32_t lanes
       cus = 256;
   }
   const int64_t per_cu = std::max<int64_t>(1, (blocks + cus - 1) / cus);
-  const int64_t avail = (160 * 1024) / per_cu - 2048;  // static LDS of the kernels
+  // 160 KiB less the kernel's static LDS (reserved as at least 2 KiB, the plans' rule)
+  const int64_t room = std::min<int64_t>(lds_dynamic_max(kernel), 160 * 1024 - 2048);
+  const int64_t avail = std::min<int64_t>(room, (160 * 1024) / per_cu - (160 * 1024 - room));
   int32_t vw = 0;
   for (int32_t w : {64, 32})
     if (vw == 0 && (int64_t)w * n * lanes * 3 <= avail) vw = w;
@@ -660,7 +693,7 @@ EvSlab ev_slab_plan(int64_t blocks, const void* kernel, int32_t n, int32_t lanes
   size_t bytes = (size_t)kl * lanes * 24 + (size_t)vw * n * lanes;
   if (bytes > 64 * 1024 &&
       hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                          160 * 1024 - 2048) != hipSuccess) {
+                          (int)room) != hipSuccess) {
     (void)hipGetLastError();  // the default 64 KiB: the heap slab alone
     vw = 0;
     kl = std::min(32, (64 * 1024) / (lanes * 24));
@@ -676,6 +709,7 @@ hipError_t launch_bk_run_episodes(const bk::BkParams& P, uint64_t seed, uint64_t
   CPR_LAYOUT_GUARD(lane_bytes, bk::bk_lane_bytes(P));
   const unsigned blocks = (unsigned)(lanes / kBlock);
   const EvSlab sl = ev_slab_plan(blocks, (const void*)k_bk_run_episodes<SeedSource>, P.n);
+  CPR_LDS_GUARD(k_bk_run_episodes<SeedSource>, sl.bytes);
   hipLaunchKernelGGL(k_bk_run_episodes<SeedSource>, dim3(blocks), dim3(kBlock), sl.bytes, st, P,
                      SeedSource{seed, first}, n_eps, mem, lane_bytes, recs, sum, no, sl.kl,
                      sl.vw);
@@ -689,6 +723,7 @@ hipError_t launch_bk_replay_episodes(const bk::BkParams& P, const TraceSource& s
   CPR_LAYOUT_GUARD(lane_bytes, bk::bk_lane_bytes(P));
   const unsigned blocks = (unsigned)(lanes / kBlock);
   const EvSlab sl = ev_slab_plan(blocks, (const void*)k_bk_run_episodes<TraceSource>, P.n);
+  CPR_LDS_GUARD(k_bk_run_episodes<TraceSource>, sl.bytes);
   hipLaunchKernelGGL(k_bk_run_episodes<TraceSource>, dim3(blocks), dim3(kBlock), sl.bytes, st, P,
                      src, n_eps, mem, lane_bytes, recs, sum, no, sl.kl, sl.vw);
   return hipGetLastError();
@@ -722,6 +757,7 @@ hipError_t launch_bk_rollout(const bk::BkParams& P, uint64_t seed, uint8_t* mem,
   const int64_t per_block = (int64_t)(kBlock / 64) * lpw;
   const unsigned blocks = (unsigned)((n + per_block - 1) / per_block);
   const EvSlab sl = ev_slab_plan(blocks, (const void*)k_bk_rollout, P.n, (int32_t)per_block);
+  CPR_LDS_GUARD(k_bk_rollout, sl.bytes);
   hipLaunchKernelGGL(k_bk_rollout, dim3(blocks), dim3(kBlock), sl.bytes, st, P, seed, mem,
                      lane_bytes, (BkSlot*)slots, n, n_steps, unit, tabs, tn, obs, reward, done,
                      sum, sl.kl, sl.vw, lpw);

@@ -493,14 +493,15 @@ __global__ __launch_bounds__(64) void k_rerun_overflow(const RerunLaunch* launch
 }
 
 // LDS per one-wave workgroup: up to a whole CU's 160 KiB when the launch needs it, less the
-// kernel's static hybrid ring (256 bytes kept)
-constexpr int64_t kRerunLdsMax = 160 * 1024 - 256;
-
+// kernels' static LDS (k_nak_exact_rerun's hybrid ring, 128 B): lds_dynamic_max, so that
+// static + dynamic never exceeds the CU (CPR_LDS_GUARD, kernels.h)
 hipError_t launch_nak_exact_rerun(const RerunLaunch* launches, int64_t n_launches,
                                   const int64_t* queue, const uint32_t* queue_n,
                                   int64_t queue_cap, uint8_t* mem, int64_t lane_bytes,
                                   int64_t lds_bytes, int64_t lanes, hipStream_t st) {
-  int64_t cap = kRerunLdsMax;
+  const int64_t room = std::min(lds_dynamic_max((const void*)k_nak_exact_rerun),
+                                lds_dynamic_max((const void*)k_rerun_overflow)) / 128 * 128;
+  int64_t cap = room;
   if (const char* v = getenv("CPR_RERUN_LDS_MAX"))  // tests: force the reduced-heap paths
     cap = std::min<int64_t>(cap, std::max<int64_t>(0, atoll(v)));
   int64_t lds = lds_bytes < cap ? lds_bytes : cap;
@@ -515,17 +516,19 @@ hipError_t launch_nak_exact_rerun(const RerunLaunch* launches, int64_t n_launche
     if (have == 0) {
       const bool a = hipFuncSetAttribute((const void*)k_nak_exact_rerun,
                                          hipFuncAttributeMaxDynamicSharedMemorySize,
-                                         (int)kRerunLdsMax) == hipSuccess;
+                                         (int)room) == hipSuccess;
       const bool b = hipFuncSetAttribute((const void*)k_rerun_overflow,
                                          hipFuncAttributeMaxDynamicSharedMemorySize,
-                                         (int)kRerunLdsMax) == hipSuccess;
-      have = a && b ? kRerunLdsMax : 64 * 1024;
+                                         (int)room) == hipSuccess;
+      have = a && b ? room : 64 * 1024 - 128;
       (void)hipGetLastError();
       g.store(have, std::memory_order_release);
     }
     if (lds > have) lds = have;
   }
   if (lds < 0) lds = 0;
+  CPR_LDS_GUARD(k_nak_exact_rerun, lds);
+  CPR_LDS_GUARD(k_rerun_overflow, lds);
   hipLaunchKernelGGL(k_nak_exact_rerun, dim3((unsigned)lanes), dim3(64), (size_t)lds, st,
                      launches, queue, queue_n, queue_cap, mem, lane_bytes, lds);
   hipLaunchKernelGGL(k_rerun_overflow, dim3((unsigned)lanes), dim3(64), (size_t)lds, st,

@@ -519,6 +519,7 @@ hipError_t launch_ts_run_episodes(const ts::TsParams& P, uint64_t seed, uint64_t
   const unsigned blocks = (unsigned)(lanes / kBlock);
   const EvSlab sl = ev_slab_plan(blocks, (const void*)k_ts_run_episodes<SeedSource>, P.n,
                                  (kBlock / 64) * lpw);
+  CPR_LDS_GUARD(k_ts_run_episodes<SeedSource>, sl.bytes);
   hipLaunchKernelGGL(k_ts_run_episodes<SeedSource>, dim3(blocks), dim3(kBlock), sl.bytes, st, P,
                      SeedSource{seed, first}, n_eps, mem, lane_bytes, recs, sum, no, sl.kl,
                      sl.vw, lpw);
@@ -535,6 +536,7 @@ hipError_t launch_ts_replay_episodes(const ts::TsParams& P, const TraceSource& s
   const unsigned blocks = (unsigned)(lanes / kBlock);
   const EvSlab sl = ev_slab_plan(blocks, (const void*)k_ts_run_episodes<TraceSource>, P.n,
                                  (kBlock / 64) * lpw);
+  CPR_LDS_GUARD(k_ts_run_episodes<TraceSource>, sl.bytes);
   hipLaunchKernelGGL(k_ts_run_episodes<TraceSource>, dim3(blocks), dim3(kBlock), sl.bytes, st, P,
                      src, n_eps, mem, lane_bytes, recs, sum, no, sl.kl, sl.vw, lpw);
   return hipGetLastError();
@@ -568,6 +570,7 @@ hipError_t launch_ts_rollout(const ts::TsParams& P, uint64_t seed, uint8_t* mem,
   const int64_t per_block = (int64_t)(kBlock / 64) * lpw;
   const unsigned blocks = (unsigned)((n + per_block - 1) / per_block);
   const EvSlab sl = ev_slab_plan(blocks, (const void*)k_ts_rollout, P.n, (int32_t)per_block);
+  CPR_LDS_GUARD(k_ts_rollout, sl.bytes);
   hipLaunchKernelGGL(k_ts_rollout, dim3(blocks), dim3(kBlock), sl.bytes, st, P, seed, mem,
                      lane_bytes, (TsSlot*)slots, n, n_steps, unit, tabs, tn, obs, reward, done,
                      sum, sl.kl, sl.vw, lpw);

@@ -197,6 +197,17 @@ def test_hybrid_rerun_equals_whole_episode_engine():
     assert out["episodes"] == 2400 and out["activations"] > 4_000_000
     # both directions exercised many times: the engine entered and left again
     assert out["entered"] > 1000 and out["entries"] > 50_000 and out["ended_closed"] > 1000
+    # the re-run kernel's layout (hring apart, the engine's rest in the LDS-sized buffer with
+    # the heap reduced where it does not fit, summary-only and records runs) gives the same
+    # outputs, and no region is written past its end (canary tails)
+    assert out["layout_mismatches"] == 0 and out["canary_hits"] == 0
+    assert out["split_configs"] == 300 and out["reduced_heap_configs"] > 0
+    # and under host AddressSanitizer + UBSan (round-5 verdict: the re-run fault study)
+    p = subprocess.run([str(exe) + "_asan", "1", "2016"], capture_output=True, text=True,
+                       timeout=600)
+    assert p.returncode == 0, p.stderr[-3000:]
+    out = json.loads(p.stdout.strip().splitlines()[-1])
+    assert out["mismatches"] == 0 and out["canary_hits"] == 0 and out["episodes"] == 300
 
 
 def test_optimal_quorum_pruned_search_equals_literal():
