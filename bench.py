@@ -483,7 +483,8 @@ def main():
     ctx.synchronize()
     torch.cuda.synchronize()
     parallel.barrier(cdev)
-    dt = parallel.allreduce_max(time.perf_counter() - t0, cdev)
+    dt_local = time.perf_counter() - t0
+    dt = parallel.allreduce_max(dt_local, cdev)
     rr1 = ctx.rerun_stats()  # this rank's exact re-runs of the timed region
     sums = read(sums_dev)
     totals = parallel.allreduce_summaries(sums, cdev)  # one packed collective
@@ -494,6 +495,13 @@ def main():
     # around the last launch of every point, on the stream the kernel runs on; activations
     # per launch = E episodes x (max_steps + 1) (every gym episode is exactly that long)
     kms = np.array([b.last_launch()[0] for b in batches])
+    # every rank's own clock, kernel time and re-runs (csv_runner.ml:105-131 reports each
+    # worker's tasks): a 1->8 GPU series that is not linear then shows which rank was slow
+    # and why; the local wall includes the barrier wait, so the slowest rank has the least
+    # wait (kernel ms = the last step's launches, rerun counts = the timed region's)
+    local_acts = sum(int(s.activations) for s in sums)
+    rows = parallel.gather_rows([rank, dt_local, float(kms.sum()), local_acts,
+                                 rr1[0] - rr0[0], rr1[2] - rr0[2], float(gpu)], cdev)
 
     # configs[1]'s gamma = 1 column in the flagged abstract-gamma mode, after the timed
     # region: same kernel, zero delays, match races decided by gamma coins; its own clock
@@ -579,6 +587,12 @@ def main():
                        "exact_reruns_rank0": rr1[0] - rr0[0],
                        "exact_rerun_flushes_rank0": rr1[1] - rr0[1],
                        "exact_rerun_ms_rank0": round(rr1[2] - rr0[2], 3)},
+            "per_rank": [{"rank": int(r[0]), "gpu": int(r[6]), "wall_s": round(r[1], 4),
+                          "kernel_ms_last_step": round(r[2], 3),
+                          "activations": int(r[3]),
+                          "activations_per_s_local": r[3] / r[1] if r[1] > 0 else None,
+                          "exact_reruns": int(r[4]), "exact_rerun_ms": round(r[5], 3)}
+                         for r in rows],
             "sweep_mean_rel_revenue": sweep,
             "abstract_gamma_1": {
                 "mode": "FLAGGED abstract-gamma (CPR_NET_ABSTRACT_GAMMA): not the reference's "

@@ -97,6 +97,20 @@ def allreduce_max(x, device=None):
     return float(t.item())
 
 
+def gather_rows(row, device=None):
+    """Every rank's row of floats (same length everywhere), in rank order: one all_gather
+    of a small f64 tensor (bench.py's per-rank diagnostics). One rank: [row]."""
+    import torch
+    import torch.distributed as dist
+
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return [list(map(float, row))]
+    t = torch.tensor([float(x) for x in row], dtype=torch.float64, device=device)
+    out = [torch.empty_like(t) for _ in range(dist.get_world_size())]
+    dist.all_gather(out, t)
+    return [o.cpu().tolist() for o in out]
+
+
 def sweep(points, episodes_per_point, first_episode=0, rank=0, world_size=1, ctx=None,
           steps=2016, policy=L.POLICY_SAPIRSHTEIN_2016_SM1, seed=0x5EED0000, records=False):
     """Run an alpha x gamma sweep; this rank runs its shard of every point.

@@ -119,6 +119,9 @@ def _bench_worker(rank, world, port, q):
         recs = [_bench_records(pt, (k * world + rank) * E_BENCH, E_BENCH) for k in range(K_BENCH)]
         sums.append(summarize(np.concatenate(recs)))
     tot = parallel.allreduce_summaries(sums)
+    # bench.py's per_rank rows: one all_gather, every rank's row in rank order everywhere
+    rows = parallel.gather_rows([rank, 10.0 * rank + 0.5, world])
+    assert rows == [[float(r), 10.0 * r + 0.5, float(world)] for r in range(world)], rows
     q.put((rank, [t.to_array().tolist() for t in tot]))
     dist.destroy_process_group()
 

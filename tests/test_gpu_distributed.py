@@ -87,3 +87,8 @@ def test_bench_starts_two_ranks_itself():
     cb = d["cpu_baseline"]
     assert cb["value"] > 0 and cb["cores"] >= 1 and cb["kind"] == "port"
     assert "other_configs" not in d  # GPU work beyond the headline stays at N = 1
+    # every rank's clock, kernel time, activations and re-runs (round-5 verdict item 7)
+    pr = d["per_rank"]
+    assert [r["rank"] for r in pr] == [0, 1]
+    assert all(r["wall_s"] > 0 and r["kernel_ms_last_step"] > 0 for r in pr)
+    assert sum(r["activations"] for r in pr) == round(d["value"] * d["ms_per_step"] * d["steps"] / 1e3)
