@@ -664,6 +664,7 @@ static int validate_ts(const cpr_config* c, ts::TsParams* P) {
   bk::BkParams B;
   int rc = validate_bk(&cb, &B);
   if (rc) return rc;
+  P->opt_budget = ts::TS_OPT_BUDGET;  // the caller may have zeroed *P (memset)
   if (c->reward_scheme != CPR_REWARD_CONSTANT && c->reward_scheme != CPR_REWARD_DISCOUNT &&
       c->reward_scheme != CPR_REWARD_PUNISH && c->reward_scheme != CPR_REWARD_HYBRID)
     return fail(CPR_E_INVALID_ARG, "'" + std::to_string(c->reward_scheme) +
