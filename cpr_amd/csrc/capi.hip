@@ -664,7 +664,6 @@ static int validate_ts(const cpr_config* c, ts::TsParams* P) {
   bk::BkParams B;
   int rc = validate_bk(&cb, &B);
   if (rc) return rc;
-  P->opt_budget = ts::TS_OPT_BUDGET;  // the caller may have zeroed *P (memset)
   if (c->reward_scheme != CPR_REWARD_CONSTANT && c->reward_scheme != CPR_REWARD_DISCOUNT &&
       c->reward_scheme != CPR_REWARD_PUNISH && c->reward_scheme != CPR_REWARD_HYBRID)
     return fail(CPR_E_INVALID_ARG, "'" + std::to_string(c->reward_scheme) +
@@ -687,6 +686,7 @@ static int validate_ts(const cpr_config* c, ts::TsParams* P) {
       if (c->policy_table[i] > 7) return fail(CPR_E_INVALID_ARG, "policy table action out of range");
   }
   memset(P, 0, sizeof(*P));
+  P->opt_budget = ts::TS_OPT_BUDGET;
   P->table_dim = c->policy == CPR_TS_POLICY_TABLE ? c->policy_table_dim : 0;
   P->t_att = B.t_att;
   P->d = B.d;
