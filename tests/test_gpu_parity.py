@@ -221,6 +221,10 @@ def test_hybrid_reruns_equal_whole_episode_reruns(ctx, gamma, prop, policy, monk
     assert _records_equal(hyb, whole) == {}
     assert np.array_equal(hyb["status"], whole["status"])
     assert ((hyb["status"] & L.ST_EXACT_RERUN) != 0).sum() > 200
+    # and against the oracle (the reference's event-driven restatement on the same keyed
+    # stream), not only against the device's own whole-episode engine: every record field
+    ref = O.run_episodes(cfg, 0, 256, threads=8)
+    assert _records_equal(hyb, ref) == {}
     # both re-ran the same episodes; the hybrid's flush is the shorter by far (the engine
     # simulates only the stretches around the flagged windows)
     assert r1[0] - r0[0] == r2[0] - r1[0]

@@ -55,7 +55,10 @@ for trace_dir in sorted(glob.glob("gpurun_out/cf_*_trace")):
         s["hbm_GB_per_s"] = (rd + wr) / (dur_ms / 1e3) / 1e9 if dur_ms else None
     if "SQ_INSTS_VALU" in c:
         s["valu_lane_ops_per_activation"] = c["SQ_INSTS_VALU"] * 64 / acts
-        s["salu_instr_per_activation"] = c["SQ_INSTS_SALU"] * 64 / acts
+        # wave instructions (a VALU wave instruction is 64 lane-ops; a SALU one is one
+        # scalar issue per wave, so it is not scaled): the two issue counts side by side
+        s["valu_wave_instr_per_activation"] = c["SQ_INSTS_VALU"] / acts
+        s["salu_wave_instr_per_activation"] = c["SQ_INSTS_SALU"] / acts
         s["wave_wait_any_frac"] = c["SQ_WAIT_ANY"] / c["SQ_WAVE_CYCLES"]
         s["valu_issue_frac_of_78.6T"] = (c["SQ_INSTS_VALU"] * 64 / (dur_ms / 1e3) / 7.86432e13
                                          if dur_ms else None)

@@ -39,7 +39,8 @@ for trace_dir in sorted(glob.glob("gpurun_out/ev_*_trace")):
     s["activations_per_s"] = acts / (dur_ns / 1e9)
     if "SQ_INSTS_VALU" in c:
         s["valu_lane_instr_per_activation"] = c["SQ_INSTS_VALU"] * 64 / acts
-        s["salu_instr_per_activation"] = c["SQ_INSTS_SALU"] * 64 / acts
+        # SALU issues once per wave instruction: a wave count, not scaled by 64 like lane-ops
+        s["salu_wave_instr_per_activation"] = c["SQ_INSTS_SALU"] / acts
         s["lds_instr_per_activation"] = c["SQ_INSTS_LDS"] * 64 / acts
         s["lds_bank_conflict_cycles_per_lds_instr"] = (
             c["SQ_LDS_BANK_CONFLICT"] / c["SQ_INSTS_LDS"] if c["SQ_INSTS_LDS"] else 0.0)
