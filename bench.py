@@ -331,7 +331,8 @@ def pmc_traffic(episodes):
         wr = d.get("hbm_write_bytes_per_dispatch (WRITE_SIZE x1024)")
         if rd is None or wr is None:
             continue
-        return rd + wr, os.path.relpath(path, HERE), d.get("valu_wave_instr_per_activation")
+        valu = d.get("valu_lane_instr_per_activation", d.get("valu_wave_instr_per_activation"))
+        return rd + wr, os.path.relpath(path, HERE), valu
     return None, None, None
 
 

@@ -55,10 +55,12 @@ for trace_dir in sorted(glob.glob("gpurun_out/cf_*_trace")):
         s["hbm_GB_per_s"] = (rd + wr) / (dur_ms / 1e3) / 1e9 if dur_ms else None
     if "SQ_INSTS_VALU" in c:
         s["valu_lane_ops_per_activation"] = c["SQ_INSTS_VALU"] * 64 / acts
-        # wave instructions (a VALU wave instruction is 64 lane-ops; a SALU one is one
-        # scalar issue per wave, so it is not scaled): the two issue counts side by side
+        # the two issue counts on one scale: wave instructions per activation (a VALU wave
+        # instruction is 64 lane-ops, a SALU one a single scalar issue; up to round 5 the
+        # SALU figure here was the count x 64 under the name salu_instr_per_activation)
         s["valu_wave_instr_per_activation"] = c["SQ_INSTS_VALU"] / acts
         s["salu_wave_instr_per_activation"] = c["SQ_INSTS_SALU"] / acts
+        s["salu_over_valu"] = c["SQ_INSTS_SALU"] / c["SQ_INSTS_VALU"] if c["SQ_INSTS_VALU"] else None
         s["wave_wait_any_frac"] = c["SQ_WAIT_ANY"] / c["SQ_WAVE_CYCLES"]
         s["valu_issue_frac_of_78.6T"] = (c["SQ_INSTS_VALU"] * 64 / (dur_ms / 1e3) / 7.86432e13
                                          if dur_ms else None)

@@ -65,10 +65,14 @@ s = {
     "episodes_per_dispatch": eps,
     "activations_per_dispatch": acts,
     "activations_per_s_in_kernel": acts / (sum(durs) / len(durs) / 1e9),
-    "valu_wave_instr_per_activation": r["SQ_INSTS_VALU"]["per_dispatch"] * 64 / acts,
-    "salu_wave_instr_per_activation": r["SQ_INSTS_SALU"]["per_dispatch"] * 64 / acts,
-    "vmem_rd_wave_instr_per_activation": r["SQ_INSTS_VMEM_RD"]["per_dispatch"] * 64 / acts,
-    "vmem_wr_wave_instr_per_activation": r["SQ_INSTS_VMEM_WR"]["per_dispatch"] * 64 / acts,
+    # per activation, in the lane's view: every wave instruction (VALU or SALU) is issued
+    # once for the 64 lanes' 64 activations, so count x 64 / activations = instructions one
+    # lane's activation takes (the figure the 40-op cost model prices); up to round 5 these
+    # keys were named *_wave_instr_per_activation
+    "valu_lane_instr_per_activation": r["SQ_INSTS_VALU"]["per_dispatch"] * 64 / acts,
+    "salu_lane_instr_per_activation": r["SQ_INSTS_SALU"]["per_dispatch"] * 64 / acts,
+    "vmem_rd_lane_instr_per_activation": r["SQ_INSTS_VMEM_RD"]["per_dispatch"] * 64 / acts,
+    "vmem_wr_lane_instr_per_activation": r["SQ_INSTS_VMEM_WR"]["per_dispatch"] * 64 / acts,
     "valu_lane_ops_per_s": r["SQ_INSTS_VALU"]["per_dispatch"] * 64 / (sum(durs) / len(durs) / 1e9),
     "hbm_read_bytes_per_dispatch (FETCH_SIZE x1024 x2, gfx950 correction)": r["FETCH_SIZE"]["per_dispatch"] * 1024 * 2,
     "hbm_write_bytes_per_dispatch (WRITE_SIZE x1024)": r["WRITE_SIZE"]["per_dispatch"] * 1024,
@@ -82,7 +86,7 @@ try:
     if "SQ_INSTS_LDS" in lk:
         lds = lk["SQ_INSTS_LDS"] / ln[(K, "SQ_INSTS_LDS")]
         conf = lk.get("SQ_LDS_BANK_CONFLICT", 0.0) / max(1, ln.get((K, "SQ_LDS_BANK_CONFLICT"), 1))
-        s["lds_wave_instr_per_activation"] = lds * 64 / acts
+        s["lds_lane_instr_per_activation"] = lds * 64 / acts
         s["lds_bank_conflict_cycles_per_lds_instr"] = conf / lds if lds else 0.0
         s["lds_counters"] = {c: {"sum": x, "dispatches": ln[(K, c)]} for c, x in lk.items()}
 except FileNotFoundError:
