@@ -197,7 +197,7 @@ def run_other_configs(ctx, cpu_seconds, with_cpu, pmc, keys=None):
             b = device.Batch(cfg, ctx=ctx, keep=keep)
             n = eps
             if n is None and roll is None:
-                n = b.launch_shape()[1]
+                n = b.launch_shape()[1] * int(os.environ.get("CPR_CFG_ROUNDS", "1"))
             t0 = time.perf_counter()
             if roll is not None:
                 import torch
@@ -450,10 +450,15 @@ def main():
     ctx = device.Context(gpu)
     gammas = [float(g) for g in args.gammas.split(",")]
     points = [(a, g) for g in gammas for a in ALPHAS]
+    # CPR_BENCH_STREAMS (A/B only): point i on context i % S, i.e. its own HIP stream
+    nstreams = int(os.environ.get("CPR_BENCH_STREAMS", "1"))
+    smap = os.environ.get("CPR_BENCH_STREAM_MAP", "gamma")
+    ctxs = [ctx] + [device.Context(gpu) for _ in range(nstreams - 1)]
     batches = []
-    for a, g in points:
+    for i, (a, g) in enumerate(points):
         cfg, keep = device.make_config(alpha=a, gamma=g, max_steps=STEPS_PER_EPISODE, seed=SEED)
-        batches.append(device.Batch(cfg, ctx=ctx, keep=keep))
+        si = (i // len(ALPHAS)) % nstreams if smap == "gamma" else i % nstreams
+        batches.append(device.Batch(cfg, ctx=ctxs[si], keep=keep))
     E = args.episodes
     sbytes = ctypes.sizeof(L.Summary)
 
@@ -471,22 +476,30 @@ def main():
     def new_sums():
         return [torch.zeros(sbytes // 8, dtype=torch.int64, device=tdev) for _ in points]
 
+    def sync_all():
+        for c in ctxs:
+            c.synchronize()
+
+    def rerun_all():
+        st = [c.rerun_stats() for c in ctxs]
+        return tuple(sum(x[i] for x in st) for i in range(3))
+
     for w in range(args.warmup):
         one_step(10**6 + w, new_sums())
-    ctx.synchronize()
-    rr0 = ctx.rerun_stats()
+    sync_all()
+    rr0 = rerun_all()
     sums_dev = new_sums()
     parallel.barrier(cdev)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for k in range(args.steps):
         one_step(k, sums_dev)
-    ctx.synchronize()
+    sync_all()
     torch.cuda.synchronize()
     parallel.barrier(cdev)
     dt_local = time.perf_counter() - t0
     dt = parallel.allreduce_max(dt_local, cdev)
-    rr1 = ctx.rerun_stats()  # this rank's exact re-runs of the timed region
+    rr1 = rerun_all()  # this rank's exact re-runs of the timed region
     sums = read(sums_dev)
     totals = parallel.allreduce_summaries(sums, cdev)  # one packed collective
     acts = sum(int(s.activations) for s in totals)
@@ -621,7 +634,8 @@ def main():
         print(json.dumps(out), flush=True)
     for b in batches + abatches:
         b.close()
-    ctx.close()
+    for c in ctxs:
+        c.close()
     if ws > 1:
         import torch.distributed as dist
 

@@ -938,6 +938,11 @@ static int64_t episode_lanes(cpr_batch* b, int64_t n_eps, bool recs) {
       (int64_t)b->ctx->cus * run_episodes_blocks_per_cu(b->P, b->cfg.mode, recs) * 256;
   const int64_t budget = (int64_t)(16ll << 30) / episode_lane_bytes(b->P);
   int64_t lanes = std::min(full, std::max<int64_t>(256, budget));
+  // A/B: a share of the resident grid (percent), e.g. for launches that run concurrently
+  if (const char* v = getenv("CPR_GRID_SCALE")) {
+    const int64_t pc = atoll(v);
+    if (pc > 0 && pc < 100) lanes = lanes * pc / 100;
+  }
   lanes = std::max<int64_t>(256, (lanes / 256) * 256);
   // equal rounds: the episodes of a launch spread evenly over the fewest rounds of the
   // resident grid, so the last round is not a partly empty one (every lane's episode has
@@ -1143,8 +1148,13 @@ static int run_async_ethwin(cpr_batch* b, int64_t n, uint64_t first, cpr_summary
   const int rc = register_rerun(b, b->EP, b->eth_bytes, first, nullptr, rec_dev, sum_dev, n,
                                 &redo, &redo_n, &launch_id, &ovf);
   if (rc) return rc;
+  // episodes beyond the first round from the context's work queue (a lane that finishes
+  // early takes the next); CPR_NAK_WQ=0 keeps the static grid stride (A/B)
+  eth::EthParams EP = b->EP;
+  const char* wq = getenv("CPR_NAK_WQ");
+  if (!(wq && wq[0] == '0')) HIP_TRY(ctx_next(b->ctx, &EP.next));
   HIP_TRY(hipEventRecord(b->ev0, b->ctx->stream));
-  HIP_TRY(launch_eth_win_episodes(b->EP, b->cfg.seed, first, n, (uint8_t*)mem, wbytes, lanes,
+  HIP_TRY(launch_eth_win_episodes(EP, b->cfg.seed, first, n, (uint8_t*)mem, wbytes, lanes,
                                   rec_dev, sum_dev, redo, redo_n, launch_id, b->ctx->rq_cap,
                                   ovf, b->ctx->stream));
   HIP_TRY(hipEventRecord(b->ev1, b->ctx->stream));
@@ -1289,10 +1299,16 @@ static int run_async(cpr_batch* b, int64_t n, uint64_t first, const TraceSource*
     HIP_TRY(launch_replay_episodes(b->P, *tr, n, b->cfg.mode, b->cfg.activations,
                                    spill, replay, lanes, rec_dev, sum_dev, redo, redo_n,
                                    launch_id, b->ctx->rq_cap, ovf, b->ctx->stream));
-  else
-    HIP_TRY(launch_run_episodes(b->P, b->cfg.seed, first, n, b->cfg.mode, b->cfg.activations,
+  else {
+    // the fused kernel's work queue (kernels.hip nak_next_episode); CPR_NAK_WQ=0 keeps the
+    // static grid stride (A/B)
+    NakParams P = b->P;
+    const char* wq = getenv("CPR_NAK_WQ");
+    if (!(wq && wq[0] == '0')) HIP_TRY(ctx_next(b->ctx, &P.next));
+    HIP_TRY(launch_run_episodes(P, b->cfg.seed, first, n, b->cfg.mode, b->cfg.activations,
                                 spill, replay, list, lanes, rec_dev, sum_dev, redo, redo_n,
                                 launch_id, b->ctx->rq_cap, ovf, b->ctx->stream));
+  }
   HIP_TRY(hipEventRecord(b->ev1, b->ctx->stream));
   return CPR_OK;
 }

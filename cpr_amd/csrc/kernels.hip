@@ -93,6 +93,24 @@ __device__ inline CPR_AI BRef run_loop(NakLane& L, const NakParams& P, const St&
   return L.head(P, M);
 }
 
+// The episode after e (k_run_episodes): with a work-queue counter, the wave's live lanes
+// take the next 64 episodes together (one atomic by the lowest live lane, broadcast), so a
+// wave that runs ahead takes more episodes and a launch ends within about one episode of
+// its slowest wave instead of after a fixed share per wave; the lanes of a wave keep
+// consecutive episodes started together, so their activation counts stay equal (the keyed
+// counter and the deferred races' wave list rely on it). Without: the static grid stride
+__device__ inline CPR_AI int64_t nak_next_episode(unsigned long long* next, int64_t e,
+                                                  int64_t nthreads) {
+  if (next == nullptr) return e + nthreads;
+  const uint64_t live = __ballot(1);
+  const int32_t leader = __builtin_ctzll(live);
+  const int32_t lane = (int32_t)(threadIdx.x % WAVE);
+  unsigned long long base = 0ull;
+  if (lane == leader) base = atomicAdd(next, (unsigned long long)WAVE);
+  base = __shfl(base, leader);
+  return nthreads + (int64_t)base + lane;
+}
+
 // lane status bits whose episodes the closed form cannot vouch for
 constexpr uint32_t kInexact = ST_OVERLAP | ST_DEEP_FORK | ST_TIE_UNRESOLVED | ST_STALE_TIME;
 
@@ -165,7 +183,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ARR == 0
   }
   NakLane L;
   const int64_t n_run = src.size(n_eps);
-  for (int64_t e = tid; e < n_run; e += nthreads) {
+  for (int64_t e = tid; e < n_run; e = nak_next_episode(P.next, e, nthreads)) {
     const auto S = src.at(e);
     int64_t steps = 0;
     const BRef hd = MODE == CPR_MODE_GYM ? run_gym<POL, TT, std::remove_const_t<decltype(S)>, LZ>(L, P, S, M, &steps)
@@ -551,6 +569,7 @@ hipError_t launch_run_episodes(const NakParams& P0, uint64_t seed, uint64_t firs
     // at once
     const ListSource ls{src, reinterpret_cast<const uint32_t*>(list), list + 1};
     const unsigned b2 = blocks;
+    P.next = nullptr;  // the second pass: the static grid stride over the listed episodes
     hipLaunchKernelGGL(second, dim3(b2), dim3(kBlock), 0, st, P, ls, n_eps, activations, spill,
                        replay, recs, sum, redo, redo_n, launch_id, redo_cap, list, ovf);
   }

@@ -183,7 +183,8 @@ __global__ __launch_bounds__(kBlock) CPR_EW_OCC void k_eth_win_episodes(
   const ethw::WinMem M = ethw::win_mem_at(mem + tid * lane_bytes, P.cap_b);
   if (!REC) recs = nullptr;
   ethw::WinLane W;
-  for (int64_t e = tid; e < n_eps; e += nthreads) {
+  // a lane that finishes takes the next episode from the work queue (P.next, wave_sched.h)
+  for (int64_t e = tid; e < n_eps; e = ev_next_episode(P.next, e, nthreads)) {
     const Stream S = src.at(e);
     W.gym_reset(P, S, M);
     bool done = W.dead != 0;

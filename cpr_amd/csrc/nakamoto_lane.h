@@ -164,6 +164,10 @@ struct NakParams {
   // lazy clock (NakLane LZ): a clock uniform U (53-bit integer) below u_lazy draws a delay
   // > 2 delta, which no later window can overlap (set by the launcher, lazy_clock_ok)
   uint64_t u_lazy;
+  // fused-episode launches (k_run_episodes): device counter of the episodes handed out
+  // beyond the first round, in chunks of one wave (zeroed before the launch); null = the
+  // static grid-stride assignment
+  unsigned long long* next = nullptr;
 };
 
 // u_lazy = floor(exp(-2.5 delta / ev) 2^53): U < u_lazy gives dt > 2 delta with margin to
