@@ -104,7 +104,29 @@ struct cpr_ctx {
   // work-queue counter of the event-engine fused-episode launches (wave_sched.h
   // ev_next_episode), zeroed on the stream before each launch
   DevBuf wq;
+  // the deferred-race kernels' eager second passes (kernels.hip launch_run_episodes) run on
+  // `side`, behind their launch's main kernel, so that they overlap the next launch on
+  // `stream`. Each reads one of two list buffers; list_ev[i] marks the end of the pass that
+  // reads lists[i], and the next launch that writes lists[i] waits for it on `stream`.
+  // side_join makes `stream` wait for every pass still pending (before a flush, a
+  // synchronization, or any read of summaries and the re-run queue)
+  hipStream_t side = nullptr;
+  hipEvent_t main_ev = nullptr;
+  DevBuf lists[2];
+  hipEvent_t list_ev[2] = {nullptr, nullptr};
+  bool list_pending[2] = {false, false};
+  int list_i = 0;
 };
+
+static hipError_t side_join(cpr_ctx* c) {
+  for (int i = 0; i < 2; ++i)
+    if (c->list_pending[i]) {
+      const hipError_t e = hipStreamWaitEvent(c->stream, c->list_ev[i], 0);
+      if (e != hipSuccess) return e;
+      c->list_pending[i] = false;
+    }
+  return hipSuccess;
+}
 
 // the context's scratch pool with at least `bytes`
 static hipError_t ctx_pool(cpr_ctx* c, size_t bytes, void** out) {
@@ -191,6 +213,10 @@ int cpr_ctx_create(int device, cpr_ctx** out) {
   c->device = device;
   c->cus = prop.multiProcessorCount;
   hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+  if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&c->main_ev, hipEventDisableTiming);
+  for (int i = 0; i < 2 && e == hipSuccess; ++i)
+    e = hipEventCreateWithFlags(&c->list_ev[i], hipEventDisableTiming);
   if (e != hipSuccess) {
     delete c;
     return fail(CPR_E_HIP, std::string("hipStreamCreate: ") + hipGetErrorString(e));
@@ -203,8 +229,9 @@ int cpr_ctx_destroy(cpr_ctx* c) {
   if (!c) return CPR_OK;
   (void)hipSetDevice(c->device);
   // pending work first: queued exact re-runs complete their callers' summaries and records
-  (void)flush_reruns(c);
+  (void)flush_reruns(c);  // joins the side stream's second passes first
   (void)hipStreamSynchronize(c->stream);
+  (void)hipStreamSynchronize(c->side);
   c->fl_free.insert(c->fl_free.end(), c->fl_pending.begin(), c->fl_pending.end());
   c->fl_pending.clear();
   for (cpr_ctx::FlushRec& r : c->fl_free) {
@@ -214,6 +241,12 @@ int cpr_ctx_destroy(cpr_ctx* c) {
     (void)hipHostFree(r.cnt);
   }
   (void)hipStreamDestroy(c->stream);
+  (void)hipStreamDestroy(c->side);
+  (void)hipEventDestroy(c->main_ev);
+  for (int i = 0; i < 2; ++i) {
+    (void)hipEventDestroy(c->list_ev[i]);
+    c->lists[i].release();
+  }
   c->rq.release();
   c->rtab.release();
   c->rmem.release();
@@ -224,7 +257,7 @@ int cpr_ctx_destroy(cpr_ctx* c) {
 
 int cpr_synchronize(cpr_ctx* c) {
   HIP_TRY(hipSetDevice(c->device));
-  int rc = flush_reruns(c);
+  int rc = flush_reruns(c);  // joins the side stream first
   if (rc) return rc;
   HIP_TRY(hipStreamSynchronize(c->stream));
   return CPR_OK;
@@ -843,6 +876,7 @@ int cpr_rerun_hbm_retries(cpr_ctx* c, int64_t* retries) {
   *retries = 0;
   if (!c->rq.p) return CPR_OK;
   HIP_TRY(hipSetDevice(c->device));
+  HIP_TRY(side_join(c));
   uint32_t v = 0;
   HIP_TRY(hipStreamSynchronize(c->stream));
   HIP_TRY(hipMemcpy(&v, (char*)c->rq.p + (size_t)kRerunQueue * 8 + 4, 4, hipMemcpyDeviceToHost));
@@ -958,6 +992,9 @@ static int64_t episode_lanes(cpr_batch* b, int64_t n_eps, bool recs) {
 constexpr size_t kOvfMaxChunks = 4;  // overflow-flag chunks (256 MiB each) before a flush
 
 static int flush_reruns(cpr_ctx* c) {
+  // the side stream's second passes append to the queue and add to summaries: everything
+  // after this point on the stream (the re-runs, the caller's reads) comes after them
+  HIP_TRY(side_join(c));
   if (c->rlaunch.empty()) return CPR_OK;
   int64_t lb = 0, rest = 0;
   for (const RerunLaunch& r : c->rlaunch) {
@@ -1262,11 +1299,29 @@ static int run_async(cpr_batch* b, int64_t n, uint64_t first, const TraceSource*
   const size_t o_list = align256(o_replay + (size_t)lanes * REPLAY_BYTES);
   const size_t list_bytes = tr ? 0 : (size_t)run_episodes_list_bytes(b->P, b->cfg.mode,
                                                                       rec_dev != nullptr, n);
+  // the second pass of a deferred-race launch runs on the side stream (cpr_ctx.side) with
+  // its list in one of the context's two list buffers; CPR_SIDE_PASS=0 keeps it on the
+  // stream with the list in the pool (A/B)
+  const char* sp = getenv("CPR_SIDE_PASS");
+  const bool side = list_bytes > 0 && !(sp && sp[0] == '0');
+  cpr_ctx* c = b->ctx;
   void* pool = nullptr;
-  HIP_TRY(ctx_pool(b->ctx, o_list + list_bytes, &pool));
+  HIP_TRY(ctx_pool(c, side ? o_list : o_list + list_bytes, &pool));
   double* spill = (double*)pool;
   uint8_t* replay = (uint8_t*)pool + o_replay;
   int64_t* list = list_bytes ? (int64_t*)((uint8_t*)pool + o_list) : nullptr;
+  const int li = c->list_i;
+  if (side) {
+    if (c->list_pending[li]) {
+      // the pass that reads this buffer (two launches ago) must be done before the main
+      // kernel rewrites it; before a reallocation, on the host
+      if (c->lists[li].bytes < list_bytes) HIP_TRY(hipEventSynchronize(c->list_ev[li]));
+      HIP_TRY(hipStreamWaitEvent(c->stream, c->list_ev[li], 0));
+      c->list_pending[li] = false;
+    }
+    HIP_TRY(c->lists[li].ensure(list_bytes));
+    list = (int64_t*)c->lists[li].p;
+  }
   if (!b->ev0) {
     HIP_TRY(hipEventCreate(&b->ev0));
     HIP_TRY(hipEventCreate(&b->ev1));
@@ -1305,9 +1360,19 @@ static int run_async(cpr_batch* b, int64_t n, uint64_t first, const TraceSource*
     NakParams P = b->P;
     const char* wq = getenv("CPR_NAK_WQ");
     if (!(wq && wq[0] == '0')) HIP_TRY(ctx_next(b->ctx, &P.next));
+    bool ran = false;
+    const SidePass sd{c->side, c->main_ev, c->list_ev[li], &ran};
     HIP_TRY(launch_run_episodes(P, b->cfg.seed, first, n, b->cfg.mode, b->cfg.activations,
                                 spill, replay, list, lanes, rec_dev, sum_dev, redo, redo_n,
-                                launch_id, b->ctx->rq_cap, ovf, b->ctx->stream));
+                                launch_id, b->ctx->rq_cap, ovf, b->ctx->stream,
+                                side ? &sd : nullptr));
+    if (ran) {
+      c->list_pending[li] = true;
+      c->list_i ^= 1;
+      // the launch's time spans both kernels: ev0 on the stream, ev1 behind the second pass
+      HIP_TRY(hipEventRecord(b->ev1, c->side));
+      return CPR_OK;
+    }
   }
   HIP_TRY(hipEventRecord(b->ev1, b->ctx->stream));
   return CPR_OK;

@@ -78,12 +78,22 @@ inline int64_t episode_lane_bytes(const NakParams& P) {
 // tagged with launch_id, at most redo_cap) instead of accumulated, for launch_nak_exact_rerun
 // list (optional, device, run_episodes_list_bytes): the deferred-race kernel's episodes for
 // its eager second pass; null = races decided eagerly
+// Where the deferred-race kernel's eager second pass runs (launch_run_episodes): on
+// `stream`, after `main_done` (recorded on the launch's stream behind the main kernel), and
+// `done` recorded behind it; *ran = whether a second pass was launched. Null: the second
+// pass follows the main kernel on the launch's own stream.
+struct SidePass {
+  hipStream_t stream;
+  hipEvent_t main_done, done;
+  bool* ran;
+};
+
 hipError_t launch_run_episodes(const NakParams& P, uint64_t seed, uint64_t first, int64_t n_eps,
                                int32_t mode, int64_t activations, double* spill,
                                uint8_t* replay, int64_t* list, int64_t lanes,
                                cpr_episode_record* recs, cpr_summary* sum, int64_t* redo,
                                uint32_t* redo_n, uint32_t launch_id, int64_t redo_cap,
-                               uint8_t* ovf, hipStream_t st);
+                               uint8_t* ovf, hipStream_t st, const SidePass* side = nullptr);
 int64_t run_episodes_list_bytes(const NakParams& P, int32_t mode, bool recs, int64_t n_eps);
 // the same fused kernel drawing from a device copy of a cpr_trace (cpr_replay)
 hipError_t launch_replay_episodes(const NakParams& P, const TraceSource& src, int64_t n_eps,

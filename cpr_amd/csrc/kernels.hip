@@ -546,9 +546,10 @@ hipError_t launch_run_episodes(const NakParams& P0, uint64_t seed, uint64_t firs
                                uint8_t* replay, int64_t* list, int64_t lanes,
                                cpr_episode_record* recs, cpr_summary* sum, int64_t* redo,
                                uint32_t* redo_n, uint32_t launch_id, int64_t redo_cap,
-                               uint8_t* ovf, hipStream_t st) {
+                               uint8_t* ovf, hipStream_t st, const SidePass* side) {
   const unsigned blocks = (unsigned)(lanes / kBlock);
   const SeedSource src{seed, first};
+  if (side) *side->ran = false;
   ListFn second = nullptr;
   const RunFn fn = run_fn(P0, mode, recs != nullptr, list != nullptr && deferred_races_ok(P0),
                           &second);
@@ -570,8 +571,26 @@ hipError_t launch_run_episodes(const NakParams& P0, uint64_t seed, uint64_t firs
     const ListSource ls{src, reinterpret_cast<const uint32_t*>(list), list + 1};
     const unsigned b2 = blocks;
     P.next = nullptr;  // the second pass: the static grid stride over the listed episodes
-    hipLaunchKernelGGL(second, dim3(b2), dim3(kBlock), 0, st, P, ls, n_eps, activations, spill,
+    hipStream_t s2 = st;
+    if (side) {
+      // on the side stream, behind this launch's main kernel: it overlaps the next launch
+      // on `st`. The summary-only d = 2 kernels touch neither the spill nor the tie-replay
+      // scratch (no block times; ties by tie_table_d2), which the next launch may use, so
+      // the second pass gets neither
+      hipError_t e = hipEventRecord(side->main_done, st);
+      if (e == hipSuccess) e = hipStreamWaitEvent(side->stream, side->main_done, 0);
+      if (e != hipSuccess) return e;
+      s2 = side->stream;
+      spill = nullptr;
+      replay = nullptr;
+    }
+    hipLaunchKernelGGL(second, dim3(b2), dim3(kBlock), 0, s2, P, ls, n_eps, activations, spill,
                        replay, recs, sum, redo, redo_n, launch_id, redo_cap, list, ovf);
+    if (side) {
+      const hipError_t e = hipEventRecord(side->done, s2);
+      if (e != hipSuccess) return e;
+      *side->ran = true;
+    }
   }
   return hipGetLastError();
 }
