@@ -79,26 +79,12 @@ constexpr int32_t NCAND = eth::NCAND, NQ = eth::NQ, NSTACK = eth::NSTACK;
 constexpr int32_t S_CAND = 0, S_KEY = 32, S_QA = 64, S_QB = 96, S_STACK = 128, S_CLOS = 192;
 constexpr int32_t S_INTS = 192 + NSTACK;
 
-// the newest kWinW blocks of a lane also sit in the workgroup's LDS (WinMem.wl): a window's
-// walks (payload ancestors and their children, jump pointers, the common-ancestor frontier,
-// the release closure, the defenders' tips) read the newest 8 blocks in 67-95 % of their
-// block reads at configs[2]'s points (host count)
-#ifndef CPR_WIN_W
-#define CPR_WIN_W 8
-#endif
-constexpr int32_t kWinW = CPR_WIN_W;  // a power of 2
-static_assert((kWinW & (kWinW - 1)) == 0, "window size");
-
 struct WinMem {
   WBlock* blk;     // [cap_b]
   double* tm;      // [cap_b] append times (Simulator.timestamp)
   int32_t* tips;   // [64]: defender j's preferred block at tips[j] (Honest.state)
   int32_t* scr;    // [S_INTS]
   ReplayMem replay;  // tie_replay scratch
-  // copies of blocks newest - kWinW + 1 .. newest at wl[s & (kWinW - 1)] (LDS in the
-  // kernel, null = none). Write-through: every store to a block goes to blk as well, so the
-  // ring stays complete and a block that leaves the window needs no write-back
-  WBlock* wl = nullptr;
 };
 
 __host__ __device__ inline int64_t win_lane_bytes(int32_t cap_b) {
@@ -150,26 +136,10 @@ struct WinLane {
     status |= eth::EST_CAPACITY;
     if (!dead) dead = why;
   }
-  // serials index the ring directly: append stops the lane before it would wrap. A block of
-  // the LDS window is read from there (only stores go through set_*, which write both)
+  // serials index the ring directly: append stops the lane before it would wrap
   __host__ __device__ inline WBlock& B(const EthParams& P, const WinMem& M, int32_t s) {
     if ((uint32_t)s > (uint32_t)newest) fail(1);
-    else if (M.wl && s > newest - kWinW) return M.wl[s & (kWinW - 1)];
     return M.blk[s & (P.cap_b - 1)];
-  }
-  __host__ __device__ inline bool in_win(const WinMem& M, int32_t s) const {
-    return M.wl && s > newest - kWinW && s <= newest;
-  }
-  // the two stores to existing blocks: a parent's newest child, an attacker block's
-  // released flag (both copies)
-  __host__ __device__ inline void set_child(const EthParams& P, const WinMem& M, int32_t s,
-                                            int32_t c) {
-    M.blk[s & (P.cap_b - 1)].child = (int16_t)c;
-    if (in_win(M, s)) M.wl[s & (kWinW - 1)].child = (int16_t)c;
-  }
-  __host__ __device__ inline void set_rel(const EthParams& P, const WinMem& M, int32_t s) {
-    M.blk[s & (P.cap_b - 1)].rel = 1;
-    if (in_win(M, s)) M.wl[s & (kWinW - 1)].rel = 1;
   }
   // Simulator.timestamp of block s (its append time)
   __host__ __device__ inline double time_of(const EthParams& P, const WinMem& M, int32_t s) {
@@ -191,10 +161,10 @@ struct WinLane {
     CPR_COST(eth::CC_PAYLOAD);
     int32_t* cand = M.scr + S_CAND;
     int32_t* key = M.scr + S_KEY;
-    int16_t ic[19];  // in-chain set: the tip and the parents of tip .. gen 5 (serials < 2^15)
+    int32_t ic[19];  // in-chain set: the tip and the parents of tip .. gen 5
     int32_t nua[6];
     int32_t ng = 0, nic = 0;
-    ic[nic++] = (int16_t)tip;
+    ic[nic++] = tip;
     {
       int32_t b = tip;
       for (int32_t gen = 0; gen < 6; ++gen) {
@@ -207,7 +177,7 @@ struct WinLane {
         }
         nua[gen] = x.p[0];
         ng = gen + 1;
-        for (int32_t i = 0; i < x.np; ++i) ic[nic++] = (int16_t)x.p[i];
+        for (int32_t i = 0; i < x.np; ++i) ic[nic++] = x.p[i];
         b = x.p[0];
       }
     }
@@ -299,7 +269,7 @@ struct WinLane {
   // simulator.ml:122-136, 377-399 (set_rewards, ethereum.ml:173-197: Constant = whitepaper)
   __host__ __device__ inline int32_t append(const EthParams& P, const WinMem& M, int32_t node,
                                             const Payload& d) {
-    const WBlock& pb = B(P, M, d.p[0]);
+    WBlock& pb = B(P, M, d.p[0]);
     int32_t ra = pb.rew_att, rd = pb.rew_def;
     const int32_t nu = d.np - 1;
     if (node == 0)
@@ -335,10 +305,7 @@ struct WinLane {
     b.sib = pb.child;  // children lists newest first (dag.ml:32)
     b.jump = (int16_t)jmp;
     b.plain = (int16_t)(d.np == 1 ? pb.plain + 1 : 0);
-    // the parent's newest child before the new block takes its window slot (the slot may be
-    // the parent's own: then the parent leaves the window, its ring copy already updated)
-    set_child(P, M, d.p[0], s);
-    if (M.wl) M.wl[s & (kWinW - 1)] = b;
+    pb.child = (int16_t)s;
     M.tm[s] = now;
     return s;
   }
@@ -618,9 +585,9 @@ struct WinLane {
     while (sp > 0 && !dead) {
       const int32_t s = st[--sp];
       CPR_COST(eth::CC_SHARE);
-      const WBlock& b = B(P, M, s);
+      WBlock& b = B(P, M, s);
       if (b.miner != 0 || b.rel) continue;  // received / released: nothing to share
-      set_rel(P, M, s);  // its link delays are keyed (c_act, off): off = position in clos
+      b.rel = 1;  // its link delays are keyed (c_act, off): off = position in clos
       clos[off++] = s;
       if (sp + b.np > NSTACK) {
         fail(5);
@@ -773,7 +740,6 @@ struct WinLane {
     r.child = r.sib = -1;
     r.jump = 0;
     r.plain = 0;
-    if (M.wl) M.wl[0] = r;  // the window holds genesis alone (newest = 0)
     M.tm[0] = 0.0;
     for (int32_t j = 0; j <= P.d; ++j) M.tips[j] = 0;
     pub = priv = 0;

@@ -167,14 +167,11 @@ __global__ __launch_bounds__(kBlock) CPR_EV_OCC void k_eth_run_episodes(
 #else
 #define CPR_EW_OCC
 #endif
-// a lane's LDS window (WinMem.wl): kWinW blocks, the lanes 8 bytes apart in bank order
-constexpr int64_t kWinLaneBytes = (int64_t)ethw::kWinW * sizeof(ethw::WBlock) + 8;
 template <int REC>
 __global__ __launch_bounds__(kBlock) CPR_EW_OCC void k_eth_win_episodes(
     eth::EthParams P, SeedSource src, int64_t n_eps, uint8_t* mem, int64_t lane_bytes,
     cpr_episode_record* recs, cpr_summary* sum, int64_t* redo, uint32_t* redo_n,
-    uint32_t launch_id, int64_t redo_cap, uint8_t* ovf, int32_t win_lds) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t win_blocks[];
+    uint32_t launch_id, int64_t redo_cap, uint8_t* ovf) {
   __shared__ int32_t hist[CPR_HIST_BINS];
   __shared__ unsigned long long acc_w[13];
   LdsAcc acc{acc_w};
@@ -183,8 +180,7 @@ __global__ __launch_bounds__(kBlock) CPR_EW_OCC void k_eth_win_episodes(
   __syncthreads();
   const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t nthreads = (int64_t)gridDim.x * blockDim.x;
-  ethw::WinMem M = ethw::win_mem_at(mem + tid * lane_bytes, P.cap_b);
-  if (win_lds) M.wl = reinterpret_cast<ethw::WBlock*>(win_blocks + threadIdx.x * kWinLaneBytes);
+  const ethw::WinMem M = ethw::win_mem_at(mem + tid * lane_bytes, P.cap_b);
   if (!REC) recs = nullptr;
   ethw::WinLane W;
   // a lane that finishes takes the next episode from the work queue (P.next, wave_sched.h)
@@ -230,40 +226,9 @@ __global__ __launch_bounds__(kBlock) CPR_EW_OCC void k_eth_win_episodes(
 
 using EthWinFn = void (*)(eth::EthParams, SeedSource, int64_t, uint8_t*, int64_t,
                           cpr_episode_record*, cpr_summary*, int64_t*, uint32_t*, uint32_t,
-                          int64_t, uint8_t*, int32_t);
+                          int64_t, uint8_t*);
 static EthWinFn eth_win_fn(bool recs) {
   return recs ? k_eth_win_episodes<1> : k_eth_win_episodes<0>;
-}
-
-// the window kernel's dynamic LDS: every lane's block window (WinMem.wl), when it fits
-// beside the kernel's static LDS at two workgroups per CU (asked for once per device beyond
-// the default 64 KiB); 0 = no window (CPR_WIN_LDS=0 for A/B runs)
-static int64_t eth_win_lds_bytes(bool recs) {
-  const char* v = getenv("CPR_WIN_LDS");
-  if (v && v[0] == '0') return 0;
-  const void* fn = (const void*)eth_win_fn(recs);
-  const int64_t want = (int64_t)kBlock * kWinLaneBytes;
-  const int64_t room = lds_dynamic_max(fn);
-  // two workgroups per CU: each gets half of the CU's LDS
-  const int64_t stat = 160 * 1024 - room;
-  if (want > room || 2 * (want + stat) > 160 * 1024) return 0;
-  if (want > 64 * 1024) {
-    static std::atomic<int> asked[64][2];
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    std::atomic<int>& a = asked[dev & 63][recs ? 1 : 0];
-    int st = a.load(std::memory_order_acquire);
-    if (st == 0) {
-      st = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)want) ==
-                   hipSuccess
-               ? 1
-               : 2;
-      (void)hipGetLastError();
-      a.store(st, std::memory_order_release);
-    }
-    if (st != 1) return 0;
-  }
-  return want;
 }
 
 hipError_t launch_eth_win_episodes(const eth::EthParams& P, uint64_t seed, uint64_t first,
@@ -272,19 +237,16 @@ hipError_t launch_eth_win_episodes(const eth::EthParams& P, uint64_t seed, uint6
                                    int64_t* redo, uint32_t* redo_n, uint32_t launch_id,
                                    int64_t redo_cap, uint8_t* ovf, hipStream_t st) {
   CPR_LAYOUT_GUARD(lane_bytes, ethw::win_lane_bytes(P.cap_b));
-  const EthWinFn fn = eth_win_fn(recs != nullptr);
-  const int64_t lds = eth_win_lds_bytes(recs != nullptr);
-  CPR_LDS_GUARD(fn, lds);
-  hipLaunchKernelGGL(fn, dim3((unsigned)(lanes / kBlock)), dim3(kBlock), (size_t)lds, st, P,
-                     SeedSource{seed, first}, n_eps, mem, lane_bytes, recs, sum, redo, redo_n,
-                     launch_id, redo_cap, ovf, lds > 0 ? 1 : 0);
+  hipLaunchKernelGGL(eth_win_fn(recs != nullptr), dim3((unsigned)(lanes / kBlock)), dim3(kBlock),
+                     0, st, P, SeedSource{seed, first}, n_eps, mem, lane_bytes, recs, sum, redo,
+                     redo_n, launch_id, redo_cap, ovf);
   return hipGetLastError();
 }
 
 int eth_win_blocks_per_cu(bool recs) {
   int blocks = 0;
   hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
-      &blocks, (const void*)eth_win_fn(recs), kBlock, (size_t)eth_win_lds_bytes(recs));
+      &blocks, (const void*)eth_win_fn(recs), kBlock, 0);
   if (e != hipSuccess || blocks <= 0) blocks = 2;
   return blocks;
 }

@@ -41,8 +41,7 @@ struct Cfg {
 };
 
 struct Counters {
-  long episodes = 0, mismatches = 0, redo = 0, ties = 0, steps = 0, overlaps = 0, ca_pairs = 0,
-       windowed = 0;
+  long episodes = 0, mismatches = 0, redo = 0, ties = 0, steps = 0, overlaps = 0, ca_pairs = 0;
 };
 
 static eth::EthParams params_of(const Cfg& cf) {
@@ -82,15 +81,7 @@ static bool run_gym(const Cfg& cf, uint64_t seed, uint64_t ep, Counters& C, std:
   g.reset(obs);
   const eth::EthParams P = params_of(cf);
   std::vector<uint8_t> mem(ethw::win_lane_bytes(P.cap_b));
-  ethw::WinMem M = ethw::win_mem_at(mem.data(), P.cap_b);
-  // odd episodes: the kernel's LDS window of the newest blocks (WinMem.wl) in a host buffer,
-  // pre-filled with garbage so that a read of a slot the window does not hold shows
-  std::vector<ethw::WBlock> win(ethw::kWinW);
-  if (ep & 1) {
-    memset(win.data(), 0xA5, win.size() * sizeof(ethw::WBlock));
-    M.wl = win.data();
-    C.windowed++;
-  }
+  const ethw::WinMem M = ethw::win_mem_at(mem.data(), P.cap_b);
   const Stream S{(uint32_t)seed, (uint32_t)(seed >> 32), (uint32_t)ep, (uint32_t)(ep >> 32)};
   ethw::WinLane L;
   L.gym_reset(P, S, M);
@@ -260,9 +251,7 @@ int main(int argc, char** argv) {
                 cfgs[ci].scheme, cfgs[ci].prop, e, why.c_str());
     }
   printf("{\"configs\": %zu, \"episodes\": %ld, \"steps\": %ld, \"mismatches\": %ld, "
-         "\"redo\": %ld, \"overlaps\": %ld, \"tie_episodes\": %ld, \"ca_pairs\": %ld, "
-         "\"windowed\": %ld}\n",
-         cfgs.size(), C.episodes, C.steps, C.mismatches, C.redo, C.overlaps, C.ties, C.ca_pairs,
-         C.windowed);
+         "\"redo\": %ld, \"overlaps\": %ld, \"tie_episodes\": %ld, \"ca_pairs\": %ld}\n",
+         cfgs.size(), C.episodes, C.steps, C.mismatches, C.redo, C.overlaps, C.ties, C.ca_pairs);
   return C.mismatches ? 1 : 0;
 }

@@ -178,9 +178,6 @@ def test_ethereum_window_lane_matches_oracle_fuzz():
     assert out["mismatches"] == 0, p.stderr[-2000:]
     assert out["episodes"] > 1000 and out["steps"] > 400000
     assert out["tie_episodes"] > 20 and out["overlaps"] > 20  # both hazards exercised
-    # odd episodes read the newest blocks from the kernel's LDS window (a garbage-filled host
-    # buffer here, write-through with the ring)
-    assert out["windowed"] > out["episodes"] // 3
 
 
 def test_hybrid_rerun_equals_whole_episode_engine():
