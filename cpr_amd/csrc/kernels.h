@@ -155,9 +155,13 @@ int32_t ev_slab_nodes(int64_t blocks, const void* kernel);
 struct EvSlab {
   int32_t kl, vw;
   size_t bytes;
+  int32_t tw = 0;      // Tailstorm list-record window rows (TsMem.tl), 0 = none
+  size_t tw_off = 0;   // its byte offset in the slab (16-aligned)
 };
-// lanes: used lanes per workgroup (0: all of kBlock)
-EvSlab ev_slab_plan(int64_t blocks, const void* kernel, int32_t n, int32_t lanes = 0);
+// lanes: used lanes per workgroup (0: all of kBlock); trec_rows: list-record window rows the
+// Tailstorm fused kernel asks for (a power of 2; halved until it fits, before the heap nodes)
+EvSlab ev_slab_plan(int64_t blocks, const void* kernel, int32_t n, int32_t lanes = 0,
+                    int32_t trec_rows = 0);
 int32_t rollout_lanes_per_wave(int64_t n, const void* kernel);
 int32_t event_lanes_per_wave();
 // Ethereum gym episodes on the selfish-mining network through the window lane

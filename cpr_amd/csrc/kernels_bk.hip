@@ -662,7 +662,8 @@ int32_t event_lanes_per_wave() {
 // newest vw vertices (BkMem.vl / TsMem.vl; 64, else 32, when they take at most a third of
 // the workgroup's share of LDS; CPR_EV_VWIN overrides it, 0 = none); kl from what is left
 // (ev_slab_nodes' rules)
-EvSlab ev_slab_plan(int64_t blocks, const void* kernel, int32_t n, int32_t lanes) {
+EvSlab ev_slab_plan(int64_t blocks, const void* kernel, int32_t n, int32_t lanes,
+                    int32_t trec_rows) {
   if (lanes <= 0) lanes = kBlock;
   static int cus = 0;
   if (!cus) {
@@ -688,18 +689,31 @@ EvSlab ev_slab_plan(int64_t blocks, const void* kernel, int32_t n, int32_t lanes
     vw = 0;
     rest = avail;
   }
+  // the list-record window (after the visibility rows, 16-aligned; a 16-byte record per row
+  // and lane) takes its share before the heap nodes
+  int32_t tw = trec_rows > 0 && (trec_rows & (trec_rows - 1)) == 0 ? trec_rows : 0;
+  while (tw > 0 && rest - 16 - (int64_t)tw * 16 * lanes < 0) tw >>= 1;
+  if (tw > 0) rest -= 16 + (int64_t)tw * 16 * lanes;
   int32_t kl = (int32_t)std::min<int64_t>(32, std::max<int64_t>(0, rest / (lanes * 24)));
   if (const char* v = getenv("CPR_EV_SLAB")) kl = std::max(0, std::min(32, atoi(v)));
-  size_t bytes = (size_t)kl * lanes * 24 + (size_t)vw * n * lanes;
-  if (bytes > 64 * 1024 &&
+  auto layout = [&](EvSlab& s) {
+    const size_t vis_end = (size_t)s.kl * lanes * 24 + (size_t)s.vw * n * lanes;
+    s.tw_off = (vis_end + 15) / 16 * 16;
+    s.bytes = s.tw > 0 ? s.tw_off + (size_t)s.tw * 16 * lanes : vis_end;
+  };
+  EvSlab sl{kl, vw, 0};
+  sl.tw = tw;
+  layout(sl);
+  if (sl.bytes > 64 * 1024 &&
       hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                           (int)room) != hipSuccess) {
     (void)hipGetLastError();  // the default 64 KiB: the heap slab alone
-    vw = 0;
-    kl = std::min(32, (64 * 1024) / (lanes * 24));
-    bytes = (size_t)kl * lanes * 24;
+    sl.vw = 0;
+    sl.tw = 0;
+    sl.kl = std::min(32, (64 * 1024) / (lanes * 24));
+    layout(sl);
   }
-  return EvSlab{kl, vw, bytes};
+  return sl;
 }
 
 hipError_t launch_bk_run_episodes(const bk::BkParams& P, uint64_t seed, uint64_t first,

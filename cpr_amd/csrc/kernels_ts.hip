@@ -127,7 +127,7 @@ template <class Src>
 __global__ __launch_bounds__(kBlock) CPR_EV_OCC void k_ts_run_episodes(
     ts::TsParams P, Src src, int64_t n_eps, uint8_t* mem,
     int64_t lane_bytes, cpr_episode_record* recs, cpr_summary* sum, NodeOut no, int32_t kl,
-    int32_t vw, int32_t lpw) {
+    int32_t vw, int32_t lpw, int32_t tw, int32_t tw_off) {
   __shared__ int32_t hist[CPR_HIST_BINS];
   if (threadIdx.x < CPR_HIST_BINS) hist[threadIdx.x] = 0;
   __syncthreads();
@@ -144,6 +144,7 @@ __global__ __launch_bounds__(kBlock) CPR_EV_OCC void k_ts_run_episodes(
   // load or store
   ts::ts_heap_slab(M, ts_slab, col, wpb * lpw, kl);
   ts::ts_vis_window(M, (uint8_t*)(ts_slab + (size_t)kl * wpb * lpw), col, vw);
+  if (tw > 0) ts::ts_trec_window(M, (ts::TRec*)((uint8_t*)ts_slab + tw_off), col, tw);
   Acc acc = {};
   ts::TsLane L;
 #if CPR_EV_SCHED
@@ -509,6 +510,14 @@ __global__ void k_ts_policy(int32_t policy, int32_t k, int unit, const double* o
 
 static unsigned ts_grid(int64_t n) { return (unsigned)((n + kBlock - 1) / kBlock); }
 
+// the fused kernel's list-record window rows (TsMem.tl, ev_slab_plan): 8 (configs[3] +2.6 %
+// in kernel, the exp-delay variant +0.5 %, profiles/r6q_ts_trec_window_ab.log; 16 rows leave
+// no heap slab and lose); CPR_TS_TWIN overrides (0 = none) for A/B runs
+static int32_t ts_trec_rows() {
+  if (const char* v = getenv("CPR_TS_TWIN")) return std::max(0, std::min(64, atoi(v)));
+  return 8;
+}
+
 hipError_t launch_ts_run_episodes(const ts::TsParams& P, uint64_t seed, uint64_t first,
                                   int64_t n_eps, uint8_t* mem, int64_t lane_bytes, int64_t lanes,
                                   cpr_episode_record* recs, cpr_summary* sum, hipStream_t st,
@@ -518,11 +527,11 @@ hipError_t launch_ts_run_episodes(const ts::TsParams& P, uint64_t seed, uint64_t
   const int32_t lpw = event_lanes_per_wave();
   const unsigned blocks = (unsigned)(lanes / kBlock);
   const EvSlab sl = ev_slab_plan(blocks, (const void*)k_ts_run_episodes<SeedSource>, P.n,
-                                 (kBlock / 64) * lpw);
+                                 (kBlock / 64) * lpw, ts_trec_rows());
   CPR_LDS_GUARD(k_ts_run_episodes<SeedSource>, sl.bytes);
   hipLaunchKernelGGL(k_ts_run_episodes<SeedSource>, dim3(blocks), dim3(kBlock), sl.bytes, st, P,
                      SeedSource{seed, first}, n_eps, mem, lane_bytes, recs, sum, no, sl.kl,
-                     sl.vw, lpw);
+                     sl.vw, lpw, sl.tw, (int32_t)sl.tw_off);
   return hipGetLastError();
 }
 
@@ -535,10 +544,11 @@ hipError_t launch_ts_replay_episodes(const ts::TsParams& P, const TraceSource& s
   const int32_t lpw = event_lanes_per_wave();
   const unsigned blocks = (unsigned)(lanes / kBlock);
   const EvSlab sl = ev_slab_plan(blocks, (const void*)k_ts_run_episodes<TraceSource>, P.n,
-                                 (kBlock / 64) * lpw);
+                                 (kBlock / 64) * lpw, ts_trec_rows());
   CPR_LDS_GUARD(k_ts_run_episodes<TraceSource>, sl.bytes);
   hipLaunchKernelGGL(k_ts_run_episodes<TraceSource>, dim3(blocks), dim3(kBlock), sl.bytes, st, P,
-                     src, n_eps, mem, lane_bytes, recs, sum, no, sl.kl, sl.vw, lpw);
+                     src, n_eps, mem, lane_bytes, recs, sum, no, sl.kl, sl.vw, lpw, sl.tw,
+                     (int32_t)sl.tw_off);
   return hipGetLastError();
 }
 

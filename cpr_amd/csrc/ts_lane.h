@@ -129,6 +129,12 @@ struct TsMem {
   // visibility rows of the newest vw vertices in the same slab (see bk_lane.h BkMem.vl)
   CPR_LDS uint8_t* vl = nullptr;
   int32_t vw = 0;
+  // list records (TRec) of the newest tw vertices in the same slab, row-major with stride hs
+  // (a copy: set_trec writes both, the ring stays complete). configs[3]'s walks read the
+  // newest 8 / 16 / 32 vertices in 76-82 / 97-99 / 99.3-99.9 % of their list reads
+  // (tools/ts_window_study.cpp)
+  CPR_LDS TRec* tl = nullptr;
+  int32_t tw = 0;
   TVtx* vtx;
   TRec* trec;
   uint8_t* vis;
@@ -208,6 +214,10 @@ __host__ __device__ inline void ts_heap_slab(TsMem& M, HNode* slab, int32_t lane
 __host__ __device__ inline void ts_vis_window(TsMem& M, uint8_t* base, int32_t lane, int32_t vw) {
   M.vl = (CPR_LDS uint8_t*)(base + lane);
   M.vw = vw;
+}
+__host__ __device__ inline void ts_trec_window(TsMem& M, TRec* base, int32_t lane, int32_t tw) {
+  M.tl = (CPR_LDS TRec*)(base + lane);
+  M.tw = tw;
 }
 __host__ __device__ inline void ts_vis_load(const TsMem& M, const TsParams& P, int32_t newest) {
   for (int32_t s = newest - M.vw + 1 < 0 ? 0 : newest - M.vw + 1; s <= newest; ++s)
@@ -305,6 +315,12 @@ __host__ __device__ inline int64_t ocaml_nck(int64_t n, int64_t k, bool* dz) {
   return (a / b) / c;
 }
 
+// host studies only (tools/ts_window_study.cpp): the age (newest serial - s) of every vertex
+// record read through X (0), TR (1) and Vg (2)
+#ifndef CPR_TS_AGE
+#define CPR_TS_AGE(kind, age)
+#endif
+
 struct TsLane {
   int32_t nrand;  // random-policy decisions so far (the keyed draw's index)
   double now;
@@ -328,21 +344,39 @@ struct TsLane {
     if (!dead) dead = why;
   }
   __host__ __device__ inline TVtx& X(const TsParams& P, const TsMem& M, int32_t s) {
+    CPR_TS_AGE(0, newest - s);
     TVtx& b = M.vtx[s & (P.cap_v - 1)];
     if (b.serial != s) fail(1);
     return b;
   }
-  // the list view of vertex s (TRec). Unchecked: the walks start from a vertex read with X,
-  // and every vertex of its lists is newer, so it is in the ring whenever the start is
-  __host__ __device__ inline TRec& TR(const TsParams& P, const TsMem& M, int32_t s) {
+  // the list view of vertex s (TRec), from the LDS window when s is among the newest tw.
+  // Unchecked: the walks start from a vertex read with X, and every vertex of its lists is
+  // newer, so it is in the ring whenever the start is. (No walk reads the record of a vertex
+  // between its ++newest and its set_trec, when its window slot still holds s - tw's.)
+  __host__ __device__ inline TRec TR(const TsParams& P, const TsMem& M, int32_t s) const {
+    CPR_TS_AGE(1, newest - s);
+    if (s > newest - M.tw) {
+      // one 16-byte LDS read; volatile keeps it a ds_read apart from the ring's global load
+      // (else both may be sunk into one generic load of a selected address)
+      typedef int32_t v4 __attribute__((ext_vector_type(4)));
+      const v4 v = *(const volatile CPR_LDS v4*)&M.tl[(int64_t)(s & (M.tw - 1)) * M.hs];
+      TRec r;
+      r.next = v.x;
+      r.depth = v.y;
+      r.pow = v.z;
+      r.parent = v.w;
+      return r;
+    }
     return M.trec[s & (P.cap_v - 1)];
   }
   __host__ __device__ inline void set_trec(const TsParams& P, const TsMem& M, const TVtx& b) {
-    TRec& r = TR(P, M, b.serial);
+    TRec r;
     r.next = b.next;
     r.depth = (b.depth & 0xffff) | (int32_t)((uint32_t)b.who << 16);
     r.pow = b.pow;
     r.parent = b.parent;
+    M.trec[b.serial & (P.cap_v - 1)] = r;
+    if (b.serial > newest - M.tw) M.tl[(int64_t)(b.serial & (M.tw - 1)) * M.hs] = r;
   }
   __host__ __device__ inline uint8_t& V(const TsParams& P, const TsMem& M, int32_t s,
                                         int32_t node) {
@@ -350,6 +384,7 @@ struct TsLane {
   }  // visibility through the LDS window of the newest vw vertices (see bk_lane.h Vg / Vs)
   __host__ __device__ inline uint8_t Vg(const TsParams& P, const TsMem& M, int32_t s,
                                         int32_t node) const {
+    CPR_TS_AGE(2, newest - s);
     if (s > newest - M.vw)
       return *(const volatile CPR_LDS uint8_t*)&M.vl[(int64_t)((s & (M.vw - 1)) * P.n + node) *
                                                       M.hs];

@@ -120,15 +120,23 @@ static ts::TsParams params_of(const Cfg& cf) {
   return P;
 }
 
-// SLABTEST=1: the lane's event-heap slab (nodes 0..5) and visibility window in host
-// buffers, stride 1, so the host fuzz runs the device kernels' LDS paths too
+// SLABTEST=1: the lane's event-heap slab (nodes 0..5), visibility window and list-record
+// window in host buffers, stride 1, so the host fuzz runs the device kernels' LDS paths too.
+// The list-record window starts out filled with garbage (a slot is read only after its
+// vertex's set_trec wrote it). TWIN=<rows> sets its size (default 8, 0 = none)
 static ts::TsMem with_slab(ts::TsMem M, const ts::TsParams& P) {
   static std::vector<bk::HNode> slab(6);
   static std::vector<uint8_t> win;
+  static std::vector<ts::TRec> twin;
   if (!getenv("SLABTEST")) return M;
   win.assign((size_t)8 * P.n, 0);
   ts::ts_heap_slab(M, slab.data(), 0, 1, 6);
   ts::ts_vis_window(M, win.data(), 0, 8);  // and the visibility rows of the newest 8 vertices
+  const int tw = getenv("TWIN") ? atoi(getenv("TWIN")) : 8;
+  if (tw > 0) {
+    twin.assign((size_t)tw, ts::TRec{0x3c3c3c3c, 0x3c3c3c3c, 0x3c3c3c3c, 0x3c3c3c3c});
+    ts::ts_trec_window(M, twin.data(), 0, tw);
+  }
   return M;
 }
 
