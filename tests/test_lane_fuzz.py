@@ -141,11 +141,14 @@ def test_tailstorm_lane_matches_oracle_fuzz():
         assert p.returncode == 0, p.stderr[-2000:]
         assert out["mismatches"] == 0, p.stderr[-2000:]
         assert out["episodes"] > 250 and out["capacity"] == 0
-    # the device kernels' LDS path (event-heap slab) in a host buffer
-    p = subprocess.run([str(exe), "2", "300", "8", "1"], capture_output=True, text=True,
-                       timeout=600, env=dict(os.environ, SLABTEST="1"))
-    out = json.loads(p.stdout.strip().splitlines()[-1])
-    assert p.returncode == 0 and out["mismatches"] == 0, p.stderr[-2000:]
+    # the device kernels' LDS paths (event-heap slab, visibility rows, list-record window from
+    # garbage-filled buffers: the fused kernel's 8 rows, and 2 rows, which wrap every other
+    # append) in host buffers
+    for twin in ("8", "2"):
+        p = subprocess.run([str(exe), "2", "300", "8", "1"], capture_output=True, text=True,
+                           timeout=600, env=dict(os.environ, SLABTEST="1", TWIN=twin))
+        out = json.loads(p.stdout.strip().splitlines()[-1])
+        assert p.returncode == 0 and out["mismatches"] == 0, p.stderr[-2000:]
 
 
 def test_device_log_and_philox_match_oracle():
