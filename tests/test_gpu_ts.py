@@ -253,3 +253,22 @@ def test_ts_rollout_envs_per_wave_ragged(ctx, monkeypatch):
                 e = O.TsGymEnv(cfg, episode=ep)
                 o = e.reset()
             assert np.array_equal(obs[t, i], o), (i, t)
+
+
+@pytest.mark.parametrize("twin", ["0", "2"])
+def test_ts_list_record_window_equals_ring(ctx, monkeypatch, twin):
+    # configs[3]'s shape at 2,048 episodes: the fused kernel with the list records of each
+    # lane's newest 8 vertices in LDS (the default, TsMem.tl) gives the summary, field for
+    # field, that it gives with every record read from the ring in HBM (CPR_TS_TWIN=0) and
+    # with a 2-row window that wraps every other append
+    cfg, keep = _cfg(alpha=0.33, network=L.NET_TWO_AGENTS, mode=L.MODE_LOOP, activations=2000,
+                     policy=L.TS_POLICY_AVOID_LOSS, seed=0x7A11)
+    b = device.Batch(cfg, keep=keep)
+    monkeypatch.delenv("CPR_TS_TWIN", raising=False)
+    s_win = b.run(2048, first_episode=0)
+    monkeypatch.setenv("CPR_TS_TWIN", twin)
+    s_alt = b.run(2048, first_episode=0)
+    assert s_win.episodes == 2048 and s_win.invalid == 0
+    for f in L.Summary.FIELDS:
+        assert getattr(s_win, f) == getattr(s_alt, f), f
+    assert list(s_win.hist) == list(s_alt.hist)
