@@ -181,6 +181,13 @@ def test_ethereum_window_lane_matches_oracle_fuzz():
     assert out["mismatches"] == 0, p.stderr[-2000:]
     assert out["episodes"] > 1000 and out["steps"] > 400000
     assert out["tie_episodes"] > 20 and out["overlaps"] > 20  # both hazards exercised
+    # the lane's region filled with pseudo-random bytes first (the device's pooled memory
+    # holds what the previous launch left): the same outputs, so nothing reads a byte the
+    # lane did not write
+    p = subprocess.run([str(exe), "2", "400"], capture_output=True, text=True, timeout=600,
+                       env=dict(os.environ, GARBAGE="7"))
+    out = json.loads(p.stdout.strip().splitlines()[-1])
+    assert p.returncode == 0 and out["mismatches"] == 0, p.stderr[-2000:]
 
 
 def test_hybrid_rerun_equals_whole_episode_engine():
