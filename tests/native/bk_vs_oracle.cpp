@@ -12,6 +12,7 @@
 #include <string>
 #include <vector>
 
+#include "garbage.h"
 #include "../../cpr_amd/csrc/bk_lane.h"
 #include "../../oracle/src/bk.h"
 
@@ -115,6 +116,7 @@ static bool run_gym(const Cfg& cf, uint64_t seed, uint64_t ep, Counters& C, std:
 
   const bk::BkParams P = params_of(cf);
   std::vector<uint8_t> mem(bk::bk_lane_bytes(P));
+  fill_garbage(mem);
   const bk::BkMem M = with_slab(bk::bk_mem_at(mem.data(), P), P);
   const Stream S{(uint32_t)seed, (uint32_t)(seed >> 32), (uint32_t)ep, (uint32_t)(ep >> 32)};
   bk::BkLane L;
@@ -229,6 +231,7 @@ static bool run_loop(const Cfg& cf, uint64_t seed, uint64_t ep, Counters& C, std
   const int64_t a0 = cf.two_agents == 2 ? L0_ANY : r.activations[0];
   const bk::BkParams P = params_of(cf);
   std::vector<uint8_t> mem(bk::bk_lane_bytes(P));
+  fill_garbage(mem);
   const bk::BkMem M = with_slab(bk::bk_mem_at(mem.data(), P), P);
   const Stream S{(uint32_t)seed, (uint32_t)(seed >> 32), (uint32_t)ep, (uint32_t)(ep >> 32)};
   bk::BkLane L;

@@ -15,6 +15,7 @@
 #include <string>
 #include <vector>
 
+#include "garbage.h"
 #include "../../cpr_amd/csrc/ethereum_lane.h"
 #include "../../include/cpr_hip.h"
 #include "../../oracle/src/ethereum.h"
@@ -120,6 +121,7 @@ static bool run_gym(const Cfg& cf, uint64_t seed, uint64_t ep, Counters& C, std:
 
   const eth::EthParams P = params_of(cf);
   std::vector<uint8_t> mem(eth::eth_lane_bytes(P.cap_b, P.cap_e, P.n));
+  fill_garbage(mem);
   const eth::EthMem M = eth::eth_mem_at(mem.data(), P.cap_b, P.cap_e, P.n);
   const Stream S{(uint32_t)seed, (uint32_t)(seed >> 32), (uint32_t)ep, (uint32_t)(ep >> 32)};
   eth::EthLane L;
@@ -204,6 +206,7 @@ static bool run_loop(const Cfg& cf, uint64_t seed, uint64_t ep, Counters& C, std
                               &g_table());
   const eth::EthParams P = params_of(cf);
   std::vector<uint8_t> mem(eth::eth_lane_bytes(P.cap_b, P.cap_e, P.n));
+  fill_garbage(mem);
   const eth::EthMem M = eth::eth_mem_at(mem.data(), P.cap_b, P.cap_e, P.n);
   const Stream S{(uint32_t)seed, (uint32_t)(seed >> 32), (uint32_t)ep, (uint32_t)(ep >> 32)};
   eth::EthLane L;
@@ -249,6 +252,7 @@ static bool run_sm_loop(const Cfg& cf, uint64_t seed, uint64_t ep, Counters& C,
   for (int i = 1; i < n; ++i) rd += rew[i];
   const eth::EthParams P = params_of(cf);
   std::vector<uint8_t> mem(eth::eth_lane_bytes(P.cap_b, P.cap_e, P.n));
+  fill_garbage(mem);
   const eth::EthMem M = eth::eth_mem_at(mem.data(), P.cap_b, P.cap_e, P.n);
   const Stream S{(uint32_t)seed, (uint32_t)(seed >> 32), (uint32_t)ep, (uint32_t)(ep >> 32)};
   eth::EthLane L;
@@ -296,6 +300,7 @@ static bool run_exp(const Cfg& cf, uint64_t seed, uint64_t ep, Counters& C, std:
   }
   const eth::EthParams P = params_of(cf);
   std::vector<uint8_t> mem(eth::eth_lane_bytes(P.cap_b, P.cap_e, P.n));
+  fill_garbage(mem);
   const eth::EthMem M = eth::eth_mem_at(mem.data(), P.cap_b, P.cap_e, P.n);
   const Stream S{(uint32_t)seed, (uint32_t)(seed >> 32), (uint32_t)ep, (uint32_t)(ep >> 32)};
   eth::EthLane L;

@@ -14,6 +14,7 @@
 #include <string>
 #include <vector>
 
+#include "garbage.h"
 #include "../../cpr_amd/csrc/ts_lane.h"
 #include "../../oracle/src/tailstorm.h"
 
@@ -153,6 +154,7 @@ static bool run_gym(const Cfg& cf, uint64_t seed, uint64_t ep, Counters& C, std:
   double obs[10];
   const ts::TsParams P = params_of(cf);
   std::vector<uint8_t> mem(ts::ts_lane_bytes(P));
+  fill_garbage(mem);
   const ts::TsMem M = with_slab(ts::ts_mem_at(mem.data(), P), P);
   const Stream S{(uint32_t)seed, (uint32_t)(seed >> 32), (uint32_t)ep, (uint32_t)(ep >> 32)};
   ts::TsLane L;
@@ -342,6 +344,7 @@ static bool run_loop(const Cfg& cf, uint64_t seed, uint64_t ep, Counters& C, std
   }
   const ts::TsParams P = params_of(cf);
   std::vector<uint8_t> mem(ts::ts_lane_bytes(P));
+  fill_garbage(mem);
   const ts::TsMem M = with_slab(ts::ts_mem_at(mem.data(), P), P);
   const Stream S{(uint32_t)seed, (uint32_t)(seed >> 32), (uint32_t)ep, (uint32_t)(ep >> 32)};
   ts::TsLane L;
@@ -420,6 +423,7 @@ int main(int argc, char** argv) {
     Cfg cf{0.33, 0.0, 1, pol, 1, 10000, 1, k};
     const ts::TsParams P = params_of(cf);
     std::vector<uint8_t> mem(ts::ts_lane_bytes(P));
+    fill_garbage(mem);
     const ts::TsMem M = with_slab(ts::ts_mem_at(mem.data(), P), P);
     long acts = 0;
     for (int e = 0; e < neps; e++) {

@@ -101,6 +101,11 @@ def test_ethereum_lane_matches_oracle_fuzz():
     assert out["mismatches"] == 0, p.stderr[-2000:]
     assert out["episodes"] > 1000 and out["steps"] > 300000
     assert out["capacity"] == 0  # heap bound: d messages per block (capi.hip validate_eth)
+    # from garbage-filled lane regions (tests/native/garbage.h: pooled device memory)
+    p = subprocess.run([str(exe), "1", "300"], capture_output=True, text=True, timeout=600,
+                       env=dict(os.environ, GARBAGE="11"))
+    out = json.loads(p.stdout.strip().splitlines()[-1])
+    assert p.returncode == 0 and out["mismatches"] == 0, p.stderr[-2000:]
 
 
 def test_bk_lane_matches_oracle_fuzz():
@@ -118,9 +123,10 @@ def test_bk_lane_matches_oracle_fuzz():
         assert p.returncode == 0, p.stderr[-2000:]
         assert out["mismatches"] == 0, p.stderr[-2000:]
         assert out["episodes"] > 700 and out["capacity"] == 0
-    # the device kernels' LDS paths (event-heap slab, visibility window) in host buffers
+    # the device kernels' LDS paths (event-heap slab, visibility window) in host buffers,
+    # the lane's region filled with garbage first (tests/native/garbage.h)
     p = subprocess.run([str(exe), "2", "400", "8"], capture_output=True, text=True,
-                       timeout=600, env=dict(os.environ, SLABTEST="1"))
+                       timeout=600, env=dict(os.environ, SLABTEST="1", GARBAGE="13"))
     out = json.loads(p.stdout.strip().splitlines()[-1])
     assert p.returncode == 0 and out["mismatches"] == 0, p.stderr[-2000:]
 
@@ -146,7 +152,8 @@ def test_tailstorm_lane_matches_oracle_fuzz():
     # append) in host buffers
     for twin in ("8", "2"):
         p = subprocess.run([str(exe), "2", "300", "8", "1"], capture_output=True, text=True,
-                           timeout=600, env=dict(os.environ, SLABTEST="1", TWIN=twin))
+                           timeout=600,
+                           env=dict(os.environ, SLABTEST="1", TWIN=twin, GARBAGE="17"))
         out = json.loads(p.stdout.strip().splitlines()[-1])
         assert p.returncode == 0 and out["mismatches"] == 0, p.stderr[-2000:]
 
