@@ -20,6 +20,7 @@
 #include <cstdlib>
 #include <vector>
 
+#include "garbage.h"
 #include "../../cpr_amd/csrc/nak_hybrid.h"
 #include "../../oracle/src/keyed_stream.h"
 
@@ -36,7 +37,10 @@ struct Guarded {
   static constexpr size_t kTail = 256;
   std::vector<uint8_t> v;
   size_t n = 0;
-  explicit Guarded(size_t bytes) : v(bytes + kTail, 0), n(bytes) { arm(); }
+  explicit Guarded(size_t bytes) : v(bytes + kTail, 0), n(bytes) {
+    fill_garbage(v.data(), n);  // GARBAGE=<seed>: pooled device memory's leftovers
+    arm();
+  }
   uint8_t* data() { return v.data(); }
   void arm() { std::fill(v.begin() + (long)n, v.end(), (uint8_t)0xCD); }
   bool intact() const {
@@ -108,6 +112,7 @@ int main(int argc, char** argv) {
     EP.max_progress = __builtin_inf();
     EP.max_time = __builtin_inf();
     std::vector<uint8_t> m1(eth::eth_lane_bytes(EP.cap_b, EP.cap_e, EP.n));
+    fill_garbage(m1);
     Guarded m2(eth::eth_lane_bytes(EP.cap_b, EP.cap_e, EP.n));
     Guarded m3(hybrid_bytes(NP.cap));
     const eth::EthMem M1 = eth::eth_mem_at(m1.data(), EP.cap_b, EP.cap_e, EP.n);

@@ -10,6 +10,7 @@
 #include <string>
 #include <vector>
 
+#include "garbage.h"
 #include "../../cpr_amd/csrc/nakamoto_lane.h"
 #include "../../oracle/src/des.h"
 
@@ -36,7 +37,11 @@ struct Cfg {
 struct HostMem {
   std::vector<double> ring, spill;
   std::vector<uint8_t> replay;
-  explicit HostMem(const NakParams& P) : ring(RING), spill(P.cap), replay(REPLAY_BYTES) {}
+  explicit HostMem(const NakParams& P) : ring(RING), spill(P.cap), replay(REPLAY_BYTES) {
+    fill_garbage(ring.data(), ring.size() * sizeof(double));
+    fill_garbage(spill.data(), spill.size() * sizeof(double));
+    fill_garbage(replay);
+  }
   LaneMem lane() {
     LaneMem M;
     M.ring = ring.data();

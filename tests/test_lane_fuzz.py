@@ -26,6 +26,11 @@ def test_lane_matches_oracle_fuzz():
     assert out["unresolved"] == 0
     assert out["episodes"] > 1000
     assert out["tie_rule_episodes"] > 100  # two-defender episodes run with the tie rule
+    # ring, spill and replay scratch filled with garbage first (tests/native/garbage.h)
+    p = subprocess.run([str(exe), "1", "400"], capture_output=True, text=True, timeout=600,
+                       env=dict(os.environ, GARBAGE="19"))
+    out = json.loads(p.stdout.strip().splitlines()[-1])
+    assert p.returncode == 0 and out["mismatches"] == 0, p.stderr[-2000:]
 
 
 def test_tie_rule_equals_heap_replay():
@@ -219,9 +224,10 @@ def test_hybrid_rerun_equals_whole_episode_engine():
     # outputs, and no region is written past its end (canary tails)
     assert out["layout_mismatches"] == 0 and out["canary_hits"] == 0
     assert out["split_configs"] == 300 and out["reduced_heap_configs"] > 0
-    # and under host AddressSanitizer + UBSan (round-5 verdict: the re-run fault study)
+    # and under host AddressSanitizer + UBSan (round-5 verdict: the re-run fault study), its
+    # regions filled with garbage first (tests/native/garbage.h)
     p = subprocess.run([str(exe) + "_asan", "1", "2016"], capture_output=True, text=True,
-                       timeout=600)
+                       timeout=600, env=dict(os.environ, GARBAGE="23"))
     assert p.returncode == 0, p.stderr[-3000:]
     out = json.loads(p.stdout.strip().splitlines()[-1])
     assert out["mismatches"] == 0 and out["canary_hits"] == 0 and out["episodes"] == 300
