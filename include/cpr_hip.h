@@ -416,7 +416,7 @@ int cpr_rerun_hbm_retries(cpr_ctx* ctx, int64_t* retries);
  * Nakamoto overlaps, deep forks and unresolved ties; Ethereum window-lane hand-backs) and
  * re-ran on the exact event engine, the flushes that ran them and those flushes' kernel
  * milliseconds (HIP events on the context's stream). Synchronizes the stream if a flush is
- * pending. Diagnostic for bench.py, no reference counterpart. ABI v10. */
+ * pending. Diagnostic for bench.py, no reference counterpart. Since ABI v10. */
 int cpr_rerun_stats(cpr_ctx* ctx, int64_t* episodes, int64_t* flushes, double* ms);
 /* exact-replay coverage of this batch's lockstep lanes (Nakamoto closed-form lanes that
  * leave the closed form continue on the exact engine from an action log): log_steps = the

@@ -1,4 +1,4 @@
-(* OCaml ctypes bindings of libcpr_hip (include/cpr_hip.h, CPR_ABI_VERSION 10).
+(* OCaml ctypes bindings of libcpr_hip (include/cpr_hip.h, CPR_ABI_VERSION 11).
 
    For a host that has OCaml: dropped next to the reference's gym engine
    (simulator/gym/), it lets Hip_engine.of_module (hip_engine.ml) stand in for
